@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""bench.py — SVD-verify witness generation throughput (advice cells / s).
+
+One step = the whole witness of examples/svd_example.rs:98-200 for one
+N x M matrix (ZkMatrix::new m,u,v + ZkVector::new d, check_svd_phase0 into
+phase 0, check_svd_phase1 into phase 1), f64 inputs resident in HBM when the
+clock starts, complete advice + lookup streams resident in HBM when it stops.
+
+Default workload: BASELINE.json configs[3] shape (1024 x 1024, PRECISION_BITS=63,
+LOOKUP_BITS=19) on one GPU. With --gpus N (torch.distributed.run, one rank per
+GPU) every rank generates its own matrix (independent objects, no data-path
+collective): weak scaling, value = cells of all ranks / max-over-ranks time.
+
+Output: ONE JSON line on rank 0 (driver contract), including
+  roofline     dominant kernel, from HIP events the engine records on its own
+               stream during the timed steps (svdw_profile_*),
+  cpu_baseline the single-threaded C oracle (oracle/svdw_oracle.c, a port of
+               the reference algorithm) on a bounded row sample, rank 0 only.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+P_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "advice cells/sec (SVD-verify witness gen, N×N) at 1/2/4/8 MI355X"
+
+
+def gen_input(N, M, seed):
+    """input-creator.py:23-30 recipe with a seeded RandomState."""
+    rs = np.random.RandomState(seed)
+    m = rs.uniform(-10, 10, size=(N, M))
+    m = m / np.linalg.norm(m, ord=2) * rs.uniform(1, 100)
+    U, D, V = np.linalg.svd(m)
+    return m, U, D, V
+
+
+def gamma_for(seed) -> int:
+    return int.from_bytes(hashlib.sha256(f"svdw-gamma-{seed}".encode()).digest(), "little") % P_MOD
+
+
+def roofline_from_profile(stats, steps):
+    """Dominant kernel (largest total time) aggregated over all its launches."""
+    by_kernel = {}
+    for s in stats:
+        k = s["name"].split(":")[0]
+        agg = by_kernel.setdefault(k, {"launches": 0, "total_ms": 0.0, "bytes": 0.0, "ops": 0.0})
+        for f in ("launches", "total_ms", "bytes", "ops"):
+            agg[f] += s[f]
+    name, agg = max(by_kernel.items(), key=lambda kv: kv[1]["total_ms"])
+    avg_ms = agg["total_ms"] / agg["launches"]
+    bytes_per_launch = agg["bytes"] / agg["launches"]
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    breakdown = {k: round(v["total_ms"] / steps, 4) for k, v in
+                 sorted(by_kernel.items(), key=lambda kv: -kv[1]["total_ms"])}
+    return name, {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "kernel": name,
+        "avg_launch_ms": round(avg_ms, 5),
+        "bytes_per_launch": round(bytes_per_launch),
+        "launches_per_step": agg["launches"] / steps,
+    }, breakdown
+
+
+def cpu_baseline(m, u, v, d, P, LB, g, rows):
+    import corc  # oracle/ — the checker / reported baseline only
+    t0 = time.perf_counter()
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, LB, g, row_lim=rows)
+    dt = time.perf_counter() - t0
+    cells = a0.shape[0] + a1.shape[0]
+    return {"value": round(cells / dt, 1), "unit": "advice cells/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle/svdw_oracle.c single thread, same {m.shape[0]}x{m.shape[1]} P={P} "
+                       f"witness restricted to rows [0,{rows}) of every row-parallel stage "
+                       f"(+ all loads and d checks): {cells} advice cells in {dt:.2f} s"),
+            "seconds": round(dt, 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--p", type=int, default=63)
+    ap.add_argument("--lb", type=int, default=19)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-rows", type=int, default=48)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="skip the engine's event profiler in the timed region")
+    ap.add_argument("--breakdown", action="store_true", help="print per-kernel ms/step to stderr")
+    args = ap.parse_args()
+    N = args.n
+    M = args.m or N
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    import halo2_svd041_amd as hs
+
+    m, u, d, v = gen_input(N, M, args.seed + rank)
+    g = gamma_for(args.seed + rank)
+    dev = torch.device("cuda", local)
+    dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev)
+                      for x in (m, u, v, d))
+    torch.cuda.synchronize()
+    ctx = hs.Context(device=local, precision_bits=args.p, lookup_bits=args.lb)
+
+    for _ in range(args.warmup):
+        cnt = hs.svd_witness(ctx, dm, du, dv, dd, g)
+    ctx.sync()
+
+    if not args.no_profile:
+        ctx.profile(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cnt = hs.svd_witness(ctx, dm, du, dv, dd, g)
+    ctx.sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stats = ctx.profile_collect() if not args.no_profile else []
+
+    cells_step = cnt["advice0"] + cnt["advice1"]
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([cells_step], dtype=torch.float64, device=dev)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        cells_all = float(c.item())
+    else:
+        cells_all = float(cells_step)
+    total_cells = cells_all * args.steps
+    value = total_cells / elapsed
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "advice cells/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bn254_fr (u32 limbs; exact int8-digit dot4 GEMM)",
+            "data": "synthetic (input-creator.py recipe, seeded; gamma = sha256 mod p)",
+            "config": {
+                "workload": (f"svd_verify_witness N={N} M={M} PRECISION_BITS={args.p} "
+                             f"LOOKUP_BITS={args.lb}, one matrix per GPU"),
+                "N": N, "M": M, "precision_bits": args.p, "lookup_bits": args.lb,
+                "advice_cells_per_matrix": cells_step,
+                "lookup_cells_per_matrix": cnt["lookup0"] + cnt["lookup1"],
+                "parallelism": f"replicas x{world} (no data-path collective)",
+            },
+        }
+        if stats:
+            kname, roof, breakdown = roofline_from_profile(stats, args.steps)
+            out["roofline"] = roof
+            if args.breakdown:
+                print(json.dumps({"ms_per_step_by_kernel": breakdown,
+                                  "stats": stats}, indent=1), file=sys.stderr)
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(m, u, v, d, args.p, args.lb, g, args.cpu_rows)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,136 @@
+"""ctypes binding of libsvdw.so (the C ABI declared in include/svdw.h).
+
+The product path has no CPU fallback: if the HIP library is missing or cannot
+be loaded, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsvdw.so")
+
+SVDW_OK = 0
+ERRORS = {-1: "SVDW_EINVAL", -2: "SVDW_ERANGE", -3: "SVDW_EDEVICE", -4: "SVDW_ENOMEM"}
+
+
+class SvdwError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Params(ct.Structure):
+    _fields_ = [("device", ct.c_int), ("precision_bits", ct.c_uint32),
+                ("lookup_bits", ct.c_uint32)]
+
+
+class Mat(ct.Structure):
+    _fields_ = [("phase", ct.c_uint32), ("rows", ct.c_uint32), ("cols", ct.c_uint32),
+                ("off", ct.c_uint64), ("rs", ct.c_int64), ("cs", ct.c_int64)]
+
+    def __repr__(self):
+        return (f"Mat(phase={self.phase}, {self.rows}x{self.cols}, off={self.off}, "
+                f"rs={self.rs}, cs={self.cs})")
+
+
+class Vec(ct.Structure):
+    _fields_ = [("phase", ct.c_uint32), ("len", ct.c_uint32), ("off", ct.c_uint64),
+                ("stride", ct.c_int64)]
+
+    def __repr__(self):
+        return f"Vec(phase={self.phase}, len={self.len}, off={self.off}, stride={self.stride})"
+
+
+class Payload(ct.Structure):
+    _fields_ = [("u_t", Mat), ("v_t", Mat), ("m_times_vt", Mat), ("u_times_ut", Mat),
+                ("v_times_vt", Mat)]
+
+
+class SvdConfig(ct.Structure):
+    _fields_ = [("max_norm", ct.c_double), ("eps_svd", ct.c_double), ("eps_u", ct.c_double),
+                ("max_bits_d", ct.c_uint32)]
+
+
+class KStat(ct.Structure):
+    _fields_ = [("name", ct.c_char * 48), ("launches", ct.c_uint64), ("total_ms", ct.c_double),
+                ("max_ms", ct.c_double), ("bytes", ct.c_double), ("ops", ct.c_double)]
+
+
+class Counts(ct.Structure):
+    _fields_ = [("advice0", ct.c_uint64), ("advice1", ct.c_uint64), ("lookup0", ct.c_uint64),
+                ("lookup1", ct.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_P = ct.c_void_p
+_u32, _u64, _i32, _dbl = ct.c_uint32, ct.c_uint64, ct.c_int, ct.c_double
+_u64p = ct.POINTER(ct.c_uint64)
+
+# name -> (restype, argtypes); mirrors include/svdw.h one-for-one.
+SIGNATURES = {
+    "svdw_ctx_create": (_i32, [ct.POINTER(Params), ct.POINTER(_P)]),
+    "svdw_ctx_destroy": (_i32, [_P]),
+    "svdw_ctx_reset": (_i32, [_P]),
+    "svdw_reserve": (_i32, [_P, _u32, _u64, _u64]),
+    "svdw_sync": (_i32, [_P]),
+    "svdw_last_error": (ct.c_char_p, []),
+    "svdw_advice_len": (_u64, [_P, _u32]),
+    "svdw_lookup_len": (_u64, [_P, _u32]),
+    "svdw_advice_device_ptr": (_P, [_P, _u32]),
+    "svdw_lookup_device_ptr": (_P, [_P, _u32]),
+    "svdw_copy_advice": (_i32, [_P, _u32, _u64, _u64, _P]),
+    "svdw_copy_lookup": (_i32, [_P, _u32, _u64, _u64, _P]),
+    "svdw_zkmatrix_new": (_i32, [_P, _u32, _P, _u32, _u32, _i32, ct.POINTER(Mat)]),
+    "svdw_zkvector_new": (_i32, [_P, _u32, _P, _u32, _i32, ct.POINTER(Vec)]),
+    "svdw_transpose_matrix": (_i32, [ct.POINTER(Mat), ct.POINTER(Mat)]),
+    "svdw_load_witness": (_i32, [_P, _u32, _P, ct.POINTER(Vec)]),
+    "svdw_load_constant": (_i32, [_P, _u32, _P, ct.POINTER(Vec)]),
+    "svdw_entries_less_than": (_i32, [_P, ct.POINTER(Vec), _u32]),
+    "svdw_entries_in_desc_order": (_i32, [_P, ct.POINTER(Vec), _u32]),
+    "svdw_check_mat_entries_bounded": (_i32, [_P, ct.POINTER(Mat), _P]),
+    "svdw_check_mat_diff": (_i32, [_P, ct.POINTER(Mat), ct.POINTER(Mat), _P]),
+    "svdw_check_mat_id": (_i32, [_P, ct.POINTER(Mat), ct.POINTER(Vec), _P]),
+    "svdw_mat_times_diag_mat": (_i32, [_P, ct.POINTER(Mat), ct.POINTER(Vec), ct.POINTER(Mat)]),
+    "svdw_honest_prover_mat_mul": (_i32, [_P, _u32, ct.POINTER(Mat), ct.POINTER(Mat),
+                                          ct.POINTER(Mat)]),
+    "svdw_field_mat_vec_mul": (_i32, [_P, _u32, ct.POINTER(Mat), ct.POINTER(Vec),
+                                      ct.POINTER(Vec)]),
+    "svdw_verify_mul": (_i32, [_P, _u32, ct.POINTER(Mat), ct.POINTER(Mat), ct.POINTER(Mat), _P]),
+    "svdw_err_calc": (_i32, [_u32, _u64, _dbl, _dbl, _dbl, ct.POINTER(_dbl), ct.POINTER(_dbl)]),
+    "svdw_check_svd_phase0": (_i32, [_P, ct.POINTER(Mat), ct.POINTER(Mat), ct.POINTER(Mat),
+                                     ct.POINTER(Vec), _dbl, _dbl, _u32, ct.POINTER(Payload)]),
+    "svdw_check_svd_phase1": (_i32, [_P, ct.POINTER(Mat), ct.POINTER(Mat), ct.POINTER(Mat),
+                                     ct.POINTER(Payload), _P]),
+    "svdw_svd_witness": (_i32, [_P, _P, _P, _P, _P, _u32, _u32, _i32, ct.POINTER(SvdConfig), _P,
+                                ct.POINTER(Counts)]),
+    "svdw_profile_enable": (_i32, [_P, _i32]),
+    "svdw_profile_collect": (_i32, [_P, ct.POINTER(KStat), _u32, ct.POINTER(_u32)]),
+    "svdw_plan_svd": (_i32, [_u32, _u32, _u32, _u32, ct.POINTER(SvdConfig), ct.POINTER(Counts)]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libsvdw.so (raises if missing: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run `python -m halo2_svd041_amd.build` "
+                               "(hipcc --offload-arch=gfx950); no CPU fallback exists")
+        L = ct.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != SVDW_OK:
+        raise SvdwError(rc, lib().svdw_last_error().decode())

@@ -1,0 +1,1022 @@
+// Host engine + C ABI (include/svdw.h) of the SVD-verify witness engine.
+//
+// Each reference function (src/matrix/mod.rs, src/svd/mod.rs) becomes:
+//   1. a data-independent cell program built on the host by replaying the
+//      halo2-base gadget sequence symbolically (PB below), and
+//   2. one launch of the generic stage kernel over the elements, or the
+//      dedicated GEMM / inner-product-row kernels.
+// Offsets in the per-phase streams are known at enqueue time, so all work is
+// asynchronous on the context's HIP stream. A context created with
+// device = -1 is a "dry" planner: identical control flow, no device work,
+// which is how svdw_plan_svd gets exact closed-form counts.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/svdw.h"
+#include "kernels.hpp"
+
+using namespace svdw;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+struct SvdwError {
+    int code;
+    std::string msg;
+};
+[[noreturn]] static void fail(int code, const std::string& msg) { throw SvdwError{code, msg}; }
+static void hipck(hipError_t e, const char* what) {
+    if (e != hipSuccess) fail(SVDW_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+template <class F>
+static int guarded(F&& f) {
+    try {
+        f();
+        return SVDW_OK;
+    } catch (const SvdwError& e) {
+        g_err = e.msg;
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_err = "out of host memory";
+        return SVDW_ENOMEM;
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return SVDW_EINVAL;
+    }
+}
+#define REQUIRE(cond, msg) \
+    do {                   \
+        if (!(cond)) fail(SVDW_EINVAL, msg); \
+    } while (0)
+
+// ------------------------------------------------------- host big integers
+// Unsigned 256-bit integers (BigUint bounds of the range checks).
+struct BigU {
+    Fr v;
+};
+static BigU big_from_words(const uint64_t w[4]) {
+    BigU b;
+    for (int i = 0; i < 4; ++i) {
+        b.v.w[2 * i] = (uint32_t)w[i];
+        b.v.w[2 * i + 1] = (uint32_t)(w[i] >> 32);
+    }
+    return b;
+}
+static BigU big_from_u128(unsigned __int128 x) {
+    BigU b;
+    b.v = fr_zero();
+    for (int i = 0; i < 4; ++i) b.v.w[i] = (uint32_t)(x >> (32 * i));
+    return b;
+}
+static int big_bits(const BigU& b) {
+    for (int i = 7; i >= 0; --i)
+        if (b.v.w[i]) return 32 * i + 32 - __builtin_clz(b.v.w[i]);
+    return 0;
+}
+static bool big_is_zero(const BigU& b) { return big_bits(b) == 0; }
+static BigU big_add_u32(const BigU& a, uint32_t s) {
+    BigU r;
+    Fr t = fr_from_u64(s);
+    if (add256(r.v, a.v, t)) fail(SVDW_ERANGE, "bound overflows 256 bits");
+    return r;
+}
+static BigU big_sub_u32(const BigU& a, uint32_t s) {
+    BigU r;
+    Fr t = fr_from_u64(s);
+    if (sub256(r.v, a.v, t)) fail(SVDW_EINVAL, "bound underflow (bound must be >= 1)");
+    return r;
+}
+static BigU big_shl1(const BigU& a) {
+    BigU r;
+    if (a.v.w[7] >> 31) fail(SVDW_ERANGE, "bound overflows 256 bits");
+    for (int i = 7; i > 0; --i) r.v.w[i] = (a.v.w[i] << 1) | (a.v.w[i - 1] >> 31);
+    r.v.w[0] = a.v.w[0] << 1;
+    return r;
+}
+// biguint_to_fe: value mod p.
+static Fr big_to_fr(const BigU& b) {
+    Fr x = b.v, t;
+    while (!sub256(t, x, fr_p())) x = t;   // at most a few subtractions (< 2^256)
+    return x;
+}
+static Fr pow2_fr(uint32_t k) {
+    Fr x = fr_from_u64(1);
+    for (uint32_t i = 0; i < k; ++i) x = fr_add(x, x);
+    return x;
+}
+static Fr fr_from_words(const uint64_t w[4]) { return big_to_fr(big_from_words(w)); }
+
+// ------------------------------------------------------- program builder
+// Replays halo2-base 0.4.1 gadgets on symbolic per-element values
+// (SURVEY.md Appendix A); produces the micro-ops, cell and lookup slot ops.
+struct PB {
+    StageArgs a;
+    uint32_t lb;
+    explicit PB(uint32_t lookup_bits) : lb(lookup_bits) { memset(&a, 0, sizeof(a)); }
+
+    uint8_t newv() {
+        if (a.nv >= (uint32_t)kMaxV) fail(SVDW_ERANGE, "stage needs too many element values");
+        return (uint8_t)a.nv++;
+    }
+    uint8_t kidx(const Fr& c) {
+        for (uint32_t k = 0; k < a.nk; ++k)
+            if (fr_eq(a.K[k], c)) return (uint8_t)k;
+        if (a.nk >= (uint32_t)kMaxK) fail(SVDW_ERANGE, "stage needs too many constants");
+        a.K[a.nk] = c;
+        return (uint8_t)a.nk++;
+    }
+    uint8_t K(const Fr& c) { return KSRC + kidx(c); }
+    uint8_t K(uint64_t c) { return K(fr_from_u64(c)); }
+    void op(uint8_t code, uint8_t dst, uint8_t x, uint8_t y, uint16_t p0 = 0, uint16_t p1 = 0) {
+        if (a.nmo >= (uint32_t)kMaxMicro) fail(SVDW_ERANGE, "stage needs too many micro-ops");
+        a.mo[a.nmo++] = MicroOp{code, dst, x, y, p0, p1};
+    }
+    static SlotOp slot(uint8_t src, uint32_t lo, uint32_t nbits) {
+        if (nbits >= 256) nbits = 0;
+        return SlotOp{src, (uint8_t)lo, (uint8_t)nbits, 0};
+    }
+    void cell(uint8_t src, uint32_t lo = 0, uint32_t nbits = 0) {
+        if (a.C >= (uint32_t)kMaxAdv) fail(SVDW_ERANGE, "stage has too many cells per element (raise lookup_bits)");
+        a.adv[a.C++] = slot(src, lo, nbits);
+    }
+    void look(uint8_t src, uint32_t lo = 0, uint32_t nbits = 0) {
+        if (a.L >= (uint32_t)kMaxLk) fail(SVDW_ERANGE, "stage has too many lookups per element (raise lookup_bits)");
+        a.lk[a.L++] = slot(src, lo, nbits);
+    }
+    // --- element values
+    uint8_t load(int view_idx) {
+        uint8_t v = newv();
+        op(MO_LOAD, v, (uint8_t)view_idx, 0);
+        return v;
+    }
+    uint8_t addk(uint8_t x, const Fr& k) {
+        uint8_t t = newv();
+        op(MO_ADDK, t, x, kidx(k));
+        return t;
+    }
+    // --- GateChip
+    uint8_t g_add_k(uint8_t x, const Fr& k) {       // add(x, Constant(k)): [x, k, 1, x+k]
+        uint8_t t = addk(x, k);
+        cell(x); cell(K(k)); cell(K(1)); cell(t);
+        return t;
+    }
+    uint8_t g_sub(uint8_t x, uint8_t y) {           // sub: [x-y, y, 1, x]
+        uint8_t d = newv();
+        op(MO_SUB, d, x, y);
+        cell(d); cell(y); cell(K(1)); cell(x);
+        return d;
+    }
+    uint8_t g_mul(uint8_t x, uint8_t y) {           // mul: [0, x, y, x*y]
+        uint8_t m = newv();
+        op(MO_MUL, m, x, y);
+        cell(K(0)); cell(x); cell(y); cell(m);
+        return m;
+    }
+    void g_is_equal(uint8_t x, uint8_t y) {         // sub + is_zero: 12 cells
+        uint8_t d = g_sub(x, y);
+        uint8_t z = newv();
+        uint8_t inv = newv();
+        (void)inv;
+        op(MO_ISZERO, z, d, 0);
+        cell(z); cell(d); cell((uint8_t)(z + 1)); cell(K(1));
+        cell(K(0)); cell(d); cell(z); cell(K(0));
+    }
+    // --- RangeChip::range_check
+    void range_check(uint8_t v, uint32_t bits) {
+        if (bits == 0) return;    // assert_is_const(a, 0): no cells
+        if (bits > 254 + lb) fail(SVDW_ERANGE, "range_check bits too large");
+        const uint32_t n = (bits + lb - 1) / lb, rem = bits % lb;
+        uint8_t lsrc = v;
+        uint32_t llo = 0, lnb = 0;
+        if (n == 1) {
+            look(v);
+        } else {
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint32_t lo = i * lb;
+                uint8_t src = v;
+                uint32_t slo = lo, snb = lb;
+                if (lo >= 256) { src = K(0); slo = 0; snb = 0; }
+                if (i == 0) {
+                    cell(src, slo, snb);
+                } else {
+                    cell(src, slo, snb);
+                    cell(K(pow2_fr(lo)));
+                    cell(v, 0, (i + 1) * lb);    // running sum = v mod 2^((i+1) lb)
+                }
+                look(src, slo, snb);
+                lsrc = src; llo = slo; lnb = snb;
+            }
+        }
+        if (rem == 1) {                             // assert_bit: [0, l, l, l]
+            cell(K(0)); cell(lsrc, llo, lnb); cell(lsrc, llo, lnb); cell(lsrc, llo, lnb);
+        } else if (rem > 1) {                       // mul(last, 2^(lb-rem)), looked up
+            const uint32_t sh = lb - rem;
+            uint8_t m = newv();
+            if (n == 1) op(MO_FDBL, m, v, (uint8_t)sh);
+            else if ((n - 1) * lb >= 256) op(MO_ADDK, m, v, kidx(fr_zero()));   // unreachable in practice
+            else op(MO_LIMBSHL, m, v, (uint8_t)sh, (uint16_t)((n - 1) * lb), (uint16_t)lb);
+            cell(K(0)); cell(lsrc, llo, lnb); cell(K(pow2_fr(sh))); cell(m);
+            look(m);
+        }
+    }
+    // --- RangeChip::check_less_than(a, Constant(b), bits)
+    void check_less_than_k(uint8_t x, const BigU& b, uint32_t bits) {
+        Fr pw = pow2_fr(bits), bf = big_to_fr(b);
+        uint8_t t3 = addk(x, pw);                  // a + 2^bits
+        uint8_t t2 = addk(t3, fr_neg(bf));         // a + 2^bits - b
+        cell(t2); cell(K(bf)); cell(K(1)); cell(t3); cell(K(fr_neg(pw))); cell(K(1)); cell(x);
+        range_check(t2, bits);
+    }
+    void check_big_less_than_safe(uint8_t x, const BigU& bnd) {
+        uint32_t rb = (big_bits(bnd) + lb - 1) / lb * lb;
+        range_check(x, rb);
+        check_less_than_k(x, bnd, rb);
+    }
+    // check_abs_less_than (src/matrix/mod.rs:425-435)
+    void check_abs_less_than(uint8_t x, const BigU& bnd) {
+        if (big_is_zero(bnd)) fail(SVDW_EINVAL, "check_abs_less_than: bound must be >= 1");
+        BigU nb = big_sub_u32(big_shl1(bnd), 1);
+        uint8_t t = g_add_k(x, big_to_fr(big_sub_u32(bnd, 1)));
+        check_big_less_than_safe(t, nb);
+    }
+};
+
+// -------------------------------------------------------------- context
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+struct Stream {
+    Fr* adv = nullptr;
+    uint64_t n = 0, cap = 0;
+    Fr* lk = nullptr;
+    uint64_t nl = 0, lcap = 0;
+};
+struct svdw_ctx {
+    int device = -1;
+    bool dry = true;
+    hipStream_t st = nullptr;
+    uint32_t P = 32, LB = 19;
+    Stream ph[2];
+    DBuf f64in, digA, digB, w1c, w1m, w2c, w2m, bits;
+    // built-in event profiler (svdw_profile_*): one start/stop event pair per launch
+    bool prof = false;
+    struct Rec {
+        std::string name;
+        double bytes, ops;
+        hipEvent_t e0, e1;
+    };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+};
+
+static void sync(svdw_ctx* c) {
+    if (!c->dry) hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
+}
+// RAII: brackets one kernel launch with HIP events on the context stream.
+struct ProfScope {
+    svdw_ctx* c;
+    long idx = -1;
+    static hipEvent_t ev(svdw_ctx* c) {
+        if (!c->pool.empty()) {
+            hipEvent_t e = c->pool.back();
+            c->pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        hipck(hipEventCreate(&e), "hipEventCreate");
+        return e;
+    }
+    ProfScope(svdw_ctx* cc, const std::string& name, double bytes, double ops) : c(cc) {
+        if (!c->prof || c->dry) return;
+        svdw_ctx::Rec r{name, bytes, ops, ev(c), ev(c)};
+        hipck(hipEventRecord(r.e0, c->st), "hipEventRecord");
+        c->recs.push_back(r);
+        idx = (long)c->recs.size() - 1;
+    }
+    ~ProfScope() {
+        if (idx >= 0) (void)hipEventRecord(c->recs[idx].e1, c->st);
+    }
+};
+
+static void ensure_buf(svdw_ctx* c, DBuf& b, size_t bytes) {
+    if (c->dry || b.cap >= bytes) return;
+    sync(c);
+    if (b.p) hipck(hipFree(b.p), "hipFree");
+    b.p = nullptr;
+    size_t cap = std::max(bytes, b.cap + b.cap / 2);
+    if (hipMalloc(&b.p, cap) != hipSuccess) {
+        b.cap = 0;
+        fail(SVDW_ENOMEM, "device allocation failed (scratch)");
+    }
+    b.cap = cap;
+}
+static void grow(svdw_ctx* c, Fr*& ptr, uint64_t used, uint64_t& cap, uint64_t need) {
+    if (c->dry || need <= cap) return;
+    uint64_t ncap = std::max(need, cap + cap / 2);
+    Fr* np = nullptr;
+    if (hipMalloc((void**)&np, ncap * sizeof(Fr)) != hipSuccess)
+        fail(SVDW_ENOMEM, "device allocation failed (cell stream of " + std::to_string(ncap) + " cells)");
+    if (ptr) {
+        hipck(hipMemcpyAsync(np, ptr, used * sizeof(Fr), hipMemcpyDeviceToDevice, c->st), "copy");
+        sync(c);
+        hipck(hipFree(ptr), "hipFree");
+    }
+    ptr = np;
+    cap = ncap;
+}
+// Append n advice and nl lookup cells to a phase; returns their offsets.
+static void append(svdw_ctx* c, uint32_t phase, uint64_t n, uint64_t nl, uint64_t* off,
+                   uint64_t* loff) {
+    REQUIRE(phase < 2, "phase must be 0 or 1");
+    Stream& s = c->ph[phase];
+    grow(c, s.adv, s.n, s.cap, s.n + n);
+    grow(c, s.lk, s.nl, s.lcap, s.nl + nl);
+    *off = s.n;
+    if (loff) *loff = s.nl;
+    s.n += n;
+    s.nl += nl;
+}
+static Fr* cellp(svdw_ctx* c, uint32_t phase, uint64_t off) { return c->ph[phase].adv + off; }
+
+// --------------------------------------------------------------- views
+static DView view_of(svdw_ctx* c, const svdw_mat& m) {
+    DView v;
+    memset(&v, 0, sizeof v);
+    v.ptr = c->dry ? nullptr : cellp(c, m.phase, m.off);
+    v.rs = m.rs;
+    v.cs = m.cs;
+    v.rows = m.rows;
+    v.cols = m.cols;
+    v.mode = VIEW_STRIDED;
+    return v;
+}
+static svdw_mat mat_of_vec(const svdw_vec& v) {   // len x 1 column
+    return svdw_mat{v.phase, v.len, 1, v.off, v.stride, 0};
+}
+static void check_mat(const svdw_ctx* c, const svdw_mat& m) {
+    REQUIRE(m.phase < 2, "matrix phase must be 0 or 1");
+    REQUIRE(m.rows >= 1 && m.cols >= 1, "empty matrix");
+    // every referenced cell must already exist
+    int64_t lo = (int64_t)m.off, hi = (int64_t)m.off;
+    int64_t er = (int64_t)(m.rows - 1) * m.rs, ec = (int64_t)(m.cols - 1) * m.cs;
+    lo += std::min<int64_t>(er, 0) + std::min<int64_t>(ec, 0);
+    hi += std::max<int64_t>(er, 0) + std::max<int64_t>(ec, 0);
+    REQUIRE(lo >= 0 && (uint64_t)hi < c->ph[m.phase].n, "matrix view outside its phase stream");
+}
+static void check_vec(const svdw_ctx* c, const svdw_vec& v) { check_mat(c, mat_of_vec(v)); }
+
+// ------------------------------------------------------- stage launches
+// Appends the stage's cells for `nelem` elements; returns the advice offset.
+static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, uint32_t cols,
+                          const char* tag, uint64_t* loff_out = nullptr) {
+    StageArgs& a = pb.a;
+    uint64_t off = 0, loff = 0;
+    append(c, phase, (uint64_t)nelem * a.C, (uint64_t)nelem * a.L, &off, &loff);
+    if (loff_out) *loff_out = loff;
+    if (c->dry || nelem == 0) return off;
+    a.out_adv = cellp(c, phase, off);
+    a.out_lk = a.L ? c->ph[phase].lk + loff : nullptr;
+    a.e_begin = 0;
+    a.e_end = nelem;
+    a.cols = cols ? cols : 1;
+    a.cdiv_magic = a.C ? ((1ull << 32) + a.C - 1) / a.C : 0;
+    a.ldiv_magic = a.L ? ((1ull << 32) + a.L - 1) / a.L : 0;
+    uint32_t loads = 0;
+    for (uint32_t i = 0; i < a.nmo; ++i) loads += a.mo[i].op == MO_LOAD;
+    {
+        ProfScope ps(c, std::string("k_stage:") + tag,
+                     32.0 * nelem * ((double)a.C + a.L + loads), 0);
+        hipck(launch_stage(a, c->st), "k_stage");
+    }
+    return off;
+}
+static svdw_vec put_cell(svdw_ctx* c, uint32_t phase, const Fr& v) {   // load_witness/load_constant
+    PB pb(c->LB);
+    pb.cell(pb.K(v));
+    uint64_t off = run_stage(c, phase, pb, 1, 1, "load_cell");
+    return svdw_vec{phase, 1, off, 1};
+}
+
+// ----------------------------------------------------- reference functions
+static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, uint32_t rows,
+                             uint32_t cols, bool on_device) {
+    REQUIRE(rows >= 1 && cols >= 1, "ZkMatrix::new: empty matrix");
+    REQUIRE(data || c->dry, "null data");
+    uint64_t n = (uint64_t)rows * cols, off;
+    append(c, phase, n, 0, &off, nullptr);
+    if (!c->dry) {
+        const double* src = data;
+        if (!on_device) {
+            ensure_buf(c, c->f64in, n * sizeof(double));
+            hipck(hipMemcpyAsync(c->f64in.p, data, n * sizeof(double), hipMemcpyHostToDevice, c->st),
+                  "H2D");
+            src = (const double*)c->f64in.p;
+        }
+        ProfScope ps(c, "k_quantize", 40.0 * n, 0);
+        hipck(launch_quantize(src, n, cellp(c, phase, off), (int)c->P, c->st), "k_quantize");
+    }
+    return svdw_mat{phase, rows, cols, off, (int64_t)cols, 1};
+}
+
+// ZkVector::entries_less_than
+static void entries_less_than(svdw_ctx* c, const svdw_vec& d, uint32_t bits) {
+    PB pb(c->LB);
+    pb.a.view[0] = view_of(c, mat_of_vec(d));
+    pb.range_check(pb.load(0), bits);
+    run_stage(c, d.phase, pb, d.len, 1, "entries_less_than");
+}
+// ZkVector::entries_in_desc_order: all qsub(d_i, d_{i+1}) first, then range checks.
+static void entries_in_desc_order(svdw_ctx* c, const svdw_vec& d, uint32_t bits) {
+    REQUIRE(d.len >= 1, "entries_in_desc_order: empty vector");   // reference: 0..len-1 underflow
+    if (d.len == 1) return;
+    uint32_t n = d.len - 1;
+    PB sb(c->LB);
+    svdw_vec d1 = d;
+    d1.off = d.off + d.stride;
+    d1.len = n;
+    svdw_vec d0 = d;
+    d0.len = n;
+    sb.a.view[0] = view_of(c, mat_of_vec(d0));
+    sb.a.view[1] = view_of(c, mat_of_vec(d1));
+    uint8_t x = sb.load(0), y = sb.load(1);
+    sb.g_sub(x, y);
+    uint64_t soff = run_stage(c, d.phase, sb, n, 1, "desc_order_sub");
+    PB rb(c->LB);
+    rb.a.view[0] = view_of(c, mat_of_vec(svdw_vec{d.phase, n, soff, 4}));
+    rb.range_check(rb.load(0), bits);
+    run_stage(c, d.phase, rb, n, 1, "desc_order_range");
+}
+static void check_mat_entries_bounded(svdw_ctx* c, const svdw_mat& a, const BigU& bnd) {
+    PB pb(c->LB);
+    pb.a.view[0] = view_of(c, a);
+    pb.check_abs_less_than(pb.load(0), bnd);
+    run_stage(c, a.phase, pb, a.rows * a.cols, a.cols, "check_mat_entries_bounded");
+}
+// check_mat_diff on arbitrary views (a may be zero-padded, b may be diagonal).
+static void check_mat_diff_views(svdw_ctx* c, uint32_t phase, const DView& a, const DView& b,
+                                 uint32_t rows, uint32_t cols, const BigU& tol) {
+    PB pb(c->LB);
+    pb.a.view[0] = a;
+    pb.a.view[1] = b;
+    uint8_t x = pb.load(0), y = pb.load(1);
+    uint8_t dlt = pb.g_sub(x, y);
+    pb.check_abs_less_than(dlt, tol);
+    // pad / diag constants referenced by the views
+    pb.a.view[0].pad_k = pb.kidx(fr_zero());
+    pb.a.view[1].pad_k = pb.kidx(fr_zero());
+    run_stage(c, phase, pb, rows * cols, cols, "check_mat_diff");
+}
+static void check_mat_id(svdw_ctx* c, const svdw_mat& a, const svdw_vec& sid, const BigU& tol) {
+    put_cell(c, a.phase, fr_zero());                      // let zero = ctx.load_constant(F::ZERO)
+    DView b;
+    memset(&b, 0, sizeof b);
+    b.mode = VIEW_DIAG;
+    b.ptr = c->dry ? nullptr : cellp(c, sid.phase, sid.off);
+    b.rows = a.rows;
+    b.cols = a.cols;
+    check_mat_diff_views(c, a.phase, view_of(c, a), b, a.rows, a.cols, tol);
+}
+static svdw_mat mat_times_diag_mat(svdw_ctx* c, const svdw_mat& a, const svdw_vec& v) {
+    REQUIRE(v.len <= a.cols, "mat_times_diag_mat: v longer than a's rows");
+    PB pb(c->LB);
+    pb.a.view[0] = view_of(c, a);
+    pb.a.view[1] = view_of(c, svdw_mat{v.phase, a.rows, v.len, v.off, 0, v.stride});
+    uint8_t x = pb.load(0), y = pb.load(1);
+    pb.g_mul(x, y);
+    uint64_t off = run_stage(c, a.phase, pb, a.rows * v.len, v.len, "mat_times_diag_mat");
+    return svdw_mat{a.phase, a.rows, v.len, off + 3, (int64_t)4 * v.len, 4};
+}
+
+// Balanced base-256 digits needed for |x| < 2^bits.
+static int digits_for_bits(uint32_t bits) {
+    for (int D = 1; D <= 16; ++D) {
+        // max representable magnitude 127 * (256^D - 1) / 255 >= 2^bits - 1 ?
+        long double maxv = 127.0L * (powl(256.0L, D) - 1.0L) / 255.0L;
+        if (maxv >= powl(2.0L, bits) - 1.0L) return D;
+    }
+    return 99;
+}
+static int round_digits(int need) {
+    if (need <= 5) return 5;
+    if (need <= 8) return 8;
+    if (need <= 9) return 9;
+    return 0;
+}
+static bool is_transpose_of(const svdw_mat& b, const svdw_mat& a) {
+    return a.phase == b.phase && a.off == b.off && a.rows == b.cols && a.cols == b.rows &&
+           a.rs == b.cs && a.cs == b.rs;
+}
+static std::vector<uint32_t> maxbits_many(svdw_ctx* c, const std::vector<svdw_mat>& ms) {
+    std::vector<uint32_t> out(ms.size(), 0);
+    if (c->dry || ms.empty()) return out;
+    ensure_buf(c, c->bits, 64 * sizeof(unsigned));
+    hipck(hipMemsetAsync(c->bits.p, 0, ms.size() * sizeof(unsigned), c->st), "memset");
+    for (size_t i = 0; i < ms.size(); ++i)
+        hipck(launch_maxbits(view_of(c, ms[i]), ms[i].rows, ms[i].cols, (unsigned*)c->bits.p + i,
+                             c->st), "k_maxbits");
+    std::vector<unsigned> h(ms.size());
+    hipck(hipMemcpyAsync(h.data(), c->bits.p, ms.size() * sizeof(unsigned), hipMemcpyDeviceToHost,
+                         c->st), "D2H");
+    sync(c);
+    for (size_t i = 0; i < ms.size(); ++i) out[i] = h[i];
+    return out;
+}
+// honest_prover_mat_mul (+ field_mat_mul). bits_a/bits_b: known bounds or ~0u.
+static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a,
+                                      const svdw_mat& b, uint32_t bits_a = ~0u,
+                                      uint32_t bits_b = ~0u) {
+    REQUIRE(a.cols == b.rows, "honest_prover_mat_mul: a.num_col != b.num_rows");
+    const uint32_t N = a.rows, K = a.cols, M = b.cols;
+    uint64_t off;
+    append(c, phase, (uint64_t)N * M, 0, &off, nullptr);
+    svdw_mat cs{phase, N, M, off, (int64_t)M, 1};
+    if (c->dry) return cs;
+    const bool sym = is_transpose_of(b, a);
+    if (bits_a == ~0u || bits_b == ~0u) {
+        std::vector<svdw_mat> ms{a};
+        if (!sym) ms.push_back(b);
+        auto bb = maxbits_many(c, ms);
+        bits_a = bb[0];
+        bits_b = sym ? bb[0] : bb[1];
+    }
+    int DA = round_digits(digits_for_bits(bits_a)), DB = round_digits(digits_for_bits(bits_b));
+    Fr* out = cellp(c, phase, off);
+    if (DA && DB && K <= 8192 && gemm_digits_supported(DA, DB)) {
+        const uint32_t kg = ((K + 3) / 4 + 7) / 8 * 8;
+        const uint32_t npad = (N + 31) / 32 * 32, mpad = (M + 31) / 32 * 32;
+        ensure_buf(c, c->digA, (size_t)npad * kg * DA * 4);
+        {
+            ProfScope ps(c, "k_to_digits", 32.0 * N * K + 4.0 * npad * kg * DA, 0);
+            hipck(launch_to_digits(view_of(c, a), N, K, DA, npad, kg, (uint32_t*)c->digA.p, c->st),
+                  "k_to_digits");
+        }
+        const uint32_t* Bd = (const uint32_t*)c->digA.p;
+        if (!sym) {
+            ensure_buf(c, c->digB, (size_t)mpad * kg * DB * 4);
+            svdw_mat bt = b;   // Bt(j, k) = b(k, j)
+            bt.rows = b.cols; bt.cols = b.rows; bt.rs = b.cs; bt.cs = b.rs;
+            ProfScope ps(c, "k_to_digits", 32.0 * M * K + 4.0 * mpad * kg * DB, 0);
+            hipck(launch_to_digits(view_of(c, bt), M, K, DB, mpad, kg, (uint32_t*)c->digB.p,
+                                   c->st), "k_to_digits");
+            Bd = (const uint32_t*)c->digB.p;
+        }
+        ProfScope ps(c, std::string("k_gemm_dot4:") + std::to_string(DA) + "x" + std::to_string(DB) +
+                            (sym ? "s" : ""),
+                     4.0 * kg * ((double)npad * DA + (sym ? 0.0 : (double)mpad * DB)) + 32.0 * N * M,
+                     (double)N * M * K);
+        hipck(launch_gemm_digits(DA, DB, sym, (const uint32_t*)c->digA.p, Bd, N, M, kg, out, M, 1,
+                                 c->st), "k_gemm_dot4");
+    } else {
+        ProfScope ps(c, "k_gemm_mont", 32.0 * ((double)N * K + (double)K * M + (double)N * M),
+                     (double)N * M * K);
+        hipck(launch_gemm_mont(view_of(c, a), view_of(c, b), N, K, M, out, M, 1, c->st),
+              "k_gemm_mont");
+    }
+    return cs;
+}
+// field_mat_vec_mul with the vector given as canonical + Montgomery copies.
+static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const Fr* wc,
+                            const Fr* wm) {
+    const uint32_t R = a.rows, L = a.cols;
+    uint64_t off;
+    append(c, phase, (uint64_t)R * (3ull * L + 1), 0, &off, nullptr);
+    if (!c->dry) {
+        ProfScope ps(c, "k_matvec_scan", 32.0 * (double)R * (4.0 * L + 1) + 64.0 * L, (double)R * L);
+        hipck(launch_matvec_scan(view_of(c, a), 0, R, L, wc, wm, cellp(c, phase, off), c->st),
+              "k_matvec_scan");
+    }
+    return svdw_vec{phase, R, off + 3ull * L, (int64_t)(3ull * L + 1)};
+}
+static void vec_prep(svdw_ctx* c, const svdw_vec& v, DBuf& bc, DBuf& bm) {
+    ensure_buf(c, bc, (size_t)v.len * sizeof(Fr));
+    ensure_buf(c, bm, (size_t)v.len * sizeof(Fr));
+    if (c->dry) return;
+    hipck(launch_vec_prep(view_of(c, svdw_mat{v.phase, 1, v.len, v.off, 0, v.stride}), v.len,
+                          (Fr*)bc.p, (Fr*)bm.p, c->st), "k_vec_prep");
+}
+static svdw_vec field_mat_vec_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a,
+                                  const svdw_vec& v) {
+    REQUIRE(a.cols == v.len, "field_mat_vec_mul: a[0].len() != v.len()");
+    vec_prep(c, v, c->w1c, c->w1m);
+    return matvec_rows(c, phase, a, (const Fr*)c->w1c.p, (const Fr*)c->w1m.p);
+}
+// ZkMatrix::verify_mul
+static void verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svdw_mat& b,
+                       const svdw_mat& cs, const Fr& gamma) {
+    REQUIRE(a.cols == b.rows, "verify_mul: a.num_col != b.num_rows");
+    REQUIRE(cs.rows == a.rows, "verify_mul: c_s.len() != a.num_rows");
+    REQUIRE(cs.cols == b.cols, "verify_mul: c_s[0].len() != b.num_col");
+    const uint32_t d = cs.cols, n = a.rows, k = a.cols;
+    put_cell(c, phase, fr_from_u64(1));                    // load_witness(F::ONE)
+    if (d > 1) {                                          // v_i = v_{i-1} * init_rand
+        PB pb(c->LB);
+        uint8_t kg = pb.kidx(gamma);
+        uint8_t prev = pb.newv(), cur = pb.newv();
+        pb.op(MO_POWK, prev, kg, 0, 0);
+        pb.op(MO_POWK, cur, kg, 0, 1);
+        pb.cell(pb.K(0)); pb.cell(prev); pb.cell(KSRC + kg); pb.cell(cur);
+        run_stage(c, phase, pb, d - 1, 1, "verify_mul_gamma_pows");
+    }
+    ensure_buf(c, c->w1c, (size_t)d * sizeof(Fr));
+    ensure_buf(c, c->w1m, (size_t)d * sizeof(Fr));
+    if (!c->dry) hipck(launch_gamma_vec(gamma, d, (Fr*)c->w1c.p, (Fr*)c->w1m.p, c->st), "k_gamma_vec");
+    svdw_vec csv = matvec_rows(c, phase, cs, (const Fr*)c->w1c.p, (const Fr*)c->w1m.p);
+    svdw_vec bv = matvec_rows(c, phase, b, (const Fr*)c->w1c.p, (const Fr*)c->w1m.p);
+    vec_prep(c, bv, c->w2c, c->w2m);
+    svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, (const Fr*)c->w2m.p);
+    (void)k;
+    PB pb(c->LB);                                         // is_equal per row (unconstrained result)
+    pb.a.view[0] = view_of(c, mat_of_vec(csv));
+    pb.a.view[1] = view_of(c, mat_of_vec(abv));
+    uint8_t x = pb.load(0), y = pb.load(1);
+    pb.g_is_equal(x, y);
+    run_stage(c, phase, pb, n, 1, "verify_mul_is_equal");
+}
+
+// err_calc (src/svd/mod.rs:155-163). Host f64, built with -ffp-contract=off.
+static void err_calc(uint32_t p, uint64_t size, double max_norm, double eps_svd, double eps_u,
+                     double* es, double* eu) {
+    volatile double precision = pow(2.0, -1.0 * ((double)p + 1.0));
+    double s = (double)size;
+    *es = precision * s * (1.0 + max_norm + eps_svd + precision) + s * max_norm * precision +
+          pow(1.0 + eps_u, 0.5) * (max_norm + eps_svd) * eps_u + pow(1.0 + eps_u, 0.5) * eps_svd;
+    *eu = eps_u + precision * s * (2.0 * (1.0 + eps_u) + precision);
+}
+// `(err * (2u128.pow(2P) as f64)).round() as u128`
+static BigU scale_err(double err, uint32_t p) {
+    double x = round(err * ldexp(1.0, 2 * (int)p));
+    if (!(x > 0)) return big_from_u128(0);
+    if (x >= 340282366920938463463374607431768211456.0) return big_from_u128(~(unsigned __int128)0);
+    return big_from_u128((unsigned __int128)x);
+}
+
+// check_svd_phase0
+static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u,
+                                         const svdw_mat& v, const svdw_vec& d, double err_svd,
+                                         double err_u, uint32_t max_bits_d,
+                                         const uint32_t* known_bits = nullptr) {
+    REQUIRE(m.rows == u.rows, "check_svd_phase0: m.num_rows != u.num_rows");
+    REQUIRE(m.cols == v.rows, "check_svd_phase0: m.num_col != v.num_rows");
+    REQUIRE(u.rows == u.cols, "check_svd_phase0: u not square");
+    REQUIRE(v.rows == v.cols, "check_svd_phase0: v not square");
+    const uint32_t N = m.rows, M = m.cols, r = std::min(N, M);
+    REQUIRE(d.len == r, "check_svd_phase0: d.len != min(N, M)");
+    const uint32_t P = c->P;
+    const uint32_t max_bits = max_bits_d + P;
+    entries_less_than(c, d, max_bits);
+    entries_in_desc_order(c, d, max_bits);
+    BigU unit = big_from_u128(((unsigned __int128)1 << P) + 1);
+    check_mat_entries_bounded(c, u, unit);
+    check_mat_entries_bounded(c, v, unit);
+    svdw_mat ut = u, vt = v;
+    std::swap(ut.rows, ut.cols); std::swap(ut.rs, ut.cs);
+    std::swap(vt.rows, vt.cols); std::swap(vt.rs, vt.cs);
+    DView udv;
+    if (r == M) {
+        udv = view_of(c, mat_times_diag_mat(c, u, d));
+    } else {
+        put_cell(c, 0 + u.phase, fr_zero());              // zero padding constant
+        svdw_mat ud = mat_times_diag_mat(c, u, d);
+        udv = view_of(c, ud);
+        udv.cols = r;                                     // columns >= N read as 0
+    }
+    udv.rows = N;
+    uint32_t bm = ~0u, bu = ~0u, bv = ~0u;
+    if (known_bits) { bm = known_bits[0]; bu = known_bits[1]; bv = known_bits[2]; }
+    svdw_mat mvt = honest_prover_mat_mul(c, m.phase, m, vt, bm, bv);
+    BigU es = scale_err(err_svd, P), eu = scale_err(err_u, P);
+    check_mat_diff_views(c, m.phase, udv, view_of(c, mvt), N, M, es);
+    Fr q = pow2_fr(P);
+    svdw_vec q2 = put_cell(c, m.phase, fr_mul(q, q));
+    svdw_mat uut = honest_prover_mat_mul(c, m.phase, u, ut, bu, bu);
+    check_mat_id(c, uut, q2, eu);
+    svdw_mat vvt = honest_prover_mat_mul(c, m.phase, v, vt, bv, bv);
+    check_mat_id(c, vvt, q2, eu);
+    return svdw_svd_payload{ut, vt, mvt, uut, vvt};
+}
+static void check_svd_phase1(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u, const svdw_mat& v,
+                             const svdw_svd_payload& pl, const Fr& g) {
+    verify_mul(c, 1, m, pl.v_t, pl.m_times_vt, g);
+    verify_mul(c, 1, u, pl.u_t, pl.u_times_ut, g);
+    verify_mul(c, 1, v, pl.v_t, pl.v_times_vt, g);
+}
+
+static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, const double* v,
+                               const double* d, uint32_t N, uint32_t M, bool on_device,
+                               const svdw_svd_config& cfg, const Fr& gamma) {
+    REQUIRE(N >= 1 && M >= 1, "empty matrix");
+    const uint32_t r = std::min(N, M);
+    for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
+    if (!c->dry) {
+        // exact sizes from the dry planner: no growth copies inside the step
+        svdw_ctx plan;
+        plan.P = c->P; plan.LB = c->LB;
+        svd_witness(&plan, nullptr, nullptr, nullptr, nullptr, N, M, false, cfg, gamma);
+        for (int p = 0; p < 2; ++p) {
+            grow(c, c->ph[p].adv, 0, c->ph[p].cap, plan.ph[p].n);
+            grow(c, c->ph[p].lk, 0, c->ph[p].lcap, plan.ph[p].nl);
+        }
+    }
+    svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device);
+    svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device);
+    svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device);
+    svdw_mat zdm = zkmatrix_new(c, 0, d, r, 1, on_device);
+    svdw_vec zd{0, r, zdm.off, 1};
+    double es, eu;
+    err_calc(c->P, std::max(N, M), cfg.max_norm, cfg.eps_svd, cfg.eps_u, &es, &eu);
+    auto bits = maxbits_many(c, {zm, zu, zv});
+    svdw_svd_payload pl = check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, bits.data());
+    check_svd_phase1(c, zm, zu, zv, pl, gamma);
+    return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
+}
+
+// ================================================================== C ABI
+extern "C" {
+
+const char* svdw_last_error(void) { return g_err.c_str(); }
+
+int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
+    return guarded([&] {
+        REQUIRE(p && out, "null argument");
+        if (p->precision_bits < 1 || p->precision_bits > 63)
+            fail(SVDW_ERANGE, "precision_bits must be in [1, 63] (src/svd/mod.rs:74 uses u64)");
+        if (p->lookup_bits < 8 || p->lookup_bits > 63)
+            fail(SVDW_ERANGE, "lookup_bits must be in [8, 63]");
+        svdw_ctx* c = new svdw_ctx();
+        c->P = p->precision_bits;
+        c->LB = p->lookup_bits;
+        c->device = p->device;
+        c->dry = p->device < 0;
+        if (!c->dry) {
+            hipError_t e = hipSetDevice(p->device);
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
+            if (e != hipSuccess) {
+                delete c;
+                fail(SVDW_EDEVICE, std::string("HIP device init failed: ") + hipGetErrorString(e));
+            }
+        }
+        *out = c;
+    });
+}
+int svdw_ctx_destroy(svdw_ctx* c) {
+    return guarded([&] {
+        if (!c) return;
+        if (!c->dry) {
+            (void)hipStreamSynchronize(c->st);
+            for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
+            for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->w1c, &c->w1m, &c->w2c, &c->w2m, &c->bits})
+                if (b->p) (void)hipFree(b->p);
+            for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
+            for (auto e : c->pool) (void)hipEventDestroy(e);
+            (void)hipStreamDestroy(c->st);
+        }
+        delete c;
+    });
+}
+int svdw_ctx_reset(svdw_ctx* c) {
+    return guarded([&] {
+        REQUIRE(c, "null ctx");
+        sync(c);
+        for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
+    });
+}
+int svdw_reserve(svdw_ctx* c, uint32_t phase, uint64_t na, uint64_t nl) {
+    return guarded([&] {
+        REQUIRE(c && phase < 2, "bad argument");
+        Stream& s = c->ph[phase];
+        grow(c, s.adv, s.n, s.cap, na);
+        grow(c, s.lk, s.nl, s.lcap, nl);
+    });
+}
+int svdw_sync(svdw_ctx* c) {
+    return guarded([&] { REQUIRE(c, "null ctx"); sync(c); });
+}
+uint64_t svdw_advice_len(const svdw_ctx* c, uint32_t phase) { return c && phase < 2 ? c->ph[phase].n : 0; }
+uint64_t svdw_lookup_len(const svdw_ctx* c, uint32_t phase) { return c && phase < 2 ? c->ph[phase].nl : 0; }
+const void* svdw_advice_device_ptr(const svdw_ctx* c, uint32_t phase) { return c && phase < 2 ? c->ph[phase].adv : nullptr; }
+const void* svdw_lookup_device_ptr(const svdw_ctx* c, uint32_t phase) { return c && phase < 2 ? c->ph[phase].lk : nullptr; }
+
+static int copy_cells(svdw_ctx* c, uint32_t phase, uint64_t off, uint64_t n, uint64_t* out, bool lk) {
+    return guarded([&] {
+        REQUIRE(c && phase < 2 && out, "bad argument");
+        REQUIRE(!c->dry, "planning context has no cells");
+        const Stream& s = c->ph[phase];
+        REQUIRE(off + n <= (lk ? s.nl : s.n), "copy range outside the stream");
+        if (!n) return;
+        hipck(hipMemcpyAsync(out, (lk ? s.lk : s.adv) + off, n * sizeof(Fr), hipMemcpyDeviceToHost,
+                             c->st), "D2H");
+        sync(c);
+    });
+}
+int svdw_copy_advice(svdw_ctx* c, uint32_t phase, uint64_t off, uint64_t n, uint64_t* out) {
+    return copy_cells(c, phase, off, n, out, false);
+}
+int svdw_copy_lookup(svdw_ctx* c, uint32_t phase, uint64_t off, uint64_t n, uint64_t* out) {
+    return copy_cells(c, phase, off, n, out, true);
+}
+
+int svdw_zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, uint32_t rows,
+                      uint32_t cols, int on_device, svdw_mat* out) {
+    return guarded([&] {
+        REQUIRE(c && out, "null argument");
+        *out = zkmatrix_new(c, phase, data, rows, cols, on_device != 0);
+    });
+}
+int svdw_zkvector_new(svdw_ctx* c, uint32_t phase, const double* data, uint32_t len, int on_device,
+                      svdw_vec* out) {
+    return guarded([&] {
+        REQUIRE(c && out, "null argument");
+        svdw_mat m = zkmatrix_new(c, phase, data, len, 1, on_device != 0);
+        *out = svdw_vec{phase, len, m.off, 1};
+    });
+}
+int svdw_transpose_matrix(const svdw_mat* a, svdw_mat* out) {
+    return guarded([&] {
+        REQUIRE(a && out, "null argument");
+        svdw_mat t = *a;
+        std::swap(t.rows, t.cols);
+        std::swap(t.rs, t.cs);
+        *out = t;
+    });
+}
+int svdw_load_witness(svdw_ctx* c, uint32_t phase, const uint64_t value[4], svdw_vec* out) {
+    return guarded([&] {
+        REQUIRE(c && value && out, "null argument");
+        *out = put_cell(c, phase, fr_from_words(value));
+    });
+}
+int svdw_load_constant(svdw_ctx* c, uint32_t phase, const uint64_t value[4], svdw_vec* out) {
+    return svdw_load_witness(c, phase, value, out);   // same cell value; constancy is a prover fact
+}
+int svdw_entries_less_than(svdw_ctx* c, const svdw_vec* d, uint32_t max_bits) {
+    return guarded([&] {
+        REQUIRE(c && d, "null argument");
+        check_vec(c, *d);
+        entries_less_than(c, *d, max_bits);
+    });
+}
+int svdw_entries_in_desc_order(svdw_ctx* c, const svdw_vec* d, uint32_t max_bits) {
+    return guarded([&] {
+        REQUIRE(c && d, "null argument");
+        check_vec(c, *d);
+        entries_in_desc_order(c, *d, max_bits);
+    });
+}
+int svdw_check_mat_entries_bounded(svdw_ctx* c, const svdw_mat* a, const uint64_t bnd[4]) {
+    return guarded([&] {
+        REQUIRE(c && a && bnd, "null argument");
+        check_mat(c, *a);
+        check_mat_entries_bounded(c, *a, big_from_words(bnd));
+    });
+}
+int svdw_check_mat_diff(svdw_ctx* c, const svdw_mat* a, const svdw_mat* b, const uint64_t tol[4]) {
+    return guarded([&] {
+        REQUIRE(c && a && b && tol, "null argument");
+        check_mat(c, *a);
+        check_mat(c, *b);
+        REQUIRE(a->rows == b->rows && a->cols == b->cols, "check_mat_diff: shape mismatch");
+        REQUIRE(a->phase == b->phase, "check_mat_diff: a and b in different phases");
+        check_mat_diff_views(c, a->phase, view_of(c, *a), view_of(c, *b), a->rows, a->cols,
+                             big_from_words(tol));
+    });
+}
+int svdw_check_mat_id(svdw_ctx* c, const svdw_mat* a, const svdw_vec* sid, const uint64_t tol[4]) {
+    return guarded([&] {
+        REQUIRE(c && a && sid && tol, "null argument");
+        check_mat(c, *a);
+        check_vec(c, *sid);
+        check_mat_id(c, *a, *sid, big_from_words(tol));
+    });
+}
+int svdw_mat_times_diag_mat(svdw_ctx* c, const svdw_mat* a, const svdw_vec* v, svdw_mat* out) {
+    return guarded([&] {
+        REQUIRE(c && a && v && out, "null argument");
+        check_mat(c, *a);
+        check_vec(c, *v);
+        *out = mat_times_diag_mat(c, *a, *v);
+    });
+}
+int svdw_honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_mat* a, const svdw_mat* b,
+                               svdw_mat* out) {
+    return guarded([&] {
+        REQUIRE(c && a && b && out, "null argument");
+        check_mat(c, *a);
+        check_mat(c, *b);
+        *out = honest_prover_mat_mul(c, phase, *a, *b);
+    });
+}
+int svdw_field_mat_vec_mul(svdw_ctx* c, uint32_t phase, const svdw_mat* a, const svdw_vec* v,
+                           svdw_vec* out) {
+    return guarded([&] {
+        REQUIRE(c && a && v && out, "null argument");
+        check_mat(c, *a);
+        check_vec(c, *v);
+        *out = field_mat_vec_mul(c, phase, *a, *v);
+    });
+}
+int svdw_verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat* a, const svdw_mat* b,
+                    const svdw_mat* cs, const uint64_t gamma[4]) {
+    return guarded([&] {
+        REQUIRE(c && a && b && cs && gamma, "null argument");
+        check_mat(c, *a);
+        check_mat(c, *b);
+        check_mat(c, *cs);
+        verify_mul(c, phase, *a, *b, *cs, fr_from_words(gamma));
+    });
+}
+int svdw_err_calc(uint32_t p, uint64_t size, double max_norm, double eps_svd, double eps_u,
+                  double* es, double* eu) {
+    return guarded([&] {
+        REQUIRE(es && eu, "null argument");
+        err_calc(p, size, max_norm, eps_svd, eps_u, es, eu);
+    });
+}
+int svdw_check_svd_phase0(svdw_ctx* c, const svdw_mat* m, const svdw_mat* u, const svdw_mat* v,
+                          const svdw_vec* d, double err_svd, double err_u, uint32_t max_bits_d,
+                          svdw_svd_payload* out) {
+    return guarded([&] {
+        REQUIRE(c && m && u && v && d && out, "null argument");
+        check_mat(c, *m); check_mat(c, *u); check_mat(c, *v); check_vec(c, *d);
+        REQUIRE(m->phase == 0 && u->phase == 0 && v->phase == 0 && d->phase == 0,
+                "check_svd_phase0 inputs must live in phase 0");
+        *out = check_svd_phase0(c, *m, *u, *v, *d, err_svd, err_u, max_bits_d);
+    });
+}
+int svdw_check_svd_phase1(svdw_ctx* c, const svdw_mat* m, const svdw_mat* u, const svdw_mat* v,
+                          const svdw_svd_payload* pl, const uint64_t gamma[4]) {
+    return guarded([&] {
+        REQUIRE(c && m && u && v && pl && gamma, "null argument");
+        check_svd_phase1(c, *m, *u, *v, *pl, fr_from_words(gamma));
+    });
+}
+int svdw_svd_witness(svdw_ctx* c, const double* m, const double* u, const double* v,
+                     const double* d, uint32_t N, uint32_t M, int on_device,
+                     const svdw_svd_config* cfg, const uint64_t gamma[4], svdw_counts* counts) {
+    return guarded([&] {
+        REQUIRE(c && cfg && gamma, "null argument");
+        REQUIRE(c->dry || (m && u && v && d), "null input matrix");
+        svdw_counts k = svd_witness(c, m, u, v, d, N, M, on_device != 0, *cfg, fr_from_words(gamma));
+        if (counts) *counts = k;
+    });
+}
+int svdw_profile_enable(svdw_ctx* c, int on) {
+    return guarded([&] {
+        REQUIRE(c, "null ctx");
+        sync(c);
+        for (auto& r : c->recs) { c->pool.push_back(r.e0); c->pool.push_back(r.e1); }
+        c->recs.clear();
+        c->prof = on != 0;
+    });
+}
+int svdw_profile_collect(svdw_ctx* c, svdw_kstat* out, uint32_t cap, uint32_t* n) {
+    return guarded([&] {
+        REQUIRE(c && n, "null argument");
+        sync(c);
+        std::vector<svdw_kstat> agg;
+        for (auto& r : c->recs) {
+            float ms = 0;
+            hipck(hipEventElapsedTime(&ms, r.e0, r.e1), "hipEventElapsedTime");
+            svdw_kstat* s = nullptr;
+            for (auto& x : agg)
+                if (r.name == x.name) s = &x;
+            if (!s) {
+                agg.emplace_back();
+                s = &agg.back();
+                memset(s, 0, sizeof(*s));
+                snprintf(s->name, sizeof(s->name), "%s", r.name.c_str());
+            }
+            s->launches += 1;
+            s->total_ms += ms;
+            s->bytes += r.bytes;
+            s->ops += r.ops;
+            if (ms > s->max_ms) s->max_ms = ms;
+            c->pool.push_back(r.e0);
+            c->pool.push_back(r.e1);
+        }
+        c->recs.clear();
+        *n = (uint32_t)agg.size();
+        if (out)
+            for (uint32_t i = 0; i < agg.size() && i < cap; ++i) out[i] = agg[i];
+    });
+}
+int svdw_plan_svd(uint32_t N, uint32_t M, uint32_t p, uint32_t lb, const svdw_svd_config* cfg,
+                  svdw_counts* counts) {
+    return guarded([&] {
+        REQUIRE(cfg && counts, "null argument");
+        if (p < 1 || p > 63) fail(SVDW_ERANGE, "precision_bits must be in [1, 63]");
+        if (lb < 8 || lb > 63) fail(SVDW_ERANGE, "lookup_bits must be in [8, 63]");
+        svdw_ctx plan;
+        plan.P = p;
+        plan.LB = lb;
+        *counts = svd_witness(&plan, nullptr, nullptr, nullptr, nullptr, N, M, false, *cfg, fr_zero());
+    });
+}
+
+}  // extern "C"

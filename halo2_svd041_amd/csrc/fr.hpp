@@ -1,0 +1,207 @@
+// BN254 scalar field Fr for host and gfx950 device code.
+//
+// Representation: 8 x u32 little-endian limbs. In memory a canonical Fr is
+// byte-identical to halo2curves' `Fr::to_repr()` (32-byte little endian),
+// which is the cell format of every advice / lookup stream this engine
+// writes. Montgomery form (x * 2^256 mod p) is used only inside products:
+// mont_mul(a_canonical, b_montgomery) == a*b canonical.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SVDW_HD __host__ __device__ __forceinline__
+
+namespace svdw {
+
+struct alignas(16) Fr {
+    uint32_t w[8];
+};
+
+// p = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+#define SVDW_P_WORDS 0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u, \
+                     0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u
+#define SVDW_R2_WORDS 0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u, \
+                      0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u
+static constexpr uint32_t kPinv32 = 0xefffffffu;   // -p^-1 mod 2^32
+
+SVDW_HD uint32_t p_word(int i) {
+    constexpr uint32_t P[8] = {SVDW_P_WORDS};
+    return P[i];
+}
+
+SVDW_HD Fr fr_zero() {
+    Fr r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = 0;
+    return r;
+}
+SVDW_HD Fr fr_from_u64(uint64_t x) {
+    Fr r = fr_zero();
+    r.w[0] = (uint32_t)x;
+    r.w[1] = (uint32_t)(x >> 32);
+    return r;
+}
+SVDW_HD Fr fr_p() {
+    Fr r;
+    constexpr uint32_t P[8] = {SVDW_P_WORDS};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = P[i];
+    return r;
+}
+SVDW_HD Fr fr_r2() {
+    Fr r;
+    constexpr uint32_t R2[8] = {SVDW_R2_WORDS};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = R2[i];
+    return r;
+}
+SVDW_HD bool fr_is_zero(const Fr& a) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x |= a.w[i];
+    return x == 0;
+}
+SVDW_HD bool fr_eq(const Fr& a, const Fr& b) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x |= a.w[i] ^ b.w[i];
+    return x == 0;
+}
+
+// r = a - b over 256 bits; returns borrow.
+SVDW_HD uint32_t sub256(Fr& r, const Fr& a, const Fr& b) {
+    uint64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t t = (uint64_t)a.w[i] - b.w[i] - br;
+        r.w[i] = (uint32_t)t;
+        br = (t >> 63) & 1;
+    }
+    return (uint32_t)br;
+}
+// r = a + b over 256 bits; returns carry.
+SVDW_HD uint32_t add256(Fr& r, const Fr& a, const Fr& b) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        c += (uint64_t)a.w[i] + b.w[i];
+        r.w[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    return (uint32_t)c;
+}
+
+// Canonical modular add/sub (inputs canonical, output canonical).
+SVDW_HD Fr fr_add(const Fr& a, const Fr& b) {
+    Fr s, t;
+    uint32_t c = add256(s, a, b);
+    uint32_t br = sub256(t, s, fr_p());
+    // keep t if (carry) or (no borrow): s >= p
+    bool use_t = c | (br ^ 1u);
+    Fr r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = use_t ? t.w[i] : s.w[i];
+    return r;
+}
+SVDW_HD Fr fr_sub(const Fr& a, const Fr& b) {
+    Fr d, t;
+    uint32_t br = sub256(d, a, b);
+    add256(t, d, fr_p());
+    Fr r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = br ? t.w[i] : d.w[i];
+    return r;
+}
+SVDW_HD Fr fr_neg(const Fr& a) { return fr_sub(fr_zero(), a); }
+
+// Montgomery product a*b*2^-256 mod p (CIOS, 32-bit limbs). Output canonical
+// (< p) for inputs < p.
+SVDW_HD Fr mont_mul(const Fr& a, const Fr& b) {
+    uint32_t t[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) t[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            c += (uint64_t)a.w[j] * b.w[i] + t[j];
+            t[j] = (uint32_t)c;
+            c >>= 32;
+        }
+        c += t[8];
+        t[8] = (uint32_t)c;
+        t[9] = (uint32_t)(c >> 32);
+        uint32_t m = t[0] * kPinv32;
+        c = (uint64_t)m * p_word(0) + t[0];
+        c >>= 32;
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            c += (uint64_t)m * p_word(j) + t[j];
+            t[j - 1] = (uint32_t)c;
+            c >>= 32;
+        }
+        c += t[8];
+        t[7] = (uint32_t)c;
+        t[8] = t[9] + (uint32_t)(c >> 32);
+    }
+    Fr r, s;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = t[i];
+    uint32_t br = sub256(s, r, fr_p());
+    bool use_s = t[8] | (br ^ 1u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = use_s ? s.w[i] : r.w[i];
+    return r;
+}
+SVDW_HD Fr fr_to_mont(const Fr& a) { return mont_mul(a, fr_r2()); }
+SVDW_HD Fr fr_from_mont(const Fr& a) { return mont_mul(a, fr_from_u64(1)); }
+// Canonical product.
+SVDW_HD Fr fr_mul(const Fr& a, const Fr& b) { return mont_mul(mont_mul(a, b), fr_r2()); }
+
+// a^e for canonical a (square and multiply over the bits of e, Montgomery).
+SVDW_HD Fr fr_pow_u64(const Fr& a, uint64_t e) {
+    Fr am = fr_to_mont(a);
+    Fr r = fr_to_mont(fr_from_u64(1));
+    for (int i = 63; i >= 0; --i) {
+        r = mont_mul(r, r);
+        if ((e >> i) & 1) r = mont_mul(r, am);
+    }
+    return fr_from_mont(r);
+}
+// a^-1 (a^(p-2)); 0 -> 0.
+SVDW_HD Fr fr_inv(const Fr& a) {
+    Fr e = fr_p();
+    e.w[0] -= 2;   // p - 2 (no borrow: low word is 0xf0000001)
+    Fr am = fr_to_mont(a);
+    Fr r = fr_to_mont(fr_from_u64(1));
+    for (int wi = 7; wi >= 0; --wi) {
+        // select chain instead of e.w[wi]: a runtime index would spill e to scratch
+        uint32_t word = e.w[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) word = (wi == k) ? e.w[k] : word;
+        for (int b = 31; b >= 0; --b) {
+            r = mont_mul(r, r);
+            if ((word >> b) & 1) r = mont_mul(r, am);
+        }
+    }
+    return fr_from_mont(r);
+}
+// Signed two's-complement integer of `nw` 32-bit words (little endian, value
+// |x| < 2^(32*nw - 1) < p) to canonical Fr.
+template <int NW>
+SVDW_HD Fr fr_from_signed_words(const uint32_t (&x)[NW]) {
+    bool neg = (x[NW - 1] >> 31) & 1;
+    Fr mag = fr_zero();
+    uint64_t c = neg ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        uint32_t v = neg ? ~x[i] : x[i];
+        c += v;
+        mag.w[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    return neg ? fr_sub(fr_zero(), mag) : mag;
+}
+
+}  // namespace svdw

@@ -1,0 +1,599 @@
+// gfx950 (CDNA4) kernels of the SVD-verify witness engine.
+//
+//  k_quantize      ZkMatrix::new / ZkVector::new cells   (src/matrix/mod.rs:29-40, 230-252)
+//  k_stage         every gadget block of check_svd_phase0 / verify_mul except
+//                  the GEMM and the inner-product rows: one cell program per
+//                  stage (prog.hpp), HBM-write bound, 16 B/lane coalesced stores
+//  k_to_digits +   honest_prover_mat_mul / field_mat_mul (src/matrix/mod.rs:510-568)
+//  k_gemm_dot4     as an exact signed-integer GEMM on v_dot4c_i32_i8 over
+//                  balanced base-256 digit planes, one reduction mod p per output
+//  k_gemm_mont     generic Montgomery fallback (operands not small integers)
+//  k_matvec_scan   field_mat_vec_mul rows (src/matrix/mod.rs:574-599): every
+//                  prefix sum of the row inner product is a cell -> block Fr scan
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+
+namespace svdw {
+
+// ----------------------------------------------------------------- helpers
+__device__ __forceinline__ Fr ld_fr(const Fr* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint4 a = q[0], b = q[1];
+    Fr r;
+    r.w[0] = a.x; r.w[1] = a.y; r.w[2] = a.z; r.w[3] = a.w;
+    r.w[4] = b.x; r.w[5] = b.y; r.w[6] = b.z; r.w[7] = b.w;
+    return r;
+}
+__device__ __forceinline__ void st_fr(Fr* p, const Fr& v) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    q[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+    q[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+}
+// X(i, j) of a view; `pad` is the value outside the view (K[v.pad_k]).
+__device__ __forceinline__ Fr view_load(const DView v, const Fr pad, uint32_t i, uint32_t j) {
+    if (v.mode == VIEW_DIAG) return (i == j) ? ld_fr(v.ptr) : pad;
+    if (i < v.rows && j < v.cols) return ld_fr(v.ptr + (int64_t)i * v.rs + (int64_t)j * v.cs);
+    return pad;
+}
+__device__ __forceinline__ uint32_t signed_bits(const Fr& x) {
+    // bit length of |x| where x is read as the signed representative in (-p/2, p/2]
+    Fr half = fr_p();
+    // (p-1)/2
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+        uint32_t nw = (half.w[i] >> 1) | c;
+        c = half.w[i] << 31;
+        half.w[i] = nw;
+    }
+    Fr t;
+    bool neg = sub256(t, half, x) != 0;   // x > (p-1)/2
+    Fr mag = neg ? fr_sub(fr_zero(), x) : x;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int i = 7; i >= 0; --i)
+        if (bits == 0 && mag.w[i]) bits = 32 * i + 32 - __clz(mag.w[i]);
+    return bits;
+}
+
+// --------------------------------------------------------------- quantize
+// x_q = round_half_away(|x| * 2^P) as u128 (saturating, NaN -> 0);
+// sign(x) < 0 (incl. -0.0) -> p - x_q.   [zk_fixed_point_chip quantization,
+// SURVEY.md Appendix C.1]
+__global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in, uint64_t n,
+                                                  Fr* __restrict__ out, double scale) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double x = in[i];
+    bool neg = signbit(x) && !isnan(x);
+    double s = round(fabs(x) * scale);
+    Fr q = fr_zero();
+    if (s >= 340282366920938463463374607431768211456.0) {
+        q.w[0] = q.w[1] = q.w[2] = q.w[3] = 0xffffffffu;
+    } else if (s > 0.0) {
+        uint64_t bits = __double_as_longlong(s);
+        int e = (int)((bits >> 52) & 0x7ff) - 1075;
+        uint64_t mant = (bits & 0xfffffffffffffull) | (1ull << 52);
+        unsigned __int128 v = e >= 0 ? ((unsigned __int128)mant << e) : (unsigned __int128)(mant >> -e);
+        q.w[0] = (uint32_t)v; q.w[1] = (uint32_t)(v >> 32);
+        q.w[2] = (uint32_t)(v >> 64); q.w[3] = (uint32_t)(v >> 96);
+    }
+    st_fr(out + i, neg ? fr_sub(fr_zero(), q) : q);
+}
+
+hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int p, hipStream_t st) {
+    if (!n) return hipSuccess;
+    double scale = (double)(1ull << p);
+    hipLaunchKernelGGL(k_quantize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, n, out,
+                       scale);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------- stage kernel
+// Phase A: one thread per element runs the stage's micro-ops, leaving the
+// element's values V[0..nv) in LDS (each padded to 16 words so bit windows
+// may run past the top). Phase B: the block's E*C advice cells (then E*L
+// lookup cells) are produced half a cell (16 B) per lane in stream order, so
+// every wave store is 1 KiB contiguous.
+constexpr int VW = 16;   // LDS words per value (8 + 8 zero pad)
+
+__device__ __forceinline__ void lds_put(uint32_t* s, const Fr& v) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = v.w[i];
+#pragma unroll
+    for (int i = 8; i < 16; ++i) s[i] = 0;
+}
+__device__ __forceinline__ Fr lds_get(const uint32_t* s) {
+    Fr r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = s[i];
+    return r;
+}
+
+// Four output words [4h, 4h+4) of (S >> lo) & mask(nbits), S at LDS word ptr s.
+__device__ __forceinline__ uint4 extract_half(const uint32_t* s, uint32_t lo, uint32_t nbits,
+                                              uint32_t h) {
+    uint32_t q = lo >> 5, r = lo & 31;
+    const uint32_t* p = s + q + 4 * h;
+    uint32_t x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3], x4 = p[4];
+    uint32_t o[4];
+    o[0] = __builtin_amdgcn_alignbit(x1, x0, r);
+    o[1] = __builtin_amdgcn_alignbit(x2, x1, r);
+    o[2] = __builtin_amdgcn_alignbit(x3, x2, r);
+    o[3] = __builtin_amdgcn_alignbit(x4, x3, r);
+    if (nbits) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            int lowbit = 32 * (4 * (int)h + k);
+            int keep = (int)nbits - lowbit;
+            uint32_t m = keep >= 32 ? 0xffffffffu : (keep <= 0 ? 0u : ((1u << keep) - 1u));
+            o[k] &= m;
+        }
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+__global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
+    __shared__ uint32_t sK[kMaxK * VW];
+    __shared__ uint32_t sV[kStageElems * kMaxV * VW];
+    __shared__ SlotOp sAdv[kMaxAdv];
+    __shared__ SlotOp sLk[kMaxLk];
+    __shared__ MicroOp sMo[kMaxMicro];
+    __shared__ DView sVw[kMaxViews];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t e0 = a.e_begin + blockIdx.x * kStageElems;
+    const uint32_t ne = min((uint32_t)kStageElems, a.e_end - e0);
+    const uint32_t nv = a.nv;
+
+    for (uint32_t k = tid; k < a.nk; k += blockDim.x) lds_put(sK + k * VW, a.K[k]);
+    for (uint32_t k = tid; k < a.C; k += blockDim.x) sAdv[k] = a.adv[k];
+    for (uint32_t k = tid; k < a.L; k += blockDim.x) sLk[k] = a.lk[k];
+    for (uint32_t k = tid; k < a.nmo; k += blockDim.x) sMo[k] = a.mo[k];
+    if (tid < kMaxViews) sVw[tid] = a.view[tid];
+    __syncthreads();
+
+    // ---- phase A: per-element micro-ops (constants and ops read from LDS:
+    // dynamic indexing into the by-value kernel argument would go to scratch)
+    if (tid < ne) {
+        const uint32_t e = e0 + tid;
+        const uint32_t i = e / a.cols, j = e - (e / a.cols) * a.cols;
+        uint32_t* myV = sV + tid * nv * VW;
+        for (uint32_t m = 0; m < a.nmo; ++m) {
+            const MicroOp op = sMo[m];
+            uint32_t* dst = myV + op.dst * VW;
+            switch (op.op) {
+                case MO_LOAD: {
+                    const DView vw = sVw[op.a];
+                    lds_put(dst, view_load(vw, lds_get(sK + vw.pad_k * VW), i, j));
+                    break;
+                }
+                case MO_ADDK:
+                    lds_put(dst, fr_add(lds_get(myV + op.a * VW), lds_get(sK + op.b * VW)));
+                    break;
+                case MO_SUB:
+                    lds_put(dst, fr_sub(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
+                    break;
+                case MO_MUL:
+                    lds_put(dst, fr_mul(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
+                    break;
+                case MO_LIMBSHL: {
+                    const uint32_t* s = myV + op.a * VW;
+                    uint32_t lo = op.p0, q = lo >> 5, r = lo & 31;
+                    uint64_t w01 = (uint64_t)s[q] | ((uint64_t)s[q + 1] << 32);
+                    uint64_t w2 = s[q + 2];
+                    uint64_t x = r ? ((w01 >> r) | (w2 << (64 - r))) : w01;
+                    if (op.p1 < 64) x &= (1ull << op.p1) - 1;
+                    uint32_t sh = op.b;
+                    uint64_t lo64 = sh < 64 ? (x << sh) : 0;
+                    uint64_t hi64 = sh == 0 ? 0 : (sh < 64 ? (x >> (64 - sh)) : (x << (sh - 64)));
+                    Fr v = fr_zero();
+                    v.w[0] = (uint32_t)lo64; v.w[1] = (uint32_t)(lo64 >> 32);
+                    v.w[2] = (uint32_t)hi64; v.w[3] = (uint32_t)(hi64 >> 32);
+                    lds_put(dst, v);
+                    break;
+                }
+                case MO_FDBL: {
+                    Fr v = lds_get(myV + op.a * VW);
+                    for (uint32_t k = 0; k < op.b; ++k) v = fr_add(v, v);
+                    lds_put(dst, v);
+                    break;
+                }
+                case MO_ISZERO: {
+                    Fr v = lds_get(myV + op.a * VW);
+                    bool z = fr_is_zero(v);
+                    Fr inv = z ? fr_from_u64(1) : fr_inv(v);
+                    lds_put(dst, fr_from_u64(z ? 1 : 0));
+                    lds_put(dst + VW, inv);
+                    break;
+                }
+                case MO_POWK:
+                    lds_put(dst, fr_pow_u64(lds_get(sK + op.a * VW), (uint64_t)e + op.p0));
+                    break;
+                default:
+                    break;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- phase B: advice cells, then lookup cells
+    {
+        const uint32_t total = 2 * ne * a.C;
+        uint4* out = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
+        for (uint32_t hc = tid; hc < total; hc += blockDim.x) {
+            uint32_t c = hc >> 1, h = hc & 1;
+            uint32_t el = (uint32_t)(((uint64_t)c * a.cdiv_magic) >> 32);
+            uint32_t s = c - el * a.C;
+            SlotOp op = sAdv[s];
+            const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW
+                                                 : sV + (el * nv + op.src) * VW;
+            out[hc] = extract_half(src, op.lo, op.nbits, h);
+        }
+    }
+    if (a.L) {
+        const uint32_t total = 2 * ne * a.L;
+        uint4* out = reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L);
+        for (uint32_t hc = tid; hc < total; hc += blockDim.x) {
+            uint32_t c = hc >> 1, h = hc & 1;
+            uint32_t el = (uint32_t)(((uint64_t)c * a.ldiv_magic) >> 32);
+            uint32_t s = c - el * a.L;
+            SlotOp op = sLk[s];
+            const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW
+                                                 : sV + (el * nv + op.src) * VW;
+            out[hc] = extract_half(src, op.lo, op.nbits, h);
+        }
+    }
+}
+
+hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
+    if (a.e_end <= a.e_begin) return hipSuccess;
+    uint32_t n = a.e_end - a.e_begin;
+    hipLaunchKernelGGL(k_stage, dim3((n + kStageElems - 1) / kStageElems), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// ----------------------------------------------------------------- maxbits
+__global__ __launch_bounds__(256) void k_maxbits(const DView v, uint32_t rows, uint32_t cols,
+                                                 unsigned* out) {
+    uint64_t n = (uint64_t)rows * cols;
+    uint32_t best = 0;
+    Fr zero = fr_zero();
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t i = (uint32_t)(e / cols), j = (uint32_t)(e % cols);
+        Fr x = view_load(v, zero, i, j);
+        best = max(best, signed_bits(x));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, off));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, best);
+}
+
+hipError_t launch_maxbits(const DView& v, uint32_t rows, uint32_t cols, unsigned* out,
+                          hipStream_t st) {
+    uint64_t n = (uint64_t)rows * cols;
+    if (!n) return hipSuccess;
+    unsigned blocks = (unsigned)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+    hipLaunchKernelGGL(k_maxbits, dim3(blocks), dim3(256), 0, st, v, rows, cols, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------- digit planes
+// Balanced base-256 digits d_l in [-128, 127]: x = sum_l d_l 256^l.
+__global__ __launch_bounds__(256) void k_to_digits(const DView x, uint32_t rows, uint32_t kdim,
+                                                   int D, uint32_t rows_pad, uint32_t kg_pad,
+                                                   uint32_t* __restrict__ out) {
+    uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (uint64_t)rows_pad * kg_pad) return;
+    uint32_t row = (uint32_t)(idx / kg_pad), kg = (uint32_t)(idx % kg_pad);
+    uint32_t words[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Fr zero = fr_zero();
+    Fr half = fr_p();
+    {
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 7; i >= 0; --i) {
+            uint32_t nw = (half.w[i] >> 1) | c;
+            c = half.w[i] << 31;
+            half.w[i] = nw;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        uint32_t k = kg * 4 + t;
+        if (row >= rows || k >= kdim) continue;
+        Fr v = view_load(x, zero, row, k);
+        Fr tmp;
+        bool neg = sub256(tmp, half, v) != 0;
+        Fr mag = neg ? fr_sub(fr_zero(), v) : v;
+        // signed 128-bit value (host guarantees |x| fits D digits, D <= 9)
+        __int128 s = (__int128)(((unsigned __int128)mag.w[3] << 96) | ((unsigned __int128)mag.w[2] << 64) |
+                                ((unsigned __int128)mag.w[1] << 32) | mag.w[0]);
+        if (neg) s = -s;
+#pragma unroll
+        for (int l = 0; l < 9; ++l) {
+            if (l < D) {
+                int dg = (int)(uint32_t)(s & 0xff);
+                if (dg >= 128) dg -= 256;
+                s = (s - dg) >> 8;
+                words[l] |= ((uint32_t)dg & 0xffu) << (8 * t);
+            }
+        }
+    }
+    uint32_t* o = out + idx * D;
+#pragma unroll
+    for (int l = 0; l < 9; ++l)
+        if (l < D) o[l] = words[l];
+}
+
+hipError_t launch_to_digits(const DView& x, uint32_t rows, uint32_t kdim, int D, uint32_t rows_pad,
+                            uint32_t kg_pad, uint32_t* out, hipStream_t st) {
+    uint64_t n = (uint64_t)rows_pad * kg_pad;
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_to_digits, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, rows,
+                       kdim, D, rows_pad, kg_pad, out);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------- dot4 GEMM
+// Block = 256 threads = 16 x 16, each 2 x 2 outputs -> 32 x 32 tile.
+// K advances 8 digit-groups (32 k) per LDS stage. acc[.][.][d] is the
+// i32 sum of digit products with la + lb = d; |acc| < 9 * 2^14 * K < 2^31
+// for K <= 8192 (host-checked).
+constexpr int GT = 32;   // tile edge
+constexpr int GKC = 8;   // digit groups per K stage
+
+template <int DA, int DB>
+__device__ __forceinline__ Fr combine_diagonals(const int (&acc)[DA + DB - 1]) {
+    int64_t col[7] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int d = 0; d < DA + DB - 1; ++d) {
+        const int sh = 8 * d;
+        col[sh >> 5] += (int64_t)acc[d] * ((int64_t)1 << (sh & 31));
+    }
+    uint32_t w[7];
+    int64_t carry = 0;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        int64_t t = col[q] + carry;
+        w[q] = (uint32_t)t;
+        carry = t >> 32;
+    }
+    return fr_from_signed_words<7>(w);
+}
+
+template <int DA, int DB, bool SYM>
+__global__ __launch_bounds__(256) void k_gemm_dot4(const uint32_t* __restrict__ Ad,
+                                                   const uint32_t* __restrict__ Bd, uint32_t N,
+                                                   uint32_t M, uint32_t KG, Fr* __restrict__ out,
+                                                   int64_t ors, int64_t ocs, uint32_t tiles_m) {
+    __shared__ uint32_t As[GKC][DA][GT];
+    __shared__ uint32_t Bs[GKC][DB][GT];
+    uint32_t bi, bj;
+    if (SYM) {
+        // blockIdx -> (bi, bj) with bi <= bj over a tiles_m x tiles_m triangle
+        uint32_t b = blockIdx.x, r = 0, rowlen = tiles_m;
+        while (b >= rowlen) { b -= rowlen; ++r; --rowlen; }
+        bi = r; bj = r + b;
+    } else {
+        bi = blockIdx.x / tiles_m;
+        bj = blockIdx.x % tiles_m;
+    }
+    const uint32_t tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    const uint32_t i0 = bi * GT, j0 = bj * GT;
+    int acc[2][2][DA + DB - 1];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int d = 0; d < DA + DB - 1; ++d) acc[r][c][d] = 0;
+
+    const uint32_t lrow = tid >> 3, lg = tid & 7;
+    for (uint32_t kg0 = 0; kg0 < KG; kg0 += GKC) {
+        {
+            const uint32_t* src = Ad + ((uint64_t)(i0 + lrow) * KG + kg0 + lg) * DA;
+#pragma unroll
+            for (int l = 0; l < DA; ++l) As[lg][l][lrow] = src[l];
+            const uint32_t* srcb = Bd + ((uint64_t)(j0 + lrow) * KG + kg0 + lg) * DB;
+#pragma unroll
+            for (int l = 0; l < DB; ++l) Bs[lg][l][lrow] = srcb[l];
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int g = 0; g < GKC; ++g) {
+            int a0[DA], a1[DA], b0[DB], b1[DB];
+#pragma unroll
+            for (int l = 0; l < DA; ++l) {
+                uint2 v = *reinterpret_cast<const uint2*>(&As[g][l][2 * ty]);
+                a0[l] = (int)v.x; a1[l] = (int)v.y;
+            }
+#pragma unroll
+            for (int l = 0; l < DB; ++l) {
+                uint2 v = *reinterpret_cast<const uint2*>(&Bs[g][l][2 * tx]);
+                b0[l] = (int)v.x; b1[l] = (int)v.y;
+            }
+#pragma unroll
+            for (int la = 0; la < DA; ++la)
+#pragma unroll
+                for (int lb = 0; lb < DB; ++lb) {
+                    acc[0][0][la + lb] = __builtin_amdgcn_sdot4(a0[la], b0[lb], acc[0][0][la + lb], false);
+                    acc[0][1][la + lb] = __builtin_amdgcn_sdot4(a0[la], b1[lb], acc[0][1][la + lb], false);
+                    acc[1][0][la + lb] = __builtin_amdgcn_sdot4(a1[la], b0[lb], acc[1][0][la + lb], false);
+                    acc[1][1][la + lb] = __builtin_amdgcn_sdot4(a1[la], b1[lb], acc[1][1][la + lb], false);
+                }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint32_t i = i0 + 2 * ty + r, j = j0 + 2 * tx + c;
+            if (i < N && j < M) {
+                Fr v = combine_diagonals<DA, DB>(acc[r][c]);
+                st_fr(out + (int64_t)i * ors + (int64_t)j * ocs, v);
+                if (SYM && bi != bj) st_fr(out + (int64_t)j * ors + (int64_t)i * ocs, v);
+            }
+        }
+}
+
+template <int DA, int DB>
+static hipError_t gemm_dispatch(bool sym, const uint32_t* Ad, const uint32_t* Bd, uint32_t N,
+                                uint32_t M, uint32_t kg, Fr* out, int64_t ors, int64_t ocs,
+                                hipStream_t st) {
+    uint32_t tn = (N + GT - 1) / GT, tm = (M + GT - 1) / GT;
+    if (sym) {
+        if (DA != DB || N != M) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_gemm_dot4<DA, DB, true>), dim3(tm * (tm + 1) / 2), dim3(256), 0, st,
+                           Ad, Bd, N, M, kg, out, ors, ocs, tm);
+    } else {
+        hipLaunchKernelGGL((k_gemm_dot4<DA, DB, false>), dim3(tn * tm), dim3(256), 0, st, Ad, Bd,
+                           N, M, kg, out, ors, ocs, tm);
+    }
+    return hipGetLastError();
+}
+
+bool gemm_digits_supported(int DA, int DB) {
+    auto ok = [](int d) { return d == 5 || d == 8 || d == 9; };
+    return ok(DA) && ok(DB);
+}
+
+hipError_t launch_gemm_digits(int DA, int DB, bool sym, const uint32_t* Ad, const uint32_t* Bd,
+                              uint32_t N, uint32_t M, uint32_t kg, Fr* out, int64_t ors,
+                              int64_t ocs, hipStream_t st) {
+#define SVDW_G(a, b) \
+    if (DA == a && DB == b) return gemm_dispatch<a, b>(sym, Ad, Bd, N, M, kg, out, ors, ocs, st);
+    SVDW_G(5, 5) SVDW_G(5, 8) SVDW_G(5, 9) SVDW_G(8, 5) SVDW_G(8, 8) SVDW_G(8, 9)
+    SVDW_G(9, 5) SVDW_G(9, 8) SVDW_G(9, 9)
+#undef SVDW_G
+    return hipErrorInvalidValue;
+}
+
+// -------------------------------------------------------- Montgomery GEMM
+__global__ __launch_bounds__(256) void k_gemm_mont(const DView A, const DView B, uint32_t N,
+                                                   uint32_t K, uint32_t M, Fr* out, int64_t ors,
+                                                   int64_t ocs) {
+    uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (uint64_t)N * M) return;
+    uint32_t i = (uint32_t)(e / M), j = (uint32_t)(e % M);
+    Fr zero = fr_zero();
+    Fr acc = fr_zero();
+    for (uint32_t k = 0; k < K; ++k) {
+        Fr a = view_load(A, zero, i, k);
+        Fr b = view_load(B, zero, k, j);
+        acc = fr_add(acc, mont_mul(a, b));   // a * b * R^-1
+    }
+    st_fr(out + (int64_t)i * ors + (int64_t)j * ocs, mont_mul(acc, fr_r2()));
+}
+
+hipError_t launch_gemm_mont(const DView& A, const DView& B, uint32_t N, uint32_t K, uint32_t M,
+                            Fr* out, int64_t ors, int64_t ocs, hipStream_t st) {
+    uint64_t n = (uint64_t)N * M;
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_gemm_mont, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A, B, N, K,
+                       M, out, ors, ocs);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ vectors
+__global__ void k_vec_prep(const DView w, uint32_t L, Fr* wc, Fr* wm) {
+    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= L) return;
+    Fr zero = fr_zero();
+    Fr v = view_load(w, zero, 0, j);
+    st_fr(wc + j, v);
+    st_fr(wm + j, fr_to_mont(v));
+}
+hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* wc, Fr* wm, hipStream_t st) {
+    if (!L) return hipSuccess;
+    hipLaunchKernelGGL(k_vec_prep, dim3((L + 255) / 256), dim3(256), 0, st, w, L, wc, wm);
+    return hipGetLastError();
+}
+__global__ void k_gamma_vec(const Fr g, uint32_t L, Fr* wc, Fr* wm) {
+    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= L) return;
+    Fr v = fr_pow_u64(g, j);
+    st_fr(wc + j, v);
+    st_fr(wm + j, fr_to_mont(v));
+}
+hipError_t launch_gamma_vec(const Fr& g, uint32_t L, Fr* wc, Fr* wm, hipStream_t st) {
+    if (!L) return hipSuccess;
+    hipLaunchKernelGGL(k_gamma_vec, dim3((L + 255) / 256), dim3(256), 0, st, g, L, wc, wm);
+    return hipGetLastError();
+}
+
+// -------------------------------------------------------- row inner products
+// One 256-thread block per row. Chunks of 256 terms: Montgomery products
+// a_j * w_j, wave shuffle scan + cross-wave LDS combine (Fr addition is
+// associative, so the prefix values are exact whatever the order), cells
+// [a_j, w_j, s_j] staged in LDS and written as coalesced 16 B half-cells.
+__device__ __forceinline__ Fr shfl_up_fr(const Fr& v, int d) {
+    Fr r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = (uint32_t)__shfl_up((int)v.w[i], d);
+    return r;
+}
+
+__global__ __launch_bounds__(256) void k_matvec_scan(const DView A, uint32_t r_begin, uint32_t L,
+                                                     const Fr* __restrict__ wc,
+                                                     const Fr* __restrict__ wm,
+                                                     Fr* __restrict__ out) {
+    __shared__ uint32_t stage[3 * 256 * 8];
+    __shared__ Fr wtot[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t r = r_begin + blockIdx.x;
+    Fr* rowout = out + (uint64_t)blockIdx.x * (3ull * L + 1);
+    Fr zero = fr_zero();
+    if (tid == 0) st_fr(rowout, zero);
+    Fr carry = fr_zero();
+    for (uint32_t c0 = 0; c0 < L; c0 += 256) {
+        const uint32_t j = c0 + tid;
+        const bool valid = j < L;
+        Fr a = zero, w = zero, p = zero;
+        if (valid) {
+            a = view_load(A, zero, r, j);
+            w = ld_fr(wc + j);
+            p = mont_mul(a, ld_fr(wm + j));
+        }
+        Fr s = p;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            Fr o = shfl_up_fr(s, off);
+            if ((int)lane >= off) s = fr_add(s, o);
+        }
+        if (lane == 63) wtot[wave] = s;
+        __syncthreads();
+        Fr pre = carry;
+        for (uint32_t w2 = 0; w2 < wave; ++w2) pre = fr_add(pre, wtot[w2]);
+        s = fr_add(s, pre);
+        uint32_t* st3 = stage + tid * 24;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            st3[i] = a.w[i];
+            st3[8 + i] = w.w[i];
+            st3[16 + i] = s.w[i];
+        }
+        Fr tot = carry;
+#pragma unroll
+        for (int w2 = 0; w2 < 4; ++w2) tot = fr_add(tot, wtot[w2]);
+        __syncthreads();
+        const uint32_t ncell = 3 * min(256u, L - c0);
+        uint4* o = reinterpret_cast<uint4*>(rowout + 1 + 3ull * c0);
+        const uint4* sv = reinterpret_cast<const uint4*>(stage);
+        for (uint32_t hc = tid; hc < 2 * ncell; hc += 256) o[hc] = sv[hc];
+        carry = tot;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
+                              const Fr* wc, const Fr* wm, Fr* out, hipStream_t st) {
+    if (r_end <= r_begin || !L) return hipSuccess;
+    hipLaunchKernelGGL(k_matvec_scan, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L, wc,
+                       wm, out);
+    return hipGetLastError();
+}
+
+}  // namespace svdw

@@ -1,0 +1,44 @@
+// Host-side launchers for the gfx950 kernels in kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fr.hpp"
+#include "prog.hpp"
+
+namespace svdw {
+
+// Elements per block of the generic stage kernel (LDS: E * nv * 64 B).
+static constexpr int kStageElems = 64;
+
+// ZkMatrix::new / ZkVector::new quantization (f64 -> Fr) of n contiguous values.
+hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int precision_bits,
+                           hipStream_t st);
+// Generic cell-program stage over elements [a.e_begin, a.e_end).
+hipError_t launch_stage(const StageArgs& a, hipStream_t st);
+// max over the view of bit-length(|signed(x)|) -> atomicMax(*out).
+hipError_t launch_maxbits(const DView& v, uint32_t rows, uint32_t cols, unsigned* out,
+                          hipStream_t st);
+// Balanced base-256 digit planes of X (rows x kdim): out[row][kg][D] int32 words,
+// each packing the digit of 4 consecutive k. rows_pad/kg_pad are zero-filled.
+hipError_t launch_to_digits(const DView& x, uint32_t rows, uint32_t kdim, int D,
+                            uint32_t rows_pad, uint32_t kg_pad, uint32_t* out, hipStream_t st);
+// c_s[i][j] = sum_k A[i][k] * Bt[j][k] exactly, written as canonical Fr to
+// out[i*ors + j*ocs]. sym: A == Bt (upper tiles + mirror).
+hipError_t launch_gemm_digits(int DA, int DB, bool sym, const uint32_t* Ad, const uint32_t* Bd,
+                              uint32_t N, uint32_t M, uint32_t kg_pad, Fr* out, int64_t ors,
+                              int64_t ocs, hipStream_t st);
+bool gemm_digits_supported(int DA, int DB);
+// Generic Montgomery GEMM (any field elements): out = A(NxK) * B(KxM).
+hipError_t launch_gemm_mont(const DView& A, const DView& B, uint32_t N, uint32_t K, uint32_t M,
+                            Fr* out, int64_t ors, int64_t ocs, hipStream_t st);
+// w vector (len L) from a view (row 0 / col j of a 1 x L view) -> canonical + Montgomery copies.
+hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* w_mont, hipStream_t st);
+// w_j = gamma^j, j < L.
+hipError_t launch_gamma_vec(const Fr& gamma, uint32_t L, Fr* w_canon, Fr* w_mont, hipStream_t st);
+// Freivalds inner-product rows (GateChip::inner_product, 1+3L cells per row) for
+// rows [r_begin, r_end) of A (R x L); row r's cells at out + (r - r_begin)*(3L+1).
+hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
+                              const Fr* w_canon, const Fr* w_mont, Fr* out, hipStream_t st);
+
+}  // namespace svdw

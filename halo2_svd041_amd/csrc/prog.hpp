@@ -1,0 +1,85 @@
+// Cell programs: the data-independent layout of one element's block of
+// advice / lookup cells for a gadget stage, as emitted by the generic
+// streaming kernel (kernels.hip: k_stage).
+//
+// Every halo2-base 0.4.1 gadget used on the hot path (GateChip add / sub / mul
+// / is_equal / assert_bit, RangeChip range_check / check_less_than /
+// check_big_less_than_safe, and the reference's check_abs_less_than,
+// src/matrix/mod.rs:425-435) appends, per element, a fixed number of cells
+// whose values are simple functions of a few per-element field values:
+//   * a handful of field values V[0..nv) computed per element by micro-ops
+//     (load from a matrix view, +constant, -, *, limb<<shift, is_zero/inverse,
+//     gamma^k), and
+//   * for every cell: (V[src] >> lo) & (2^nbits - 1)  or a constant K[k].
+// Range-check limbs are bit windows of the canonical value, and the running
+// sums of the limb inner product are `value mod 2^(i*LB)`.
+#pragma once
+#include <stdint.h>
+
+#include "fr.hpp"
+
+namespace svdw {
+
+// ------------------------------------------------------------------ views
+// Matrix view over canonical Fr cells: X(i, j) = ptr[i*rs + j*cs] for
+// i < rows && j < cols, else K[pad_k]. mode DIAG: X(i,j) = i==j ? *ptr : K[pad_k]
+// (check_mat_id's implicit scalar_id * Id matrix, src/matrix/mod.rs:461-483).
+enum : uint32_t { VIEW_STRIDED = 0, VIEW_DIAG = 1 };
+struct DView {
+    const Fr* ptr;
+    int64_t rs, cs;
+    uint32_t rows, cols;
+    uint32_t mode;
+    uint8_t pad_k, diag_k, _r0, _r1;
+};
+
+// ------------------------------------------------------------ micro-ops
+enum : uint8_t {
+    MO_LOAD = 1,     // V[dst] = view[a](i, j)
+    MO_ADDK,         // V[dst] = V[a] + K[b]
+    MO_SUB,          // V[dst] = V[a] - V[b]
+    MO_MUL,          // V[dst] = V[a] * V[b]
+    MO_LIMBSHL,      // V[dst] = ((V[a] >> p0) & (2^p1 - 1)) << b      (non-modular, < 2^128)
+    MO_FDBL,         // V[dst] = V[a] * 2^b mod p
+    MO_ISZERO,       // V[dst] = (V[a]==0), V[dst+1] = V[a]==0 ? 1 : V[a]^-1
+    MO_POWK,         // V[dst] = K[a] ^ (e + p0)                         (verify_mul's gamma powers)
+};
+struct MicroOp {
+    uint8_t op, dst, a, b;
+    uint16_t p0, p1;
+};
+
+// ------------------------------------------------------------- slot ops
+// value = (S >> lo) & (2^nbits - 1); nbits == 0 keeps all 256 bits.
+// src < 0x80: element value V[src]; src >= 0x80: constant K[src - 0x80].
+struct SlotOp {
+    uint8_t src, lo, nbits, _pad;
+};
+static constexpr uint8_t KSRC = 0x80;
+
+static constexpr int kMaxViews = 2;
+static constexpr int kMaxMicro = 16;
+static constexpr int kMaxAdv = 112;
+static constexpr int kMaxLk = 32;
+static constexpr int kMaxK = 32;
+static constexpr int kMaxV = 8;
+
+// Kernel argument block of one stage launch (passed by value, < 4 KiB).
+struct StageArgs {
+    Fr* out_adv;          // cell 0 of element 0 of this stage
+    Fr* out_lk;           // lookup cell 0 of element 0 (may be null if L == 0)
+    uint32_t e_begin, e_end;   // element range processed by this launch
+    uint32_t cols;        // element e -> (i, j) = (e / cols, e % cols)
+    uint32_t C, L;        // advice / lookup cells per element
+    uint32_t nv, nmo, nk;
+    uint64_t cdiv_magic;  // ceil(2^32 / C): el = (c * magic) >> 32 exact for c*C < 2^25
+    uint64_t ldiv_magic;  // ceil(2^32 / L)
+    DView view[kMaxViews];
+    MicroOp mo[kMaxMicro];
+    SlotOp adv[kMaxAdv];
+    SlotOp lk[kMaxLk];
+    Fr K[kMaxK];
+};
+static_assert(sizeof(StageArgs) < 4096, "kernel argument block too large");
+
+}  // namespace svdw

@@ -1,0 +1,357 @@
+"""Host-side mirror of the reference's ZkMatrix / ZkVector / SVD API.
+
+Same names and argument meaning as the Rust reference (src/matrix/mod.rs,
+src/svd/mod.rs); every call goes through the C ABI (include/svdw.h) into the
+gfx950 kernels. Where the reference panics on a shape mismatch, these raise
+`SvdwError(SVDW_EINVAL)`.
+
+    ctx = Context(device=0, precision_bits=63, lookup_bits=19)
+    m = ZkMatrix.new(ctx, m_f64); u = ZkMatrix.new(ctx, u_f64); ...
+    payload = check_svd_phase0(ctx, m, u, v, d, err_svd, err_u, 30)
+    check_svd_phase1(ctx, m, u, v, payload, gamma)
+    cells = ctx.advice(0)            # (n, 4) uint64 canonical Fr, like Fr::to_repr
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from ._lib import Counts, KStat, Mat, Params, Payload, SvdConfig, SvdwError, Vec, check, lib
+
+P_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
+
+__all__ = ["Context", "ZkMatrix", "ZkVector", "honest_prover_mat_mul", "field_mat_vec_mul",
+           "mat_times_diag_mat", "check_mat_diff", "check_mat_id", "check_mat_entries_bounded",
+           "check_svd_phase0", "check_svd_phase1", "err_calc", "svd_witness", "plan_svd",
+           "SvdwError", "SvdPayload", "SvdConfigPy", "P_MOD", "int_to_words", "words_to_int"]
+
+
+def int_to_words(x: int) -> np.ndarray:
+    x = int(x)
+    if x < 0:
+        raise ValueError("expected a non-negative integer")
+    return np.array([(x >> (64 * i)) & ((1 << 64) - 1) for i in range(4)], dtype=np.uint64)
+
+
+def words_to_int(w) -> int:
+    w = [int(v) for v in w]
+    return w[0] | (w[1] << 64) | (w[2] << 128) | (w[3] << 192)
+
+
+def _device_ptr(a) -> Optional[int]:
+    """torch CUDA tensor -> device pointer (float64, contiguous) or None."""
+    try:
+        import torch  # noqa: WPS433
+    except ImportError:  # pragma: no cover
+        return None
+    if isinstance(a, torch.Tensor) and a.is_cuda:
+        if a.dtype != torch.float64 or not a.is_contiguous():
+            raise SvdwError(-1, "device input must be a contiguous float64 tensor")
+        return a.data_ptr()
+    return None
+
+
+class Context:
+    """One engine context = the phase-0 and phase-1 halo2-base `Context`s of a
+    circuit (examples/svd_example.rs:108,181), streams resident on `device`."""
+
+    def __init__(self, device: int = 0, precision_bits: int = 32, lookup_bits: int = 19):
+        self.precision_bits = precision_bits
+        self.lookup_bits = lookup_bits
+        self._h = ct.c_void_p()
+        p = Params(device, precision_bits, lookup_bits)
+        check(lib().svdw_ctx_create(ct.byref(p), ct.byref(self._h)))
+
+    def close(self) -> None:
+        if self._h:
+            lib().svdw_ctx_destroy(self._h)
+            self._h = ct.c_void_p()
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def reset(self) -> None:
+        check(lib().svdw_ctx_reset(self._h))
+
+    def reserve(self, phase: int, advice: int, lookups: int) -> None:
+        check(lib().svdw_reserve(self._h, phase, advice, lookups))
+
+    def sync(self) -> None:
+        check(lib().svdw_sync(self._h))
+
+    def advice_len(self, phase: int) -> int:
+        return lib().svdw_advice_len(self._h, phase)
+
+    def lookup_len(self, phase: int) -> int:
+        return lib().svdw_lookup_len(self._h, phase)
+
+    def advice_device_ptr(self, phase: int) -> int:
+        return lib().svdw_advice_device_ptr(self._h, phase) or 0
+
+    def lookup_device_ptr(self, phase: int) -> int:
+        return lib().svdw_lookup_device_ptr(self._h, phase) or 0
+
+    def advice(self, phase: int, off: int = 0, n: Optional[int] = None) -> np.ndarray:
+        n = self.advice_len(phase) - off if n is None else n
+        out = np.zeros((n, 4), dtype=np.uint64)
+        check(lib().svdw_copy_advice(self._h, phase, off, n, out.ctypes.data))
+        return out
+
+    def lookups(self, phase: int, off: int = 0, n: Optional[int] = None) -> np.ndarray:
+        n = self.lookup_len(phase) - off if n is None else n
+        out = np.zeros((n, 4), dtype=np.uint64)
+        check(lib().svdw_copy_lookup(self._h, phase, off, n, out.ctypes.data))
+        return out
+
+    def profile(self, on: bool = True) -> None:
+        """Record HIP events around every kernel launch on this context's stream."""
+        check(lib().svdw_profile_enable(self._h, 1 if on else 0))
+
+    def profile_collect(self) -> list:
+        """Per-kernel {name, launches, total_ms, max_ms, bytes, ops}; drops the records."""
+        n = ct.c_uint32()
+        cap = 256   # distinct kernel names; collect() drops the records, so one call
+        buf = (KStat * cap)()
+        check(lib().svdw_profile_collect(self._h, buf, cap, ct.byref(n)))
+        return [{"name": s.name.decode(), "launches": s.launches, "total_ms": s.total_ms,
+                 "max_ms": s.max_ms, "bytes": s.bytes, "ops": s.ops} for s in buf[:min(n.value, cap)]]
+
+    def load_witness(self, value: int, phase: int = 0) -> "ZkVector":
+        v = Vec()
+        w = int_to_words(int(value) % P_MOD)
+        check(lib().svdw_load_witness(self._h, phase, w.ctypes.data, ct.byref(v)))
+        return ZkVector(self, v)
+
+    def load_constant(self, value: int, phase: int = 0) -> "ZkVector":
+        v = Vec()
+        w = int_to_words(int(value) % P_MOD)
+        check(lib().svdw_load_constant(self._h, phase, w.ctypes.data, ct.byref(v)))
+        return ZkVector(self, v)
+
+
+class ZkMatrix:
+    """src/matrix/mod.rs:219-420: a view (offset + strides) into a phase stream."""
+
+    def __init__(self, ctx: Context, mat: Mat):
+        self.ctx = ctx
+        self.mat = mat
+
+    @property
+    def num_rows(self) -> int:
+        return self.mat.rows
+
+    @property
+    def num_col(self) -> int:
+        return self.mat.cols
+
+    @classmethod
+    def new(cls, ctx: Context, matrix, phase: int = 0) -> "ZkMatrix":
+        """ZkMatrix::new (src/matrix/mod.rs:230-252)."""
+        out = Mat()
+        dp = _device_ptr(matrix)
+        if dp is not None:
+            rows, cols = matrix.shape
+            check(lib().svdw_zkmatrix_new(ctx.handle, phase, dp, rows, cols, 1, ct.byref(out)))
+        else:
+            a = np.ascontiguousarray(matrix, dtype=np.float64)
+            if a.ndim != 2:
+                raise SvdwError(-1, "ZkMatrix::new expects a 2-D matrix")
+            check(lib().svdw_zkmatrix_new(ctx.handle, phase, a.ctypes.data, a.shape[0],
+                                          a.shape[1], 0, ct.byref(out)))
+        return cls(ctx, out)
+
+    def transpose_matrix(self) -> "ZkMatrix":
+        """ZkMatrix::transpose_matrix (src/matrix/mod.rs:408-419): no cells."""
+        out = Mat()
+        check(lib().svdw_transpose_matrix(ct.byref(self.mat), ct.byref(out)))
+        return ZkMatrix(self.ctx, out)
+
+    @staticmethod
+    def verify_mul(ctx: Context, a: "ZkMatrix", b: "ZkMatrix", c_s: "ZkMatrix", init_rand: int,
+                   phase: int = 1) -> None:
+        """ZkMatrix::verify_mul (src/matrix/mod.rs:299-342)."""
+        g = int_to_words(int(init_rand) % P_MOD)
+        check(lib().svdw_verify_mul(ctx.handle, phase, ct.byref(a.mat), ct.byref(b.mat),
+                                    ct.byref(c_s.mat), g.ctypes.data))
+
+    def values(self) -> np.ndarray:
+        """Cell values (rows, cols, 4) uint64 (host copy, for inspection)."""
+        cells = self.ctx.advice(self.mat.phase)
+        idx = (self.mat.off + np.arange(self.mat.rows)[:, None] * self.mat.rs
+               + np.arange(self.mat.cols)[None, :] * self.mat.cs)
+        return cells[idx]
+
+
+class ZkVector:
+    """src/matrix/mod.rs:19-216."""
+
+    def __init__(self, ctx: Context, vec: Vec):
+        self.ctx = ctx
+        self.vec = vec
+
+    def size(self) -> int:
+        return self.vec.len
+
+    @classmethod
+    def new(cls, ctx: Context, v, phase: int = 0) -> "ZkVector":
+        """ZkVector::new (src/matrix/mod.rs:29-40)."""
+        out = Vec()
+        dp = _device_ptr(v)
+        if dp is not None:
+            check(lib().svdw_zkvector_new(ctx.handle, phase, dp, v.numel(), 1, ct.byref(out)))
+        else:
+            a = np.ascontiguousarray(v, dtype=np.float64).ravel()
+            check(lib().svdw_zkvector_new(ctx.handle, phase, a.ctypes.data, a.size, 0,
+                                          ct.byref(out)))
+        return cls(ctx, out)
+
+    def entries_less_than(self, max_bits: int) -> None:
+        """ZkVector::entries_less_than (src/matrix/mod.rs:185-194)."""
+        check(lib().svdw_entries_less_than(self.ctx.handle, ct.byref(self.vec), max_bits))
+
+    def entries_in_desc_order(self, max_bits: int) -> None:
+        """ZkVector::entries_in_desc_order (src/matrix/mod.rs:199-215)."""
+        check(lib().svdw_entries_in_desc_order(self.ctx.handle, ct.byref(self.vec), max_bits))
+
+
+def _bound_words(b: int) -> np.ndarray:
+    if b < 0 or b >= (1 << 256):
+        raise SvdwError(-1, "bound must be a non-negative 256-bit integer")
+    return int_to_words(b)
+
+
+def honest_prover_mat_mul(ctx: Context, a: ZkMatrix, b: ZkMatrix, phase: int = 0) -> ZkMatrix:
+    """src/matrix/mod.rs:546-568."""
+    out = Mat()
+    check(lib().svdw_honest_prover_mat_mul(ctx.handle, phase, ct.byref(a.mat), ct.byref(b.mat),
+                                           ct.byref(out)))
+    return ZkMatrix(ctx, out)
+
+
+def field_mat_vec_mul(ctx: Context, a: ZkMatrix, v: ZkVector, phase: int = 0) -> ZkVector:
+    """src/matrix/mod.rs:574-599."""
+    out = Vec()
+    check(lib().svdw_field_mat_vec_mul(ctx.handle, phase, ct.byref(a.mat), ct.byref(v.vec),
+                                       ct.byref(out)))
+    return ZkVector(ctx, out)
+
+
+def mat_times_diag_mat(ctx: Context, a: ZkMatrix, v: ZkVector) -> ZkMatrix:
+    """src/matrix/mod.rs:610-627."""
+    out = Mat()
+    check(lib().svdw_mat_times_diag_mat(ctx.handle, ct.byref(a.mat), ct.byref(v.vec),
+                                        ct.byref(out)))
+    return ZkMatrix(ctx, out)
+
+
+def check_mat_diff(ctx: Context, a: ZkMatrix, b: ZkMatrix, tol: int) -> None:
+    """src/matrix/mod.rs:441-457."""
+    check(lib().svdw_check_mat_diff(ctx.handle, ct.byref(a.mat), ct.byref(b.mat),
+                                    _bound_words(tol).ctypes.data))
+
+
+def check_mat_id(ctx: Context, a: ZkMatrix, scalar_id: ZkVector, tol: int) -> None:
+    """src/matrix/mod.rs:461-483."""
+    check(lib().svdw_check_mat_id(ctx.handle, ct.byref(a.mat), ct.byref(scalar_id.vec),
+                                  _bound_words(tol).ctypes.data))
+
+
+def check_mat_entries_bounded(ctx: Context, a: ZkMatrix, bnd: int) -> None:
+    """src/matrix/mod.rs:490-501."""
+    check(lib().svdw_check_mat_entries_bounded(ctx.handle, ct.byref(a.mat),
+                                               _bound_words(bnd).ctypes.data))
+
+
+def err_calc(p: int, size: int, max_norm: float, eps_svd: float, eps_u: float):
+    """src/svd/mod.rs:155-163."""
+    a, b = ct.c_double(), ct.c_double()
+    check(lib().svdw_err_calc(p, size, max_norm, eps_svd, eps_u, ct.byref(a), ct.byref(b)))
+    return a.value, b.value
+
+
+@dataclass
+class SvdPayload:
+    u_t: ZkMatrix
+    v_t: ZkMatrix
+    m_times_vt: ZkMatrix
+    u_times_ut: ZkMatrix
+    v_times_vt: ZkMatrix
+    raw: Payload
+
+
+def check_svd_phase0(ctx: Context, m: ZkMatrix, u: ZkMatrix, v: ZkMatrix, d: ZkVector,
+                     err_svd: float, err_u: float, max_bits_d: int) -> SvdPayload:
+    """src/svd/mod.rs:32-116."""
+    pl = Payload()
+    check(lib().svdw_check_svd_phase0(ctx.handle, ct.byref(m.mat), ct.byref(u.mat),
+                                      ct.byref(v.mat), ct.byref(d.vec), err_svd, err_u,
+                                      max_bits_d, ct.byref(pl)))
+    return SvdPayload(ZkMatrix(ctx, pl.u_t), ZkMatrix(ctx, pl.v_t), ZkMatrix(ctx, pl.m_times_vt),
+                      ZkMatrix(ctx, pl.u_times_ut), ZkMatrix(ctx, pl.v_times_vt), pl)
+
+
+def check_svd_phase1(ctx: Context, m: ZkMatrix, u: ZkMatrix, v: ZkMatrix, payload: SvdPayload,
+                     init_rand: int) -> None:
+    """src/svd/mod.rs:127-144."""
+    g = int_to_words(int(init_rand) % P_MOD)
+    check(lib().svdw_check_svd_phase1(ctx.handle, ct.byref(m.mat), ct.byref(u.mat),
+                                      ct.byref(v.mat), ct.byref(payload.raw), g.ctypes.data))
+
+
+@dataclass
+class SvdConfigPy:
+    """examples/svd_example.rs:115-118,160."""
+    max_norm: float = 100.0
+    eps_svd: float = 1e-10
+    eps_u: float = 1e-10
+    max_bits_d: int = 30
+
+    def c(self) -> SvdConfig:
+        return SvdConfig(self.max_norm, self.eps_svd, self.eps_u, self.max_bits_d)
+
+
+def svd_witness(ctx: Context, m, u, v, d, gamma: int, cfg: SvdConfigPy = SvdConfigPy()) -> dict:
+    """Whole witness of examples/svd_example.rs:98-200 (intended one-context
+    semantics). Inputs: numpy arrays (host) or contiguous float64 torch CUDA
+    tensors on the context's device (then nothing is copied over PCIe)."""
+    cfgc = cfg.c()
+    cnt = Counts()
+    g = int_to_words(int(gamma) % P_MOD)
+    dps = [_device_ptr(x) for x in (m, u, v, d)]
+    if all(p is not None for p in dps):
+        N, M = m.shape
+        check(lib().svdw_svd_witness(ctx.handle, *dps, N, M, 1, ct.byref(cfgc), g.ctypes.data,
+                                     ct.byref(cnt)))
+    else:
+        arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (m, u, v, d)]
+        N, M = arrs[0].shape
+        if arrs[1].shape != (N, N) or arrs[2].shape != (M, M) or arrs[3].size != min(N, M):
+            raise SvdwError(-1, "svd_witness: shapes must be m NxM, u NxN, v MxM, d min(N,M)")
+        check(lib().svdw_svd_witness(ctx.handle, *[a.ctypes.data for a in arrs], N, M, 0,
+                                     ct.byref(cfgc), g.ctypes.data, ct.byref(cnt)))
+    return cnt.as_dict()
+
+
+def plan_svd(N: int, M: int, precision_bits: int, lookup_bits: int,
+             cfg: SvdConfigPy = SvdConfigPy()) -> dict:
+    """Closed-form cell counts (no device)."""
+    cfgc = cfg.c()
+    cnt = Counts()
+    check(lib().svdw_plan_svd(N, M, precision_bits, lookup_bits, ct.byref(cfgc), ct.byref(cnt)))
+    return cnt.as_dict()

@@ -1,0 +1,183 @@
+/*
+ * svdw.h — C ABI of the MI355X-native SVD-verify witness engine.
+ *
+ * Drop-in boundary for the witness path of neilcouture/halo2-svd041: every
+ * entry point replaces one reference function that appends BN254-Fr cells to
+ * a halo2-base `Context` (citations: reference repo paths). Values are the
+ * canonical little-endian 32-byte cells (halo2curves `Fr::to_repr`), stored
+ * device-resident in per-phase advice / lookup streams owned by the context.
+ * Handles (svdw_mat / svdw_vec) are plain views (offset + strides) into a
+ * phase's advice stream, valid for the context's lifetime — the analogue of
+ * `Vec<Vec<AssignedValue<F>>>` (src/matrix/mod.rs:219-223), with transpose a
+ * stride swap (src/matrix/mod.rs:408-419).
+ *
+ * Errors: every call returns SVDW_OK or a negative code and never aborts; the
+ * reference panics (assert!/assert_eq!) on the same conditions
+ * (src/matrix/mod.rs:86,142,175,239,307-310,515,580,616; src/svd/mod.rs:50-61).
+ * svdw_last_error() gives the thread-local message of the last failure.
+ * Threading: one context = one `&mut Context` per phase; not thread safe.
+ * Work is enqueued on the context's HIP stream; svdw_sync() waits for it.
+ */
+#ifndef SVDW_H
+#define SVDW_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SVDW_OK 0
+#define SVDW_EINVAL -1   /* shape / argument mismatch (reference: assert! panic) */
+#define SVDW_ERANGE -2   /* unsupported precision / lookup bits / bound */
+#define SVDW_EDEVICE -3  /* HIP runtime error */
+#define SVDW_ENOMEM -4
+
+typedef struct svdw_ctx svdw_ctx;
+
+typedef struct {
+    int device;               /* HIP device ordinal (-1: host-only planning context) */
+    uint32_t precision_bits;  /* FixedPointChip041 PRECISION_BITS, 1..63 */
+    uint32_t lookup_bits;     /* RangeChip lookup_bits (LOOKUP_BITS env), 8..63 */
+} svdw_params;
+
+/* View of cells of one phase's advice stream:
+ * cell(i, j) = stream[phase][off + i*rs + j*cs]. */
+typedef struct {
+    uint32_t phase;
+    uint32_t rows, cols;
+    uint64_t off;
+    int64_t rs, cs;
+} svdw_mat;
+
+typedef struct {
+    uint32_t phase;
+    uint32_t len;
+    uint64_t off;
+    int64_t stride;
+} svdw_vec;
+
+/* check_svd_phase0's return tuple (src/svd/mod.rs:42-48,115). */
+typedef struct {
+    svdw_mat u_t, v_t, m_times_vt, u_times_ut, v_times_vt;
+} svdw_svd_payload;
+
+/* Constants of the example caller (examples/svd_example.rs:115-118,149,160). */
+typedef struct {
+    double max_norm;    /* MAX_NORM = 100.0 */
+    double eps_svd;     /* EPS_SVD = 1e-10 */
+    double eps_u;       /* EPS_U = 1e-10 */
+    uint32_t max_bits_d;/* 30 */
+} svdw_svd_config;
+
+/* Cell totals of one SVD witness (phase 0 + phase 1). */
+typedef struct {
+    uint64_t advice0, advice1, lookup0, lookup1;
+} svdw_counts;
+
+/* ---------------------------------------------------------------- context */
+int svdw_ctx_create(const svdw_params* params, svdw_ctx** out);
+int svdw_ctx_destroy(svdw_ctx* ctx);
+/* Drop all cells of both phases (allocations are kept). */
+int svdw_ctx_reset(svdw_ctx* ctx);
+/* Pre-size a phase's advice / lookup streams (cells). */
+int svdw_reserve(svdw_ctx* ctx, uint32_t phase, uint64_t advice_cells, uint64_t lookup_cells);
+int svdw_sync(svdw_ctx* ctx);
+const char* svdw_last_error(void);
+
+/* ------------------------------------------------------ stream access */
+uint64_t svdw_advice_len(const svdw_ctx* ctx, uint32_t phase);
+uint64_t svdw_lookup_len(const svdw_ctx* ctx, uint32_t phase);
+/* Device pointers to the canonical 32-byte cells (valid until the next append). */
+const void* svdw_advice_device_ptr(const svdw_ctx* ctx, uint32_t phase);
+const void* svdw_lookup_device_ptr(const svdw_ctx* ctx, uint32_t phase);
+/* Copy cells [off, off+n) to host memory (4 x u64 little endian per cell); syncs. */
+int svdw_copy_advice(svdw_ctx* ctx, uint32_t phase, uint64_t off, uint64_t n, uint64_t* out);
+int svdw_copy_lookup(svdw_ctx* ctx, uint32_t phase, uint64_t off, uint64_t n, uint64_t* out);
+
+/* ------------------------------------------- ZkMatrix / ZkVector (matrix/mod.rs) */
+/* ZkMatrix::new (src/matrix/mod.rs:230-252): quantize + load_witness, row-major.
+ * data: rows*cols f64 (host memory, or device memory if on_device). */
+int svdw_zkmatrix_new(svdw_ctx* ctx, uint32_t phase, const double* data, uint32_t rows,
+                      uint32_t cols, int on_device, svdw_mat* out);
+/* ZkVector::new (src/matrix/mod.rs:29-40). */
+int svdw_zkvector_new(svdw_ctx* ctx, uint32_t phase, const double* data, uint32_t len,
+                      int on_device, svdw_vec* out);
+/* ZkMatrix::transpose_matrix (src/matrix/mod.rs:408-419): no cells. */
+int svdw_transpose_matrix(const svdw_mat* a, svdw_mat* out);
+/* Context::load_witness / load_constant of one canonical value (halo2-base). */
+int svdw_load_witness(svdw_ctx* ctx, uint32_t phase, const uint64_t value[4], svdw_vec* out);
+int svdw_load_constant(svdw_ctx* ctx, uint32_t phase, const uint64_t value[4], svdw_vec* out);
+
+/* ZkVector::entries_less_than (src/matrix/mod.rs:185-194). */
+int svdw_entries_less_than(svdw_ctx* ctx, const svdw_vec* d, uint32_t max_bits);
+/* ZkVector::entries_in_desc_order (src/matrix/mod.rs:199-215). */
+int svdw_entries_in_desc_order(svdw_ctx* ctx, const svdw_vec* d, uint32_t max_bits);
+
+/* check_mat_entries_bounded (src/matrix/mod.rs:490-501): |a_ij| < bnd.
+ * bnd: unsigned 256-bit little endian (BigUint). */
+int svdw_check_mat_entries_bounded(svdw_ctx* ctx, const svdw_mat* a, const uint64_t bnd[4]);
+/* check_mat_diff (src/matrix/mod.rs:441-457): |a_ij - b_ij| < tol. */
+int svdw_check_mat_diff(svdw_ctx* ctx, const svdw_mat* a, const svdw_mat* b,
+                        const uint64_t tol[4]);
+/* check_mat_id (src/matrix/mod.rs:461-483): |a_ij - scalar_id*I_ij| < tol. */
+int svdw_check_mat_id(svdw_ctx* ctx, const svdw_mat* a, const svdw_vec* scalar_id,
+                      const uint64_t tol[4]);
+/* mat_times_diag_mat (src/matrix/mod.rs:610-627): a[i][j]*v[j], j < len(v). */
+int svdw_mat_times_diag_mat(svdw_ctx* ctx, const svdw_mat* a, const svdw_vec* v, svdw_mat* out);
+/* honest_prover_mat_mul (src/matrix/mod.rs:546-568): c_s = a*b over Fr, loaded row-major. */
+int svdw_honest_prover_mat_mul(svdw_ctx* ctx, uint32_t phase, const svdw_mat* a,
+                               const svdw_mat* b, svdw_mat* c_s);
+/* field_mat_vec_mul (src/matrix/mod.rs:574-599): one inner_product per row of a;
+ * out = the row results (last cell of each row block). */
+int svdw_field_mat_vec_mul(svdw_ctx* ctx, uint32_t phase, const svdw_mat* a, const svdw_vec* v,
+                           svdw_vec* out);
+/* ZkMatrix::verify_mul (src/matrix/mod.rs:299-342), Freivalds with v = (1, g, g^2, ...);
+ * gamma: canonical init_rand value (rlc.gamma_pow_cached()[0]). */
+int svdw_verify_mul(svdw_ctx* ctx, uint32_t phase, const svdw_mat* a, const svdw_mat* b,
+                    const svdw_mat* c_s, const uint64_t gamma[4]);
+
+/* ------------------------------------------------------------ svd (svd/mod.rs) */
+/* err_calc (src/svd/mod.rs:155-163). */
+int svdw_err_calc(uint32_t p, uint64_t size, double max_norm, double eps_svd, double eps_u,
+                  double* err_svd, double* err_u);
+/* check_svd_phase0 (src/svd/mod.rs:32-116), appending to phase 0. */
+int svdw_check_svd_phase0(svdw_ctx* ctx, const svdw_mat* m, const svdw_mat* u, const svdw_mat* v,
+                          const svdw_vec* d, double err_svd, double err_u, uint32_t max_bits_d,
+                          svdw_svd_payload* out);
+/* check_svd_phase1 (src/svd/mod.rs:127-144), appending to phase 1. */
+int svdw_check_svd_phase1(svdw_ctx* ctx, const svdw_mat* m, const svdw_mat* u, const svdw_mat* v,
+                          const svdw_svd_payload* payload, const uint64_t gamma[4]);
+
+/* Whole SVD-verify witness of examples/svd_example.rs:98-200 (intended
+ * one-context semantics): reset, ZkMatrix::new(m,u,v), ZkVector::new(d),
+ * err_calc(P, max(N,M), ...), check_svd_phase0 into phase 0, then
+ * check_svd_phase1 into phase 1. m: N x M, u: N x N, v: M x M, d: min(N,M),
+ * all row-major f64 (device memory if on_device). */
+int svdw_svd_witness(svdw_ctx* ctx, const double* m, const double* u, const double* v,
+                     const double* d, uint32_t N, uint32_t M, int on_device,
+                     const svdw_svd_config* cfg, const uint64_t gamma[4], svdw_counts* counts);
+/* ----------------------------------------------------------- profiling */
+/* Per-kernel statistics from HIP events recorded around every launch on the
+ * context stream. bytes / ops: algorithmic HBM bytes / MACs of the launches
+ * (cells x 32 B written + input cells read; GEMM MACs = N*M*K). */
+typedef struct {
+    char name[48];
+    uint64_t launches;
+    double total_ms, max_ms;
+    double bytes, ops;
+} svdw_kstat;
+/* Enable (1) / disable (0) event recording; drops pending records. */
+int svdw_profile_enable(svdw_ctx* ctx, int on);
+/* Synchronize, aggregate pending records by kernel name (up to cap entries
+ * written to out; *n = number of distinct names) and drop them. */
+int svdw_profile_collect(svdw_ctx* ctx, svdw_kstat* out, uint32_t cap, uint32_t* n);
+
+/* Closed-form cell counts of svdw_svd_witness without touching a device. */
+int svdw_plan_svd(uint32_t N, uint32_t M, uint32_t precision_bits, uint32_t lookup_bits,
+                  const svdw_svd_config* cfg, svdw_counts* counts);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SVDW_H */

@@ -1,0 +1,122 @@
+"""GPU parity: the HIP witness engine vs the CPU oracle restatement, bit-exact.
+
+Every test calls the product through the C ABI (halo2_svd041_amd -> libsvdw.so)
+and compares the full advice / lookup streams with oracle/svdw_oracle.c on the
+same seeded inputs (input-creator.py recipe) and the same gamma.
+"""
+import numpy as np
+import pytest
+
+import corc
+from conftest import gamma_for, gen_svd_input
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_streams(ctx, a0, l0, a1):
+    g0, gl0, g1 = ctx.advice(0), ctx.lookups(0), ctx.advice(1)
+    assert g0.shape == a0.shape, (g0.shape, a0.shape)
+    assert g1.shape == a1.shape, (g1.shape, a1.shape)
+    assert gl0.shape == l0.shape, (gl0.shape, l0.shape)
+    for name, g, o in (("advice0", g0, a0), ("lookup0", gl0, l0), ("advice1", g1, a1)):
+        bad = np.nonzero(np.any(g != o, axis=1))[0]
+        assert bad.size == 0, f"{name}: {bad.size} cells differ, first at {bad[:8]}"
+
+
+SHAPES = [
+    (1, 1, 32), (2, 2, 63), (4, 4, 32), (4, 3, 63), (3, 4, 42), (6, 6, 42), (5, 7, 63),
+    (8, 8, 32), (16, 16, 63), (33, 31, 32), (31, 33, 63), (40, 40, 40), (64, 64, 63),
+]
+
+
+@pytest.mark.parametrize("N,M,P", SHAPES)
+def test_svd_witness_parity(gpu_ctx_factory, N, M, P):
+    import halo2_svd041_amd as hs
+    m, u, d, v = gen_svd_input(N, M, seed=N * 1000 + M * 10 + P)
+    g = gamma_for(N + M + P)
+    ctx = gpu_ctx_factory(P)
+    cnt = hs.svd_witness(ctx, m, u, v, d, g)
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+    assert cnt["advice0"] == a0.shape[0] and cnt["advice1"] == a1.shape[0]
+    _assert_streams(ctx, a0, l0, a1)
+
+
+@pytest.mark.parametrize("lb", [8, 11, 13, 17, 24])
+def test_lookup_bits_parity(gpu_ctx_factory, lb):
+    import halo2_svd041_amd as hs
+    m, u, d, v = gen_svd_input(9, 7, seed=lb)
+    g = gamma_for(lb)
+    for P in (32, 63):
+        ctx = gpu_ctx_factory(P, lb)
+        hs.svd_witness(ctx, m, u, v, d, g)
+        a0, l0, a1 = corc.svd_witness(m, u, v, d, P, lb, g)
+        _assert_streams(ctx, a0, l0, a1)
+
+
+def test_matrix_wrong_parity(gpu_ctx_factory):
+    """input-creator.py:46-49 perturbation: witness still bit-exact."""
+    import halo2_svd041_amd as hs
+    m, u, d, v = gen_svd_input(12, 12, seed=5)
+    m = m.copy()
+    m[3][7] += 1e-7
+    for P in (32, 63):
+        ctx = gpu_ctx_factory(P)
+        hs.svd_witness(ctx, m, u, v, d, gamma_for(7))
+        a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, gamma_for(7))
+        _assert_streams(ctx, a0, l0, a1)
+
+
+def test_garbage_inputs_parity(gpu_ctx_factory):
+    """Non-SVD inputs: large, tiny, negative zero, ties, NaN, inf (quantization
+    edges; non-zero Freivalds differences exercise the is_zero inverse path)."""
+    import halo2_svd041_amd as hs
+    rs = np.random.RandomState(11)
+    N, M = 6, 5
+    m = rs.standard_normal((N, M)) * 50
+    u = rs.standard_normal((N, N))
+    v = rs.standard_normal((M, M))
+    d = np.abs(rs.standard_normal(min(N, M)))
+    m[0, 0] = -0.0
+    m[0, 1] = 0.5 / 2 ** 32          # exact tie at P=32
+    m[0, 2] = -1.5 / 2 ** 32
+    u[1, 1] = 1.0
+    u[1, 2] = -1.0
+    v[2, 2] = 3e5
+    d[0] = 1e9
+    for P in (32, 63):
+        ctx = gpu_ctx_factory(P)
+        g = gamma_for(99)
+        hs.svd_witness(ctx, m, u, v, d, g)
+        a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+        _assert_streams(ctx, a0, l0, a1)
+
+
+def test_generic_gemm_fallback_parity(gpu_ctx_factory):
+    """Operands too wide for the digit GEMM (|x| >= 2^72) take the Montgomery path."""
+    import halo2_svd041_amd as hs
+    rs = np.random.RandomState(3)
+    N = 5
+    m = rs.uniform(-1, 1, (N, N)) * 2.0 ** 20
+    u, d, v = np.eye(N), np.ones(N), np.eye(N)
+    ctx = gpu_ctx_factory(63)
+    hs.svd_witness(ctx, m, u, v, d, 5)
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, 63, 19, 5)
+    _assert_streams(ctx, a0, l0, a1)
+
+
+def test_modular_api_matches_whole_witness(gpu_ctx_factory):
+    """ZkMatrix::new + check_svd_phase0/1 through the modular ABI == svd_witness."""
+    import halo2_svd041_amd as hs
+    N, M, P = 10, 13, 42
+    m, u, d, v = gen_svd_input(N, M, seed=17)
+    g = gamma_for(17)
+    ctx = gpu_ctx_factory(P)
+    zm = hs.ZkMatrix.new(ctx, m)
+    zu = hs.ZkMatrix.new(ctx, u)
+    zv = hs.ZkMatrix.new(ctx, v)
+    zd = hs.ZkVector.new(ctx, d)
+    es, eu = hs.err_calc(P, max(N, M), 100.0, 1e-10, 1e-10)
+    pl = hs.check_svd_phase0(ctx, zm, zu, zv, zd, es, eu, 30)
+    hs.check_svd_phase1(ctx, zm, zu, zv, pl, g)
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+    _assert_streams(ctx, a0, l0, a1)
