@@ -30,6 +30,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+ORACLE_DIR = os.path.join(ROOT, "oracle")   # cpu_baseline leg only
 
 P_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -78,6 +79,7 @@ def roofline_from_profile(stats, steps):
 
 
 def cpu_baseline(m, u, v, d, P, LB, g, rows):
+    sys.path.insert(0, ORACLE_DIR)
     import corc  # oracle/ — the checker / reported baseline only
     t0 = time.perf_counter()
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, LB, g, row_lim=rows)

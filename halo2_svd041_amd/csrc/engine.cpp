@@ -274,10 +274,35 @@ struct svdw_ctx {
     };
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
+    // second stream: GEMMs (integer-VALU bound) overlap the HBM-bound stages
+    hipStream_t st2 = nullptr;
+    bool overlap = true;
+    struct PreGemm {
+        uint64_t off;
+        hipEvent_t ev;
+    };
+    std::vector<PreGemm> pre;               // GEMMs launched ahead on st2, in append order
+    std::vector<uint64_t>* gemm_log = nullptr;   // dry run: offsets of honest_prover_mat_mul
+    std::vector<hipEvent_t> deps;           // dependency events (no timing)
+    size_t dep_next = 0;
 };
 
 static void sync(svdw_ctx* c) {
-    if (!c->dry) hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
+    if (c->dry) return;
+    hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
+    hipck(hipStreamSynchronize(c->st2), "hipStreamSynchronize");
+}
+// Event recorded on `from`; `to` waits for it (cross-stream dependency).
+static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
+    if (c->dep_next == c->deps.size()) {
+        hipEvent_t e;
+        hipck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        c->deps.push_back(e);
+    }
+    hipEvent_t e = c->deps[c->dep_next++];
+    hipck(hipEventRecord(e, from), "hipEventRecord");
+    if (to) hipck(hipStreamWaitEvent(to, e, 0), "hipStreamWaitEvent");
+    return e;
 }
 // RAII: brackets one kernel launch with HIP events on the context stream.
 struct ProfScope {
@@ -293,15 +318,17 @@ struct ProfScope {
         hipck(hipEventCreate(&e), "hipEventCreate");
         return e;
     }
-    ProfScope(svdw_ctx* cc, const std::string& name, double bytes, double ops) : c(cc) {
+    hipStream_t s = nullptr;
+    ProfScope(svdw_ctx* cc, hipStream_t ss, const std::string& name, double bytes, double ops)
+        : c(cc), s(ss) {
         if (!c->prof || c->dry) return;
         svdw_ctx::Rec r{name, bytes, ops, ev(c), ev(c)};
-        hipck(hipEventRecord(r.e0, c->st), "hipEventRecord");
+        hipck(hipEventRecord(r.e0, s), "hipEventRecord");
         c->recs.push_back(r);
         idx = (long)c->recs.size() - 1;
     }
     ~ProfScope() {
-        if (idx >= 0) (void)hipEventRecord(c->recs[idx].e1, c->st);
+        if (idx >= 0) (void)hipEventRecord(c->recs[idx].e1, s);
     }
 };
 
@@ -391,7 +418,7 @@ static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, u
     uint32_t loads = 0;
     for (uint32_t i = 0; i < a.nmo; ++i) loads += a.mo[i].op == MO_LOAD;
     {
-        ProfScope ps(c, std::string("k_stage:") + tag,
+        ProfScope ps(c, c->st, std::string("k_stage:") + tag,
                      32.0 * nelem * ((double)a.C + a.L + loads), 0);
         hipck(launch_stage(a, c->st), "k_stage");
     }
@@ -419,7 +446,7 @@ static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, ui
                   "H2D");
             src = (const double*)c->f64in.p;
         }
-        ProfScope ps(c, "k_quantize", 40.0 * n, 0);
+        ProfScope ps(c, c->st, "k_quantize", 40.0 * n, 0);
         hipck(launch_quantize(src, n, cellp(c, phase, off), (int)c->P, c->st), "k_quantize");
     }
     return svdw_mat{phase, rows, cols, off, (int64_t)cols, 1};
@@ -528,16 +555,63 @@ static std::vector<uint32_t> maxbits_many(svdw_ctx* c, const std::vector<svdw_ma
     for (size_t i = 0; i < ms.size(); ++i) out[i] = h[i];
     return out;
 }
-// honest_prover_mat_mul (+ field_mat_mul). bits_a/bits_b: known bounds or ~0u.
+// field_mat_mul (src/matrix/mod.rs:510-537) on stream `s`: c_s = a * b written
+// as canonical cells at `out` (row-major). Exact: balanced base-256 digit planes
+// + v_dot4c_i32_i8 when |entries| fit 9 digits, else Montgomery per MAC.
+static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_mat& b, Fr* out,
+                      uint32_t bits_a, uint32_t bits_b) {
+    const uint32_t N = a.rows, K = a.cols, M = b.cols;
+    const bool sym = is_transpose_of(b, a);
+    int DA = round_digits(digits_for_bits(bits_a)), DB = round_digits(digits_for_bits(bits_b));
+    if (DA && DB && K <= 8192 && gemm_digits_supported(DA, DB)) {
+        const uint32_t kg = ((K + 3) / 4 + 7) / 8 * 8;
+        const uint32_t npad = (N + 31) / 32 * 32, mpad = (M + 31) / 32 * 32;
+        ensure_buf(c, c->digA, (size_t)npad * kg * DA * 4);
+        {
+            ProfScope ps(c, s, "k_to_digits", 32.0 * N * K + 4.0 * npad * kg * DA, 0);
+            hipck(launch_to_digits(view_of(c, a), N, K, DA, npad, kg, (uint32_t*)c->digA.p, s),
+                  "k_to_digits");
+        }
+        const uint32_t* Bd = (const uint32_t*)c->digA.p;
+        if (!sym) {
+            ensure_buf(c, c->digB, (size_t)mpad * kg * DB * 4);
+            svdw_mat bt = b;   // Bt(j, k) = b(k, j)
+            bt.rows = b.cols; bt.cols = b.rows; bt.rs = b.cs; bt.cs = b.rs;
+            ProfScope ps(c, s, "k_to_digits", 32.0 * M * K + 4.0 * mpad * kg * DB, 0);
+            hipck(launch_to_digits(view_of(c, bt), M, K, DB, mpad, kg, (uint32_t*)c->digB.p, s),
+                  "k_to_digits");
+            Bd = (const uint32_t*)c->digB.p;
+        }
+        ProfScope ps(c, s, std::string("k_gemm_dot4:") + std::to_string(DA) + "x" +
+                               std::to_string(DB) + (sym ? "s" : ""),
+                     4.0 * kg * ((double)npad * DA + (sym ? 0.0 : (double)mpad * DB)) + 32.0 * N * M,
+                     (double)N * M * K);
+        hipck(launch_gemm_digits(DA, DB, sym, (const uint32_t*)c->digA.p, Bd, N, M, kg, out, M, 1, s),
+              "k_gemm_dot4");
+    } else {
+        ProfScope ps(c, s, "k_gemm_mont", 32.0 * ((double)N * K + (double)K * M + (double)N * M),
+                     (double)N * M * K);
+        hipck(launch_gemm_mont(view_of(c, a), view_of(c, b), N, K, M, out, M, 1, s), "k_gemm_mont");
+    }
+}
+// honest_prover_mat_mul (src/matrix/mod.rs:546-568). bits_a/bits_b: known bounds or ~0u.
+// If the product was launched ahead on st2 (c->pre), only append and order st after it.
 static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a,
                                       const svdw_mat& b, uint32_t bits_a = ~0u,
                                       uint32_t bits_b = ~0u) {
     REQUIRE(a.cols == b.rows, "honest_prover_mat_mul: a.num_col != b.num_rows");
-    const uint32_t N = a.rows, K = a.cols, M = b.cols;
+    const uint32_t N = a.rows, M = b.cols;
     uint64_t off;
     append(c, phase, (uint64_t)N * M, 0, &off, nullptr);
     svdw_mat cs{phase, N, M, off, (int64_t)M, 1};
+    if (c->gemm_log) c->gemm_log->push_back(off);
     if (c->dry) return cs;
+    if (!c->pre.empty()) {
+        if (c->pre.front().off != off) fail(SVDW_EDEVICE, "internal: pre-launched GEMM offset mismatch");
+        hipck(hipStreamWaitEvent(c->st, c->pre.front().ev, 0), "hipStreamWaitEvent");
+        c->pre.erase(c->pre.begin());
+        return cs;
+    }
     const bool sym = is_transpose_of(b, a);
     if (bits_a == ~0u || bits_b == ~0u) {
         std::vector<svdw_mat> ms{a};
@@ -546,39 +620,7 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
         bits_a = bb[0];
         bits_b = sym ? bb[0] : bb[1];
     }
-    int DA = round_digits(digits_for_bits(bits_a)), DB = round_digits(digits_for_bits(bits_b));
-    Fr* out = cellp(c, phase, off);
-    if (DA && DB && K <= 8192 && gemm_digits_supported(DA, DB)) {
-        const uint32_t kg = ((K + 3) / 4 + 7) / 8 * 8;
-        const uint32_t npad = (N + 31) / 32 * 32, mpad = (M + 31) / 32 * 32;
-        ensure_buf(c, c->digA, (size_t)npad * kg * DA * 4);
-        {
-            ProfScope ps(c, "k_to_digits", 32.0 * N * K + 4.0 * npad * kg * DA, 0);
-            hipck(launch_to_digits(view_of(c, a), N, K, DA, npad, kg, (uint32_t*)c->digA.p, c->st),
-                  "k_to_digits");
-        }
-        const uint32_t* Bd = (const uint32_t*)c->digA.p;
-        if (!sym) {
-            ensure_buf(c, c->digB, (size_t)mpad * kg * DB * 4);
-            svdw_mat bt = b;   // Bt(j, k) = b(k, j)
-            bt.rows = b.cols; bt.cols = b.rows; bt.rs = b.cs; bt.cs = b.rs;
-            ProfScope ps(c, "k_to_digits", 32.0 * M * K + 4.0 * mpad * kg * DB, 0);
-            hipck(launch_to_digits(view_of(c, bt), M, K, DB, mpad, kg, (uint32_t*)c->digB.p,
-                                   c->st), "k_to_digits");
-            Bd = (const uint32_t*)c->digB.p;
-        }
-        ProfScope ps(c, std::string("k_gemm_dot4:") + std::to_string(DA) + "x" + std::to_string(DB) +
-                            (sym ? "s" : ""),
-                     4.0 * kg * ((double)npad * DA + (sym ? 0.0 : (double)mpad * DB)) + 32.0 * N * M,
-                     (double)N * M * K);
-        hipck(launch_gemm_digits(DA, DB, sym, (const uint32_t*)c->digA.p, Bd, N, M, kg, out, M, 1,
-                                 c->st), "k_gemm_dot4");
-    } else {
-        ProfScope ps(c, "k_gemm_mont", 32.0 * ((double)N * K + (double)K * M + (double)N * M),
-                     (double)N * M * K);
-        hipck(launch_gemm_mont(view_of(c, a), view_of(c, b), N, K, M, out, M, 1, c->st),
-              "k_gemm_mont");
-    }
+    gemm_exec(c, c->st, a, b, cellp(c, phase, off), bits_a, bits_b);
     return cs;
 }
 // field_mat_vec_mul with the vector given as canonical + Montgomery copies.
@@ -588,7 +630,7 @@ static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, cons
     uint64_t off;
     append(c, phase, (uint64_t)R * (3ull * L + 1), 0, &off, nullptr);
     if (!c->dry) {
-        ProfScope ps(c, "k_matvec_scan", 32.0 * (double)R * (4.0 * L + 1) + 64.0 * L, (double)R * L);
+        ProfScope ps(c, c->st, "k_matvec_scan", 32.0 * (double)R * (4.0 * L + 1) + 64.0 * L, (double)R * L);
         hipck(launch_matvec_scan(view_of(c, a), 0, R, L, wc, wm, cellp(c, phase, off), c->st),
               "k_matvec_scan");
     }
@@ -614,19 +656,27 @@ static void verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svd
     REQUIRE(cs.rows == a.rows, "verify_mul: c_s.len() != a.num_rows");
     REQUIRE(cs.cols == b.cols, "verify_mul: c_s[0].len() != b.num_col");
     const uint32_t d = cs.cols, n = a.rows, k = a.cols;
-    put_cell(c, phase, fr_from_u64(1));                    // load_witness(F::ONE)
-    if (d > 1) {                                          // v_i = v_{i-1} * init_rand
-        PB pb(c->LB);
-        uint8_t kg = pb.kidx(gamma);
-        uint8_t prev = pb.newv(), cur = pb.newv();
-        pb.op(MO_POWK, prev, kg, 0, 0);
-        pb.op(MO_POWK, cur, kg, 0, 1);
-        pb.cell(pb.K(0)); pb.cell(prev); pb.cell(KSRC + kg); pb.cell(cur);
-        run_stage(c, phase, pb, d - 1, 1, "verify_mul_gamma_pows");
-    }
+    // v = (1, g, g^2, ...): canonical + Montgomery copies for the row scans
     ensure_buf(c, c->w1c, (size_t)d * sizeof(Fr));
     ensure_buf(c, c->w1m, (size_t)d * sizeof(Fr));
-    if (!c->dry) hipck(launch_gamma_vec(gamma, d, (Fr*)c->w1c.p, (Fr*)c->w1m.p, c->st), "k_gamma_vec");
+    if (!c->dry) {
+        ProfScope ps(c, c->st, "k_gamma_vec", 64.0 * d, 0);
+        hipck(launch_gamma_vec(gamma, d, (Fr*)c->w1c.p, (Fr*)c->w1m.p, c->st), "k_gamma_vec");
+    }
+    put_cell(c, phase, fr_from_u64(1));                    // load_witness(F::ONE)
+    if (d > 1) {                                          // v_i = mul(v_{i-1}, init_rand)
+        PB pb(c->LB);
+        DView w;
+        memset(&w, 0, sizeof w);
+        w.ptr = (const Fr*)c->w1c.p;
+        w.rs = 1; w.cs = 0; w.rows = d; w.cols = 1;
+        pb.a.view[0] = w;
+        pb.a.view[1] = w;
+        if (!c->dry) pb.a.view[1].ptr = (const Fr*)c->w1c.p + 1;
+        uint8_t prev = pb.load(0), cur = pb.load(1);
+        pb.cell(pb.K(0)); pb.cell(prev); pb.cell(pb.K(gamma)); pb.cell(cur);
+        run_stage(c, phase, pb, d - 1, 1, "verify_mul_gamma_pows");
+    }
     svdw_vec csv = matvec_rows(c, phase, cs, (const Fr*)c->w1c.p, (const Fr*)c->w1m.p);
     svdw_vec bv = matvec_rows(c, phase, b, (const Fr*)c->w1c.p, (const Fr*)c->w1m.p);
     vec_prep(c, bv, c->w2c, c->w2m);
@@ -670,6 +720,29 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     REQUIRE(d.len == r, "check_svd_phase0: d.len != min(N, M)");
     const uint32_t P = c->P;
     const uint32_t max_bits = max_bits_d + P;
+    if (!c->dry && c->overlap && known_bits && c->pre.empty()) {
+        // The three products depend only on m, u, v: take their stream offsets
+        // from a dry replay of this function and launch them now on st2, so the
+        // integer-VALU GEMMs run under the HBM-bound check stages on st.
+        svdw_ctx plan;
+        plan.P = c->P; plan.LB = c->LB;
+        for (int p = 0; p < 2; ++p) { plan.ph[p].n = c->ph[p].n; plan.ph[p].nl = c->ph[p].nl; }
+        std::vector<uint64_t> log;
+        plan.gemm_log = &log;
+        check_svd_phase0(&plan, m, u, v, d, err_svd, err_u, max_bits_d, known_bits);
+        REQUIRE(log.size() == 3, "internal: expected three products in check_svd_phase0");
+        svdw_mat ut = u, vt = v;
+        std::swap(ut.rows, ut.cols); std::swap(ut.rs, ut.cs);
+        std::swap(vt.rows, vt.cols); std::swap(vt.rs, vt.cs);
+        stream_dep(c, c->st, c->st2);                      // loads of m, u, v done
+        const svdw_mat A[3] = {m, u, v}, B[3] = {vt, ut, vt};
+        const uint32_t ba[3] = {known_bits[0], known_bits[1], known_bits[2]};
+        const uint32_t bb[3] = {known_bits[2], known_bits[1], known_bits[2]};
+        for (int g = 0; g < 3; ++g) {
+            gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ba[g], bb[g]);
+            c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
+        }
+    }
     entries_less_than(c, d, max_bits);
     entries_in_desc_order(c, d, max_bits);
     BigU unit = big_from_u128(((unsigned __int128)1 << P) + 1);
@@ -714,6 +787,8 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     REQUIRE(N >= 1 && M >= 1, "empty matrix");
     const uint32_t r = std::min(N, M);
     for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
+    c->dep_next = 0;
+    c->pre.clear();
     if (!c->dry) {
         // exact sizes from the dry planner: no growth copies inside the step
         svdw_ctx plan;
@@ -757,6 +832,7 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
         if (!c->dry) {
             hipError_t e = hipSetDevice(p->device);
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking);
             if (e != hipSuccess) {
                 delete c;
                 fail(SVDW_EDEVICE, std::string("HIP device init failed: ") + hipGetErrorString(e));
@@ -775,6 +851,9 @@ int svdw_ctx_destroy(svdw_ctx* c) {
                 if (b->p) (void)hipFree(b->p);
             for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
             for (auto e : c->pool) (void)hipEventDestroy(e);
+            for (auto e : c->deps) (void)hipEventDestroy(e);
+            (void)hipStreamSynchronize(c->st2);
+            (void)hipStreamDestroy(c->st2);
             (void)hipStreamDestroy(c->st);
         }
         delete c;

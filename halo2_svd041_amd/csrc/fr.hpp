@@ -159,11 +159,11 @@ SVDW_HD Fr fr_from_mont(const Fr& a) { return mont_mul(a, fr_from_u64(1)); }
 // Canonical product.
 SVDW_HD Fr fr_mul(const Fr& a, const Fr& b) { return mont_mul(mont_mul(a, b), fr_r2()); }
 
-// a^e for canonical a (square and multiply over the bits of e, Montgomery).
-SVDW_HD Fr fr_pow_u64(const Fr& a, uint64_t e) {
+// a^e for canonical a (square and multiply over the low `nbits` bits of e).
+SVDW_HD Fr fr_pow_u64(const Fr& a, uint64_t e, int nbits = 64) {
     Fr am = fr_to_mont(a);
     Fr r = fr_to_mont(fr_from_u64(1));
-    for (int i = 63; i >= 0; --i) {
+    for (int i = nbits - 1; i >= 0; --i) {
         r = mont_mul(r, r);
         if ((e >> i) & 1) r = mont_mul(r, am);
     }

@@ -511,16 +511,18 @@ hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* wc, Fr* wm, hipStream
     hipLaunchKernelGGL(k_vec_prep, dim3((L + 255) / 256), dim3(256), 0, st, w, L, wc, wm);
     return hipGetLastError();
 }
-__global__ void k_gamma_vec(const Fr g, uint32_t L, Fr* wc, Fr* wm) {
+__global__ void k_gamma_vec(const Fr g, uint32_t L, int nbits, Fr* wc, Fr* wm) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= L) return;
-    Fr v = fr_pow_u64(g, j);
+    Fr v = fr_pow_u64(g, j, nbits);
     st_fr(wc + j, v);
     st_fr(wm + j, fr_to_mont(v));
 }
 hipError_t launch_gamma_vec(const Fr& g, uint32_t L, Fr* wc, Fr* wm, hipStream_t st) {
     if (!L) return hipSuccess;
-    hipLaunchKernelGGL(k_gamma_vec, dim3((L + 255) / 256), dim3(256), 0, st, g, L, wc, wm);
+    int nbits = 1;
+    while (nbits < 32 && (L - 1) >> nbits) ++nbits;
+    hipLaunchKernelGGL(k_gamma_vec, dim3((L + 255) / 256), dim3(256), 0, st, g, L, nbits, wc, wm);
     return hipGetLastError();
 }
 
