@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -274,7 +275,8 @@ struct svdw_ctx {
     };
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
-    // second stream: GEMMs (integer-VALU bound) overlap the HBM-bound stages
+    int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
+    // second stream: GEMMs overlap the HBM-bound stages
     hipStream_t st2 = nullptr;
     bool overlap = true;
     struct PreGemm {
@@ -433,7 +435,7 @@ static svdw_vec put_cell(svdw_ctx* c, uint32_t phase, const Fr& v) {   // load_w
 
 // ----------------------------------------------------- reference functions
 static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, uint32_t rows,
-                             uint32_t cols, bool on_device) {
+                             uint32_t cols, bool on_device, unsigned* maxbits = nullptr) {
     REQUIRE(rows >= 1 && cols >= 1, "ZkMatrix::new: empty matrix");
     REQUIRE(data || c->dry, "null data");
     uint64_t n = (uint64_t)rows * cols, off;
@@ -447,7 +449,7 @@ static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, ui
             src = (const double*)c->f64in.p;
         }
         ProfScope ps(c, c->st, "k_quantize", 40.0 * n, 0);
-        hipck(launch_quantize(src, n, cellp(c, phase, off), (int)c->P, c->st), "k_quantize");
+        hipck(launch_quantize(src, n, cellp(c, phase, off), (int)c->P, maxbits, c->st), "k_quantize");
     }
     return svdw_mat{phase, rows, cols, off, (int64_t)cols, 1};
 }
@@ -563,7 +565,33 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
     const uint32_t N = a.rows, K = a.cols, M = b.cols;
     const bool sym = is_transpose_of(b, a);
     int DA = round_digits(digits_for_bits(bits_a)), DB = round_digits(digits_for_bits(bits_b));
-    if (DA && DB && K <= 8192 && gemm_digits_supported(DA, DB)) {
+    const bool digits_ok = DA && DB && K <= 8192 && gemm_digits_supported(DA, DB);
+    if (digits_ok && c->gemm_impl == SVDW_GEMM_MFMA) {
+        const uint32_t kcn = (K + 63) / 64;
+        const uint32_t npad = (N + 31) / 32 * 32, mpad = (M + 31) / 32 * 32;
+        ensure_buf(c, c->digA, (size_t)npad * kcn * DA * 64);
+        {
+            ProfScope ps(c, s, "k_to_digits_mf", 32.0 * N * K + 64.0 * npad * kcn * DA, 0);
+            hipck(launch_to_digits_mf(view_of(c, a), N, K, DA, npad, kcn, (uint32_t*)c->digA.p, s),
+                  "k_to_digits_mf");
+        }
+        const uint8_t* Bd = (const uint8_t*)c->digA.p;
+        if (!sym) {
+            ensure_buf(c, c->digB, (size_t)mpad * kcn * DB * 64);
+            svdw_mat bt = b;   // Bt(j, k) = b(k, j)
+            bt.rows = b.cols; bt.cols = b.rows; bt.rs = b.cs; bt.cs = b.rs;
+            ProfScope ps(c, s, "k_to_digits_mf", 32.0 * M * K + 64.0 * mpad * kcn * DB, 0);
+            hipck(launch_to_digits_mf(view_of(c, bt), M, K, DB, mpad, kcn, (uint32_t*)c->digB.p, s),
+                  "k_to_digits_mf");
+            Bd = (const uint8_t*)c->digB.p;
+        }
+        ProfScope ps(c, s, std::string("k_gemm_mfma:") + std::to_string(DA) + "x" +
+                               std::to_string(DB) + (sym ? "s" : ""),
+                     64.0 * kcn * ((double)npad * DA + (sym ? 0.0 : (double)mpad * DB)) + 32.0 * N * M,
+                     (double)N * M * K);
+        hipck(launch_gemm_mfma(DA, DB, sym, (const uint8_t*)c->digA.p, Bd, N, M, kcn, out, M, 1, s),
+              "k_gemm_mfma");
+    } else if (digits_ok) {
         const uint32_t kg = ((K + 3) / 4 + 7) / 8 * 8;
         const uint32_t npad = (N + 31) / 32 * 32, mpad = (M + 31) / 32 * 32;
         ensure_buf(c, c->digA, (size_t)npad * kg * DA * 4);
@@ -799,14 +827,26 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
             grow(c, c->ph[p].lk, 0, c->ph[p].lcap, plan.ph[p].nl);
         }
     }
-    svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device);
-    svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device);
-    svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device);
+    unsigned* dbits = nullptr;
+    if (!c->dry) {
+        ensure_buf(c, c->bits, 64 * sizeof(unsigned));
+        dbits = (unsigned*)c->bits.p;
+        hipck(hipMemsetAsync(dbits, 0, 3 * sizeof(unsigned), c->st), "memset");
+    }
+    svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device, dbits);
+    svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device, dbits ? dbits + 1 : nullptr);
+    svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device, dbits ? dbits + 2 : nullptr);
     svdw_mat zdm = zkmatrix_new(c, 0, d, r, 1, on_device);
     svdw_vec zd{0, r, zdm.off, 1};
     double es, eu;
     err_calc(c->P, std::max(N, M), cfg.max_norm, cfg.eps_svd, cfg.eps_u, &es, &eu);
-    auto bits = maxbits_many(c, {zm, zu, zv});
+    std::vector<uint32_t> bits(3, 0);
+    if (!c->dry) {   // the one host synchronisation of a witness: digit counts of the GEMMs
+        unsigned hb[3];
+        hipck(hipMemcpyAsync(hb, dbits, sizeof hb, hipMemcpyDeviceToHost, c->st), "D2H");
+        hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
+        for (int i = 0; i < 3; ++i) bits[i] = hb[i];
+    }
     svdw_svd_payload pl = check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, bits.data());
     check_svd_phase1(c, zm, zu, zv, pl, gamma);
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
@@ -829,6 +869,8 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
         c->LB = p->lookup_bits;
         c->device = p->device;
         c->dry = p->device < 0;
+        if (const char* g = getenv("SVDW_GEMM"))
+            c->gemm_impl = (!strcmp(g, "valu") || !strcmp(g, "dot4")) ? SVDW_GEMM_VALU : SVDW_GEMM_MFMA;
         if (!c->dry) {
             hipError_t e = hipSetDevice(p->device);
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
@@ -864,6 +906,7 @@ int svdw_ctx_reset(svdw_ctx* c) {
         REQUIRE(c, "null ctx");
         sync(c);
         for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
+        c->pre.clear();
     });
 }
 int svdw_reserve(svdw_ctx* c, uint32_t phase, uint64_t na, uint64_t nl) {
@@ -1043,6 +1086,14 @@ int svdw_svd_witness(svdw_ctx* c, const double* m, const double* u, const double
         REQUIRE(c->dry || (m && u && v && d), "null input matrix");
         svdw_counts k = svd_witness(c, m, u, v, d, N, M, on_device != 0, *cfg, fr_from_words(gamma));
         if (counts) *counts = k;
+    });
+}
+int svdw_set_gemm_impl(svdw_ctx* c, int impl) {
+    return guarded([&] {
+        REQUIRE(c, "null ctx");
+        REQUIRE(impl == SVDW_GEMM_MFMA || impl == SVDW_GEMM_VALU, "unknown GEMM implementation");
+        sync(c);
+        c->gemm_impl = impl;
     });
 }
 int svdw_profile_enable(svdw_ctx* c, int on) {

@@ -62,8 +62,21 @@ __device__ __forceinline__ uint32_t signed_bits(const Fr& x) {
 // sign(x) < 0 (incl. -0.0) -> p - x_q.   [zk_fixed_point_chip quantization,
 // SURVEY.md Appendix C.1]
 __global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in, uint64_t n,
-                                                  Fr* __restrict__ out, double scale) {
+                                                  Fr* __restrict__ out, double scale,
+                                                  unsigned* __restrict__ maxbits) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // bit length of |x_q| for the GEMM digit-count choice (wave max, one atomic)
+    uint32_t bits = 0;
+    if (i < n) {
+        double s = round(fabs(in[i]) * scale);
+        if (s >= 340282366920938463463374607431768211456.0) bits = 128;
+        else if (s >= 1.0) bits = (uint32_t)ilogb(s) + 1;
+    }
+    if (maxbits) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, off));
+        if ((threadIdx.x & 63) == 0 && bits) atomicMax(maxbits, bits);
+    }
     if (i >= n) return;
     double x = in[i];
     bool neg = signbit(x) && !isnan(x);
@@ -82,11 +95,12 @@ __global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in,
     st_fr(out + i, neg ? fr_sub(fr_zero(), q) : q);
 }
 
-hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int p, hipStream_t st) {
+hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int p, unsigned* maxbits,
+                           hipStream_t st) {
     if (!n) return hipSuccess;
     double scale = (double)(1ull << p);
     hipLaunchKernelGGL(k_quantize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, n, out,
-                       scale);
+                       scale, maxbits);
     return hipGetLastError();
 }
 
@@ -465,6 +479,173 @@ hipError_t launch_gemm_digits(int DA, int DB, bool sym, const uint32_t* Ad, cons
                               int64_t ocs, hipStream_t st) {
 #define SVDW_G(a, b) \
     if (DA == a && DB == b) return gemm_dispatch<a, b>(sym, Ad, Bd, N, M, kg, out, ors, ocs, st);
+    SVDW_G(5, 5) SVDW_G(5, 8) SVDW_G(5, 9) SVDW_G(8, 5) SVDW_G(8, 8) SVDW_G(8, 9)
+    SVDW_G(9, 5) SVDW_G(9, 8) SVDW_G(9, 9)
+#undef SVDW_G
+    return hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------- MFMA GEMM
+// Same exact decomposition on the matrix cores: v_mfma_i32_16x16x64_i8 over
+// balanced base-256 digit planes. Global digit layout: [row][kc][D][64 B]
+// (kc = 64-k chunk; byte b = digit of X(row, 64 kc + b)), rows padded to 32.
+// Fragment (one digit, 16 rows x 64 k): lane l holds row (l & 15), bytes
+// [16 (l >> 4), +16) of the chunk; A and B use the same k mapping, so the
+// product is independent of the hardware's k order inside the chunk.
+// C/D (16x16 i32): col = lane & 15, row = 4 (lane >> 4) + reg.
+typedef int v4i __attribute__((ext_vector_type(4)));
+constexpr int MT = 32;        // block tile (2 x 2 waves of 16 x 16)
+constexpr int LROW = 80;      // LDS bytes per (digit, row): 64 + 16 pad
+
+__global__ __launch_bounds__(256) void k_to_digits_mf(const DView x, uint32_t rows, uint32_t kdim,
+                                                      int D, uint32_t rows_pad, uint32_t kcn,
+                                                      uint32_t* __restrict__ out) {
+    uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (uint64_t)rows_pad * kcn * 16) return;
+    const uint32_t g = (uint32_t)(idx & 15);
+    const uint64_t rk = idx >> 4;
+    const uint32_t row = (uint32_t)(rk / kcn), kc = (uint32_t)(rk % kcn);
+    uint32_t words[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    Fr zero = fr_zero();
+    Fr half = fr_p();
+    {
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 7; i >= 0; --i) {
+            uint32_t nw = (half.w[i] >> 1) | c;
+            c = half.w[i] << 31;
+            half.w[i] = nw;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        uint32_t k = kc * 64 + g * 4 + t;
+        if (row >= rows || k >= kdim) continue;
+        Fr v = view_load(x, zero, row, k);
+        Fr tmp;
+        bool neg = sub256(tmp, half, v) != 0;
+        Fr mag = neg ? fr_sub(fr_zero(), v) : v;
+        __int128 s = (__int128)(((unsigned __int128)mag.w[3] << 96) | ((unsigned __int128)mag.w[2] << 64) |
+                                ((unsigned __int128)mag.w[1] << 32) | mag.w[0]);
+        if (neg) s = -s;
+#pragma unroll
+        for (int l = 0; l < 9; ++l) {
+            if (l < D) {
+                int dg = (int)(uint32_t)(s & 0xff);
+                if (dg >= 128) dg -= 256;
+                s = (s - dg) >> 8;
+                words[l] |= ((uint32_t)dg & 0xffu) << (8 * t);
+            }
+        }
+    }
+    uint32_t* o = out + rk * (uint64_t)D * 16 + g;
+#pragma unroll
+    for (int l = 0; l < 9; ++l)
+        if (l < D) o[l * 16] = words[l];
+}
+
+hipError_t launch_to_digits_mf(const DView& x, uint32_t rows, uint32_t kdim, int D, uint32_t rows_pad,
+                               uint32_t kcn, uint32_t* out, hipStream_t st) {
+    uint64_t n = (uint64_t)rows_pad * kcn * 16;
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_to_digits_mf, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, rows,
+                       kdim, D, rows_pad, kcn, out);
+    return hipGetLastError();
+}
+
+template <int DA, int DB>
+__device__ __forceinline__ Fr combine_diag_reg(const v4i (&acc)[DA + DB - 1], int reg) {
+    int a[DA + DB - 1];
+#pragma unroll
+    for (int d = 0; d < DA + DB - 1; ++d) a[d] = acc[d][reg];
+    return combine_diagonals<DA, DB>(a);
+}
+
+template <int DA, int DB, bool SYM>
+__global__ __launch_bounds__(256) void k_gemm_mfma(const uint8_t* __restrict__ Ad,
+                                                   const uint8_t* __restrict__ Bd, uint32_t N,
+                                                   uint32_t M, uint32_t kcn, Fr* __restrict__ out,
+                                                   int64_t ors, int64_t ocs, uint32_t tiles_m) {
+    __shared__ __attribute__((aligned(16))) uint8_t As[DA * MT * LROW];
+    __shared__ __attribute__((aligned(16))) uint8_t Bs[DB * MT * LROW];
+    uint32_t bi, bj;
+    if (SYM) {
+        uint32_t b = blockIdx.x, r = 0, rowlen = tiles_m;
+        while (b >= rowlen) { b -= rowlen; ++r; --rowlen; }
+        bi = r; bj = r + b;
+    } else {
+        bi = blockIdx.x / tiles_m;
+        bj = blockIdx.x % tiles_m;
+    }
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t wr = wave >> 1, wc = wave & 1;
+    const uint32_t i0 = bi * MT, j0 = bj * MT;
+    v4i acc[DA + DB - 1];
+#pragma unroll
+    for (int d = 0; d < DA + DB - 1; ++d) acc[d] = v4i{0, 0, 0, 0};
+
+    const uint32_t frow = lane & 15, fk = (lane >> 4) * 16;
+    for (uint32_t kc = 0; kc < kcn; ++kc) {
+        // stage the A / B slabs: rows x D x 64 B, 16 B per thread-iteration
+        for (uint32_t q = tid; q < (uint32_t)(MT * DA * 4); q += 256) {
+            const uint32_t row = q / (DA * 4), rem = q % (DA * 4), l = rem >> 2, part = rem & 3;
+            const uint4 v = *reinterpret_cast<const uint4*>(
+                Ad + (((uint64_t)(i0 + row) * kcn + kc) * DA + l) * 64 + part * 16);
+            *reinterpret_cast<uint4*>(As + (l * MT + row) * LROW + part * 16) = v;
+        }
+        for (uint32_t q = tid; q < (uint32_t)(MT * DB * 4); q += 256) {
+            const uint32_t row = q / (DB * 4), rem = q % (DB * 4), l = rem >> 2, part = rem & 3;
+            const uint4 v = *reinterpret_cast<const uint4*>(
+                Bd + (((uint64_t)(j0 + row) * kcn + kc) * DB + l) * 64 + part * 16);
+            *reinterpret_cast<uint4*>(Bs + (l * MT + row) * LROW + part * 16) = v;
+        }
+        __syncthreads();
+        v4i bf[DB];
+#pragma unroll
+        for (int lb = 0; lb < DB; ++lb)
+            bf[lb] = *reinterpret_cast<const v4i*>(Bs + (lb * MT + wc * 16 + frow) * LROW + fk);
+#pragma unroll
+        for (int la = 0; la < DA; ++la) {
+            const v4i af = *reinterpret_cast<const v4i*>(As + (la * MT + wr * 16 + frow) * LROW + fk);
+#pragma unroll
+            for (int lb = 0; lb < DB; ++lb)
+                acc[la + lb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af, bf[lb], acc[la + lb], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    const uint32_t col = j0 + wc * 16 + (lane & 15);
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+        const uint32_t row = i0 + wr * 16 + (lane >> 4) * 4 + reg;
+        if (row < N && col < M) {
+            Fr v = combine_diag_reg<DA, DB>(acc, reg);
+            st_fr(out + (int64_t)row * ors + (int64_t)col * ocs, v);
+            if (SYM && bi != bj) st_fr(out + (int64_t)col * ors + (int64_t)row * ocs, v);
+        }
+    }
+}
+
+template <int DA, int DB>
+static hipError_t gemm_mfma_dispatch(bool sym, const uint8_t* Ad, const uint8_t* Bd, uint32_t N,
+                                     uint32_t M, uint32_t kcn, Fr* out, int64_t ors, int64_t ocs,
+                                     hipStream_t st) {
+    uint32_t tn = (N + MT - 1) / MT, tm = (M + MT - 1) / MT;
+    if (sym) {
+        if (DA != DB || N != M) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_gemm_mfma<DA, DB, true>), dim3(tm * (tm + 1) / 2), dim3(256), 0, st,
+                           Ad, Bd, N, M, kcn, out, ors, ocs, tm);
+    } else {
+        hipLaunchKernelGGL((k_gemm_mfma<DA, DB, false>), dim3(tn * tm), dim3(256), 0, st, Ad, Bd, N,
+                           M, kcn, out, ors, ocs, tm);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_gemm_mfma(int DA, int DB, bool sym, const uint8_t* Ad, const uint8_t* Bd,
+                            uint32_t N, uint32_t M, uint32_t kcn, Fr* out, int64_t ors,
+                            int64_t ocs, hipStream_t st) {
+#define SVDW_G(a, b) \
+    if (DA == a && DB == b) return gemm_mfma_dispatch<a, b>(sym, Ad, Bd, N, M, kcn, out, ors, ocs, st);
     SVDW_G(5, 5) SVDW_G(5, 8) SVDW_G(5, 9) SVDW_G(8, 5) SVDW_G(8, 8) SVDW_G(8, 9)
     SVDW_G(9, 5) SVDW_G(9, 8) SVDW_G(9, 9)
 #undef SVDW_G

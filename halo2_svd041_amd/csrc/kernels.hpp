@@ -12,8 +12,9 @@ namespace svdw {
 static constexpr int kStageElems = 64;
 
 // ZkMatrix::new / ZkVector::new quantization (f64 -> Fr) of n contiguous values.
+// maxbits (nullable): atomicMax of bit-length(|x_q|) over the values.
 hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int precision_bits,
-                           hipStream_t st);
+                           unsigned* maxbits, hipStream_t st);
 // Generic cell-program stage over elements [a.e_begin, a.e_end).
 hipError_t launch_stage(const StageArgs& a, hipStream_t st);
 // max over the view of bit-length(|signed(x)|) -> atomicMax(*out).
@@ -29,6 +30,12 @@ hipError_t launch_gemm_digits(int DA, int DB, bool sym, const uint32_t* Ad, cons
                               uint32_t N, uint32_t M, uint32_t kg_pad, Fr* out, int64_t ors,
                               int64_t ocs, hipStream_t st);
 bool gemm_digits_supported(int DA, int DB);
+// Matrix-core variant: digit planes laid out [row][kc][D][64 B] (kc = 64-k chunks).
+hipError_t launch_to_digits_mf(const DView& x, uint32_t rows, uint32_t kdim, int D, uint32_t rows_pad,
+                               uint32_t kcn, uint32_t* out, hipStream_t st);
+hipError_t launch_gemm_mfma(int DA, int DB, bool sym, const uint8_t* Ad, const uint8_t* Bd,
+                            uint32_t N, uint32_t M, uint32_t kcn, Fr* out, int64_t ors,
+                            int64_t ocs, hipStream_t st);
 // Generic Montgomery GEMM (any field elements): out = A(NxK) * B(KxM).
 hipError_t launch_gemm_mont(const DView& A, const DView& B, uint32_t N, uint32_t K, uint32_t M,
                             Fr* out, int64_t ors, int64_t ocs, hipStream_t st);

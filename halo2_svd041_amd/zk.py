@@ -119,6 +119,10 @@ class Context:
         check(lib().svdw_copy_lookup(self._h, phase, off, n, out.ctypes.data))
         return out
 
+    def set_gemm_impl(self, impl: str) -> None:
+        """'mfma' (matrix cores, default) or 'valu' (v_dot4): bit-identical GEMM paths."""
+        check(lib().svdw_set_gemm_impl(self._h, {"mfma": 0, "valu": 1}[impl]))
+
     def profile(self, on: bool = True) -> None:
         """Record HIP events around every kernel launch on this context's stream."""
         check(lib().svdw_profile_enable(self._h, 1 if on else 0))

@@ -157,6 +157,15 @@ int svdw_check_svd_phase1(svdw_ctx* ctx, const svdw_mat* m, const svdw_mat* u, c
 int svdw_svd_witness(svdw_ctx* ctx, const double* m, const double* u, const double* v,
                      const double* d, uint32_t N, uint32_t M, int on_device,
                      const svdw_svd_config* cfg, const uint64_t gamma[4], svdw_counts* counts);
+/* Exact integer GEMM of honest_prover_mat_mul: balanced base-256 digit planes
+ * with i32 diagonal sums on the matrix cores (v_mfma_i32_16x16x64_i8, default)
+ * or on the vector ALUs (v_dot4c_i32_i8). Both are bit-identical; operands
+ * wider than 9 digits (|x| >= ~2^71) use a Montgomery GEMM either way.
+ * The environment variable SVDW_GEMM=valu selects the VALU path at create. */
+#define SVDW_GEMM_MFMA 0
+#define SVDW_GEMM_VALU 1
+int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
+
 /* ----------------------------------------------------------- profiling */
 /* Per-kernel statistics from HIP events recorded around every launch on the
  * context stream. bytes / ops: algorithmic HBM bytes / MACs of the launches

@@ -120,3 +120,39 @@ def test_modular_api_matches_whole_witness(gpu_ctx_factory):
     hs.check_svd_phase1(ctx, zm, zu, zv, pl, g)
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
     _assert_streams(ctx, a0, l0, a1)
+
+
+@pytest.mark.parametrize("impl", ["mfma", "valu"])
+@pytest.mark.parametrize("N,M,P", [(33, 47, 63), (64, 64, 32), (70, 65, 42), (96, 96, 63)])
+def test_gemm_impls_parity(gpu_ctx_factory, impl, N, M, P):
+    """Both exact GEMM paths (matrix cores / v_dot4) give the oracle's c_s cells."""
+    import halo2_svd041_amd as hs
+    m, u, d, v = gen_svd_input(N, M, seed=N + 3 * M)
+    g = gamma_for(N * 7)
+    ctx = gpu_ctx_factory(P)
+    ctx.set_gemm_impl(impl)
+    hs.svd_witness(ctx, m, u, v, d, g)
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+    _assert_streams(ctx, a0, l0, a1)
+
+
+def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
+    """Modular GEMM with K not a multiple of 64 / 32 and non-square shapes."""
+    import halo2_svd041_amd as hs
+    import pyoracle as po
+    rs = np.random.RandomState(8)
+    A = rs.uniform(-3, 3, (37, 131))
+    B = rs.uniform(-3, 3, (131, 29))
+    for impl in ("mfma", "valu"):
+        ctx = gpu_ctx_factory(40)
+        ctx.set_gemm_impl(impl)
+        za, zb = hs.ZkMatrix.new(ctx, A), hs.ZkMatrix.new(ctx, B)
+        c = hs.honest_prover_mat_mul(ctx, za, zb)
+        got = c.values()
+        qa = [[po.quantize(x, 40) for x in r] for r in A.tolist()]
+        qb = [[po.quantize(x, 40) for x in r] for r in B.tolist()]
+        for i in (0, 17, 36):
+            for j in (0, 11, 28):
+                want = sum(qa[i][k] * qb[k][j] for k in range(131)) % po.P_MOD
+                assert int(got[i, j, 0]) | (int(got[i, j, 1]) << 64) | (int(got[i, j, 2]) << 128) \
+                    | (int(got[i, j, 3]) << 192) == want
