@@ -265,7 +265,10 @@ struct svdw_ctx {
     hipStream_t st = nullptr;
     uint32_t P = 32, LB = 19;
     Stream ph[2];
-    DBuf f64in, digA, digB, w1c, w1m, w2c, w2m, bits;
+    DBuf f64in, digA, digB, w1c, w1m, w2c, w2m, bits, gpc, gpm;
+    // gamma^j cache (canonical gpc / Montgomery gpm), shared by verify_mul calls
+    Fr gp_gamma{};
+    uint32_t gp_len = 0;
     // built-in event profiler (svdw_profile_*): one start/stop event pair per launch
     bool prof = false;
     struct Rec {
@@ -276,6 +279,7 @@ struct svdw_ctx {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
+    uint32_t stage_flags = 0;               // SVDW_NT_STORES=1 -> STAGE_NT_STORES
     // second stream: GEMMs overlap the HBM-bound stages
     hipStream_t st2 = nullptr;
     bool overlap = true;
@@ -415,6 +419,7 @@ static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, u
     a.e_begin = 0;
     a.e_end = nelem;
     a.cols = cols ? cols : 1;
+    a.flags = c->stage_flags;
     a.cdiv_magic = a.C ? ((1ull << 32) + a.C - 1) / a.C : 0;
     a.ldiv_magic = a.L ? ((1ull << 32) + a.L - 1) / a.L : 0;
     uint32_t loads = 0;
@@ -684,29 +689,35 @@ static void verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svd
     REQUIRE(cs.rows == a.rows, "verify_mul: c_s.len() != a.num_rows");
     REQUIRE(cs.cols == b.cols, "verify_mul: c_s[0].len() != b.num_col");
     const uint32_t d = cs.cols, n = a.rows, k = a.cols;
-    // v = (1, g, g^2, ...): canonical + Montgomery copies for the row scans
-    ensure_buf(c, c->w1c, (size_t)d * sizeof(Fr));
-    ensure_buf(c, c->w1m, (size_t)d * sizeof(Fr));
-    if (!c->dry) {
-        ProfScope ps(c, c->st, "k_gamma_vec", 64.0 * d, 0);
-        hipck(launch_gamma_vec(gamma, d, (Fr*)c->w1c.p, (Fr*)c->w1m.p, c->st), "k_gamma_vec");
+    // v = (1, g, g^2, ...): canonical + Montgomery copies for the row scans,
+    // computed once per (gamma, length) and reused by later verify_mul calls
+    if (!c->dry && (c->gp_len < d || !fr_eq(c->gp_gamma, gamma))) {
+        const uint32_t len = std::max(d, c->gp_len);
+        ensure_buf(c, c->gpc, (size_t)len * sizeof(Fr));
+        ensure_buf(c, c->gpm, (size_t)len * sizeof(Fr));
+        ProfScope ps(c, c->st, "k_gamma_vec", 64.0 * len, 0);
+        hipck(launch_gamma_vec(gamma, len, (Fr*)c->gpc.p, (Fr*)c->gpm.p, c->st), "k_gamma_vec");
+        c->gp_len = len;
+        c->gp_gamma = gamma;
     }
+    const Fr* gpc = (const Fr*)c->gpc.p;
+    const Fr* gpm = (const Fr*)c->gpm.p;
     put_cell(c, phase, fr_from_u64(1));                    // load_witness(F::ONE)
     if (d > 1) {                                          // v_i = mul(v_{i-1}, init_rand)
         PB pb(c->LB);
         DView w;
         memset(&w, 0, sizeof w);
-        w.ptr = (const Fr*)c->w1c.p;
+        w.ptr = gpc;
         w.rs = 1; w.cs = 0; w.rows = d; w.cols = 1;
         pb.a.view[0] = w;
         pb.a.view[1] = w;
-        if (!c->dry) pb.a.view[1].ptr = (const Fr*)c->w1c.p + 1;
+        if (!c->dry) pb.a.view[1].ptr = gpc + 1;
         uint8_t prev = pb.load(0), cur = pb.load(1);
         pb.cell(pb.K(0)); pb.cell(prev); pb.cell(pb.K(gamma)); pb.cell(cur);
         run_stage(c, phase, pb, d - 1, 1, "verify_mul_gamma_pows");
     }
-    svdw_vec csv = matvec_rows(c, phase, cs, (const Fr*)c->w1c.p, (const Fr*)c->w1m.p);
-    svdw_vec bv = matvec_rows(c, phase, b, (const Fr*)c->w1c.p, (const Fr*)c->w1m.p);
+    svdw_vec csv = matvec_rows(c, phase, cs, gpc, gpm);
+    svdw_vec bv = matvec_rows(c, phase, b, gpc, gpm);
     vec_prep(c, bv, c->w2c, c->w2m);
     svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, (const Fr*)c->w2m.p);
     (void)k;
@@ -869,6 +880,8 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
         c->LB = p->lookup_bits;
         c->device = p->device;
         c->dry = p->device < 0;
+        if (const char* nt = getenv("SVDW_NT_STORES"))
+            c->stage_flags = (nt[0] == '1') ? STAGE_NT_STORES : 0;
         if (const char* g = getenv("SVDW_GEMM"))
             c->gemm_impl = (!strcmp(g, "valu") || !strcmp(g, "dot4")) ? SVDW_GEMM_VALU : SVDW_GEMM_MFMA;
         if (!c->dry) {
@@ -889,7 +902,8 @@ int svdw_ctx_destroy(svdw_ctx* c) {
         if (!c->dry) {
             (void)hipStreamSynchronize(c->st);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
-            for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->w1c, &c->w1m, &c->w2c, &c->w2m, &c->bits})
+            for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->w1c, &c->w1m, &c->w2c, &c->w2m,
+                            &c->bits, &c->gpc, &c->gpm})
                 if (b->p) (void)hipFree(b->p);
             for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
             for (auto e : c->pool) (void)hipEventDestroy(e);

@@ -73,9 +73,19 @@ __global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in,
         else if (s >= 1.0) bits = (uint32_t)ilogb(s) + 1;
     }
     if (maxbits) {
+        // wave max -> block max (LDS) -> one atomic per block, skipped when the
+        // running maximum already covers it (one contended word otherwise
+        // serialises every block: ~10 ns per atomic)
+        __shared__ uint32_t wmax[4];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, off));
-        if ((threadIdx.x & 63) == 0 && bits) atomicMax(maxbits, bits);
+        if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = bits;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t b = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+            if (b && b > __hip_atomic_load(maxbits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                atomicMax(maxbits, b);
+        }
     }
     if (i >= n) return;
     double x = in[i];
@@ -105,60 +115,93 @@ hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int p, unsigne
 }
 
 // ----------------------------------------------------------- stage kernel
-// Phase A: one thread per element runs the stage's micro-ops, leaving the
-// element's values V[0..nv) in LDS (each padded to 16 words so bit windows
-// may run past the top). Phase B: the block's E*C advice cells (then E*L
-// lookup cells) are produced half a cell (16 B) per lane in stream order, so
-// every wave store is 1 KiB contiguous.
-constexpr int VW = 16;   // LDS words per value (8 + 8 zero pad)
+// Phase A: one thread per element (kStageElems = 256 = block size) runs the
+// stage's micro-ops, leaving the element's values V[0..nv) (8 words each) in
+// LDS. Phase B: the block's E*C advice cells (then E*L lookup cells) are
+// produced half a cell (16 B) per lane in stream order, so every wave store
+// is 1 KiB contiguous: cell = (V[src] >> lo) & (2^nbits - 1).
+constexpr int VW = 8;    // LDS words per value
 
 __device__ __forceinline__ void lds_put(uint32_t* s, const Fr& v) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s[i] = v.w[i];
-#pragma unroll
-    for (int i = 8; i < 16; ++i) s[i] = 0;
+    uint4* q = reinterpret_cast<uint4*>(s);
+    q[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+    q[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
 }
 __device__ __forceinline__ Fr lds_get(const uint32_t* s) {
+    const uint4* q = reinterpret_cast<const uint4*>(s);
+    uint4 a = q[0], b = q[1];
     Fr r;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r.w[i] = s[i];
+    r.w[0] = a.x; r.w[1] = a.y; r.w[2] = a.z; r.w[3] = a.w;
+    r.w[4] = b.x; r.w[5] = b.y; r.w[6] = b.z; r.w[7] = b.w;
     return r;
 }
 
-// Four output words [4h, 4h+4) of (S >> lo) & mask(nbits), S at LDS word ptr s.
+// Output words [4h, 4h+4) of (S >> lo) & mask(nbits), S = 8 LDS words at s;
+// words past the top read as 0 (reads are clamped in-bounds, then masked).
 __device__ __forceinline__ uint4 extract_half(const uint32_t* s, uint32_t lo, uint32_t nbits,
                                               uint32_t h) {
-    uint32_t q = lo >> 5, r = lo & 31;
-    const uint32_t* p = s + q + 4 * h;
-    uint32_t x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3], x4 = p[4];
+    const uint32_t q = (lo >> 5) + 4 * h, r = lo & 31;
+    uint32_t x[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t w = q + i;
+        const uint32_t v = s[w < 8 ? w : 7];
+        x[i] = w < 8 ? v : 0u;
+    }
     uint32_t o[4];
-    o[0] = __builtin_amdgcn_alignbit(x1, x0, r);
-    o[1] = __builtin_amdgcn_alignbit(x2, x1, r);
-    o[2] = __builtin_amdgcn_alignbit(x3, x2, r);
-    o[3] = __builtin_amdgcn_alignbit(x4, x3, r);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = __builtin_amdgcn_alignbit(x[i + 1], x[i], r);
     if (nbits) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            int lowbit = 32 * (4 * (int)h + k);
-            int keep = (int)nbits - lowbit;
-            uint32_t m = keep >= 32 ? 0xffffffffu : (keep <= 0 ? 0u : ((1u << keep) - 1u));
-            o[k] &= m;
+        for (int i = 0; i < 4; ++i) {
+            const int keep = (int)nbits - 32 * (4 * (int)h + i);
+            const uint32_t m = keep >= 32 ? 0xffffffffu : (keep <= 0 ? 0u : ((1u << keep) - 1u));
+            o[i] &= m;
         }
     }
     return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// LDS carve (bytes, all 16-aligned): consts | element values | slot ops | micro-ops | views
+__host__ __device__ constexpr uint32_t stage_lds_bytes(uint32_t nv) {
+    return kMaxK * 32 + kStageElems * nv * 32 + (kMaxAdv + kMaxLk) * 4 + kMaxMicro * 8 +
+           kMaxViews * 48;
+}
+
+template <bool NT>
+__device__ __forceinline__ void stream_cells(uint4* __restrict__ out, uint32_t total,
+                                             const SlotOp* __restrict__ ops, uint32_t C,
+                                             uint64_t magic, const uint32_t* sK, const uint32_t* sV,
+                                             uint32_t nv) {
+    for (uint32_t hc = threadIdx.x; hc < total; hc += blockDim.x) {
+        const uint32_t c = hc >> 1, h = hc & 1;
+        const uint32_t el = (uint32_t)(((uint64_t)c * magic) >> 32);
+        const SlotOp op = ops[c - el * C];
+        const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + (el * nv + op.src) * VW;
+        const uint4 v = extract_half(src, op.lo, op.nbits, h);
+        if (NT) {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 w = {v.x, v.y, v.z, v.w};
+            __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(out + hc));
+        } else {
+            out[hc] = v;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
-    __shared__ uint32_t sK[kMaxK * VW];
-    __shared__ uint32_t sV[kStageElems * kMaxV * VW];
-    __shared__ SlotOp sAdv[kMaxAdv];
-    __shared__ SlotOp sLk[kMaxLk];
-    __shared__ MicroOp sMo[kMaxMicro];
-    __shared__ DView sVw[kMaxViews];
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const uint32_t nv = a.nv;
+    uint32_t* sK = smem;
+    uint32_t* sV = sK + kMaxK * VW;
+    SlotOp* sAdv = reinterpret_cast<SlotOp*>(sV + kStageElems * nv * VW);
+    SlotOp* sLk = sAdv + kMaxAdv;
+    MicroOp* sMo = reinterpret_cast<MicroOp*>(sLk + kMaxLk);
+    DView* sVw = reinterpret_cast<DView*>(sMo + kMaxMicro);
+
     const uint32_t tid = threadIdx.x;
     const uint32_t e0 = a.e_begin + blockIdx.x * kStageElems;
     const uint32_t ne = min((uint32_t)kStageElems, a.e_end - e0);
-    const uint32_t nv = a.nv;
 
     for (uint32_t k = tid; k < a.nk; k += blockDim.x) lds_put(sK + k * VW, a.K[k]);
     for (uint32_t k = tid; k < a.C; k += blockDim.x) sAdv[k] = a.adv[k];
@@ -167,7 +210,7 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     if (tid < kMaxViews) sVw[tid] = a.view[tid];
     __syncthreads();
 
-    // ---- phase A: per-element micro-ops (constants and ops read from LDS:
+    // ---- phase A: per-element micro-ops (constants / ops / views read from LDS:
     // dynamic indexing into the by-value kernel argument would go to scratch)
     if (tid < ne) {
         const uint32_t e = e0 + tid;
@@ -192,15 +235,22 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
                     lds_put(dst, fr_mul(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
                     break;
                 case MO_LIMBSHL: {
-                    const uint32_t* s = myV + op.a * VW;
-                    uint32_t lo = op.p0, q = lo >> 5, r = lo & 31;
-                    uint64_t w01 = (uint64_t)s[q] | ((uint64_t)s[q + 1] << 32);
-                    uint64_t w2 = s[q + 2];
-                    uint64_t x = r ? ((w01 >> r) | (w2 << (64 - r))) : w01;
+                    const Fr sv = lds_get(myV + op.a * VW);
+                    // 64-bit window at bit p0 (p0 < 256), masked to p1 bits, << b
+                    const uint32_t lo = op.p0, q = lo >> 5, r = lo & 31;
+                    uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        w0 = (t == (int)q) ? sv.w[t] : w0;
+                        w1 = (t == (int)q + 1) ? sv.w[t] : w1;
+                        w2 = (t == (int)q + 2) ? sv.w[t] : w2;
+                    }
+                    const uint64_t w01 = (uint64_t)w0 | ((uint64_t)w1 << 32);
+                    uint64_t x = r ? ((w01 >> r) | ((uint64_t)w2 << (64 - r))) : w01;
                     if (op.p1 < 64) x &= (1ull << op.p1) - 1;
-                    uint32_t sh = op.b;
-                    uint64_t lo64 = sh < 64 ? (x << sh) : 0;
-                    uint64_t hi64 = sh == 0 ? 0 : (sh < 64 ? (x >> (64 - sh)) : (x << (sh - 64)));
+                    const uint32_t sh = op.b;
+                    const uint64_t lo64 = sh < 64 ? (x << sh) : 0;
+                    const uint64_t hi64 = sh == 0 ? 0 : (sh < 64 ? (x >> (64 - sh)) : (x << (sh - 64)));
                     Fr v = fr_zero();
                     v.w[0] = (uint32_t)lo64; v.w[1] = (uint32_t)(lo64 >> 32);
                     v.w[2] = (uint32_t)hi64; v.w[3] = (uint32_t)(hi64 >> 32);
@@ -209,14 +259,14 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
                 }
                 case MO_FDBL: {
                     Fr v = lds_get(myV + op.a * VW);
-                    for (uint32_t k = 0; k < op.b; ++k) v = fr_add(v, v);
+                    for (uint32_t t = 0; t < op.b; ++t) v = fr_add(v, v);
                     lds_put(dst, v);
                     break;
                 }
                 case MO_ISZERO: {
-                    Fr v = lds_get(myV + op.a * VW);
-                    bool z = fr_is_zero(v);
-                    Fr inv = z ? fr_from_u64(1) : fr_inv(v);
+                    const Fr v = lds_get(myV + op.a * VW);
+                    const bool z = fr_is_zero(v);
+                    const Fr inv = z ? fr_from_u64(1) : fr_inv(v);
                     lds_put(dst, fr_from_u64(z ? 1 : 0));
                     lds_put(dst + VW, inv);
                     break;
@@ -232,38 +282,22 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     __syncthreads();
 
     // ---- phase B: advice cells, then lookup cells
-    {
-        const uint32_t total = 2 * ne * a.C;
-        uint4* out = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
-        for (uint32_t hc = tid; hc < total; hc += blockDim.x) {
-            uint32_t c = hc >> 1, h = hc & 1;
-            uint32_t el = (uint32_t)(((uint64_t)c * a.cdiv_magic) >> 32);
-            uint32_t s = c - el * a.C;
-            SlotOp op = sAdv[s];
-            const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW
-                                                 : sV + (el * nv + op.src) * VW;
-            out[hc] = extract_half(src, op.lo, op.nbits, h);
-        }
-    }
-    if (a.L) {
-        const uint32_t total = 2 * ne * a.L;
-        uint4* out = reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L);
-        for (uint32_t hc = tid; hc < total; hc += blockDim.x) {
-            uint32_t c = hc >> 1, h = hc & 1;
-            uint32_t el = (uint32_t)(((uint64_t)c * a.ldiv_magic) >> 32);
-            uint32_t s = c - el * a.L;
-            SlotOp op = sLk[s];
-            const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW
-                                                 : sV + (el * nv + op.src) * VW;
-            out[hc] = extract_half(src, op.lo, op.nbits, h);
-        }
+    uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
+    uint4* outL = a.L ? reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L) : nullptr;
+    if (a.flags & STAGE_NT_STORES) {
+        stream_cells<true>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
+        if (a.L) stream_cells<true>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
+    } else {
+        stream_cells<false>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
+        if (a.L) stream_cells<false>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
     }
 }
 
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     if (a.e_end <= a.e_begin) return hipSuccess;
-    uint32_t n = a.e_end - a.e_begin;
-    hipLaunchKernelGGL(k_stage, dim3((n + kStageElems - 1) / kStageElems), dim3(256), 0, st, a);
+    const uint32_t n = a.e_end - a.e_begin;
+    const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1);
+    hipLaunchKernelGGL(k_stage, dim3((n + kStageElems - 1) / kStageElems), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 
@@ -566,8 +600,12 @@ __global__ __launch_bounds__(256) void k_gemm_mfma(const uint8_t* __restrict__ A
                                                    const uint8_t* __restrict__ Bd, uint32_t N,
                                                    uint32_t M, uint32_t kcn, Fr* __restrict__ out,
                                                    int64_t ors, int64_t ocs, uint32_t tiles_m) {
-    __shared__ __attribute__((aligned(16))) uint8_t As[DA * MT * LROW];
-    __shared__ __attribute__((aligned(16))) uint8_t Bs[DB * MT * LROW];
+    // one LDS array: operand slabs during the K loop, the output tile after it
+    constexpr int kOps = (DA + DB) * MT * LROW, kTile = MT * MT * 32;
+    __shared__ __attribute__((aligned(16))) uint8_t S[kOps > kTile ? kOps : kTile];
+    uint8_t* As = S;
+    uint8_t* Bs = S + DA * MT * LROW;
+    uint8_t* Ts = S;
     uint32_t bi, bj;
     if (SYM) {
         uint32_t b = blockIdx.x, r = 0, rowlen = tiles_m;
@@ -613,14 +651,37 @@ __global__ __launch_bounds__(256) void k_gemm_mfma(const uint8_t* __restrict__ A
         }
         __syncthreads();
     }
-    const uint32_t col = j0 + wc * 16 + (lane & 15);
+    // Epilogue: reduce the 17 diagonals to canonical Fr, stage the 32 x 32 cell
+    // tile (32 KiB) in the (now free) operand LDS, then write whole 1 KiB tile
+    // rows — and, for a symmetric off-diagonal tile, the transposed rows too —
+    // as contiguous 16 B-per-lane stores.
+    {
+        const uint32_t tc = wc * 16 + (lane & 15);
 #pragma unroll
-    for (int reg = 0; reg < 4; ++reg) {
-        const uint32_t row = i0 + wr * 16 + (lane >> 4) * 4 + reg;
-        if (row < N && col < M) {
+        for (int reg = 0; reg < 4; ++reg) {
+            const uint32_t tr = wr * 16 + (lane >> 4) * 4 + reg;
             Fr v = combine_diag_reg<DA, DB>(acc, reg);
-            st_fr(out + (int64_t)row * ors + (int64_t)col * ocs, v);
-            if (SYM && bi != bj) st_fr(out + (int64_t)col * ors + (int64_t)row * ocs, v);
+            uint4* dst = reinterpret_cast<uint4*>(Ts + (tr * MT + tc) * 32);
+            dst[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+            dst[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+        }
+    }
+    __syncthreads();
+    // direct tile: 32 rows x 64 half-cells; thread -> (row, half-cell)
+    for (uint32_t q = tid; q < MT * 64; q += 256) {
+        const uint32_t tr = q >> 6, hc = q & 63, tc = hc >> 1, h = hc & 1;
+        const uint32_t row = i0 + tr, col = j0 + tc;
+        if (row < N && col < M)
+            reinterpret_cast<uint4*>(out + (int64_t)row * ors + (int64_t)col * ocs)[h] =
+                reinterpret_cast<const uint4*>(Ts + (tr * MT + tc) * 32)[h];
+    }
+    if (SYM && bi != bj) {
+        for (uint32_t q = tid; q < MT * 64; q += 256) {
+            const uint32_t tc = q >> 6, hc = q & 63, tr = hc >> 1, h = hc & 1;   // out row = j
+            const uint32_t row = j0 + tc, col = i0 + tr;
+            if (row < M && col < N)
+                reinterpret_cast<uint4*>(out + (int64_t)row * ors + (int64_t)col * ocs)[h] =
+                    reinterpret_cast<const uint4*>(Ts + (tr * MT + tc) * 32)[h];
         }
     }
 }

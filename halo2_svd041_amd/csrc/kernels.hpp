@@ -8,8 +8,8 @@
 
 namespace svdw {
 
-// Elements per block of the generic stage kernel (LDS: E * nv * 64 B).
-static constexpr int kStageElems = 64;
+// Elements per block of the generic stage kernel (= block size; LDS: E * nv * 32 B).
+static constexpr int kStageElems = 256;
 
 // ZkMatrix::new / ZkVector::new quantization (f64 -> Fr) of n contiguous values.
 // maxbits (nullable): atomicMax of bit-length(|x_q|) over the values.

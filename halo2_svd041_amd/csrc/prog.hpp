@@ -57,6 +57,8 @@ struct SlotOp {
 };
 static constexpr uint8_t KSRC = 0x80;
 
+static constexpr uint32_t STAGE_NT_STORES = 1;   // non-temporal cell stores
+
 static constexpr int kMaxViews = 2;
 static constexpr int kMaxMicro = 16;
 static constexpr int kMaxAdv = 112;
@@ -72,6 +74,7 @@ struct StageArgs {
     uint32_t cols;        // element e -> (i, j) = (e / cols, e % cols)
     uint32_t C, L;        // advice / lookup cells per element
     uint32_t nv, nmo, nk;
+    uint32_t flags;       // STAGE_* bits
     uint64_t cdiv_magic;  // ceil(2^32 / C): el = (c * magic) >> 32 exact for c*C < 2^25
     uint64_t ldiv_magic;  // ceil(2^32 / L)
     DView view[kMaxViews];
