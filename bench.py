@@ -102,7 +102,7 @@ def main():
     ap.add_argument("--p", type=int, default=63)
     ap.add_argument("--lb", type=int, default=19)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-rows", type=int, default=48)
+    ap.add_argument("--cpu-rows", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true",
                     help="skip the engine's event profiler in the timed region")

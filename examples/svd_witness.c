@@ -1,0 +1,74 @@
+/*
+ * svd_witness.c — C caller of the engine, the witness part of the reference's
+ * examples/svd_example.rs (do_zk_svd -> virtual_assign_phase0/1).
+ *
+ *   gcc examples/svd_witness.c -Iinclude -Lhalo2_svd041_amd -lsvdw -lm \
+ *       -Wl,-rpath,$PWD/halo2_svd041_amd -o svd_witness
+ *   ./svd_witness [N] [P]            (device 0; N x N input with known SVD)
+ *
+ * Input: m = u diag(d) v with u, v signed permutations scaled by cos/sin
+ * (Givens rotations), so u, v are exactly orthogonal up to f64 rounding.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "svdw.h"
+
+#define CHECK(x)                                                        \
+    do {                                                                \
+        int rc_ = (x);                                                  \
+        if (rc_ != SVDW_OK) {                                           \
+            fprintf(stderr, "%s failed (%d): %s\n", #x, rc_, svdw_last_error()); \
+            return 1;                                                   \
+        }                                                               \
+    } while (0)
+
+static void rotation(double* a, uint32_t n, double theta) {
+    /* block-diagonal 2x2 rotations */
+    for (uint32_t i = 0; i < n * n; ++i) a[i] = 0.0;
+    for (uint32_t i = 0; i + 1 < n; i += 2) {
+        double c = cos(theta * (i + 1)), s = sin(theta * (i + 1));
+        a[i * n + i] = c; a[i * n + i + 1] = -s;
+        a[(i + 1) * n + i] = s; a[(i + 1) * n + i + 1] = c;
+    }
+    if (n % 2) a[(n - 1) * n + n - 1] = 1.0;
+}
+
+int main(int argc, char** argv) {
+    uint32_t N = argc > 1 ? (uint32_t)atoi(argv[1]) : 64;
+    uint32_t P = argc > 2 ? (uint32_t)atoi(argv[2]) : 42;
+    double* u = malloc(sizeof(double) * N * N);
+    double* v = malloc(sizeof(double) * N * N);
+    double* m = malloc(sizeof(double) * N * N);
+    double* d = malloc(sizeof(double) * N);
+    rotation(u, N, 0.3);
+    rotation(v, N, 0.7);
+    for (uint32_t i = 0; i < N; ++i) d[i] = 50.0 / (1.0 + i);
+    for (uint32_t i = 0; i < N; ++i)
+        for (uint32_t j = 0; j < N; ++j) {
+            double s = 0;
+            for (uint32_t k = 0; k < N; ++k) s += u[i * N + k] * d[k] * v[k * N + j];
+            m[i * N + j] = s;
+        }
+    svdw_params p = {0, P, 19};
+    svdw_ctx* ctx = NULL;
+    CHECK(svdw_ctx_create(&p, &ctx));
+    svdw_svd_config cfg = {100.0, 1e-10, 1e-10, 30};
+    uint64_t gamma[4] = {0x1234567890abcdefull, 0x0fedcba987654321ull, 0x1111ull, 0x0ull};
+    svdw_counts cnt;
+    CHECK(svdw_svd_witness(ctx, m, u, v, d, N, N, 0, &cfg, gamma, &cnt));
+    CHECK(svdw_sync(ctx));
+    printf("N=%u P=%u advice0=%llu advice1=%llu lookup0=%llu\n", N, P,
+           (unsigned long long)cnt.advice0, (unsigned long long)cnt.advice1,
+           (unsigned long long)cnt.lookup0);
+    uint64_t cell[4];
+    CHECK(svdw_copy_advice(ctx, 0, 0, 1, cell));   /* quantized m[0][0] */
+    printf("advice0[0] = %016llx%016llx%016llx%016llx (m[0][0]=%.17g)\n",
+           (unsigned long long)cell[3], (unsigned long long)cell[2],
+           (unsigned long long)cell[1], (unsigned long long)cell[0], m[0]);
+    CHECK(svdw_ctx_destroy(ctx));
+    free(u); free(v); free(m); free(d);
+    return 0;
+}
