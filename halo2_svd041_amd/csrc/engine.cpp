@@ -280,6 +280,7 @@ struct svdw_ctx {
     std::vector<hipEvent_t> pool;
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
     uint32_t stage_flags = 0;               // SVDW_NT_STORES=1 -> STAGE_NT_STORES
+    uint32_t stage_grid = 256;              // persistent k_stage grid (CU count; SVDW_STAGE_GRID)
     // second stream: GEMMs overlap the HBM-bound stages
     hipStream_t st2 = nullptr;
     bool overlap = true;
@@ -420,8 +421,19 @@ static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, u
     a.e_end = nelem;
     a.cols = cols ? cols : 1;
     a.flags = c->stage_flags;
-    a.cdiv_magic = a.C ? ((1ull << 32) + a.C - 1) / a.C : 0;
-    a.ldiv_magic = a.L ? ((1ull << 32) + a.L - 1) / a.L : 0;
+    uint32_t nviews = 0;
+    for (uint32_t i = 0; i < a.nmo; ++i)
+        if (a.mo[i].op == MO_LOAD) nviews = std::max<uint32_t>(nviews, a.mo[i].a + 1u);
+    a.nviews = nviews;
+    // sweep geometry: ~4 KiB of advice cells per block per round
+    a.eb = std::max<uint32_t>(1, std::min<uint32_t>(256, (128 + a.C / 2) / std::max<uint32_t>(a.C, 1)));
+    a.rb = 256 / a.eb;
+    a.grid = c->stage_grid;
+    auto magic = [](uint64_t d) -> uint64_t { return d ? ((1ull << 32) + d - 1) / d : 0; };
+    a.cdiv_magic = magic(a.C);
+    a.ldiv_magic = magic(a.L);
+    a.ecdiv_magic = magic((uint64_t)a.eb * a.C);
+    a.eldiv_magic = magic((uint64_t)a.eb * a.L);
     uint32_t loads = 0;
     for (uint32_t i = 0; i < a.nmo; ++i) loads += a.mo[i].op == MO_LOAD;
     {
@@ -880,6 +892,13 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
         c->LB = p->lookup_bits;
         c->device = p->device;
         c->dry = p->device < 0;
+        if (!c->dry) {
+            int cus = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) ==
+                    hipSuccess && cus > 0)
+                c->stage_grid = (uint32_t)cus;
+        }
+        if (const char* g = getenv("SVDW_STAGE_GRID")) c->stage_grid = (uint32_t)std::max(1, atoi(g));
         if (const char* nt = getenv("SVDW_NT_STORES"))
             c->stage_flags = (nt[0] == '1') ? STAGE_NT_STORES : 0;
         if (const char* g = getenv("SVDW_GEMM"))

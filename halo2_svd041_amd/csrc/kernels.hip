@@ -168,23 +168,45 @@ __host__ __device__ constexpr uint32_t stage_lds_bytes(uint32_t nv) {
            kMaxViews * 48;
 }
 
+// Element e of the stage in the sweep order: round r covers elements
+// [r*G*Eb, (r+1)*G*Eb); block b owns [r*G*Eb + b*Eb, +Eb) of every round, and
+// its output for one round is Eb*C consecutive cells. A batch is Rb rounds
+// (Rb*Eb <= 256 elements, one per thread in phase A). All blocks advance round
+// by round, so the chip writes one ~G*Eb*C*32 B window at a time (a "sweep
+// front": 6.2-6.4 TB/s in tools/storepat*.hip vs ~5.5 for per-block chunks).
+__device__ __forceinline__ uint32_t sweep_elem(uint32_t batch, uint32_t q, uint32_t t, uint32_t Rb,
+                                               uint32_t G, uint32_t Eb, uint32_t b) {
+    return ((batch * Rb + q) * G + b) * Eb + t;
+}
+
 template <bool NT>
-__device__ __forceinline__ void stream_cells(uint4* __restrict__ out, uint32_t total,
-                                             const SlotOp* __restrict__ ops, uint32_t C,
-                                             uint64_t magic, const uint32_t* sK, const uint32_t* sV,
-                                             uint32_t nv) {
+__device__ __forceinline__ void sweep_cells(Fr* __restrict__ outbase, uint32_t C, uint32_t Eb,
+                                            uint32_t Rb, uint32_t G, uint32_t batch, uint32_t nel,
+                                            const SlotOp* __restrict__ ops, uint64_t magicC,
+                                            uint64_t magicEC, const uint32_t* sK,
+                                            const uint32_t* sV, uint32_t nv) {
+    const uint32_t EC = Eb * C;
+    const uint32_t total = 2 * Rb * EC;
+    const uint32_t b = blockIdx.x;
     for (uint32_t hc = threadIdx.x; hc < total; hc += blockDim.x) {
         const uint32_t c = hc >> 1, h = hc & 1;
-        const uint32_t el = (uint32_t)(((uint64_t)c * magic) >> 32);
-        const SlotOp op = ops[c - el * C];
+        const uint32_t q = (uint32_t)(((uint64_t)c * magicEC) >> 32);       // round in batch
+        const uint32_t within = c - q * EC;
+        const uint32_t t = (uint32_t)(((uint64_t)within * magicC) >> 32);   // element in group
+        const uint32_t slot = within - t * C;
+        const uint32_t e = sweep_elem(batch, q, t, Rb, G, Eb, b);
+        if (e >= nel) continue;
+        const SlotOp op = ops[slot];
+        const uint32_t el = q * Eb + t;                                     // thread of phase A
         const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + (el * nv + op.src) * VW;
         const uint4 v = extract_half(src, op.lo, op.nbits, h);
+        uint4* dst = reinterpret_cast<uint4*>(outbase + (uint64_t)e * C + slot) + h;
         if (NT) {
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
             u32x4 w = {v.x, v.y, v.z, v.w};
-            __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(out + hc));
+            __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(dst));
         } else {
-            out[hc] = v;
+            *dst = v;
         }
     }
 }
@@ -200,8 +222,10 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     DView* sVw = reinterpret_cast<DView*>(sMo + kMaxMicro);
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t e0 = a.e_begin + blockIdx.x * kStageElems;
-    const uint32_t ne = min((uint32_t)kStageElems, a.e_end - e0);
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    const uint32_t Eb = a.eb, Rb = a.rb;
+    const uint32_t nel = a.e_end;   // elements [0, e_end) of the stage (e_begin == 0)
+    const uint32_t nbatch = (nel + G * Eb * Rb - 1) / (G * Eb * Rb);
 
     for (uint32_t k = tid; k < a.nk; k += blockDim.x) lds_put(sK + k * VW, a.K[k]);
     for (uint32_t k = tid; k < a.C; k += blockDim.x) sAdv[k] = a.adv[k];
@@ -210,94 +234,109 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     if (tid < kMaxViews) sVw[tid] = a.view[tid];
     __syncthreads();
 
-    // ---- phase A: per-element micro-ops (constants / ops / views read from LDS:
-    // dynamic indexing into the by-value kernel argument would go to scratch)
-    if (tid < ne) {
-        const uint32_t e = e0 + tid;
-        const uint32_t i = e / a.cols, j = e - (e / a.cols) * a.cols;
-        uint32_t* myV = sV + tid * nv * VW;
-        for (uint32_t m = 0; m < a.nmo; ++m) {
-            const MicroOp op = sMo[m];
-            uint32_t* dst = myV + op.dst * VW;
-            switch (op.op) {
-                case MO_LOAD: {
-                    const DView vw = sVw[op.a];
-                    lds_put(dst, view_load(vw, lds_get(sK + vw.pad_k * VW), i, j));
-                    break;
-                }
-                case MO_ADDK:
-                    lds_put(dst, fr_add(lds_get(myV + op.a * VW), lds_get(sK + op.b * VW)));
-                    break;
-                case MO_SUB:
-                    lds_put(dst, fr_sub(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
-                    break;
-                case MO_MUL:
-                    lds_put(dst, fr_mul(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
-                    break;
-                case MO_LIMBSHL: {
-                    const Fr sv = lds_get(myV + op.a * VW);
-                    // 64-bit window at bit p0 (p0 < 256), masked to p1 bits, << b
-                    const uint32_t lo = op.p0, q = lo >> 5, r = lo & 31;
-                    uint32_t w0 = 0, w1 = 0, w2 = 0;
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) {
-                        w0 = (t == (int)q) ? sv.w[t] : w0;
-                        w1 = (t == (int)q + 1) ? sv.w[t] : w1;
-                        w2 = (t == (int)q + 2) ? sv.w[t] : w2;
-                    }
-                    const uint64_t w01 = (uint64_t)w0 | ((uint64_t)w1 << 32);
-                    uint64_t x = r ? ((w01 >> r) | ((uint64_t)w2 << (64 - r))) : w01;
-                    if (op.p1 < 64) x &= (1ull << op.p1) - 1;
-                    const uint32_t sh = op.b;
-                    const uint64_t lo64 = sh < 64 ? (x << sh) : 0;
-                    const uint64_t hi64 = sh == 0 ? 0 : (sh < 64 ? (x >> (64 - sh)) : (x << (sh - 64)));
-                    Fr v = fr_zero();
-                    v.w[0] = (uint32_t)lo64; v.w[1] = (uint32_t)(lo64 >> 32);
-                    v.w[2] = (uint32_t)hi64; v.w[3] = (uint32_t)(hi64 >> 32);
-                    lds_put(dst, v);
-                    break;
-                }
-                case MO_FDBL: {
-                    Fr v = lds_get(myV + op.a * VW);
-                    for (uint32_t t = 0; t < op.b; ++t) v = fr_add(v, v);
-                    lds_put(dst, v);
-                    break;
-                }
-                case MO_ISZERO: {
-                    const Fr v = lds_get(myV + op.a * VW);
-                    const bool z = fr_is_zero(v);
-                    const Fr inv = z ? fr_from_u64(1) : fr_inv(v);
-                    lds_put(dst, fr_from_u64(z ? 1 : 0));
-                    lds_put(dst + VW, inv);
-                    break;
-                }
-                case MO_POWK:
-                    lds_put(dst, fr_pow_u64(lds_get(sK + op.a * VW), (uint64_t)e + op.p0));
-                    break;
-                default:
-                    break;
+    const bool active = tid < Eb * Rb;
+    const uint32_t q_me = tid / Eb, t_me = tid - (tid / Eb) * Eb;
+    // inputs of this thread's element, prefetched one batch ahead
+    Fr pre0 = fr_zero(), pre1 = fr_zero();
+    auto prefetch = [&](uint32_t batch) {
+        const uint32_t e = sweep_elem(batch, q_me, t_me, Rb, G, Eb, b);
+        if (active && e < nel && a.nviews) {
+            const uint32_t i = e / a.cols, j = e - (e / a.cols) * a.cols;
+            const DView v0 = sVw[0];
+            pre0 = view_load(v0, lds_get(sK + v0.pad_k * VW), i, j);
+            if (a.nviews > 1) {
+                const DView v1 = sVw[1];
+                pre1 = view_load(v1, lds_get(sK + v1.pad_k * VW), i, j);
             }
         }
-    }
-    __syncthreads();
-
-    // ---- phase B: advice cells, then lookup cells
-    uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
-    uint4* outL = a.L ? reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L) : nullptr;
-    if (a.flags & STAGE_NT_STORES) {
-        stream_cells<true>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
-        if (a.L) stream_cells<true>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
-    } else {
-        stream_cells<false>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
-        if (a.L) stream_cells<false>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
+    };
+    prefetch(0);
+    for (uint32_t batch = 0; batch < nbatch; ++batch) {
+        // ---- phase A: micro-ops of this thread's element
+        const uint32_t e = sweep_elem(batch, q_me, t_me, Rb, G, Eb, b);
+        if (active && e < nel) {
+            uint32_t* myV = sV + tid * nv * VW;
+            for (uint32_t m = 0; m < a.nmo; ++m) {
+                const MicroOp op = sMo[m];
+                uint32_t* dst = myV + op.dst * VW;
+                switch (op.op) {
+                    case MO_LOAD:
+                        lds_put(dst, op.a == 0 ? pre0 : pre1);
+                        break;
+                    case MO_ADDK:
+                        lds_put(dst, fr_add(lds_get(myV + op.a * VW), lds_get(sK + op.b * VW)));
+                        break;
+                    case MO_SUB:
+                        lds_put(dst, fr_sub(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
+                        break;
+                    case MO_MUL:
+                        lds_put(dst, fr_mul(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
+                        break;
+                    case MO_LIMBSHL: {
+                        const Fr sv = lds_get(myV + op.a * VW);
+                        const uint32_t lo = op.p0, qq = lo >> 5, r = lo & 31;
+                        uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) {
+                            w0 = (t == (int)qq) ? sv.w[t] : w0;
+                            w1 = (t == (int)qq + 1) ? sv.w[t] : w1;
+                            w2 = (t == (int)qq + 2) ? sv.w[t] : w2;
+                        }
+                        const uint64_t w01 = (uint64_t)w0 | ((uint64_t)w1 << 32);
+                        uint64_t x = r ? ((w01 >> r) | ((uint64_t)w2 << (64 - r))) : w01;
+                        if (op.p1 < 64) x &= (1ull << op.p1) - 1;
+                        const uint32_t sh = op.b;
+                        const uint64_t lo64 = sh < 64 ? (x << sh) : 0;
+                        const uint64_t hi64 = sh == 0 ? 0 : (sh < 64 ? (x >> (64 - sh)) : (x << (sh - 64)));
+                        Fr v = fr_zero();
+                        v.w[0] = (uint32_t)lo64; v.w[1] = (uint32_t)(lo64 >> 32);
+                        v.w[2] = (uint32_t)hi64; v.w[3] = (uint32_t)(hi64 >> 32);
+                        lds_put(dst, v);
+                        break;
+                    }
+                    case MO_FDBL: {
+                        Fr v = lds_get(myV + op.a * VW);
+                        for (uint32_t t = 0; t < op.b; ++t) v = fr_add(v, v);
+                        lds_put(dst, v);
+                        break;
+                    }
+                    case MO_ISZERO: {
+                        const Fr v = lds_get(myV + op.a * VW);
+                        const bool z = fr_is_zero(v);
+                        const Fr inv = z ? fr_from_u64(1) : fr_inv(v);
+                        lds_put(dst, fr_from_u64(z ? 1 : 0));
+                        lds_put(dst + VW, inv);
+                        break;
+                    }
+                    case MO_POWK:
+                        lds_put(dst, fr_pow_u64(lds_get(sK + op.a * VW), (uint64_t)e + op.p0));
+                        break;
+                    default:
+                        break;
+                }
+            }
+        }
+        __syncthreads();
+        if (batch + 1 < nbatch) prefetch(batch + 1);   // in flight under the stores below
+        // ---- phase B: this block's cells of the batch's rounds, round by round
+        if (a.flags & STAGE_NT_STORES) {
+            sweep_cells<true>(a.out_adv, a.C, Eb, Rb, G, batch, nel, sAdv, a.cdiv_magic, a.ecdiv_magic, sK, sV, nv);
+            if (a.L) sweep_cells<true>(a.out_lk, a.L, Eb, Rb, G, batch, nel, sLk, a.ldiv_magic, a.eldiv_magic, sK, sV, nv);
+        } else {
+            sweep_cells<false>(a.out_adv, a.C, Eb, Rb, G, batch, nel, sAdv, a.cdiv_magic, a.ecdiv_magic, sK, sV, nv);
+            if (a.L) sweep_cells<false>(a.out_lk, a.L, Eb, Rb, G, batch, nel, sLk, a.ldiv_magic, a.eldiv_magic, sK, sV, nv);
+        }
+        __syncthreads();
     }
 }
 
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
-    if (a.e_end <= a.e_begin) return hipSuccess;
-    const uint32_t n = a.e_end - a.e_begin;
+    if (a.e_end == 0) return hipSuccess;
     const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1);
-    hipLaunchKernelGGL(k_stage, dim3((n + kStageElems - 1) / kStageElems), dim3(256), lds, st, a);
+    // grid: never more blocks than groups of work
+    const uint64_t groups = ((uint64_t)a.e_end + (uint64_t)a.eb * a.rb - 1) / ((uint64_t)a.eb * a.rb);
+    const uint32_t G = (uint32_t)(groups < a.grid ? groups : a.grid);
+    hipLaunchKernelGGL(k_stage, dim3(G ? G : 1), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 
