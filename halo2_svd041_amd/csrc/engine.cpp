@@ -425,11 +425,17 @@ static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, u
     for (uint32_t i = 0; i < a.nmo; ++i)
         if (a.mo[i].op == MO_LOAD) nviews = std::max<uint32_t>(nviews, a.mo[i].a + 1u);
     a.nviews = nviews;
-    // sweep geometry: ~4 KiB of advice cells per block per round
-    a.eb = std::max<uint32_t>(1, std::min<uint32_t>(256, (128 + a.C / 2) / std::max<uint32_t>(a.C, 1)));
+    // sweep geometry: ~4 KiB of advice cells per block per round, rounded so a
+    // block-round is whole 128 B lines (Eb*C and Eb*L multiples of 4 cells)
+    {
+        uint32_t eb = std::max<uint32_t>(1, std::min<uint32_t>(256, (128 + a.C / 2) / std::max<uint32_t>(a.C, 1)));
+        while (eb < 256 && (((uint64_t)eb * a.C) % 4 || ((uint64_t)eb * a.L) % 4)) ++eb;
+        a.eb = eb;
+    }
     a.rb = 256 / a.eb;
     a.grid = c->stage_grid;
-    auto magic = [](uint64_t d) -> uint64_t { return d ? ((1ull << 32) + d - 1) / d : 0; };
+    // 32-bit magics for fastdiv (d == 1 handled in the kernel; x * d < 2^32 there)
+    auto magic = [](uint64_t d) -> uint64_t { return d > 1 ? ((1ull << 32) + d - 1) / d : 0; };
     a.cdiv_magic = magic(a.C);
     a.ldiv_magic = magic(a.L);
     a.ecdiv_magic = magic((uint64_t)a.eb * a.C);

@@ -179,34 +179,54 @@ __device__ __forceinline__ uint32_t sweep_elem(uint32_t batch, uint32_t q, uint3
     return ((batch * Rb + q) * G + b) * Eb + t;
 }
 
-template <bool NT>
+// x / d for x * d < 2^32 via one 32-bit mul_hi (magic = ceil(2^32 / d), d >= 2).
+__device__ __forceinline__ uint32_t fastdiv(uint32_t x, uint32_t d, uint32_t magic) {
+    return d == 1 ? x : __umulhi(x, magic);
+}
+
+// U independent half-cells per thread per iteration: their LDS reads are all
+// in flight before the first wait (one block per CU gives little TLP).
+template <bool NT, int U>
 __device__ __forceinline__ void sweep_cells(Fr* __restrict__ outbase, uint32_t C, uint32_t Eb,
                                             uint32_t Rb, uint32_t G, uint32_t batch, uint32_t nel,
-                                            const SlotOp* __restrict__ ops, uint64_t magicC,
-                                            uint64_t magicEC, const uint32_t* sK,
+                                            const SlotOp* __restrict__ ops, uint32_t magicC,
+                                            uint32_t magicEC, const uint32_t* sK,
                                             const uint32_t* sV, uint32_t nv) {
     const uint32_t EC = Eb * C;
     const uint32_t total = 2 * Rb * EC;
     const uint32_t b = blockIdx.x;
-    for (uint32_t hc = threadIdx.x; hc < total; hc += blockDim.x) {
-        const uint32_t c = hc >> 1, h = hc & 1;
-        const uint32_t q = (uint32_t)(((uint64_t)c * magicEC) >> 32);       // round in batch
-        const uint32_t within = c - q * EC;
-        const uint32_t t = (uint32_t)(((uint64_t)within * magicC) >> 32);   // element in group
-        const uint32_t slot = within - t * C;
-        const uint32_t e = sweep_elem(batch, q, t, Rb, G, Eb, b);
-        if (e >= nel) continue;
-        const SlotOp op = ops[slot];
-        const uint32_t el = q * Eb + t;                                     // thread of phase A
-        const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + (el * nv + op.src) * VW;
-        const uint4 v = extract_half(src, op.lo, op.nbits, h);
-        uint4* dst = reinterpret_cast<uint4*>(outbase + (uint64_t)e * C + slot) + h;
-        if (NT) {
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 w = {v.x, v.y, v.z, v.w};
-            __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(dst));
-        } else {
-            *dst = v;
+    for (uint32_t base = threadIdx.x; base < total; base += blockDim.x * U) {
+        uint4 v[U];
+        uint64_t off[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t hc = base + u * blockDim.x;
+            const uint32_t c = hc >> 1, h = hc & 1;
+            const uint32_t q = fastdiv(c, EC, magicEC);          // round in batch
+            const uint32_t within = c - q * EC;
+            const uint32_t t = fastdiv(within, C, magicC);       // element in group
+            const uint32_t slot = within - t * C;
+            const uint32_t e = sweep_elem(batch, q, t, Rb, G, Eb, b);
+            ok[u] = hc < total && e < nel;
+            const SlotOp op = ops[ok[u] ? slot : 0];
+            const uint32_t el = q * Eb + t;
+            const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW
+                                                 : sV + ((ok[u] ? el : 0) * nv + op.src) * VW;
+            v[u] = extract_half(src, op.lo, op.nbits, h);
+            off[u] = ((uint64_t)e * C + slot) * 2 + h;           // in 16 B units
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            uint4* dst = reinterpret_cast<uint4*>(outbase) + off[u];
+            if (NT) {
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                u32x4 w = {v[u].x, v[u].y, v[u].z, v[u].w};
+                __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(dst));
+            } else {
+                *dst = v[u];
+            }
         }
     }
 }
@@ -320,11 +340,11 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
         if (batch + 1 < nbatch) prefetch(batch + 1);   // in flight under the stores below
         // ---- phase B: this block's cells of the batch's rounds, round by round
         if (a.flags & STAGE_NT_STORES) {
-            sweep_cells<true>(a.out_adv, a.C, Eb, Rb, G, batch, nel, sAdv, a.cdiv_magic, a.ecdiv_magic, sK, sV, nv);
-            if (a.L) sweep_cells<true>(a.out_lk, a.L, Eb, Rb, G, batch, nel, sLk, a.ldiv_magic, a.eldiv_magic, sK, sV, nv);
+            sweep_cells<true, 4>(a.out_adv, a.C, Eb, Rb, G, batch, nel, sAdv, (uint32_t)a.cdiv_magic, (uint32_t)a.ecdiv_magic, sK, sV, nv);
+            if (a.L) sweep_cells<true, 4>(a.out_lk, a.L, Eb, Rb, G, batch, nel, sLk, (uint32_t)a.ldiv_magic, (uint32_t)a.eldiv_magic, sK, sV, nv);
         } else {
-            sweep_cells<false>(a.out_adv, a.C, Eb, Rb, G, batch, nel, sAdv, a.cdiv_magic, a.ecdiv_magic, sK, sV, nv);
-            if (a.L) sweep_cells<false>(a.out_lk, a.L, Eb, Rb, G, batch, nel, sLk, a.ldiv_magic, a.eldiv_magic, sK, sV, nv);
+            sweep_cells<false, 4>(a.out_adv, a.C, Eb, Rb, G, batch, nel, sAdv, (uint32_t)a.cdiv_magic, (uint32_t)a.ecdiv_magic, sK, sV, nv);
+            if (a.L) sweep_cells<false, 4>(a.out_lk, a.L, Eb, Rb, G, batch, nel, sLk, (uint32_t)a.ldiv_magic, (uint32_t)a.eldiv_magic, sK, sV, nv);
         }
         __syncthreads();
     }
