@@ -280,7 +280,6 @@ struct svdw_ctx {
     std::vector<hipEvent_t> pool;
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
     uint32_t stage_flags = 0;               // SVDW_NT_STORES=1 -> STAGE_NT_STORES
-    uint32_t stage_grid = 256;              // persistent k_stage grid (CU count; SVDW_STAGE_GRID)
     // second stream: GEMMs overlap the HBM-bound stages
     hipStream_t st2 = nullptr;
     bool overlap = true;
@@ -421,25 +420,10 @@ static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, u
     a.e_end = nelem;
     a.cols = cols ? cols : 1;
     a.flags = c->stage_flags;
-    uint32_t nviews = 0;
-    for (uint32_t i = 0; i < a.nmo; ++i)
-        if (a.mo[i].op == MO_LOAD) nviews = std::max<uint32_t>(nviews, a.mo[i].a + 1u);
-    a.nviews = nviews;
-    // sweep geometry: ~4 KiB of advice cells per block per round, rounded so a
-    // block-round is whole 128 B lines (Eb*C and Eb*L multiples of 4 cells)
-    {
-        uint32_t eb = std::max<uint32_t>(1, std::min<uint32_t>(256, (128 + a.C / 2) / std::max<uint32_t>(a.C, 1)));
-        while (eb < 256 && (((uint64_t)eb * a.C) % 4 || ((uint64_t)eb * a.L) % 4)) ++eb;
-        a.eb = eb;
-    }
-    a.rb = 256 / a.eb;
-    a.grid = c->stage_grid;
-    // 32-bit magics for fastdiv (d == 1 handled in the kernel; x * d < 2^32 there)
-    auto magic = [](uint64_t d) -> uint64_t { return d > 1 ? ((1ull << 32) + d - 1) / d : 0; };
+    // 32-bit magics for fastdiv (divisor 1 is handled in the kernel)
+    auto magic = [](uint64_t d) -> uint32_t { return d > 1 ? (uint32_t)(((1ull << 32) + d - 1) / d) : 0; };
     a.cdiv_magic = magic(a.C);
     a.ldiv_magic = magic(a.L);
-    a.ecdiv_magic = magic((uint64_t)a.eb * a.C);
-    a.eldiv_magic = magic((uint64_t)a.eb * a.L);
     uint32_t loads = 0;
     for (uint32_t i = 0; i < a.nmo; ++i) loads += a.mo[i].op == MO_LOAD;
     {
@@ -898,13 +882,6 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
         c->LB = p->lookup_bits;
         c->device = p->device;
         c->dry = p->device < 0;
-        if (!c->dry) {
-            int cus = 0;
-            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device) ==
-                    hipSuccess && cus > 0)
-                c->stage_grid = (uint32_t)cus;
-        }
-        if (const char* g = getenv("SVDW_STAGE_GRID")) c->stage_grid = (uint32_t)std::max(1, atoi(g));
         if (const char* nt = getenv("SVDW_NT_STORES"))
             c->stage_flags = (nt[0] == '1') ? STAGE_NT_STORES : 0;
         if (const char* g = getenv("SVDW_GEMM"))

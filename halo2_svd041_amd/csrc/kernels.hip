@@ -168,64 +168,40 @@ __host__ __device__ constexpr uint32_t stage_lds_bytes(uint32_t nv) {
            kMaxViews * 48;
 }
 
-// Element e of the stage in the sweep order: round r covers elements
-// [r*G*Eb, (r+1)*G*Eb); block b owns [r*G*Eb + b*Eb, +Eb) of every round, and
-// its output for one round is Eb*C consecutive cells. A batch is Rb rounds
-// (Rb*Eb <= 256 elements, one per thread in phase A). All blocks advance round
-// by round, so the chip writes one ~G*Eb*C*32 B window at a time (a "sweep
-// front": 6.2-6.4 TB/s in tools/storepat*.hip vs ~5.5 for per-block chunks).
-__device__ __forceinline__ uint32_t sweep_elem(uint32_t batch, uint32_t q, uint32_t t, uint32_t Rb,
-                                               uint32_t G, uint32_t Eb, uint32_t b) {
-    return ((batch * Rb + q) * G + b) * Eb + t;
-}
-
 // x / d for x * d < 2^32 via one 32-bit mul_hi (magic = ceil(2^32 / d), d >= 2).
 __device__ __forceinline__ uint32_t fastdiv(uint32_t x, uint32_t d, uint32_t magic) {
     return d == 1 ? x : __umulhi(x, magic);
 }
 
-// U independent half-cells per thread per iteration: their LDS reads are all
-// in flight before the first wait (one block per CU gives little TLP).
+// The block's cells in stream order, half a cell (16 B) per lane: every wave
+// store is 1 KiB contiguous. U independent half-cells per thread per iteration
+// keep several LDS round trips in flight.
 template <bool NT, int U>
-__device__ __forceinline__ void sweep_cells(Fr* __restrict__ outbase, uint32_t C, uint32_t Eb,
-                                            uint32_t Rb, uint32_t G, uint32_t batch, uint32_t nel,
-                                            const SlotOp* __restrict__ ops, uint32_t magicC,
-                                            uint32_t magicEC, const uint32_t* sK,
-                                            const uint32_t* sV, uint32_t nv) {
-    const uint32_t EC = Eb * C;
-    const uint32_t total = 2 * Rb * EC;
-    const uint32_t b = blockIdx.x;
+__device__ __forceinline__ void stream_cells(uint4* __restrict__ out, uint32_t total,
+                                             const SlotOp* __restrict__ ops, uint32_t C,
+                                             uint32_t magic, const uint32_t* sK, const uint32_t* sV,
+                                             uint32_t nv) {
     for (uint32_t base = threadIdx.x; base < total; base += blockDim.x * U) {
         uint4 v[U];
-        uint64_t off[U];
-        bool ok[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint32_t hc = base + u * blockDim.x;
+            const uint32_t hc = min(base + u * blockDim.x, total - 1);
             const uint32_t c = hc >> 1, h = hc & 1;
-            const uint32_t q = fastdiv(c, EC, magicEC);          // round in batch
-            const uint32_t within = c - q * EC;
-            const uint32_t t = fastdiv(within, C, magicC);       // element in group
-            const uint32_t slot = within - t * C;
-            const uint32_t e = sweep_elem(batch, q, t, Rb, G, Eb, b);
-            ok[u] = hc < total && e < nel;
-            const SlotOp op = ops[ok[u] ? slot : 0];
-            const uint32_t el = q * Eb + t;
-            const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW
-                                                 : sV + ((ok[u] ? el : 0) * nv + op.src) * VW;
+            const uint32_t el = fastdiv(c, C, magic);
+            const SlotOp op = ops[c - el * C];
+            const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + (el * nv + op.src) * VW;
             v[u] = extract_half(src, op.lo, op.nbits, h);
-            off[u] = ((uint64_t)e * C + slot) * 2 + h;           // in 16 B units
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (!ok[u]) continue;
-            uint4* dst = reinterpret_cast<uint4*>(outbase) + off[u];
+            const uint32_t hc = base + u * blockDim.x;
+            if (hc >= total) break;
             if (NT) {
                 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
                 u32x4 w = {v[u].x, v[u].y, v[u].z, v[u].w};
-                __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(dst));
+                __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(out + hc));
             } else {
-                *dst = v[u];
+                out[hc] = v[u];
             }
         }
     }
@@ -242,10 +218,8 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     DView* sVw = reinterpret_cast<DView*>(sMo + kMaxMicro);
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t G = gridDim.x, b = blockIdx.x;
-    const uint32_t Eb = a.eb, Rb = a.rb;
-    const uint32_t nel = a.e_end;   // elements [0, e_end) of the stage (e_begin == 0)
-    const uint32_t nbatch = (nel + G * Eb * Rb - 1) / (G * Eb * Rb);
+    const uint32_t e0 = a.e_begin + blockIdx.x * kStageElems;
+    const uint32_t ne = min((uint32_t)kStageElems, a.e_end - e0);
 
     for (uint32_t k = tid; k < a.nk; k += blockDim.x) lds_put(sK + k * VW, a.K[k]);
     for (uint32_t k = tid; k < a.C; k += blockDim.x) sAdv[k] = a.adv[k];
@@ -254,109 +228,94 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     if (tid < kMaxViews) sVw[tid] = a.view[tid];
     __syncthreads();
 
-    const bool active = tid < Eb * Rb;
-    const uint32_t q_me = tid / Eb, t_me = tid - (tid / Eb) * Eb;
-    // inputs of this thread's element, prefetched one batch ahead
-    Fr pre0 = fr_zero(), pre1 = fr_zero();
-    auto prefetch = [&](uint32_t batch) {
-        const uint32_t e = sweep_elem(batch, q_me, t_me, Rb, G, Eb, b);
-        if (active && e < nel && a.nviews) {
-            const uint32_t i = e / a.cols, j = e - (e / a.cols) * a.cols;
-            const DView v0 = sVw[0];
-            pre0 = view_load(v0, lds_get(sK + v0.pad_k * VW), i, j);
-            if (a.nviews > 1) {
-                const DView v1 = sVw[1];
-                pre1 = view_load(v1, lds_get(sK + v1.pad_k * VW), i, j);
-            }
-        }
-    };
-    prefetch(0);
-    for (uint32_t batch = 0; batch < nbatch; ++batch) {
-        // ---- phase A: micro-ops of this thread's element
-        const uint32_t e = sweep_elem(batch, q_me, t_me, Rb, G, Eb, b);
-        if (active && e < nel) {
-            uint32_t* myV = sV + tid * nv * VW;
-            for (uint32_t m = 0; m < a.nmo; ++m) {
-                const MicroOp op = sMo[m];
-                uint32_t* dst = myV + op.dst * VW;
-                switch (op.op) {
-                    case MO_LOAD:
-                        lds_put(dst, op.a == 0 ? pre0 : pre1);
-                        break;
-                    case MO_ADDK:
-                        lds_put(dst, fr_add(lds_get(myV + op.a * VW), lds_get(sK + op.b * VW)));
-                        break;
-                    case MO_SUB:
-                        lds_put(dst, fr_sub(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
-                        break;
-                    case MO_MUL:
-                        lds_put(dst, fr_mul(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
-                        break;
-                    case MO_LIMBSHL: {
-                        const Fr sv = lds_get(myV + op.a * VW);
-                        const uint32_t lo = op.p0, qq = lo >> 5, r = lo & 31;
-                        uint32_t w0 = 0, w1 = 0, w2 = 0;
-#pragma unroll
-                        for (int t = 0; t < 8; ++t) {
-                            w0 = (t == (int)qq) ? sv.w[t] : w0;
-                            w1 = (t == (int)qq + 1) ? sv.w[t] : w1;
-                            w2 = (t == (int)qq + 2) ? sv.w[t] : w2;
-                        }
-                        const uint64_t w01 = (uint64_t)w0 | ((uint64_t)w1 << 32);
-                        uint64_t x = r ? ((w01 >> r) | ((uint64_t)w2 << (64 - r))) : w01;
-                        if (op.p1 < 64) x &= (1ull << op.p1) - 1;
-                        const uint32_t sh = op.b;
-                        const uint64_t lo64 = sh < 64 ? (x << sh) : 0;
-                        const uint64_t hi64 = sh == 0 ? 0 : (sh < 64 ? (x >> (64 - sh)) : (x << (sh - 64)));
-                        Fr v = fr_zero();
-                        v.w[0] = (uint32_t)lo64; v.w[1] = (uint32_t)(lo64 >> 32);
-                        v.w[2] = (uint32_t)hi64; v.w[3] = (uint32_t)(hi64 >> 32);
-                        lds_put(dst, v);
-                        break;
-                    }
-                    case MO_FDBL: {
-                        Fr v = lds_get(myV + op.a * VW);
-                        for (uint32_t t = 0; t < op.b; ++t) v = fr_add(v, v);
-                        lds_put(dst, v);
-                        break;
-                    }
-                    case MO_ISZERO: {
-                        const Fr v = lds_get(myV + op.a * VW);
-                        const bool z = fr_is_zero(v);
-                        const Fr inv = z ? fr_from_u64(1) : fr_inv(v);
-                        lds_put(dst, fr_from_u64(z ? 1 : 0));
-                        lds_put(dst + VW, inv);
-                        break;
-                    }
-                    case MO_POWK:
-                        lds_put(dst, fr_pow_u64(lds_get(sK + op.a * VW), (uint64_t)e + op.p0));
-                        break;
-                    default:
-                        break;
+    // ---- phase A: per-element micro-ops (constants / ops / views read from LDS:
+    // dynamic indexing into the by-value kernel argument would go to scratch)
+    if (tid < ne) {
+        const uint32_t e = e0 + tid;
+        const uint32_t i = e / a.cols, j = e - (e / a.cols) * a.cols;
+        uint32_t* myV = sV + tid * nv * VW;
+        for (uint32_t m = 0; m < a.nmo; ++m) {
+            const MicroOp op = sMo[m];
+            uint32_t* dst = myV + op.dst * VW;
+            switch (op.op) {
+                case MO_LOAD: {
+                    const DView vw = sVw[op.a];
+                    lds_put(dst, view_load(vw, lds_get(sK + vw.pad_k * VW), i, j));
+                    break;
                 }
+                case MO_ADDK:
+                    lds_put(dst, fr_add(lds_get(myV + op.a * VW), lds_get(sK + op.b * VW)));
+                    break;
+                case MO_SUB:
+                    lds_put(dst, fr_sub(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
+                    break;
+                case MO_MUL:
+                    lds_put(dst, fr_mul(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
+                    break;
+                case MO_LIMBSHL: {
+                    const Fr sv = lds_get(myV + op.a * VW);
+                    // 64-bit window at bit p0 (p0 < 256), masked to p1 bits, << b
+                    const uint32_t lo = op.p0, q = lo >> 5, r = lo & 31;
+                    uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        w0 = (t == (int)q) ? sv.w[t] : w0;
+                        w1 = (t == (int)q + 1) ? sv.w[t] : w1;
+                        w2 = (t == (int)q + 2) ? sv.w[t] : w2;
+                    }
+                    const uint64_t w01 = (uint64_t)w0 | ((uint64_t)w1 << 32);
+                    uint64_t x = r ? ((w01 >> r) | ((uint64_t)w2 << (64 - r))) : w01;
+                    if (op.p1 < 64) x &= (1ull << op.p1) - 1;
+                    const uint32_t sh = op.b;
+                    const uint64_t lo64 = sh < 64 ? (x << sh) : 0;
+                    const uint64_t hi64 = sh == 0 ? 0 : (sh < 64 ? (x >> (64 - sh)) : (x << (sh - 64)));
+                    Fr v = fr_zero();
+                    v.w[0] = (uint32_t)lo64; v.w[1] = (uint32_t)(lo64 >> 32);
+                    v.w[2] = (uint32_t)hi64; v.w[3] = (uint32_t)(hi64 >> 32);
+                    lds_put(dst, v);
+                    break;
+                }
+                case MO_FDBL: {
+                    Fr v = lds_get(myV + op.a * VW);
+                    for (uint32_t t = 0; t < op.b; ++t) v = fr_add(v, v);
+                    lds_put(dst, v);
+                    break;
+                }
+                case MO_ISZERO: {
+                    const Fr v = lds_get(myV + op.a * VW);
+                    const bool z = fr_is_zero(v);
+                    const Fr inv = z ? fr_from_u64(1) : fr_inv(v);
+                    lds_put(dst, fr_from_u64(z ? 1 : 0));
+                    lds_put(dst + VW, inv);
+                    break;
+                }
+                case MO_POWK:
+                    lds_put(dst, fr_pow_u64(lds_get(sK + op.a * VW), (uint64_t)e + op.p0));
+                    break;
+                default:
+                    break;
             }
         }
-        __syncthreads();
-        if (batch + 1 < nbatch) prefetch(batch + 1);   // in flight under the stores below
-        // ---- phase B: this block's cells of the batch's rounds, round by round
-        if (a.flags & STAGE_NT_STORES) {
-            sweep_cells<true, 4>(a.out_adv, a.C, Eb, Rb, G, batch, nel, sAdv, (uint32_t)a.cdiv_magic, (uint32_t)a.ecdiv_magic, sK, sV, nv);
-            if (a.L) sweep_cells<true, 4>(a.out_lk, a.L, Eb, Rb, G, batch, nel, sLk, (uint32_t)a.ldiv_magic, (uint32_t)a.eldiv_magic, sK, sV, nv);
-        } else {
-            sweep_cells<false, 4>(a.out_adv, a.C, Eb, Rb, G, batch, nel, sAdv, (uint32_t)a.cdiv_magic, (uint32_t)a.ecdiv_magic, sK, sV, nv);
-            if (a.L) sweep_cells<false, 4>(a.out_lk, a.L, Eb, Rb, G, batch, nel, sLk, (uint32_t)a.ldiv_magic, (uint32_t)a.eldiv_magic, sK, sV, nv);
-        }
-        __syncthreads();
+    }
+    __syncthreads();
+
+    // ---- phase B: advice cells, then lookup cells
+    uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
+    uint4* outL = a.L ? reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L) : nullptr;
+    if (a.flags & STAGE_NT_STORES) {
+        stream_cells<true, 4>(outA, 2 * ne * a.C, sAdv, a.C, (uint32_t)a.cdiv_magic, sK, sV, nv);
+        if (a.L) stream_cells<true, 4>(outL, 2 * ne * a.L, sLk, a.L, (uint32_t)a.ldiv_magic, sK, sV, nv);
+    } else {
+        stream_cells<false, 4>(outA, 2 * ne * a.C, sAdv, a.C, (uint32_t)a.cdiv_magic, sK, sV, nv);
+        if (a.L) stream_cells<false, 4>(outL, 2 * ne * a.L, sLk, a.L, (uint32_t)a.ldiv_magic, sK, sV, nv);
     }
 }
 
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
-    if (a.e_end == 0) return hipSuccess;
+    if (a.e_end <= a.e_begin) return hipSuccess;
+    const uint32_t n = a.e_end - a.e_begin;
     const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1);
-    // grid: never more blocks than groups of work
-    const uint64_t groups = ((uint64_t)a.e_end + (uint64_t)a.eb * a.rb - 1) / ((uint64_t)a.eb * a.rb);
-    const uint32_t G = (uint32_t)(groups < a.grid ? groups : a.grid);
-    hipLaunchKernelGGL(k_stage, dim3(G ? G : 1), dim3(256), lds, st, a);
+    hipLaunchKernelGGL(k_stage, dim3((n + kStageElems - 1) / kStageElems), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 
@@ -843,50 +802,56 @@ __global__ __launch_bounds__(256) void k_matvec_scan(const DView A, uint32_t r_b
                                                      const Fr* __restrict__ wc,
                                                      const Fr* __restrict__ wm,
                                                      Fr* __restrict__ out) {
-    __shared__ uint32_t stage[3 * 256 * 8];
+    // T consecutive terms per thread: products, sequential local prefix, one
+    // cross-lane Fr scan per T terms, then the thread's 3T consecutive cells
+    // [a_j, w_j, s_j] are stored directly (16 B pieces; each 128 B line is
+    // completed by one lane's consecutive stores and merged in L2).
+    constexpr int T = 4;
     __shared__ Fr wtot[4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t r = r_begin + blockIdx.x;
     Fr* rowout = out + (uint64_t)blockIdx.x * (3ull * L + 1);
-    Fr zero = fr_zero();
+    const Fr zero = fr_zero();
     if (tid == 0) st_fr(rowout, zero);
     Fr carry = fr_zero();
-    for (uint32_t c0 = 0; c0 < L; c0 += 256) {
-        const uint32_t j = c0 + tid;
-        const bool valid = j < L;
-        Fr a = zero, w = zero, p = zero;
-        if (valid) {
-            a = view_load(A, zero, r, j);
-            w = ld_fr(wc + j);
-            p = mont_mul(a, ld_fr(wm + j));
+    for (uint32_t c0 = 0; c0 < L; c0 += 256 * T) {
+        const uint32_t j0 = c0 + tid * T;
+        Fr a[T], s[T];
+#pragma unroll
+        for (int i = 0; i < T; ++i) {
+            const uint32_t j = j0 + i;
+            a[i] = j < L ? view_load(A, zero, r, j) : zero;
+            s[i] = j < L ? mont_mul(a[i], ld_fr(wm + j)) : zero;   // a_j * w_j (canonical)
         }
-        Fr s = p;
+#pragma unroll
+        for (int i = 1; i < T; ++i) s[i] = fr_add(s[i], s[i - 1]);
+        // inclusive wave scan of the per-thread totals
+        Fr tot = s[T - 1];
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
-            Fr o = shfl_up_fr(s, off);
-            if ((int)lane >= off) s = fr_add(s, o);
+            Fr o = shfl_up_fr(tot, off);
+            if ((int)lane >= off) tot = fr_add(tot, o);
         }
-        if (lane == 63) wtot[wave] = s;
+        if (lane == 63) wtot[wave] = tot;
         __syncthreads();
-        Fr pre = carry;
+        // exclusive prefix of this thread = carry + earlier waves + (tot - own total)
+        Fr pre = fr_sub(tot, s[T - 1]);
+        pre = fr_add(pre, carry);
         for (uint32_t w2 = 0; w2 < wave; ++w2) pre = fr_add(pre, wtot[w2]);
-        s = fr_add(s, pre);
-        uint32_t* st3 = stage + tid * 24;
+        Fr ctot = carry;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            st3[i] = a.w[i];
-            st3[8 + i] = w.w[i];
-            st3[16 + i] = s.w[i];
+        for (int w2 = 0; w2 < 4; ++w2) ctot = fr_add(ctot, wtot[w2]);
+#pragma unroll
+        for (int i = 0; i < T; ++i) {
+            const uint32_t j = j0 + i;
+            if (j < L) {
+                Fr* cell = rowout + 1 + 3ull * j;
+                st_fr(cell, a[i]);
+                st_fr(cell + 1, ld_fr(wc + j));
+                st_fr(cell + 2, fr_add(s[i], pre));
+            }
         }
-        Fr tot = carry;
-#pragma unroll
-        for (int w2 = 0; w2 < 4; ++w2) tot = fr_add(tot, wtot[w2]);
-        __syncthreads();
-        const uint32_t ncell = 3 * min(256u, L - c0);
-        uint4* o = reinterpret_cast<uint4*>(rowout + 1 + 3ull * c0);
-        const uint4* sv = reinterpret_cast<const uint4*>(stage);
-        for (uint32_t hc = tid; hc < 2 * ncell; hc += 256) o[hc] = sv[hc];
-        carry = tot;
+        carry = ctot;
         __syncthreads();
     }
 }

@@ -70,17 +70,13 @@ static constexpr int kMaxV = 8;
 struct StageArgs {
     Fr* out_adv;          // cell 0 of element 0 of this stage
     Fr* out_lk;           // lookup cell 0 of element 0 (may be null if L == 0)
-    uint32_t e_begin, e_end;   // elements [0, e_end) (e_begin reserved, must be 0)
+    uint32_t e_begin, e_end;   // element range processed by this launch
     uint32_t cols;        // element e -> (i, j) = (e / cols, e % cols)
     uint32_t C, L;        // advice / lookup cells per element
-    uint32_t nv, nmo, nk, nviews;
+    uint32_t nv, nmo, nk;
     uint32_t flags;       // STAGE_* bits
-    uint32_t eb, rb;      // sweep: elements per block per round, rounds per batch (eb*rb <= 256)
-    uint32_t grid;        // persistent grid size (blocks)
-    uint64_t cdiv_magic;  // ceil(2^32 / C): x / C = (x * magic) >> 32, exact for x*C < 2^25
-    uint64_t ldiv_magic;  // ceil(2^32 / L)
-    uint64_t ecdiv_magic; // ceil(2^32 / (eb*C))
-    uint64_t eldiv_magic; // ceil(2^32 / (eb*L))
+    uint32_t cdiv_magic;  // ceil(2^32 / C) (C >= 2): x / C = mul_hi(x, magic) for x * C < 2^32
+    uint32_t ldiv_magic;  // ceil(2^32 / L)
     DView view[kMaxViews];
     MicroOp mo[kMaxMicro];
     SlotOp adv[kMaxAdv];
