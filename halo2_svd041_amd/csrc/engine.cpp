@@ -279,7 +279,8 @@ struct svdw_ctx {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
-    uint32_t stage_flags = 0;               // SVDW_NT_STORES=1 -> STAGE_NT_STORES
+    uint32_t stage_flags = 0;               // STAGE_* (svdw_set_option "nt_stores", "stage_ilp")
+    int scan_impl = 1;                      // svdw_set_option "scan_impl"
     // second stream: GEMMs overlap the HBM-bound stages
     hipStream_t st2 = nullptr;
     bool overlap = true;
@@ -666,8 +667,8 @@ static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, cons
     append(c, phase, (uint64_t)R * (3ull * L + 1), 0, &off, nullptr);
     if (!c->dry) {
         ProfScope ps(c, c->st, "k_matvec_scan", 32.0 * (double)R * (4.0 * L + 1) + 64.0 * L, (double)R * L);
-        hipck(launch_matvec_scan(view_of(c, a), 0, R, L, wc, wm, cellp(c, phase, off), c->st),
-              "k_matvec_scan");
+        hipck(launch_matvec_scan(view_of(c, a), 0, R, L, wc, wm, cellp(c, phase, off), c->scan_impl,
+                                 c->st), "k_matvec_scan");
     }
     return svdw_vec{phase, R, off + 3ull * L, (int64_t)(3ull * L + 1)};
 }
@@ -1102,6 +1103,30 @@ int svdw_svd_witness(svdw_ctx* c, const double* m, const double* u, const double
         REQUIRE(c->dry || (m && u && v && d), "null input matrix");
         svdw_counts k = svd_witness(c, m, u, v, d, N, M, on_device != 0, *cfg, fr_from_words(gamma));
         if (counts) *counts = k;
+    });
+}
+int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
+    return guarded([&] {
+        REQUIRE(c && name, "null argument");
+        sync(c);
+        const std::string n(name);
+        if (n == "gemm_impl") {
+            REQUIRE(value == SVDW_GEMM_MFMA || value == SVDW_GEMM_VALU, "gemm_impl: 0 (mfma) or 1 (valu)");
+            c->gemm_impl = (int)value;
+        } else if (n == "nt_stores") {
+            c->stage_flags = (c->stage_flags & ~STAGE_NT_STORES) | (value ? STAGE_NT_STORES : 0);
+        } else if (n == "stage_ilp") {
+            REQUIRE(value == 1 || value == 2 || value == 4, "stage_ilp: 1, 2 or 4");
+            c->stage_flags = (c->stage_flags & ~(STAGE_ILP2 | STAGE_ILP4)) |
+                             (value == 2 ? STAGE_ILP2 : value == 4 ? STAGE_ILP4 : 0);
+        } else if (n == "scan_impl") {
+            REQUIRE(value == 1 || value == 2, "scan_impl: 1 or 2");
+            c->scan_impl = (int)value;
+        } else if (n == "overlap") {
+            c->overlap = value != 0;
+        } else {
+            fail(SVDW_EINVAL, "unknown option " + n);
+        }
     });
 }
 int svdw_set_gemm_impl(svdw_ctx* c, int impl) {

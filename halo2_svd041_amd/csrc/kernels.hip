@@ -302,13 +302,16 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     // ---- phase B: advice cells, then lookup cells
     uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
     uint4* outL = a.L ? reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L) : nullptr;
-    if (a.flags & STAGE_NT_STORES) {
-        stream_cells<true, 4>(outA, 2 * ne * a.C, sAdv, a.C, (uint32_t)a.cdiv_magic, sK, sV, nv);
-        if (a.L) stream_cells<true, 4>(outL, 2 * ne * a.L, sLk, a.L, (uint32_t)a.ldiv_magic, sK, sV, nv);
-    } else {
-        stream_cells<false, 4>(outA, 2 * ne * a.C, sAdv, a.C, (uint32_t)a.cdiv_magic, sK, sV, nv);
-        if (a.L) stream_cells<false, 4>(outL, 2 * ne * a.L, sLk, a.L, (uint32_t)a.ldiv_magic, sK, sV, nv);
-    }
+#define SVDW_STREAM(NT, U)                                                                         \
+    do {                                                                                           \
+        stream_cells<NT, U>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);             \
+        if (a.L) stream_cells<NT, U>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);     \
+    } while (0)
+    if (a.flags & STAGE_NT_STORES) SVDW_STREAM(true, 1);
+    else if (a.flags & STAGE_ILP4) SVDW_STREAM(false, 4);
+    else if (a.flags & STAGE_ILP2) SVDW_STREAM(false, 2);
+    else SVDW_STREAM(false, 1);
+#undef SVDW_STREAM
 }
 
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
@@ -798,6 +801,58 @@ __device__ __forceinline__ Fr shfl_up_fr(const Fr& v, int d) {
     return r;
 }
 
+__global__ __launch_bounds__(256) void k_matvec_scan_v1(const DView A, uint32_t r_begin, uint32_t L,
+                                                     const Fr* __restrict__ wc,
+                                                     const Fr* __restrict__ wm,
+                                                     Fr* __restrict__ out) {
+    __shared__ uint32_t stage[3 * 256 * 8];
+    __shared__ Fr wtot[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t r = r_begin + blockIdx.x;
+    Fr* rowout = out + (uint64_t)blockIdx.x * (3ull * L + 1);
+    Fr zero = fr_zero();
+    if (tid == 0) st_fr(rowout, zero);
+    Fr carry = fr_zero();
+    for (uint32_t c0 = 0; c0 < L; c0 += 256) {
+        const uint32_t j = c0 + tid;
+        const bool valid = j < L;
+        Fr a = zero, w = zero, p = zero;
+        if (valid) {
+            a = view_load(A, zero, r, j);
+            w = ld_fr(wc + j);
+            p = mont_mul(a, ld_fr(wm + j));
+        }
+        Fr s = p;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            Fr o = shfl_up_fr(s, off);
+            if ((int)lane >= off) s = fr_add(s, o);
+        }
+        if (lane == 63) wtot[wave] = s;
+        __syncthreads();
+        Fr pre = carry;
+        for (uint32_t w2 = 0; w2 < wave; ++w2) pre = fr_add(pre, wtot[w2]);
+        s = fr_add(s, pre);
+        uint32_t* st3 = stage + tid * 24;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            st3[i] = a.w[i];
+            st3[8 + i] = w.w[i];
+            st3[16 + i] = s.w[i];
+        }
+        Fr tot = carry;
+#pragma unroll
+        for (int w2 = 0; w2 < 4; ++w2) tot = fr_add(tot, wtot[w2]);
+        __syncthreads();
+        const uint32_t ncell = 3 * min(256u, L - c0);
+        uint4* o = reinterpret_cast<uint4*>(rowout + 1 + 3ull * c0);
+        const uint4* sv = reinterpret_cast<const uint4*>(stage);
+        for (uint32_t hc = tid; hc < 2 * ncell; hc += 256) o[hc] = sv[hc];
+        carry = tot;
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(256) void k_matvec_scan(const DView A, uint32_t r_begin, uint32_t L,
                                                      const Fr* __restrict__ wc,
                                                      const Fr* __restrict__ wm,
@@ -857,10 +912,14 @@ __global__ __launch_bounds__(256) void k_matvec_scan(const DView A, uint32_t r_b
 }
 
 hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
-                              const Fr* wc, const Fr* wm, Fr* out, hipStream_t st) {
+                              const Fr* wc, const Fr* wm, Fr* out, int impl, hipStream_t st) {
     if (r_end <= r_begin || !L) return hipSuccess;
-    hipLaunchKernelGGL(k_matvec_scan, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L, wc,
-                       wm, out);
+    if (impl == 1)
+        hipLaunchKernelGGL(k_matvec_scan_v1, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L,
+                           wc, wm, out);
+    else
+        hipLaunchKernelGGL(k_matvec_scan, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L, wc,
+                           wm, out);
     return hipGetLastError();
 }
 

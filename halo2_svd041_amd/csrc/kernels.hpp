@@ -45,7 +45,8 @@ hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* w_mont, 
 hipError_t launch_gamma_vec(const Fr& gamma, uint32_t L, Fr* w_canon, Fr* w_mont, hipStream_t st);
 // Freivalds inner-product rows (GateChip::inner_product, 1+3L cells per row) for
 // rows [r_begin, r_end) of A (R x L); row r's cells at out + (r - r_begin)*(3L+1).
+// impl 1: one term per thread, LDS-staged coalesced stores; 2: four terms per thread.
 hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
-                              const Fr* w_canon, const Fr* w_mont, Fr* out, hipStream_t st);
+                              const Fr* w_canon, const Fr* w_mont, Fr* out, int impl, hipStream_t st);
 
 }  // namespace svdw

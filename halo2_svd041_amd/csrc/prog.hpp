@@ -58,6 +58,8 @@ struct SlotOp {
 static constexpr uint8_t KSRC = 0x80;
 
 static constexpr uint32_t STAGE_NT_STORES = 1;   // non-temporal cell stores
+static constexpr uint32_t STAGE_ILP2 = 2;        // 2 / 4 independent half-cells per iteration
+static constexpr uint32_t STAGE_ILP4 = 4;
 
 static constexpr int kMaxViews = 2;
 static constexpr int kMaxMicro = 16;

@@ -123,6 +123,10 @@ class Context:
         """'mfma' (matrix cores, default) or 'valu' (v_dot4): bit-identical GEMM paths."""
         check(lib().svdw_set_gemm_impl(self._h, {"mfma": 0, "valu": 1}[impl]))
 
+    def set_option(self, name: str, value: int) -> None:
+        """Tuning knobs (include/svdw.h): gemm_impl, nt_stores, stage_ilp, scan_impl, overlap."""
+        check(lib().svdw_set_option(self._h, name.encode(), int(value)))
+
     def profile(self, on: bool = True) -> None:
         """Record HIP events around every kernel launch on this context's stream."""
         check(lib().svdw_profile_enable(self._h, 1 if on else 0))

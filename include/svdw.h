@@ -165,6 +165,11 @@ int svdw_svd_witness(svdw_ctx* ctx, const double* m, const double* u, const doub
 #define SVDW_GEMM_MFMA 0
 #define SVDW_GEMM_VALU 1
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
+/* Tuning knobs (bit-identical results for every value):
+ *   "gemm_impl" 0 | 1, "nt_stores" 0 | 1 (non-temporal cell stores),
+ *   "stage_ilp" 1 | 2 | 4 (half-cells in flight per thread), "scan_impl" 1 | 2
+ *   (row-scan kernel variant), "overlap" 0 | 1 (GEMMs ahead on a second stream). */
+int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);
 
 /* ----------------------------------------------------------- profiling */
 /* Per-kernel statistics from HIP events recorded around every launch on the

@@ -156,3 +156,19 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                 want = sum(qa[i][k] * qb[k][j] for k in range(131)) % po.P_MOD
                 assert int(got[i, j, 0]) | (int(got[i, j, 1]) << 64) | (int(got[i, j, 2]) << 128) \
                     | (int(got[i, j, 3]) << 192) == want
+
+
+@pytest.mark.parametrize("opts", [{"stage_ilp": 2}, {"stage_ilp": 4}, {"nt_stores": 1},
+                                  {"scan_impl": 2}, {"overlap": 0}])
+def test_tuning_options_parity(gpu_ctx_factory, opts):
+    """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
+    import halo2_svd041_amd as hs
+    N, M, P = 45, 37, 63
+    m, u, d, v = gen_svd_input(N, M, seed=4)
+    g = gamma_for(4)
+    ctx = gpu_ctx_factory(P)
+    for k, val in opts.items():
+        ctx.set_option(k, val)
+    hs.svd_witness(ctx, m, u, v, d, g)
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+    _assert_streams(ctx, a0, l0, a1)

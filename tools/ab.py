@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of engine tuning options in ONE process (guide rule 24).
+
+    python tools/ab.py --n 1024 --p 63 --rounds 5 --steps 3 \
+        --variant base: --variant ilp4:stage_ilp=4 --variant scan2:scan_impl=2
+Prints median / min ms per step and per-kernel medians for each variant.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import gamma_for, gen_input  # noqa: E402
+
+
+def parse_variant(s):
+    name, _, rest = s.partition(":")
+    opts = {}
+    for kv in filter(None, rest.split(",")):
+        k, v = kv.split("=")
+        opts[k] = int(v)
+    return name, opts
+
+
+DEFAULTS = {"gemm_impl": 0, "nt_stores": 0, "stage_ilp": 1, "scan_impl": 1, "overlap": 1}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--p", type=int, default=63)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--variant", action="append", default=[])
+    a = ap.parse_args()
+    import torch
+    import halo2_svd041_amd as hs
+    N, M = a.n, a.m or a.n
+    m, u, d, v = gen_input(N, M, 0)
+    g = gamma_for(0)
+    dev = torch.device("cuda", 0)
+    dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev) for x in (m, u, v, d))
+    ctx = hs.Context(device=0, precision_bits=a.p, lookup_bits=19)
+    variants = [parse_variant(s) for s in (a.variant or ["base:"])]
+    res = {name: [] for name, _ in variants}
+    kern = {name: {} for name, _ in variants}
+    for name, opts in variants:          # warm every variant once
+        for k, val in {**DEFAULTS, **opts}.items():
+            ctx.set_option(k, val)
+        hs.svd_witness(ctx, dm, du, dv, dd, g)
+    ctx.sync()
+    for _ in range(a.rounds):
+        for name, opts in variants:
+            for k, val in {**DEFAULTS, **opts}.items():
+                ctx.set_option(k, val)
+            hs.svd_witness(ctx, dm, du, dv, dd, g)
+            ctx.sync()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                hs.svd_witness(ctx, dm, du, dv, dd, g)
+            ctx.sync()
+            res[name].append((time.perf_counter() - t0) / a.steps * 1e3)
+            ctx.profile(True)
+            hs.svd_witness(ctx, dm, du, dv, dd, g)
+            for s in ctx.profile_collect():
+                kern[name].setdefault(s["name"], []).append(s["total_ms"])
+            ctx.profile(False)
+    cells = sum(hs.plan_svd(N, M, a.p, 19)[k] for k in ("advice0", "advice1"))
+    for name, _ in variants:
+        med = statistics.median(res[name])
+        print(f"{name:12s} median {med:.4f} ms  min {min(res[name]):.4f}  -> {cells / med / 1e6:.2f} Gcells/s")
+        top = sorted(kern[name].items(), key=lambda kv: -statistics.median(kv[1]))[:8]
+        print("   " + "  ".join(f"{k}={statistics.median(vv):.3f}" for k, vv in top))
+    print(json.dumps({n: statistics.median(r) for n, r in res.items()}))
+
+
+if __name__ == "__main__":
+    main()
