@@ -12,8 +12,11 @@ GPU) every rank generates its own matrix (independent objects, no data-path
 collective): weak scaling, value = cells of all ranks / max-over-ranks time.
 
 Output: ONE JSON line on rank 0 (driver contract), including
-  roofline     dominant kernel, from HIP events the engine records on its own
-               stream during the timed steps (svdw_profile_*),
+  roofline     dominant kernel (k_stage, the cell-program stage kernel), from
+               HIP events the engine records around each of its launches on
+               its own stream during the timed steps (svdw_profile_*; only that
+               kernel is bracketed, so the clock sees two event packets per
+               stage launch and nothing else),
   cpu_baseline the single-threaded C oracle (oracle/svdw_oracle.c, a port of
                the reference algorithm) on a bounded row sample, rank 0 only.
 """
@@ -106,6 +109,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true",
                     help="skip the engine's event profiler in the timed region")
+    ap.add_argument("--profile-prefix", default="k_stage",
+                    help="kernel-name prefix the timed-region profiler records ('' = all)")
     ap.add_argument("--breakdown", action="store_true", help="print per-kernel ms/step to stderr")
     args = ap.parse_args()
     N = args.n
@@ -138,7 +143,7 @@ def main():
     ctx.sync()
 
     if not args.no_profile:
-        ctx.profile(True)
+        ctx.profile(True, args.profile_prefix)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -177,7 +182,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bn254_fr (u32 limbs; exact int8-digit dot4 GEMM)",
+            "dtype": "bn254_fr (u32 limbs; exact int8-digit MFMA GEMM)",
             "data": "synthetic (input-creator.py recipe, seeded; gamma = sha256 mod p)",
             "config": {
                 "workload": (f"svd_verify_witness N={N} M={M} PRECISION_BITS={args.p} "

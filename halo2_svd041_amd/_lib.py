@@ -110,6 +110,7 @@ SIGNATURES = {
     "svdw_set_gemm_impl": (_i32, [_P, _i32]),
     "svdw_set_option": (_i32, [_P, ct.c_char_p, ct.c_int64]),
     "svdw_profile_enable": (_i32, [_P, _i32]),
+    "svdw_profile_filter": (_i32, [_P, ct.c_char_p]),
     "svdw_profile_collect": (_i32, [_P, ct.POINTER(KStat), _u32, ct.POINTER(_u32)]),
     "svdw_plan_svd": (_i32, [_u32, _u32, _u32, _u32, ct.POINTER(SvdConfig), ct.POINTER(Counts)]),
 }

@@ -266,11 +266,19 @@ struct svdw_ctx {
     uint32_t P = 32, LB = 19;
     Stream ph[2];
     DBuf f64in, digA, digB, w1c, w1m, w2c, w2m, bits, gpc, gpm;
+    DBuf wbc[kMaxScanJobs], wbs[kMaxScanJobs];   // b.v per batched verify_mul (canonical, scaled)
     // gamma^j cache (canonical gpc / Montgomery gpm), shared by verify_mul calls
     Fr gp_gamma{};
     uint32_t gp_len = 0;
+    DBuf gps[9];                            // gamma powers * 2^(32 na), valid if gps_ok bit na
+    uint32_t gps_ok = 0;
+    // Known magnitude bounds of matrices written in this witness: cell (i, j) of
+    // `m` satisfies |signed value| < 2^bits. Cleared with the streams.
+    struct MatBits { svdw_mat m; uint32_t bits; };
+    std::vector<MatBits> mbits;
     // built-in event profiler (svdw_profile_*): one start/stop event pair per launch
     bool prof = false;
+    std::string prof_filter;                // record only kernels whose name starts with this
     struct Rec {
         std::string name;
         double bytes, ops;
@@ -280,7 +288,7 @@ struct svdw_ctx {
     std::vector<hipEvent_t> pool;
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
     uint32_t stage_flags = 0;               // STAGE_* (svdw_set_option "nt_stores", "stage_ilp")
-    int scan_impl = 1;                      // svdw_set_option "scan_impl"
+    int scan_impl = 4;                      // svdw_set_option "scan_impl"
     // second stream: GEMMs overlap the HBM-bound stages
     hipStream_t st2 = nullptr;
     bool overlap = true;
@@ -303,13 +311,35 @@ static void sync(svdw_ctx* c) {
 static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
     if (c->dep_next == c->deps.size()) {
         hipEvent_t e;
-        hipck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        // same-device consumer only: agent-scope release, no system-scope writeback
+        hipck(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice),
+              "hipEventCreate");
         c->deps.push_back(e);
     }
     hipEvent_t e = c->deps[c->dep_next++];
     hipck(hipEventRecord(e, from), "hipEventRecord");
     if (to) hipck(hipStreamWaitEvent(to, e, 0), "hipStreamWaitEvent");
     return e;
+}
+static bool same_cells(const svdw_mat& a, const svdw_mat& b) {
+    if (a.phase != b.phase || a.off != b.off) return false;
+    return (a.rows == b.rows && a.cols == b.cols && a.rs == b.rs && a.cs == b.cs) ||
+           (a.rows == b.cols && a.cols == b.rows && a.rs == b.cs && a.cs == b.rs);
+}
+static void reg_bits(svdw_ctx* c, const svdw_mat& m, uint32_t bits) {
+    if (bits == ~0u) return;
+    for (auto& r : c->mbits)
+        if (same_cells(r.m, m)) { r.bits = bits; return; }
+    c->mbits.push_back({m, bits});
+}
+static uint32_t bits_of(const svdw_ctx* c, const svdw_mat& m) {
+    for (auto& r : c->mbits)
+        if (same_cells(r.m, m)) return r.bits;
+    return ~0u;
+}
+static void clear_streams(svdw_ctx* c) {
+    for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
+    c->mbits.clear();
 }
 // RAII: brackets one kernel launch with HIP events on the context stream.
 struct ProfScope {
@@ -321,14 +351,18 @@ struct ProfScope {
             c->pool.pop_back();
             return e;
         }
+        // timing-only events: skip the system-scope fence (cache writeback and
+        // invalidate) a default event performs, which would perturb what it measures
         hipEvent_t e;
-        hipck(hipEventCreate(&e), "hipEventCreate");
+        hipck(hipEventCreateWithFlags(&e, hipEventDisableSystemFence), "hipEventCreate");
         return e;
     }
     hipStream_t s = nullptr;
     ProfScope(svdw_ctx* cc, hipStream_t ss, const std::string& name, double bytes, double ops)
         : c(cc), s(ss) {
         if (!c->prof || c->dry) return;
+        if (!c->prof_filter.empty() && name.compare(0, c->prof_filter.size(), c->prof_filter) != 0)
+            return;
         svdw_ctx::Rec r{name, bytes, ops, ev(c), ev(c)};
         hipck(hipEventRecord(r.e0, s), "hipEventRecord");
         c->recs.push_back(r);
@@ -408,13 +442,11 @@ static void check_vec(const svdw_ctx* c, const svdw_vec& v) { check_mat(c, mat_o
 
 // ------------------------------------------------------- stage launches
 // Appends the stage's cells for `nelem` elements; returns the advice offset.
-static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, uint32_t cols,
-                          const char* tag, uint64_t* loff_out = nullptr) {
+// Launch a stage whose cells were appended at (off, loff) earlier.
+static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, uint32_t cols,
+                         uint64_t off, uint64_t loff, const char* tag) {
     StageArgs& a = pb.a;
-    uint64_t off = 0, loff = 0;
-    append(c, phase, (uint64_t)nelem * a.C, (uint64_t)nelem * a.L, &off, &loff);
-    if (loff_out) *loff_out = loff;
-    if (c->dry || nelem == 0) return off;
+    if (c->dry || nelem == 0) return;
     a.out_adv = cellp(c, phase, off);
     a.out_lk = a.L ? c->ph[phase].lk + loff : nullptr;
     a.e_begin = 0;
@@ -432,6 +464,13 @@ static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, u
                      32.0 * nelem * ((double)a.C + a.L + loads), 0);
         hipck(launch_stage(a, c->st), "k_stage");
     }
+}
+static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, uint32_t cols,
+                          const char* tag, uint64_t* loff_out = nullptr) {
+    uint64_t off = 0, loff = 0;
+    append(c, phase, (uint64_t)nelem * pb.a.C, (uint64_t)nelem * pb.a.L, &off, &loff);
+    if (loff_out) *loff_out = loff;
+    stage_launch(c, phase, pb, nelem, cols, off, loff, tag);
     return off;
 }
 static svdw_vec put_cell(svdw_ctx* c, uint32_t phase, const Fr& v) {   // load_witness/load_constant
@@ -641,6 +680,14 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
     append(c, phase, (uint64_t)N * M, 0, &off, nullptr);
     svdw_mat cs{phase, N, M, off, (int64_t)M, 1};
     if (c->gemm_log) c->gemm_log->push_back(off);
+    if (bits_a == ~0u) bits_a = bits_of(c, a);
+    if (bits_b == ~0u) bits_b = bits_of(c, b);
+    auto reg_cs = [&] {   // |c_s| <= K * 2^bits_a * 2^bits_b
+        uint32_t lk = 0;
+        while ((1ull << lk) < a.cols) ++lk;
+        reg_bits(c, cs, bits_a + bits_b + lk);
+    };
+    if (bits_a != ~0u && bits_b != ~0u) reg_cs();
     if (c->dry) return cs;
     if (!c->pre.empty()) {
         if (c->pre.front().off != off) fail(SVDW_EDEVICE, "internal: pre-launched GEMM offset mismatch");
@@ -655,56 +702,100 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
         auto bb = maxbits_many(c, ms);
         bits_a = bb[0];
         bits_b = sym ? bb[0] : bb[1];
+        reg_bits(c, a, bits_a);
+        reg_bits(c, b, bits_b);
+        reg_cs();
     }
     gemm_exec(c, c->st, a, b, cellp(c, phase, off), bits_a, bits_b);
     return cs;
 }
-// field_mat_vec_mul with the vector given as canonical + Montgomery copies.
+// Words of the small operand for the row-scan products: |signed a| < 2^(32 na)
+// when a's bound is known (scan_impl 4 / 5), else 8 (full Montgomery product).
+static int scan_na(const svdw_ctx* c, const svdw_mat& a) {
+    if (c->scan_impl < 4) return 8;
+    const uint32_t b = bits_of(c, a);
+    if (b == ~0u || b > 192) return 8;
+    return std::max(1, (int)((b + 31) / 32));
+}
+// Factor f with mont_mul(w, f) = w * 2^(32 na) mod p (na = 8: Montgomery form).
+static Fr scale_factor(int na) {
+    if (na >= 8) return fr_r2();
+    Fr x = fr_zero();
+    x.w[na] = 1;                                          // 2^(32 na) < p for na <= 6
+    return mont_mul(x, fr_r2());
+}
+// field_mat_vec_mul with the vector given as canonical + scaled copies
+// (ws = w * 2^(32 na) mod p, see scan_na).
 static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const Fr* wc,
-                            const Fr* wm) {
+                            const Fr* wm, int na) {
     const uint32_t R = a.rows, L = a.cols;
     uint64_t off;
     append(c, phase, (uint64_t)R * (3ull * L + 1), 0, &off, nullptr);
     if (!c->dry) {
-        ProfScope ps(c, c->st, "k_matvec_scan", 32.0 * (double)R * (4.0 * L + 1) + 64.0 * L, (double)R * L);
+        ProfScope ps(c, c->st, a.cs == 1 ? "k_matvec_scan:rows" : "k_matvec_scan:cols", 32.0 * (double)R * (4.0 * L + 1) + 64.0 * L, (double)R * L);
         hipck(launch_matvec_scan(view_of(c, a), 0, R, L, wc, wm, cellp(c, phase, off), c->scan_impl,
-                                 c->st), "k_matvec_scan");
+                                 na, c->st), "k_matvec_scan");
     }
     return svdw_vec{phase, R, off + 3ull * L, (int64_t)(3ull * L + 1)};
 }
-static void vec_prep(svdw_ctx* c, const svdw_vec& v, DBuf& bc, DBuf& bm) {
+static void vec_prep(svdw_ctx* c, const svdw_vec& v, DBuf& bc, DBuf& bm, int na) {
     ensure_buf(c, bc, (size_t)v.len * sizeof(Fr));
     ensure_buf(c, bm, (size_t)v.len * sizeof(Fr));
     if (c->dry) return;
     hipck(launch_vec_prep(view_of(c, svdw_mat{v.phase, 1, v.len, v.off, 0, v.stride}), v.len,
-                          (Fr*)bc.p, (Fr*)bm.p, c->st), "k_vec_prep");
+                          (Fr*)bc.p, (Fr*)bm.p, scale_factor(na), c->st), "k_vec_prep");
 }
 static svdw_vec field_mat_vec_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a,
                                   const svdw_vec& v) {
     REQUIRE(a.cols == v.len, "field_mat_vec_mul: a[0].len() != v.len()");
-    vec_prep(c, v, c->w1c, c->w1m);
-    return matvec_rows(c, phase, a, (const Fr*)c->w1c.p, (const Fr*)c->w1m.p);
+    const int na = scan_na(c, a);
+    vec_prep(c, v, c->w1c, c->w1m, na);
+    return matvec_rows(c, phase, a, (const Fr*)c->w1c.p, (const Fr*)c->w1m.p, na);
 }
-// ZkMatrix::verify_mul
-static void verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svdw_mat& b,
+// gamma powers scaled for `na` (cached with the gamma vector)
+static const Fr* gamma_scaled(svdw_ctx* c, int na) {
+    if (na >= 8) return (const Fr*)c->gpm.p;
+    if (!c->dry && !(c->gps_ok >> na & 1)) {
+        ensure_buf(c, c->gps[na], (size_t)c->gp_len * sizeof(Fr));
+        DView w;
+        memset(&w, 0, sizeof w);
+        w.ptr = (const Fr*)c->gpc.p;
+        w.rs = 0; w.cs = 1; w.rows = 1; w.cols = c->gp_len;
+        hipck(launch_vec_prep(w, c->gp_len, nullptr, (Fr*)c->gps[na].p, scale_factor(na), c->st),
+              "k_vec_prep");
+        c->gps_ok |= 1u << na;
+    }
+    return (const Fr*)c->gps[na].p;
+}
+// ZkMatrix::verify_mul (src/matrix/mod.rs:251-282) for several (a, b, c_s) triples
+// with one gamma: cells are appended exactly as consecutive verify_mul calls
+// would append them, then the row scans run as three batched launches (all
+// c_s.v scans, all b.v scans, all a.(b.v) scans) so the rows of every call
+// share one wave of blocks.
+struct VMul {
+    svdw_mat a, b, cs;
+};
+static void ensure_gamma_vec(svdw_ctx* c, uint32_t d, const Fr& gamma) {
+    // v = (1, g, g^2, ...) canonical + Montgomery, cached per (gamma, length)
+    if (c->dry || (c->gp_len >= d && fr_eq(c->gp_gamma, gamma))) return;
+    const uint32_t len = std::max(d, c->gp_len);
+    ensure_buf(c, c->gpc, (size_t)len * sizeof(Fr));
+    ensure_buf(c, c->gpm, (size_t)len * sizeof(Fr));
+    ProfScope ps(c, c->st, "k_gamma_vec", 64.0 * len, 0);
+    hipck(launch_gamma_vec(gamma, len, (Fr*)c->gpc.p, (Fr*)c->gpm.p, c->st), "k_gamma_vec");
+    c->gp_len = len;
+    c->gp_gamma = gamma;
+    c->gps_ok = 0;
+}
+// ZkMatrix::verify_mul, one call at a time (scan_impl 1 / 2)
+static void verify_mul_legacy(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svdw_mat& b,
                        const svdw_mat& cs, const Fr& gamma) {
     REQUIRE(a.cols == b.rows, "verify_mul: a.num_col != b.num_rows");
     REQUIRE(cs.rows == a.rows, "verify_mul: c_s.len() != a.num_rows");
     REQUIRE(cs.cols == b.cols, "verify_mul: c_s[0].len() != b.num_col");
     const uint32_t d = cs.cols, n = a.rows, k = a.cols;
-    // v = (1, g, g^2, ...): canonical + Montgomery copies for the row scans,
-    // computed once per (gamma, length) and reused by later verify_mul calls
-    if (!c->dry && (c->gp_len < d || !fr_eq(c->gp_gamma, gamma))) {
-        const uint32_t len = std::max(d, c->gp_len);
-        ensure_buf(c, c->gpc, (size_t)len * sizeof(Fr));
-        ensure_buf(c, c->gpm, (size_t)len * sizeof(Fr));
-        ProfScope ps(c, c->st, "k_gamma_vec", 64.0 * len, 0);
-        hipck(launch_gamma_vec(gamma, len, (Fr*)c->gpc.p, (Fr*)c->gpm.p, c->st), "k_gamma_vec");
-        c->gp_len = len;
-        c->gp_gamma = gamma;
-    }
+    ensure_gamma_vec(c, d, gamma);
     const Fr* gpc = (const Fr*)c->gpc.p;
-    const Fr* gpm = (const Fr*)c->gpm.p;
     put_cell(c, phase, fr_from_u64(1));                    // load_witness(F::ONE)
     if (d > 1) {                                          // v_i = mul(v_{i-1}, init_rand)
         PB pb(c->LB);
@@ -719,10 +810,11 @@ static void verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svd
         pb.cell(pb.K(0)); pb.cell(prev); pb.cell(pb.K(gamma)); pb.cell(cur);
         run_stage(c, phase, pb, d - 1, 1, "verify_mul_gamma_pows");
     }
-    svdw_vec csv = matvec_rows(c, phase, cs, gpc, gpm);
-    svdw_vec bv = matvec_rows(c, phase, b, gpc, gpm);
-    vec_prep(c, bv, c->w2c, c->w2m);
-    svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, (const Fr*)c->w2m.p);
+    const int na_cs = scan_na(c, cs), na_b = scan_na(c, b), na_a = scan_na(c, a);
+    svdw_vec csv = matvec_rows(c, phase, cs, gpc, gamma_scaled(c, na_cs), na_cs);
+    svdw_vec bv = matvec_rows(c, phase, b, gpc, gamma_scaled(c, na_b), na_b);
+    vec_prep(c, bv, c->w2c, c->w2m, na_a);
+    svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, (const Fr*)c->w2m.p, na_a);
     (void)k;
     PB pb(c->LB);                                         // is_equal per row (unconstrained result)
     pb.a.view[0] = view_of(c, mat_of_vec(csv));
@@ -730,6 +822,120 @@ static void verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svd
     uint8_t x = pb.load(0), y = pb.load(1);
     pb.g_is_equal(x, y);
     run_stage(c, phase, pb, n, 1, "verify_mul_is_equal");
+}
+
+static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, const Fr& gamma) {
+    REQUIRE(n >= 1 && n <= kMaxScanJobs, "internal: verify_mul batch size");
+    struct Plan {
+        PB one, pows, eq;
+        uint64_t one_off = 0, one_loff = 0, pows_off = 0, pows_loff = 0, eq_off = 0, eq_loff = 0;
+        svdw_vec csv{}, bv{}, abv{};
+        explicit Plan(uint32_t lb) : one(lb), pows(lb), eq(lb) {}
+    };
+    std::vector<Plan> pl;
+    pl.reserve(n);
+    uint32_t dmax = 0;
+    auto scan_append = [&](const svdw_mat& a) {
+        uint64_t off;
+        append(c, phase, (uint64_t)a.rows * (3ull * a.cols + 1), 0, &off, nullptr);
+        return svdw_vec{phase, a.rows, off + 3ull * a.cols, (int64_t)(3ull * a.cols + 1)};
+    };
+    // pass 1: the cell layout, in the reference's order
+    for (int i = 0; i < n; ++i) {
+        const svdw_mat &a = vm[i].a, &b = vm[i].b, &cs = vm[i].cs;
+        REQUIRE(a.cols == b.rows, "verify_mul: a.num_col != b.num_rows");
+        REQUIRE(cs.rows == a.rows, "verify_mul: c_s.len() != a.num_rows");
+        REQUIRE(cs.cols == b.cols, "verify_mul: c_s[0].len() != b.num_col");
+        const uint32_t d = cs.cols;
+        dmax = std::max(dmax, d);
+        pl.emplace_back(c->LB);
+        Plan& p = pl.back();
+        p.one.cell(p.one.K(fr_from_u64(1)));                  // load_witness(F::ONE)
+        append(c, phase, p.one.a.C, 0, &p.one_off, &p.one_loff);
+        if (d > 1) {                                          // v_i = mul(v_{i-1}, init_rand)
+            uint8_t prev = p.pows.load(0), cur = p.pows.load(1);
+            p.pows.cell(p.pows.K(0)); p.pows.cell(prev); p.pows.cell(p.pows.K(gamma)); p.pows.cell(cur);
+            append(c, phase, (uint64_t)(d - 1) * p.pows.a.C, 0, &p.pows_off, &p.pows_loff);
+        }
+        p.csv = scan_append(cs);
+        p.bv = scan_append(b);
+        p.abv = scan_append(a);
+        uint8_t x = p.eq.load(0), y = p.eq.load(1);           // is_equal per row (result unused)
+        p.eq.g_is_equal(x, y);
+        append(c, phase, (uint64_t)a.rows * p.eq.a.C, (uint64_t)a.rows * p.eq.a.L, &p.eq_off,
+               &p.eq_loff);
+    }
+    if (c->dry) return;
+    // pass 2: launches
+    ensure_gamma_vec(c, dmax, gamma);
+    const Fr* gpc = (const Fr*)c->gpc.p;
+    for (int i = 0; i < n; ++i) {
+        Plan& p = pl[i];
+        const uint32_t d = vm[i].cs.cols;
+        stage_launch(c, phase, p.one, 1, 1, p.one_off, p.one_loff, "load_cell");
+        if (d > 1) {
+            DView w;
+            memset(&w, 0, sizeof w);
+            w.ptr = gpc;
+            w.rs = 1; w.cs = 0; w.rows = d; w.cols = 1;
+            p.pows.a.view[0] = w;
+            p.pows.a.view[1] = w;
+            p.pows.a.view[1].ptr = gpc + 1;
+            stage_launch(c, phase, p.pows, d - 1, 1, p.pows_off, p.pows_loff, "verify_mul_gamma_pows");
+        }
+    }
+    auto run_batch = [&](const char* name, auto mat_of, auto vec_of, auto wc_of, auto ws_of, int na) {
+        ScanBatch sb;
+        memset(&sb, 0, sizeof sb);
+        double bytes = 0, ops = 0;
+        for (int i = 0; i < n; ++i) {
+            const svdw_mat a = mat_of(i);
+            const svdw_vec v = vec_of(i);
+            sb.job[i] = ScanJob{view_of(c, a), wc_of(i), ws_of(i),
+                                cellp(c, phase, v.off - 3ull * a.cols), a.cols, a.rows, 0, 0};
+            bytes += 32.0 * a.rows * (4.0 * a.cols + 1) + 64.0 * a.cols;
+            ops += (double)a.rows * a.cols;
+        }
+        sb.njobs = n;
+        const int T = c->scan_impl == 5 ? 4 : c->scan_impl == 3 ? 1 : 2;
+        ProfScope ps(c, c->st, name, bytes, ops);
+        hipck(launch_scan_batch(sb, T, T == 1 ? 8 : na, c->st), "k_matvec_scan");
+    };
+    auto group_na = [&](auto mat_of) {
+        int na = 1;
+        for (int i = 0; i < n; ++i) na = std::max(na, scan_na(c, mat_of(i)));
+        return c->scan_impl == 3 ? 8 : na;
+    };
+    auto cs_of = [&](int i) { return vm[i].cs; };
+    auto b_of = [&](int i) { return vm[i].b; };
+    auto a_of = [&](int i) { return vm[i].a; };
+    const int na_cs = group_na(cs_of), na_b = group_na(b_of), na_a = group_na(a_of);
+    const Fr* g_cs = gamma_scaled(c, na_cs);
+    const Fr* g_b = gamma_scaled(c, na_b);
+    auto gc = [&](int) { return gpc; };
+    run_batch("k_matvec_scan:cs", cs_of, [&](int i) { return pl[i].csv; }, gc,
+              [&](int) { return g_cs; }, na_cs);
+    run_batch("k_matvec_scan:b", b_of, [&](int i) { return pl[i].bv; }, gc,
+              [&](int) { return g_b; }, na_b);
+    for (int i = 0; i < n; ++i) vec_prep(c, pl[i].bv, c->wbc[i], c->wbs[i], na_a);
+    run_batch("k_matvec_scan:a", a_of, [&](int i) { return pl[i].abv; },
+              [&](int i) { return (const Fr*)c->wbc[i].p; },
+              [&](int i) { return (const Fr*)c->wbs[i].p; }, na_a);
+    for (int i = 0; i < n; ++i) {
+        Plan& p = pl[i];
+        p.eq.a.view[0] = view_of(c, mat_of_vec(p.csv));
+        p.eq.a.view[1] = view_of(c, mat_of_vec(p.abv));
+        stage_launch(c, phase, p.eq, vm[i].a.rows, 1, p.eq_off, p.eq_loff, "verify_mul_is_equal");
+    }
+}
+static void verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svdw_mat& b,
+                       const svdw_mat& cs, const Fr& gamma) {
+    if (c->scan_impl < 3) {                       // legacy per-call path (A/B only)
+        verify_mul_legacy(c, phase, a, b, cs, gamma);
+        return;
+    }
+    VMul v{a, b, cs};
+    verify_mul_many(c, phase, &v, 1, gamma);
 }
 
 // err_calc (src/svd/mod.rs:155-163). Host f64, built with -ffp-contract=off.
@@ -818,9 +1024,15 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
 }
 static void check_svd_phase1(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u, const svdw_mat& v,
                              const svdw_svd_payload& pl, const Fr& g) {
-    verify_mul(c, 1, m, pl.v_t, pl.m_times_vt, g);
-    verify_mul(c, 1, u, pl.u_t, pl.u_times_ut, g);
-    verify_mul(c, 1, v, pl.v_t, pl.v_times_vt, g);
+    if (c->scan_impl < 3) {
+        verify_mul(c, 1, m, pl.v_t, pl.m_times_vt, g);
+        verify_mul(c, 1, u, pl.u_t, pl.u_times_ut, g);
+        verify_mul(c, 1, v, pl.v_t, pl.v_times_vt, g);
+        return;
+    }
+    const VMul vm[3] = {{m, pl.v_t, pl.m_times_vt}, {u, pl.u_t, pl.u_times_ut},
+                        {v, pl.v_t, pl.v_times_vt}};
+    verify_mul_many(c, 1, vm, 3, g);
 }
 
 static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, const double* v,
@@ -828,7 +1040,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
                                const svdw_svd_config& cfg, const Fr& gamma) {
     REQUIRE(N >= 1 && M >= 1, "empty matrix");
     const uint32_t r = std::min(N, M);
-    for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
+    clear_streams(c);
     c->dep_next = 0;
     c->pre.clear();
     if (!c->dry) {
@@ -860,6 +1072,9 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         hipck(hipMemcpyAsync(hb, dbits, sizeof hb, hipMemcpyDeviceToHost, c->st), "D2H");
         hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
         for (int i = 0; i < 3; ++i) bits[i] = hb[i];
+        reg_bits(c, zm, bits[0]);
+        reg_bits(c, zu, bits[1]);
+        reg_bits(c, zv, bits[2]);
     }
     svdw_svd_payload pl = check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, bits.data());
     check_svd_phase1(c, zm, zu, zv, pl, gamma);
@@ -922,7 +1137,7 @@ int svdw_ctx_reset(svdw_ctx* c) {
     return guarded([&] {
         REQUIRE(c, "null ctx");
         sync(c);
-        for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
+        clear_streams(c);
         c->pre.clear();
     });
 }
@@ -1120,7 +1335,7 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->stage_flags = (c->stage_flags & ~(STAGE_ILP2 | STAGE_ILP4)) |
                              (value == 2 ? STAGE_ILP2 : value == 4 ? STAGE_ILP4 : 0);
         } else if (n == "scan_impl") {
-            REQUIRE(value == 1 || value == 2, "scan_impl: 1 or 2");
+            REQUIRE(value >= 1 && value <= 5, "scan_impl: 1..5");
             c->scan_impl = (int)value;
         } else if (n == "overlap") {
             c->overlap = value != 0;
@@ -1144,6 +1359,12 @@ int svdw_profile_enable(svdw_ctx* c, int on) {
         for (auto& r : c->recs) { c->pool.push_back(r.e0); c->pool.push_back(r.e1); }
         c->recs.clear();
         c->prof = on != 0;
+    });
+}
+int svdw_profile_filter(svdw_ctx* c, const char* prefix) {
+    return guarded([&] {
+        REQUIRE(c, "null ctx");
+        c->prof_filter = prefix ? prefix : "";
     });
 }
 int svdw_profile_collect(svdw_ctx* c, svdw_kstat* out, uint32_t cap, uint32_t* n) {

@@ -154,6 +154,64 @@ SVDW_HD Fr mont_mul(const Fr& a, const Fr& b) {
     for (int i = 0; i < 8; ++i) r.w[i] = use_s ? s.w[i] : r.w[i];
     return r;
 }
+// a * b * 2^(-32 NA) mod p for a < 2^(32 NA) (words >= NA of `a` ignored):
+// CIOS with NA outer rounds, one per word of the small operand. Output < p.
+template <int NA>
+SVDW_HD Fr mont_mul_small(const Fr& a, const Fr& b) {
+    uint32_t t[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) t[i] = 0;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            c += (uint64_t)b.w[j] * a.w[i] + t[j];
+            t[j] = (uint32_t)c;
+            c >>= 32;
+        }
+        c += t[8];
+        t[8] = (uint32_t)c;
+        t[9] = (uint32_t)(c >> 32);
+        uint32_t m = t[0] * kPinv32;
+        c = (uint64_t)m * p_word(0) + t[0];
+        c >>= 32;
+#pragma unroll
+        for (int j = 1; j < 8; ++j) {
+            c += (uint64_t)m * p_word(j) + t[j];
+            t[j - 1] = (uint32_t)c;
+            c >>= 32;
+        }
+        c += t[8];
+        t[7] = (uint32_t)c;
+        t[8] = t[9] + (uint32_t)(c >> 32);
+    }
+    Fr r, s;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = t[i];
+    uint32_t br = sub256(s, r, fr_p());
+    bool use_s = t[8] | (br ^ 1u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = use_s ? s.w[i] : r.w[i];
+    return r;
+}
+// a * b mod p for a canonical `a` whose signed value (a or a - p) has magnitude
+// < 2^(32 NA), with bs = b * 2^(32 NA) mod p.
+template <int NA>
+SVDW_HD Fr fr_mul_small_signed(const Fr& a, const Fr& bs) {
+    Fr n, d;
+    sub256(n, fr_p(), a);                       // p - a
+    const uint32_t neg = sub256(d, n, a);       // p - a < a: a is negative
+    Fr mag;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mag.w[i] = neg ? n.w[i] : a.w[i];
+    const Fr r = mont_mul_small<NA>(mag, bs);
+    const Fr nr = fr_neg(r);
+    Fr o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o.w[i] = neg ? nr.w[i] : r.w[i];
+    return o;
+}
 SVDW_HD Fr fr_to_mont(const Fr& a) { return mont_mul(a, fr_r2()); }
 SVDW_HD Fr fr_from_mont(const Fr& a) { return mont_mul(a, fr_from_u64(1)); }
 // Canonical product.

@@ -11,6 +11,7 @@
 //  k_matvec_scan   field_mat_vec_mul rows (src/matrix/mod.rs:574-599): every
 //                  prefix sum of the row inner product is a cell -> block Fr scan
 #include <hip/hip_runtime.h>
+#include <string.h>
 
 #include "kernels.hpp"
 
@@ -761,17 +762,17 @@ hipError_t launch_gemm_mont(const DView& A, const DView& B, uint32_t N, uint32_t
 }
 
 // ------------------------------------------------------------ vectors
-__global__ void k_vec_prep(const DView w, uint32_t L, Fr* wc, Fr* wm) {
+__global__ void k_vec_prep(const DView w, uint32_t L, Fr* wc, Fr* ws, const Fr f) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= L) return;
     Fr zero = fr_zero();
     Fr v = view_load(w, zero, 0, j);
-    st_fr(wc + j, v);
-    st_fr(wm + j, fr_to_mont(v));
+    if (wc) st_fr(wc + j, v);
+    st_fr(ws + j, mont_mul(v, f));
 }
-hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* wc, Fr* wm, hipStream_t st) {
+hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* wc, Fr* ws, const Fr& f, hipStream_t st) {
     if (!L) return hipSuccess;
-    hipLaunchKernelGGL(k_vec_prep, dim3((L + 255) / 256), dim3(256), 0, st, w, L, wc, wm);
+    hipLaunchKernelGGL(k_vec_prep, dim3((L + 255) / 256), dim3(256), 0, st, w, L, wc, ws, f);
     return hipGetLastError();
 }
 __global__ void k_gamma_vec(const Fr g, uint32_t L, int nbits, Fr* wc, Fr* wm) {
@@ -801,6 +802,117 @@ __device__ __forceinline__ Fr shfl_up_fr(const Fr& v, int d) {
     return r;
 }
 
+// Row handled by block b of a row scan. Blocks are dealt round-robin to the 8
+// XCDs (b % 8); give each XCD a contiguous run of rows so that a column-strided
+// view (row r of a transposed matrix = column r) finds its neighbours' 128 B
+// lines in the same L2 instead of every XCD fetching them separately.
+__device__ __forceinline__ uint32_t scan_row(uint32_t b, uint32_t nb) {
+    return (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);
+}
+
+// Inclusive wave64 scan of Fr values with DPP lane moves (GFX9 row_shr 1/2/4/8
+// inside 16-lane rows, then row_bcast:15 / row_bcast:31 across rows); lanes
+// without a source receive 0 (bound_ctrl / row_mask), and adding 0 is a no-op.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ Fr dpp_fr(const Fr& v) {
+    Fr r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        r.w[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.w[i], CTRL, ROW_MASK, 0xf, true);
+    return r;
+}
+__device__ __forceinline__ Fr wave_scan_fr(Fr s) {
+    s = fr_add(s, dpp_fr<0x111, 0xf>(s));   // row_shr:1
+    s = fr_add(s, dpp_fr<0x112, 0xf>(s));   // row_shr:2
+    s = fr_add(s, dpp_fr<0x114, 0xf>(s));   // row_shr:4
+    s = fr_add(s, dpp_fr<0x118, 0xf>(s));   // row_shr:8
+    s = fr_add(s, dpp_fr<0x142, 0xa>(s));   // row_bcast:15 -> rows 1, 3
+    s = fr_add(s, dpp_fr<0x143, 0xc>(s));   // row_bcast:31 -> rows 2, 3
+    return s;
+}
+
+// T terms per thread, DPP scan. The cells go through a 24 KB LDS stage (768
+// cells) in T rounds -- round q stages the 3T cells of threads [q*256/T,
+// (q+1)*256/T) and the whole block writes them as coalesced 16 B half-cells --
+// so four blocks fit a CU and N = 1024 rows run as one wave of blocks.
+// NA < 8: |signed a| < 2^(32 NA) and wm = w * 2^(32 NA) (fr_mul_small_signed);
+// NA = 8: wm is Montgomery form (any field elements).
+// One launch serves up to kMaxScanJobs independent scans (blocks [blk0, blk0 + rows)
+// of the grid belong to job q), so the scans of several verify_mul calls share
+// one wave of blocks.
+template <int T, int NA>
+__global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
+    static_assert(256 % T == 0, "T divides the block");
+    constexpr uint32_t TPR = 256 / T;                     // threads staged per round
+    __shared__ __attribute__((aligned(16))) uint32_t stage[3 * 256 * 8];
+    __shared__ Fr wtot[4];
+    ScanJob J = B.job[0];
+#pragma unroll
+    for (int q = 1; q < kMaxScanJobs; ++q)
+        if ((uint32_t)q < B.njobs && blockIdx.x >= B.job[q].blk0) J = B.job[q];
+    const DView& A = J.A;
+    const uint32_t L = J.L;
+    const Fr* __restrict__ wc = J.wc;
+    const Fr* __restrict__ wm = J.ws;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t lb = blockIdx.x - J.blk0;
+    const uint32_t rb = (J.blk0 & 7) ? lb : scan_row(lb, J.rows), r = J.r_begin + rb;
+    Fr* rowout = J.out + (uint64_t)rb * (3ull * L + 1);
+    const Fr zero = fr_zero();
+    if (tid == 0) st_fr(rowout, zero);
+    Fr carry = fr_zero();
+    for (uint32_t c0 = 0; c0 < L; c0 += 256 * T) {
+        const uint32_t j0 = c0 + tid * T;
+        Fr a[T], s[T];
+#pragma unroll
+        for (int i = 0; i < T; ++i) {
+            const uint32_t j = j0 + i;
+            a[i] = j < L ? view_load(A, zero, r, j) : zero;
+            if constexpr (NA == 8)
+                s[i] = j < L ? mont_mul(a[i], ld_fr(wm + j)) : zero;
+            else
+                s[i] = j < L ? fr_mul_small_signed<NA>(a[i], ld_fr(wm + j)) : zero;
+        }
+#pragma unroll
+        for (int i = 1; i < T; ++i) s[i] = fr_add(s[i], s[i - 1]);
+        const Fr tot = wave_scan_fr(s[T - 1]);
+        if (lane == 63) wtot[wave] = tot;
+        __syncthreads();
+        Fr pre = fr_add(fr_sub(tot, s[T - 1]), carry);
+        for (uint32_t w2 = 0; w2 < wave; ++w2) pre = fr_add(pre, wtot[w2]);
+        Fr ctot = carry;
+#pragma unroll
+        for (int w2 = 0; w2 < 4; ++w2) ctot = fr_add(ctot, wtot[w2]);
+#pragma unroll
+        for (int q = 0; q < T; ++q) {
+            const uint32_t t0 = c0 + q * 256;                 // first term of this round
+            if (t0 >= L) break;
+            if (tid / TPR == (uint32_t)q) {
+#pragma unroll
+                for (int i = 0; i < T; ++i) {
+                    const uint32_t j = j0 + i;
+                    const Fr w = j < L ? ld_fr(wc + j) : zero;
+                    const Fr si = fr_add(s[i], pre);
+                    uint4* st3 = reinterpret_cast<uint4*>(stage + ((tid % TPR) * T + i) * 24);
+                    st3[0] = make_uint4(a[i].w[0], a[i].w[1], a[i].w[2], a[i].w[3]);
+                    st3[1] = make_uint4(a[i].w[4], a[i].w[5], a[i].w[6], a[i].w[7]);
+                    st3[2] = make_uint4(w.w[0], w.w[1], w.w[2], w.w[3]);
+                    st3[3] = make_uint4(w.w[4], w.w[5], w.w[6], w.w[7]);
+                    st3[4] = make_uint4(si.w[0], si.w[1], si.w[2], si.w[3]);
+                    st3[5] = make_uint4(si.w[4], si.w[5], si.w[6], si.w[7]);
+                }
+            }
+            __syncthreads();
+            const uint32_t ncell = 3 * min(256u, L - t0);
+            uint4* o = reinterpret_cast<uint4*>(rowout + 1 + 3ull * t0);
+            const uint4* sv = reinterpret_cast<const uint4*>(stage);
+            for (uint32_t hc = tid; hc < 2 * ncell; hc += 256) o[hc] = sv[hc];
+            __syncthreads();
+        }
+        carry = ctot;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_matvec_scan_v1(const DView A, uint32_t r_begin, uint32_t L,
                                                      const Fr* __restrict__ wc,
                                                      const Fr* __restrict__ wm,
@@ -808,8 +920,8 @@ __global__ __launch_bounds__(256) void k_matvec_scan_v1(const DView A, uint32_t 
     __shared__ uint32_t stage[3 * 256 * 8];
     __shared__ Fr wtot[4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t r = r_begin + blockIdx.x;
-    Fr* rowout = out + (uint64_t)blockIdx.x * (3ull * L + 1);
+    const uint32_t rb = scan_row(blockIdx.x, gridDim.x), r = r_begin + rb;
+    Fr* rowout = out + (uint64_t)rb * (3ull * L + 1);
     Fr zero = fr_zero();
     if (tid == 0) st_fr(rowout, zero);
     Fr carry = fr_zero();
@@ -864,8 +976,8 @@ __global__ __launch_bounds__(256) void k_matvec_scan(const DView A, uint32_t r_b
     constexpr int T = 4;
     __shared__ Fr wtot[4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t r = r_begin + blockIdx.x;
-    Fr* rowout = out + (uint64_t)blockIdx.x * (3ull * L + 1);
+    const uint32_t rb = scan_row(blockIdx.x, gridDim.x), r = r_begin + rb;
+    Fr* rowout = out + (uint64_t)rb * (3ull * L + 1);
     const Fr zero = fr_zero();
     if (tid == 0) st_fr(rowout, zero);
     Fr carry = fr_zero();
@@ -911,13 +1023,50 @@ __global__ __launch_bounds__(256) void k_matvec_scan(const DView A, uint32_t r_b
     }
 }
 
+template <int T>
+static void launch_scan_t(const ScanBatch& b, int na, dim3 g, hipStream_t st) {
+    const dim3 blk(256);
+    switch (na) {
+    case 1: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 1>), g, blk, 0, st, b); break;
+    case 2: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 2>), g, blk, 0, st, b); break;
+    case 3: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 3>), g, blk, 0, st, b); break;
+    case 4: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 4>), g, blk, 0, st, b); break;
+    case 5: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 5>), g, blk, 0, st, b); break;
+    case 6: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 6>), g, blk, 0, st, b); break;
+    default: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 8>), g, blk, 0, st, b); break;
+    }
+}
+hipError_t launch_scan_batch(const ScanBatch& b0, int T, int na, hipStream_t st) {
+    ScanBatch b = b0;
+    uint32_t blocks = 0;
+    for (uint32_t q = 0; q < b.njobs; ++q) {
+        b.job[q].blk0 = blocks;
+        blocks += b.job[q].L ? b.job[q].rows : 0;
+        if (!b.job[q].L) b.job[q].rows = 0;
+    }
+    if (!blocks) return hipSuccess;
+    if (T == 1) {
+        hipLaunchKernelGGL((k_matvec_scan_dpp<1, 8>), dim3(blocks), dim3(256), 0, st, b);
+    } else if (T == 2) {
+        launch_scan_t<2>(b, na, dim3(blocks), st);
+    } else {
+        launch_scan_t<4>(b, na, dim3(blocks), st);
+    }
+    return hipGetLastError();
+}
 hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
-                              const Fr* wc, const Fr* wm, Fr* out, int impl, hipStream_t st) {
+                              const Fr* wc, const Fr* wm, Fr* out, int impl, int na, hipStream_t st) {
     if (r_end <= r_begin || !L) return hipSuccess;
     if (impl == 1)
         hipLaunchKernelGGL(k_matvec_scan_v1, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L,
                            wc, wm, out);
-    else
+    else if (impl >= 3 && impl <= 5) {
+        ScanBatch b;
+        memset(&b, 0, sizeof b);
+        b.njobs = 1;
+        b.job[0] = ScanJob{A, wc, wm, out, L, r_end - r_begin, 0, r_begin};
+        return launch_scan_batch(b, impl == 3 ? 1 : impl == 4 ? 2 : 4, impl == 3 ? 8 : na, st);
+    } else
         hipLaunchKernelGGL(k_matvec_scan, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L, wc,
                            wm, out);
     return hipGetLastError();

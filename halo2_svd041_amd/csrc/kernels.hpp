@@ -8,6 +8,22 @@
 
 namespace svdw {
 
+// One row scan of a batched launch: rows [r_begin, r_begin + rows) of A (L
+// columns) against w, row i's 3L+1 cells at out + i*(3L+1). blk0 is set by
+// launch_scan_batch.
+struct ScanJob {
+    DView A;
+    const Fr* wc;
+    const Fr* ws;
+    Fr* out;
+    uint32_t L, rows, blk0, r_begin;
+};
+static constexpr int kMaxScanJobs = 4;
+struct ScanBatch {
+    ScanJob job[kMaxScanJobs];
+    uint32_t njobs;
+};
+
 // Elements per block of the generic stage kernel (= block size; LDS: E * nv * 32 B).
 static constexpr int kStageElems = 256;
 
@@ -39,14 +55,23 @@ hipError_t launch_gemm_mfma(int DA, int DB, bool sym, const uint8_t* Ad, const u
 // Generic Montgomery GEMM (any field elements): out = A(NxK) * B(KxM).
 hipError_t launch_gemm_mont(const DView& A, const DView& B, uint32_t N, uint32_t K, uint32_t M,
                             Fr* out, int64_t ors, int64_t ocs, hipStream_t st);
-// w vector (len L) from a view (row 0 / col j of a 1 x L view) -> canonical + Montgomery copies.
-hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* w_mont, hipStream_t st);
+// w vector (len L) from a view (row 0 / col j of a 1 x L view) -> canonical copy
+// (w_canon nullable) and w_scaled = mont_mul(w, f) (f = R^2: Montgomery form).
+hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* w_scaled, const Fr& f,
+                           hipStream_t st);
 // w_j = gamma^j, j < L.
 hipError_t launch_gamma_vec(const Fr& gamma, uint32_t L, Fr* w_canon, Fr* w_mont, hipStream_t st);
 // Freivalds inner-product rows (GateChip::inner_product, 1+3L cells per row) for
 // rows [r_begin, r_end) of A (R x L); row r's cells at out + (r - r_begin)*(3L+1).
-// impl 1: one term per thread, LDS-staged coalesced stores; 2: four terms per thread.
+// impl 1: one term per thread, shuffle scan, LDS-staged coalesced stores; 2: four
+// terms per thread, direct stores; 3: DPP scan; 4 / 5: DPP scan, two / four terms per
+// thread and small-operand products when na < 8 (|signed A| < 2^(32 na), w_scaled =
+// w * 2^(32 na)); impls 1-3 and na = 8 take w_scaled in Montgomery form.
 hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
-                              const Fr* w_canon, const Fr* w_mont, Fr* out, int impl, hipStream_t st);
+                              const Fr* w_canon, const Fr* w_scaled, Fr* out, int impl, int na,
+                              hipStream_t st);
+// Up to kMaxScanJobs DPP row scans in one launch (T terms per thread: 1, 2, 4;
+// na as above, shared by every job: each job's w_scaled = w * 2^(32 na)).
+hipError_t launch_scan_batch(const ScanBatch& b, int T, int na, hipStream_t st);
 
 }  // namespace svdw

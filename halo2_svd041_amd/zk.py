@@ -127,8 +127,9 @@ class Context:
         """Tuning knobs (include/svdw.h): gemm_impl, nt_stores, stage_ilp, scan_impl, overlap."""
         check(lib().svdw_set_option(self._h, name.encode(), int(value)))
 
-    def profile(self, on: bool = True) -> None:
-        """Record HIP events around every kernel launch on this context's stream."""
+    def profile(self, on: bool = True, prefix: str = "") -> None:
+        """Record HIP events around kernel launches (names starting with `prefix`)."""
+        check(lib().svdw_profile_filter(self._h, prefix.encode()))
         check(lib().svdw_profile_enable(self._h, 1 if on else 0))
 
     def profile_collect(self) -> list:

@@ -167,8 +167,11 @@ int svdw_svd_witness(svdw_ctx* ctx, const double* m, const double* u, const doub
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
 /* Tuning knobs (bit-identical results for every value):
  *   "gemm_impl" 0 | 1, "nt_stores" 0 | 1 (non-temporal cell stores),
- *   "stage_ilp" 1 | 2 | 4 (half-cells in flight per thread), "scan_impl" 1 | 2
- *   (row-scan kernel variant), "overlap" 0 | 1 (GEMMs ahead on a second stream). */
+ *   "stage_ilp" 1 | 2 | 4 (half-cells in flight per thread), "scan_impl" 1..5
+ *   (row-scan kernel variant: 1 shuffle scan, 2 four terms/thread direct stores,
+ *   3 DPP scan, 4 (default) / 5 DPP scan with two / four terms per thread and
+ *   small-operand products where bounds are known), "overlap" 0 | 1 (GEMMs ahead on a
+ *   second stream). */
 int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);
 
 /* ----------------------------------------------------------- profiling */
@@ -183,6 +186,9 @@ typedef struct {
 } svdw_kstat;
 /* Enable (1) / disable (0) event recording; drops pending records. */
 int svdw_profile_enable(svdw_ctx* ctx, int on);
+/* Record only launches whose kernel name starts with `prefix` ("" / NULL = all):
+ * each recorded launch adds two event packets to the stream. */
+int svdw_profile_filter(svdw_ctx* ctx, const char* prefix);
 /* Synchronize, aggregate pending records by kernel name (up to cap entries
  * written to out; *n = number of distinct names) and drop them. */
 int svdw_profile_collect(svdw_ctx* ctx, svdw_kstat* out, uint32_t cap, uint32_t* n);

@@ -159,7 +159,8 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
 
 
 @pytest.mark.parametrize("opts", [{"stage_ilp": 2}, {"stage_ilp": 4}, {"nt_stores": 1},
-                                  {"scan_impl": 2}, {"overlap": 0}])
+                                  {"scan_impl": 2}, {"scan_impl": 3}, {"scan_impl": 1}, {"scan_impl": 5},
+                                  {"overlap": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
@@ -172,3 +173,33 @@ def test_tuning_options_parity(gpu_ctx_factory, opts):
     hs.svd_witness(ctx, m, u, v, d, g)
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
     _assert_streams(ctx, a0, l0, a1)
+
+
+@pytest.mark.parametrize("impl", [4, 1])
+def test_modular_verify_mul_parity(gpu_ctx_factory, impl):
+    """ZkMatrix::verify_mul through the ABI, twice (honest and wrong c_s), vs the
+    Python restatement of src/matrix/mod.rs:299-342 on the same quantized cells."""
+    import halo2_svd041_amd as hs
+    import pyoracle as po
+    rs = np.random.RandomState(21)
+    P = 42
+    A = rs.uniform(-3, 3, (5, 7))
+    B = rs.uniform(-3, 3, (7, 4))
+    W = rs.uniform(-50, 50, (5, 4))
+    g = gamma_for(21)
+    ctx = gpu_ctx_factory(P)
+    ctx.set_option("scan_impl", impl)
+    za, zb, zw = hs.ZkMatrix.new(ctx, A), hs.ZkMatrix.new(ctx, B), hs.ZkMatrix.new(ctx, W)
+    cs = hs.honest_prover_mat_mul(ctx, za, zb)
+    hs.ZkMatrix.verify_mul(ctx, za, zb, cs, g)
+    hs.ZkMatrix.verify_mul(ctx, za, zb, zw, g)
+    o0, o1, orlc = po.Context(phase=0), po.Context(phase=1), po.Context(phase=1)
+    oa, ob, ow = (po.zkmatrix_new(o0, P, x.tolist()) for x in (A, B, W))
+    ocs = po.honest_prover_mat_mul(o0, oa, ob)
+    gam = po.load_witness(orlc, g)
+    po.verify_mul(o1, oa, ob, ocs, gam)
+    po.verify_mul(o1, oa, ob, ow, gam)
+    def ints(cells):
+        return [int(r[0]) | int(r[1]) << 64 | int(r[2]) << 128 | int(r[3]) << 192 for r in cells]
+    assert ints(ctx.advice(0)) == o0.advice
+    assert ints(ctx.advice(1)) == o1.advice

@@ -28,7 +28,9 @@ def parse_variant(s):
     return name, opts
 
 
-DEFAULTS = {"gemm_impl": 0, "nt_stores": 0, "stage_ilp": 1, "scan_impl": 1, "overlap": 1}
+DEFAULTS = {"gemm_impl": 0, "nt_stores": 0, "stage_ilp": 1, "scan_impl": 4, "overlap": 1}
+# pseudo-option "prof": event profiler during the timed steps (0 off, 1 all, 2 k_stage only)
+PROF_PREFIX = {1: "", 2: "k_stage"}
 
 
 def main():
@@ -53,20 +55,28 @@ def main():
     kern = {name: {} for name, _ in variants}
     for name, opts in variants:          # warm every variant once
         for k, val in {**DEFAULTS, **opts}.items():
-            ctx.set_option(k, val)
+            if k != "prof":
+                ctx.set_option(k, val)
         hs.svd_witness(ctx, dm, du, dv, dd, g)
     ctx.sync()
     for _ in range(a.rounds):
         for name, opts in variants:
+            prof = opts.get("prof", 0)
             for k, val in {**DEFAULTS, **opts}.items():
-                ctx.set_option(k, val)
+                if k != "prof":
+                    ctx.set_option(k, val)
             hs.svd_witness(ctx, dm, du, dv, dd, g)
             ctx.sync()
+            if prof:
+                ctx.profile(True, PROF_PREFIX[prof])
             t0 = time.perf_counter()
             for _ in range(a.steps):
                 hs.svd_witness(ctx, dm, du, dv, dd, g)
             ctx.sync()
             res[name].append((time.perf_counter() - t0) / a.steps * 1e3)
+            if prof:
+                ctx.profile_collect()
+                ctx.profile(False)
             ctx.profile(True)
             hs.svd_witness(ctx, dm, du, dv, dd, g)
             for s in ctx.profile_collect():
