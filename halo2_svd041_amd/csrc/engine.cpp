@@ -276,6 +276,14 @@ struct svdw_ctx {
     // `m` satisfies |signed value| < 2^bits. Cleared with the streams.
     struct MatBits { svdw_mat m; uint32_t bits; };
     std::vector<MatBits> mbits;
+    // svd_witness: bit lengths of quantized m, u, v travel to pinned host memory
+    // behind ev_bits; the host waits for them only where the GEMM launches need
+    // them (fetch_bits), with check stages already queued on the device.
+    uint32_t* hbits = nullptr;
+    hipEvent_t ev_bits = nullptr;
+    bool bits_pending = false;
+    uint32_t qbits[3] = {0, 0, 0};
+    svdw_mat qmat[3] = {};
     // built-in event profiler (svdw_profile_*): one start/stop event pair per launch
     bool prof = false;
     std::string prof_filter;                // record only kernels whose name starts with this
@@ -289,6 +297,7 @@ struct svdw_ctx {
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
     uint32_t stage_flags = 0;               // STAGE_* (svdw_set_option "nt_stores", "stage_ilp")
     int scan_impl = 4;                      // svdw_set_option "scan_impl"
+    int prelaunch_at = 0;                   // "prelaunch_at": GEMMs queued before stage 0/1/2
     // second stream: GEMMs overlap the HBM-bound stages
     hipStream_t st2 = nullptr;
     bool overlap = true;
@@ -337,7 +346,19 @@ static uint32_t bits_of(const svdw_ctx* c, const svdw_mat& m) {
         if (same_cells(r.m, m)) return r.bits;
     return ~0u;
 }
+static void fetch_bits(svdw_ctx* c) {
+    if (!c->bits_pending) return;
+    hipck(hipEventSynchronize(c->ev_bits), "hipEventSynchronize");
+    c->bits_pending = false;
+    for (int i = 0; i < 3; ++i) {
+        uint32_t b = 0;
+        for (int s = 0; s < kBitSlots; ++s) b = std::max(b, c->hbits[i * kBitSlots + s]);
+        c->qbits[i] = b;
+        reg_bits(c, c->qmat[i], b);
+    }
+}
 static void clear_streams(svdw_ctx* c) {
+    c->bits_pending = false;
     for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
     c->mbits.clear();
 }
@@ -592,16 +613,17 @@ static bool is_transpose_of(const svdw_mat& b, const svdw_mat& a) {
 static std::vector<uint32_t> maxbits_many(svdw_ctx* c, const std::vector<svdw_mat>& ms) {
     std::vector<uint32_t> out(ms.size(), 0);
     if (c->dry || ms.empty()) return out;
-    ensure_buf(c, c->bits, 64 * sizeof(unsigned));
-    hipck(hipMemsetAsync(c->bits.p, 0, ms.size() * sizeof(unsigned), c->st), "memset");
+    const size_t words = ms.size() * kBitSlots;
+    ensure_buf(c, c->bits, words * sizeof(unsigned));
+    hipck(hipMemsetAsync(c->bits.p, 0, words * sizeof(unsigned), c->st), "memset");
     for (size_t i = 0; i < ms.size(); ++i)
-        hipck(launch_maxbits(view_of(c, ms[i]), ms[i].rows, ms[i].cols, (unsigned*)c->bits.p + i,
-                             c->st), "k_maxbits");
-    std::vector<unsigned> h(ms.size());
-    hipck(hipMemcpyAsync(h.data(), c->bits.p, ms.size() * sizeof(unsigned), hipMemcpyDeviceToHost,
+        hipck(launch_maxbits(view_of(c, ms[i]), ms[i].rows, ms[i].cols,
+                             (unsigned*)c->bits.p + i * kBitSlots, c->st), "k_maxbits");
+    std::vector<unsigned> h(words);
+    hipck(hipMemcpyAsync(h.data(), c->bits.p, words * sizeof(unsigned), hipMemcpyDeviceToHost,
                          c->st), "D2H");
     sync(c);
-    for (size_t i = 0; i < ms.size(); ++i) out[i] = h[i];
+    for (size_t i = 0; i < words; ++i) out[i / kBitSlots] = std::max(out[i / kBitSlots], h[i]);
     return out;
 }
 // field_mat_mul (src/matrix/mod.rs:510-537) on stream `s`: c_s = a * b written
@@ -968,13 +990,19 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     REQUIRE(d.len == r, "check_svd_phase0: d.len != min(N, M)");
     const uint32_t P = c->P;
     const uint32_t max_bits = max_bits_d + P;
-    if (!c->dry && c->overlap && known_bits && c->pre.empty()) {
+    uint64_t n0[2], nl0[2];                               // stream state at entry (for the replay)
+    for (int p = 0; p < 2; ++p) { n0[p] = c->ph[p].n; nl0[p] = c->ph[p].nl; }
+    auto prelaunch = [&] {
+        if (c->dry || !c->overlap || !known_bits || !c->pre.empty()) return;
         // The three products depend only on m, u, v: take their stream offsets
         // from a dry replay of this function and launch them now on st2, so the
-        // integer-VALU GEMMs run under the HBM-bound check stages on st.
+        // integer GEMMs run under the HBM-bound check stages on st. Called after
+        // the first check stage is queued, so the device is busy while the host
+        // waits for the operand bit lengths.
+        fetch_bits(c);
         svdw_ctx plan;
         plan.P = c->P; plan.LB = c->LB;
-        for (int p = 0; p < 2; ++p) { plan.ph[p].n = c->ph[p].n; plan.ph[p].nl = c->ph[p].nl; }
+        for (int p = 0; p < 2; ++p) { plan.ph[p].n = n0[p]; plan.ph[p].nl = nl0[p]; }
         std::vector<uint64_t> log;
         plan.gemm_log = &log;
         check_svd_phase0(&plan, m, u, v, d, err_svd, err_u, max_bits_d, known_bits);
@@ -990,11 +1018,14 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
             gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ba[g], bb[g]);
             c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
         }
-    }
+    };
+    if (c->prelaunch_at == 0) prelaunch();
     entries_less_than(c, d, max_bits);
     entries_in_desc_order(c, d, max_bits);
+    if (c->prelaunch_at == 1) prelaunch();
     BigU unit = big_from_u128(((unsigned __int128)1 << P) + 1);
     check_mat_entries_bounded(c, u, unit);
+    if (c->prelaunch_at == 2) prelaunch();
     check_mat_entries_bounded(c, v, unit);
     svdw_mat ut = u, vt = v;
     std::swap(ut.rows, ut.cols); std::swap(ut.rs, ut.cs);
@@ -1010,7 +1041,10 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     }
     udv.rows = N;
     uint32_t bm = ~0u, bu = ~0u, bv = ~0u;
-    if (known_bits) { bm = known_bits[0]; bu = known_bits[1]; bv = known_bits[2]; }
+    if (known_bits) {
+        fetch_bits(c);
+        bm = known_bits[0]; bu = known_bits[1]; bv = known_bits[2];
+    }
     svdw_mat mvt = honest_prover_mat_mul(c, m.phase, m, vt, bm, bv);
     BigU es = scale_err(err_svd, P), eu = scale_err(err_u, P);
     check_mat_diff_views(c, m.phase, udv, view_of(c, mvt), N, M, es);
@@ -1055,28 +1089,26 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     }
     unsigned* dbits = nullptr;
     if (!c->dry) {
-        ensure_buf(c, c->bits, 64 * sizeof(unsigned));
+        ensure_buf(c, c->bits, 3 * kBitSlots * sizeof(unsigned));
         dbits = (unsigned*)c->bits.p;
-        hipck(hipMemsetAsync(dbits, 0, 3 * sizeof(unsigned), c->st), "memset");
+        hipck(hipMemsetAsync(dbits, 0, 3 * kBitSlots * sizeof(unsigned), c->st), "memset");
     }
     svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device, dbits);
-    svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device, dbits ? dbits + 1 : nullptr);
-    svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device, dbits ? dbits + 2 : nullptr);
+    svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device, dbits ? dbits + kBitSlots : nullptr);
+    svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device, dbits ? dbits + 2 * kBitSlots : nullptr);
     svdw_mat zdm = zkmatrix_new(c, 0, d, r, 1, on_device);
     svdw_vec zd{0, r, zdm.off, 1};
     double es, eu;
     err_calc(c->P, std::max(N, M), cfg.max_norm, cfg.eps_svd, cfg.eps_u, &es, &eu);
-    std::vector<uint32_t> bits(3, 0);
-    if (!c->dry) {   // the one host synchronisation of a witness: digit counts of the GEMMs
-        unsigned hb[3];
-        hipck(hipMemcpyAsync(hb, dbits, sizeof hb, hipMemcpyDeviceToHost, c->st), "D2H");
-        hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
-        for (int i = 0; i < 3; ++i) bits[i] = hb[i];
-        reg_bits(c, zm, bits[0]);
-        reg_bits(c, zu, bits[1]);
-        reg_bits(c, zv, bits[2]);
+    if (!c->dry) {   // operand bit lengths (GEMM digit counts): read lazily, see fetch_bits
+        hipck(hipMemcpyAsync(c->hbits, dbits, 3 * kBitSlots * sizeof(uint32_t),
+                             hipMemcpyDeviceToHost, c->st), "D2H");
+        hipck(hipEventRecord(c->ev_bits, c->st), "hipEventRecord");
+        c->bits_pending = true;
+        c->qmat[0] = zm; c->qmat[1] = zu; c->qmat[2] = zv;
     }
-    svdw_svd_payload pl = check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, bits.data());
+    svdw_svd_payload pl = check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits);
+    fetch_bits(c);
     check_svd_phase1(c, zm, zu, zv, pl, gamma);
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
 }
@@ -1106,6 +1138,9 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
             hipError_t e = hipSetDevice(p->device);
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipHostMalloc((void**)&c->hbits, 3 * kBitSlots * sizeof(uint32_t),
+                                               hipHostMallocDefault);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bits, hipEventDisableTiming);
             if (e != hipSuccess) {
                 delete c;
                 fail(SVDW_EDEVICE, std::string("HIP device init failed: ") + hipGetErrorString(e));
@@ -1119,10 +1154,18 @@ int svdw_ctx_destroy(svdw_ctx* c) {
         if (!c) return;
         if (!c->dry) {
             (void)hipStreamSynchronize(c->st);
+            (void)hipStreamSynchronize(c->st2);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
             for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->w1c, &c->w1m, &c->w2c, &c->w2m,
                             &c->bits, &c->gpc, &c->gpm})
                 if (b->p) (void)hipFree(b->p);
+            for (auto& b : c->gps) if (b.p) (void)hipFree(b.p);
+            for (int i = 0; i < kMaxScanJobs; ++i) {
+                if (c->wbc[i].p) (void)hipFree(c->wbc[i].p);
+                if (c->wbs[i].p) (void)hipFree(c->wbs[i].p);
+            }
+            if (c->hbits) (void)hipHostFree(c->hbits);
+            if (c->ev_bits) (void)hipEventDestroy(c->ev_bits);
             for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
             for (auto e : c->pool) (void)hipEventDestroy(e);
             for (auto e : c->deps) (void)hipEventDestroy(e);
@@ -1334,6 +1377,22 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             REQUIRE(value == 1 || value == 2 || value == 4, "stage_ilp: 1, 2 or 4");
             c->stage_flags = (c->stage_flags & ~(STAGE_ILP2 | STAGE_ILP4)) |
                              (value == 2 ? STAGE_ILP2 : value == 4 ? STAGE_ILP4 : 0);
+        } else if (n == "gemm_priority") {
+            // second (GEMM) stream priority: 0 normal, 1 high
+            REQUIRE(value == 0 || value == 1, "gemm_priority: 0 or 1");
+            if (!c->dry) {
+                sync(c);
+                int lo = 0, hi = 0;
+                hipck(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+                hipStream_t s;
+                hipck(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, value ? hi : lo),
+                      "hipStreamCreateWithPriority");
+                hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
+                c->st2 = s;
+            }
+        } else if (n == "prelaunch_at") {
+            REQUIRE(value >= 0 && value <= 2, "prelaunch_at: 0, 1 or 2");
+            c->prelaunch_at = (int)value;
         } else if (n == "scan_impl") {
             REQUIRE(value >= 1 && value <= 5, "scan_impl: 1..5");
             c->scan_impl = (int)value;

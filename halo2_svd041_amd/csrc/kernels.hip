@@ -74,9 +74,9 @@ __global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in,
         else if (s >= 1.0) bits = (uint32_t)ilogb(s) + 1;
     }
     if (maxbits) {
-        // wave max -> block max (LDS) -> one atomic per block, skipped when the
-        // running maximum already covers it (one contended word otherwise
-        // serialises every block: ~10 ns per atomic)
+        // wave max -> block max (LDS) -> one atomic per block into one of
+        // kBitSlots words (a single contended word serialises the blocks at
+        // ~10 ns per atomic); the reader takes the max over the slots
         __shared__ uint32_t wmax[4];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, off));
@@ -84,8 +84,7 @@ __global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in,
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t b = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-            if (b && b > __hip_atomic_load(maxbits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                atomicMax(maxbits, b);
+            if (b) atomicMax(maxbits + (blockIdx.x & (kBitSlots - 1)), b);
         }
     }
     if (i >= n) return;
@@ -337,7 +336,7 @@ __global__ __launch_bounds__(256) void k_maxbits(const DView v, uint32_t rows, u
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, off));
-    if ((threadIdx.x & 63) == 0) atomicMax(out, best);
+    if ((threadIdx.x & 63) == 0 && best) atomicMax(out + (blockIdx.x & (kBitSlots - 1)), best);
 }
 
 hipError_t launch_maxbits(const DView& v, uint32_t rows, uint32_t cols, unsigned* out,

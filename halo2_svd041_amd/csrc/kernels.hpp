@@ -27,13 +27,16 @@ struct ScanBatch {
 // Elements per block of the generic stage kernel (= block size; LDS: E * nv * 32 B).
 static constexpr int kStageElems = 256;
 
+// Bit-length maxima are accumulated into kBitSlots words (atomicMax spread by
+// block); the result is the max over the slots.
+static constexpr int kBitSlots = 64;
 // ZkMatrix::new / ZkVector::new quantization (f64 -> Fr) of n contiguous values.
-// maxbits (nullable): atomicMax of bit-length(|x_q|) over the values.
+// maxbits (nullable, kBitSlots words): bit-length(|x_q|) maxima.
 hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int precision_bits,
                            unsigned* maxbits, hipStream_t st);
 // Generic cell-program stage over elements [a.e_begin, a.e_end).
 hipError_t launch_stage(const StageArgs& a, hipStream_t st);
-// max over the view of bit-length(|signed(x)|) -> atomicMax(*out).
+// max over the view of bit-length(|signed(x)|) -> out[kBitSlots] slot maxima.
 hipError_t launch_maxbits(const DView& v, uint32_t rows, uint32_t cols, unsigned* out,
                           hipStream_t st);
 // Balanced base-256 digit planes of X (rows x kdim): out[row][kg][D] int32 words,

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Per-step timeline from a rocprofv3 kernel trace (run_kernel_trace.csv).
+
+    python tools/timeline.py gpurun_out/prof_X/run_kernel_trace.csv [--steps 5]
+
+Splits the trace into witness steps (each starts with the first k_quantize of
+the step), then for the last step prints every dispatch (stream, start offset,
+duration, grid) and the busy / idle time of the union of all streams, so
+launch gaps and serial tails are visible.
+"""
+import argparse
+import csv
+from collections import defaultdict
+
+
+def short(name):
+    n = name.split("(")[0]
+    for pre in ("void svdw::", "svdw::"):
+        if n.startswith(pre):
+            n = n[len(pre):]
+    return n[:60]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--all", action="store_true", help="print every dispatch of the last step")
+    a = ap.parse_args()
+    rows = []
+    with open(a.trace) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
+                         r.get("Stream_Id", r.get("Queue_Id")), int(r["Grid_Size_X"])))
+    rows.sort()
+    # step boundaries: a k_quantize preceded by a gap or a non-quantize kernel
+    starts = [i for i, r in enumerate(rows) if r[2].startswith("k_quantize")
+              and (i == 0 or not rows[i - 1][2].startswith("k_quantize"))]
+    if len(starts) < 2:
+        raise SystemExit("could not find step boundaries")
+    s0, s1 = starts[-2], starts[-1]
+    step = rows[s0:s1]
+    t0 = step[0][0]
+    tend = max(r[1] for r in step)
+    span = (rows[s1][0] - t0) / 1e3
+    # union busy time
+    busy, cur_s, cur_e = 0, None, None
+    for s, e, *_ in step:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    print(f"step span (start to next step start) {span:.1f} us, last kernel end {(tend - t0) / 1e3:.1f} us, "
+          f"GPU busy (union) {busy / 1e3:.1f} us, idle {span - busy / 1e3:.1f} us, dispatches {len(step)}")
+    agg = defaultdict(lambda: [0, 0.0])
+    for s, e, n, st, g in step:
+        agg[n][0] += 1
+        agg[n][1] += (e - s) / 1e3
+    for n, (cnt, tot) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        print(f"  {tot:9.1f} us  x{cnt:3d}  {n}")
+    if a.all:
+        prev_end = t0
+        for s, e, n, st, g in step:
+            print(f"  s{st} +{(s - t0) / 1e3:8.1f} dur {(e - s) / 1e3:7.1f} gap {(s - prev_end) / 1e3:6.1f} "
+                  f"grid {g:9d}  {n}")
+            prev_end = max(prev_end, e)
+
+
+if __name__ == "__main__":
+    main()
