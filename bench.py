@@ -81,6 +81,23 @@ def roofline_from_profile(stats, steps):
     }, breakdown
 
 
+def pmc_traffic(kernel, N, M, P, LB):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
+    summary of this exact workload (profiles/*_pmc_summary.json, written by
+    tools/pmc_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE passes)."""
+    import glob
+    want = {"N": N, "M": M, "P": P, "LB": LB}
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")), reverse=True):
+        try:
+            with open(f) as fh:
+                s = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if s.get("config") == want and kernel in s.get("kernels", {}):
+            return s["kernels"][kernel]["traffic_per_launch"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def cpu_baseline(m, u, v, d, P, LB, g, rows):
     sys.path.insert(0, ORACLE_DIR)
     import corc  # oracle/ — the checker / reported baseline only
@@ -195,6 +212,10 @@ def main():
         }
         if stats:
             kname, roof, breakdown = roofline_from_profile(stats, args.steps)
+            traffic, src = pmc_traffic(kname, N, M, args.p, args.lb)
+            if traffic is not None:
+                roof["traffic"] = traffic
+                roof["traffic_source"] = src
             out["roofline"] = roof
             if args.breakdown:
                 print(json.dumps({"ms_per_step_by_kernel": breakdown,

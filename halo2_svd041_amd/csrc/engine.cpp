@@ -276,6 +276,9 @@ struct svdw_ctx {
     // `m` satisfies |signed value| < 2^bits. Cleared with the streams.
     struct MatBits { svdw_mat m; uint32_t bits; };
     std::vector<MatBits> mbits;
+    // products c_s = a * b (K = 2^lk-bounded inner dimension): |c_s| < 2^(bits_a + bits_b + lk)
+    struct Prod { svdw_mat cs, a, b; uint32_t lk; };
+    std::vector<Prod> prods;
     // svd_witness: bit lengths of quantized m, u, v travel to pinned host memory
     // behind ev_bits; the host waits for them only where the GEMM launches need
     // them (fetch_bits), with check stages already queued on the device.
@@ -297,7 +300,8 @@ struct svdw_ctx {
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
     uint32_t stage_flags = 0;               // STAGE_* (svdw_set_option "nt_stores", "stage_ilp")
     int scan_impl = 4;                      // svdw_set_option "scan_impl"
-    int prelaunch_at = 0;                   // "prelaunch_at": GEMMs queued before stage 0/1/2
+    int prelaunch_at = 0;
+    int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device                   // "prelaunch_at": GEMMs queued before stage 0/1/2
     // second stream: GEMMs overlap the HBM-bound stages
     hipStream_t st2 = nullptr;
     bool overlap = true;
@@ -344,6 +348,11 @@ static void reg_bits(svdw_ctx* c, const svdw_mat& m, uint32_t bits) {
 static uint32_t bits_of(const svdw_ctx* c, const svdw_mat& m) {
     for (auto& r : c->mbits)
         if (same_cells(r.m, m)) return r.bits;
+    for (auto& p : c->prods)
+        if (same_cells(p.cs, m)) {
+            const uint32_t ba = bits_of(c, p.a), bb = bits_of(c, p.b);
+            if (ba != ~0u && bb != ~0u) return ba + bb + p.lk;
+        }
     return ~0u;
 }
 static void fetch_bits(svdw_ctx* c) {
@@ -361,6 +370,7 @@ static void clear_streams(svdw_ctx* c) {
     c->bits_pending = false;
     for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
     c->mbits.clear();
+    c->prods.clear();
 }
 // RAII: brackets one kernel launch with HIP events on the context stream.
 struct ProfScope {
@@ -433,6 +443,25 @@ static void append(svdw_ctx* c, uint32_t phase, uint64_t n, uint64_t nl, uint64_
     s.nl += nl;
 }
 static Fr* cellp(svdw_ctx* c, uint32_t phase, uint64_t off) { return c->ph[phase].adv + off; }
+
+// Device pointers into the cell streams (views) are taken while a gadget is
+// being built; a stream reallocation in between would leave them pointing at
+// the freed buffer. Every ABI entry point that appends after taking a view
+// therefore sizes the streams first from a dry replay of itself (layouts are
+// data independent), so nothing reallocates inside the call.
+template <class F>
+static void pregrow(svdw_ctx* c, F&& fn) {
+    if (c->dry) return;
+    svdw_ctx plan;
+    plan.P = c->P;
+    plan.LB = c->LB;
+    for (int p = 0; p < 2; ++p) { plan.ph[p].n = c->ph[p].n; plan.ph[p].nl = c->ph[p].nl; }
+    fn(&plan);
+    for (int p = 0; p < 2; ++p) {
+        grow(c, c->ph[p].adv, c->ph[p].n, c->ph[p].cap, plan.ph[p].n);
+        grow(c, c->ph[p].lk, c->ph[p].nl, c->ph[p].lcap, plan.ph[p].nl);
+    }
+}
 
 // --------------------------------------------------------------- views
 static DView view_of(svdw_ctx* c, const svdw_mat& m) {
@@ -629,10 +658,42 @@ static std::vector<uint32_t> maxbits_many(svdw_ctx* c, const std::vector<svdw_ma
 // field_mat_mul (src/matrix/mod.rs:510-537) on stream `s`: c_s = a * b written
 // as canonical cells at `out` (row-major). Exact: balanced base-256 digit planes
 // + v_dot4c_i32_i8 when |entries| fit 9 digits, else Montgomery per MAC.
+// With bit-maxima slots (sa, sb: device, kBitSlots words each) the digit counts
+// are read by the kernels themselves and the host needs no operand bounds.
 static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_mat& b, Fr* out,
-                      uint32_t bits_a, uint32_t bits_b) {
+                      uint32_t bits_a, uint32_t bits_b, const unsigned* sa = nullptr,
+                      const unsigned* sb = nullptr) {
     const uint32_t N = a.rows, K = a.cols, M = b.cols;
     const bool sym = is_transpose_of(b, a);
+    if (sa && sb && K <= 8192) {
+        const uint32_t kcn = (K + 63) / 64;
+        const uint32_t npad = (N + 31) / 32 * 32, mpad = (M + 31) / 32 * 32;
+        ensure_buf(c, c->digA, (size_t)npad * kcn * 9 * 64);
+        {
+            ProfScope ps(c, s, "k_to_digits_mf", 32.0 * N * K + 64.0 * npad * kcn * 9, 0);
+            hipck(launch_to_digits_mf(view_of(c, a), N, K, 9, npad, kcn, (uint32_t*)c->digA.p, s, sa),
+                  "k_to_digits_mf");
+        }
+        const uint8_t* Bd = (const uint8_t*)c->digA.p;
+        if (!sym) {
+            ensure_buf(c, c->digB, (size_t)mpad * kcn * 9 * 64);
+            svdw_mat bt = b;   // Bt(j, k) = b(k, j)
+            bt.rows = b.cols; bt.cols = b.rows; bt.rs = b.cs; bt.cs = b.rs;
+            ProfScope ps(c, s, "k_to_digits_mf", 32.0 * M * K + 64.0 * mpad * kcn * 9, 0);
+            hipck(launch_to_digits_mf(view_of(c, bt), M, K, 9, mpad, kcn, (uint32_t*)c->digB.p, s, sb),
+                  "k_to_digits_mf");
+            Bd = (const uint8_t*)c->digB.p;
+        }
+        {
+            ProfScope ps(c, s, std::string("k_gemm_mfma:rt") + (sym ? "s" : ""),
+                         32.0 * N * M, (double)N * M * K);
+            hipck(launch_gemm_mfma_rt(sym, (const uint8_t*)c->digA.p, Bd, N, M, kcn, out, M, 1, sa,
+                                      sym ? sa : sb, s), "k_gemm_mfma_rt");
+        }
+        hipck(launch_gemm_mont(view_of(c, a), view_of(c, b), N, K, M, out, M, 1, s, sa,
+                               sym ? sa : sb), "k_gemm_mont");
+        return;
+    }
     int DA = round_digits(digits_for_bits(bits_a)), DB = round_digits(digits_for_bits(bits_b));
     const bool digits_ok = DA && DB && K <= 8192 && gemm_digits_supported(DA, DB);
     if (digits_ok && c->gemm_impl == SVDW_GEMM_MFMA) {
@@ -702,14 +763,13 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
     append(c, phase, (uint64_t)N * M, 0, &off, nullptr);
     svdw_mat cs{phase, N, M, off, (int64_t)M, 1};
     if (c->gemm_log) c->gemm_log->push_back(off);
-    if (bits_a == ~0u) bits_a = bits_of(c, a);
-    if (bits_b == ~0u) bits_b = bits_of(c, b);
-    auto reg_cs = [&] {   // |c_s| <= K * 2^bits_a * 2^bits_b
+    {   // |c_s| <= K * 2^bits_a * 2^bits_b, resolved when the operand bounds are known
         uint32_t lk = 0;
         while ((1ull << lk) < a.cols) ++lk;
-        reg_bits(c, cs, bits_a + bits_b + lk);
-    };
-    if (bits_a != ~0u && bits_b != ~0u) reg_cs();
+        c->prods.push_back({cs, a, b, lk});
+    }
+    if (bits_a == ~0u) bits_a = bits_of(c, a);
+    if (bits_b == ~0u) bits_b = bits_of(c, b);
     if (c->dry) return cs;
     if (!c->pre.empty()) {
         if (c->pre.front().off != off) fail(SVDW_EDEVICE, "internal: pre-launched GEMM offset mismatch");
@@ -726,7 +786,6 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
         bits_b = sym ? bb[0] : bb[1];
         reg_bits(c, a, bits_a);
         reg_bits(c, b, bits_b);
-        reg_cs();
     }
     gemm_exec(c, c->st, a, b, cellp(c, phase, off), bits_a, bits_b);
     return cs;
@@ -981,7 +1040,8 @@ static BigU scale_err(double err, uint32_t p) {
 static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u,
                                          const svdw_mat& v, const svdw_vec& d, double err_svd,
                                          double err_u, uint32_t max_bits_d,
-                                         const uint32_t* known_bits = nullptr) {
+                                         const uint32_t* known_bits = nullptr,
+                                         const unsigned* dev_slots = nullptr) {
     REQUIRE(m.rows == u.rows, "check_svd_phase0: m.num_rows != u.num_rows");
     REQUIRE(m.cols == v.rows, "check_svd_phase0: m.num_col != v.num_rows");
     REQUIRE(u.rows == u.cols, "check_svd_phase0: u not square");
@@ -999,7 +1059,8 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         // integer GEMMs run under the HBM-bound check stages on st. Called after
         // the first check stage is queued, so the device is busy while the host
         // waits for the operand bit lengths.
-        fetch_bits(c);
+        const bool on_device = dev_slots && c->gemm_impl == SVDW_GEMM_MFMA && c->gemm_rt;
+        if (!on_device) fetch_bits(c);
         svdw_ctx plan;
         plan.P = c->P; plan.LB = c->LB;
         for (int p = 0; p < 2; ++p) { plan.ph[p].n = n0[p]; plan.ph[p].nl = nl0[p]; }
@@ -1014,8 +1075,16 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         const svdw_mat A[3] = {m, u, v}, B[3] = {vt, ut, vt};
         const uint32_t ba[3] = {known_bits[0], known_bits[1], known_bits[2]};
         const uint32_t bb[3] = {known_bits[2], known_bits[1], known_bits[2]};
+        (void)ba; (void)bb;
+        const unsigned* sl[3] = {dev_slots, dev_slots ? dev_slots + kBitSlots : nullptr,
+                                 dev_slots ? dev_slots + 2 * kBitSlots : nullptr};
+        const unsigned* sa[3] = {sl[0], sl[1], sl[2]};
+        const unsigned* sb[3] = {sl[2], sl[1], sl[2]};
         for (int g = 0; g < 3; ++g) {
-            gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ba[g], bb[g]);
+            if (on_device)
+                gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ~0u, ~0u, sa[g], sb[g]);
+            else
+                gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ba[g], bb[g]);
             c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
         }
     };
@@ -1041,7 +1110,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     }
     udv.rows = N;
     uint32_t bm = ~0u, bu = ~0u, bv = ~0u;
-    if (known_bits) {
+    if (known_bits && c->pre.empty()) {                  // products not launched ahead
         fetch_bits(c);
         bm = known_bits[0]; bu = known_bits[1]; bv = known_bits[2];
     }
@@ -1107,7 +1176,8 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         c->bits_pending = true;
         c->qmat[0] = zm; c->qmat[1] = zu; c->qmat[2] = zv;
     }
-    svdw_svd_payload pl = check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits);
+    svdw_svd_payload pl =
+        check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits, dbits);
     fetch_bits(c);
     check_svd_phase1(c, zm, zu, zv, pl, gamma);
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
@@ -1256,6 +1326,7 @@ int svdw_entries_less_than(svdw_ctx* c, const svdw_vec* d, uint32_t max_bits) {
     return guarded([&] {
         REQUIRE(c && d, "null argument");
         check_vec(c, *d);
+        pregrow(c, [&](svdw_ctx* x) { entries_less_than(x, *d, max_bits); });
         entries_less_than(c, *d, max_bits);
     });
 }
@@ -1263,6 +1334,7 @@ int svdw_entries_in_desc_order(svdw_ctx* c, const svdw_vec* d, uint32_t max_bits
     return guarded([&] {
         REQUIRE(c && d, "null argument");
         check_vec(c, *d);
+        pregrow(c, [&](svdw_ctx* x) { entries_in_desc_order(x, *d, max_bits); });
         entries_in_desc_order(c, *d, max_bits);
     });
 }
@@ -1270,6 +1342,7 @@ int svdw_check_mat_entries_bounded(svdw_ctx* c, const svdw_mat* a, const uint64_
     return guarded([&] {
         REQUIRE(c && a && bnd, "null argument");
         check_mat(c, *a);
+        pregrow(c, [&](svdw_ctx* x) { check_mat_entries_bounded(x, *a, big_from_words(bnd)); });
         check_mat_entries_bounded(c, *a, big_from_words(bnd));
     });
 }
@@ -1280,6 +1353,10 @@ int svdw_check_mat_diff(svdw_ctx* c, const svdw_mat* a, const svdw_mat* b, const
         check_mat(c, *b);
         REQUIRE(a->rows == b->rows && a->cols == b->cols, "check_mat_diff: shape mismatch");
         REQUIRE(a->phase == b->phase, "check_mat_diff: a and b in different phases");
+        pregrow(c, [&](svdw_ctx* x) {
+            check_mat_diff_views(x, a->phase, view_of(x, *a), view_of(x, *b), a->rows, a->cols,
+                                 big_from_words(tol));
+        });
         check_mat_diff_views(c, a->phase, view_of(c, *a), view_of(c, *b), a->rows, a->cols,
                              big_from_words(tol));
     });
@@ -1289,6 +1366,7 @@ int svdw_check_mat_id(svdw_ctx* c, const svdw_mat* a, const svdw_vec* sid, const
         REQUIRE(c && a && sid && tol, "null argument");
         check_mat(c, *a);
         check_vec(c, *sid);
+        pregrow(c, [&](svdw_ctx* x) { check_mat_id(x, *a, *sid, big_from_words(tol)); });
         check_mat_id(c, *a, *sid, big_from_words(tol));
     });
 }
@@ -1297,6 +1375,7 @@ int svdw_mat_times_diag_mat(svdw_ctx* c, const svdw_mat* a, const svdw_vec* v, s
         REQUIRE(c && a && v && out, "null argument");
         check_mat(c, *a);
         check_vec(c, *v);
+        pregrow(c, [&](svdw_ctx* x) { mat_times_diag_mat(x, *a, *v); });
         *out = mat_times_diag_mat(c, *a, *v);
     });
 }
@@ -1315,6 +1394,7 @@ int svdw_field_mat_vec_mul(svdw_ctx* c, uint32_t phase, const svdw_mat* a, const
         REQUIRE(c && a && v && out, "null argument");
         check_mat(c, *a);
         check_vec(c, *v);
+        pregrow(c, [&](svdw_ctx* x) { field_mat_vec_mul(x, phase, *a, *v); });
         *out = field_mat_vec_mul(c, phase, *a, *v);
     });
 }
@@ -1325,6 +1405,7 @@ int svdw_verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat* a, const svdw_m
         check_mat(c, *a);
         check_mat(c, *b);
         check_mat(c, *cs);
+        pregrow(c, [&](svdw_ctx* x) { verify_mul(x, phase, *a, *b, *cs, fr_from_words(gamma)); });
         verify_mul(c, phase, *a, *b, *cs, fr_from_words(gamma));
     });
 }
@@ -1343,6 +1424,9 @@ int svdw_check_svd_phase0(svdw_ctx* c, const svdw_mat* m, const svdw_mat* u, con
         check_mat(c, *m); check_mat(c, *u); check_mat(c, *v); check_vec(c, *d);
         REQUIRE(m->phase == 0 && u->phase == 0 && v->phase == 0 && d->phase == 0,
                 "check_svd_phase0 inputs must live in phase 0");
+        pregrow(c, [&](svdw_ctx* x) {
+            check_svd_phase0(x, *m, *u, *v, *d, err_svd, err_u, max_bits_d);
+        });
         *out = check_svd_phase0(c, *m, *u, *v, *d, err_svd, err_u, max_bits_d);
     });
 }
@@ -1350,6 +1434,7 @@ int svdw_check_svd_phase1(svdw_ctx* c, const svdw_mat* m, const svdw_mat* u, con
                           const svdw_svd_payload* pl, const uint64_t gamma[4]) {
     return guarded([&] {
         REQUIRE(c && m && u && v && pl && gamma, "null argument");
+        pregrow(c, [&](svdw_ctx* x) { check_svd_phase1(x, *m, *u, *v, *pl, fr_from_words(gamma)); });
         check_svd_phase1(c, *m, *u, *v, *pl, fr_from_words(gamma));
     });
 }
@@ -1390,6 +1475,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                 hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
                 c->st2 = s;
             }
+        } else if (n == "gemm_rt") {
+            REQUIRE(value == 0 || value == 1, "gemm_rt: 0 or 1");
+            c->gemm_rt = (int)value;
         } else if (n == "prelaunch_at") {
             REQUIRE(value >= 0 && value <= 2, "prelaunch_at: 0, 1 or 2");
             c->prelaunch_at = (int)value;

@@ -552,9 +552,25 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int MT = 32;        // block tile (2 x 2 waves of 16 x 16)
 constexpr int LROW = 80;      // LDS bytes per (digit, row): 64 + 16 pad
 
+// Digit planes chosen on the device from kBitSlots bit-length maxima (the
+// engine's digits_for_bits + round_digits): 5, 8 or 9 planes, 0 = too wide for
+// the digit GEMM (Montgomery fallback).
+__device__ __forceinline__ int device_digits(const unsigned* __restrict__ slots) {
+    uint32_t b = 0;
+#pragma unroll 8
+    for (int s = 0; s < kBitSlots; ++s) b = max(b, slots[s]);
+    const int need = b <= 7 ? 1 : (int)((b + 9) / 8);
+    return need <= 5 ? 5 : need <= 8 ? 8 : need <= 9 ? 9 : 0;
+}
+
 __global__ __launch_bounds__(256) void k_to_digits_mf(const DView x, uint32_t rows, uint32_t kdim,
                                                       int D, uint32_t rows_pad, uint32_t kcn,
-                                                      uint32_t* __restrict__ out) {
+                                                      uint32_t* __restrict__ out,
+                                                      const unsigned* __restrict__ slots) {
+    if (slots) {
+        D = device_digits(slots);
+        if (!D) return;
+    }
     uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (uint64_t)rows_pad * kcn * 16) return;
     const uint32_t g = (uint32_t)(idx & 15);
@@ -600,11 +616,11 @@ __global__ __launch_bounds__(256) void k_to_digits_mf(const DView x, uint32_t ro
 }
 
 hipError_t launch_to_digits_mf(const DView& x, uint32_t rows, uint32_t kdim, int D, uint32_t rows_pad,
-                               uint32_t kcn, uint32_t* out, hipStream_t st) {
+                               uint32_t kcn, uint32_t* out, hipStream_t st, const unsigned* slots) {
     uint64_t n = (uint64_t)rows_pad * kcn * 16;
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_to_digits_mf, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, rows,
-                       kdim, D, rows_pad, kcn, out);
+                       kdim, D, rows_pad, kcn, out, slots);
     return hipGetLastError();
 }
 
@@ -616,14 +632,16 @@ __device__ __forceinline__ Fr combine_diag_reg(const v4i (&acc)[DA + DB - 1], in
     return combine_diagonals<DA, DB>(a);
 }
 
+template <int DA, int DB>
+constexpr int gemm_lds_bytes() {
+    return (DA + DB) * MT * LROW > MT * MT * 32 ? (DA + DB) * MT * LROW : MT * MT * 32;
+}
 template <int DA, int DB, bool SYM>
-__global__ __launch_bounds__(256) void k_gemm_mfma(const uint8_t* __restrict__ Ad,
-                                                   const uint8_t* __restrict__ Bd, uint32_t N,
-                                                   uint32_t M, uint32_t kcn, Fr* __restrict__ out,
-                                                   int64_t ors, int64_t ocs, uint32_t tiles_m) {
+__device__ __forceinline__ void gemm_mfma_body(uint8_t* S, const uint8_t* __restrict__ Ad,
+                                               const uint8_t* __restrict__ Bd, uint32_t N,
+                                               uint32_t M, uint32_t kcn, Fr* __restrict__ out,
+                                               int64_t ors, int64_t ocs, uint32_t tiles_m) {
     // one LDS array: operand slabs during the K loop, the output tile after it
-    constexpr int kOps = (DA + DB) * MT * LROW, kTile = MT * MT * 32;
-    __shared__ __attribute__((aligned(16))) uint8_t S[kOps > kTile ? kOps : kTile];
     uint8_t* As = S;
     uint8_t* Bs = S + DA * MT * LROW;
     uint8_t* Ts = S;
@@ -707,6 +725,50 @@ __global__ __launch_bounds__(256) void k_gemm_mfma(const uint8_t* __restrict__ A
     }
 }
 
+template <int DA, int DB, bool SYM>
+__global__ __launch_bounds__(256) void k_gemm_mfma(const uint8_t* __restrict__ Ad,
+                                                   const uint8_t* __restrict__ Bd, uint32_t N,
+                                                   uint32_t M, uint32_t kcn, Fr* __restrict__ out,
+                                                   int64_t ors, int64_t ocs, uint32_t tiles_m) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[gemm_lds_bytes<DA, DB>()];
+    gemm_mfma_body<DA, DB, SYM>(S, Ad, Bd, N, M, kcn, out, ors, ocs, tiles_m);
+}
+// Digit counts read on the device (no host round trip for the operand bounds):
+// every (DA, DB) pair is compiled in and the block branches uniformly.
+template <bool SYM>
+__global__ __launch_bounds__(256) void k_gemm_mfma_rt(const uint8_t* __restrict__ Ad,
+                                                      const uint8_t* __restrict__ Bd, uint32_t N,
+                                                      uint32_t M, uint32_t kcn, Fr* __restrict__ out,
+                                                      int64_t ors, int64_t ocs, uint32_t tiles_m,
+                                                      const unsigned* __restrict__ sa,
+                                                      const unsigned* __restrict__ sb) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[gemm_lds_bytes<9, 9>()];
+    const int DA = device_digits(sa), DB = SYM ? DA : device_digits(sb);
+#define SVDW_RT(a, b) \
+    if (DA == a && DB == b) { gemm_mfma_body<a, b, SYM>(S, Ad, Bd, N, M, kcn, out, ors, ocs, tiles_m); return; }
+    if (SYM) {
+        SVDW_RT(5, 5) SVDW_RT(8, 8) SVDW_RT(9, 9)
+    } else {
+        SVDW_RT(5, 5) SVDW_RT(5, 8) SVDW_RT(5, 9) SVDW_RT(8, 5) SVDW_RT(8, 8) SVDW_RT(8, 9)
+        SVDW_RT(9, 5) SVDW_RT(9, 8) SVDW_RT(9, 9)
+    }
+#undef SVDW_RT
+}
+hipError_t launch_gemm_mfma_rt(bool sym, const uint8_t* Ad, const uint8_t* Bd, uint32_t N,
+                               uint32_t M, uint32_t kcn, Fr* out, int64_t ors, int64_t ocs,
+                               const unsigned* slots_a, const unsigned* slots_b, hipStream_t st) {
+    uint32_t tn = (N + MT - 1) / MT, tm = (M + MT - 1) / MT;
+    if (sym) {
+        if (N != M) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_gemm_mfma_rt<true>, dim3(tm * (tm + 1) / 2), dim3(256), 0, st, Ad, Ad, N,
+                           M, kcn, out, ors, ocs, tm, slots_a, slots_a);
+    } else {
+        hipLaunchKernelGGL(k_gemm_mfma_rt<false>, dim3(tn * tm), dim3(256), 0, st, Ad, Bd, N, M, kcn,
+                           out, ors, ocs, tm, slots_a, slots_b);
+    }
+    return hipGetLastError();
+}
+
 template <int DA, int DB>
 static hipError_t gemm_mfma_dispatch(bool sym, const uint8_t* Ad, const uint8_t* Bd, uint32_t N,
                                      uint32_t M, uint32_t kcn, Fr* out, int64_t ors, int64_t ocs,
@@ -737,7 +799,9 @@ hipError_t launch_gemm_mfma(int DA, int DB, bool sym, const uint8_t* Ad, const u
 // -------------------------------------------------------- Montgomery GEMM
 __global__ __launch_bounds__(256) void k_gemm_mont(const DView A, const DView B, uint32_t N,
                                                    uint32_t K, uint32_t M, Fr* out, int64_t ors,
-                                                   int64_t ocs) {
+                                                   int64_t ocs, const unsigned* __restrict__ sa,
+                                                   const unsigned* __restrict__ sb) {
+    if (sa && device_digits(sa) && device_digits(sb)) return;   // digit GEMM took it
     uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (uint64_t)N * M) return;
     uint32_t i = (uint32_t)(e / M), j = (uint32_t)(e % M);
@@ -752,11 +816,12 @@ __global__ __launch_bounds__(256) void k_gemm_mont(const DView A, const DView B,
 }
 
 hipError_t launch_gemm_mont(const DView& A, const DView& B, uint32_t N, uint32_t K, uint32_t M,
-                            Fr* out, int64_t ors, int64_t ocs, hipStream_t st) {
+                            Fr* out, int64_t ors, int64_t ocs, hipStream_t st,
+                            const unsigned* slots_a, const unsigned* slots_b) {
     uint64_t n = (uint64_t)N * M;
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_gemm_mont, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A, B, N, K,
-                       M, out, ors, ocs);
+                       M, out, ors, ocs, slots_a, slots_b);
     return hipGetLastError();
 }
 

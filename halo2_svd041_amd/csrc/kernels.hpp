@@ -50,14 +50,25 @@ hipError_t launch_gemm_digits(int DA, int DB, bool sym, const uint32_t* Ad, cons
                               int64_t ocs, hipStream_t st);
 bool gemm_digits_supported(int DA, int DB);
 // Matrix-core variant: digit planes laid out [row][kc][D][64 B] (kc = 64-k chunks).
+// slots (nullable, kBitSlots words): take D from the device-side bit maxima
+// instead (5 / 8 / 9 planes; nothing written when wider than 9 digits).
 hipError_t launch_to_digits_mf(const DView& x, uint32_t rows, uint32_t kdim, int D, uint32_t rows_pad,
-                               uint32_t kcn, uint32_t* out, hipStream_t st);
+                               uint32_t kcn, uint32_t* out, hipStream_t st,
+                               const unsigned* slots = nullptr);
 hipError_t launch_gemm_mfma(int DA, int DB, bool sym, const uint8_t* Ad, const uint8_t* Bd,
                             uint32_t N, uint32_t M, uint32_t kcn, Fr* out, int64_t ors,
                             int64_t ocs, hipStream_t st);
-// Generic Montgomery GEMM (any field elements): out = A(NxK) * B(KxM).
+// Same product with DA / DB read from bit-maxima slots on the device (planes
+// laid out for those counts by launch_to_digits_mf with the same slots); a
+// no-op when either operand is wider than 9 digits.
+hipError_t launch_gemm_mfma_rt(bool sym, const uint8_t* Ad, const uint8_t* Bd, uint32_t N,
+                               uint32_t M, uint32_t kcn, Fr* out, int64_t ors, int64_t ocs,
+                               const unsigned* slots_a, const unsigned* slots_b, hipStream_t st);
+// Generic Montgomery GEMM (any field elements): out = A(NxK) * B(KxM). With
+// slots, a no-op unless an operand is too wide for the digit GEMM.
 hipError_t launch_gemm_mont(const DView& A, const DView& B, uint32_t N, uint32_t K, uint32_t M,
-                            Fr* out, int64_t ors, int64_t ocs, hipStream_t st);
+                            Fr* out, int64_t ors, int64_t ocs, hipStream_t st,
+                            const unsigned* slots_a = nullptr, const unsigned* slots_b = nullptr);
 // w vector (len L) from a view (row 0 / col j of a 1 x L view) -> canonical copy
 // (w_canon nullable) and w_scaled = mont_mul(w, f) (f = R^2: Montgomery form).
 hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* w_scaled, const Fr& f,
