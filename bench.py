@@ -129,6 +129,8 @@ def main():
     ap.add_argument("--profile-prefix", default="k_stage",
                     help="kernel-name prefix the timed-region profiler records ('' = all)")
     ap.add_argument("--breakdown", action="store_true", help="print per-kernel ms/step to stderr")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="engine tuning option name=value (svdw_set_option), repeatable")
     args = ap.parse_args()
     N = args.n
     M = args.m or N
@@ -154,6 +156,9 @@ def main():
                       for x in (m, u, v, d))
     torch.cuda.synchronize()
     ctx = hs.Context(device=local, precision_bits=args.p, lookup_bits=args.lb)
+    for kv in args.opt:
+        name, _, val = kv.partition("=")
+        ctx.set_option(name, int(val))
 
     for _ in range(args.warmup):
         cnt = hs.svd_witness(ctx, dm, du, dv, dd, g)

@@ -265,7 +265,7 @@ struct svdw_ctx {
     hipStream_t st = nullptr;
     uint32_t P = 32, LB = 19;
     Stream ph[2];
-    DBuf f64in, digA, digB, w1c, w1m, w2c, w2m, bits, gpc, gpm;
+    DBuf f64in, digA, digB, w1c, w1m, w2c, w2m, bits, gpc, gpm, crtR, gbits;
     DBuf wbc[kMaxScanJobs], wbs[kMaxScanJobs];   // b.v per batched verify_mul (canonical, scaled)
     // gamma^j cache (canonical gpc / Montgomery gpm), shared by verify_mul calls
     Fr gp_gamma{};
@@ -299,9 +299,11 @@ struct svdw_ctx {
     std::vector<hipEvent_t> pool;
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
     uint32_t stage_flags = 0;               // STAGE_* (svdw_set_option "nt_stores", "stage_ilp")
+    uint32_t stage_sweep = 0;               // "stage_sweep": persistent grid of the sweep mode (0 off)
     int scan_impl = 4;                      // svdw_set_option "scan_impl"
     int prelaunch_at = 0;
-    int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device                   // "prelaunch_at": GEMMs queued before stage 0/1/2
+    int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
+    int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)                   // "prelaunch_at": GEMMs queued before stage 0/1/2
     // second stream: GEMMs overlap the HBM-bound stages
     hipStream_t st2 = nullptr;
     bool overlap = true;
@@ -360,10 +362,8 @@ static void fetch_bits(svdw_ctx* c) {
     hipck(hipEventSynchronize(c->ev_bits), "hipEventSynchronize");
     c->bits_pending = false;
     for (int i = 0; i < 3; ++i) {
-        uint32_t b = 0;
-        for (int s = 0; s < kBitSlots; ++s) b = std::max(b, c->hbits[i * kBitSlots + s]);
-        c->qbits[i] = b;
-        reg_bits(c, c->qmat[i], b);
+        c->qbits[i] = c->hbits[i];
+        reg_bits(c, c->qmat[i], c->qbits[i]);
     }
 }
 static void clear_streams(svdw_ctx* c) {
@@ -503,6 +503,10 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     a.e_end = nelem;
     a.cols = cols ? cols : 1;
     a.flags = c->stage_flags;
+    a.sweep_nb = c->stage_sweep;
+    // interleaved groups only pay off on big stages (and need whole batches of work)
+    if (c->stage_sweep && (uint64_t)nelem >= 4ull * kStageElems * c->stage_sweep / kSweepG)
+        a.flags |= STAGE_SWEEP;
     // 32-bit magics for fastdiv (divisor 1 is handled in the kernel)
     auto magic = [](uint64_t d) -> uint32_t { return d > 1 ? (uint32_t)(((1ull << 32) + d - 1) / d) : 0; };
     a.cdiv_magic = magic(a.C);
@@ -532,7 +536,7 @@ static svdw_vec put_cell(svdw_ctx* c, uint32_t phase, const Fr& v) {   // load_w
 
 // ----------------------------------------------------- reference functions
 static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, uint32_t rows,
-                             uint32_t cols, bool on_device, unsigned* maxbits = nullptr) {
+                             uint32_t cols, bool on_device, unsigned* blockmax = nullptr) {
     REQUIRE(rows >= 1 && cols >= 1, "ZkMatrix::new: empty matrix");
     REQUIRE(data || c->dry, "null data");
     uint64_t n = (uint64_t)rows * cols, off;
@@ -546,7 +550,7 @@ static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, ui
             src = (const double*)c->f64in.p;
         }
         ProfScope ps(c, c->st, "k_quantize", 40.0 * n, 0);
-        hipck(launch_quantize(src, n, cellp(c, phase, off), (int)c->P, maxbits, c->st), "k_quantize");
+        hipck(launch_quantize(src, n, cellp(c, phase, off), (int)c->P, blockmax, c->st), "k_quantize");
     }
     return svdw_mat{phase, rows, cols, off, (int64_t)cols, 1};
 }
@@ -642,29 +646,79 @@ static bool is_transpose_of(const svdw_mat& b, const svdw_mat& a) {
 static std::vector<uint32_t> maxbits_many(svdw_ctx* c, const std::vector<svdw_mat>& ms) {
     std::vector<uint32_t> out(ms.size(), 0);
     if (c->dry || ms.empty()) return out;
-    const size_t words = ms.size() * kBitSlots;
+    const size_t words = ms.size() * kMaxBitBlocks;
     ensure_buf(c, c->bits, words * sizeof(unsigned));
-    hipck(hipMemsetAsync(c->bits.p, 0, words * sizeof(unsigned), c->st), "memset");
-    for (size_t i = 0; i < ms.size(); ++i)
+    std::vector<uint32_t> nb(ms.size());
+    for (size_t i = 0; i < ms.size(); ++i) {
+        const uint64_t n = (uint64_t)ms[i].rows * ms[i].cols;
+        nb[i] = (uint32_t)std::min<uint64_t>((n + 255) / 256, kMaxBitBlocks);
         hipck(launch_maxbits(view_of(c, ms[i]), ms[i].rows, ms[i].cols,
-                             (unsigned*)c->bits.p + i * kBitSlots, c->st), "k_maxbits");
+                             (unsigned*)c->bits.p + i * kMaxBitBlocks, c->st), "k_maxbits");
+    }
     std::vector<unsigned> h(words);
     hipck(hipMemcpyAsync(h.data(), c->bits.p, words * sizeof(unsigned), hipMemcpyDeviceToHost,
                          c->st), "D2H");
     sync(c);
-    for (size_t i = 0; i < words; ++i) out[i / kBitSlots] = std::max(out[i / kBitSlots], h[i]);
+    for (size_t i = 0; i < ms.size(); ++i)
+        for (uint32_t b = 0; b < nb[i]; ++b) out[i] = std::max(out[i], h[i * kMaxBitBlocks + b]);
     return out;
 }
 // field_mat_mul (src/matrix/mod.rs:510-537) on stream `s`: c_s = a * b written
 // as canonical cells at `out` (row-major). Exact: balanced base-256 digit planes
 // + v_dot4c_i32_i8 when |entries| fit 9 digits, else Montgomery per MAC.
-// With bit-maxima slots (sa, sb: device, kBitSlots words each) the digit counts
-// are read by the kernels themselves and the host needs no operand bounds.
+// With device bit-length words (sa, sb: one word each) the digit counts are
+// read by the kernels themselves and the host needs no operand bounds.
 static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_mat& b, Fr* out,
                       uint32_t bits_a, uint32_t bits_b, const unsigned* sa = nullptr,
                       const unsigned* sb = nullptr) {
     const uint32_t N = a.rows, K = a.cols, M = b.cols;
     const bool sym = is_transpose_of(b, a);
+    if (!sa && !sb && c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA && bits_a <= 128 &&
+        bits_b <= 128 && K <= 8192 && !c->dry) {
+        // host-known bounds: hand them to the CRT kernels as device words
+        // (stream-ordered memsets, one pair per stream)
+        const int slot = s == c->st2 ? 2 : 0;
+        ensure_buf(c, c->gbits, 4 * sizeof(unsigned));
+        unsigned* w = (unsigned*)c->gbits.p + slot;
+        hipck(hipMemsetD32Async((hipDeviceptr_t)w, bits_a, 1, s), "hipMemsetD32Async");
+        hipck(hipMemsetD32Async((hipDeviceptr_t)(w + 1), bits_b, 1, s), "hipMemsetD32Async");
+        sa = w;
+        sb = w + 1;
+    }
+    if (sa && sb && c->gemm_crt && K <= 8192) {   // |acc| <= K 2^14 <= 2^27 (bias in k_gemm_crt)
+        // multi-modular path: residue planes, one int8 GEMM per modulus, CRT
+        uint32_t lk = 0;
+        while ((1ull << lk) < K) ++lk;
+        const uint32_t kpad = (K + 63) / 64 * 64;
+        const uint32_t rpa = (N + 127) / 128 * 128, rpb = (M + 127) / 128 * 128;
+        ensure_buf(c, c->digA, (size_t)kCrtMaxResidues * rpa * kpad);
+        ensure_buf(c, c->crtR, (size_t)kCrtMaxResidues * rpa * (sym ? rpa : rpb));
+        {
+            ProfScope ps(c, s, "k_to_residues", 32.0 * N * K, 0);
+            hipck(launch_to_residues(view_of(c, a), N, K, rpa, kpad, (uint32_t*)c->digA.p, sa,
+                                     sym ? sa : sb, lk, s), "k_to_residues");
+        }
+        const uint8_t* Br = (const uint8_t*)c->digA.p;
+        if (!sym) {
+            ensure_buf(c, c->digB, (size_t)kCrtMaxResidues * rpb * kpad);
+            svdw_mat bt = b;   // Bt(j, k) = b(k, j)
+            bt.rows = b.cols; bt.cols = b.rows; bt.rs = b.cs; bt.cs = b.rs;
+            ProfScope ps(c, s, "k_to_residues", 32.0 * M * K, 0);
+            hipck(launch_to_residues(view_of(c, bt), M, K, rpb, kpad, (uint32_t*)c->digB.p, sa, sb,
+                                     lk, s), "k_to_residues");
+            Br = (const uint8_t*)c->digB.p;
+        }
+        {
+            ProfScope ps(c, s, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * N * M,
+                         (double)N * M * K);
+            hipck(launch_gemm_crt(sym, (const uint8_t*)c->digA.p, Br, N, M, rpa, sym ? rpa : rpb,
+                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s),
+                  "k_gemm_crt");
+        }
+        hipck(launch_gemm_mont(view_of(c, a), view_of(c, b), N, K, M, out, M, 1, s, sa,
+                               sym ? sa : sb, (int)lk), "k_gemm_mont");
+        return;
+    }
     if (sa && sb && K <= 8192) {
         const uint32_t kcn = (K + 63) / 64;
         const uint32_t npad = (N + 31) / 32 * 32, mpad = (M + 31) / 32 * 32;
@@ -805,48 +859,59 @@ static Fr scale_factor(int na) {
     x.w[na] = 1;                                          // 2^(32 na) < p for na <= 6
     return mont_mul(x, fr_r2());
 }
-// field_mat_vec_mul with the vector given as canonical + scaled copies
-// (ws = w * 2^(32 na) mod p, see scan_na).
+// Scaled copies of a vector: ws = w * 2^(32 na) mod p (see scan_na) and, for
+// na < 8, wn = -ws.
+struct WScaled {
+    const Fr* ws;
+    const Fr* wn;
+};
+// field_mat_vec_mul with the vector given as canonical + scaled copies.
 static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const Fr* wc,
-                            const Fr* wm, int na) {
+                            WScaled w, int na) {
     const uint32_t R = a.rows, L = a.cols;
     uint64_t off;
     append(c, phase, (uint64_t)R * (3ull * L + 1), 0, &off, nullptr);
     if (!c->dry) {
         ProfScope ps(c, c->st, a.cs == 1 ? "k_matvec_scan:rows" : "k_matvec_scan:cols", 32.0 * (double)R * (4.0 * L + 1) + 64.0 * L, (double)R * L);
-        hipck(launch_matvec_scan(view_of(c, a), 0, R, L, wc, wm, cellp(c, phase, off), c->scan_impl,
-                                 na, c->st), "k_matvec_scan");
+        hipck(launch_matvec_scan(view_of(c, a), 0, R, L, wc, w.ws, w.wn, cellp(c, phase, off),
+                                 c->scan_impl, na, c->st), "k_matvec_scan");
     }
     return svdw_vec{phase, R, off + 3ull * L, (int64_t)(3ull * L + 1)};
 }
-static void vec_prep(svdw_ctx* c, const svdw_vec& v, DBuf& bc, DBuf& bm, int na) {
+// canonical copy into bc, scaled copies into bm ([0, len): ws, [len, 2 len): -ws)
+static WScaled vec_prep(svdw_ctx* c, const svdw_vec& v, DBuf& bc, DBuf& bm, int na) {
     ensure_buf(c, bc, (size_t)v.len * sizeof(Fr));
-    ensure_buf(c, bm, (size_t)v.len * sizeof(Fr));
-    if (c->dry) return;
-    hipck(launch_vec_prep(view_of(c, svdw_mat{v.phase, 1, v.len, v.off, 0, v.stride}), v.len,
-                          (Fr*)bc.p, (Fr*)bm.p, scale_factor(na), c->st), "k_vec_prep");
+    ensure_buf(c, bm, 2 * (size_t)v.len * sizeof(Fr));
+    Fr* ws = (Fr*)bm.p;
+    Fr* wn = na < 8 && ws ? ws + v.len : nullptr;
+    if (!c->dry)
+        hipck(launch_vec_prep(view_of(c, svdw_mat{v.phase, 1, v.len, v.off, 0, v.stride}), v.len,
+                              (Fr*)bc.p, ws, wn, scale_factor(na), c->st), "k_vec_prep");
+    return WScaled{ws, wn};
 }
 static svdw_vec field_mat_vec_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a,
                                   const svdw_vec& v) {
     REQUIRE(a.cols == v.len, "field_mat_vec_mul: a[0].len() != v.len()");
     const int na = scan_na(c, a);
-    vec_prep(c, v, c->w1c, c->w1m, na);
-    return matvec_rows(c, phase, a, (const Fr*)c->w1c.p, (const Fr*)c->w1m.p, na);
+    const WScaled w = vec_prep(c, v, c->w1c, c->w1m, na);
+    return matvec_rows(c, phase, a, (const Fr*)c->w1c.p, w, na);
 }
 // gamma powers scaled for `na` (cached with the gamma vector)
-static const Fr* gamma_scaled(svdw_ctx* c, int na) {
-    if (na >= 8) return (const Fr*)c->gpm.p;
+static WScaled gamma_scaled(svdw_ctx* c, int na) {
+    if (na >= 8) return WScaled{(const Fr*)c->gpm.p, nullptr};
+    const uint32_t len = c->gp_len;
     if (!c->dry && !(c->gps_ok >> na & 1)) {
-        ensure_buf(c, c->gps[na], (size_t)c->gp_len * sizeof(Fr));
+        ensure_buf(c, c->gps[na], 2 * (size_t)len * sizeof(Fr));
         DView w;
         memset(&w, 0, sizeof w);
         w.ptr = (const Fr*)c->gpc.p;
-        w.rs = 0; w.cs = 1; w.rows = 1; w.cols = c->gp_len;
-        hipck(launch_vec_prep(w, c->gp_len, nullptr, (Fr*)c->gps[na].p, scale_factor(na), c->st),
-              "k_vec_prep");
+        w.rs = 0; w.cs = 1; w.rows = 1; w.cols = len;
+        hipck(launch_vec_prep(w, len, nullptr, (Fr*)c->gps[na].p, (Fr*)c->gps[na].p + len,
+                              scale_factor(na), c->st), "k_vec_prep");
         c->gps_ok |= 1u << na;
     }
-    return (const Fr*)c->gps[na].p;
+    const Fr* ws = (const Fr*)c->gps[na].p;
+    return WScaled{ws, ws ? ws + len : nullptr};
 }
 // ZkMatrix::verify_mul (src/matrix/mod.rs:251-282) for several (a, b, c_s) triples
 // with one gamma: cells are appended exactly as consecutive verify_mul calls
@@ -894,8 +959,8 @@ static void verify_mul_legacy(svdw_ctx* c, uint32_t phase, const svdw_mat& a, co
     const int na_cs = scan_na(c, cs), na_b = scan_na(c, b), na_a = scan_na(c, a);
     svdw_vec csv = matvec_rows(c, phase, cs, gpc, gamma_scaled(c, na_cs), na_cs);
     svdw_vec bv = matvec_rows(c, phase, b, gpc, gamma_scaled(c, na_b), na_b);
-    vec_prep(c, bv, c->w2c, c->w2m, na_a);
-    svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, (const Fr*)c->w2m.p, na_a);
+    const WScaled w2 = vec_prep(c, bv, c->w2c, c->w2m, na_a);
+    svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, w2, na_a);
     (void)k;
     PB pb(c->LB);                                         // is_equal per row (unconstrained result)
     pb.a.view[0] = view_of(c, mat_of_vec(csv));
@@ -972,7 +1037,8 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         for (int i = 0; i < n; ++i) {
             const svdw_mat a = mat_of(i);
             const svdw_vec v = vec_of(i);
-            sb.job[i] = ScanJob{view_of(c, a), wc_of(i), ws_of(i),
+            const WScaled w = ws_of(i);
+            sb.job[i] = ScanJob{view_of(c, a), wc_of(i), w.ws, w.wn,
                                 cellp(c, phase, v.off - 3ull * a.cols), a.cols, a.rows, 0, 0};
             bytes += 32.0 * a.rows * (4.0 * a.cols + 1) + 64.0 * a.cols;
             ops += (double)a.rows * a.cols;
@@ -991,17 +1057,17 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     auto b_of = [&](int i) { return vm[i].b; };
     auto a_of = [&](int i) { return vm[i].a; };
     const int na_cs = group_na(cs_of), na_b = group_na(b_of), na_a = group_na(a_of);
-    const Fr* g_cs = gamma_scaled(c, na_cs);
-    const Fr* g_b = gamma_scaled(c, na_b);
+    const WScaled g_cs = gamma_scaled(c, na_cs);
+    const WScaled g_b = gamma_scaled(c, na_b);
     auto gc = [&](int) { return gpc; };
     run_batch("k_matvec_scan:cs", cs_of, [&](int i) { return pl[i].csv; }, gc,
               [&](int) { return g_cs; }, na_cs);
     run_batch("k_matvec_scan:b", b_of, [&](int i) { return pl[i].bv; }, gc,
               [&](int) { return g_b; }, na_b);
-    for (int i = 0; i < n; ++i) vec_prep(c, pl[i].bv, c->wbc[i], c->wbs[i], na_a);
+    WScaled wb[kMaxScanJobs];
+    for (int i = 0; i < n; ++i) wb[i] = vec_prep(c, pl[i].bv, c->wbc[i], c->wbs[i], na_a);
     run_batch("k_matvec_scan:a", a_of, [&](int i) { return pl[i].abv; },
-              [&](int i) { return (const Fr*)c->wbc[i].p; },
-              [&](int i) { return (const Fr*)c->wbs[i].p; }, na_a);
+              [&](int i) { return (const Fr*)c->wbc[i].p; }, [&](int i) { return wb[i]; }, na_a);
     for (int i = 0; i < n; ++i) {
         Plan& p = pl[i];
         p.eq.a.view[0] = view_of(c, mat_of_vec(p.csv));
@@ -1041,7 +1107,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
                                          const svdw_mat& v, const svdw_vec& d, double err_svd,
                                          double err_u, uint32_t max_bits_d,
                                          const uint32_t* known_bits = nullptr,
-                                         const unsigned* dev_slots = nullptr) {
+                                         const unsigned* dev_bits = nullptr) {
     REQUIRE(m.rows == u.rows, "check_svd_phase0: m.num_rows != u.num_rows");
     REQUIRE(m.cols == v.rows, "check_svd_phase0: m.num_col != v.num_rows");
     REQUIRE(u.rows == u.cols, "check_svd_phase0: u not square");
@@ -1059,7 +1125,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         // integer GEMMs run under the HBM-bound check stages on st. Called after
         // the first check stage is queued, so the device is busy while the host
         // waits for the operand bit lengths.
-        const bool on_device = dev_slots && c->gemm_impl == SVDW_GEMM_MFMA && c->gemm_rt;
+        const bool on_device = dev_bits && c->gemm_impl == SVDW_GEMM_MFMA && c->gemm_rt;
         if (!on_device) fetch_bits(c);
         svdw_ctx plan;
         plan.P = c->P; plan.LB = c->LB;
@@ -1076,8 +1142,8 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         const uint32_t ba[3] = {known_bits[0], known_bits[1], known_bits[2]};
         const uint32_t bb[3] = {known_bits[2], known_bits[1], known_bits[2]};
         (void)ba; (void)bb;
-        const unsigned* sl[3] = {dev_slots, dev_slots ? dev_slots + kBitSlots : nullptr,
-                                 dev_slots ? dev_slots + 2 * kBitSlots : nullptr};
+        const unsigned* sl[3] = {dev_bits, dev_bits ? dev_bits + 1 : nullptr,
+                                 dev_bits ? dev_bits + 2 : nullptr};
         const unsigned* sa[3] = {sl[0], sl[1], sl[2]};
         const unsigned* sb[3] = {sl[2], sl[1], sl[2]};
         for (int g = 0; g < 3; ++g) {
@@ -1157,21 +1223,30 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         }
     }
     unsigned* dbits = nullptr;
+    const uint32_t nbm = (uint32_t)(((uint64_t)N * M + 255) / 256);
+    const uint32_t nbu = (uint32_t)(((uint64_t)N * N + 255) / 256);
+    const uint32_t nbv = (uint32_t)(((uint64_t)M * M + 255) / 256);
     if (!c->dry) {
-        ensure_buf(c, c->bits, 3 * kBitSlots * sizeof(unsigned));
+        // [0, 3): bit-length maxima of m, u, v; from word 64: per-block maxima
+        ensure_buf(c, c->bits, (64 + nbm + nbu + nbv) * sizeof(unsigned));
         dbits = (unsigned*)c->bits.p;
-        hipck(hipMemsetAsync(dbits, 0, 3 * kBitSlots * sizeof(unsigned), c->st), "memset");
     }
-    svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device, dbits);
-    svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device, dbits ? dbits + kBitSlots : nullptr);
-    svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device, dbits ? dbits + 2 * kBitSlots : nullptr);
+    svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device, dbits ? dbits + 64 : nullptr);
+    svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device, dbits ? dbits + 64 + nbm : nullptr);
+    svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device, dbits ? dbits + 64 + nbm + nbu : nullptr);
     svdw_mat zdm = zkmatrix_new(c, 0, d, r, 1, on_device);
     svdw_vec zd{0, r, zdm.off, 1};
     double es, eu;
     err_calc(c->P, std::max(N, M), cfg.max_norm, cfg.eps_svd, cfg.eps_u, &es, &eu);
     if (!c->dry) {   // operand bit lengths (GEMM digit counts): read lazily, see fetch_bits
-        hipck(hipMemcpyAsync(c->hbits, dbits, 3 * kBitSlots * sizeof(uint32_t),
-                             hipMemcpyDeviceToHost, c->st), "D2H");
+        BitSegs seg{};
+        seg.begin[0] = 0;
+        seg.begin[1] = nbm;
+        seg.begin[2] = nbm + nbu;
+        seg.begin[3] = nbm + nbu + nbv;
+        hipck(launch_bits_reduce(dbits + 64, seg, 3, dbits, c->st), "k_bits_reduce");
+        hipck(hipMemcpyAsync(c->hbits, dbits, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st),
+              "D2H");
         hipck(hipEventRecord(c->ev_bits, c->st), "hipEventRecord");
         c->bits_pending = true;
         c->qmat[0] = zm; c->qmat[1] = zu; c->qmat[2] = zv;
@@ -1208,7 +1283,7 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
             hipError_t e = hipSetDevice(p->device);
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking);
-            if (e == hipSuccess) e = hipHostMalloc((void**)&c->hbits, 3 * kBitSlots * sizeof(uint32_t),
+            if (e == hipSuccess) e = hipHostMalloc((void**)&c->hbits, 64 * sizeof(uint32_t),
                                                hipHostMallocDefault);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bits, hipEventDisableTiming);
             if (e != hipSuccess) {
@@ -1227,7 +1302,7 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             (void)hipStreamSynchronize(c->st2);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
             for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->w1c, &c->w1m, &c->w2c, &c->w2m,
-                            &c->bits, &c->gpc, &c->gpm})
+                            &c->bits, &c->gpc, &c->gpm, &c->crtR, &c->gbits})
                 if (b->p) (void)hipFree(b->p);
             for (auto& b : c->gps) if (b.p) (void)hipFree(b.p);
             for (int i = 0; i < kMaxScanJobs; ++i) {
@@ -1458,6 +1533,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_impl = (int)value;
         } else if (n == "nt_stores") {
             c->stage_flags = (c->stage_flags & ~STAGE_NT_STORES) | (value ? STAGE_NT_STORES : 0);
+        } else if (n == "stage_sweep") {
+            REQUIRE(value >= 0 && value <= 4096, "stage_sweep: 0 (off) or a grid size <= 4096");
+            c->stage_sweep = (uint32_t)value;
         } else if (n == "stage_ilp") {
             REQUIRE(value == 1 || value == 2 || value == 4, "stage_ilp: 1, 2 or 4");
             c->stage_flags = (c->stage_flags & ~(STAGE_ILP2 | STAGE_ILP4)) |
@@ -1475,6 +1553,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                 hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
                 c->st2 = s;
             }
+        } else if (n == "gemm_crt") {
+            REQUIRE(value == 0 || value == 1, "gemm_crt: 0 or 1");
+            c->gemm_crt = (int)value;
         } else if (n == "gemm_rt") {
             REQUIRE(value == 0 || value == 1, "gemm_rt: 0 or 1");
             c->gemm_rt = (int)value;

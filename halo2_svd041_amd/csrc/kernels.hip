@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include "kernels.hpp"
+#include "crt_tables.hpp"
 
 namespace svdw {
 
@@ -64,7 +65,7 @@ __device__ __forceinline__ uint32_t signed_bits(const Fr& x) {
 // SURVEY.md Appendix C.1]
 __global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in, uint64_t n,
                                                   Fr* __restrict__ out, double scale,
-                                                  unsigned* __restrict__ maxbits) {
+                                                  unsigned* __restrict__ blockmax) {
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     // bit length of |x_q| for the GEMM digit-count choice (wave max, one atomic)
     uint32_t bits = 0;
@@ -73,19 +74,16 @@ __global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in,
         if (s >= 340282366920938463463374607431768211456.0) bits = 128;
         else if (s >= 1.0) bits = (uint32_t)ilogb(s) + 1;
     }
-    if (maxbits) {
-        // wave max -> block max (LDS) -> one atomic per block into one of
-        // kBitSlots words (a single contended word serialises the blocks at
-        // ~10 ns per atomic); the reader takes the max over the slots
+    if (blockmax) {
+        // wave max -> block max (LDS) -> one plain store per block; the maxima
+        // are folded by k_bits_reduce (no contended atomics)
         __shared__ uint32_t wmax[4];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, off));
         if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = bits;
         __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t b = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
-            if (b) atomicMax(maxbits + (blockIdx.x & (kBitSlots - 1)), b);
-        }
+        if (threadIdx.x == 0)
+            blockmax[blockIdx.x] = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
     }
     if (i >= n) return;
     double x = in[i];
@@ -105,12 +103,31 @@ __global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in,
     st_fr(out + i, neg ? fr_sub(fr_zero(), q) : q);
 }
 
-hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int p, unsigned* maxbits,
+hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int p, unsigned* blockmax,
                            hipStream_t st) {
     if (!n) return hipSuccess;
     double scale = (double)(1ull << p);
     hipLaunchKernelGGL(k_quantize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, n, out,
-                       scale, maxbits);
+                       scale, blockmax);
+    return hipGetLastError();
+}
+// block s: out[s] = max(blockmax[seg.begin[s] .. seg.begin[s + 1]))
+__global__ __launch_bounds__(256) void k_bits_reduce(const unsigned* __restrict__ blockmax,
+                                                     const BitSegs seg, unsigned* __restrict__ out) {
+    __shared__ uint32_t wmax[4];
+    const uint32_t s = blockIdx.x;
+    uint32_t b = 0;
+    for (uint32_t i = seg.begin[s] + threadIdx.x; i < seg.begin[s + 1]; i += 256) b = max(b, blockmax[i]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) b = max(b, (uint32_t)__shfl_xor((int)b, off));
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) out[s] = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+}
+hipError_t launch_bits_reduce(const unsigned* blockmax, const BitSegs& seg, uint32_t nseg,
+                              unsigned* out, hipStream_t st) {
+    if (!nseg || nseg >= (uint32_t)kMaxBitSegs) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_bits_reduce, dim3(nseg), dim3(256), 0, st, blockmax, seg, out);
     return hipGetLastError();
 }
 
@@ -207,6 +224,31 @@ __device__ __forceinline__ void stream_cells(uint4* __restrict__ out, uint32_t t
     }
 }
 
+// Sweep mode: local element l of batch jb of block b is global element
+// e_begin + G (b + nb (jb E/G + l/G)) + l % G.
+struct SweepMap {
+    uint32_t e_begin, b, nb, jb;
+    __device__ __forceinline__ uint32_t elem(uint32_t l) const {
+        return e_begin + kSweepG * (b + nb * (jb * (kStageElems / kSweepG) + l / kSweepG)) +
+               l % kSweepG;
+    }
+};
+// The batch's cells element by element: half-cell hc of local element el goes
+// to global half-cell 2 (e(el) C + slot) + h.
+__device__ __forceinline__ void stream_cells_sweep(uint4* __restrict__ out, uint32_t total,
+                                                   const SlotOp* __restrict__ ops, uint32_t C,
+                                                   uint32_t magic, const uint32_t* sK,
+                                                   const uint32_t* sV, uint32_t nv,
+                                                   const SweepMap& map) {
+    for (uint32_t hc = threadIdx.x; hc < total; hc += blockDim.x) {
+        const uint32_t c = hc >> 1, h = hc & 1;
+        const uint32_t el = fastdiv(c, C, magic), slot = c - el * C;
+        const SlotOp op = ops[slot];
+        const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + (el * nv + op.src) * VW;
+        out[((uint64_t)map.elem(el) * C + slot) * 2 + h] = extract_half(src, op.lo, op.nbits, h);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t nv = a.nv;
@@ -218,8 +260,8 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     DView* sVw = reinterpret_cast<DView*>(sMo + kMaxMicro);
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t e0 = a.e_begin + blockIdx.x * kStageElems;
-    const uint32_t ne = min((uint32_t)kStageElems, a.e_end - e0);
+    const bool sweep = (a.flags & STAGE_SWEEP) != 0;
+    SweepMap map{a.e_begin, blockIdx.x, gridDim.x, 0};
 
     for (uint32_t k = tid; k < a.nk; k += blockDim.x) lds_put(sK + k * VW, a.K[k]);
     for (uint32_t k = tid; k < a.C; k += blockDim.x) sAdv[k] = a.adv[k];
@@ -228,10 +270,21 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     if (tid < kMaxViews) sVw[tid] = a.view[tid];
     __syncthreads();
 
+  for (;; ++map.jb) {
+    uint32_t e0, ne, e;
+    if (sweep) {
+        if (map.elem(0) >= a.e_end) break;                // uniform: this block is done
+        e = map.elem(tid);
+        ne = __syncthreads_count(e < a.e_end);            // valid elements form a prefix
+        e0 = 0;
+    } else {
+        e0 = a.e_begin + blockIdx.x * kStageElems;
+        ne = min((uint32_t)kStageElems, a.e_end - e0);
+        e = e0 + tid;
+    }
     // ---- phase A: per-element micro-ops (constants / ops / views read from LDS:
     // dynamic indexing into the by-value kernel argument would go to scratch)
     if (tid < ne) {
-        const uint32_t e = e0 + tid;
         const uint32_t i = e / a.cols, j = e - (e / a.cols) * a.cols;
         uint32_t* myV = sV + tid * nv * VW;
         for (uint32_t m = 0; m < a.nmo; ++m) {
@@ -300,6 +353,15 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     __syncthreads();
 
     // ---- phase B: advice cells, then lookup cells
+    if (sweep) {
+        stream_cells_sweep(reinterpret_cast<uint4*>(a.out_adv), 2 * ne * a.C, sAdv, a.C,
+                           a.cdiv_magic, sK, sV, nv, map);
+        if (a.L)
+            stream_cells_sweep(reinterpret_cast<uint4*>(a.out_lk), 2 * ne * a.L, sLk, a.L,
+                               a.ldiv_magic, sK, sV, nv, map);
+        __syncthreads();                                  // LDS values reused by the next batch
+        continue;
+    }
     uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
     uint4* outL = a.L ? reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L) : nullptr;
 #define SVDW_STREAM(NT, U)                                                                         \
@@ -312,13 +374,22 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     else if (a.flags & STAGE_ILP2) SVDW_STREAM(false, 2);
     else SVDW_STREAM(false, 1);
 #undef SVDW_STREAM
+    break;
+  }
 }
 
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     if (a.e_end <= a.e_begin) return hipSuccess;
     const uint32_t n = a.e_end - a.e_begin;
     const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1);
-    hipLaunchKernelGGL(k_stage, dim3((n + kStageElems - 1) / kStageElems), dim3(256), lds, st, a);
+    uint32_t grid = (n + kStageElems - 1) / kStageElems;
+    if (a.flags & STAGE_SWEEP) {
+        // persistent blocks; every block needs at least one group
+        const uint32_t groups = (n + kSweepG - 1) / kSweepG;
+        grid = a.sweep_nb < groups ? a.sweep_nb : groups;
+        if (!grid) return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(k_stage, dim3(grid), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 
@@ -334,16 +405,19 @@ __global__ __launch_bounds__(256) void k_maxbits(const DView v, uint32_t rows, u
         Fr x = view_load(v, zero, i, j);
         best = max(best, signed_bits(x));
     }
+    __shared__ uint32_t wmax[4];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) best = max(best, (uint32_t)__shfl_xor((int)best, off));
-    if ((threadIdx.x & 63) == 0 && best) atomicMax(out + (blockIdx.x & (kBitSlots - 1)), best);
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) out[blockIdx.x] = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
 }
 
 hipError_t launch_maxbits(const DView& v, uint32_t rows, uint32_t cols, unsigned* out,
                           hipStream_t st) {
     uint64_t n = (uint64_t)rows * cols;
     if (!n) return hipSuccess;
-    unsigned blocks = (unsigned)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+    unsigned blocks = (unsigned)((n + 255) / 256 < kMaxBitBlocks ? (n + 255) / 256 : kMaxBitBlocks);
     hipLaunchKernelGGL(k_maxbits, dim3(blocks), dim3(256), 0, st, v, rows, cols, out);
     return hipGetLastError();
 }
@@ -552,13 +626,11 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 constexpr int MT = 32;        // block tile (2 x 2 waves of 16 x 16)
 constexpr int LROW = 80;      // LDS bytes per (digit, row): 64 + 16 pad
 
-// Digit planes chosen on the device from kBitSlots bit-length maxima (the
+// Digit planes chosen on the device from an operand's bit-length maximum (the
 // engine's digits_for_bits + round_digits): 5, 8 or 9 planes, 0 = too wide for
 // the digit GEMM (Montgomery fallback).
-__device__ __forceinline__ int device_digits(const unsigned* __restrict__ slots) {
-    uint32_t b = 0;
-#pragma unroll 8
-    for (int s = 0; s < kBitSlots; ++s) b = max(b, slots[s]);
+__device__ __forceinline__ int device_digits(const unsigned* __restrict__ bits) {
+    const uint32_t b = *bits;
     const int need = b <= 7 ? 1 : (int)((b + 9) / 8);
     return need <= 5 ? 5 : need <= 8 ? 8 : need <= 9 ? 9 : 0;
 }
@@ -566,9 +638,9 @@ __device__ __forceinline__ int device_digits(const unsigned* __restrict__ slots)
 __global__ __launch_bounds__(256) void k_to_digits_mf(const DView x, uint32_t rows, uint32_t kdim,
                                                       int D, uint32_t rows_pad, uint32_t kcn,
                                                       uint32_t* __restrict__ out,
-                                                      const unsigned* __restrict__ slots) {
-    if (slots) {
-        D = device_digits(slots);
+                                                      const unsigned* __restrict__ dbits) {
+    if (dbits) {
+        D = device_digits(dbits);
         if (!D) return;
     }
     uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -616,11 +688,11 @@ __global__ __launch_bounds__(256) void k_to_digits_mf(const DView x, uint32_t ro
 }
 
 hipError_t launch_to_digits_mf(const DView& x, uint32_t rows, uint32_t kdim, int D, uint32_t rows_pad,
-                               uint32_t kcn, uint32_t* out, hipStream_t st, const unsigned* slots) {
+                               uint32_t kcn, uint32_t* out, hipStream_t st, const unsigned* dbits) {
     uint64_t n = (uint64_t)rows_pad * kcn * 16;
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_to_digits_mf, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, rows,
-                       kdim, D, rows_pad, kcn, out, slots);
+                       kdim, D, rows_pad, kcn, out, dbits);
     return hipGetLastError();
 }
 
@@ -756,15 +828,15 @@ __global__ __launch_bounds__(256) void k_gemm_mfma_rt(const uint8_t* __restrict_
 }
 hipError_t launch_gemm_mfma_rt(bool sym, const uint8_t* Ad, const uint8_t* Bd, uint32_t N,
                                uint32_t M, uint32_t kcn, Fr* out, int64_t ors, int64_t ocs,
-                               const unsigned* slots_a, const unsigned* slots_b, hipStream_t st) {
+                               const unsigned* bits_a, const unsigned* bits_b, hipStream_t st) {
     uint32_t tn = (N + MT - 1) / MT, tm = (M + MT - 1) / MT;
     if (sym) {
         if (N != M) return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_gemm_mfma_rt<true>, dim3(tm * (tm + 1) / 2), dim3(256), 0, st, Ad, Ad, N,
-                           M, kcn, out, ors, ocs, tm, slots_a, slots_a);
+                           M, kcn, out, ors, ocs, tm, bits_a, bits_a);
     } else {
         hipLaunchKernelGGL(k_gemm_mfma_rt<false>, dim3(tn * tm), dim3(256), 0, st, Ad, Bd, N, M, kcn,
-                           out, ors, ocs, tm, slots_a, slots_b);
+                           out, ors, ocs, tm, bits_a, bits_b);
     }
     return hipGetLastError();
 }
@@ -796,12 +868,365 @@ hipError_t launch_gemm_mfma(int DA, int DB, bool sym, const uint8_t* Ad, const u
     return hipErrorInvalidValue;
 }
 
+// ------------------------------------------- multi-modular (CRT) exact GEMM
+// c_s = A * Bt exactly for |A| < 2^ba, |B| < 2^bb (ba, bb <= 128): with n
+// pairwise coprime moduli m_k <= 256 whose product Mtot exceeds 2^(ba+bb+lk+2),
+// every residue product C mod m_k is one plain int8 GEMM of the balanced
+// residue planes (|r| <= 128, K <= 2^17 keeps the i32 sums exact), and C is
+// rebuilt from its n residues (crt_tables.hpp). ~19 int8 GEMMs at P = 63
+// instead of 72 digit-pair products. n is decided on the device from the
+// operand bit-length words, like the digit path.
+__device__ __forceinline__ int crt_nmod(uint32_t ba, uint32_t bb, uint32_t lk) {
+    if (ba > 128 || bb > 128) return 0;
+    const uint32_t need = ba + bb + lk + 2;
+    for (int n = 1; n <= kCrtMaxMod; ++n)
+        if (c_crt_cum_bits[n] >= need) return n;
+    return 0;
+}
+
+// NH 16-bit halves of |x| per element (|x| < 2^(16 NH)); moduli loop unrolled
+// so the table loads are scalar and hoisted.
+template <int NH>
+__device__ __forceinline__ void residues_body(const DView& x, uint32_t rows, uint32_t kdim,
+                                              uint32_t rows_pad, uint32_t kw,
+                                              uint32_t* __restrict__ out, int n, uint32_t row,
+                                              uint32_t kg, const Fr& half) {
+    const Fr zero = fr_zero();
+    uint32_t h[4][NH];
+    bool neg[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const uint32_t kk = kg * 4 + t;
+        Fr v = zero;
+        if (row < rows && kk < kdim) v = view_load(x, zero, row, kk);
+        Fr tmp;
+        neg[t] = sub256(tmp, half, v) != 0;
+        const Fr mag = neg[t] ? fr_sub(zero, v) : v;
+#pragma unroll
+        for (int j = 0; j < NH; ++j) h[t][j] = (mag.w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+    }
+    uint32_t* o = out + (uint64_t)row * kw + kg;
+    const uint64_t plane = (uint64_t)rows_pad * kw;
+#pragma unroll
+    for (int k = 0; k < kCrtMaxMod; ++k) {
+        if (k >= n) break;
+        const int m = (int)c_crt_mod[k];
+        const float inv = c_crt_invf[k];
+        uint32_t word = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            uint32_t s = 0;
+#pragma unroll
+            for (int j = 0; j < NH; ++j) s = __umul24(h[t][j], c_crt_pow16[k][j]) + s;   // < 2^27
+            // quotient from fp32 (off by at most one for m >= 71), 24-bit products
+            const int q = (int)((float)s * inv);
+            int r = (int)s - __mul24(q, m);
+            r += r < 0 ? m : 0;
+            r -= r >= m ? m : 0;
+            if (neg[t] && r) r = m - r;
+            if (2 * r >= m) r -= m;                            // balanced: [-128, 127]
+            word |= ((uint32_t)r & 0xffu) << (8 * t);
+        }
+        o[k * plane] = word;
+    }
+}
+// Balanced residue planes: out[k][row][kpad] int8 (= u32 words of 4 consecutive
+// k), k < n; rows >= `rows` and columns >= kdim are zero.
+__global__ __launch_bounds__(256) void k_to_residues(const DView x, uint32_t rows, uint32_t kdim,
+                                                     uint32_t rows_pad, uint32_t kw,
+                                                     uint32_t* __restrict__ out,
+                                                     const unsigned* __restrict__ bits_a,
+                                                     const unsigned* __restrict__ bits_b,
+                                                     uint32_t lk) {
+    const int n = crt_nmod(*bits_a, *bits_b, lk);
+    if (!n) return;
+    const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (uint64_t)rows_pad * kw) return;
+    const uint32_t row = (uint32_t)(idx / kw), kg = (uint32_t)(idx % kw);
+    Fr half = fr_p();
+    {
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 7; i >= 0; --i) {
+            const uint32_t nw = (half.w[i] >> 1) | c;
+            c = half.w[i] << 31;
+            half.w[i] = nw;
+        }
+    }
+    const uint32_t bmax = max(*bits_a, *bits_b);
+    if (bmax <= 64)
+        residues_body<4>(x, rows, kdim, rows_pad, kw, out, n, row, kg, half);
+    else if (bmax <= 96)
+        residues_body<6>(x, rows, kdim, rows_pad, kw, out, n, row, kg, half);
+    else
+        residues_body<8>(x, rows, kdim, rows_pad, kw, out, n, row, kg, half);
+}
+hipError_t launch_to_residues(const DView& x, uint32_t rows, uint32_t kdim, uint32_t rows_pad,
+                              uint32_t kpad, uint32_t* out, const unsigned* bits_a,
+                              const unsigned* bits_b, uint32_t lk, hipStream_t st) {
+    const uint64_t n = (uint64_t)rows_pad * (kpad / 4);
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_to_residues, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, rows,
+                       kdim, rows_pad, kpad / 4, out, bits_a, bits_b, lk);
+    return hipGetLastError();
+}
+
+static constexpr int CT = 128;     // CRT GEMM block tile (4 waves of 64 x 64)
+static constexpr int CROW = 80;    // LDS bytes per staged row (64 + 16 pad)
+
+// One (128 x 128 tile, modulus) per block: residues of C mod m_k as bytes
+// R[k][row][rpad_m]. SYM: A == B, upper tiles only.
+template <bool SYM>
+__global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar,
+                                                  const uint8_t* __restrict__ Br, uint32_t rpad_a,
+                                                  uint32_t rpad_b, uint32_t kpad, uint32_t tiles_m,
+                                                  uint8_t* __restrict__ R,
+                                                  const unsigned* __restrict__ bits_a,
+                                                  const unsigned* __restrict__ bits_b, uint32_t lk) {
+    const int n = crt_nmod(*bits_a, *bits_b, lk);
+    const int mod = blockIdx.y;
+    if (mod >= n) return;
+    __shared__ __attribute__((aligned(16))) uint8_t S[2 * CT * CROW];
+    uint8_t* As = S;
+    uint8_t* Bs = S + CT * CROW;
+    uint32_t bi, bj;
+    if (SYM) {
+        uint32_t b = blockIdx.x, r = 0, rowlen = tiles_m;
+        while (b >= rowlen) { b -= rowlen; ++r; --rowlen; }
+        bi = r; bj = r + b;
+    } else {
+        bi = blockIdx.x / tiles_m;
+        bj = blockIdx.x % tiles_m;
+    }
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t wr = wave >> 1, wc = wave & 1;
+    const uint8_t* Ap = Ar + ((uint64_t)mod * rpad_a + bi * CT) * kpad;
+    const uint8_t* Bp = Br + ((uint64_t)mod * rpad_b + bj * CT) * kpad;
+    // staging map: 512 x 16 B per operand chunk; thread -> (row, part) for q = tid, tid + 256
+    const uint32_t r0 = tid >> 2, r1 = (tid + 256) >> 2, part = tid & 3;
+    uint4 ra0, ra1, rb0, rb1;
+    auto gload = [&](uint32_t kc) {
+        const uint64_t ko = (uint64_t)kc * 64 + part * 16;
+        ra0 = *reinterpret_cast<const uint4*>(Ap + (uint64_t)r0 * kpad + ko);
+        ra1 = *reinterpret_cast<const uint4*>(Ap + (uint64_t)r1 * kpad + ko);
+        rb0 = *reinterpret_cast<const uint4*>(Bp + (uint64_t)r0 * kpad + ko);
+        rb1 = *reinterpret_cast<const uint4*>(Bp + (uint64_t)r1 * kpad + ko);
+    };
+    v4i acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = v4i{0, 0, 0, 0};
+    const uint32_t kcn = kpad / 64;
+    const uint32_t frow = lane & 15, fk = (lane >> 4) * 16;
+    gload(0);
+    for (uint32_t kc = 0; kc < kcn; ++kc) {
+        *reinterpret_cast<uint4*>(As + r0 * CROW + part * 16) = ra0;
+        *reinterpret_cast<uint4*>(As + r1 * CROW + part * 16) = ra1;
+        *reinterpret_cast<uint4*>(Bs + r0 * CROW + part * 16) = rb0;
+        *reinterpret_cast<uint4*>(Bs + r1 * CROW + part * 16) = rb1;
+        __syncthreads();
+        if (kc + 1 < kcn) gload(kc + 1);                      // next chunk in flight
+        v4i af[4], bf[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+            af[a] = *reinterpret_cast<const v4i*>(As + (wr * 64 + a * 16 + frow) * CROW + fk);
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            bf[b] = *reinterpret_cast<const v4i*>(Bs + (wc * 64 + b * 16 + frow) * CROW + fk);
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
+        __syncthreads();
+    }
+    // residues -> 128 x 128 byte tile in LDS -> 128 B rows
+    const int m = (int)c_crt_mod[mod];
+    const float inv = c_crt_invf[mod];
+    uint8_t* T = S;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                // |acc| <= 2^27: fp32 quotient off by at most one (m >= 71)
+                const int av = acc[a][b][reg];
+                const int q = (int)floorf((float)av * inv);
+                int r = av - __mul24(q, m);
+                r += r < 0 ? m : 0;
+                r -= r >= m ? m : 0;
+                const uint32_t tr = wr * 64 + a * 16 + (lane >> 4) * 4 + reg;
+                const uint32_t tc = wc * 64 + b * 16 + (lane & 15);
+                T[tr * CT + tc] = (uint8_t)r;
+            }
+    __syncthreads();
+    uint8_t* Rp = R + ((uint64_t)mod * rpad_a + bi * CT) * (uint64_t)rpad_b + bj * CT;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t e = tid + q * 256, tr = e >> 3, c16 = (e & 7) * 16;
+        *reinterpret_cast<uint4*>(Rp + (uint64_t)tr * rpad_b + c16) =
+            *reinterpret_cast<const uint4*>(T + tr * CT + c16);
+    }
+}
+
+// x mod p for a 9-word x < 2^270
+__device__ __forceinline__ Fr reduce9(const uint32_t (&x)[9]) {
+    const double two32 = 4294967296.0;
+    const double xd = ((double)x[8] * two32 + (double)x[7]) * two32 + (double)x[6];
+    const double pd = ((double)p_word(7) * two32 + (double)p_word(6)) + (double)p_word(5) / two32;
+    const double qd = floor(xd / pd) - 1.0;
+    const uint32_t q = qd > 0.0 ? (uint32_t)qd : 0u;
+    Fr r;
+    uint64_t carry = 0;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint64_t pr = (uint64_t)q * p_word(i) + carry;
+        carry = pr >> 32;
+        const uint64_t d = (uint64_t)x[i] - (uint32_t)pr - br;
+        r.w[i] = (uint32_t)d;
+        br = (uint32_t)(d >> 63);
+    }
+    // x - q p < 3p < 2^256: the ninth word is gone; two conditional subtractions
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        Fr t;
+        const uint32_t b = sub256(t, r, fr_p());
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.w[i] = b ? r.w[i] : t.w[i];
+    }
+    return r;
+}
+
+// C from its n residues, written as canonical Fr to out[i*ors + j*ocs]; one
+// 32 x 32 tile per block (SYM: upper tiles, mirrored through LDS).
+template <bool SYM>
+__global__ __launch_bounds__(256) void k_crt_combine(const uint8_t* __restrict__ R, uint32_t rpad_a,
+                                                     uint32_t rpad_b, uint32_t N, uint32_t M,
+                                                     uint32_t tiles_m, Fr* __restrict__ out,
+                                                     int64_t ors, int64_t ocs,
+                                                     const unsigned* __restrict__ bits_a,
+                                                     const unsigned* __restrict__ bits_b, uint32_t lk) {
+    const int n = crt_nmod(*bits_a, *bits_b, lk);
+    if (!n) return;
+    __shared__ __attribute__((aligned(16))) uint8_t Ts[MT * MT * 32];
+    uint32_t bi, bj;
+    if (SYM) {
+        uint32_t b = blockIdx.x, r = 0, rowlen = tiles_m;
+        while (b >= rowlen) { b -= rowlen; ++r; --rowlen; }
+        bi = r; bj = r + b;
+    } else {
+        bi = blockIdx.x / tiles_m;
+        bj = blockIdx.x % tiles_m;
+    }
+    const uint32_t tid = threadIdx.x;
+    const uint32_t i0 = bi * MT, j0 = bj * MT;
+    const int off = n * (n - 1) / 2;
+    const uint64_t plane = (uint64_t)rpad_a * rpad_b;
+    // four elements per thread (rows tr0 + 8 q, one column), interleaved for ILP
+    const uint32_t tc = tid & 31, tr0 = tid >> 5;
+    const uint8_t* rp = R + (uint64_t)(i0 + tr0) * rpad_b + j0 + tc;
+    // 16 accumulators per element, one per 16-bit limb of ep: r (8 bit) x limb
+    // (16 bit) < 2^24, n <= 40 terms plus q x nmp stay below 2^31 -> no carries
+    uint32_t acc[4][16];
+    double s[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        s[q] = 0.0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) acc[q][w] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kCrtMaxMod; ++k) {
+        if (k >= n) break;
+        uint32_t r[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[q] = rp[k * plane + (uint64_t)q * 8 * rpad_b];
+        const double fr = c_crt_frac[off + k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[q] = fma((double)r[q], fr, s[q]);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const uint32_t e = c_crt_ep[off + k][w], lo = e & 0xffffu, hi = e >> 16;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                acc[q][2 * w] = __umul24(r[q], lo) + acc[q][2 * w];
+                acc[q][2 * w + 1] = __umul24(r[q], hi) + acc[q][2 * w + 1];
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t qq = (uint32_t)floor(s[q] + 0.5);   // < 2^14
+        uint32_t x[9];
+        uint64_t t = 0;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const uint32_t e = c_crt_nmp[n][w];
+            t += (uint64_t)(__umul24(qq, e & 0xffffu) + acc[q][2 * w]) +
+                 ((uint64_t)(__umul24(qq, e >> 16) + acc[q][2 * w + 1]) << 16);
+            x[w] = (uint32_t)t;
+            t >>= 32;
+        }
+        x[8] = (uint32_t)t;
+        const Fr v = reduce9(x);
+        const uint32_t tr = tr0 + 8 * q;
+        uint4* dst = reinterpret_cast<uint4*>(Ts + (tr * MT + tc) * 32);
+        dst[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+        dst[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+    }
+    __syncthreads();
+    for (uint32_t q = tid; q < MT * 64; q += 256) {
+        const uint32_t tr = q >> 6, hc = q & 63, tc = hc >> 1, h = hc & 1;
+        const uint32_t row = i0 + tr, col = j0 + tc;
+        if (row < N && col < M)
+            reinterpret_cast<uint4*>(out + (int64_t)row * ors + (int64_t)col * ocs)[h] =
+                reinterpret_cast<const uint4*>(Ts + (tr * MT + tc) * 32)[h];
+    }
+    if (SYM && bi != bj) {
+        for (uint32_t q = tid; q < MT * 64; q += 256) {
+            const uint32_t tc = q >> 6, hc = q & 63, tr = hc >> 1, h = hc & 1;
+            const uint32_t row = j0 + tc, col = i0 + tr;
+            if (row < M && col < N)
+                reinterpret_cast<uint4*>(out + (int64_t)row * ors + (int64_t)col * ocs)[h] =
+                    reinterpret_cast<const uint4*>(Ts + (tr * MT + tc) * 32)[h];
+        }
+    }
+}
+
+hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
+                           uint32_t rpad_a, uint32_t rpad_b, uint32_t kpad, uint8_t* R, Fr* out,
+                           int64_t ors, int64_t ocs, const unsigned* bits_a,
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st) {
+    if (rpad_a % CT || rpad_b % CT || kpad % 64) return hipErrorInvalidValue;
+    const uint32_t ta = rpad_a / CT, tb = rpad_b / CT;
+    const uint32_t sa = (N + MT - 1) / MT, sb = (M + MT - 1) / MT;
+    if (sym) {
+        if (N != M || rpad_a != rpad_b) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_gemm_crt<true>, dim3(ta * (ta + 1) / 2, kCrtMaxMod), dim3(256), 0, st,
+                           Ar, Ar, rpad_a, rpad_b, kpad, ta, R, bits_a, bits_b, lk);
+        hipLaunchKernelGGL(k_crt_combine<true>, dim3(sa * (sa + 1) / 2), dim3(256), 0, st, R, rpad_a,
+                           rpad_b, N, M, sa, out, ors, ocs, bits_a, bits_b, lk);
+    } else {
+        hipLaunchKernelGGL(k_gemm_crt<false>, dim3(ta * tb, kCrtMaxMod), dim3(256), 0, st, Ar, Br,
+                           rpad_a, rpad_b, kpad, tb, R, bits_a, bits_b, lk);
+        hipLaunchKernelGGL(k_crt_combine<false>, dim3(sa * sb), dim3(256), 0, st, R, rpad_a, rpad_b,
+                           N, M, sb, out, ors, ocs, bits_a, bits_b, lk);
+    }
+    return hipGetLastError();
+}
+
 // -------------------------------------------------------- Montgomery GEMM
 __global__ __launch_bounds__(256) void k_gemm_mont(const DView A, const DView B, uint32_t N,
                                                    uint32_t K, uint32_t M, Fr* out, int64_t ors,
                                                    int64_t ocs, const unsigned* __restrict__ sa,
-                                                   const unsigned* __restrict__ sb) {
-    if (sa && device_digits(sa) && device_digits(sb)) return;   // digit GEMM took it
+                                                   const unsigned* __restrict__ sb, int crt_lk) {
+    if (sa) {   // the digit (crt_lk < 0) or CRT GEMM already produced the product
+        if (crt_lk < 0 ? (device_digits(sa) && device_digits(sb)) : crt_nmod(*sa, *sb, crt_lk) > 0)
+            return;
+    }
     uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (uint64_t)N * M) return;
     uint32_t i = (uint32_t)(e / M), j = (uint32_t)(e % M);
@@ -817,26 +1242,29 @@ __global__ __launch_bounds__(256) void k_gemm_mont(const DView A, const DView B,
 
 hipError_t launch_gemm_mont(const DView& A, const DView& B, uint32_t N, uint32_t K, uint32_t M,
                             Fr* out, int64_t ors, int64_t ocs, hipStream_t st,
-                            const unsigned* slots_a, const unsigned* slots_b) {
+                            const unsigned* bits_a, const unsigned* bits_b, int crt_lk) {
     uint64_t n = (uint64_t)N * M;
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_gemm_mont, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A, B, N, K,
-                       M, out, ors, ocs, slots_a, slots_b);
+                       M, out, ors, ocs, bits_a, bits_b, crt_lk);
     return hipGetLastError();
 }
 
 // ------------------------------------------------------------ vectors
-__global__ void k_vec_prep(const DView w, uint32_t L, Fr* wc, Fr* ws, const Fr f) {
+__global__ void k_vec_prep(const DView w, uint32_t L, Fr* wc, Fr* ws, Fr* wsn, const Fr f) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= L) return;
     Fr zero = fr_zero();
     Fr v = view_load(w, zero, 0, j);
     if (wc) st_fr(wc + j, v);
-    st_fr(ws + j, mont_mul(v, f));
+    const Fr s = mont_mul(v, f);
+    st_fr(ws + j, s);
+    if (wsn) st_fr(wsn + j, fr_neg(s));
 }
-hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* wc, Fr* ws, const Fr& f, hipStream_t st) {
+hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* wc, Fr* ws, Fr* wsn, const Fr& f,
+                           hipStream_t st) {
     if (!L) return hipSuccess;
-    hipLaunchKernelGGL(k_vec_prep, dim3((L + 255) / 256), dim3(256), 0, st, w, L, wc, ws, f);
+    hipLaunchKernelGGL(k_vec_prep, dim3((L + 255) / 256), dim3(256), 0, st, w, L, wc, ws, wsn, f);
     return hipGetLastError();
 }
 __global__ void k_gamma_vec(const Fr g, uint32_t L, int nbits, Fr* wc, Fr* wm) {
@@ -909,7 +1337,7 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
     static_assert(256 % T == 0, "T divides the block");
     constexpr uint32_t TPR = 256 / T;                     // threads staged per round
     __shared__ __attribute__((aligned(16))) uint32_t stage[3 * 256 * 8];
-    __shared__ Fr wtot[4];
+    __shared__ Fr wtot[4], wpre[4], carry_s;
     ScanJob J = B.job[0];
 #pragma unroll
     for (int q = 1; q < kMaxScanJobs; ++q)
@@ -918,13 +1346,16 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
     const uint32_t L = J.L;
     const Fr* __restrict__ wc = J.wc;
     const Fr* __restrict__ wm = J.ws;
+    const Fr* __restrict__ wn = J.wsn;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t lb = blockIdx.x - J.blk0;
     const uint32_t rb = (J.blk0 & 7) ? lb : scan_row(lb, J.rows), r = J.r_begin + rb;
     Fr* rowout = J.out + (uint64_t)rb * (3ull * L + 1);
     const Fr zero = fr_zero();
-    if (tid == 0) st_fr(rowout, zero);
-    Fr carry = fr_zero();
+    if (tid == 0) {
+        st_fr(rowout, zero);
+        carry_s = zero;
+    }
     for (uint32_t c0 = 0; c0 < L; c0 += 256 * T) {
         const uint32_t j0 = c0 + tid * T;
         Fr a[T], s[T];
@@ -932,21 +1363,39 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
         for (int i = 0; i < T; ++i) {
             const uint32_t j = j0 + i;
             a[i] = j < L ? view_load(A, zero, r, j) : zero;
-            if constexpr (NA == 8)
+            if constexpr (NA == 8) {
                 s[i] = j < L ? mont_mul(a[i], ld_fr(wm + j)) : zero;
-            else
-                s[i] = j < L ? fr_mul_small_signed<NA>(a[i], ld_fr(wm + j)) : zero;
+            } else {
+                // |signed a| < 2^(32 NA): a negative value p - x has a non-zero top
+                // word; multiply |a| (NA words) by w or by the pre-negated -w
+                const bool neg = a[i].w[7] != 0;
+                Fr mag = zero;
+                uint32_t br = 0;
+#pragma unroll
+                for (int q = 0; q < NA; ++q) {
+                    const uint64_t t = (uint64_t)p_word(q) - a[i].w[q] - br;
+                    br = (uint32_t)(t >> 63);
+                    mag.w[q] = neg ? (uint32_t)t : a[i].w[q];
+                }
+                s[i] = j < L ? mont_mul_small<NA>(mag, ld_fr((neg ? wn : wm) + j)) : zero;
+            }
         }
 #pragma unroll
         for (int i = 1; i < T; ++i) s[i] = fr_add(s[i], s[i - 1]);
         const Fr tot = wave_scan_fr(s[T - 1]);
         if (lane == 63) wtot[wave] = tot;
         __syncthreads();
-        Fr pre = fr_add(fr_sub(tot, s[T - 1]), carry);
-        for (uint32_t w2 = 0; w2 < wave; ++w2) pre = fr_add(pre, wtot[w2]);
-        Fr ctot = carry;
+        if (tid == 0) {                                   // wave prefixes and the running carry
+            Fr acc = carry_s;
 #pragma unroll
-        for (int w2 = 0; w2 < 4; ++w2) ctot = fr_add(ctot, wtot[w2]);
+            for (int w2 = 0; w2 < 4; ++w2) {
+                wpre[w2] = acc;
+                acc = fr_add(acc, wtot[w2]);
+            }
+            carry_s = acc;
+        }
+        __syncthreads();
+        const Fr pre = fr_add(fr_sub(tot, s[T - 1]), wpre[wave]);
 #pragma unroll
         for (int q = 0; q < T; ++q) {
             const uint32_t t0 = c0 + q * 256;                 // first term of this round
@@ -973,7 +1422,6 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
             for (uint32_t hc = tid; hc < 2 * ncell; hc += 256) o[hc] = sv[hc];
             __syncthreads();
         }
-        carry = ctot;
     }
 }
 
@@ -1119,7 +1567,8 @@ hipError_t launch_scan_batch(const ScanBatch& b0, int T, int na, hipStream_t st)
     return hipGetLastError();
 }
 hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
-                              const Fr* wc, const Fr* wm, Fr* out, int impl, int na, hipStream_t st) {
+                              const Fr* wc, const Fr* wm, const Fr* wn, Fr* out, int impl, int na,
+                              hipStream_t st) {
     if (r_end <= r_begin || !L) return hipSuccess;
     if (impl == 1)
         hipLaunchKernelGGL(k_matvec_scan_v1, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L,
@@ -1128,7 +1577,7 @@ hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, 
         ScanBatch b;
         memset(&b, 0, sizeof b);
         b.njobs = 1;
-        b.job[0] = ScanJob{A, wc, wm, out, L, r_end - r_begin, 0, r_begin};
+        b.job[0] = ScanJob{A, wc, wm, wn, out, L, r_end - r_begin, 0, r_begin};
         return launch_scan_batch(b, impl == 3 ? 1 : impl == 4 ? 2 : 4, impl == 3 ? 8 : na, st);
     } else
         hipLaunchKernelGGL(k_matvec_scan, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L, wc,

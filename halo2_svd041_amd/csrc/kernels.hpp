@@ -15,6 +15,7 @@ struct ScanJob {
     DView A;
     const Fr* wc;
     const Fr* ws;
+    const Fr* wsn;   // -ws (na < 8)
     Fr* out;
     uint32_t L, rows, blk0, r_begin;
 };
@@ -27,16 +28,23 @@ struct ScanBatch {
 // Elements per block of the generic stage kernel (= block size; LDS: E * nv * 32 B).
 static constexpr int kStageElems = 256;
 
-// Bit-length maxima are accumulated into kBitSlots words (atomicMax spread by
-// block); the result is the max over the slots.
-static constexpr int kBitSlots = 64;
 // ZkMatrix::new / ZkVector::new quantization (f64 -> Fr) of n contiguous values.
-// maxbits (nullable, kBitSlots words): bit-length(|x_q|) maxima.
+// blockmax (nullable, ceil(n / 256) words): per-block max of bit-length(|x_q|).
 hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int precision_bits,
-                           unsigned* maxbits, hipStream_t st);
+                           unsigned* blockmax, hipStream_t st);
+// Fold per-block maxima: out[s] = max(blockmax[begin[s] .. begin[s + 1])), s < nseg.
+static constexpr int kMaxBitSegs = 8;
+struct BitSegs {
+    uint32_t begin[kMaxBitSegs];
+};
+hipError_t launch_bits_reduce(const unsigned* blockmax, const BitSegs& seg, uint32_t nseg,
+                              unsigned* out, hipStream_t st);
+// k_maxbits grid bound (= words written to `out`).
+static constexpr uint32_t kMaxBitBlocks = 2048;
 // Generic cell-program stage over elements [a.e_begin, a.e_end).
 hipError_t launch_stage(const StageArgs& a, hipStream_t st);
-// max over the view of bit-length(|signed(x)|) -> out[kBitSlots] slot maxima.
+// max over the view of bit-length(|signed(x)|): out[b] = max of block b
+// (min(ceil(rows * cols / 256), kMaxBitBlocks) blocks).
 hipError_t launch_maxbits(const DView& v, uint32_t rows, uint32_t cols, unsigned* out,
                           hipStream_t st);
 // Balanced base-256 digit planes of X (rows x kdim): out[row][kg][D] int32 words,
@@ -50,29 +58,45 @@ hipError_t launch_gemm_digits(int DA, int DB, bool sym, const uint32_t* Ad, cons
                               int64_t ocs, hipStream_t st);
 bool gemm_digits_supported(int DA, int DB);
 // Matrix-core variant: digit planes laid out [row][kc][D][64 B] (kc = 64-k chunks).
-// slots (nullable, kBitSlots words): take D from the device-side bit maxima
+// dbits (nullable, one word): take D from this device-side bit-length maximum
 // instead (5 / 8 / 9 planes; nothing written when wider than 9 digits).
 hipError_t launch_to_digits_mf(const DView& x, uint32_t rows, uint32_t kdim, int D, uint32_t rows_pad,
                                uint32_t kcn, uint32_t* out, hipStream_t st,
-                               const unsigned* slots = nullptr);
+                               const unsigned* dbits = nullptr);
 hipError_t launch_gemm_mfma(int DA, int DB, bool sym, const uint8_t* Ad, const uint8_t* Bd,
                             uint32_t N, uint32_t M, uint32_t kcn, Fr* out, int64_t ors,
                             int64_t ocs, hipStream_t st);
-// Same product with DA / DB read from bit-maxima slots on the device (planes
-// laid out for those counts by launch_to_digits_mf with the same slots); a
+// Same product with DA / DB decided on the device from bit-length words (planes
+// laid out for those counts by launch_to_digits_mf with the same words); a
 // no-op when either operand is wider than 9 digits.
 hipError_t launch_gemm_mfma_rt(bool sym, const uint8_t* Ad, const uint8_t* Bd, uint32_t N,
                                uint32_t M, uint32_t kcn, Fr* out, int64_t ors, int64_t ocs,
-                               const unsigned* slots_a, const unsigned* slots_b, hipStream_t st);
+                               const unsigned* bits_a, const unsigned* bits_b, hipStream_t st);
 // Generic Montgomery GEMM (any field elements): out = A(NxK) * B(KxM). With
-// slots, a no-op unless an operand is too wide for the digit GEMM.
+// bit-length words, a no-op unless an operand is too wide for the digit GEMM.
+// crt_lk >= 0: the skip test is the CRT GEMM's (ceil(log2 K) = crt_lk).
 hipError_t launch_gemm_mont(const DView& A, const DView& B, uint32_t N, uint32_t K, uint32_t M,
                             Fr* out, int64_t ors, int64_t ocs, hipStream_t st,
-                            const unsigned* slots_a = nullptr, const unsigned* slots_b = nullptr);
+                            const unsigned* bits_a = nullptr, const unsigned* bits_b = nullptr,
+                            int crt_lk = -1);
+// Multi-modular exact GEMM (device-decided modulus count from bits_a / bits_b,
+// no-op when an operand exceeds 128 bits). Residue planes of X: out =
+// [kCrtMaxResidues][rows_pad][kpad] int8 (rows_pad % 128 == 0, kpad % 64 == 0).
+hipError_t launch_to_residues(const DView& x, uint32_t rows, uint32_t kdim, uint32_t rows_pad,
+                              uint32_t kpad, uint32_t* out, const unsigned* bits_a,
+                              const unsigned* bits_b, uint32_t lk, hipStream_t st);
+// c_s = A * Bt from residue planes Ar (rows_pad rpad_a) and Br (rpad_b); R is
+// the residue scratch [kCrtMaxResidues][rpad_a][rpad_b] bytes.
+hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
+                           uint32_t rpad_a, uint32_t rpad_b, uint32_t kpad, uint8_t* R, Fr* out,
+                           int64_t ors, int64_t ocs, const unsigned* bits_a,
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st);
+static constexpr int kCrtMaxResidues = 40;   // = kCrtMaxMod (crt_tables.hpp)
 // w vector (len L) from a view (row 0 / col j of a 1 x L view) -> canonical copy
-// (w_canon nullable) and w_scaled = mont_mul(w, f) (f = R^2: Montgomery form).
-hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* w_scaled, const Fr& f,
-                           hipStream_t st);
+// (w_canon nullable), w_scaled = mont_mul(w, f) (f = R^2: Montgomery form) and
+// its negation (w_neg nullable).
+hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* w_scaled, Fr* w_neg,
+                           const Fr& f, hipStream_t st);
 // w_j = gamma^j, j < L.
 hipError_t launch_gamma_vec(const Fr& gamma, uint32_t L, Fr* w_canon, Fr* w_mont, hipStream_t st);
 // Freivalds inner-product rows (GateChip::inner_product, 1+3L cells per row) for
@@ -82,8 +106,8 @@ hipError_t launch_gamma_vec(const Fr& gamma, uint32_t L, Fr* w_canon, Fr* w_mont
 // thread and small-operand products when na < 8 (|signed A| < 2^(32 na), w_scaled =
 // w * 2^(32 na)); impls 1-3 and na = 8 take w_scaled in Montgomery form.
 hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
-                              const Fr* w_canon, const Fr* w_scaled, Fr* out, int impl, int na,
-                              hipStream_t st);
+                              const Fr* w_canon, const Fr* w_scaled, const Fr* w_neg, Fr* out,
+                              int impl, int na, hipStream_t st);
 // Up to kMaxScanJobs DPP row scans in one launch (T terms per thread: 1, 2, 4;
 // na as above, shared by every job: each job's w_scaled = w * 2^(32 na)).
 hipError_t launch_scan_batch(const ScanBatch& b, int T, int na, hipStream_t st);
