@@ -668,9 +668,11 @@ static std::vector<uint32_t> maxbits_many(svdw_ctx* c, const std::vector<svdw_ma
 // + v_dot4c_i32_i8 when |entries| fit 9 digits, else Montgomery per MAC.
 // With device bit-length words (sa, sb: one word each) the digit counts are
 // read by the kernels themselves and the host needs no operand bounds.
+// quantized: both operands are ZkMatrix::new cells (|x| < 2^128 by the u128
+// saturation), so the CRT path always applies and no fallback is queued.
 static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_mat& b, Fr* out,
                       uint32_t bits_a, uint32_t bits_b, const unsigned* sa = nullptr,
-                      const unsigned* sb = nullptr) {
+                      const unsigned* sb = nullptr, bool quantized = false) {
     const uint32_t N = a.rows, K = a.cols, M = b.cols;
     const bool sym = is_transpose_of(b, a);
     if (!sa && !sb && c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA && bits_a <= 128 &&
@@ -715,8 +717,9 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
                                   kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s),
                   "k_gemm_crt");
         }
-        hipck(launch_gemm_mont(view_of(c, a), view_of(c, b), N, K, M, out, M, 1, s, sa,
-                               sym ? sa : sb, (int)lk), "k_gemm_mont");
+        if (!quantized)
+            hipck(launch_gemm_mont(view_of(c, a), view_of(c, b), N, K, M, out, M, 1, s, sa,
+                                   sym ? sa : sb, (int)lk), "k_gemm_mont");
         return;
     }
     if (sa && sb && K <= 8192) {
@@ -1107,7 +1110,8 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
                                          const svdw_mat& v, const svdw_vec& d, double err_svd,
                                          double err_u, uint32_t max_bits_d,
                                          const uint32_t* known_bits = nullptr,
-                                         const unsigned* dev_bits = nullptr) {
+                                         const unsigned* dev_bits = nullptr,
+                                         bool dev_quantized = false) {
     REQUIRE(m.rows == u.rows, "check_svd_phase0: m.num_rows != u.num_rows");
     REQUIRE(m.cols == v.rows, "check_svd_phase0: m.num_col != v.num_rows");
     REQUIRE(u.rows == u.cols, "check_svd_phase0: u not square");
@@ -1148,7 +1152,8 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         const unsigned* sb[3] = {sl[2], sl[1], sl[2]};
         for (int g = 0; g < 3; ++g) {
             if (on_device)
-                gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ~0u, ~0u, sa[g], sb[g]);
+                gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ~0u, ~0u, sa[g], sb[g],
+                          dev_quantized);
             else
                 gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ba[g], bb[g]);
             c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
@@ -1252,7 +1257,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         c->qmat[0] = zm; c->qmat[1] = zu; c->qmat[2] = zv;
     }
     svdw_svd_payload pl =
-        check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits, dbits);
+        check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits, dbits, true);
     fetch_bits(c);
     check_svd_phase1(c, zm, zu, zv, pl, gamma);
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};

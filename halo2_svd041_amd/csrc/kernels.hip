@@ -131,6 +131,37 @@ hipError_t launch_bits_reduce(const unsigned* blockmax, const BitSegs& seg, uint
     return hipGetLastError();
 }
 
+// x mod p for a 9-word x < 2^270
+__device__ __forceinline__ Fr reduce9(const uint32_t (&x)[9]) {
+    const double two32 = 4294967296.0;
+    // 1 / (p / 2^192): quotient estimate within 2 of floor(x / p) (x < 2^270)
+    constexpr double inv_pd = 1.0 / (((double)0x30644e72u * 4294967296.0 + (double)0xe131a029u) +
+                                     (double)0xb85045b6u / 4294967296.0);
+    const double xd = ((double)x[8] * two32 + (double)x[7]) * two32 + (double)x[6];
+    const double qd = floor(xd * inv_pd) - 1.0;
+    const uint32_t q = qd > 0.0 ? (uint32_t)qd : 0u;
+    Fr r;
+    uint64_t carry = 0;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint64_t pr = (uint64_t)q * p_word(i) + carry;
+        carry = pr >> 32;
+        const uint64_t d = (uint64_t)x[i] - (uint32_t)pr - br;
+        r.w[i] = (uint32_t)d;
+        br = (uint32_t)(d >> 63);
+    }
+    // x - q p < 3p < 2^256: the ninth word is gone; two conditional subtractions
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        Fr t;
+        const uint32_t b = sub256(t, r, fr_p());
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.w[i] = b ? r.w[i] : t.w[i];
+    }
+    return r;
+}
+
 // ----------------------------------------------------------- stage kernel
 // Phase A: one thread per element (kStageElems = 256 = block size) runs the
 // stage's micro-ops, leaving the element's values V[0..nv) (8 words each) in
@@ -235,17 +266,30 @@ struct SweepMap {
 };
 // The batch's cells element by element: half-cell hc of local element el goes
 // to global half-cell 2 (e(el) C + slot) + h.
+template <int U>
 __device__ __forceinline__ void stream_cells_sweep(uint4* __restrict__ out, uint32_t total,
                                                    const SlotOp* __restrict__ ops, uint32_t C,
                                                    uint32_t magic, const uint32_t* sK,
                                                    const uint32_t* sV, uint32_t nv,
                                                    const SweepMap& map) {
-    for (uint32_t hc = threadIdx.x; hc < total; hc += blockDim.x) {
-        const uint32_t c = hc >> 1, h = hc & 1;
-        const uint32_t el = fastdiv(c, C, magic), slot = c - el * C;
-        const SlotOp op = ops[slot];
-        const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + (el * nv + op.src) * VW;
-        out[((uint64_t)map.elem(el) * C + slot) * 2 + h] = extract_half(src, op.lo, op.nbits, h);
+    for (uint32_t base = threadIdx.x; base < total; base += blockDim.x * U) {
+        uint4 v[U];
+        uint64_t dst[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t hc = min(base + u * blockDim.x, total - 1);
+            const uint32_t c = hc >> 1, h = hc & 1;
+            const uint32_t el = fastdiv(c, C, magic), slot = c - el * C;
+            const SlotOp op = ops[slot];
+            const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + (el * nv + op.src) * VW;
+            v[u] = extract_half(src, op.lo, op.nbits, h);
+            dst[u] = ((uint64_t)map.elem(el) * C + slot) * 2 + h;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (base + u * blockDim.x >= total) break;
+            out[dst[u]] = v[u];
+        }
     }
 }
 
@@ -354,11 +398,11 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
 
     // ---- phase B: advice cells, then lookup cells
     if (sweep) {
-        stream_cells_sweep(reinterpret_cast<uint4*>(a.out_adv), 2 * ne * a.C, sAdv, a.C,
-                           a.cdiv_magic, sK, sV, nv, map);
+        stream_cells_sweep<4>(reinterpret_cast<uint4*>(a.out_adv), 2 * ne * a.C, sAdv, a.C,
+                              a.cdiv_magic, sK, sV, nv, map);
         if (a.L)
-            stream_cells_sweep(reinterpret_cast<uint4*>(a.out_lk), 2 * ne * a.L, sLk, a.L,
-                               a.ldiv_magic, sK, sV, nv, map);
+            stream_cells_sweep<4>(reinterpret_cast<uint4*>(a.out_lk), 2 * ne * a.L, sLk, a.L,
+                                  a.ldiv_magic, sK, sV, nv, map);
         __syncthreads();                                  // LDS values reused by the next batch
         continue;
     }
@@ -1071,35 +1115,6 @@ __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar
     }
 }
 
-// x mod p for a 9-word x < 2^270
-__device__ __forceinline__ Fr reduce9(const uint32_t (&x)[9]) {
-    const double two32 = 4294967296.0;
-    const double xd = ((double)x[8] * two32 + (double)x[7]) * two32 + (double)x[6];
-    const double pd = ((double)p_word(7) * two32 + (double)p_word(6)) + (double)p_word(5) / two32;
-    const double qd = floor(xd / pd) - 1.0;
-    const uint32_t q = qd > 0.0 ? (uint32_t)qd : 0u;
-    Fr r;
-    uint64_t carry = 0;
-    uint32_t br = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint64_t pr = (uint64_t)q * p_word(i) + carry;
-        carry = pr >> 32;
-        const uint64_t d = (uint64_t)x[i] - (uint32_t)pr - br;
-        r.w[i] = (uint32_t)d;
-        br = (uint32_t)(d >> 63);
-    }
-    // x - q p < 3p < 2^256: the ninth word is gone; two conditional subtractions
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-        Fr t;
-        const uint32_t b = sub256(t, r, fr_p());
-#pragma unroll
-        for (int i = 0; i < 8; ++i) r.w[i] = b ? r.w[i] : t.w[i];
-    }
-    return r;
-}
-
 // C from its n residues, written as canonical Fr to out[i*ors + j*ocs]; one
 // 32 x 32 tile per block (SYM: upper tiles, mirrored through LDS).
 template <bool SYM>
@@ -1323,6 +1338,58 @@ __device__ __forceinline__ Fr wave_scan_fr(Fr s) {
     return s;
 }
 
+// Unreduced 9-word sums (values < 2^288, exact integers) for the scan network.
+struct U9 {
+    uint32_t w[9];
+};
+__device__ __forceinline__ U9 u9_from(const Fr& a) {
+    U9 r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = a.w[i];
+    r.w[8] = 0;
+    return r;
+}
+__device__ __forceinline__ U9 u9_add(const U9& a, const U9& b) {
+    U9 r;
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        c += (uint64_t)a.w[i] + b.w[i];
+        r.w[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    return r;
+}
+__device__ __forceinline__ U9 u9_sub(const U9& a, const U9& b) {   // a >= b
+    U9 r;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const uint64_t d = (uint64_t)a.w[i] - b.w[i] - br;
+        r.w[i] = (uint32_t)d;
+        br = (uint32_t)(d >> 63);
+    }
+    return r;
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ U9 dpp_u9(const U9& v) {
+    U9 r;
+#pragma unroll
+    for (int i = 0; i < 9; ++i)
+        r.w[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.w[i], CTRL, ROW_MASK, 0xf, true);
+    return r;
+}
+// inclusive wave scan without modular reduction (64 terms < 2^b -> < 2^(b+6))
+__device__ __forceinline__ U9 wave_scan_u9(U9 s) {
+    s = u9_add(s, dpp_u9<0x111, 0xf>(s));
+    s = u9_add(s, dpp_u9<0x112, 0xf>(s));
+    s = u9_add(s, dpp_u9<0x114, 0xf>(s));
+    s = u9_add(s, dpp_u9<0x118, 0xf>(s));
+    s = u9_add(s, dpp_u9<0x142, 0xa>(s));
+    s = u9_add(s, dpp_u9<0x143, 0xc>(s));
+    return s;
+}
+
 // T terms per thread, DPP scan. The cells go through a 24 KB LDS stage (768
 // cells) in T rounds -- round q stages the 3T cells of threads [q*256/T,
 // (q+1)*256/T) and the whole block writes them as coalesced 16 B half-cells --
@@ -1337,7 +1404,8 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
     static_assert(256 % T == 0, "T divides the block");
     constexpr uint32_t TPR = 256 / T;                     // threads staged per round
     __shared__ __attribute__((aligned(16))) uint32_t stage[3 * 256 * 8];
-    __shared__ Fr wtot[4], wpre[4], carry_s;
+    __shared__ U9 wtot[4], wpre[4];
+    __shared__ Fr carry_s;
     ScanJob J = B.job[0];
 #pragma unroll
     for (int q = 1; q < kMaxScanJobs; ++q)
@@ -1380,22 +1448,26 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
                 s[i] = j < L ? mont_mul_small<NA>(mag, ld_fr((neg ? wn : wm) + j)) : zero;
             }
         }
+        // local inclusive sums (< T p), the wave scan and the prefixes stay
+        // unreduced (exact, < 2^265); each output is reduced once
+        U9 loc[T];
+        loc[0] = u9_from(s[0]);
 #pragma unroll
-        for (int i = 1; i < T; ++i) s[i] = fr_add(s[i], s[i - 1]);
-        const Fr tot = wave_scan_fr(s[T - 1]);
+        for (int i = 1; i < T; ++i) loc[i] = u9_add(loc[i - 1], u9_from(s[i]));
+        const U9 tot = wave_scan_u9(loc[T - 1]);
         if (lane == 63) wtot[wave] = tot;
         __syncthreads();
         if (tid == 0) {                                   // wave prefixes and the running carry
-            Fr acc = carry_s;
+            U9 acc = u9_from(carry_s);
 #pragma unroll
             for (int w2 = 0; w2 < 4; ++w2) {
                 wpre[w2] = acc;
-                acc = fr_add(acc, wtot[w2]);
+                acc = u9_add(acc, wtot[w2]);
             }
-            carry_s = acc;
+            carry_s = reduce9(acc.w);
         }
         __syncthreads();
-        const Fr pre = fr_add(fr_sub(tot, s[T - 1]), wpre[wave]);
+        const U9 pre = u9_add(u9_sub(tot, loc[T - 1]), wpre[wave]);
 #pragma unroll
         for (int q = 0; q < T; ++q) {
             const uint32_t t0 = c0 + q * 256;                 // first term of this round
@@ -1405,7 +1477,7 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
                 for (int i = 0; i < T; ++i) {
                     const uint32_t j = j0 + i;
                     const Fr w = j < L ? ld_fr(wc + j) : zero;
-                    const Fr si = fr_add(s[i], pre);
+                    const Fr si = reduce9(u9_add(loc[i], pre).w);
                     uint4* st3 = reinterpret_cast<uint4*>(stage + ((tid % TPR) * T + i) * 24);
                     st3[0] = make_uint4(a[i].w[0], a[i].w[1], a[i].w[2], a[i].w[3]);
                     st3[1] = make_uint4(a[i].w[4], a[i].w[5], a[i].w[6], a[i].w[7]);

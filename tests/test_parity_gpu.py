@@ -91,14 +91,18 @@ def test_garbage_inputs_parity(gpu_ctx_factory):
         _assert_streams(ctx, a0, l0, a1)
 
 
-def test_generic_gemm_fallback_parity(gpu_ctx_factory):
-    """Operands too wide for the digit GEMM (|x| >= 2^72) take the Montgomery path."""
+@pytest.mark.parametrize("crt", [1, 0])
+def test_generic_gemm_fallback_parity(gpu_ctx_factory, crt):
+    """Operands too wide for the digit GEMM (|x| >= 2^72): the CRT GEMM takes them
+    (up to 2^128), the digit path falls back to the Montgomery GEMM."""
     import halo2_svd041_amd as hs
     rs = np.random.RandomState(3)
     N = 5
     m = rs.uniform(-1, 1, (N, N)) * 2.0 ** 20
+    m[0, 0] = 3.0e19                       # saturates to 2^128 - 1 at P = 63
     u, d, v = np.eye(N), np.ones(N), np.eye(N)
     ctx = gpu_ctx_factory(63)
+    ctx.set_option("gemm_crt", crt)
     hs.svd_witness(ctx, m, u, v, d, 5)
     a0, l0, a1 = corc.svd_witness(m, u, v, d, 63, 19, 5)
     _assert_streams(ctx, a0, l0, a1)
