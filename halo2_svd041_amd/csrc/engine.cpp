@@ -300,6 +300,7 @@ struct svdw_ctx {
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
     uint32_t stage_flags = 0;               // STAGE_* (svdw_set_option "nt_stores", "stage_ilp")
     uint32_t stage_sweep = 0;               // "stage_sweep": persistent grid of the sweep mode (0 off)
+    uint32_t stage_elems = 64;              // "stage_elems": elements per stage block (16..256)
     int scan_impl = 4;                      // svdw_set_option "scan_impl"
     int prelaunch_at = 0;
     int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
@@ -504,8 +505,10 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     a.cols = cols ? cols : 1;
     a.flags = c->stage_flags;
     a.sweep_nb = c->stage_sweep;
+    a.E = c->stage_elems;
     // interleaved groups only pay off on big stages (and need whole batches of work)
-    if (c->stage_sweep && (uint64_t)nelem >= 4ull * kStageElems * c->stage_sweep / kSweepG)
+    if (c->stage_sweep && c->stage_elems == kStageElems &&
+        (uint64_t)nelem >= 4ull * kStageElems * c->stage_sweep / kSweepG)
         a.flags |= STAGE_SWEEP;
     // 32-bit magics for fastdiv (divisor 1 is handled in the kernel)
     auto magic = [](uint64_t d) -> uint32_t { return d > 1 ? (uint32_t)(((1ull << 32) + d - 1) / d) : 0; };
@@ -670,9 +673,13 @@ static std::vector<uint32_t> maxbits_many(svdw_ctx* c, const std::vector<svdw_ma
 // read by the kernels themselves and the host needs no operand bounds.
 // quantized: both operands are ZkMatrix::new cells (|x| < 2^128 by the u128
 // saturation), so the CRT path always applies and no fallback is queued.
+// CRT path residue reuse (prelaunched products of check_svd_phase0): b_cover
+// makes b's planes (kept in digB) also valid for the product (b, b); a_from_b
+// takes a's planes from digB (a is that b) instead of recomputing them.
 static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_mat& b, Fr* out,
                       uint32_t bits_a, uint32_t bits_b, const unsigned* sa = nullptr,
-                      const unsigned* sb = nullptr, bool quantized = false) {
+                      const unsigned* sb = nullptr, bool quantized = false,
+                      const unsigned* b_cover = nullptr, bool a_from_b = false) {
     const uint32_t N = a.rows, K = a.cols, M = b.cols;
     const bool sym = is_transpose_of(b, a);
     if (!sa && !sb && c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA && bits_a <= 128 &&
@@ -693,27 +700,31 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
         while ((1ull << lk) < K) ++lk;
         const uint32_t kpad = (K + 63) / 64 * 64;
         const uint32_t rpa = (N + 127) / 128 * 128, rpb = (M + 127) / 128 * 128;
-        ensure_buf(c, c->digA, (size_t)kCrtMaxResidues * rpa * kpad);
         ensure_buf(c, c->crtR, (size_t)kCrtMaxResidues * rpa * (sym ? rpa : rpb));
-        {
+        const uint8_t* Ar;
+        if (a_from_b && sym) {
+            Ar = (const uint8_t*)c->digB.p;               // planes of this operand already built
+        } else {
+            ensure_buf(c, c->digA, (size_t)kCrtMaxResidues * rpa * kpad);
             ProfScope ps(c, s, "k_to_residues", 32.0 * N * K, 0);
             hipck(launch_to_residues(view_of(c, a), N, K, rpa, kpad, (uint32_t*)c->digA.p, sa,
                                      sym ? sa : sb, lk, s), "k_to_residues");
+            Ar = (const uint8_t*)c->digA.p;
         }
-        const uint8_t* Br = (const uint8_t*)c->digA.p;
+        const uint8_t* Br = Ar;
         if (!sym) {
             ensure_buf(c, c->digB, (size_t)kCrtMaxResidues * rpb * kpad);
             svdw_mat bt = b;   // Bt(j, k) = b(k, j)
             bt.rows = b.cols; bt.cols = b.rows; bt.rs = b.cs; bt.cs = b.rs;
             ProfScope ps(c, s, "k_to_residues", 32.0 * M * K, 0);
             hipck(launch_to_residues(view_of(c, bt), M, K, rpb, kpad, (uint32_t*)c->digB.p, sa, sb,
-                                     lk, s), "k_to_residues");
+                                     lk, s, b_cover), "k_to_residues");
             Br = (const uint8_t*)c->digB.p;
         }
         {
             ProfScope ps(c, s, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * N * M,
                          (double)N * M * K);
-            hipck(launch_gemm_crt(sym, (const uint8_t*)c->digA.p, Br, N, M, rpa, sym ? rpa : rpb,
+            hipck(launch_gemm_crt(sym, Ar, Br, N, M, rpa, sym ? rpa : rpb,
                                   kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s),
                   "k_gemm_crt");
         }
@@ -1151,9 +1162,10 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         const unsigned* sa[3] = {sl[0], sl[1], sl[2]};
         const unsigned* sb[3] = {sl[2], sl[1], sl[2]};
         for (int g = 0; g < 3; ++g) {
+            // CRT: v's residue planes from m.v^T (covering v.v^T too) serve v.v^T
             if (on_device)
                 gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ~0u, ~0u, sa[g], sb[g],
-                          dev_quantized);
+                          dev_quantized, g == 0 ? sl[2] : nullptr, g == 2);
             else
                 gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ba[g], bb[g]);
             c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
@@ -1538,6 +1550,10 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_impl = (int)value;
         } else if (n == "nt_stores") {
             c->stage_flags = (c->stage_flags & ~STAGE_NT_STORES) | (value ? STAGE_NT_STORES : 0);
+        } else if (n == "stage_elems") {
+            REQUIRE(value >= 16 && value <= 256 && value % 16 == 0,
+                    "stage_elems: a multiple of 16 in [16, 256]");
+            c->stage_elems = (uint32_t)value;
         } else if (n == "stage_sweep") {
             REQUIRE(value >= 0 && value <= 4096, "stage_sweep: 0 (off) or a grid size <= 4096");
             c->stage_sweep = (uint32_t)value;

@@ -211,9 +211,8 @@ __device__ __forceinline__ uint4 extract_half(const uint32_t* s, uint32_t lo, ui
 }
 
 // LDS carve (bytes, all 16-aligned): consts | element values | slot ops | micro-ops | views
-__host__ __device__ constexpr uint32_t stage_lds_bytes(uint32_t nv) {
-    return kMaxK * 32 + kStageElems * nv * 32 + (kMaxAdv + kMaxLk) * 4 + kMaxMicro * 8 +
-           kMaxViews * 48;
+__host__ __device__ constexpr uint32_t stage_lds_bytes(uint32_t nv, uint32_t E) {
+    return kMaxK * 32 + E * nv * 32 + (kMaxAdv + kMaxLk) * 4 + kMaxMicro * 8 + kMaxViews * 48;
 }
 
 // x / d for x * d < 2^32 via one 32-bit mul_hi (magic = ceil(2^32 / d), d >= 2).
@@ -298,7 +297,8 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     const uint32_t nv = a.nv;
     uint32_t* sK = smem;
     uint32_t* sV = sK + kMaxK * VW;
-    SlotOp* sAdv = reinterpret_cast<SlotOp*>(sV + kStageElems * nv * VW);
+    const uint32_t E = a.E ? a.E : kStageElems;
+    SlotOp* sAdv = reinterpret_cast<SlotOp*>(sV + E * nv * VW);
     SlotOp* sLk = sAdv + kMaxAdv;
     MicroOp* sMo = reinterpret_cast<MicroOp*>(sLk + kMaxLk);
     DView* sVw = reinterpret_cast<DView*>(sMo + kMaxMicro);
@@ -322,8 +322,8 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
         ne = __syncthreads_count(e < a.e_end);            // valid elements form a prefix
         e0 = 0;
     } else {
-        e0 = a.e_begin + blockIdx.x * kStageElems;
-        ne = min((uint32_t)kStageElems, a.e_end - e0);
+        e0 = a.e_begin + blockIdx.x * E;
+        ne = min(E, a.e_end - e0);
         e = e0 + tid;
     }
     // ---- phase A: per-element micro-ops (constants / ops / views read from LDS:
@@ -425,8 +425,10 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     if (a.e_end <= a.e_begin) return hipSuccess;
     const uint32_t n = a.e_end - a.e_begin;
-    const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1);
-    uint32_t grid = (n + kStageElems - 1) / kStageElems;
+    const uint32_t E = a.E ? a.E : kStageElems;
+    if (E > kStageElems || ((a.flags & STAGE_SWEEP) && E != kStageElems)) return hipErrorInvalidValue;
+    const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1, E);
+    uint32_t grid = (n + E - 1) / E;
     if (a.flags & STAGE_SWEEP) {
         // persistent blocks; every block needs at least one group
         const uint32_t groups = (n + kSweepG - 1) / kSweepG;
@@ -981,8 +983,11 @@ __global__ __launch_bounds__(256) void k_to_residues(const DView x, uint32_t row
                                                      uint32_t* __restrict__ out,
                                                      const unsigned* __restrict__ bits_a,
                                                      const unsigned* __restrict__ bits_b,
+                                                     const unsigned* __restrict__ bits_c,
                                                      uint32_t lk) {
-    const int n = crt_nmod(*bits_a, *bits_b, lk);
+    // planes for the product (a, b) and, when bits_c is given, also for (c, c)
+    int n = crt_nmod(*bits_a, *bits_b, lk);
+    if (bits_c) n = max(n, crt_nmod(*bits_c, *bits_c, lk));
     if (!n) return;
     const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (uint64_t)rows_pad * kw) return;
@@ -997,7 +1002,7 @@ __global__ __launch_bounds__(256) void k_to_residues(const DView x, uint32_t row
             half.w[i] = nw;
         }
     }
-    const uint32_t bmax = max(*bits_a, *bits_b);
+    const uint32_t bmax = max(max(*bits_a, *bits_b), bits_c ? *bits_c : 0u);
     if (bmax <= 64)
         residues_body<4>(x, rows, kdim, rows_pad, kw, out, n, row, kg, half);
     else if (bmax <= 96)
@@ -1007,11 +1012,12 @@ __global__ __launch_bounds__(256) void k_to_residues(const DView x, uint32_t row
 }
 hipError_t launch_to_residues(const DView& x, uint32_t rows, uint32_t kdim, uint32_t rows_pad,
                               uint32_t kpad, uint32_t* out, const unsigned* bits_a,
-                              const unsigned* bits_b, uint32_t lk, hipStream_t st) {
+                              const unsigned* bits_b, uint32_t lk, hipStream_t st,
+                              const unsigned* bits_c) {
     const uint64_t n = (uint64_t)rows_pad * (kpad / 4);
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_to_residues, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, rows,
-                       kdim, rows_pad, kpad / 4, out, bits_a, bits_b, lk);
+                       kdim, rows_pad, kpad / 4, out, bits_a, bits_b, bits_c, lk);
     return hipGetLastError();
 }
 

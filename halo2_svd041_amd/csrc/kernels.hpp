@@ -82,9 +82,11 @@ hipError_t launch_gemm_mont(const DView& A, const DView& B, uint32_t N, uint32_t
 // Multi-modular exact GEMM (device-decided modulus count from bits_a / bits_b,
 // no-op when an operand exceeds 128 bits). Residue planes of X: out =
 // [kCrtMaxResidues][rows_pad][kpad] int8 (rows_pad % 128 == 0, kpad % 64 == 0).
+// bits_c (nullable): also cover the product (c, c), so the planes can be reused.
 hipError_t launch_to_residues(const DView& x, uint32_t rows, uint32_t kdim, uint32_t rows_pad,
                               uint32_t kpad, uint32_t* out, const unsigned* bits_a,
-                              const unsigned* bits_b, uint32_t lk, hipStream_t st);
+                              const unsigned* bits_b, uint32_t lk, hipStream_t st,
+                              const unsigned* bits_c = nullptr);
 // c_s = A * Bt from residue planes Ar (rows_pad rpad_a) and Br (rpad_b); R is
 // the residue scratch [kCrtMaxResidues][rpad_a][rpad_b] bytes.
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,

@@ -85,6 +85,7 @@ struct StageArgs {
     uint32_t cdiv_magic;  // ceil(2^32 / C) (C >= 2): x / C = mul_hi(x, magic) for x * C < 2^32
     uint32_t ldiv_magic;  // ceil(2^32 / L)
     uint32_t sweep_nb;    // STAGE_SWEEP: persistent grid size
+    uint32_t E;           // elements per block (<= 256 = block size); 0 -> 256
     DView view[kMaxViews];
     MicroOp mo[kMaxMicro];
     SlotOp adv[kMaxAdv];

@@ -157,21 +157,35 @@ int svdw_check_svd_phase1(svdw_ctx* ctx, const svdw_mat* m, const svdw_mat* u, c
 int svdw_svd_witness(svdw_ctx* ctx, const double* m, const double* u, const double* v,
                      const double* d, uint32_t N, uint32_t M, int on_device,
                      const svdw_svd_config* cfg, const uint64_t gamma[4], svdw_counts* counts);
-/* Exact integer GEMM of honest_prover_mat_mul: balanced base-256 digit planes
- * with i32 diagonal sums on the matrix cores (v_mfma_i32_16x16x64_i8, default)
- * or on the vector ALUs (v_dot4c_i32_i8). Both are bit-identical; operands
- * wider than 9 digits (|x| >= ~2^71) use a Montgomery GEMM either way.
- * The environment variable SVDW_GEMM=valu selects the VALU path at create. */
+/* Exact integer GEMM of honest_prover_mat_mul (the integer sum of quantized
+ * products, reduced mod p once). Matrix-core paths (SVDW_GEMM_MFMA, default):
+ *   - multi-modular / CRT (option "gemm_crt" 1, default): balanced residues
+ *     modulo n pairwise coprime moduli <= 256 (n from the operand bit lengths:
+ *     19 for m.v^T at P = 63), one int8 v_mfma_i32_16x16x64_i8 GEMM per
+ *     modulus, CRT reconstruction; operands up to 2^128, K <= 8192;
+ *   - balanced base-256 digit planes with i32 digit-pair diagonal sums
+ *     ("gemm_crt" 0), operands up to ~2^71.
+ * SVDW_GEMM_VALU: the digit planes on v_dot4c_i32_i8. All paths are
+ * bit-identical; wider operands use a Montgomery GEMM. The environment
+ * variable SVDW_GEMM=valu selects the VALU path at create. */
 #define SVDW_GEMM_MFMA 0
 #define SVDW_GEMM_VALU 1
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
-/* Tuning knobs (bit-identical results for every value):
- *   "gemm_impl" 0 | 1, "nt_stores" 0 | 1 (non-temporal cell stores),
- *   "stage_ilp" 1 | 2 | 4 (half-cells in flight per thread), "scan_impl" 1..5
- *   (row-scan kernel variant: 1 shuffle scan, 2 four terms/thread direct stores,
- *   3 DPP scan, 4 (default) / 5 DPP scan with two / four terms per thread and
- *   small-operand products where bounds are known), "overlap" 0 | 1 (GEMMs ahead on a
- *   second stream). */
+/* Tuning knobs (bit-identical results for every value; defaults first):
+ *   "gemm_impl" 0 | 1; "gemm_crt" 1 | 0 (CRT or digit-plane matrix-core GEMM);
+ *   "gemm_rt" 1 | 0 (svd_witness: GEMM sizes decided on the device from the
+ *   quantized operands' bit lengths, no host round trip);
+ *   "overlap" 1 | 0 (the three check_svd_phase0 products run ahead on a second
+ *   stream); "prelaunch_at" 0 | 1 | 2 (how many phase-0 stages are queued
+ *   before them); "gemm_priority" 0 | 1 (second stream priority);
+ *   "stage_elems" 64 (elements per stage block, multiple of 16 in [16, 256]);
+ *   "stage_ilp" 1 | 2 | 4 (half-cells in flight per thread); "nt_stores" 0 | 1
+ *   (non-temporal cell stores); "stage_sweep" 0 | grid (persistent blocks over
+ *   interleaved element groups; needs stage_elems 256);
+ *   "scan_impl" 4 | 1 | 2 | 3 | 5 (row-scan kernel: 1 shuffle scan, 2 four
+ *   terms/thread direct stores, 3 DPP scan, 4 / 5 DPP scan with two / four
+ *   terms per thread, unreduced partial sums and small-operand products where
+ *   bounds are known). */
 int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);
 
 /* ----------------------------------------------------------- profiling */
