@@ -81,6 +81,25 @@ def roofline_from_profile(stats, steps):
     }, breakdown
 
 
+def rank_workload(seed, rank, N, M):
+    """Rank r witnesses its own matrix (seed + r): independent objects, no
+    data-path exchange (north_star: matrices shard embarrassingly)."""
+    m, u, d, v = gen_input(N, M, seed + rank)
+    return m, u, d, v, gamma_for(seed + rank)
+
+
+def reduce_over_ranks(elapsed, cells_step, dist, device):
+    """Job clock = slowest rank (max), cells = all ranks (sum). dist None: 1 rank."""
+    if dist is None:
+        return elapsed, float(cells_step)
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    c = torch.tensor([float(cells_step)], dtype=torch.float64, device=device)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(c.item())
+
+
 def pmc_traffic(kernel, N, M, P, LB):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
     summary of this exact workload (profiles/*_pmc_summary.json, written by
@@ -149,8 +168,7 @@ def main():
 
     import halo2_svd041_amd as hs
 
-    m, u, d, v = gen_input(N, M, args.seed + rank)
-    g = gamma_for(args.seed + rank)
+    m, u, d, v, g = rank_workload(args.seed, rank, N, M)
     dev = torch.device("cuda", local)
     dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev)
                       for x in (m, u, v, d))
@@ -180,15 +198,7 @@ def main():
     stats = ctx.profile_collect() if not args.no_profile else []
 
     cells_step = cnt["advice0"] + cnt["advice1"]
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([cells_step], dtype=torch.float64, device=dev)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        cells_all = float(c.item())
-    else:
-        cells_all = float(cells_step)
+    elapsed, cells_all = reduce_over_ranks(elapsed, cells_step, dist, dev)
     total_cells = cells_all * args.steps
     value = total_cells / elapsed
 
