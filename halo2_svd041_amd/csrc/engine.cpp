@@ -304,7 +304,9 @@ struct svdw_ctx {
     int scan_impl = 4;                      // svdw_set_option "scan_impl"
     int prelaunch_at = 0;
     int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
-    int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)                   // "prelaunch_at": GEMMs queued before stage 0/1/2
+    int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
+    int phase1_overlap = 1;                 // "phase1_overlap": phase 1 on st2 behind the GEMMs
+    bool prelaunched = false;               // this witness's products were queued on st2                   // "prelaunch_at": GEMMs queued before stage 0/1/2
     // second stream: GEMMs overlap the HBM-bound stages
     hipStream_t st2 = nullptr;
     bool overlap = true;
@@ -1170,6 +1172,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
                 gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ba[g], bb[g]);
             c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
         }
+        c->prelaunched = true;
     };
     if (c->prelaunch_at == 0) prelaunch();
     entries_less_than(c, d, max_bits);
@@ -1228,6 +1231,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     const uint32_t r = std::min(N, M);
     clear_streams(c);
     c->dep_next = 0;
+    c->prelaunched = false;
     c->pre.clear();
     if (!c->dry) {
         // exact sizes from the dry planner: no growth copies inside the step
@@ -1271,7 +1275,21 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     svdw_svd_payload pl =
         check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits, dbits, true);
     fetch_bits(c);
-    check_svd_phase1(c, zm, zu, zv, pl, gamma);
+    // Phase 1 needs only the products (already queued on st2), the quantized
+    // operands and gamma: run it on st2 behind the GEMMs, concurrently with the
+    // HBM-bound phase-0 checks still on st (its row scans are VALU-bound), and
+    // join the streams afterwards.
+    const bool p1_overlap = c->phase1_overlap && c->prelaunched && !c->dry;
+    {
+        struct Swap {
+            svdw_ctx* c;
+            bool on;
+            Swap(svdw_ctx* cc, bool o) : c(cc), on(o) { if (on) std::swap(c->st, c->st2); }
+            ~Swap() { if (on) std::swap(c->st, c->st2); }
+        } sw(c, p1_overlap);
+        check_svd_phase1(c, zm, zu, zv, pl, gamma);
+    }
+    if (p1_overlap) stream_dep(c, c->st2, c->st);
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
 }
 
@@ -1574,6 +1592,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                 hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
                 c->st2 = s;
             }
+        } else if (n == "phase1_overlap") {
+            REQUIRE(value == 0 || value == 1, "phase1_overlap: 0 or 1");
+            c->phase1_overlap = (int)value;
         } else if (n == "gemm_crt") {
             REQUIRE(value == 0 || value == 1, "gemm_crt: 0 or 1");
             c->gemm_crt = (int)value;
