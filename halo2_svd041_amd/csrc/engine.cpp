@@ -300,7 +300,7 @@ struct svdw_ctx {
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
     uint32_t stage_flags = 0;               // STAGE_* (svdw_set_option "nt_stores", "stage_ilp")
     uint32_t stage_sweep = 0;               // "stage_sweep": persistent grid of the sweep mode (0 off)
-    uint32_t stage_elems = 64;              // "stage_elems": elements per stage block (16..256)
+    uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
     int scan_impl = 4;                      // svdw_set_option "scan_impl"
     int prelaunch_at = 0;
     int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
@@ -507,7 +507,12 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     a.cols = cols ? cols : 1;
     a.flags = c->stage_flags;
     a.sweep_nb = c->stage_sweep;
-    a.E = c->stage_elems;
+    // small blocks overlap better with concurrent work, but a stage with field
+    // multiplications / inversions keeps one element per thread of a full block
+    bool heavy = false;
+    for (uint32_t i = 0; i < a.nmo; ++i)
+        heavy |= a.mo[i].op == MO_MUL || a.mo[i].op == MO_ISZERO || a.mo[i].op == MO_POWK;
+    a.E = heavy ? kStageElems : c->stage_elems;
     // interleaved groups only pay off on big stages (and need whole batches of work)
     if (c->stage_sweep && c->stage_elems == kStageElems &&
         (uint64_t)nelem >= 4ull * kStageElems * c->stage_sweep / kSweepG)

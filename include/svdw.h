@@ -179,7 +179,7 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   stream); "phase1_overlap" 1 | 0 (svd_witness: phase 1 runs on that stream
  *   behind the products, concurrently with the phase-0 checks); "prelaunch_at" 0 | 1 | 2 (how many phase-0 stages are queued
  *   before them); "gemm_priority" 0 | 1 (second stream priority);
- *   "stage_elems" 64 (elements per stage block, multiple of 16 in [16, 256]);
+ *   "stage_elems" 256 (elements per stage block, multiple of 16 in [16, 256]);
  *   "stage_ilp" 1 | 2 | 4 (half-cells in flight per thread); "nt_stores" 0 | 1
  *   (non-temporal cell stores); "stage_sweep" 0 | grid (persistent blocks over
  *   interleaved element groups; needs stage_elems 256);

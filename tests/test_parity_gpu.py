@@ -165,7 +165,7 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
 @pytest.mark.parametrize("opts", [{"stage_ilp": 2}, {"stage_ilp": 4}, {"nt_stores": 1},
                                   {"scan_impl": 2}, {"scan_impl": 3}, {"scan_impl": 1}, {"scan_impl": 5},
                                   {"gemm_rt": 0}, {"prelaunch_at": 2}, {"gemm_crt": 0},
-                                  {"stage_sweep": 1}, {"stage_sweep": 3}, {"stage_elems": 256},
+                                  {"stage_sweep": 1}, {"stage_sweep": 3}, {"stage_elems": 64},
                                   {"stage_elems": 192}, {"phase1_overlap": 0},
                                   {"overlap": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
