@@ -302,13 +302,17 @@ struct svdw_ctx {
     uint32_t stage_sweep = 0;               // "stage_sweep": persistent grid of the sweep mode (0 off)
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
     int scan_impl = 4;                      // svdw_set_option "scan_impl"
-    int prelaunch_at = 0;
+    int prelaunch_at = 0;                   // "prelaunch_at": GEMMs queued before stage 0/1/2
     int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
-    int phase1_overlap = 1;                 // "phase1_overlap": phase 1 on st2 behind the GEMMs
-    bool prelaunched = false;               // this witness's products were queued on st2                   // "prelaunch_at": GEMMs queued before stage 0/1/2
-    // second stream: GEMMs overlap the HBM-bound stages
+    int phase1_overlap = 1;                 // "phase1_overlap": 0 off, 1 on st2 behind the
+                                            // GEMMs, 2 on st3 from quantization on
+    bool prelaunched = false;               // this witness's products were queued on st2
+    std::vector<hipEvent_t> gemm_done;      // their completion events (this witness)
+    std::vector<hipEvent_t> wait_before_cs; // verify_mul_many: wait before the c_s scans
+    // second stream: GEMMs overlap the HBM-bound stages; third: phase 1
     hipStream_t st2 = nullptr;
+    hipStream_t st3 = nullptr;
     bool overlap = true;
     struct PreGemm {
         uint64_t off;
@@ -324,6 +328,7 @@ static void sync(svdw_ctx* c) {
     if (c->dry) return;
     hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
     hipck(hipStreamSynchronize(c->st2), "hipStreamSynchronize");
+    if (c->st3) hipck(hipStreamSynchronize(c->st3), "hipStreamSynchronize");
 }
 // Event recorded on `from`; `to` waits for it (cross-stream dependency).
 static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
@@ -1081,14 +1086,18 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     const WScaled g_cs = gamma_scaled(c, na_cs);
     const WScaled g_b = gamma_scaled(c, na_b);
     auto gc = [&](int) { return gpc; };
-    run_batch("k_matvec_scan:cs", cs_of, [&](int i) { return pl[i].csv; }, gc,
-              [&](int) { return g_cs; }, na_cs);
+    // launch order != append order: the b and a.(b.g) scans need only the
+    // operands, the c_s scans wait for the products when those run elsewhere
     run_batch("k_matvec_scan:b", b_of, [&](int i) { return pl[i].bv; }, gc,
               [&](int) { return g_b; }, na_b);
     WScaled wb[kMaxScanJobs];
     for (int i = 0; i < n; ++i) wb[i] = vec_prep(c, pl[i].bv, c->wbc[i], c->wbs[i], na_a);
     run_batch("k_matvec_scan:a", a_of, [&](int i) { return pl[i].abv; },
               [&](int i) { return (const Fr*)c->wbc[i].p; }, [&](int i) { return wb[i]; }, na_a);
+    for (hipEvent_t ev : c->wait_before_cs)
+        hipck(hipStreamWaitEvent(c->st, ev, 0), "hipStreamWaitEvent");
+    run_batch("k_matvec_scan:cs", cs_of, [&](int i) { return pl[i].csv; }, gc,
+              [&](int) { return g_cs; }, na_cs);
     for (int i = 0; i < n; ++i) {
         Plan& p = pl[i];
         p.eq.a.view[0] = view_of(c, mat_of_vec(p.csv));
@@ -1176,6 +1185,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
             else
                 gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ba[g], bb[g]);
             c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
+            c->gemm_done.push_back(c->pre.back().ev);
         }
         c->prelaunched = true;
     };
@@ -1237,6 +1247,8 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     clear_streams(c);
     c->dep_next = 0;
     c->prelaunched = false;
+    c->gemm_done.clear();
+    c->wait_before_cs.clear();
     c->pre.clear();
     if (!c->dry) {
         // exact sizes from the dry planner: no growth copies inside the step
@@ -1284,17 +1296,27 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     // operands and gamma: run it on st2 behind the GEMMs, concurrently with the
     // HBM-bound phase-0 checks still on st (its row scans are VALU-bound), and
     // join the streams afterwards.
+    // Mode 2: on a third stream that starts after quantization; the b.g and
+    // a.(b.g) scans run at once, the c_s.g scans wait for the products.
     const bool p1_overlap = c->phase1_overlap && c->prelaunched && !c->dry;
+    if (p1_overlap && c->phase1_overlap == 2 && !c->st3)   // created on first use
+        hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
+    hipStream_t p1s = c->phase1_overlap == 2 ? c->st3 : c->st2;
+    if (p1_overlap && p1s == c->st3) {
+        hipck(hipStreamWaitEvent(c->st3, c->ev_bits, 0), "hipStreamWaitEvent");
+        c->wait_before_cs = c->gemm_done;
+    }
     {
         struct Swap {
             svdw_ctx* c;
-            bool on;
-            Swap(svdw_ctx* cc, bool o) : c(cc), on(o) { if (on) std::swap(c->st, c->st2); }
-            ~Swap() { if (on) std::swap(c->st, c->st2); }
-        } sw(c, p1_overlap);
+            hipStream_t* other;
+            Swap(svdw_ctx* cc, hipStream_t* o) : c(cc), other(o) { if (other) std::swap(c->st, *other); }
+            ~Swap() { if (other) std::swap(c->st, *other); }
+        } sw(c, p1_overlap ? (p1s == c->st3 ? &c->st3 : &c->st2) : nullptr);
         check_svd_phase1(c, zm, zu, zv, pl, gamma);
     }
-    if (p1_overlap) stream_dep(c, c->st2, c->st);
+    c->wait_before_cs.clear();
+    if (p1_overlap) stream_dep(c, p1s, c->st);
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
 }
 
@@ -1340,6 +1362,7 @@ int svdw_ctx_destroy(svdw_ctx* c) {
         if (!c->dry) {
             (void)hipStreamSynchronize(c->st);
             (void)hipStreamSynchronize(c->st2);
+            if (c->st3) (void)hipStreamSynchronize(c->st3);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
             for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->w1c, &c->w1m, &c->w2c, &c->w2m,
                             &c->bits, &c->gpc, &c->gpm, &c->crtR, &c->gbits})
@@ -1355,6 +1378,10 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             for (auto e : c->pool) (void)hipEventDestroy(e);
             for (auto e : c->deps) (void)hipEventDestroy(e);
             (void)hipStreamSynchronize(c->st2);
+            if (c->st3) {
+                (void)hipStreamSynchronize(c->st3);
+                (void)hipStreamDestroy(c->st3);
+            }
             (void)hipStreamDestroy(c->st2);
             (void)hipStreamDestroy(c->st);
         }
@@ -1598,7 +1625,7 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                 c->st2 = s;
             }
         } else if (n == "phase1_overlap") {
-            REQUIRE(value == 0 || value == 1, "phase1_overlap: 0 or 1");
+            REQUIRE(value >= 0 && value <= 2, "phase1_overlap: 0, 1 or 2");
             c->phase1_overlap = (int)value;
         } else if (n == "gemm_crt") {
             REQUIRE(value == 0 || value == 1, "gemm_crt: 0 or 1");

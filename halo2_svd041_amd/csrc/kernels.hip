@@ -307,6 +307,27 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     const bool sweep = (a.flags & STAGE_SWEEP) != 0;
     SweepMap map{a.e_begin, blockIdx.x, gridDim.x, 0};
 
+    // Issue this thread's in-bounds strided view loads before the LDS set-up,
+    // so their latency overlaps it (phase A falls back to view_load otherwise).
+    Fr pf0 = fr_zero(), pf1 = fr_zero();
+    bool in0 = false, in1 = false;
+    if (!sweep) {
+        const uint32_t pe = a.e_begin + blockIdx.x * E + tid;
+        if (tid < E && pe < a.e_end) {
+            const uint32_t pi = pe / a.cols, pj = pe - pi * a.cols;
+            const DView& v0 = a.view[0];
+            if (v0.ptr && v0.mode == VIEW_STRIDED && pi < v0.rows && pj < v0.cols) {
+                pf0 = ld_fr(v0.ptr + (int64_t)pi * v0.rs + (int64_t)pj * v0.cs);
+                in0 = true;
+            }
+            const DView& v1 = a.view[1];
+            if (v1.ptr && v1.mode == VIEW_STRIDED && pi < v1.rows && pj < v1.cols) {
+                pf1 = ld_fr(v1.ptr + (int64_t)pi * v1.rs + (int64_t)pj * v1.cs);
+                in1 = true;
+            }
+        }
+    }
+
     for (uint32_t k = tid; k < a.nk; k += blockDim.x) lds_put(sK + k * VW, a.K[k]);
     for (uint32_t k = tid; k < a.C; k += blockDim.x) sAdv[k] = a.adv[k];
     for (uint32_t k = tid; k < a.L; k += blockDim.x) sLk[k] = a.lk[k];
@@ -336,8 +357,14 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
             uint32_t* dst = myV + op.dst * VW;
             switch (op.op) {
                 case MO_LOAD: {
-                    const DView vw = sVw[op.a];
-                    lds_put(dst, view_load(vw, lds_get(sK + vw.pad_k * VW), i, j));
+                    if (op.a == 0 && in0) {
+                        lds_put(dst, pf0);
+                    } else if (op.a == 1 && in1) {
+                        lds_put(dst, pf1);
+                    } else {
+                        const DView vw = sVw[op.a];
+                        lds_put(dst, view_load(vw, lds_get(sK + vw.pad_k * VW), i, j));
+                    }
                     break;
                 }
                 case MO_ADDK:

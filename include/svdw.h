@@ -176,8 +176,9 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   "gemm_rt" 1 | 0 (svd_witness: GEMM sizes decided on the device from the
  *   quantized operands' bit lengths, no host round trip);
  *   "overlap" 1 | 0 (the three check_svd_phase0 products run ahead on a second
- *   stream); "phase1_overlap" 1 | 0 (svd_witness: phase 1 runs on that stream
- *   behind the products, concurrently with the phase-0 checks); "prelaunch_at" 0 | 1 | 2 (how many phase-0 stages are queued
+ *   stream); "phase1_overlap" 1 | 2 | 0 (svd_witness: phase 1 runs on the
+ *   second stream behind the products / on a third stream from quantization
+ *   on, its c_s scans waiting for the products / after phase 0); "prelaunch_at" 0 | 1 | 2 (how many phase-0 stages are queued
  *   before them); "gemm_priority" 0 | 1 (second stream priority);
  *   "stage_elems" 256 (elements per stage block, multiple of 16 in [16, 256]);
  *   "stage_ilp" 1 | 2 | 4 (half-cells in flight per thread); "nt_stores" 0 | 1
