@@ -148,6 +148,9 @@ def main():
     ap.add_argument("--profile-prefix", default="k_stage",
                     help="kernel-name prefix the timed-region profiler records ('' = all)")
     ap.add_argument("--breakdown", action="store_true", help="print per-kernel ms/step to stderr")
+    ap.add_argument("--shard", choices=["replicas", "rows"], default="replicas",
+                    help="N>1: one matrix per rank (weak scaling, default) or one matrix "
+                         "row-block sharded over the ranks (strong scaling, BASELINE config 4)")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine tuning option name=value (svdw_set_option), repeatable")
     args = ap.parse_args()
@@ -158,17 +161,26 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
+    # Rehearsal on fewer GPUs than ranks (e.g. a 1-GPU box): BENCH_DIST_BACKEND=gloo
+    # and ranks share devices round-robin. Timings are then not per-GPU numbers.
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
 
     import halo2_svd041_amd as hs
 
-    m, u, d, v, g = rank_workload(args.seed, rank, N, M)
+    rows_mode = args.shard == "rows" and world > 1
+    m, u, d, v, g = rank_workload(args.seed, 0 if rows_mode else rank, N, M)
     dev = torch.device("cuda", local)
     dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev)
                       for x in (m, u, v, d))
@@ -177,6 +189,8 @@ def main():
     for kv in args.opt:
         name, _, val = kv.partition("=")
         ctx.set_option(name, int(val))
+    if rows_mode:
+        ctx.set_shard(rank, world)
 
     for _ in range(args.warmup):
         cnt = hs.svd_witness(ctx, dm, du, dv, dd, g)
@@ -198,7 +212,10 @@ def main():
     stats = ctx.profile_collect() if not args.no_profile else []
 
     cells_step = cnt["advice0"] + cnt["advice1"]
-    elapsed, cells_all = reduce_over_ranks(elapsed, cells_step, dist, dev)
+    elapsed, cells_all = reduce_over_ranks(elapsed, cells_step, dist,
+                                           dev if backend == "nccl" else torch.device("cpu"))
+    if rows_mode:
+        cells_all = float(cells_step)        # one witness, split over the ranks
     total_cells = cells_all * args.steps
     value = total_cells / elapsed
 
@@ -212,22 +229,27 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if rows_mode else "weak",
             "vs_baseline": None,
             "dtype": "bn254_fr (u32 limbs; exact int8-digit MFMA GEMM)",
             "data": "synthetic (input-creator.py recipe, seeded; gamma = sha256 mod p)",
             "config": {
                 "workload": (f"svd_verify_witness N={N} M={M} PRECISION_BITS={args.p} "
-                             f"LOOKUP_BITS={args.lb}, one matrix per GPU"),
+                             f"LOOKUP_BITS={args.lb}, "
+                             + ("one matrix row-sharded over the GPUs" if rows_mode
+                                else "one matrix per GPU")),
                 "N": N, "M": M, "precision_bits": args.p, "lookup_bits": args.lb,
                 "advice_cells_per_matrix": cells_step,
                 "lookup_cells_per_matrix": cnt["lookup0"] + cnt["lookup1"],
-                "parallelism": f"replicas x{world} (no data-path collective)",
+                "parallelism": (f"row blocks x{world} of one matrix (no data-path collective)"
+                                if rows_mode else f"replicas x{world} (no data-path collective)"),
             },
         }
         if stats:
             kname, roof, breakdown = roofline_from_profile(stats, args.steps)
-            traffic, src = pmc_traffic(kname, N, M, args.p, args.lb)
+            # the committed PMC summary is for the whole witness on one GPU
+            traffic, src = (None, None) if rows_mode else pmc_traffic(kname, N, M, args.p,
+                                                                         args.lb)
             if traffic is not None:
                 roof["traffic"] = traffic
                 roof["traffic_source"] = src

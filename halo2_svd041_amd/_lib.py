@@ -58,6 +58,11 @@ class KStat(ct.Structure):
                 ("max_ms", ct.c_double), ("bytes", ct.c_double), ("ops", ct.c_double)]
 
 
+class Segment(ct.Structure):
+    _fields_ = [("phase", ct.c_uint32), ("lookup", ct.c_uint32), ("off", ct.c_uint64),
+                ("n", ct.c_uint64)]
+
+
 class Counts(ct.Structure):
     _fields_ = [("advice0", ct.c_uint64), ("advice1", ct.c_uint64), ("lookup0", ct.c_uint64),
                 ("lookup1", ct.c_uint64)]
@@ -111,6 +116,8 @@ SIGNATURES = {
     "svdw_set_option": (_i32, [_P, ct.c_char_p, ct.c_int64]),
     "svdw_profile_enable": (_i32, [_P, _i32]),
     "svdw_profile_filter": (_i32, [_P, ct.c_char_p]),
+    "svdw_set_shard": (_i32, [_P, _u32, _u32]),
+    "svdw_shard_segments": (_i32, [_P, ct.POINTER(Segment), _u64, _u64p]),
     "svdw_profile_collect": (_i32, [_P, ct.POINTER(KStat), _u32, ct.POINTER(_u32)]),
     "svdw_plan_svd": (_i32, [_u32, _u32, _u32, _u32, ct.POINTER(SvdConfig), ct.POINTER(Counts)]),
 }

@@ -310,6 +310,16 @@ struct svdw_ctx {
     bool prelaunched = false;               // this witness's products were queued on st2
     std::vector<hipEvent_t> gemm_done;      // their completion events (this witness)
     std::vector<hipEvent_t> wait_before_cs; // verify_mul_many: wait before the c_s scans
+    // Row-block sharding of one witness: this context computes the
+    // rows [R rank / world, R (rank + 1) / world) of every row-parallel stage
+    // (R = that stage's row count) into the globally laid-out streams; shared
+    // inputs (quantized operands, single constants, the Freivalds b.g values)
+    // are computed in full. `owned` lists the cell ranges this rank is the
+    // source of, for reassembly.
+    uint32_t shard_rank = 0, shard_world = 1;
+    struct Seg { uint32_t phase, lookup; uint64_t off, n; };
+    std::vector<Seg> owned;
+    DBuf bvfull[kMaxScanJobs];              // shard mode: full b.g values per verify_mul
     // second stream: GEMMs overlap the HBM-bound stages; third: phase 1
     hipStream_t st2 = nullptr;
     hipStream_t st3 = nullptr;
@@ -374,7 +384,17 @@ static void fetch_bits(svdw_ctx* c) {
         reg_bits(c, c->qmat[i], c->qbits[i]);
     }
 }
+static bool sharded(const svdw_ctx* c) { return c->shard_world > 1; }
+// rows of a row-parallel stage (R rows) that this rank computes / owns
+static void shard_rows(const svdw_ctx* c, uint64_t R, uint64_t* r0, uint64_t* r1) {
+    *r0 = R * c->shard_rank / c->shard_world;
+    *r1 = R * (c->shard_rank + 1) / c->shard_world;
+}
+static void own(svdw_ctx* c, uint32_t phase, bool lookup, uint64_t off, uint64_t n) {
+    if (sharded(c) && n) c->owned.push_back({phase, lookup ? 1u : 0u, off, n});
+}
 static void clear_streams(svdw_ctx* c) {
+    c->owned.clear();
     c->bits_pending = false;
     for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
     c->mbits.clear();
@@ -504,11 +524,21 @@ static void check_vec(const svdw_ctx* c, const svdw_vec& v) { check_mat(c, mat_o
 static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, uint32_t cols,
                          uint64_t off, uint64_t loff, const char* tag) {
     StageArgs& a = pb.a;
-    if (c->dry || nelem == 0) return;
+    uint32_t eb = 0, ee = nelem;
+    if (sharded(c) && nelem) {
+        const uint64_t cw = cols ? cols : 1, R = nelem / cw;
+        uint64_t r0, r1;
+        shard_rows(c, R, &r0, &r1);
+        if (R > 1) {                                      // single cells: every rank
+            eb = (uint32_t)(r0 * cw);
+            ee = (uint32_t)(r1 * cw);
+        }
+    }
+    if (c->dry || ee <= eb) return;
     a.out_adv = cellp(c, phase, off);
     a.out_lk = a.L ? c->ph[phase].lk + loff : nullptr;
-    a.e_begin = 0;
-    a.e_end = nelem;
+    a.e_begin = eb;
+    a.e_end = ee;
     a.cols = cols ? cols : 1;
     a.flags = c->stage_flags;
     a.sweep_nb = c->stage_sweep;
@@ -530,14 +560,25 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     for (uint32_t i = 0; i < a.nmo; ++i) loads += a.mo[i].op == MO_LOAD;
     {
         ProfScope ps(c, c->st, std::string("k_stage:") + tag,
-                     32.0 * nelem * ((double)a.C + a.L + loads), 0);
+                     32.0 * (ee - eb) * ((double)a.C + a.L + loads), 0);
         hipck(launch_stage(a, c->st), "k_stage");
     }
+}
+// shard ownership of a stage's cells: this rank's rows (single cells: the last rank)
+static void stage_own(svdw_ctx* c, uint32_t phase, const PB& pb, uint32_t nelem, uint32_t cols,
+                      uint64_t off, uint64_t loff) {
+    if (!sharded(c) || !nelem) return;
+    const uint64_t cw = cols ? cols : 1, R = nelem / cw;
+    uint64_t r0, r1;
+    shard_rows(c, R, &r0, &r1);
+    own(c, phase, false, off + r0 * cw * pb.a.C, (r1 - r0) * cw * pb.a.C);
+    own(c, phase, true, loff + r0 * cw * pb.a.L, (r1 - r0) * cw * pb.a.L);
 }
 static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, uint32_t cols,
                           const char* tag, uint64_t* loff_out = nullptr) {
     uint64_t off = 0, loff = 0;
     append(c, phase, (uint64_t)nelem * pb.a.C, (uint64_t)nelem * pb.a.L, &off, &loff);
+    stage_own(c, phase, pb, nelem, cols, off, loff);
     if (loff_out) *loff_out = loff;
     stage_launch(c, phase, pb, nelem, cols, off, loff, tag);
     return off;
@@ -566,6 +607,11 @@ static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, ui
         }
         ProfScope ps(c, c->st, "k_quantize", 40.0 * n, 0);
         hipck(launch_quantize(src, n, cellp(c, phase, off), (int)c->P, blockmax, c->st), "k_quantize");
+    }
+    if (sharded(c)) {            // every rank quantizes all of it (operands of the products)
+        uint64_t r0, r1;
+        shard_rows(c, rows, &r0, &r1);
+        own(c, phase, false, off + r0 * cols, (r1 - r0) * cols);
     }
     return svdw_mat{phase, rows, cols, off, (int64_t)cols, 1};
 }
@@ -832,6 +878,10 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
         hipck(launch_gemm_mont(view_of(c, a), view_of(c, b), N, K, M, out, M, 1, s), "k_gemm_mont");
     }
 }
+// rows [r0, r1) of a matrix view
+static svdw_mat row_block(const svdw_mat& a, uint64_t r0, uint64_t r1) {
+    return svdw_mat{a.phase, (uint32_t)(r1 - r0), a.cols, a.off + r0 * a.rs, a.rs, a.cs};
+}
 // honest_prover_mat_mul (src/matrix/mod.rs:546-568). bits_a/bits_b: known bounds or ~0u.
 // If the product was launched ahead on st2 (c->pre), only append and order st after it.
 static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a,
@@ -843,6 +893,11 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
     append(c, phase, (uint64_t)N * M, 0, &off, nullptr);
     svdw_mat cs{phase, N, M, off, (int64_t)M, 1};
     if (c->gemm_log) c->gemm_log->push_back(off);
+    uint64_t sr0 = 0, sr1 = N;                            // shard: rows of c_s computed here
+    if (sharded(c)) {
+        shard_rows(c, N, &sr0, &sr1);
+        own(c, phase, false, off + sr0 * M, (sr1 - sr0) * M);
+    }
     {   // |c_s| <= K * 2^bits_a * 2^bits_b, resolved when the operand bounds are known
         uint32_t lk = 0;
         while ((1ull << lk) < a.cols) ++lk;
@@ -866,6 +921,12 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
         bits_b = sym ? bb[0] : bb[1];
         reg_bits(c, a, bits_a);
         reg_bits(c, b, bits_b);
+    }
+    if (sharded(c)) {
+        if (sr1 > sr0)
+            gemm_exec(c, c->st, row_block(a, sr0, sr1), b, cellp(c, phase, off + sr0 * M), bits_a,
+                      bits_b);
+        return cs;
     }
     gemm_exec(c, c->st, a, b, cellp(c, phase, off), bits_a, bits_b);
     return cs;
@@ -897,10 +958,17 @@ static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, cons
     const uint32_t R = a.rows, L = a.cols;
     uint64_t off;
     append(c, phase, (uint64_t)R * (3ull * L + 1), 0, &off, nullptr);
+    uint64_t r0 = 0, r1 = R;
+    if (sharded(c)) {
+        REQUIRE(c->scan_impl >= 3, "row sharding needs scan_impl >= 3");
+        shard_rows(c, R, &r0, &r1);
+        own(c, phase, false, off + r0 * (3ull * L + 1), (r1 - r0) * (3ull * L + 1));
+    }
     if (!c->dry) {
         ProfScope ps(c, c->st, a.cs == 1 ? "k_matvec_scan:rows" : "k_matvec_scan:cols", 32.0 * (double)R * (4.0 * L + 1) + 64.0 * L, (double)R * L);
-        hipck(launch_matvec_scan(view_of(c, a), 0, R, L, wc, w.ws, w.wn, cellp(c, phase, off),
-                                 c->scan_impl, na, c->st), "k_matvec_scan");
+        hipck(launch_matvec_scan(view_of(c, a), (uint32_t)r0, (uint32_t)r1, L, wc, w.ws, w.wn,
+                                 cellp(c, phase, off + r0 * (3ull * L + 1)), c->scan_impl, na,
+                                 c->st), "k_matvec_scan");
     }
     return svdw_vec{phase, R, off + 3ull * L, (int64_t)(3ull * L + 1)};
 }
@@ -913,6 +981,21 @@ static WScaled vec_prep(svdw_ctx* c, const svdw_vec& v, DBuf& bc, DBuf& bm, int 
     if (!c->dry)
         hipck(launch_vec_prep(view_of(c, svdw_mat{v.phase, 1, v.len, v.off, 0, v.stride}), v.len,
                               (Fr*)bc.p, ws, wn, scale_factor(na), c->st), "k_vec_prep");
+    return WScaled{ws, wn};
+}
+// the same from a device vector of len canonical values
+static WScaled vec_prep_ptr(svdw_ctx* c, const Fr* src, uint32_t len, DBuf& bc, DBuf& bm, int na) {
+    ensure_buf(c, bc, (size_t)len * sizeof(Fr));
+    ensure_buf(c, bm, 2 * (size_t)len * sizeof(Fr));
+    Fr* ws = (Fr*)bm.p;
+    Fr* wn = na < 8 && ws ? ws + len : nullptr;
+    if (!c->dry) {
+        DView w;
+        memset(&w, 0, sizeof w);
+        w.ptr = src;
+        w.rs = 0; w.cs = 1; w.rows = 1; w.cols = len;
+        hipck(launch_vec_prep(w, len, (Fr*)bc.p, ws, wn, scale_factor(na), c->st), "k_vec_prep");
+    }
     return WScaled{ws, wn};
 }
 static svdw_vec field_mat_vec_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a,
@@ -1024,18 +1107,30 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         Plan& p = pl.back();
         p.one.cell(p.one.K(fr_from_u64(1)));                  // load_witness(F::ONE)
         append(c, phase, p.one.a.C, 0, &p.one_off, &p.one_loff);
+        stage_own(c, phase, p.one, 1, 1, p.one_off, p.one_loff);
         if (d > 1) {                                          // v_i = mul(v_{i-1}, init_rand)
             uint8_t prev = p.pows.load(0), cur = p.pows.load(1);
             p.pows.cell(p.pows.K(0)); p.pows.cell(prev); p.pows.cell(p.pows.K(gamma)); p.pows.cell(cur);
             append(c, phase, (uint64_t)(d - 1) * p.pows.a.C, 0, &p.pows_off, &p.pows_loff);
+            stage_own(c, phase, p.pows, d - 1, 1, p.pows_off, p.pows_loff);
         }
         p.csv = scan_append(cs);
         p.bv = scan_append(b);
         p.abv = scan_append(a);
+        if (sharded(c)) {                                 // this rank's rows of the three scans
+            for (const auto& sv : {std::make_pair(cs, p.csv), std::make_pair(b, p.bv),
+                                   std::make_pair(a, p.abv)}) {
+                const uint64_t rowc = 3ull * sv.first.cols + 1, base = sv.second.off - 3ull * sv.first.cols;
+                uint64_t r0, r1;
+                shard_rows(c, sv.first.rows, &r0, &r1);
+                own(c, phase, false, base + r0 * rowc, (r1 - r0) * rowc);
+            }
+        }
         uint8_t x = p.eq.load(0), y = p.eq.load(1);           // is_equal per row (result unused)
         p.eq.g_is_equal(x, y);
         append(c, phase, (uint64_t)a.rows * p.eq.a.C, (uint64_t)a.rows * p.eq.a.L, &p.eq_off,
                &p.eq_loff);
+        stage_own(c, phase, p.eq, a.rows, 1, p.eq_off, p.eq_loff);
     }
     if (c->dry) return;
     // pass 2: launches
@@ -1064,8 +1159,12 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
             const svdw_mat a = mat_of(i);
             const svdw_vec v = vec_of(i);
             const WScaled w = ws_of(i);
+            uint64_t r0 = 0, r1 = a.rows;                 // shard: this rank's rows
+            const uint64_t rowc = 3ull * a.cols + 1, base = v.off - 3ull * a.cols;
+            if (sharded(c)) shard_rows(c, a.rows, &r0, &r1);
             sb.job[i] = ScanJob{view_of(c, a), wc_of(i), w.ws, w.wn,
-                                cellp(c, phase, v.off - 3ull * a.cols), a.cols, a.rows, 0, 0};
+                                cellp(c, phase, base + r0 * rowc), a.cols, (uint32_t)(r1 - r0), 0,
+                                (uint32_t)r0};
             bytes += 32.0 * a.rows * (4.0 * a.cols + 1) + 64.0 * a.cols;
             ops += (double)a.rows * a.cols;
         }
@@ -1091,7 +1190,19 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     run_batch("k_matvec_scan:b", b_of, [&](int i) { return pl[i].bv; }, gc,
               [&](int) { return g_b; }, na_b);
     WScaled wb[kMaxScanJobs];
-    for (int i = 0; i < n; ++i) wb[i] = vec_prep(c, pl[i].bv, c->wbc[i], c->wbs[i], na_a);
+    for (int i = 0; i < n; ++i) {
+        if (sharded(c)) {
+            // only this rank's rows of the b.g scans exist: every entry of b.g
+            // comes from the values-only mat-vec instead
+            const svdw_mat b = vm[i].b;
+            ensure_buf(c, c->bvfull[i], (size_t)b.rows * sizeof(Fr));
+            hipck(launch_matvec_values(view_of(c, b), b.rows, b.cols, g_b.ws, g_b.wn, na_b,
+                                       (Fr*)c->bvfull[i].p, c->st), "k_matvec_values");
+            wb[i] = vec_prep_ptr(c, (const Fr*)c->bvfull[i].p, b.rows, c->wbc[i], c->wbs[i], na_a);
+        } else {
+            wb[i] = vec_prep(c, pl[i].bv, c->wbc[i], c->wbs[i], na_a);
+        }
+    }
     run_batch("k_matvec_scan:a", a_of, [&](int i) { return pl[i].abv; },
               [&](int i) { return (const Fr*)c->wbc[i].p; }, [&](int i) { return wb[i]; }, na_a);
     for (hipEvent_t ev : c->wait_before_cs)
@@ -1108,6 +1219,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
 static void verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svdw_mat& b,
                        const svdw_mat& cs, const Fr& gamma) {
     if (c->scan_impl < 3) {                       // legacy per-call path (A/B only)
+        REQUIRE(!sharded(c), "row sharding needs scan_impl >= 3");
         verify_mul_legacy(c, phase, a, b, cs, gamma);
         return;
     }
@@ -1178,12 +1290,20 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         const unsigned* sa[3] = {sl[0], sl[1], sl[2]};
         const unsigned* sb[3] = {sl[2], sl[1], sl[2]};
         for (int g = 0; g < 3; ++g) {
+            // shard: rows [r0, r1) of the product only
+            uint64_t r0 = 0, r1 = A[g].rows;
+            if (sharded(c)) shard_rows(c, A[g].rows, &r0, &r1);
+            const svdw_mat Ag = sharded(c) ? row_block(A[g], r0, r1) : A[g];
+            Fr* outg = cellp(c, m.phase, log[g] + r0 * B[g].cols);
             // CRT: v's residue planes from m.v^T (covering v.v^T too) serve v.v^T
-            if (on_device)
-                gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ~0u, ~0u, sa[g], sb[g],
-                          dev_quantized, g == 0 ? sl[2] : nullptr, g == 2);
+            const bool reuse = !sharded(c);
+            if (r1 <= r0) {
+                // nothing of this product on this rank
+            } else if (on_device)
+                gemm_exec(c, c->st2, Ag, B[g], outg, ~0u, ~0u, sa[g], sb[g], dev_quantized,
+                          reuse && g == 0 ? sl[2] : nullptr, reuse && g == 2);
             else
-                gemm_exec(c, c->st2, A[g], B[g], cellp(c, m.phase, log[g]), ba[g], bb[g]);
+                gemm_exec(c, c->st2, Ag, B[g], outg, ba[g], bb[g]);
             c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
             c->gemm_done.push_back(c->pre.back().ev);
         }
@@ -1229,6 +1349,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
 static void check_svd_phase1(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u, const svdw_mat& v,
                              const svdw_svd_payload& pl, const Fr& g) {
     if (c->scan_impl < 3) {
+        REQUIRE(!sharded(c), "row sharding needs scan_impl >= 3");
         verify_mul(c, 1, m, pl.v_t, pl.m_times_vt, g);
         verify_mul(c, 1, u, pl.u_t, pl.u_times_ut, g);
         verify_mul(c, 1, v, pl.v_t, pl.v_times_vt, g);
@@ -1371,6 +1492,7 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             for (int i = 0; i < kMaxScanJobs; ++i) {
                 if (c->wbc[i].p) (void)hipFree(c->wbc[i].p);
                 if (c->wbs[i].p) (void)hipFree(c->wbs[i].p);
+                if (c->bvfull[i].p) (void)hipFree(c->bvfull[i].p);
             }
             if (c->hbits) (void)hipHostFree(c->hbits);
             if (c->ev_bits) (void)hipEventDestroy(c->ev_bits);
@@ -1588,6 +1710,24 @@ int svdw_svd_witness(svdw_ctx* c, const double* m, const double* u, const double
         REQUIRE(c->dry || (m && u && v && d), "null input matrix");
         svdw_counts k = svd_witness(c, m, u, v, d, N, M, on_device != 0, *cfg, fr_from_words(gamma));
         if (counts) *counts = k;
+    });
+}
+int svdw_set_shard(svdw_ctx* c, uint32_t rank, uint32_t world) {
+    return guarded([&] {
+        REQUIRE(c, "null ctx");
+        REQUIRE(world >= 1 && rank < world, "svdw_set_shard: need rank < world");
+        c->shard_rank = rank;
+        c->shard_world = world;
+        c->owned.clear();
+    });
+}
+int svdw_shard_segments(const svdw_ctx* c, svdw_segment* out, uint64_t cap, uint64_t* n) {
+    return guarded([&] {
+        REQUIRE(c && n, "null argument");
+        *n = c->owned.size();
+        for (uint64_t i = 0; i < c->owned.size() && i < cap && out; ++i)
+            out[i] = svdw_segment{c->owned[i].phase, c->owned[i].lookup, c->owned[i].off,
+                                  c->owned[i].n};
     });
 }
 int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {

@@ -1640,6 +1640,62 @@ __global__ __launch_bounds__(256) void k_matvec_scan(const DView A, uint32_t r_b
     }
 }
 
+// out[r] = sum_j A(r, j) w_j mod p for rows [0, R) (values only, no cells): the
+// row-sharded witness needs every entry of b.g while it emits the b.g scan
+// cells of its own rows only. One block per row; products as in the scan.
+template <int NA>
+__global__ __launch_bounds__(256) void k_matvec_values(const DView A, uint32_t L,
+                                                       const Fr* __restrict__ wm,
+                                                       const Fr* __restrict__ wn,
+                                                       Fr* __restrict__ out) {
+    __shared__ U9 part[256];
+    const uint32_t r = blockIdx.x, tid = threadIdx.x;
+    const Fr zero = fr_zero();
+    U9 acc = u9_from(zero);
+    for (uint32_t j = tid; j < L; j += 256) {
+        const Fr a = view_load(A, zero, r, j);
+        Fr s;
+        if constexpr (NA == 8) {
+            s = mont_mul(a, ld_fr(wm + j));
+        } else {
+            const bool neg = a.w[7] != 0;
+            Fr mag = zero;
+            uint32_t br = 0;
+#pragma unroll
+            for (int q = 0; q < NA; ++q) {
+                const uint64_t t = (uint64_t)p_word(q) - a.w[q] - br;
+                br = (uint32_t)(t >> 63);
+                mag.w[q] = neg ? (uint32_t)t : a.w[q];
+            }
+            s = mont_mul_small<NA>(mag, ld_fr((neg ? wn : wm) + j));
+        }
+        acc = u9_add(acc, u9_from(s));                     // <= 2^13 terms of < p: < 2^267
+    }
+    part[tid] = acc;
+    __syncthreads();
+    for (uint32_t h = 128; h > 0; h >>= 1) {
+        if (tid < h) part[tid] = u9_add(part[tid], part[tid + h]);
+        __syncthreads();
+    }
+    if (tid == 0) st_fr(out + r, reduce9(part[0].w));
+}
+hipError_t launch_matvec_values(const DView& A, uint32_t R, uint32_t L, const Fr* w_scaled,
+                                const Fr* w_neg, int na, Fr* out, hipStream_t st) {
+    if (!R || !L) return hipSuccess;
+    if (L > 8192) return hipErrorInvalidValue;
+    const dim3 g(R), b(256);
+    switch (na) {
+    case 1: hipLaunchKernelGGL(k_matvec_values<1>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
+    case 2: hipLaunchKernelGGL(k_matvec_values<2>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
+    case 3: hipLaunchKernelGGL(k_matvec_values<3>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
+    case 4: hipLaunchKernelGGL(k_matvec_values<4>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
+    case 5: hipLaunchKernelGGL(k_matvec_values<5>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
+    case 6: hipLaunchKernelGGL(k_matvec_values<6>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
+    default: hipLaunchKernelGGL(k_matvec_values<8>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
+    }
+    return hipGetLastError();
+}
+
 template <int T>
 static void launch_scan_t(const ScanBatch& b, int na, dim3 g, hipStream_t st) {
     const dim3 blk(256);

@@ -19,7 +19,8 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import Counts, KStat, Mat, Params, Payload, SvdConfig, SvdwError, Vec, check, lib
+from ._lib import (Counts, KStat, Mat, Params, Payload, Segment, SvdConfig, SvdwError, Vec, check,
+                   lib)
 
 P_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 
@@ -124,8 +125,20 @@ class Context:
         check(lib().svdw_set_gemm_impl(self._h, {"mfma": 0, "valu": 1}[impl]))
 
     def set_option(self, name: str, value: int) -> None:
-        """Tuning knobs (include/svdw.h): gemm_impl, nt_stores, stage_ilp, scan_impl, overlap."""
+        """Tuning knobs of svdw_set_option (include/svdw.h); results are bit-identical."""
         check(lib().svdw_set_option(self._h, name.encode(), int(value)))
+
+    def set_shard(self, rank: int, world: int) -> None:
+        """Row-block sharding of one witness over `world` contexts (svdw_set_shard)."""
+        check(lib().svdw_set_shard(self._h, int(rank), int(world)))
+
+    def shard_segments(self) -> list:
+        """[(phase, lookup, off, n)] cell ranges this rank is the source of."""
+        n = ct.c_uint64()
+        check(lib().svdw_shard_segments(self._h, None, 0, ct.byref(n)))
+        buf = (Segment * max(n.value, 1))()
+        check(lib().svdw_shard_segments(self._h, buf, n.value, ct.byref(n)))
+        return [(s.phase, s.lookup, s.off, s.n) for s in buf[:n.value]]
 
     def profile(self, on: bool = True, prefix: str = "") -> None:
         """Record HIP events around kernel launches (names starting with `prefix`)."""

@@ -209,6 +209,26 @@ int svdw_profile_filter(svdw_ctx* ctx, const char* prefix);
  * written to out; *n = number of distinct names) and drop them. */
 int svdw_profile_collect(svdw_ctx* ctx, svdw_kstat* out, uint32_t cap, uint32_t* n);
 
+/* ---------------------------------------------- row-block sharding
+ * One witness split over `world` contexts (one per GPU, no data exchange):
+ * after svdw_set_shard(ctx, rank, world), svdw_svd_witness / check_svd_phase0/1
+ * compute on this context only the rows [R*rank/world, R*(rank+1)/world) of
+ * every row-parallel stage (R = the stage's row count: N or M), writing them
+ * at their global offsets of full-size streams; the shared operands (quantized
+ * m, u, v, d, single constants, the Freivalds b.g vector values) are computed
+ * by every rank. svdw_shard_segments lists the cell ranges this rank is the
+ * source of; over all ranks they tile every stream exactly once, so the global
+ * witness is the union (a gather to one device, or kept sharded-resident).
+ * Works on planning contexts too (segments without cells). world = 1: off. */
+typedef struct {
+    uint32_t phase;     /* 0 / 1 */
+    uint32_t lookup;    /* 0: advice stream, 1: lookup stream */
+    uint64_t off, n;    /* cells [off, off + n) */
+} svdw_segment;
+int svdw_set_shard(svdw_ctx* ctx, uint32_t rank, uint32_t world);
+/* Up to cap segments of the last witness into out; *n = total count. */
+int svdw_shard_segments(const svdw_ctx* ctx, svdw_segment* out, uint64_t cap, uint64_t* n);
+
 /* Closed-form cell counts of svdw_svd_witness without touching a device. */
 int svdw_plan_svd(uint32_t N, uint32_t M, uint32_t precision_bits, uint32_t lookup_bits,
                   const svdw_svd_config* cfg, svdw_counts* counts);
