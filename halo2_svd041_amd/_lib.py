@@ -63,6 +63,12 @@ class Segment(ct.Structure):
                 ("n", ct.c_uint64)]
 
 
+class InputDims(ct.Structure):
+    _fields_ = [("m_rows", ct.c_uint32), ("m_cols", ct.c_uint32), ("u_rows", ct.c_uint32),
+                ("u_cols", ct.c_uint32), ("v_rows", ct.c_uint32), ("v_cols", ct.c_uint32),
+                ("d_len", ct.c_uint32)]
+
+
 class Counts(ct.Structure):
     _fields_ = [("advice0", ct.c_uint64), ("advice1", ct.c_uint64), ("lookup0", ct.c_uint64),
                 ("lookup1", ct.c_uint64)]
@@ -117,6 +123,7 @@ SIGNATURES = {
     "svdw_profile_enable": (_i32, [_P, _i32]),
     "svdw_profile_filter": (_i32, [_P, ct.c_char_p]),
     "svdw_set_shard": (_i32, [_P, _u32, _u32]),
+    "svdw_parse_svd_input": (_i32, [ct.c_char_p, _u64, _i32, ct.POINTER(InputDims), _P, _P, _P, _P]),
     "svdw_shard_segments": (_i32, [_P, ct.POINTER(Segment), _u64, _u64p]),
     "svdw_profile_collect": (_i32, [_P, ct.POINTER(KStat), _u32, ct.POINTER(_u32)]),
     "svdw_plan_svd": (_i32, [_u32, _u32, _u32, _u32, ct.POINTER(SvdConfig), ct.POINTER(Counts)]),

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libsvdw.so")
 SOURCES = ["kernels.hip", "engine.cpp"]
-HEADERS = ["fr.hpp", "prog.hpp", "kernels.hpp"]
+HEADERS = ["fr.hpp", "prog.hpp", "kernels.hpp", "crt_tables.hpp", "ingest.hpp"]
 ARCH = os.environ.get("SVDW_OFFLOAD_ARCH", "gfx950")
 
 

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/svdw.h"
+#include "ingest.hpp"
 #include "kernels.hpp"
 
 using namespace svdw;
@@ -1710,6 +1711,25 @@ int svdw_svd_witness(svdw_ctx* c, const double* m, const double* u, const double
         REQUIRE(c->dry || (m && u && v && d), "null input matrix");
         svdw_counts k = svd_witness(c, m, u, v, d, N, M, on_device != 0, *cfg, fr_from_words(gamma));
         if (counts) *counts = k;
+    });
+}
+int svdw_parse_svd_input(const char* text, uint64_t len, int mode, svdw_input_dims* dims,
+                         double* m, double* u, double* d, double* v) {
+    return guarded([&] {
+        REQUIRE(text && dims, "null argument");
+        REQUIRE(mode == SVDW_PARSE_SERDE || mode == SVDW_PARSE_CORRECT, "parse mode: 0 or 1");
+        svdw_ingest::SvdInput in;
+        std::string err;
+        svdw_ingest::Parser ps(text, len, mode);
+        if (!ps.parse(in, err)) fail(SVDW_EINVAL, "svd input: " + err);
+        REQUIRE(in.d.rows == 0 && in.m.rows && in.u.rows && in.v.rows,
+                "svd input: m, u, v must be matrices and d a vector");
+        *dims = svdw_input_dims{in.m.rows, in.m.cols, in.u.rows, in.u.cols, in.v.rows, in.v.cols,
+                                in.d.cols};
+        const std::pair<double*, const svdw_ingest::Array*> outs[4] = {
+            {m, &in.m}, {u, &in.u}, {d, &in.d}, {v, &in.v}};
+        for (const auto& o : outs)
+            if (o.first) memcpy(o.first, o.second->v.data(), o.second->v.size() * sizeof(double));
     });
 }
 int svdw_set_shard(svdw_ctx* c, uint32_t rank, uint32_t world) {

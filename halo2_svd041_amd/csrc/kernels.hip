@@ -980,9 +980,7 @@ __device__ __forceinline__ void residues_body(const DView& x, uint32_t rows, uin
     }
     uint32_t* o = out + (uint64_t)row * kw + kg;
     const uint64_t plane = (uint64_t)rows_pad * kw;
-#pragma unroll
-    for (int k = 0; k < kCrtMaxMod; ++k) {
-        if (k >= n) break;
+    for (int k = 0; k < n; ++k) {
         const int m = (int)c_crt_mod[k];
         const float inv = c_crt_invf[k];
         uint32_t word = 0;
@@ -1186,9 +1184,7 @@ __global__ __launch_bounds__(256) void k_crt_combine(const uint8_t* __restrict__
 #pragma unroll
         for (int w = 0; w < 16; ++w) acc[q][w] = 0;
     }
-#pragma unroll
-    for (int k = 0; k < kCrtMaxMod; ++k) {
-        if (k >= n) break;
+    for (int k = 0; k < n; ++k) {
         uint32_t r[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) r[q] = rp[k * plane + (uint64_t)q * 8 * rpad_b];

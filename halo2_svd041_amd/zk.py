@@ -19,8 +19,8 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import (Counts, KStat, Mat, Params, Payload, Segment, SvdConfig, SvdwError, Vec, check,
-                   lib)
+from ._lib import (Counts, InputDims, KStat, Mat, Params, Payload, Segment, SvdConfig, SvdwError,
+                   Vec, check, lib)
 
 P_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
 
@@ -368,6 +368,30 @@ def svd_witness(ctx: Context, m, u, v, d, gamma: int, cfg: SvdConfigPy = SvdConf
         check(lib().svdw_svd_witness(ctx.handle, *[a.ctypes.data for a in arrs], N, M, 0,
                                      ct.byref(cfgc), g.ctypes.data, ct.byref(cnt)))
     return cnt.as_dict()
+
+
+def parse_svd_input(src, mode: str = "serde") -> dict:
+    """Arrays m, u, d, v of the example's input file (data/matrix.in; a path,
+    bytes or str), parsed natively like serde_json's default float path
+    ("serde", what examples/svd_example.rs:326-330 reads) or correctly rounded
+    ("correct"); svdw_parse_svd_input."""
+    if isinstance(src, (bytes, bytearray)):
+        text = bytes(src)
+    elif isinstance(src, str) and src.lstrip().startswith("{"):
+        text = src.encode()
+    else:
+        with open(src, "rb") as fh:
+            text = fh.read()
+    md = {"serde": 0, "correct": 1}[mode]
+    dims = InputDims()
+    check(lib().svdw_parse_svd_input(text, len(text), md, ct.byref(dims), None, None, None, None))
+    m = np.empty((dims.m_rows, dims.m_cols))
+    u = np.empty((dims.u_rows, dims.u_cols))
+    v = np.empty((dims.v_rows, dims.v_cols))
+    d = np.empty(dims.d_len)
+    check(lib().svdw_parse_svd_input(text, len(text), md, ct.byref(dims), m.ctypes.data,
+                                     u.ctypes.data, d.ctypes.data, v.ctypes.data))
+    return {"m": m, "u": u, "d": d, "v": v}
 
 
 def plan_svd(N: int, M: int, precision_bits: int, lookup_bits: int,

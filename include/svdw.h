@@ -229,6 +229,22 @@ int svdw_set_shard(svdw_ctx* ctx, uint32_t rank, uint32_t world);
 /* Up to cap segments of the last witness into out; *n = total count. */
 int svdw_shard_segments(const svdw_ctx* ctx, svdw_segment* out, uint64_t cap, uint64_t* n);
 
+/* ------------------------------------------------------------ input ingest
+ * Parse the example's input file (data/matrix.in of input-creator.py:23-44;
+ * read by examples/svd_example.rs:326-330 with serde_json::from_str) into
+ * row-major f64 arrays. mode SVDW_PARSE_SERDE reproduces serde_json's default
+ * float parse (u64 significand x / / 10^|e| in f64; 1 ulp off correct rounding
+ * on ~10 % of the values, which changes quantized cells), SVDW_PARSE_CORRECT
+ * rounds correctly. Call with null arrays to get the shapes, then again with
+ * arrays of those sizes. */
+#define SVDW_PARSE_SERDE 0
+#define SVDW_PARSE_CORRECT 1
+typedef struct {
+    uint32_t m_rows, m_cols, u_rows, u_cols, v_rows, v_cols, d_len;
+} svdw_input_dims;
+int svdw_parse_svd_input(const char* text, uint64_t len, int mode, svdw_input_dims* dims,
+                         double* m, double* u, double* d, double* v);
+
 /* Closed-form cell counts of svdw_svd_witness without touching a device. */
 int svdw_plan_svd(uint32_t N, uint32_t M, uint32_t precision_bits, uint32_t lookup_bits,
                   const svdw_svd_config* cfg, svdw_counts* counts);
