@@ -1764,6 +1764,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             REQUIRE(value >= 16 && value <= 256 && value % 16 == 0,
                     "stage_elems: a multiple of 16 in [16, 256]");
             c->stage_elems = (uint32_t)value;
+        } else if (n == "stage_divide") {
+            c->stage_flags = (c->stage_flags & ~STAGE_DIVIDE) | (value ? STAGE_DIVIDE : 0);
         } else if (n == "stage_sweep") {
             REQUIRE(value >= 0 && value <= 4096, "stage_sweep: 0 (off) or a grid size <= 4096");
             c->stage_sweep = (uint32_t)value;

@@ -254,6 +254,39 @@ __device__ __forceinline__ void stream_cells(uint4* __restrict__ out, uint32_t t
     }
 }
 
+// Default path: one half-cell per lane per iteration, the (element, slot) of
+// the lane's next cell tracked incrementally (the cell index advances by
+// blockDim/2 each step) instead of a mul_hi division per half-cell.
+template <bool NT>
+__device__ __forceinline__ void stream_cells_inc(uint4* __restrict__ out, uint32_t total,
+                                                 const SlotOp* __restrict__ ops, uint32_t C,
+                                                 uint32_t magic, const uint32_t* sK,
+                                                 const uint32_t* sV, uint32_t nv) {
+    const uint32_t h = threadIdx.x & 1, step = blockDim.x >> 1;
+    const uint32_t dq = step / C, dr = step - dq * C, ev = nv * VW;
+    uint32_t c = threadIdx.x >> 1;
+    uint32_t el = fastdiv(c, C, magic), slot = c - el * C;
+    uint32_t vbase = el * ev;                             // LDS word offset of this element
+    for (uint32_t hc = threadIdx.x; hc < total; hc += blockDim.x) {
+        const SlotOp op = ops[slot];
+        const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + vbase + op.src * VW;
+        const uint4 v = extract_half(src, op.lo, op.nbits, h);
+        if (NT) {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 w = {v.x, v.y, v.z, v.w};
+            __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(out + hc));
+        } else {
+            out[hc] = v;
+        }
+        slot += dr;
+        vbase += dq * ev;
+        if (slot >= C) {
+            slot -= C;
+            vbase += ev;
+        }
+    }
+}
+
 // Sweep mode: local element l of batch jb of block b is global element
 // e_begin + G (b + nb (jb E/G + l/G)) + l % G.
 struct SweepMap {
@@ -443,7 +476,11 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     if (a.flags & STAGE_NT_STORES) SVDW_STREAM(true, 1);
     else if (a.flags & STAGE_ILP4) SVDW_STREAM(false, 4);
     else if (a.flags & STAGE_ILP2) SVDW_STREAM(false, 2);
-    else SVDW_STREAM(false, 1);
+    else if (a.flags & STAGE_DIVIDE) SVDW_STREAM(false, 1);
+    else {
+        stream_cells_inc<false>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
+        if (a.L) stream_cells_inc<false>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
+    }
 #undef SVDW_STREAM
     break;
   }

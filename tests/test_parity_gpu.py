@@ -167,6 +167,7 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                                   {"gemm_rt": 0}, {"prelaunch_at": 2}, {"gemm_crt": 0},
                                   {"stage_sweep": 1}, {"stage_sweep": 3}, {"stage_elems": 64},
                                   {"stage_elems": 192}, {"phase1_overlap": 0}, {"phase1_overlap": 2},
+                                  {"stage_divide": 1},
                                   {"overlap": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
