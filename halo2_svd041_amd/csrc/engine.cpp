@@ -301,6 +301,7 @@ struct svdw_ctx {
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
     uint32_t stage_flags = 0;               // STAGE_* (svdw_set_option "nt_stores", "stage_ilp")
     uint32_t stage_sweep = 0;               // "stage_sweep": persistent grid of the sweep mode (0 off)
+    uint32_t stage_asweep = 0;              // "stage_asweep": grid of the aligned-chunk sweep (0 off)
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
     int scan_impl = 4;                      // svdw_set_option "scan_impl"
     int prelaunch_at = 0;                   // "prelaunch_at": GEMMs queued before stage 0/1/2
@@ -553,6 +554,10 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     if (c->stage_sweep && c->stage_elems == kStageElems &&
         (uint64_t)nelem >= 4ull * kStageElems * c->stage_sweep / kSweepG)
         a.flags |= STAGE_SWEEP;
+    if (c->stage_asweep && (uint64_t)(ee - eb) >= 64ull * kStageElems) {
+        a.flags |= STAGE_ASWEEP;
+        a.sweep_nb = c->stage_asweep;
+    }
     // 32-bit magics for fastdiv (divisor 1 is handled in the kernel)
     auto magic = [](uint64_t d) -> uint32_t { return d > 1 ? (uint32_t)(((1ull << 32) + d - 1) / d) : 0; };
     a.cdiv_magic = magic(a.C);
@@ -1764,6 +1769,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             REQUIRE(value >= 16 && value <= 256 && value % 16 == 0,
                     "stage_elems: a multiple of 16 in [16, 256]");
             c->stage_elems = (uint32_t)value;
+        } else if (n == "stage_asweep") {
+            REQUIRE(value >= 0 && value <= 4096, "stage_asweep: 0 (off) or a grid size <= 4096");
+            c->stage_asweep = (uint32_t)value;
         } else if (n == "stage_divide") {
             c->stage_flags = (c->stage_flags & ~STAGE_DIVIDE) | (value ? STAGE_DIVIDE : 0);
         } else if (n == "stage_sweep") {

@@ -325,6 +325,82 @@ __device__ __forceinline__ void stream_cells_sweep(uint4* __restrict__ out, uint
     }
 }
 
+// Phase A for one element: run the stage's micro-ops, values into myV (LDS).
+__device__ __forceinline__ void element_program(const StageArgs& a, uint32_t e, uint32_t* myV,
+                                                const uint32_t* sK, const MicroOp* sMo,
+                                                const DView* sVw, const Fr& pf0, bool in0,
+                                                const Fr& pf1, bool in1) {
+    const uint32_t i = e / a.cols, j = e - (e / a.cols) * a.cols;
+    for (uint32_t m = 0; m < a.nmo; ++m) {
+        const MicroOp op = sMo[m];
+        uint32_t* dst = myV + op.dst * VW;
+        switch (op.op) {
+            case MO_LOAD: {
+                if (op.a == 0 && in0) {
+                    lds_put(dst, pf0);
+                } else if (op.a == 1 && in1) {
+                    lds_put(dst, pf1);
+                } else {
+                    const DView vw = sVw[op.a];
+                    lds_put(dst, view_load(vw, lds_get(sK + vw.pad_k * VW), i, j));
+                }
+                break;
+            }
+            case MO_ADDK:
+                lds_put(dst, fr_add(lds_get(myV + op.a * VW), lds_get(sK + op.b * VW)));
+                break;
+            case MO_SUB:
+                lds_put(dst, fr_sub(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
+                break;
+            case MO_MUL:
+                lds_put(dst, fr_mul(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
+                break;
+            case MO_LIMBSHL: {
+                const Fr sv = lds_get(myV + op.a * VW);
+                // 64-bit window at bit p0 (p0 < 256), masked to p1 bits, << b
+                const uint32_t lo = op.p0, q = lo >> 5, r = lo & 31;
+                uint32_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    w0 = (t == (int)q) ? sv.w[t] : w0;
+                    w1 = (t == (int)q + 1) ? sv.w[t] : w1;
+                    w2 = (t == (int)q + 2) ? sv.w[t] : w2;
+                }
+                const uint64_t w01 = (uint64_t)w0 | ((uint64_t)w1 << 32);
+                uint64_t x = r ? ((w01 >> r) | ((uint64_t)w2 << (64 - r))) : w01;
+                if (op.p1 < 64) x &= (1ull << op.p1) - 1;
+                const uint32_t sh = op.b;
+                const uint64_t lo64 = sh < 64 ? (x << sh) : 0;
+                const uint64_t hi64 = sh == 0 ? 0 : (sh < 64 ? (x >> (64 - sh)) : (x << (sh - 64)));
+                Fr v = fr_zero();
+                v.w[0] = (uint32_t)lo64; v.w[1] = (uint32_t)(lo64 >> 32);
+                v.w[2] = (uint32_t)hi64; v.w[3] = (uint32_t)(hi64 >> 32);
+                lds_put(dst, v);
+                break;
+            }
+            case MO_FDBL: {
+                Fr v = lds_get(myV + op.a * VW);
+                for (uint32_t t = 0; t < op.b; ++t) v = fr_add(v, v);
+                lds_put(dst, v);
+                break;
+            }
+            case MO_ISZERO: {
+                const Fr v = lds_get(myV + op.a * VW);
+                const bool z = fr_is_zero(v);
+                const Fr inv = z ? fr_from_u64(1) : fr_inv(v);
+                lds_put(dst, fr_from_u64(z ? 1 : 0));
+                lds_put(dst + VW, inv);
+                break;
+            }
+            case MO_POWK:
+                lds_put(dst, fr_pow_u64(lds_get(sK + op.a * VW), (uint64_t)e + op.p0));
+                break;
+            default:
+                break;
+        }
+    }
+    }
+
 __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t nv = a.nv;
@@ -382,78 +458,8 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     }
     // ---- phase A: per-element micro-ops (constants / ops / views read from LDS:
     // dynamic indexing into the by-value kernel argument would go to scratch)
-    if (tid < ne) {
-        const uint32_t i = e / a.cols, j = e - (e / a.cols) * a.cols;
-        uint32_t* myV = sV + tid * nv * VW;
-        for (uint32_t m = 0; m < a.nmo; ++m) {
-            const MicroOp op = sMo[m];
-            uint32_t* dst = myV + op.dst * VW;
-            switch (op.op) {
-                case MO_LOAD: {
-                    if (op.a == 0 && in0) {
-                        lds_put(dst, pf0);
-                    } else if (op.a == 1 && in1) {
-                        lds_put(dst, pf1);
-                    } else {
-                        const DView vw = sVw[op.a];
-                        lds_put(dst, view_load(vw, lds_get(sK + vw.pad_k * VW), i, j));
-                    }
-                    break;
-                }
-                case MO_ADDK:
-                    lds_put(dst, fr_add(lds_get(myV + op.a * VW), lds_get(sK + op.b * VW)));
-                    break;
-                case MO_SUB:
-                    lds_put(dst, fr_sub(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
-                    break;
-                case MO_MUL:
-                    lds_put(dst, fr_mul(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
-                    break;
-                case MO_LIMBSHL: {
-                    const Fr sv = lds_get(myV + op.a * VW);
-                    // 64-bit window at bit p0 (p0 < 256), masked to p1 bits, << b
-                    const uint32_t lo = op.p0, q = lo >> 5, r = lo & 31;
-                    uint32_t w0 = 0, w1 = 0, w2 = 0;
-#pragma unroll
-                    for (int t = 0; t < 8; ++t) {
-                        w0 = (t == (int)q) ? sv.w[t] : w0;
-                        w1 = (t == (int)q + 1) ? sv.w[t] : w1;
-                        w2 = (t == (int)q + 2) ? sv.w[t] : w2;
-                    }
-                    const uint64_t w01 = (uint64_t)w0 | ((uint64_t)w1 << 32);
-                    uint64_t x = r ? ((w01 >> r) | ((uint64_t)w2 << (64 - r))) : w01;
-                    if (op.p1 < 64) x &= (1ull << op.p1) - 1;
-                    const uint32_t sh = op.b;
-                    const uint64_t lo64 = sh < 64 ? (x << sh) : 0;
-                    const uint64_t hi64 = sh == 0 ? 0 : (sh < 64 ? (x >> (64 - sh)) : (x << (sh - 64)));
-                    Fr v = fr_zero();
-                    v.w[0] = (uint32_t)lo64; v.w[1] = (uint32_t)(lo64 >> 32);
-                    v.w[2] = (uint32_t)hi64; v.w[3] = (uint32_t)(hi64 >> 32);
-                    lds_put(dst, v);
-                    break;
-                }
-                case MO_FDBL: {
-                    Fr v = lds_get(myV + op.a * VW);
-                    for (uint32_t t = 0; t < op.b; ++t) v = fr_add(v, v);
-                    lds_put(dst, v);
-                    break;
-                }
-                case MO_ISZERO: {
-                    const Fr v = lds_get(myV + op.a * VW);
-                    const bool z = fr_is_zero(v);
-                    const Fr inv = z ? fr_from_u64(1) : fr_inv(v);
-                    lds_put(dst, fr_from_u64(z ? 1 : 0));
-                    lds_put(dst + VW, inv);
-                    break;
-                }
-                case MO_POWK:
-                    lds_put(dst, fr_pow_u64(lds_get(sK + op.a * VW), (uint64_t)e + op.p0));
-                    break;
-                default:
-                    break;
-            }
-        }
-    }
+    if (tid < ne)
+        element_program(a, e, sV + tid * nv * VW, sK, sMo, sVw, pf0, in0, pf1, in1);
     __syncthreads();
 
     // ---- phase B: advice cells, then lookup cells
@@ -486,9 +492,113 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
   }
 }
 
+// Address-sweep variant (STAGE_ASWEEP): persistent grid; every block writes
+// whole 4 KiB-aligned chunks of the stream (128 cells) -- chunk q goes to block
+// q % grid -- so at any moment the chip writes a narrow window of aligned
+// chunks (the store pattern that reaches ~6.4 TB/s, tools/storepat3.hip).
+// A batch = K chunks of this block; its elements (those whose cells touch
+// the chunks; boundary elements are also computed by the neighbouring
+// block) get phase A, then the chunks are written 16 B per lane.
+__global__ __launch_bounds__(256) void k_stage_as(const StageArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const uint32_t nv = a.nv;
+    uint32_t* sK = smem;
+    uint32_t* sV = sK + kMaxK * VW;
+    SlotOp* sAdv = reinterpret_cast<SlotOp*>(sV + kStageElems * nv * VW);
+    SlotOp* sLk = sAdv + kMaxAdv;
+    MicroOp* sMo = reinterpret_cast<MicroOp*>(sLk + kMaxLk);
+    DView* sVw = reinterpret_cast<DView*>(sMo + kMaxMicro);
+    __shared__ uint32_t sOff[65], sElo[64];
+    const uint32_t tid = threadIdx.x, NB = gridDim.x;
+    for (uint32_t q = tid; q < a.nk; q += blockDim.x) lds_put(sK + q * VW, a.K[q]);
+    for (uint32_t q = tid; q < a.C; q += blockDim.x) sAdv[q] = a.adv[q];
+    for (uint32_t q = tid; q < a.L; q += blockDim.x) sLk[q] = a.lk[q];
+    for (uint32_t q = tid; q < a.nmo; q += blockDim.x) sMo[q] = a.mo[q];
+    if (tid < kMaxViews) sVw[tid] = a.view[tid];
+    __syncthreads();
+    const Fr zero = fr_zero();
+    for (int pass = 0; pass < 2; ++pass) {
+        const uint32_t Cp = pass ? a.L : a.C;
+        if (!Cp) continue;
+        const SlotOp* ops = pass ? sLk : sAdv;
+        const uint32_t magic = pass ? a.ldiv_magic : a.cdiv_magic;
+        Fr* outp = pass ? a.out_lk : a.out_adv;            // cell 0 of element 0
+        const uint64_t abs0 = (uint64_t)(uintptr_t)outp >> 5;   // absolute cell index
+        const uint64_t F = abs0 + (uint64_t)a.e_begin * Cp, Lc = abs0 + (uint64_t)a.e_end * Cp;
+        const uint64_t q0 = F >> 7, q1 = (Lc + 127) >> 7;
+        const uint32_t per = (128 + Cp - 1) / Cp + 1;      // elements touching one chunk
+        const uint32_t K = min(64u, kStageElems / per);
+        for (uint64_t j = 0;; ++j) {
+            const uint64_t qb = q0 + blockIdx.x + (uint64_t)NB * K * j;
+            if (qb >= q1) break;                          // uniform
+            if (tid < K) {                                // element range of each chunk
+                const uint64_t q = qb + (uint64_t)NB * tid;
+                uint32_t n = 0, elo = 0;
+                if (q < q1) {
+                    const uint64_t c0 = max(q << 7, F), c1 = min((q + 1) << 7, Lc);   // [c0, c1)
+                    elo = (uint32_t)((c0 - abs0) / Cp);
+                    const uint32_t ehi = (uint32_t)((c1 - 1 - abs0) / Cp);
+                    n = ehi - elo + 1;
+                }
+                sElo[tid] = elo;
+                sOff[tid + 1] = n;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                sOff[0] = 0;
+                for (uint32_t q = 1; q <= K; ++q) sOff[q] += sOff[q - 1];
+            }
+            __syncthreads();
+            // phase A: local element t -> (chunk k, element)
+            if (tid < sOff[K]) {
+                uint32_t kk = 0;
+                while (sOff[kk + 1] <= tid) ++kk;
+                const uint32_t e = sElo[kk] + (tid - sOff[kk]);
+                element_program(a, e, sV + tid * nv * VW, sK, sMo, sVw, zero, false, zero, false);
+            }
+            __syncthreads();
+            // phase B: chunk by chunk, 256 half-cells each; four chunks in
+            // flight per thread (one block per CU has few waves to hide latency)
+            constexpr int U = 4;
+            for (uint32_t k0 = 0; k0 < K; k0 += U) {
+                uint4 val[U];
+                uint64_t dst[U];
+                bool ok[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t kk = k0 + u;
+                    const uint64_t q = qb + (uint64_t)NB * kk;
+                    const uint64_t A = (q << 7) + (tid >> 1);   // absolute cell
+                    ok[u] = kk < K && q < q1 && A >= F && A < Lc;
+                    const uint32_t rel = ok[u] ? (uint32_t)(A - abs0) : 0u, h = tid & 1;
+                    const uint32_t e = fastdiv(rel, Cp, magic), slot = rel - e * Cp;
+                    const SlotOp op = ops[slot];
+                    const uint32_t kc = ok[u] ? kk : 0u;
+                    const uint32_t local = ok[u] ? sOff[kc] + (e - sElo[kc]) : 0u;
+                    const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW
+                                                         : sV + (local * nv + op.src) * VW;
+                    val[u] = extract_half(src, op.lo, op.nbits, h);
+                    dst[u] = (uint64_t)rel * 2 + h;
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (ok[u]) reinterpret_cast<uint4*>(outp)[dst[u]] = val[u];
+            }
+            __syncthreads();
+        }
+    }
+}
+
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     if (a.e_end <= a.e_begin) return hipSuccess;
     const uint32_t n = a.e_end - a.e_begin;
+    if (a.flags & STAGE_ASWEEP) {
+        const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1, kStageElems);
+        // rel = cell index from element 0 must fit the 32-bit fastdiv
+        if ((uint64_t)a.e_end * (a.C > a.L ? a.C : a.L) >= (1ull << 31)) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_stage_as, dim3(a.sweep_nb ? a.sweep_nb : 256), dim3(256), lds, st, a);
+        return hipGetLastError();
+    }
     const uint32_t E = a.E ? a.E : kStageElems;
     if (E > kStageElems || ((a.flags & STAGE_SWEEP) && E != kStageElems)) return hipErrorInvalidValue;
     const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1, E);

@@ -65,6 +65,7 @@ static constexpr uint32_t STAGE_ILP4 = 4;
 // neighbouring groups, a narrow front across the cell stream.
 static constexpr uint32_t STAGE_SWEEP = 8;
 static constexpr uint32_t STAGE_DIVIDE = 16;      // per-half-cell division (A/B reference)
+static constexpr uint32_t STAGE_ASWEEP = 32;      // persistent grid over 4 KiB-aligned chunks
 static constexpr uint32_t kSweepG = 4;
 
 static constexpr int kMaxViews = 2;

@@ -270,3 +270,18 @@ def test_row_sharded_matches_unsharded_256(gpu_ctx_factory):
     assert np.array_equal(got[(0, 0)], full.advice(0))
     assert np.array_equal(got[(1, 0)], full.advice(1))
     assert np.array_equal(got[(0, 1)], full.lookups(0))
+
+
+@pytest.mark.parametrize("grid", [1, 7, 256])
+def test_address_sweep_stages_parity(gpu_ctx_factory, grid):
+    """Aligned-chunk sweep stage kernel (stage_asweep): stages of >= 16384 elements
+    take it; chunk edges cut elements, which both neighbouring blocks compute."""
+    import halo2_svd041_amd as hs
+    N, M, P = 150, 131, 63
+    m, u, d, v = gen_svd_input(N, M, seed=grid)
+    g = gamma_for(grid)
+    ctx = gpu_ctx_factory(P)
+    ctx.set_option("stage_asweep", grid)
+    hs.svd_witness(ctx, m, u, v, d, g)
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+    _assert_streams(ctx, a0, l0, a1)
