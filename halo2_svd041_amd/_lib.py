@@ -69,6 +69,10 @@ class InputDims(ct.Structure):
                 ("d_len", ct.c_uint32)]
 
 
+class DivScale(ct.Structure):
+    _fields_ = [("shift_bits", ct.c_uint32), ("num_bits", ct.c_uint32)]
+
+
 class Counts(ct.Structure):
     _fields_ = [("advice0", ct.c_uint64), ("advice1", ct.c_uint64), ("lookup0", ct.c_uint64),
                 ("lookup1", ct.c_uint64)]
@@ -106,6 +110,11 @@ SIGNATURES = {
     "svdw_check_mat_diff": (_i32, [_P, ct.POINTER(Mat), ct.POINTER(Mat), _P]),
     "svdw_check_mat_id": (_i32, [_P, ct.POINTER(Mat), ct.POINTER(Vec), _P]),
     "svdw_mat_times_diag_mat": (_i32, [_P, ct.POINTER(Mat), ct.POINTER(Vec), ct.POINTER(Mat)]),
+    "svdw_rescale_matrix": (_i32, [_P, ct.POINTER(Mat), ct.POINTER(DivScale), ct.POINTER(Mat)]),
+    "svdw_zkvector_inner_product": (_i32, [_P, _u32, ct.POINTER(Vec), ct.POINTER(Vec),
+                                           ct.POINTER(DivScale), ct.POINTER(Vec)]),
+    "svdw_zkvector_mul": (_i32, [_P, _u32, ct.POINTER(Vec), ct.POINTER(Mat), ct.POINTER(DivScale),
+                                 ct.POINTER(Vec)]),
     "svdw_honest_prover_mat_mul": (_i32, [_P, _u32, ct.POINTER(Mat), ct.POINTER(Mat),
                                           ct.POINTER(Mat)]),
     "svdw_field_mat_vec_mul": (_i32, [_P, _u32, ct.POINTER(Mat), ct.POINTER(Vec),

@@ -82,6 +82,12 @@ static int big_bits(const BigU& b) {
     return 0;
 }
 static bool big_is_zero(const BigU& b) { return big_bits(b) == 0; }
+static BigU big_pow2(uint32_t k) {     // k < 256
+    BigU b;
+    b.v = fr_zero();
+    b.v.w[k / 32] = 1u << (k % 32);
+    return b;
+}
 static BigU big_add_u32(const BigU& a, uint32_t s) {
     BigU r;
     Fr t = fr_from_u64(s);
@@ -168,6 +174,11 @@ struct PB {
         cell(x); cell(K(k)); cell(K(1)); cell(t);
         return t;
     }
+    uint8_t g_sub_k(uint8_t x, const Fr& k) {       // sub(x, Constant(k)): [x-k, k, 1, x]
+        uint8_t d = addk(x, fr_neg(k));
+        cell(d); cell(K(k)); cell(K(1)); cell(x);
+        return d;
+    }
     uint8_t g_sub(uint8_t x, uint8_t y) {           // sub: [x-y, y, 1, x]
         uint8_t d = newv();
         op(MO_SUB, d, x, y);
@@ -239,6 +250,26 @@ struct PB {
         uint32_t rb = (big_bits(bnd) + lb - 1) / lb * lb;
         range_check(x, rb);
         check_less_than_k(x, bnd, rb);
+    }
+    // RangeChip::div_mod(t, 2^p, nb) [ext halo2-base 0.4.1]: [r, 2^p, q, t], then
+    // check_big_less_than_safe(q, 2^nb / 2^p + 1), check_big_less_than_safe(r, 2^p)
+    uint8_t div_mod_pow2(uint8_t t, uint32_t p, uint32_t nb) {
+        uint8_t q = newv();
+        op(MO_SHR, q, t, 0, (uint16_t)p);
+        uint8_t r = newv();
+        op(MO_LIMBSHL, r, t, 0, 0, (uint16_t)p);
+        cell(r); cell(K(pow2_fr(p))); cell(q); cell(t);
+        check_big_less_than_safe(q, big_add_u32(big_pow2(nb - p), 1));
+        check_big_less_than_safe(r, big_pow2(p));
+        return q;
+    }
+    // FixedPointChip041::signed_div_scale, parameterised (oracle/pyoracle.py
+    // signed_div_scale; chip source unavailable, parity unpinned): add 2^s,
+    // div_mod by 2^p on nb bits, subtract 2^(s-p). Returns the quotient value.
+    uint8_t signed_div_scale(uint8_t x, uint32_t p, uint32_t s, uint32_t nb) {
+        uint8_t t = g_add_k(x, pow2_fr(s));
+        uint8_t q = div_mod_pow2(t, p, nb);
+        return g_sub_k(q, pow2_fr(s - p));
     }
     // check_abs_less_than (src/matrix/mod.rs:425-435)
     void check_abs_less_than(uint8_t x, const BigU& bnd) {
@@ -550,11 +581,15 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     for (uint32_t i = 0; i < a.nmo; ++i)
         heavy |= a.mo[i].op == MO_MUL || a.mo[i].op == MO_ISZERO || a.mo[i].op == MO_POWK;
     a.E = heavy ? kStageElems : c->stage_elems;
+    // keep the block's LDS (element values) within 64 KiB: fewer elements per
+    // block for stages with many values (signed_div_scale)
+    while (a.E > 64 && stage_lds_bytes(a.nv ? a.nv : 1, a.E) > 65536) a.E -= 64;
     // interleaved groups only pay off on big stages (and need whole batches of work)
-    if (c->stage_sweep && c->stage_elems == kStageElems &&
+    if (c->stage_sweep && c->stage_elems == kStageElems && a.E == kStageElems &&
         (uint64_t)nelem >= 4ull * kStageElems * c->stage_sweep / kSweepG)
         a.flags |= STAGE_SWEEP;
-    if (c->stage_asweep && (uint64_t)(ee - eb) >= 64ull * kStageElems) {
+    if (c->stage_asweep && (uint64_t)(ee - eb) >= 64ull * kStageElems &&
+        stage_lds_bytes(a.nv ? a.nv : 1, kStageElems) <= 65536) {
         a.flags |= STAGE_ASWEEP;
         a.sweep_nb = c->stage_asweep;
     }
@@ -689,6 +724,59 @@ static svdw_mat mat_times_diag_mat(svdw_ctx* c, const svdw_mat& a, const svdw_ve
     pb.g_mul(x, y);
     uint64_t off = run_stage(c, a.phase, pb, a.rows * v.len, v.len, "mat_times_diag_mat");
     return svdw_mat{a.phase, a.rows, v.len, off + 3, (int64_t)4 * v.len, 4};
+}
+
+// signed_div_scale constants (svdw_div_scale; zero fields -> 3P, shift + 1)
+struct DivScale {
+    uint32_t s, nb;
+};
+static DivScale div_scale_of(const svdw_ctx* c, const svdw_div_scale* cfg) {
+    DivScale d;
+    d.s = cfg && cfg->shift_bits ? cfg->shift_bits : 3 * c->P;
+    d.nb = cfg && cfg->num_bits ? cfg->num_bits : d.s + 1;
+    REQUIRE(d.s >= c->P && d.s < 254 && d.nb > d.s && d.nb <= 253 && d.nb - c->P <= 200,
+            "signed_div_scale: need P <= shift_bits < num_bits <= 253, num_bits - P <= 200");
+    return d;
+}
+// ZkMatrix::rescale_matrix (src/matrix/mod.rs:354-375): signed_div_scale of
+// every entry of c_s, row-major; the result matrix is the final sub's cell 0.
+static svdw_mat rescale_matrix(svdw_ctx* c, const svdw_mat& cs, DivScale d) {
+    PB pb(c->LB);
+    pb.a.view[0] = view_of(c, cs);
+    pb.signed_div_scale(pb.load(0), c->P, d.s, d.nb);
+    const uint32_t C = pb.a.C;
+    uint64_t off = run_stage(c, cs.phase, pb, cs.rows * cs.cols, cs.cols, "rescale_matrix");
+    return svdw_mat{cs.phase, cs.rows, cs.cols, off + C - 4, (int64_t)C * cs.cols, C};
+}
+static svdw_vec field_mat_vec_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svdw_vec& v);
+// ZkVector::inner_product (src/matrix/mod.rs:79-106): gate.inner_product(x, self)
+// (the field_mat_vec_mul row layout with x as the row), then signed_div_scale.
+static svdw_vec zkvector_inner_product(svdw_ctx* c, uint32_t phase, const svdw_vec& self,
+                                       const svdw_vec& x, DivScale d) {
+    REQUIRE(self.len == x.len && x.len >= 1, "ZkVector::inner_product: length mismatch");
+    svdw_vec s = field_mat_vec_mul(c, phase, svdw_mat{x.phase, 1, x.len, x.off, 0, x.stride}, self);
+    PB pb(c->LB);
+    pb.a.view[0] = view_of(c, mat_of_vec(s));
+    pb.signed_div_scale(pb.load(0), c->P, d.s, d.nb);
+    const uint32_t C = pb.a.C;
+    uint64_t off = run_stage(c, phase, pb, 1, 1, "signed_div_scale");
+    return svdw_vec{phase, 1, off + C - 4, 1};
+}
+// ZkVector::mul (src/matrix/mod.rs:169-182): inner_product with each row of a
+// (one row scan + one stage per row; config-1 plumbing, not the hot path).
+static svdw_vec zkvector_mul(svdw_ctx* c, uint32_t phase, const svdw_vec& self, const svdw_mat& a,
+                             DivScale d) {
+    REQUIRE(a.cols == self.len, "ZkVector::mul: a.num_col != self.size()");
+    svdw_vec first{}, prev{};
+    for (uint32_t i = 0; i < a.rows; ++i) {
+        svdw_vec row{a.phase, a.cols, a.off + (uint64_t)((int64_t)i * a.rs), a.cs};
+        svdw_vec y = zkvector_inner_product(c, phase, self, row, d);
+        if (i == 0) first = y;
+        if (i == 1) first.stride = (int64_t)(y.off - prev.off);
+        prev = y;
+    }
+    first.len = a.rows;
+    return first;
 }
 
 // Balanced base-256 digits needed for |x| < 2^bits.
@@ -1647,6 +1735,39 @@ int svdw_mat_times_diag_mat(svdw_ctx* c, const svdw_mat* a, const svdw_vec* v, s
         check_vec(c, *v);
         pregrow(c, [&](svdw_ctx* x) { mat_times_diag_mat(x, *a, *v); });
         *out = mat_times_diag_mat(c, *a, *v);
+    });
+}
+int svdw_rescale_matrix(svdw_ctx* c, const svdw_mat* cs, const svdw_div_scale* cfg, svdw_mat* out) {
+    return guarded([&] {
+        REQUIRE(c && cs && out, "null argument");
+        check_mat(c, *cs);
+        const DivScale d = div_scale_of(c, cfg);
+        pregrow(c, [&](svdw_ctx* x) { rescale_matrix(x, *cs, d); });
+        *out = rescale_matrix(c, *cs, d);
+    });
+}
+int svdw_zkvector_inner_product(svdw_ctx* c, uint32_t phase, const svdw_vec* self, const svdw_vec* x,
+                                const svdw_div_scale* cfg, svdw_vec* out) {
+    return guarded([&] {
+        REQUIRE(c && self && x && out, "null argument");
+        REQUIRE(phase < 2, "phase must be 0 or 1");
+        check_vec(c, *self);
+        check_vec(c, *x);
+        const DivScale d = div_scale_of(c, cfg);
+        pregrow(c, [&](svdw_ctx* y) { zkvector_inner_product(y, phase, *self, *x, d); });
+        *out = zkvector_inner_product(c, phase, *self, *x, d);
+    });
+}
+int svdw_zkvector_mul(svdw_ctx* c, uint32_t phase, const svdw_vec* self, const svdw_mat* a,
+                      const svdw_div_scale* cfg, svdw_vec* out) {
+    return guarded([&] {
+        REQUIRE(c && self && a && out, "null argument");
+        REQUIRE(phase < 2, "phase must be 0 or 1");
+        check_vec(c, *self);
+        check_mat(c, *a);
+        const DivScale d = div_scale_of(c, cfg);
+        pregrow(c, [&](svdw_ctx* y) { zkvector_mul(y, phase, *self, *a, d); });
+        *out = zkvector_mul(c, phase, *self, *a, d);
     });
 }
 int svdw_honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_mat* a, const svdw_mat* b,

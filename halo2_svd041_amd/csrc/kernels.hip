@@ -211,9 +211,6 @@ __device__ __forceinline__ uint4 extract_half(const uint32_t* s, uint32_t lo, ui
 }
 
 // LDS carve (bytes, all 16-aligned): consts | element values | slot ops | micro-ops | views
-__host__ __device__ constexpr uint32_t stage_lds_bytes(uint32_t nv, uint32_t E) {
-    return kMaxK * 32 + E * nv * 32 + (kMaxAdv + kMaxLk) * 4 + kMaxMicro * 8 + kMaxViews * 48;
-}
 
 // x / d for x * d < 2^32 via one 32-bit mul_hi (magic = ceil(2^32 / d), d >= 2).
 __device__ __forceinline__ uint32_t fastdiv(uint32_t x, uint32_t d, uint32_t magic) {
@@ -395,6 +392,19 @@ __device__ __forceinline__ void element_program(const StageArgs& a, uint32_t e, 
             case MO_POWK:
                 lds_put(dst, fr_pow_u64(lds_get(sK + op.a * VW), (uint64_t)e + op.p0));
                 break;
+            case MO_SHR: {
+                const uint32_t* s = myV + op.a * VW;    // words straight from LDS
+                const uint32_t q = op.p0 >> 5, r = op.p0 & 31;
+                Fr v;
+#pragma unroll
+                for (uint32_t t = 0; t < 8; ++t) {
+                    const uint32_t lo = t + q < 8 ? s[t + q] : 0u;
+                    const uint32_t hi = t + q + 1 < 8 ? s[t + q + 1] : 0u;
+                    v.w[t] = r ? (lo >> r) | (hi << (32 - r)) : lo;
+                }
+                lds_put(dst, v);
+                break;
+            }
             default:
                 break;
         }

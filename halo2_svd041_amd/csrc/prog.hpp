@@ -43,6 +43,7 @@ enum : uint8_t {
     MO_FDBL,         // V[dst] = V[a] * 2^b mod p
     MO_ISZERO,       // V[dst] = (V[a]==0), V[dst+1] = V[a]==0 ? 1 : V[a]^-1
     MO_POWK,         // V[dst] = K[a] ^ (e + p0)                         (verify_mul's gamma powers)
+    MO_SHR,          // V[dst] = V[a] >> p0 (canonical value, full width; div_mod quotients)
 };
 struct MicroOp {
     uint8_t op, dst, a, b;
@@ -73,7 +74,7 @@ static constexpr int kMaxMicro = 16;
 static constexpr int kMaxAdv = 112;
 static constexpr int kMaxLk = 32;
 static constexpr int kMaxK = 32;
-static constexpr int kMaxV = 8;
+static constexpr int kMaxV = 12;
 
 // Kernel argument block of one stage launch (passed by value, < 4 KiB).
 struct StageArgs {
@@ -95,5 +96,11 @@ struct StageArgs {
     Fr K[kMaxK];
 };
 static_assert(sizeof(StageArgs) < 4096, "kernel argument block too large");
+
+// Dynamic LDS of a stage block: constants, E elements' values, slot / micro-op
+// tables and views (constexpr: host and device).
+constexpr uint32_t stage_lds_bytes(uint32_t nv, uint32_t E) {
+    return kMaxK * 32 + E * nv * 32 + (kMaxAdv + kMaxLk) * 4 + kMaxMicro * 8 + kMaxViews * 48;
+}
 
 }  // namespace svdw

@@ -19,7 +19,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import (Counts, InputDims, KStat, Mat, Params, Payload, Segment, SvdConfig, SvdwError,
+from ._lib import (Counts, DivScale, InputDims, KStat, Mat, Params, Payload, Segment, SvdConfig, SvdwError,
                    Vec, check, lib)
 
 P_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
@@ -212,6 +212,16 @@ class ZkMatrix:
         check(lib().svdw_verify_mul(ctx.handle, phase, ct.byref(a.mat), ct.byref(b.mat),
                                     ct.byref(c_s.mat), g.ctypes.data))
 
+    @staticmethod
+    def rescale_matrix(ctx: Context, c_s: "ZkMatrix", shift_bits: int = 0,
+                       num_bits: int = 0) -> "ZkMatrix":
+        """ZkMatrix::rescale_matrix (src/matrix/mod.rs:354-375). signed_div_scale's
+        layout is parity unpinned (include/svdw.h, svdw_div_scale)."""
+        out = Mat()
+        cfg = DivScale(shift_bits, num_bits)
+        check(lib().svdw_rescale_matrix(ctx.handle, ct.byref(c_s.mat), ct.byref(cfg), ct.byref(out)))
+        return ZkMatrix(ctx, out)
+
     def values(self) -> np.ndarray:
         """Cell values (rows, cols, 4) uint64 (host copy, for inspection)."""
         cells = self.ctx.advice(self.mat.phase)
@@ -242,6 +252,29 @@ class ZkVector:
             check(lib().svdw_zkvector_new(ctx.handle, phase, a.ctypes.data, a.size, 0,
                                           ct.byref(out)))
         return cls(ctx, out)
+
+    def values(self) -> np.ndarray:
+        """Cell values (len, 4) uint64 (host copy, for inspection)."""
+        cells = self.ctx.advice(self.vec.phase)
+        return cells[self.vec.off + np.arange(self.vec.len) * self.vec.stride]
+
+    def inner_product(self, x: "ZkVector", phase: int = 0, shift_bits: int = 0,
+                      num_bits: int = 0) -> "ZkVector":
+        """ZkVector::inner_product (src/matrix/mod.rs:79-106): 1-element vector."""
+        out = Vec()
+        cfg = DivScale(shift_bits, num_bits)
+        check(lib().svdw_zkvector_inner_product(self.ctx.handle, phase, ct.byref(self.vec),
+                                                ct.byref(x.vec), ct.byref(cfg), ct.byref(out)))
+        return ZkVector(self.ctx, out)
+
+    def mul(self, a: ZkMatrix, phase: int = 0, shift_bits: int = 0,
+            num_bits: int = 0) -> "ZkVector":
+        """ZkVector::mul (src/matrix/mod.rs:169-182): a . self, rescaled."""
+        out = Vec()
+        cfg = DivScale(shift_bits, num_bits)
+        check(lib().svdw_zkvector_mul(self.ctx.handle, phase, ct.byref(self.vec), ct.byref(a.mat),
+                                      ct.byref(cfg), ct.byref(out)))
+        return ZkVector(self.ctx, out)
 
     def entries_less_than(self, max_bits: int) -> None:
         """ZkVector::entries_less_than (src/matrix/mod.rs:185-194)."""

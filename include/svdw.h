@@ -125,6 +125,29 @@ int svdw_check_mat_id(svdw_ctx* ctx, const svdw_mat* a, const svdw_vec* scalar_i
                       const uint64_t tol[4]);
 /* mat_times_diag_mat (src/matrix/mod.rs:610-627): a[i][j]*v[j], j < len(v). */
 int svdw_mat_times_diag_mat(svdw_ctx* ctx, const svdw_mat* a, const svdw_vec* v, svdw_mat* out);
+/* FixedPointChip041::signed_div_scale constants. The chip's source
+ * (zk_fixed_point_chip, git HEAD) is not available offline, so its layout is
+ * PARITY UNPINNED; the engine emits the parameterised construction
+ *   add(x, 2^S) ; RangeChip::div_mod(t, 2^P, NB) ; sub(q, 2^(S-P))
+ * (div_mod = [r, 2^P, q, t] + check_big_less_than_safe(q, 2^NB/2^P + 1)
+ *  + check_big_less_than_safe(r, 2^P)), i.e. floor(x / 2^P) for |x| < 2^S.
+ * Zero fields (or a null pointer) select S = 3P (the domain rescale_matrix's
+ * doc states, src/matrix/mod.rs:350-353) and NB = S + 1. */
+typedef struct {
+    uint32_t shift_bits;
+    uint32_t num_bits;
+} svdw_div_scale;
+/* ZkMatrix::rescale_matrix (src/matrix/mod.rs:354-375): signed_div_scale of
+ * every c_s entry, row-major, into c_s's phase; out = the quotient cells. */
+int svdw_rescale_matrix(svdw_ctx* ctx, const svdw_mat* c_s, const svdw_div_scale* cfg,
+                        svdw_mat* out);
+/* ZkVector::inner_product (src/matrix/mod.rs:79-106): gate.inner_product(x, self)
+ * then signed_div_scale; out = 1-element vector. */
+int svdw_zkvector_inner_product(svdw_ctx* ctx, uint32_t phase, const svdw_vec* self,
+                                const svdw_vec* x, const svdw_div_scale* cfg, svdw_vec* out);
+/* ZkVector::mul (src/matrix/mod.rs:169-182): inner_product with every row of a. */
+int svdw_zkvector_mul(svdw_ctx* ctx, uint32_t phase, const svdw_vec* self, const svdw_mat* a,
+                      const svdw_div_scale* cfg, svdw_vec* out);
 /* honest_prover_mat_mul (src/matrix/mod.rs:546-568): c_s = a*b over Fr, loaded row-major. */
 int svdw_honest_prover_mat_mul(svdw_ctx* ctx, uint32_t phase, const svdw_mat* a,
                                const svdw_mat* b, svdw_mat* c_s);

@@ -364,6 +364,65 @@ def verify_mul(ctx, a, b, c_s, init_rand: AV) -> None:
 
 
 # ---------------------------------------------------------------------------
+# FixedPointChip041::signed_div_scale [ext, PARITY UNPINNED] and its callers
+# ---------------------------------------------------------------------------
+def div_scale_defaults(p: int, shift_bits: int = 0, num_bits: int = 0):
+    """Default constants: the input domain |x| < 2^(3P) that rescale_matrix's
+    doc comment states (src/matrix/mod.rs:350-353): shift 2^(3P), div_mod on
+    3P+1 bits."""
+    s = shift_bits or 3 * p
+    nb = num_bits or s + 1
+    assert p <= s < 254 and s < nb <= 253 and nb - p <= 200
+    return s, nb
+
+
+def range_div_mod(ctx, rc: RangeChip, a: AV, b: int, a_num_bits: int):
+    """RangeChip::div_mod [ext halo2-base 0.4.1, recalled]: [r, C(b), q, a]
+    (gate r + b*q = a), then check_big_less_than_safe(q, 2^nb / b + 1) and
+    check_big_less_than_safe(r, b)."""
+    q, r = divmod(a.value, b)
+    base = assign_region(ctx, [W(r), C(b), W(q), E(a)], [0])
+    rem, div = ctx.get(base), ctx.get(base + 2)
+    rc.check_big_less_than_safe(ctx, div, (1 << a_num_bits) // b + 1)
+    rc.check_big_less_than_safe(ctx, rem, b)
+    return div, rem
+
+
+def signed_div_scale(ctx, rc: RangeChip, a: AV, p: int, shift_bits: int = 0, num_bits: int = 0):
+    """FixedPointChip041::signed_div_scale (called at src/matrix/mod.rs:104,369;
+    src/matrix/test_matrix.rs:259). The chip's source (zk_fixed_point_chip git
+    HEAD) is not available offline, so this is a parameterised restatement of
+    the usual shift / div_mod / unshift construction: t = a + 2^S (add),
+    (q, r) = div_mod(t, 2^P, nb), y = q - 2^(S-P) (sub). For |x| < 2^S the
+    result is floor(x / 2^P) in signed encoding. Returns (y, r)."""
+    s, nb = div_scale_defaults(p, shift_bits, num_bits)
+    t = gate_add(ctx, E(a), C(1 << s))
+    q, r = range_div_mod(ctx, rc, t, 1 << p, nb)
+    y = gate_sub(ctx, E(q), C(1 << (s - p)))
+    return y, r
+
+
+def rescale_matrix(ctx, rc, c_s, p: int, shift_bits: int = 0, num_bits: int = 0):
+    """ZkMatrix::rescale_matrix (src/matrix/mod.rs:354-375): row-major
+    signed_div_scale of every entry; returns the quotient matrix."""
+    return [[signed_div_scale(ctx, rc, x, p, shift_bits, num_bits)[0] for x in row] for row in c_s]
+
+
+def zkvector_inner_product(ctx, rc, vec, x, p: int, shift_bits: int = 0, num_bits: int = 0) -> AV:
+    """ZkVector::inner_product (src/matrix/mod.rs:79-106): gate.inner_product(x,
+    self) then signed_div_scale."""
+    assert len(vec) == len(x) and len(x) >= 1
+    res_s = gate_inner_product(ctx, [E(a) for a in x], [E(b) for b in vec])
+    return signed_div_scale(ctx, rc, res_s, p, shift_bits, num_bits)[0]
+
+
+def zkvector_mul(ctx, rc, vec, a, p: int, shift_bits: int = 0, num_bits: int = 0) -> List[AV]:
+    """ZkVector::mul (src/matrix/mod.rs:169-182): inner_product with each row of a."""
+    assert len(a[0]) == len(vec)
+    return [zkvector_inner_product(ctx, rc, vec, row, p, shift_bits, num_bits) for row in a]
+
+
+# ---------------------------------------------------------------------------
 # src/svd/mod.rs
 # ---------------------------------------------------------------------------
 def err_calc(p: int, size: int, max_norm: float, eps_svd: float, eps_u: float):

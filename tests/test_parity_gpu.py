@@ -285,3 +285,47 @@ def test_address_sweep_stages_parity(gpu_ctx_factory, grid):
     hs.svd_witness(ctx, m, u, v, d, g)
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
     _assert_streams(ctx, a0, l0, a1)
+
+
+def _ints(cells):
+    return [int(r[0]) | int(r[1]) << 64 | int(r[2]) << 128 | int(r[3]) << 192 for r in cells]
+
+
+@pytest.mark.parametrize("P,LB,S,NB", [(32, 12, 0, 0), (32, 19, 0, 0), (63, 19, 0, 0),
+                                      (42, 16, 100, 110), (40, 19, 120, 0)])
+def test_rescale_and_inner_product_parity(gpu_ctx_factory, P, LB, S, NB):
+    """rescale_matrix / ZkVector::inner_product / ZkVector::mul through the ABI vs
+    the oracle's parameterised signed_div_scale (chip layout parity unpinned:
+    both sides follow include/svdw.h's svdw_div_scale construction); advice and
+    lookup streams must match cell for cell, the oracle's constraint checker
+    must pass, and the quotients must be floor(c / 2^P)."""
+    import halo2_svd041_amd as hs
+    import pyoracle as po
+    rs = np.random.RandomState(P + LB)
+    A = rs.uniform(-9, 9, (6, 11))
+    B = rs.uniform(-9, 9, (11, 7))
+    x = rs.uniform(-50, 50, 11)
+    ctx = gpu_ctx_factory(P, LB)
+    za, zb, zx = hs.ZkMatrix.new(ctx, A), hs.ZkMatrix.new(ctx, B), hs.ZkVector.new(ctx, x)
+    cs = hs.honest_prover_mat_mul(ctx, za, zb)
+    c = hs.ZkMatrix.rescale_matrix(ctx, cs, S, NB)
+    ip = zx.inner_product(zx, 0, S, NB)
+    y = zx.mul(za, 0, S, NB)
+    o = po.Context(phase=0)
+    rc = po.RangeChip(LB)
+    oa, ob = po.zkmatrix_new(o, P, A.tolist()), po.zkmatrix_new(o, P, B.tolist())
+    ox = po.zkvector_new(o, P, x.tolist())
+    ocs = po.honest_prover_mat_mul(o, oa, ob)
+    oc = po.rescale_matrix(o, rc, ocs, P, S, NB)
+    oip = po.zkvector_inner_product(o, rc, ox, ox, P, S, NB)
+    oy = po.zkvector_mul(o, rc, ox, oa, P, S, NB)
+    assert po.check_constraints(o, LB) == []
+    assert _ints(ctx.advice(0)) == o.advice
+    assert _ints(ctx.lookups(0)) == o.lookups
+    got = np.array(_ints(c.values().reshape(-1, 4))).reshape(6, 7)
+    assert [[int(v) for v in r] for r in got] == [[e.value for e in r] for r in oc]
+    for i in range(6):
+        for j in range(7):
+            assert po.to_signed(oc[i][j].value) == po.to_signed(ocs[i][j].value) >> P
+    assert _ints(ip.values()) == [oip.value]
+    assert _ints(y.values()) == [e.value for e in oy]
