@@ -330,9 +330,8 @@ struct svdw_ctx {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
-    uint32_t stage_flags = 0;               // STAGE_* (svdw_set_option "nt_stores", "stage_ilp")
+    uint32_t stage_flags = STAGE_ALIGN;     // STAGE_* (svdw_set_option "nt_stores", "stage_ilp", ...)
     uint32_t stage_sweep = 0;               // "stage_sweep": persistent grid of the sweep mode (0 off)
-    uint32_t stage_asweep = 0;              // "stage_asweep": grid of the aligned-chunk sweep (0 off)
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
     int scan_impl = 4;                      // svdw_set_option "scan_impl"
     int prelaunch_at = 0;                   // "prelaunch_at": GEMMs queued before stage 0/1/2
@@ -588,11 +587,6 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     if (c->stage_sweep && c->stage_elems == kStageElems && a.E == kStageElems &&
         (uint64_t)nelem >= 4ull * kStageElems * c->stage_sweep / kSweepG)
         a.flags |= STAGE_SWEEP;
-    if (c->stage_asweep && (uint64_t)(ee - eb) >= 64ull * kStageElems &&
-        stage_lds_bytes(a.nv ? a.nv : 1, kStageElems) <= 65536) {
-        a.flags |= STAGE_ASWEEP;
-        a.sweep_nb = c->stage_asweep;
-    }
     // 32-bit magics for fastdiv (divisor 1 is handled in the kernel)
     auto magic = [](uint64_t d) -> uint32_t { return d > 1 ? (uint32_t)(((1ull << 32) + d - 1) / d) : 0; };
     a.cdiv_magic = magic(a.C);
@@ -1553,7 +1547,7 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
         c->device = p->device;
         c->dry = p->device < 0;
         if (const char* nt = getenv("SVDW_NT_STORES"))
-            c->stage_flags = (nt[0] == '1') ? STAGE_NT_STORES : 0;
+            c->stage_flags = (c->stage_flags & ~STAGE_NT_STORES) | (nt[0] == '1' ? STAGE_NT_STORES : 0);
         if (const char* g = getenv("SVDW_GEMM"))
             c->gemm_impl = (!strcmp(g, "valu") || !strcmp(g, "dot4")) ? SVDW_GEMM_VALU : SVDW_GEMM_MFMA;
         if (!c->dry) {
@@ -1890,14 +1884,17 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             REQUIRE(value >= 16 && value <= 256 && value % 16 == 0,
                     "stage_elems: a multiple of 16 in [16, 256]");
             c->stage_elems = (uint32_t)value;
-        } else if (n == "stage_asweep") {
-            REQUIRE(value >= 0 && value <= 4096, "stage_asweep: 0 (off) or a grid size <= 4096");
-            c->stage_asweep = (uint32_t)value;
         } else if (n == "stage_divide") {
             c->stage_flags = (c->stage_flags & ~STAGE_DIVIDE) | (value ? STAGE_DIVIDE : 0);
         } else if (n == "stage_sweep") {
             REQUIRE(value >= 0 && value <= 4096, "stage_sweep: 0 (off) or a grid size <= 4096");
             c->stage_sweep = (uint32_t)value;
+        } else if (n == "stage_align") {
+            c->stage_flags = (c->stage_flags & ~STAGE_ALIGN) | (value ? STAGE_ALIGN : 0);
+        } else if (n == "stage_probe") {             // timing probe, wrong cells (tools/ab.py)
+            REQUIRE(value >= 0 && value <= 2, "stage_probe: 0 off, 1 skip phase A, 2 constant stores");
+            c->stage_flags = (c->stage_flags & ~(STAGE_PROBE_NOA | STAGE_PROBE_CONST)) |
+                             (value == 1 ? STAGE_PROBE_NOA : value == 2 ? STAGE_PROBE_CONST : 0);
         } else if (n == "stage_ilp") {
             REQUIRE(value == 1 || value == 2 || value == 4, "stage_ilp: 1, 2 or 4");
             c->stage_flags = (c->stage_flags & ~(STAGE_ILP2 | STAGE_ILP4)) |

@@ -254,17 +254,25 @@ __device__ __forceinline__ void stream_cells(uint4* __restrict__ out, uint32_t t
 // Default path: one half-cell per lane per iteration, the (element, slot) of
 // the lane's next cell tracked incrementally (the cell index advances by
 // blockDim/2 each step) instead of a mul_hi division per half-cell.
-template <bool NT>
+// ALIGN: the block's iterations cover whole (blockDim * 16 B)-aligned address
+// windows (the first one partially), so every wave store is one aligned 1 KiB.
+template <bool NT, bool ALIGN>
 __device__ __forceinline__ void stream_cells_inc(uint4* __restrict__ out, uint32_t total,
                                                  const SlotOp* __restrict__ ops, uint32_t C,
                                                  uint32_t magic, const uint32_t* sK,
                                                  const uint32_t* sV, uint32_t nv) {
     const uint32_t h = threadIdx.x & 1, step = blockDim.x >> 1;
     const uint32_t dq = step / C, dr = step - dq * C, ev = nv * VW;
-    uint32_t c = threadIdx.x >> 1;
+    uint32_t hc0 = threadIdx.x;
+    if (ALIGN) {
+        // misalignment of the region start in half-cells (even: cells are 32 B aligned)
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) >> 4) & (blockDim.x - 1);
+        hc0 = threadIdx.x >= mis ? threadIdx.x - mis : threadIdx.x + blockDim.x - mis;
+    }
+    uint32_t c = hc0 >> 1;
     uint32_t el = fastdiv(c, C, magic), slot = c - el * C;
     uint32_t vbase = el * ev;                             // LDS word offset of this element
-    for (uint32_t hc = threadIdx.x; hc < total; hc += blockDim.x) {
+    for (uint32_t hc = hc0; hc < total; hc += blockDim.x) {
         const SlotOp op = ops[slot];
         const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + vbase + op.src * VW;
         const uint4 v = extract_half(src, op.lo, op.nbits, h);
@@ -468,7 +476,7 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     }
     // ---- phase A: per-element micro-ops (constants / ops / views read from LDS:
     // dynamic indexing into the by-value kernel argument would go to scratch)
-    if (tid < ne)
+    if (tid < ne && !(a.flags & (STAGE_PROBE_NOA | STAGE_PROBE_CONST)))
         element_program(a, e, sV + tid * nv * VW, sK, sMo, sVw, pf0, in0, pf1, in1);
     __syncthreads();
 
@@ -489,126 +497,30 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
         stream_cells<NT, U>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);             \
         if (a.L) stream_cells<NT, U>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);     \
     } while (0)
-    if (a.flags & STAGE_NT_STORES) SVDW_STREAM(true, 1);
+    if (a.flags & STAGE_PROBE_CONST) {
+        const uint4 z = make_uint4(pf0.w[0] ^ pf1.w[0], 0, 0, 0);
+        for (uint32_t hc = tid; hc < 2 * ne * a.C; hc += blockDim.x) outA[hc] = z;
+        if (a.L)
+            for (uint32_t hc = tid; hc < 2 * ne * a.L; hc += blockDim.x) outL[hc] = z;
+    } else if (a.flags & STAGE_NT_STORES) SVDW_STREAM(true, 1);
     else if (a.flags & STAGE_ILP4) SVDW_STREAM(false, 4);
     else if (a.flags & STAGE_ILP2) SVDW_STREAM(false, 2);
     else if (a.flags & STAGE_DIVIDE) SVDW_STREAM(false, 1);
-    else {
-        stream_cells_inc<false>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
-        if (a.L) stream_cells_inc<false>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
+    else if (a.flags & STAGE_ALIGN) {
+        stream_cells_inc<false, true>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
+        if (a.L) stream_cells_inc<false, true>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
+    } else {
+        stream_cells_inc<false, false>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
+        if (a.L) stream_cells_inc<false, false>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
     }
 #undef SVDW_STREAM
     break;
   }
 }
 
-// Address-sweep variant (STAGE_ASWEEP): persistent grid; every block writes
-// whole 4 KiB-aligned chunks of the stream (128 cells) -- chunk q goes to block
-// q % grid -- so at any moment the chip writes a narrow window of aligned
-// chunks (the store pattern that reaches ~6.4 TB/s, tools/storepat3.hip).
-// A batch = K chunks of this block; its elements (those whose cells touch
-// the chunks; boundary elements are also computed by the neighbouring
-// block) get phase A, then the chunks are written 16 B per lane.
-__global__ __launch_bounds__(256) void k_stage_as(const StageArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const uint32_t nv = a.nv;
-    uint32_t* sK = smem;
-    uint32_t* sV = sK + kMaxK * VW;
-    SlotOp* sAdv = reinterpret_cast<SlotOp*>(sV + kStageElems * nv * VW);
-    SlotOp* sLk = sAdv + kMaxAdv;
-    MicroOp* sMo = reinterpret_cast<MicroOp*>(sLk + kMaxLk);
-    DView* sVw = reinterpret_cast<DView*>(sMo + kMaxMicro);
-    __shared__ uint32_t sOff[65], sElo[64];
-    const uint32_t tid = threadIdx.x, NB = gridDim.x;
-    for (uint32_t q = tid; q < a.nk; q += blockDim.x) lds_put(sK + q * VW, a.K[q]);
-    for (uint32_t q = tid; q < a.C; q += blockDim.x) sAdv[q] = a.adv[q];
-    for (uint32_t q = tid; q < a.L; q += blockDim.x) sLk[q] = a.lk[q];
-    for (uint32_t q = tid; q < a.nmo; q += blockDim.x) sMo[q] = a.mo[q];
-    if (tid < kMaxViews) sVw[tid] = a.view[tid];
-    __syncthreads();
-    const Fr zero = fr_zero();
-    for (int pass = 0; pass < 2; ++pass) {
-        const uint32_t Cp = pass ? a.L : a.C;
-        if (!Cp) continue;
-        const SlotOp* ops = pass ? sLk : sAdv;
-        const uint32_t magic = pass ? a.ldiv_magic : a.cdiv_magic;
-        Fr* outp = pass ? a.out_lk : a.out_adv;            // cell 0 of element 0
-        const uint64_t abs0 = (uint64_t)(uintptr_t)outp >> 5;   // absolute cell index
-        const uint64_t F = abs0 + (uint64_t)a.e_begin * Cp, Lc = abs0 + (uint64_t)a.e_end * Cp;
-        const uint64_t q0 = F >> 7, q1 = (Lc + 127) >> 7;
-        const uint32_t per = (128 + Cp - 1) / Cp + 1;      // elements touching one chunk
-        const uint32_t K = min(64u, kStageElems / per);
-        for (uint64_t j = 0;; ++j) {
-            const uint64_t qb = q0 + blockIdx.x + (uint64_t)NB * K * j;
-            if (qb >= q1) break;                          // uniform
-            if (tid < K) {                                // element range of each chunk
-                const uint64_t q = qb + (uint64_t)NB * tid;
-                uint32_t n = 0, elo = 0;
-                if (q < q1) {
-                    const uint64_t c0 = max(q << 7, F), c1 = min((q + 1) << 7, Lc);   // [c0, c1)
-                    elo = (uint32_t)((c0 - abs0) / Cp);
-                    const uint32_t ehi = (uint32_t)((c1 - 1 - abs0) / Cp);
-                    n = ehi - elo + 1;
-                }
-                sElo[tid] = elo;
-                sOff[tid + 1] = n;
-            }
-            __syncthreads();
-            if (tid == 0) {
-                sOff[0] = 0;
-                for (uint32_t q = 1; q <= K; ++q) sOff[q] += sOff[q - 1];
-            }
-            __syncthreads();
-            // phase A: local element t -> (chunk k, element)
-            if (tid < sOff[K]) {
-                uint32_t kk = 0;
-                while (sOff[kk + 1] <= tid) ++kk;
-                const uint32_t e = sElo[kk] + (tid - sOff[kk]);
-                element_program(a, e, sV + tid * nv * VW, sK, sMo, sVw, zero, false, zero, false);
-            }
-            __syncthreads();
-            // phase B: chunk by chunk, 256 half-cells each; four chunks in
-            // flight per thread (one block per CU has few waves to hide latency)
-            constexpr int U = 4;
-            for (uint32_t k0 = 0; k0 < K; k0 += U) {
-                uint4 val[U];
-                uint64_t dst[U];
-                bool ok[U];
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t kk = k0 + u;
-                    const uint64_t q = qb + (uint64_t)NB * kk;
-                    const uint64_t A = (q << 7) + (tid >> 1);   // absolute cell
-                    ok[u] = kk < K && q < q1 && A >= F && A < Lc;
-                    const uint32_t rel = ok[u] ? (uint32_t)(A - abs0) : 0u, h = tid & 1;
-                    const uint32_t e = fastdiv(rel, Cp, magic), slot = rel - e * Cp;
-                    const SlotOp op = ops[slot];
-                    const uint32_t kc = ok[u] ? kk : 0u;
-                    const uint32_t local = ok[u] ? sOff[kc] + (e - sElo[kc]) : 0u;
-                    const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW
-                                                         : sV + (local * nv + op.src) * VW;
-                    val[u] = extract_half(src, op.lo, op.nbits, h);
-                    dst[u] = (uint64_t)rel * 2 + h;
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (ok[u]) reinterpret_cast<uint4*>(outp)[dst[u]] = val[u];
-            }
-            __syncthreads();
-        }
-    }
-}
-
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     if (a.e_end <= a.e_begin) return hipSuccess;
     const uint32_t n = a.e_end - a.e_begin;
-    if (a.flags & STAGE_ASWEEP) {
-        const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1, kStageElems);
-        // rel = cell index from element 0 must fit the 32-bit fastdiv
-        if ((uint64_t)a.e_end * (a.C > a.L ? a.C : a.L) >= (1ull << 31)) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_stage_as, dim3(a.sweep_nb ? a.sweep_nb : 256), dim3(256), lds, st, a);
-        return hipGetLastError();
-    }
     const uint32_t E = a.E ? a.E : kStageElems;
     if (E > kStageElems || ((a.flags & STAGE_SWEEP) && E != kStageElems)) return hipErrorInvalidValue;
     const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1, E);

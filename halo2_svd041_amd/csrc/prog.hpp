@@ -66,7 +66,10 @@ static constexpr uint32_t STAGE_ILP4 = 4;
 // neighbouring groups, a narrow front across the cell stream.
 static constexpr uint32_t STAGE_SWEEP = 8;
 static constexpr uint32_t STAGE_DIVIDE = 16;      // per-half-cell division (A/B reference)
-static constexpr uint32_t STAGE_ASWEEP = 32;      // persistent grid over 4 KiB-aligned chunks
+// Timing probes (wrong cells; tools/ab.py only): skip phase A / store a constant
+static constexpr uint32_t STAGE_PROBE_NOA = 64;
+static constexpr uint32_t STAGE_PROBE_CONST = 128;
+static constexpr uint32_t STAGE_ALIGN = 256;     // 4 KiB-aligned block store windows
 static constexpr uint32_t kSweepG = 4;
 
 static constexpr int kMaxViews = 2;

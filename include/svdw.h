@@ -206,11 +206,15 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   "stage_elems" 256 (elements per stage block, multiple of 16 in [16, 256]);
  *   "stage_ilp" 1 | 2 | 4 (half-cells in flight per thread); "nt_stores" 0 | 1
  *   (non-temporal cell stores); "stage_sweep" 0 | grid (persistent blocks over
- *   interleaved element groups; needs stage_elems 256);
+ *   interleaved element groups; needs stage_elems 256); "stage_align" 1 | 0
+ *   (each block's store windows aligned to 4 KiB); "stage_divide" 0 | 1
+ *   (per-half-cell division instead of incremental slot tracking);
  *   "scan_impl" 4 | 1 | 2 | 3 | 5 (row-scan kernel: 1 shuffle scan, 2 four
  *   terms/thread direct stores, 3 DPP scan, 4 / 5 DPP scan with two / four
  *   terms per thread, unreduced partial sums and small-operand products where
- *   bounds are known). */
+ *   bounds are known).
+ * Timing probe (NOT bit-identical, for A/B measurements only): "stage_probe"
+ *   0 | 1 (skip the stage programs) | 2 (store a constant instead of cells). */
 int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);
 
 /* ----------------------------------------------------------- profiling */

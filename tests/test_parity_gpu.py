@@ -167,7 +167,7 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                                   {"gemm_rt": 0}, {"prelaunch_at": 2}, {"gemm_crt": 0},
                                   {"stage_sweep": 1}, {"stage_sweep": 3}, {"stage_elems": 64},
                                   {"stage_elems": 192}, {"phase1_overlap": 0}, {"phase1_overlap": 2},
-                                  {"stage_divide": 1},
+                                  {"stage_divide": 1}, {"stage_align": 1}, {"stage_align": 1, "stage_elems": 64},
                                   {"overlap": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
@@ -270,21 +270,6 @@ def test_row_sharded_matches_unsharded_256(gpu_ctx_factory):
     assert np.array_equal(got[(0, 0)], full.advice(0))
     assert np.array_equal(got[(1, 0)], full.advice(1))
     assert np.array_equal(got[(0, 1)], full.lookups(0))
-
-
-@pytest.mark.parametrize("grid", [1, 7, 256])
-def test_address_sweep_stages_parity(gpu_ctx_factory, grid):
-    """Aligned-chunk sweep stage kernel (stage_asweep): stages of >= 16384 elements
-    take it; chunk edges cut elements, which both neighbouring blocks compute."""
-    import halo2_svd041_amd as hs
-    N, M, P = 150, 131, 63
-    m, u, d, v = gen_svd_input(N, M, seed=grid)
-    g = gamma_for(grid)
-    ctx = gpu_ctx_factory(P)
-    ctx.set_option("stage_asweep", grid)
-    hs.svd_witness(ctx, m, u, v, d, g)
-    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
-    _assert_streams(ctx, a0, l0, a1)
 
 
 def _ints(cells):
