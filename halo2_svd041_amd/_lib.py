@@ -9,7 +9,8 @@ import ctypes as ct
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsvdw.so")
+# SVDW_LIB: load another build of the library (tools/ab_lib.sh A/B runs of two builds)
+LIB_PATH = os.environ.get("SVDW_LIB") or os.path.join(HERE, "libsvdw.so")
 
 SVDW_OK = 0
 ERRORS = {-1: "SVDW_EINVAL", -2: "SVDW_ERANGE", -3: "SVDW_EDEVICE", -4: "SVDW_ENOMEM"}

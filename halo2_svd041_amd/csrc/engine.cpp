@@ -566,6 +566,12 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
             ee = (uint32_t)(r1 * cw);
         }
     }
+    if (getenv("SVDW_STAGE_LOG")) {
+        uint32_t nmul = 0;
+        for (uint32_t i = 0; i < a.nmo; ++i) nmul += a.mo[i].op == MO_MUL;
+        fprintf(stderr, "stage %-28s elems %8u C %3u L %3u nv %2u nmo %2u muls %u nk %u\n", tag, ee - eb,
+                a.C, a.L, a.nv, a.nmo, nmul, a.nk);
+    }
     if (c->dry || ee <= eb) return;
     a.out_adv = cellp(c, phase, off);
     a.out_lk = a.L ? c->ph[phase].lk + loff : nullptr;
@@ -582,7 +588,7 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     a.E = heavy ? kStageElems : c->stage_elems;
     // keep the block's LDS (element values) within 64 KiB: fewer elements per
     // block for stages with many values (signed_div_scale)
-    while (a.E > 64 && stage_lds_bytes(a.nv ? a.nv : 1, a.E) > 65536) a.E -= 64;
+    while (a.E > 64 && stage_lds_bytes(a.nv ? a.nv : 1, a.E, a.C + a.L) > 65536) a.E -= 64;
     // interleaved groups only pay off on big stages (and need whole batches of work)
     if (c->stage_sweep && c->stage_elems == kStageElems && a.E == kStageElems &&
         (uint64_t)nelem >= 4ull * kStageElems * c->stage_sweep / kSweepG)
@@ -1889,6 +1895,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "stage_sweep") {
             REQUIRE(value >= 0 && value <= 4096, "stage_sweep: 0 (off) or a grid size <= 4096");
             c->stage_sweep = (uint32_t)value;
+        } else if (n == "stage_inc") {             // previous phase B (per-half-cell decode)
+            c->stage_flags = (c->stage_flags & ~STAGE_INC) | (value ? STAGE_INC : 0);
         } else if (n == "stage_align") {
             c->stage_flags = (c->stage_flags & ~STAGE_ALIGN) | (value ? STAGE_ALIGN : 0);
         } else if (n == "stage_probe") {             // timing probe, wrong cells (tools/ab.py)
@@ -1911,6 +1919,40 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                       "hipStreamCreateWithPriority");
                 hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
                 c->st2 = s;
+            }
+        } else if (n == "cu_split") {
+            // Give the second stream (products, phase 1) `value` CUs of its own and
+            // the cell stream the rest (0: both streams on every CU). Masks pick
+            // groups of 8 consecutive mask bits, so the split is even over the
+            // XCDs whether the mask order is XCD-major or XCD-interleaved.
+            REQUIRE(value >= 0 && value % 8 == 0, "cu_split: a multiple of 8, >= 0");
+            if (!c->dry) {
+                hipDeviceProp_t prop;
+                hipck(hipGetDeviceProperties(&prop, c->device), "hipGetDeviceProperties");
+                const uint32_t ncu = (uint32_t)prop.multiProcessorCount;
+                REQUIRE(value < ncu && ncu % 8 == 0, "cu_split: fewer CUs than the device has");
+                hipStream_t s1 = nullptr, s2 = nullptr;
+                if (value) {
+                    const uint32_t groups = ncu / 8, g2 = (uint32_t)value / 8;
+                    std::vector<uint32_t> m1((ncu + 31) / 32, 0), m2((ncu + 31) / 32, 0);
+                    for (uint32_t g = 0; g < groups; ++g) {
+                        // g2 of the groups, spread evenly (Bresenham) over the mask
+                        const bool two = (g + 1) * g2 / groups != g * g2 / groups;
+                        for (uint32_t b = 8 * g; b < 8 * g + 8; ++b)
+                            (two ? m2 : m1)[b / 32] |= 1u << (b % 32);
+                    }
+                    hipck(hipExtStreamCreateWithCUMask(&s1, (uint32_t)m1.size(), m1.data()),
+                          "hipExtStreamCreateWithCUMask");
+                    hipck(hipExtStreamCreateWithCUMask(&s2, (uint32_t)m2.size(), m2.data()),
+                          "hipExtStreamCreateWithCUMask");
+                } else {
+                    hipck(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking), "hipStreamCreate");
+                    hipck(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking), "hipStreamCreate");
+                }
+                hipck(hipStreamDestroy(c->st), "hipStreamDestroy");
+                hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
+                c->st = s1;
+                c->st2 = s2;
             }
         } else if (n == "phase1_overlap") {
             REQUIRE(value >= 0 && value <= 2, "phase1_overlap: 0, 1 or 2");

@@ -68,34 +68,49 @@ SVDW_HD bool fr_eq(const Fr& a, const Fr& b) {
     return x == 0;
 }
 
+// Carry chains: __builtin_addc / __builtin_subc lower to v_add_co_u32 /
+// v_addc_co_u32 (v_sub_co / v_subb_co) on gfx950, one instruction per word.
+// The 64-bit "c += a + b; c >>= 32" idiom instead compiles to v_lshl_add_u64
+// plus a v_mov per word to zero the high half (3-4x the instructions).
+SVDW_HD uint32_t addc32(uint32_t a, uint32_t b, uint32_t& c) {
+    unsigned co;
+    const uint32_t r = __builtin_addc(a, b, c, &co);
+    c = co;
+    return r;
+}
+SVDW_HD uint32_t subb32(uint32_t a, uint32_t b, uint32_t& br) {
+    unsigned bo;
+    const uint32_t r = __builtin_subc(a, b, br, &bo);
+    br = bo;
+    return r;
+}
 // r = a - b over 256 bits; returns borrow.
 SVDW_HD uint32_t sub256(Fr& r, const Fr& a, const Fr& b) {
-    uint64_t br = 0;
+    uint32_t br = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint64_t t = (uint64_t)a.w[i] - b.w[i] - br;
-        r.w[i] = (uint32_t)t;
-        br = (t >> 63) & 1;
-    }
-    return (uint32_t)br;
+    for (int i = 0; i < 8; ++i) r.w[i] = subb32(a.w[i], b.w[i], br);
+    return br;
 }
 // r = a + b over 256 bits; returns carry.
 SVDW_HD uint32_t add256(Fr& r, const Fr& a, const Fr& b) {
-    uint64_t c = 0;
+    uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        c += (uint64_t)a.w[i] + b.w[i];
-        r.w[i] = (uint32_t)c;
-        c >>= 32;
-    }
-    return (uint32_t)c;
+    for (int i = 0; i < 8; ++i) r.w[i] = addc32(a.w[i], b.w[i], c);
+    return c;
+}
+// r = a - p over 256 bits; returns borrow.
+SVDW_HD uint32_t sub_p(Fr& r, const Fr& a) {
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.w[i] = subb32(a.w[i], p_word(i), br);
+    return br;
 }
 
 // Canonical modular add/sub (inputs canonical, output canonical).
 SVDW_HD Fr fr_add(const Fr& a, const Fr& b) {
     Fr s, t;
     uint32_t c = add256(s, a, b);
-    uint32_t br = sub256(t, s, fr_p());
+    uint32_t br = sub_p(t, s);
     // keep t if (carry) or (no borrow): s >= p
     bool use_t = c | (br ^ 1u);
     Fr r;
@@ -106,7 +121,9 @@ SVDW_HD Fr fr_add(const Fr& a, const Fr& b) {
 SVDW_HD Fr fr_sub(const Fr& a, const Fr& b) {
     Fr d, t;
     uint32_t br = sub256(d, a, b);
-    add256(t, d, fr_p());
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t.w[i] = addc32(d.w[i], p_word(i), c);
     Fr r;
 #pragma unroll
     for (int i = 0; i < 8; ++i) r.w[i] = br ? t.w[i] : d.w[i];
@@ -114,87 +131,54 @@ SVDW_HD Fr fr_sub(const Fr& a, const Fr& b) {
 }
 SVDW_HD Fr fr_neg(const Fr& a) { return fr_sub(fr_zero(), a); }
 
-// Montgomery product a*b*2^-256 mod p (CIOS, 32-bit limbs). Output canonical
-// (< p) for inputs < p.
-SVDW_HD Fr mont_mul(const Fr& a, const Fr& b) {
+// t + a*b + c as (lo, new carry c): one v_mad_u64_u32 (a*b + t < 2^64 - 2^32)
+// and an add-with-carry of c.
+SVDW_HD uint32_t mac32(uint32_t a, uint32_t b, uint32_t t, uint32_t& c) {
+    const uint64_t pr = (uint64_t)a * b + t;
+    uint32_t cy = 0;
+    const uint32_t lo = addc32((uint32_t)pr, c, cy);
+    c = (uint32_t)(pr >> 32) + cy;
+    return lo;
+}
+// NR rounds of CIOS Montgomery multiplication, one per word of `a`:
+// a * b * 2^(-32 NR) mod p for a < 2^(32 NR), b < p. Output canonical.
+template <int NR>
+SVDW_HD Fr mont_mul_rounds(const Fr& a, const Fr& b) {
     uint32_t t[10];
 #pragma unroll
     for (int i = 0; i < 10; ++i) t[i] = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint64_t c = 0;
+    for (int i = 0; i < NR; ++i) {
+        uint32_t c = 0, cy = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            c += (uint64_t)a.w[j] * b.w[i] + t[j];
-            t[j] = (uint32_t)c;
-            c >>= 32;
-        }
-        c += t[8];
-        t[8] = (uint32_t)c;
-        t[9] = (uint32_t)(c >> 32);
-        uint32_t m = t[0] * kPinv32;
-        c = (uint64_t)m * p_word(0) + t[0];
-        c >>= 32;
+        for (int j = 0; j < 8; ++j) t[j] = mac32(b.w[j], a.w[i], t[j], c);
+        t[8] = addc32(t[8], c, cy);
+        t[9] = cy;
+        const uint32_t m = t[0] * kPinv32;
+        c = 0;
+        (void)mac32(m, p_word(0), t[0], c);               // low word cancels
 #pragma unroll
-        for (int j = 1; j < 8; ++j) {
-            c += (uint64_t)m * p_word(j) + t[j];
-            t[j - 1] = (uint32_t)c;
-            c >>= 32;
-        }
-        c += t[8];
-        t[7] = (uint32_t)c;
-        t[8] = t[9] + (uint32_t)(c >> 32);
+        for (int j = 1; j < 8; ++j) t[j - 1] = mac32(m, p_word(j), t[j], c);
+        cy = 0;
+        t[7] = addc32(t[8], c, cy);
+        t[8] = t[9] + cy;
     }
     Fr r, s;
 #pragma unroll
     for (int i = 0; i < 8; ++i) r.w[i] = t[i];
-    uint32_t br = sub256(s, r, fr_p());
-    bool use_s = t[8] | (br ^ 1u);
+    const uint32_t br = sub_p(s, r);
+    const bool use_s = t[8] | (br ^ 1u);
 #pragma unroll
     for (int i = 0; i < 8; ++i) r.w[i] = use_s ? s.w[i] : r.w[i];
     return r;
 }
+// Montgomery product a*b*2^-256 mod p (CIOS, 32-bit limbs). Output canonical
+// (< p) for inputs < p.
+SVDW_HD Fr mont_mul(const Fr& a, const Fr& b) { return mont_mul_rounds<8>(b, a); }
 // a * b * 2^(-32 NA) mod p for a < 2^(32 NA) (words >= NA of `a` ignored):
 // CIOS with NA outer rounds, one per word of the small operand. Output < p.
 template <int NA>
-SVDW_HD Fr mont_mul_small(const Fr& a, const Fr& b) {
-    uint32_t t[10];
-#pragma unroll
-    for (int i = 0; i < 10; ++i) t[i] = 0;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-        uint64_t c = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            c += (uint64_t)b.w[j] * a.w[i] + t[j];
-            t[j] = (uint32_t)c;
-            c >>= 32;
-        }
-        c += t[8];
-        t[8] = (uint32_t)c;
-        t[9] = (uint32_t)(c >> 32);
-        uint32_t m = t[0] * kPinv32;
-        c = (uint64_t)m * p_word(0) + t[0];
-        c >>= 32;
-#pragma unroll
-        for (int j = 1; j < 8; ++j) {
-            c += (uint64_t)m * p_word(j) + t[j];
-            t[j - 1] = (uint32_t)c;
-            c >>= 32;
-        }
-        c += t[8];
-        t[7] = (uint32_t)c;
-        t[8] = t[9] + (uint32_t)(c >> 32);
-    }
-    Fr r, s;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r.w[i] = t[i];
-    uint32_t br = sub256(s, r, fr_p());
-    bool use_s = t[8] | (br ^ 1u);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) r.w[i] = use_s ? s.w[i] : r.w[i];
-    return r;
-}
+SVDW_HD Fr mont_mul_small(const Fr& a, const Fr& b) { return mont_mul_rounds<NA>(a, b); }
 // a * b mod p for a canonical `a` whose signed value (a or a - p) has magnitude
 // < 2^(32 NA), with bs = b * 2^(32 NA) mod p.
 template <int NA>

@@ -141,21 +141,18 @@ __device__ __forceinline__ Fr reduce9(const uint32_t (&x)[9]) {
     const double qd = floor(xd * inv_pd) - 1.0;
     const uint32_t q = qd > 0.0 ? (uint32_t)qd : 0u;
     Fr r;
-    uint64_t carry = 0;
-    uint32_t br = 0;
+    uint32_t carry = 0, br = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const uint64_t pr = (uint64_t)q * p_word(i) + carry;
-        carry = pr >> 32;
-        const uint64_t d = (uint64_t)x[i] - (uint32_t)pr - br;
-        r.w[i] = (uint32_t)d;
-        br = (uint32_t)(d >> 63);
+        const uint64_t pr = (uint64_t)q * p_word(i) + carry;   // v_mad_u64_u32
+        carry = (uint32_t)(pr >> 32);
+        r.w[i] = subb32(x[i], (uint32_t)pr, br);
     }
     // x - q p < 3p < 2^256: the ninth word is gone; two conditional subtractions
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
         Fr t;
-        const uint32_t b = sub256(t, r, fr_p());
+        const uint32_t b = sub_p(t, r);
 #pragma unroll
         for (int i = 0; i < 8; ++i) r.w[i] = b ? r.w[i] : t.w[i];
     }
@@ -290,6 +287,64 @@ __device__ __forceinline__ void stream_cells_inc(uint4* __restrict__ out, uint32
             vbase += ev;
         }
     }
+}
+
+// Default path: per-(slot, half) descriptors and masks prepared once per block
+// (half_desc, prog.hpp), so a half-cell costs one descriptor + one mask LDS
+// read, five word reads, four alignbit and four and (no per-cell decoding,
+// clamping or mask arithmetic). The (element, slot) of the lane's next cell is
+// tracked incrementally as in stream_cells_inc; ALIGN as there.
+template <bool ALIGN>
+__device__ __forceinline__ void stream_cells_desc(uint4* __restrict__ out, uint32_t total,
+                                                  const uint32_t* __restrict__ sHD,
+                                                  const uint4* __restrict__ sHM, uint32_t C,
+                                                  uint32_t magic, const uint32_t* smem,
+                                                  uint32_t vbase0, uint32_t nv) {
+    const uint32_t h = threadIdx.x & 1, step = blockDim.x >> 1;
+    const uint32_t dq = step / C, dr = step - dq * C, ev = nv * VW;
+    uint32_t hc0 = threadIdx.x;
+    if (ALIGN) {
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) >> 4) & (blockDim.x - 1);
+        hc0 = threadIdx.x >= mis ? threadIdx.x - mis : threadIdx.x + blockDim.x - mis;
+    }
+    uint32_t c = hc0 >> 1;
+    uint32_t el = fastdiv(c, C, magic), slot = c - el * C;
+    uint32_t vbase = vbase0 + el * ev;                    // LDS word of this element's values
+    for (uint32_t hc = hc0; hc < total; hc += blockDim.x) {
+        const uint32_t k = 2 * slot + h;
+        const uint32_t d = sHD[k];
+        const uint4 m = sHM[k];
+        const uint32_t* x = smem + ((d & kHalfElem) ? vbase : 0u) + (d & 0xffffu);
+        const uint32_t r = (d >> 16) & 31u;
+        const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4];
+        out[hc] = make_uint4(__builtin_amdgcn_alignbit(x1, x0, r) & m.x,
+                             __builtin_amdgcn_alignbit(x2, x1, r) & m.y,
+                             __builtin_amdgcn_alignbit(x3, x2, r) & m.z,
+                             __builtin_amdgcn_alignbit(x4, x3, r) & m.w);
+        slot += dr;
+        vbase += dq * ev;
+        if (slot >= C) {
+            slot -= C;
+            vbase += ev;
+        }
+    }
+}
+
+// Descriptor and masks of half h of a slot (see half_desc).
+__device__ __forceinline__ void make_half(const SlotOp op, uint32_t h, uint32_t* d, uint4* m) {
+    const uint32_t lo = op.lo;
+    uint32_t nb = op.nbits ? op.nbits : 256u;
+    nb = min(nb, 256u - lo);
+    const bool elem = op.src < KSRC;
+    const uint32_t base = (elem ? op.src : op.src - KSRC) * VW;
+    *d = half_desc(base + (lo >> 5) + 4 * h, lo & 31u, elem);
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int keep = (int)nb - 32 * (4 * (int)h + i);
+        w[i] = keep >= 32 ? 0xffffffffu : (keep <= 0 ? 0u : ((1u << keep) - 1u));
+    }
+    *m = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // Sweep mode: local element l of batch jb of block b is global element
@@ -429,6 +484,13 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     SlotOp* sLk = sAdv + kMaxAdv;
     MicroOp* sMo = reinterpret_cast<MicroOp*>(sLk + kMaxLk);
     DView* sVw = reinterpret_cast<DView*>(sMo + kMaxMicro);
+    // (stage_lds_bytes counts 48 B per view, >= sizeof(DView) + the alignment slack)
+    static_assert(sizeof(DView) <= 40, "DView grew: recheck stage_lds_bytes");
+    // (word offsets from smem, not integer casts: a cast pointer would lose its
+    // LDS address space and every table read would become a flat load)
+    const uint32_t hm_off = ((uint32_t)(reinterpret_cast<uint32_t*>(sVw + kMaxViews) - smem) + 3u) & ~3u;
+    uint4* sHM = reinterpret_cast<uint4*>(smem + hm_off);
+    uint32_t* sHD = reinterpret_cast<uint32_t*>(sHM + 2 * (a.C + a.L));
 
     const uint32_t tid = threadIdx.x;
     const bool sweep = (a.flags & STAGE_SWEEP) != 0;
@@ -460,6 +522,10 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     for (uint32_t k = tid; k < a.L; k += blockDim.x) sLk[k] = a.lk[k];
     for (uint32_t k = tid; k < a.nmo; k += blockDim.x) sMo[k] = a.mo[k];
     if (tid < kMaxViews) sVw[tid] = a.view[tid];
+    for (uint32_t k = tid; k < 2 * (a.C + a.L); k += blockDim.x) {
+        const uint32_t sl = k >> 1;
+        make_half(sl < a.C ? a.adv[sl] : a.lk[sl - a.C], k & 1, sHD + k, sHM + k);
+    }
     __syncthreads();
 
   for (;; ++map.jb) {
@@ -506,12 +572,22 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     else if (a.flags & STAGE_ILP4) SVDW_STREAM(false, 4);
     else if (a.flags & STAGE_ILP2) SVDW_STREAM(false, 2);
     else if (a.flags & STAGE_DIVIDE) SVDW_STREAM(false, 1);
-    else if (a.flags & STAGE_ALIGN) {
+    else if (a.flags & STAGE_INC) {
         stream_cells_inc<false, true>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
         if (a.L) stream_cells_inc<false, true>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
     } else {
-        stream_cells_inc<false, false>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
-        if (a.L) stream_cells_inc<false, false>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
+        const uint32_t vb0 = (uint32_t)(sV - smem);
+        if (a.flags & STAGE_ALIGN) {
+            stream_cells_desc<true>(outA, 2 * ne * a.C, sHD, sHM, a.C, a.cdiv_magic, smem, vb0, nv);
+            if (a.L)
+                stream_cells_desc<true>(outL, 2 * ne * a.L, sHD + 2 * a.C, sHM + 2 * a.C, a.L,
+                                        a.ldiv_magic, smem, vb0, nv);
+        } else {
+            stream_cells_desc<false>(outA, 2 * ne * a.C, sHD, sHM, a.C, a.cdiv_magic, smem, vb0, nv);
+            if (a.L)
+                stream_cells_desc<false>(outL, 2 * ne * a.L, sHD + 2 * a.C, sHM + 2 * a.C, a.L,
+                                         a.ldiv_magic, smem, vb0, nv);
+        }
     }
 #undef SVDW_STREAM
     break;
@@ -523,7 +599,7 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     const uint32_t n = a.e_end - a.e_begin;
     const uint32_t E = a.E ? a.E : kStageElems;
     if (E > kStageElems || ((a.flags & STAGE_SWEEP) && E != kStageElems)) return hipErrorInvalidValue;
-    const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1, E);
+    const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1, E, a.C + a.L);
     uint32_t grid = (n + E - 1) / E;
     if (a.flags & STAGE_SWEEP) {
         // persistent blocks; every block needs at least one group
@@ -1449,24 +1525,16 @@ __device__ __forceinline__ U9 u9_from(const Fr& a) {
 }
 __device__ __forceinline__ U9 u9_add(const U9& a, const U9& b) {
     U9 r;
-    uint64_t c = 0;
+    uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-        c += (uint64_t)a.w[i] + b.w[i];
-        r.w[i] = (uint32_t)c;
-        c >>= 32;
-    }
+    for (int i = 0; i < 9; ++i) r.w[i] = addc32(a.w[i], b.w[i], c);
     return r;
 }
 __device__ __forceinline__ U9 u9_sub(const U9& a, const U9& b) {   // a >= b
     U9 r;
     uint32_t br = 0;
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-        const uint64_t d = (uint64_t)a.w[i] - b.w[i] - br;
-        r.w[i] = (uint32_t)d;
-        br = (uint32_t)(d >> 63);
-    }
+    for (int i = 0; i < 9; ++i) r.w[i] = subb32(a.w[i], b.w[i], br);
     return r;
 }
 template <int CTRL, int ROW_MASK>
@@ -1539,9 +1607,8 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
                 uint32_t br = 0;
 #pragma unroll
                 for (int q = 0; q < NA; ++q) {
-                    const uint64_t t = (uint64_t)p_word(q) - a[i].w[q] - br;
-                    br = (uint32_t)(t >> 63);
-                    mag.w[q] = neg ? (uint32_t)t : a[i].w[q];
+                    const uint32_t t = subb32(p_word(q), a[i].w[q], br);
+                    mag.w[q] = neg ? t : a[i].w[q];
                 }
                 s[i] = j < L ? mont_mul_small<NA>(mag, ld_fr((neg ? wn : wm) + j)) : zero;
             }
@@ -1728,9 +1795,8 @@ __global__ __launch_bounds__(256) void k_matvec_values(const DView A, uint32_t L
             uint32_t br = 0;
 #pragma unroll
             for (int q = 0; q < NA; ++q) {
-                const uint64_t t = (uint64_t)p_word(q) - a.w[q] - br;
-                br = (uint32_t)(t >> 63);
-                mag.w[q] = neg ? (uint32_t)t : a.w[q];
+                const uint32_t t = subb32(p_word(q), a.w[q], br);
+                mag.w[q] = neg ? t : a.w[q];
             }
             s = mont_mul_small<NA>(mag, ld_fr((neg ? wn : wm) + j));
         }

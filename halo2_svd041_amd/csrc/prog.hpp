@@ -70,6 +70,7 @@ static constexpr uint32_t STAGE_DIVIDE = 16;      // per-half-cell division (A/B
 static constexpr uint32_t STAGE_PROBE_NOA = 64;
 static constexpr uint32_t STAGE_PROBE_CONST = 128;
 static constexpr uint32_t STAGE_ALIGN = 256;     // 4 KiB-aligned block store windows
+static constexpr uint32_t STAGE_INC = 512;       // phase B decoding slot ops per half-cell (A/B reference)
 static constexpr uint32_t kSweepG = 4;
 
 static constexpr int kMaxViews = 2;
@@ -100,10 +101,24 @@ struct StageArgs {
 };
 static_assert(sizeof(StageArgs) < 4096, "kernel argument block too large");
 
+// Phase-B half-cell descriptor (one per slot and half, built per block in LDS):
+// output words [4h, 4h+4) of a cell are alignbit(x[i+1], x[i], r) & mask[i]
+// with x = the 5 LDS words from word `off` of the constants (bit 31 clear) or
+// of the element's values (bit 31 set); the masks already clip the window to
+// `nbits` and to the 256 bits of the source, so words read past the source
+// value (up to 12) are masked off.
+static constexpr uint32_t kHalfElem = 0x80000000u;
+constexpr uint32_t half_desc(uint32_t off, uint32_t r, bool elem) {
+    return off | (r << 16) | (elem ? kHalfElem : 0u);
+}
+static constexpr uint32_t kStageLdsPad = 64;   // over-read slack after the last table
+
 // Dynamic LDS of a stage block: constants, E elements' values, slot / micro-op
-// tables and views (constexpr: host and device).
-constexpr uint32_t stage_lds_bytes(uint32_t nv, uint32_t E) {
-    return kMaxK * 32 + E * nv * 32 + (kMaxAdv + kMaxLk) * 4 + kMaxMicro * 8 + kMaxViews * 48;
+// tables, views, and per (slot, half) descriptors (4 B) + masks (16 B) for the
+// C + L slots (constexpr: host and device).
+constexpr uint32_t stage_lds_bytes(uint32_t nv, uint32_t E, uint32_t CL = kMaxAdv + kMaxLk) {
+    return kMaxK * 32 + E * nv * 32 + (kMaxAdv + kMaxLk) * 4 + kMaxMicro * 8 + kMaxViews * 48 +
+           CL * 2 * 20 + kStageLdsPad;
 }
 
 }  // namespace svdw
