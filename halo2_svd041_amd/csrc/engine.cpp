@@ -1914,11 +1914,32 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                 sync(c);
                 int lo = 0, hi = 0;
                 hipck(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+                (void)lo;                                  // 0: the default priority
                 hipStream_t s;
-                hipck(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, value ? hi : lo),
-                      "hipStreamCreateWithPriority");
+                if (value)
+                    hipck(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi),
+                          "hipStreamCreateWithPriority");
+                else
+                    hipck(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
                 hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
                 c->st2 = s;
+            }
+        } else if (n == "stage_priority") {
+            // cell stream priority: 0 normal, 1 high (its blocks dispatch ahead of the
+            // products / phase-1 scans on the second stream)
+            REQUIRE(value == 0 || value == 1, "stage_priority: 0 or 1");
+            if (!c->dry) {
+                int lo = 0, hi = 0;
+                hipck(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+                (void)lo;                                  // 0: the default priority
+                hipStream_t s;
+                if (value)
+                    hipck(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi),
+                          "hipStreamCreateWithPriority");
+                else
+                    hipck(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+                hipck(hipStreamDestroy(c->st), "hipStreamDestroy");
+                c->st = s;
             }
         } else if (n == "cu_split") {
             // Give the second stream (products, phase 1) `value` CUs of its own and

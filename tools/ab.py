@@ -31,7 +31,7 @@ def parse_variant(s):
 DEFAULTS = {"gemm_impl": 0, "nt_stores": 0, "stage_ilp": 1, "scan_impl": 4, "overlap": 1,
             "prelaunch_at": 0, "gemm_priority": 0, "gemm_rt": 1, "gemm_crt": 1, "stage_sweep": 0,
             "stage_elems": 256, "phase1_overlap": 1, "stage_divide": 0,
-            "stage_probe": 0, "stage_align": 1, "cu_split": 0, "stage_inc": 0}
+            "stage_probe": 0, "stage_align": 1, "cu_split": 0, "stage_inc": 0, "stage_priority": 0}
 # pseudo-option "prof": event profiler during the timed steps (0 off, 1 all, 2 k_stage only)
 PROF_PREFIX = {1: "", 2: "k_stage"}
 
@@ -88,7 +88,8 @@ def main():
     cells = sum(hs.plan_svd(N, M, a.p, 19)[k] for k in ("advice0", "advice1"))
     for name, _ in variants:
         med = statistics.median(res[name])
-        print(f"{name:12s} median {med:.4f} ms  min {min(res[name]):.4f}  -> {cells / med / 1e6:.2f} Gcells/s")
+        print(f"{name:12s} median {med:.4f} ms  min {min(res[name]):.4f}  -> {cells / med / 1e6:.2f} Gcells/s"
+              f"  samples {' '.join(f'{x:.3f}' for x in sorted(res[name]))}")
         top = sorted(kern[name].items(), key=lambda kv: -statistics.median(kv[1]))[:8]
         print("   " + "  ".join(f"{k}={statistics.median(vv):.3f}" for k, vv in top))
     print(json.dumps({n: statistics.median(r) for n, r in res.items()}))
