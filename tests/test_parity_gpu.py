@@ -168,7 +168,8 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                                   {"stage_sweep": 1}, {"stage_sweep": 3}, {"stage_elems": 64},
                                   {"stage_elems": 192}, {"phase1_overlap": 0}, {"phase1_overlap": 2},
                                   {"stage_divide": 1}, {"stage_align": 1}, {"stage_align": 1, "stage_elems": 64},
-                                  {"overlap": 0}])
+                                  {"overlap": 0}, {"stage_inc": 1}, {"stage_priority": 1}, {"gemm_priority": 1},
+                                  {"cu_split": 64}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
@@ -276,9 +277,10 @@ def _ints(cells):
     return [int(r[0]) | int(r[1]) << 64 | int(r[2]) << 128 | int(r[3]) << 192 for r in cells]
 
 
-@pytest.mark.parametrize("P,LB,S,NB", [(32, 12, 0, 0), (32, 19, 0, 0), (63, 19, 0, 0),
-                                      (42, 16, 100, 110), (40, 19, 120, 0)])
-def test_rescale_and_inner_product_parity(gpu_ctx_factory, P, LB, S, NB):
+@pytest.mark.parametrize("P,LB,S,NB,elems", [(32, 12, 0, 0, 256), (32, 19, 0, 0, 256), (63, 19, 0, 0, 256),
+                                            (42, 16, 100, 110, 256), (40, 19, 120, 0, 256),
+                                            (32, 12, 0, 0, 64), (63, 19, 0, 0, 128)])
+def test_rescale_and_inner_product_parity(gpu_ctx_factory, P, LB, S, NB, elems):
     """rescale_matrix / ZkVector::inner_product / ZkVector::mul through the ABI vs
     the oracle's parameterised signed_div_scale (chip layout parity unpinned:
     both sides follow include/svdw.h's svdw_div_scale construction); advice and
@@ -291,6 +293,7 @@ def test_rescale_and_inner_product_parity(gpu_ctx_factory, P, LB, S, NB):
     B = rs.uniform(-9, 9, (11, 7))
     x = rs.uniform(-50, 50, 11)
     ctx = gpu_ctx_factory(P, LB)
+    ctx.set_option("stage_elems", elems)
     za, zb, zx = hs.ZkMatrix.new(ctx, A), hs.ZkMatrix.new(ctx, B), hs.ZkVector.new(ctx, x)
     cs = hs.honest_prover_mat_mul(ctx, za, zb)
     c = hs.ZkMatrix.rescale_matrix(ctx, cs, S, NB)
