@@ -337,6 +337,7 @@ struct svdw_ctx {
     int prelaunch_at = 0;                   // "prelaunch_at": GEMMs queued before stage 0/1/2
     int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
+    bool fused_quantize = true;             // "fused_quantize": m, u, v, d in one launch
     int phase1_overlap = 1;                 // "phase1_overlap": 0 off, 1 on st2 behind the
                                             // GEMMs, 2 on st3 from quantization on
     bool prelaunched = false;               // this witness's products were queued on st2
@@ -632,8 +633,11 @@ static svdw_vec put_cell(svdw_ctx* c, uint32_t phase, const Fr& v) {   // load_w
 }
 
 // ----------------------------------------------------- reference functions
+// qs: collect the quantization into one k_quantize_multi launch (device inputs
+// only) instead of launching it here.
 static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, uint32_t rows,
-                             uint32_t cols, bool on_device, unsigned* blockmax = nullptr) {
+                             uint32_t cols, bool on_device, unsigned* blockmax = nullptr,
+                             QuantSegs* qs = nullptr) {
     REQUIRE(rows >= 1 && cols >= 1, "ZkMatrix::new: empty matrix");
     REQUIRE(data || c->dry, "null data");
     uint64_t n = (uint64_t)rows * cols, off;
@@ -646,8 +650,18 @@ static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, ui
                   "H2D");
             src = (const double*)c->f64in.p;
         }
-        ProfScope ps(c, c->st, "k_quantize", 40.0 * n, 0);
-        hipck(launch_quantize(src, n, cellp(c, phase, off), (int)c->P, blockmax, c->st), "k_quantize");
+        if (qs && on_device && qs->nseg < (uint32_t)kMaxQuantSegs) {
+            const uint32_t k = qs->nseg++;
+            qs->in[k] = src;
+            qs->out[k] = cellp(c, phase, off);
+            qs->blockmax[k] = blockmax;
+            qs->n[k] = n;
+            qs->blk0[k + 1] = qs->blk0[k] + (uint32_t)((n + 255) / 256);
+        } else {
+            ProfScope ps(c, c->st, "k_quantize", 40.0 * n, 0);
+            hipck(launch_quantize(src, n, cellp(c, phase, off), (int)c->P, blockmax, c->st),
+                  "k_quantize");
+        }
     }
     if (sharded(c)) {            // every rank quantizes all of it (operands of the products)
         uint64_t r0, r1;
@@ -1484,10 +1498,17 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         ensure_buf(c, c->bits, (64 + nbm + nbu + nbv) * sizeof(unsigned));
         dbits = (unsigned*)c->bits.p;
     }
-    svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device, dbits ? dbits + 64 : nullptr);
-    svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device, dbits ? dbits + 64 + nbm : nullptr);
-    svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device, dbits ? dbits + 64 + nbm + nbu : nullptr);
-    svdw_mat zdm = zkmatrix_new(c, 0, d, r, 1, on_device);
+    QuantSegs qs;
+    memset(&qs, 0, sizeof qs);
+    QuantSegs* qp = c->fused_quantize ? &qs : nullptr;
+    svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device, dbits ? dbits + 64 : nullptr, qp);
+    svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device, dbits ? dbits + 64 + nbm : nullptr, qp);
+    svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device, dbits ? dbits + 64 + nbm + nbu : nullptr, qp);
+    svdw_mat zdm = zkmatrix_new(c, 0, d, r, 1, on_device, nullptr, qp);
+    if (qs.nseg) {
+        ProfScope ps(c, c->st, "k_quantize", 40.0 * ((double)N * M + (double)N * N + (double)M * M + r), 0);
+        hipck(launch_quantize_multi(qs, (int)c->P, c->st), "k_quantize_multi");
+    }
     svdw_vec zd{0, r, zdm.off, 1};
     double es, eu;
     err_calc(c->P, std::max(N, M), cfg.max_norm, cfg.eps_svd, cfg.eps_u, &es, &eu);
@@ -1924,6 +1945,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                 hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
                 c->st2 = s;
             }
+        } else if (n == "fused_quantize") {
+            c->fused_quantize = value != 0;
         } else if (n == "stage_priority") {
             // cell stream priority: 0 normal, 1 high (its blocks dispatch ahead of the
             // products / phase-1 scans on the second stream)

@@ -63,10 +63,10 @@ __device__ __forceinline__ uint32_t signed_bits(const Fr& x) {
 // x_q = round_half_away(|x| * 2^P) as u128 (saturating, NaN -> 0);
 // sign(x) < 0 (incl. -0.0) -> p - x_q.   [zk_fixed_point_chip quantization,
 // SURVEY.md Appendix C.1]
-__global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in, uint64_t n,
-                                                  Fr* __restrict__ out, double scale,
-                                                  unsigned* __restrict__ blockmax) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void quantize_body(const double* __restrict__ in, uint64_t n,
+                                              Fr* __restrict__ out, double scale,
+                                              unsigned* __restrict__ blockmax, uint32_t blk) {
+    uint64_t i = (uint64_t)blk * blockDim.x + threadIdx.x;
     // bit length of |x_q| for the GEMM digit-count choice (wave max, one atomic)
     uint32_t bits = 0;
     if (i < n) {
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in,
         if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = bits;
         __syncthreads();
         if (threadIdx.x == 0)
-            blockmax[blockIdx.x] = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+            blockmax[blk] = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
     }
     if (i >= n) return;
     double x = in[i];
@@ -101,6 +101,33 @@ __global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in,
         q.w[2] = (uint32_t)(v >> 64); q.w[3] = (uint32_t)(v >> 96);
     }
     st_fr(out + i, neg ? fr_sub(fr_zero(), q) : q);
+}
+__global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in, uint64_t n,
+                                                  Fr* __restrict__ out, double scale,
+                                                  unsigned* __restrict__ blockmax) {
+    quantize_body(in, n, out, scale, blockmax, blockIdx.x);
+}
+// m, u, v, d in one launch (their ZkMatrix::new calls are back to back,
+// examples/svd_example.rs:138-144): one ramp-up / tail instead of four.
+__global__ __launch_bounds__(256) void k_quantize_multi(const QuantSegs q, double scale) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxQuantSegs; ++k) s += (uint32_t)k < q.nseg && blockIdx.x >= q.blk0[k];
+    const double* in = q.in[0];
+    Fr* out = q.out[0];
+    unsigned* bm = q.blockmax[0];
+    uint64_t n = q.n[0];
+    uint32_t b0 = q.blk0[0];
+#pragma unroll
+    for (int k = 1; k < kMaxQuantSegs; ++k)      // selects, not a dynamic index into the argument
+        if (s == (uint32_t)k) { in = q.in[k]; out = q.out[k]; bm = q.blockmax[k]; n = q.n[k]; b0 = q.blk0[k]; }
+    quantize_body(in, n, out, scale, bm, blockIdx.x - b0);
+}
+hipError_t launch_quantize_multi(const QuantSegs& q, int p, hipStream_t st) {
+    if (!q.nseg || q.nseg > (uint32_t)kMaxQuantSegs || !q.blk0[q.nseg]) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_quantize_multi, dim3(q.blk0[q.nseg]), dim3(256), 0, st, q,
+                       (double)(1ull << p));
+    return hipGetLastError();
 }
 
 hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int p, unsigned* blockmax,

@@ -33,6 +33,18 @@ static constexpr int kStageElems = 256;
 hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int precision_bits,
                            unsigned* blockmax, hipStream_t st);
 // Fold per-block maxima: out[s] = max(blockmax[begin[s] .. begin[s + 1])), s < nseg.
+// One launch quantizing up to 4 matrices (m, u, v, d of the SVD witness):
+// segment s covers blocks [blk0[s], blk0[s+1]) of 256 values.
+static constexpr int kMaxQuantSegs = 4;
+struct QuantSegs {
+    const double* in[kMaxQuantSegs];
+    Fr* out[kMaxQuantSegs];
+    unsigned* blockmax[kMaxQuantSegs];
+    uint64_t n[kMaxQuantSegs];
+    uint32_t blk0[kMaxQuantSegs + 1];
+    uint32_t nseg;
+};
+hipError_t launch_quantize_multi(const QuantSegs& q, int precision_bits, hipStream_t st);
 static constexpr int kMaxBitSegs = 8;
 struct BitSegs {
     uint32_t begin[kMaxBitSegs];

@@ -169,7 +169,7 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                                   {"stage_elems": 192}, {"phase1_overlap": 0}, {"phase1_overlap": 2},
                                   {"stage_divide": 1}, {"stage_align": 1}, {"stage_align": 1, "stage_elems": 64},
                                   {"overlap": 0}, {"stage_inc": 1}, {"stage_priority": 1}, {"gemm_priority": 1},
-                                  {"cu_split": 64}])
+                                  {"cu_split": 64}, {"fused_quantize": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
@@ -317,3 +317,22 @@ def test_rescale_and_inner_product_parity(gpu_ctx_factory, P, LB, S, NB, elems):
             assert po.to_signed(oc[i][j].value) == po.to_signed(ocs[i][j].value) >> P
     assert _ints(ip.values()) == [oip.value]
     assert _ints(y.values()) == [e.value for e in oy]
+
+
+@pytest.mark.parametrize("fused", [1, 0])
+@pytest.mark.parametrize("N,M,P", [(130, 97, 63), (64, 200, 32)])
+def test_device_inputs_parity(gpu_ctx_factory, fused, N, M, P):
+    """The bench path: m, u, v, d already resident in HBM (torch float64 CUDA
+    tensors), quantized in one fused launch (or four), witness vs the oracle."""
+    import torch
+    import halo2_svd041_amd as hs
+    m, u, d, v = gen_svd_input(N, M, seed=N * M)
+    g = gamma_for(N + M)
+    ctx = gpu_ctx_factory(P)
+    ctx.set_option("fused_quantize", fused)
+    dev = torch.device("cuda", 0)
+    dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev)
+                      for x in (m, u, v, d))
+    hs.svd_witness(ctx, dm, du, dv, dd, g)
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+    _assert_streams(ctx, a0, l0, a1)
