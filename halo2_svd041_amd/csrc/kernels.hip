@@ -474,14 +474,22 @@ __device__ __forceinline__ void element_program(const StageArgs& a, uint32_t e, 
             case MO_ISZERO: {
                 const Fr v = lds_get(myV + op.a * VW);
                 const bool z = fr_is_zero(v);
-                const Fr inv = z ? fr_from_u64(1) : fr_inv(v);
+                // the exponentiation only where some lane needs it (honest
+                // is_equal rows are all zero): a select would always run it
+                Fr inv = fr_from_u64(1);
+                if (__any(!z)) {
+                    const Fr t = fr_inv(v);
+                    inv = z ? inv : t;
+                }
                 lds_put(dst, fr_from_u64(z ? 1 : 0));
                 lds_put(dst + VW, inv);
                 break;
             }
-            case MO_POWK:
-                lds_put(dst, fr_pow_u64(lds_get(sK + op.a * VW), (uint64_t)e + op.p0));
+            case MO_POWK: {
+                const uint64_t x = (uint64_t)e + op.p0;       // square-and-multiply over its bits only
+                lds_put(dst, fr_pow_u64(lds_get(sK + op.a * VW), x, x ? 64 - __clzll(x) : 1));
                 break;
+            }
             case MO_SHR: {
                 const uint32_t* s = myV + op.a * VW;    // words straight from LDS
                 const uint32_t q = op.p0 >> 5, r = op.p0 & 31;
