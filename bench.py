@@ -215,6 +215,22 @@ def main():
     elapsed = time.perf_counter() - t0
     stats = ctx.profile_collect() if not args.no_profile else []
 
+    # The same kernel alone on the GPU (one untimed step with both streams
+    # serialised): its intrinsic rate, reported beside the contended in-step rate.
+    solo = None
+    if not args.no_profile and not rows_mode:
+        ctx.set_option("overlap", 0)
+        ctx.set_option("phase1_overlap", 0)
+        ctx.profile(True, args.profile_prefix)
+        hs.svd_witness(ctx, dm, du, dv, dd, g)
+        ctx.sync()
+        solo_stats = ctx.profile_collect()
+        ctx.profile(False)
+        ctx.set_option("overlap", 1)
+        ctx.set_option("phase1_overlap", 1)
+        if solo_stats:
+            _, solo, _ = roofline_from_profile(solo_stats, 1)
+
     reasm = None
     if rows_mode and args.gather != "none":
         # witness + reassembly per step, timed like the witness-only loop
@@ -282,6 +298,10 @@ def main():
             if traffic is not None:
                 roof["traffic"] = traffic
                 roof["traffic_source"] = src
+            if solo is not None and solo["kernel"] == roof["kernel"]:
+                roof["standalone"] = {k: solo[k] for k in ("achieved", "frac", "avg_launch_ms")}
+                roof["standalone"]["note"] = ("same kernel, one extra untimed step with the "
+                                              "streams serialised (no concurrent products/scans)")
             out["roofline"] = roof
             if args.breakdown:
                 print(json.dumps({"ms_per_step_by_kernel": breakdown,
