@@ -297,7 +297,7 @@ struct svdw_ctx {
     hipStream_t st = nullptr;
     uint32_t P = 32, LB = 19;
     Stream ph[2];
-    DBuf f64in, digA, digB, w1c, w1m, w2c, w2m, bits, gpc, gpm, crtR, gbits;
+    DBuf f64in, digA, digB, digC, w1c, w1m, w2c, w2m, bits, gpc, gpm, crtR, gbits;
     DBuf wbc[kMaxScanJobs], wbs[kMaxScanJobs];   // b.v per batched verify_mul (canonical, scaled)
     // gamma^j cache (canonical gpc / Montgomery gpm), shared by verify_mul calls
     Fr gp_gamma{};
@@ -842,10 +842,14 @@ static std::vector<uint32_t> maxbits_many(svdw_ctx* c, const std::vector<svdw_ma
 // CRT path residue reuse (prelaunched products of check_svd_phase0): b_cover
 // makes b's planes (kept in digB) also valid for the product (b, b); a_from_b
 // takes a's planes from digB (a is that b) instead of recomputing them.
+// bbuf: where b's planes live (default digB); b_ready: they are already there
+// (row-sharded v.v^T after m.v^T: same b, planes built with b_cover).
 static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_mat& b, Fr* out,
                       uint32_t bits_a, uint32_t bits_b, const unsigned* sa = nullptr,
                       const unsigned* sb = nullptr, bool quantized = false,
-                      const unsigned* b_cover = nullptr, bool a_from_b = false) {
+                      const unsigned* b_cover = nullptr, bool a_from_b = false,
+                      DBuf* bbuf = nullptr, bool b_ready = false) {
+    DBuf& BB = bbuf ? *bbuf : c->digB;
     const uint32_t N = a.rows, K = a.cols, M = b.cols;
     const bool sym = is_transpose_of(b, a);
     if (!sa && !sb && c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA && bits_a <= 128 &&
@@ -869,7 +873,7 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
         ensure_buf(c, c->crtR, (size_t)kCrtMaxResidues * rpa * (sym ? rpa : rpb));
         const uint8_t* Ar;
         if (a_from_b && sym) {
-            Ar = (const uint8_t*)c->digB.p;               // planes of this operand already built
+            Ar = (const uint8_t*)BB.p;                    // planes of this operand already built
         } else {
             ensure_buf(c, c->digA, (size_t)kCrtMaxResidues * rpa * kpad);
             ProfScope ps(c, s, "k_to_residues", 32.0 * N * K, 0);
@@ -878,15 +882,15 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
             Ar = (const uint8_t*)c->digA.p;
         }
         const uint8_t* Br = Ar;
-        if (!sym) {
-            ensure_buf(c, c->digB, (size_t)kCrtMaxResidues * rpb * kpad);
+        if (!sym && !b_ready) {
+            ensure_buf(c, BB, (size_t)kCrtMaxResidues * rpb * kpad);
             svdw_mat bt = b;   // Bt(j, k) = b(k, j)
             bt.rows = b.cols; bt.cols = b.rows; bt.rs = b.cs; bt.cs = b.rs;
             ProfScope ps(c, s, "k_to_residues", 32.0 * M * K, 0);
-            hipck(launch_to_residues(view_of(c, bt), M, K, rpb, kpad, (uint32_t*)c->digB.p, sa, sb,
+            hipck(launch_to_residues(view_of(c, bt), M, K, rpb, kpad, (uint32_t*)BB.p, sa, sb,
                                      lk, s, b_cover), "k_to_residues");
-            Br = (const uint8_t*)c->digB.p;
         }
+        if (!sym) Br = (const uint8_t*)BB.p;
         {
             ProfScope ps(c, s, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * N * M,
                          (double)N * M * K);
@@ -1298,14 +1302,24 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     run_batch("k_matvec_scan:b", b_of, [&](int i) { return pl[i].bv; }, gc,
               [&](int) { return g_b; }, na_b);
     WScaled wb[kMaxScanJobs];
-    for (int i = 0; i < n; ++i) {
-        if (sharded(c)) {
-            // only this rank's rows of the b.g scans exist: every entry of b.g
-            // comes from the values-only mat-vec instead
+    if (sharded(c)) {
+        // only this rank's rows of the b.g scans exist: every entry of b.g comes
+        // from the values-only mat-vec instead (all n products in one launch)
+        ScanBatch vb;
+        memset(&vb, 0, sizeof vb);
+        for (int i = 0; i < n; ++i) {
             const svdw_mat b = vm[i].b;
             ensure_buf(c, c->bvfull[i], (size_t)b.rows * sizeof(Fr));
-            hipck(launch_matvec_values(view_of(c, b), b.rows, b.cols, g_b.ws, g_b.wn, na_b,
-                                       (Fr*)c->bvfull[i].p, c->st), "k_matvec_values");
+            vb.job[i] = ScanJob{view_of(c, b), nullptr, g_b.ws, g_b.wn, (Fr*)c->bvfull[i].p,
+                                b.cols, b.rows, 0, 0};
+        }
+        vb.njobs = n;
+        ProfScope ps(c, c->st, "k_matvec_values", 0, 0);
+        hipck(launch_matvec_values(vb, na_b, c->st), "k_matvec_values");
+    }
+    for (int i = 0; i < n; ++i) {
+        if (sharded(c)) {
+            const svdw_mat b = vm[i].b;
             wb[i] = vec_prep_ptr(c, (const Fr*)c->bvfull[i].p, b.rows, c->wbc[i], c->wbs[i], na_a);
         } else {
             wb[i] = vec_prep(c, pl[i].bv, c->wbc[i], c->wbs[i], na_a);
@@ -1397,21 +1411,26 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
                                  dev_bits ? dev_bits + 2 : nullptr};
         const unsigned* sa[3] = {sl[0], sl[1], sl[2]};
         const unsigned* sb[3] = {sl[2], sl[1], sl[2]};
+        bool vplanes = false;                            // v's planes built (digB) on this rank
         for (int g = 0; g < 3; ++g) {
             // shard: rows [r0, r1) of the product only
             uint64_t r0 = 0, r1 = A[g].rows;
             if (sharded(c)) shard_rows(c, A[g].rows, &r0, &r1);
             const svdw_mat Ag = sharded(c) ? row_block(A[g], r0, r1) : A[g];
             Fr* outg = cellp(c, m.phase, log[g] + r0 * B[g].cols);
-            // CRT: v's residue planes from m.v^T (covering v.v^T too) serve v.v^T
-            const bool reuse = !sharded(c);
+            // CRT: v's residue planes from m.v^T (covering v.v^T too) serve v.v^T:
+            // as both operands unsharded (v.v^T symmetric), as the b operand when
+            // the rows are sharded (u's planes go to digC so v's survive)
+            const bool shd = sharded(c);
             if (r1 <= r0) {
                 // nothing of this product on this rank
             } else if (on_device)
                 gemm_exec(c, c->st2, Ag, B[g], outg, ~0u, ~0u, sa[g], sb[g], dev_quantized,
-                          reuse && g == 0 ? sl[2] : nullptr, reuse && g == 2);
+                          g == 0 ? sl[2] : nullptr, !shd && g == 2,
+                          shd && g == 1 ? &c->digC : nullptr, shd && g == 2 && vplanes);
             else
                 gemm_exec(c, c->st2, Ag, B[g], outg, ba[g], bb[g]);
+            if (g == 0 && r1 > r0 && on_device) vplanes = true;
             c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
             c->gemm_done.push_back(c->pre.back().ev);
         }
@@ -1600,7 +1619,7 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             (void)hipStreamSynchronize(c->st2);
             if (c->st3) (void)hipStreamSynchronize(c->st3);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
-            for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->w1c, &c->w1m, &c->w2c, &c->w2m,
+            for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->w1c, &c->w1m, &c->w2c, &c->w2m,
                             &c->bits, &c->gpc, &c->gpm, &c->crtR, &c->gbits})
                 if (b->p) (void)hipFree(b->p);
             for (auto& b : c->gps) if (b.p) (void)hipFree(b.p);

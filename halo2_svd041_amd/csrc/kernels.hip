@@ -1810,13 +1810,20 @@ __global__ __launch_bounds__(256) void k_matvec_scan(const DView A, uint32_t r_b
 // out[r] = sum_j A(r, j) w_j mod p for rows [0, R) (values only, no cells): the
 // row-sharded witness needs every entry of b.g while it emits the b.g scan
 // cells of its own rows only. One block per row; products as in the scan.
+// Batched like the scans: job q owns blocks [blk0, blk0 + rows) of the grid.
 template <int NA>
-__global__ __launch_bounds__(256) void k_matvec_values(const DView A, uint32_t L,
-                                                       const Fr* __restrict__ wm,
-                                                       const Fr* __restrict__ wn,
-                                                       Fr* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_matvec_values(const ScanBatch B) {
     __shared__ U9 part[256];
-    const uint32_t r = blockIdx.x, tid = threadIdx.x;
+    ScanJob J = B.job[0];
+#pragma unroll
+    for (int q = 1; q < kMaxScanJobs; ++q)
+        if ((uint32_t)q < B.njobs && blockIdx.x >= B.job[q].blk0) J = B.job[q];
+    const DView& A = J.A;
+    const uint32_t L = J.L;
+    const Fr* __restrict__ wm = J.ws;
+    const Fr* __restrict__ wn = J.wsn;
+    Fr* __restrict__ out = J.out;
+    const uint32_t r = blockIdx.x - J.blk0, tid = threadIdx.x;
     const Fr zero = fr_zero();
     U9 acc = u9_from(zero);
     for (uint32_t j = tid; j < L; j += 256) {
@@ -1845,19 +1852,25 @@ __global__ __launch_bounds__(256) void k_matvec_values(const DView A, uint32_t L
     }
     if (tid == 0) st_fr(out + r, reduce9(part[0].w));
 }
-hipError_t launch_matvec_values(const DView& A, uint32_t R, uint32_t L, const Fr* w_scaled,
-                                const Fr* w_neg, int na, Fr* out, hipStream_t st) {
-    if (!R || !L) return hipSuccess;
-    if (L > 8192) return hipErrorInvalidValue;
-    const dim3 g(R), b(256);
+hipError_t launch_matvec_values(const ScanBatch& b0, int na, hipStream_t st) {
+    ScanBatch b = b0;
+    uint32_t blocks = 0;
+    for (uint32_t q = 0; q < b.njobs; ++q) {
+        if (b.job[q].L > 8192) return hipErrorInvalidValue;
+        b.job[q].blk0 = blocks;
+        blocks += b.job[q].L ? b.job[q].rows : 0;
+        if (!b.job[q].L) b.job[q].rows = 0;
+    }
+    if (!blocks) return hipSuccess;
+    const dim3 g(blocks), blk(256);
     switch (na) {
-    case 1: hipLaunchKernelGGL(k_matvec_values<1>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
-    case 2: hipLaunchKernelGGL(k_matvec_values<2>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
-    case 3: hipLaunchKernelGGL(k_matvec_values<3>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
-    case 4: hipLaunchKernelGGL(k_matvec_values<4>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
-    case 5: hipLaunchKernelGGL(k_matvec_values<5>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
-    case 6: hipLaunchKernelGGL(k_matvec_values<6>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
-    default: hipLaunchKernelGGL(k_matvec_values<8>, g, b, 0, st, A, L, w_scaled, w_neg, out); break;
+    case 1: hipLaunchKernelGGL(k_matvec_values<1>, g, blk, 0, st, b); break;
+    case 2: hipLaunchKernelGGL(k_matvec_values<2>, g, blk, 0, st, b); break;
+    case 3: hipLaunchKernelGGL(k_matvec_values<3>, g, blk, 0, st, b); break;
+    case 4: hipLaunchKernelGGL(k_matvec_values<4>, g, blk, 0, st, b); break;
+    case 5: hipLaunchKernelGGL(k_matvec_values<5>, g, blk, 0, st, b); break;
+    case 6: hipLaunchKernelGGL(k_matvec_values<6>, g, blk, 0, st, b); break;
+    default: hipLaunchKernelGGL(k_matvec_values<8>, g, blk, 0, st, b); break;
     }
     return hipGetLastError();
 }

@@ -124,8 +124,9 @@ hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, 
                               int impl, int na, hipStream_t st);
 // out[r] = sum_j A(r, j) w_j mod p, r < R, L <= 8192 (values of the scans' last
 // cells without the cells); w_scaled / w_neg as for the scans with the same na.
-hipError_t launch_matvec_values(const DView& A, uint32_t R, uint32_t L, const Fr* w_scaled,
-                                const Fr* w_neg, int na, Fr* out, hipStream_t st);
+// out[r] = sum_j A(r, j) w_j per job (job.ws / job.wsn = w scaled / negated as
+// in the scans, job.out = the values, rows [0, job.rows)); one launch for all jobs.
+hipError_t launch_matvec_values(const ScanBatch& b, int na, hipStream_t st);
 // Up to kMaxScanJobs DPP row scans in one launch (T terms per thread: 1, 2, 4;
 // na as above, shared by every job: each job's w_scaled = w * 2^(32 na)).
 hipError_t launch_scan_batch(const ScanBatch& b, int T, int na, hipStream_t st);

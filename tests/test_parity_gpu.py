@@ -232,16 +232,19 @@ def _reassemble(ctxs, counts):
     return out
 
 
-@pytest.mark.parametrize("N,M,P,world", [(40, 33, 63, 2), (33, 40, 32, 3), (24, 24, 42, 5)])
-def test_row_sharded_witness_parity(gpu_ctx_factory, N, M, P, world):
+@pytest.mark.parametrize("N,M,P,world,crt", [(40, 33, 63, 2, 1), (33, 40, 32, 3, 1), (24, 24, 42, 5, 1),
+                                              (40, 33, 63, 2, 0), (70, 70, 63, 8, 1)])
+def test_row_sharded_witness_parity(gpu_ctx_factory, N, M, P, world, crt):
     """Row-block sharding (BASELINE config 4 layout): the union of the ranks'
-    owned cells is the oracle's witness, bit for bit."""
+    owned cells is the oracle's witness, bit for bit (CRT products, with v's
+    residue planes reused by v.v^T on each rank; and the digit-plane GEMM)."""
     import halo2_svd041_amd as hs
     m, u, d, v = gen_svd_input(N, M, seed=N * M + world)
     g = gamma_for(world)
     ctxs = []
     for rank in range(world):
         ctx = gpu_ctx_factory(P)
+        ctx.set_option("gemm_crt", crt)
         ctx.set_shard(rank, world)
         counts = hs.svd_witness(ctx, m, u, v, d, g)
         ctxs.append(ctx)
