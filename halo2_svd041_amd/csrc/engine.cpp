@@ -1553,10 +1553,15 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     // join the streams afterwards.
     // Mode 2: on a third stream that starts after quantization; the b.g and
     // a.(b.g) scans run at once, the c_s.g scans wait for the products.
-    const bool p1_overlap = c->phase1_overlap && c->prelaunched && !c->dry;
-    if (p1_overlap && c->phase1_overlap == 2 && !c->st3)   // created on first use
+    // Mode 1 on a row-sharded rank becomes mode 2: there the products are only a
+    // row block, the st2 chain (products + phase 1) is the critical path and the
+    // operand-only scans fit beside the products (tools/shard_sim.py, 8 ranks:
+    // 0.62 -> 0.54 ms); unsharded, mode 2 costs ~2 %.
+    const int p1mode = c->phase1_overlap == 1 && sharded(c) ? 2 : c->phase1_overlap;
+    const bool p1_overlap = p1mode && c->prelaunched && !c->dry;
+    if (p1_overlap && p1mode == 2 && !c->st3)   // created on first use
         hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
-    hipStream_t p1s = c->phase1_overlap == 2 ? c->st3 : c->st2;
+    hipStream_t p1s = p1mode == 2 ? c->st3 : c->st2;
     if (p1_overlap && p1s == c->st3) {
         hipck(hipStreamWaitEvent(c->st3, c->ev_bits, 0), "hipStreamWaitEvent");
         c->wait_before_cs = c->gemm_done;

@@ -1823,7 +1823,10 @@ __global__ __launch_bounds__(256) void k_matvec_values(const ScanBatch B) {
     const Fr* __restrict__ wm = J.ws;
     const Fr* __restrict__ wn = J.wsn;
     Fr* __restrict__ out = J.out;
-    const uint32_t r = blockIdx.x - J.blk0, tid = threadIdx.x;
+    // rows dealt XCD-contiguously (as the scans): a transposed b's neighbouring
+    // rows are neighbouring columns, one 128 B line per 4 rows in one L2
+    const uint32_t lb = blockIdx.x - J.blk0;
+    const uint32_t r = (J.blk0 & 7) ? lb : scan_row(lb, J.rows), tid = threadIdx.x;
     const Fr zero = fr_zero();
     U9 acc = u9_from(zero);
     for (uint32_t j = tid; j < L; j += 256) {

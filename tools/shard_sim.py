@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--rank", type=int, default=None, help="time only this rank of each world")
+    ap.add_argument("--opt", action="append", default=[], help="svdw_set_option name=value")
     a = ap.parse_args()
     import torch
     import halo2_svd041_amd as hs
@@ -45,6 +46,9 @@ def main():
         per_rank = []
         for r in (range(W) if a.rank is None else [a.rank % W]):
             ctx = hs.Context(device=0, precision_bits=a.p, lookup_bits=19)
+            for kv in a.opt:
+                k, _, val = kv.partition("=")
+                ctx.set_option(k, int(val))
             if W > 1:
                 ctx.set_shard(r, W)
             cnt = hs.svd_witness(ctx, dm, du, dv, dd, g)   # warm-up
