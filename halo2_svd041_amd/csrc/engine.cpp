@@ -330,8 +330,7 @@ struct svdw_ctx {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
-    uint32_t stage_flags = STAGE_ALIGN;     // STAGE_* (svdw_set_option "nt_stores", "stage_ilp", ...)
-    uint32_t stage_sweep = 0;               // "stage_sweep": persistent grid of the sweep mode (0 off)
+    uint32_t stage_flags = STAGE_ALIGN;     // STAGE_* (svdw_set_option "stage_align", "stage_inc", ...)
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
     int scan_impl = 4;                      // svdw_set_option "scan_impl"
     int prelaunch_at = 0;                   // "prelaunch_at": GEMMs queued before stage 0/1/2
@@ -580,7 +579,6 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     a.e_end = ee;
     a.cols = cols ? cols : 1;
     a.flags = c->stage_flags;
-    a.sweep_nb = c->stage_sweep;
     // small blocks overlap better with concurrent work, but a stage with field
     // multiplications / inversions keeps one element per thread of a full block
     bool heavy = false;
@@ -590,10 +588,6 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     // keep the block's LDS (element values) within 64 KiB: fewer elements per
     // block for stages with many values (signed_div_scale)
     while (a.E > 64 && stage_lds_bytes(a.nv ? a.nv : 1, a.E, a.C + a.L) > 65536) a.E -= 64;
-    // interleaved groups only pay off on big stages (and need whole batches of work)
-    if (c->stage_sweep && c->stage_elems == kStageElems && a.E == kStageElems &&
-        (uint64_t)nelem >= 4ull * kStageElems * c->stage_sweep / kSweepG)
-        a.flags |= STAGE_SWEEP;
     // 32-bit magics for fastdiv (divisor 1 is handled in the kernel)
     auto magic = [](uint64_t d) -> uint32_t { return d > 1 ? (uint32_t)(((1ull << 32) + d - 1) / d) : 0; };
     a.cdiv_magic = magic(a.C);
@@ -1597,8 +1591,6 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
         c->LB = p->lookup_bits;
         c->device = p->device;
         c->dry = p->device < 0;
-        if (const char* nt = getenv("SVDW_NT_STORES"))
-            c->stage_flags = (c->stage_flags & ~STAGE_NT_STORES) | (nt[0] == '1' ? STAGE_NT_STORES : 0);
         if (const char* g = getenv("SVDW_GEMM"))
             c->gemm_impl = (!strcmp(g, "valu") || !strcmp(g, "dot4")) ? SVDW_GEMM_VALU : SVDW_GEMM_MFMA;
         if (!c->dry) {
@@ -1929,17 +1921,10 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         if (n == "gemm_impl") {
             REQUIRE(value == SVDW_GEMM_MFMA || value == SVDW_GEMM_VALU, "gemm_impl: 0 (mfma) or 1 (valu)");
             c->gemm_impl = (int)value;
-        } else if (n == "nt_stores") {
-            c->stage_flags = (c->stage_flags & ~STAGE_NT_STORES) | (value ? STAGE_NT_STORES : 0);
         } else if (n == "stage_elems") {
             REQUIRE(value >= 16 && value <= 256 && value % 16 == 0,
                     "stage_elems: a multiple of 16 in [16, 256]");
             c->stage_elems = (uint32_t)value;
-        } else if (n == "stage_divide") {
-            c->stage_flags = (c->stage_flags & ~STAGE_DIVIDE) | (value ? STAGE_DIVIDE : 0);
-        } else if (n == "stage_sweep") {
-            REQUIRE(value >= 0 && value <= 4096, "stage_sweep: 0 (off) or a grid size <= 4096");
-            c->stage_sweep = (uint32_t)value;
         } else if (n == "stage_inc") {             // previous phase B (per-half-cell decode)
             c->stage_flags = (c->stage_flags & ~STAGE_INC) | (value ? STAGE_INC : 0);
         } else if (n == "stage_align") {
@@ -1948,10 +1933,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             REQUIRE(value >= 0 && value <= 2, "stage_probe: 0 off, 1 skip phase A, 2 constant stores");
             c->stage_flags = (c->stage_flags & ~(STAGE_PROBE_NOA | STAGE_PROBE_CONST)) |
                              (value == 1 ? STAGE_PROBE_NOA : value == 2 ? STAGE_PROBE_CONST : 0);
-        } else if (n == "stage_ilp") {
-            REQUIRE(value == 1 || value == 2 || value == 4, "stage_ilp: 1, 2 or 4");
-            c->stage_flags = (c->stage_flags & ~(STAGE_ILP2 | STAGE_ILP4)) |
-                             (value == 2 ? STAGE_ILP2 : value == 4 ? STAGE_ILP4 : 0);
         } else if (n == "gemm_priority") {
             // second (GEMM) stream priority: 0 normal, 1 high
             REQUIRE(value == 0 || value == 1, "gemm_priority: 0 or 1");

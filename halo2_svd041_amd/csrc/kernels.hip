@@ -241,46 +241,13 @@ __device__ __forceinline__ uint32_t fastdiv(uint32_t x, uint32_t d, uint32_t mag
     return d == 1 ? x : __umulhi(x, magic);
 }
 
-// The block's cells in stream order, half a cell (16 B) per lane: every wave
-// store is 1 KiB contiguous. U independent half-cells per thread per iteration
-// keep several LDS round trips in flight.
-template <bool NT, int U>
-__device__ __forceinline__ void stream_cells(uint4* __restrict__ out, uint32_t total,
-                                             const SlotOp* __restrict__ ops, uint32_t C,
-                                             uint32_t magic, const uint32_t* sK, const uint32_t* sV,
-                                             uint32_t nv) {
-    for (uint32_t base = threadIdx.x; base < total; base += blockDim.x * U) {
-        uint4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t hc = min(base + u * blockDim.x, total - 1);
-            const uint32_t c = hc >> 1, h = hc & 1;
-            const uint32_t el = fastdiv(c, C, magic);
-            const SlotOp op = ops[c - el * C];
-            const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + (el * nv + op.src) * VW;
-            v[u] = extract_half(src, op.lo, op.nbits, h);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t hc = base + u * blockDim.x;
-            if (hc >= total) break;
-            if (NT) {
-                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                u32x4 w = {v[u].x, v[u].y, v[u].z, v[u].w};
-                __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(out + hc));
-            } else {
-                out[hc] = v[u];
-            }
-        }
-    }
-}
-
-// Default path: one half-cell per lane per iteration, the (element, slot) of
-// the lane's next cell tracked incrementally (the cell index advances by
-// blockDim/2 each step) instead of a mul_hi division per half-cell.
+// Previous phase B (STAGE_INC, kept as the A/B reference of the descriptor
+// path): one half-cell per lane per iteration, each lane decoding its slot op
+// and building the masks; the (element, slot) of the lane's next cell tracked
+// incrementally (the cell index advances by blockDim/2 each step).
 // ALIGN: the block's iterations cover whole (blockDim * 16 B)-aligned address
 // windows (the first one partially), so every wave store is one aligned 1 KiB.
-template <bool NT, bool ALIGN>
+template <bool ALIGN>
 __device__ __forceinline__ void stream_cells_inc(uint4* __restrict__ out, uint32_t total,
                                                  const SlotOp* __restrict__ ops, uint32_t C,
                                                  uint32_t magic, const uint32_t* sK,
@@ -299,14 +266,7 @@ __device__ __forceinline__ void stream_cells_inc(uint4* __restrict__ out, uint32
     for (uint32_t hc = hc0; hc < total; hc += blockDim.x) {
         const SlotOp op = ops[slot];
         const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + vbase + op.src * VW;
-        const uint4 v = extract_half(src, op.lo, op.nbits, h);
-        if (NT) {
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 w = {v.x, v.y, v.z, v.w};
-            __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(out + hc));
-        } else {
-            out[hc] = v;
-        }
+        out[hc] = extract_half(src, op.lo, op.nbits, h);
         slot += dr;
         vbase += dq * ev;
         if (slot >= C) {
@@ -316,7 +276,7 @@ __device__ __forceinline__ void stream_cells_inc(uint4* __restrict__ out, uint32
     }
 }
 
-// Default path: per-(slot, half) descriptors and masks prepared once per block
+// Phase B: per-(slot, half) descriptors and masks prepared once per block
 // (half_desc, prog.hpp), so a half-cell costs one descriptor + one mask LDS
 // read, five word reads, four alignbit and four and (no per-cell decoding,
 // clamping or mask arithmetic). The (element, slot) of the lane's next cell is
@@ -372,44 +332,6 @@ __device__ __forceinline__ void make_half(const SlotOp op, uint32_t h, uint32_t*
         w[i] = keep >= 32 ? 0xffffffffu : (keep <= 0 ? 0u : ((1u << keep) - 1u));
     }
     *m = make_uint4(w[0], w[1], w[2], w[3]);
-}
-
-// Sweep mode: local element l of batch jb of block b is global element
-// e_begin + G (b + nb (jb E/G + l/G)) + l % G.
-struct SweepMap {
-    uint32_t e_begin, b, nb, jb;
-    __device__ __forceinline__ uint32_t elem(uint32_t l) const {
-        return e_begin + kSweepG * (b + nb * (jb * (kStageElems / kSweepG) + l / kSweepG)) +
-               l % kSweepG;
-    }
-};
-// The batch's cells element by element: half-cell hc of local element el goes
-// to global half-cell 2 (e(el) C + slot) + h.
-template <int U>
-__device__ __forceinline__ void stream_cells_sweep(uint4* __restrict__ out, uint32_t total,
-                                                   const SlotOp* __restrict__ ops, uint32_t C,
-                                                   uint32_t magic, const uint32_t* sK,
-                                                   const uint32_t* sV, uint32_t nv,
-                                                   const SweepMap& map) {
-    for (uint32_t base = threadIdx.x; base < total; base += blockDim.x * U) {
-        uint4 v[U];
-        uint64_t dst[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t hc = min(base + u * blockDim.x, total - 1);
-            const uint32_t c = hc >> 1, h = hc & 1;
-            const uint32_t el = fastdiv(c, C, magic), slot = c - el * C;
-            const SlotOp op = ops[slot];
-            const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + (el * nv + op.src) * VW;
-            v[u] = extract_half(src, op.lo, op.nbits, h);
-            dst[u] = ((uint64_t)map.elem(el) * C + slot) * 2 + h;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (base + u * blockDim.x >= total) break;
-            out[dst[u]] = v[u];
-        }
-    }
 }
 
 // Phase A for one element: run the stage's micro-ops, values into myV (LDS).
@@ -528,27 +450,24 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     uint32_t* sHD = reinterpret_cast<uint32_t*>(sHM + 2 * (a.C + a.L));
 
     const uint32_t tid = threadIdx.x;
-    const bool sweep = (a.flags & STAGE_SWEEP) != 0;
-    SweepMap map{a.e_begin, blockIdx.x, gridDim.x, 0};
+    const uint32_t e0 = a.e_begin + blockIdx.x * E;
+    const uint32_t ne = min(E, a.e_end - e0), e = e0 + tid;
 
     // Issue this thread's in-bounds strided view loads before the LDS set-up,
     // so their latency overlaps it (phase A falls back to view_load otherwise).
     Fr pf0 = fr_zero(), pf1 = fr_zero();
     bool in0 = false, in1 = false;
-    if (!sweep) {
-        const uint32_t pe = a.e_begin + blockIdx.x * E + tid;
-        if (tid < E && pe < a.e_end) {
-            const uint32_t pi = pe / a.cols, pj = pe - pi * a.cols;
-            const DView& v0 = a.view[0];
-            if (v0.ptr && v0.mode == VIEW_STRIDED && pi < v0.rows && pj < v0.cols) {
-                pf0 = ld_fr(v0.ptr + (int64_t)pi * v0.rs + (int64_t)pj * v0.cs);
-                in0 = true;
-            }
-            const DView& v1 = a.view[1];
-            if (v1.ptr && v1.mode == VIEW_STRIDED && pi < v1.rows && pj < v1.cols) {
-                pf1 = ld_fr(v1.ptr + (int64_t)pi * v1.rs + (int64_t)pj * v1.cs);
-                in1 = true;
-            }
+    if (tid < ne) {
+        const uint32_t pi = e / a.cols, pj = e - pi * a.cols;
+        const DView& v0 = a.view[0];
+        if (v0.ptr && v0.mode == VIEW_STRIDED && pi < v0.rows && pj < v0.cols) {
+            pf0 = ld_fr(v0.ptr + (int64_t)pi * v0.rs + (int64_t)pj * v0.cs);
+            in0 = true;
+        }
+        const DView& v1 = a.view[1];
+        if (v1.ptr && v1.mode == VIEW_STRIDED && pi < v1.rows && pj < v1.cols) {
+            pf1 = ld_fr(v1.ptr + (int64_t)pi * v1.rs + (int64_t)pj * v1.cs);
+            in1 = true;
         }
     }
 
@@ -563,18 +482,6 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     }
     __syncthreads();
 
-  for (;; ++map.jb) {
-    uint32_t e0, ne, e;
-    if (sweep) {
-        if (map.elem(0) >= a.e_end) break;                // uniform: this block is done
-        e = map.elem(tid);
-        ne = __syncthreads_count(e < a.e_end);            // valid elements form a prefix
-        e0 = 0;
-    } else {
-        e0 = a.e_begin + blockIdx.x * E;
-        ne = min(E, a.e_end - e0);
-        e = e0 + tid;
-    }
     // ---- phase A: per-element micro-ops (constants / ops / views read from LDS:
     // dynamic indexing into the by-value kernel argument would go to scratch)
     if (tid < ne && !(a.flags & (STAGE_PROBE_NOA | STAGE_PROBE_CONST)))
@@ -582,34 +489,16 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     __syncthreads();
 
     // ---- phase B: advice cells, then lookup cells
-    if (sweep) {
-        stream_cells_sweep<4>(reinterpret_cast<uint4*>(a.out_adv), 2 * ne * a.C, sAdv, a.C,
-                              a.cdiv_magic, sK, sV, nv, map);
-        if (a.L)
-            stream_cells_sweep<4>(reinterpret_cast<uint4*>(a.out_lk), 2 * ne * a.L, sLk, a.L,
-                                  a.ldiv_magic, sK, sV, nv, map);
-        __syncthreads();                                  // LDS values reused by the next batch
-        continue;
-    }
     uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
     uint4* outL = a.L ? reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L) : nullptr;
-#define SVDW_STREAM(NT, U)                                                                         \
-    do {                                                                                           \
-        stream_cells<NT, U>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);             \
-        if (a.L) stream_cells<NT, U>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);     \
-    } while (0)
     if (a.flags & STAGE_PROBE_CONST) {
         const uint4 z = make_uint4(pf0.w[0] ^ pf1.w[0], 0, 0, 0);
         for (uint32_t hc = tid; hc < 2 * ne * a.C; hc += blockDim.x) outA[hc] = z;
         if (a.L)
             for (uint32_t hc = tid; hc < 2 * ne * a.L; hc += blockDim.x) outL[hc] = z;
-    } else if (a.flags & STAGE_NT_STORES) SVDW_STREAM(true, 1);
-    else if (a.flags & STAGE_ILP4) SVDW_STREAM(false, 4);
-    else if (a.flags & STAGE_ILP2) SVDW_STREAM(false, 2);
-    else if (a.flags & STAGE_DIVIDE) SVDW_STREAM(false, 1);
-    else if (a.flags & STAGE_INC) {
-        stream_cells_inc<false, true>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
-        if (a.L) stream_cells_inc<false, true>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
+    } else if (a.flags & STAGE_INC) {
+        stream_cells_inc<true>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
+        if (a.L) stream_cells_inc<true>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
     } else {
         const uint32_t vb0 = (uint32_t)(sV - smem);
         if (a.flags & STAGE_ALIGN) {
@@ -624,24 +513,15 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
                                          a.ldiv_magic, smem, vb0, nv);
         }
     }
-#undef SVDW_STREAM
-    break;
-  }
 }
 
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     if (a.e_end <= a.e_begin) return hipSuccess;
     const uint32_t n = a.e_end - a.e_begin;
     const uint32_t E = a.E ? a.E : kStageElems;
-    if (E > kStageElems || ((a.flags & STAGE_SWEEP) && E != kStageElems)) return hipErrorInvalidValue;
+    if (E > kStageElems) return hipErrorInvalidValue;
     const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1, E, a.C + a.L);
-    uint32_t grid = (n + E - 1) / E;
-    if (a.flags & STAGE_SWEEP) {
-        // persistent blocks; every block needs at least one group
-        const uint32_t groups = (n + kSweepG - 1) / kSweepG;
-        grid = a.sweep_nb < groups ? a.sweep_nb : groups;
-        if (!grid) return hipErrorInvalidValue;
-    }
+    const uint32_t grid = (n + E - 1) / E;
     hipLaunchKernelGGL(k_stage, dim3(grid), dim3(256), lds, st, a);
     return hipGetLastError();
 }

@@ -58,20 +58,11 @@ struct SlotOp {
 };
 static constexpr uint8_t KSRC = 0x80;
 
-static constexpr uint32_t STAGE_NT_STORES = 1;   // non-temporal cell stores
-static constexpr uint32_t STAGE_ILP2 = 2;        // 2 / 4 independent half-cells per iteration
-static constexpr uint32_t STAGE_ILP4 = 4;
-// Persistent blocks over groups of kSweepG consecutive elements interleaved
-// across the grid (group g -> block g % grid): at any moment the blocks write
-// neighbouring groups, a narrow front across the cell stream.
-static constexpr uint32_t STAGE_SWEEP = 8;
-static constexpr uint32_t STAGE_DIVIDE = 16;      // per-half-cell division (A/B reference)
 // Timing probes (wrong cells; tools/ab.py only): skip phase A / store a constant
 static constexpr uint32_t STAGE_PROBE_NOA = 64;
 static constexpr uint32_t STAGE_PROBE_CONST = 128;
 static constexpr uint32_t STAGE_ALIGN = 256;     // 4 KiB-aligned block store windows
 static constexpr uint32_t STAGE_INC = 512;       // phase B decoding slot ops per half-cell (A/B reference)
-static constexpr uint32_t kSweepG = 4;
 
 static constexpr int kMaxViews = 2;
 static constexpr int kMaxMicro = 16;
@@ -91,7 +82,6 @@ struct StageArgs {
     uint32_t flags;       // STAGE_* bits
     uint32_t cdiv_magic;  // ceil(2^32 / C) (C >= 2): x / C = mul_hi(x, magic) for x * C < 2^32
     uint32_t ldiv_magic;  // ceil(2^32 / L)
-    uint32_t sweep_nb;    // STAGE_SWEEP: persistent grid size
     uint32_t E;           // elements per block (<= 256 = block size); 0 -> 256
     DView view[kMaxViews];
     MicroOp mo[kMaxMicro];

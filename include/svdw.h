@@ -201,14 +201,17 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   "overlap" 1 | 0 (the three check_svd_phase0 products run ahead on a second
  *   stream); "phase1_overlap" 1 | 2 | 0 (svd_witness: phase 1 runs on the
  *   second stream behind the products / on a third stream from quantization
- *   on, its c_s scans waiting for the products / after phase 0); "prelaunch_at" 0 | 1 | 2 (how many phase-0 stages are queued
- *   before them); "gemm_priority" 0 | 1 (second stream priority);
+ *   on, its c_s scans waiting for the products / after phase 0; 1 acts as 2 on
+ *   a row-sharded context); "prelaunch_at" 0 | 1 | 2 (how many phase-0 stages
+ *   are queued before them); "gemm_priority" 0 | 1 (second stream priority:
+ *   default | high); "stage_priority" 0 | 1 (cell stream priority);
+ *   "cu_split" 0 | multiple of 8 (CUs masked to the second stream, the rest to
+ *   the cell stream); "fused_quantize" 1 | 0 (m, u, v, d quantized in one
+ *   launch when resident in HBM);
  *   "stage_elems" 256 (elements per stage block, multiple of 16 in [16, 256]);
- *   "stage_ilp" 1 | 2 | 4 (half-cells in flight per thread); "nt_stores" 0 | 1
- *   (non-temporal cell stores); "stage_sweep" 0 | grid (persistent blocks over
- *   interleaved element groups; needs stage_elems 256); "stage_align" 1 | 0
- *   (each block's store windows aligned to 4 KiB); "stage_divide" 0 | 1
- *   (per-half-cell division instead of incremental slot tracking);
+ *   "stage_align" 1 | 0 (each block's store windows aligned to 4 KiB);
+ *   "stage_inc" 0 | 1 (previous phase B: slot ops decoded per half-cell
+ *   instead of per-block descriptors);
  *   "scan_impl" 4 | 1 | 2 | 3 | 5 (row-scan kernel: 1 shuffle scan, 2 four
  *   terms/thread direct stores, 3 DPP scan, 4 / 5 DPP scan with two / four
  *   terms per thread, unreduced partial sums and small-operand products where

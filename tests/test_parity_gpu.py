@@ -162,14 +162,13 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                     | (int(got[i, j, 3]) << 192) == want
 
 
-@pytest.mark.parametrize("opts", [{"stage_ilp": 2}, {"stage_ilp": 4}, {"nt_stores": 1},
-                                  {"scan_impl": 2}, {"scan_impl": 3}, {"scan_impl": 1}, {"scan_impl": 5},
+@pytest.mark.parametrize("opts", [{"scan_impl": 2}, {"scan_impl": 3}, {"scan_impl": 1}, {"scan_impl": 5},
                                   {"gemm_rt": 0}, {"prelaunch_at": 2}, {"gemm_crt": 0},
-                                  {"stage_sweep": 1}, {"stage_sweep": 3}, {"stage_elems": 64},
-                                  {"stage_elems": 192}, {"phase1_overlap": 0}, {"phase1_overlap": 2},
-                                  {"stage_divide": 1}, {"stage_align": 1}, {"stage_align": 1, "stage_elems": 64},
-                                  {"overlap": 0}, {"stage_inc": 1}, {"stage_priority": 1}, {"gemm_priority": 1},
-                                  {"cu_split": 64}, {"fused_quantize": 0}])
+                                  {"stage_elems": 64}, {"stage_elems": 192},
+                                  {"phase1_overlap": 0}, {"phase1_overlap": 2},
+                                  {"stage_align": 0}, {"stage_align": 0, "stage_elems": 64},
+                                  {"overlap": 0}, {"stage_inc": 1}, {"stage_priority": 1},
+                                  {"gemm_priority": 1}, {"cu_split": 64}, {"fused_quantize": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
