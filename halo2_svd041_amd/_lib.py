@@ -64,6 +64,12 @@ class Segment(ct.Structure):
                 ("n", ct.c_uint64)]
 
 
+class Region(ct.Structure):
+    _fields_ = [("phase", ct.c_uint32), ("_pad", ct.c_uint32), ("off", ct.c_uint64),
+                ("n", ct.c_uint64), ("loff", ct.c_uint64), ("nl", ct.c_uint64),
+                ("rows", ct.c_uint64), ("tag", ct.c_char * 40)]
+
+
 class InputDims(ct.Structure):
     _fields_ = [("m_rows", ct.c_uint32), ("m_cols", ct.c_uint32), ("u_rows", ct.c_uint32),
                 ("u_cols", ct.c_uint32), ("v_rows", ct.c_uint32), ("v_cols", ct.c_uint32),
@@ -135,6 +141,7 @@ SIGNATURES = {
     "svdw_set_shard": (_i32, [_P, _u32, _u32]),
     "svdw_parse_svd_input": (_i32, [ct.c_char_p, _u64, _i32, ct.POINTER(InputDims), _P, _P, _P, _P]),
     "svdw_shard_segments": (_i32, [_P, ct.POINTER(Segment), _u64, _u64p]),
+    "svdw_layout": (_i32, [_P, ct.POINTER(Region), _u64, _u64p]),
     "svdw_profile_collect": (_i32, [_P, ct.POINTER(KStat), _u32, ct.POINTER(_u32)]),
     "svdw_plan_svd": (_i32, [_u32, _u32, _u32, _u32, ct.POINTER(SvdConfig), ct.POINTER(Counts)]),
 }

@@ -361,6 +361,7 @@ struct svdw_ctx {
         hipEvent_t ev;
     };
     std::vector<PreGemm> pre;               // GEMMs launched ahead on st2, in append order
+    std::vector<svdw_region> layout;        // every appended region of the current witness
     std::vector<uint64_t>* gemm_log = nullptr;   // dry run: offsets of honest_prover_mat_mul
     std::vector<hipEvent_t> deps;           // dependency events (no timing)
     size_t dep_next = 0;
@@ -427,6 +428,7 @@ static void own(svdw_ctx* c, uint32_t phase, bool lookup, uint64_t off, uint64_t
 }
 static void clear_streams(svdw_ctx* c) {
     c->owned.clear();
+    c->layout.clear();
     c->bits_pending = false;
     for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
     c->mbits.clear();
@@ -491,14 +493,28 @@ static void grow(svdw_ctx* c, Fr*& ptr, uint64_t used, uint64_t& cap, uint64_t n
     cap = ncap;
 }
 // Append n advice and nl lookup cells to a phase; returns their offsets.
+// Every cell region of a witness is appended here, in the reference's order;
+// the layout table (svdw_layout) records what each region is: the gadget /
+// function that appends it and its rows (row-parallel regions hold `rows`
+// equal runs of cells).
 static void append(svdw_ctx* c, uint32_t phase, uint64_t n, uint64_t nl, uint64_t* off,
-                   uint64_t* loff) {
+                   uint64_t* loff, const char* tag, uint64_t rows = 1) {
     REQUIRE(phase < 2, "phase must be 0 or 1");
     Stream& s = c->ph[phase];
     grow(c, s.adv, s.n, s.cap, s.n + n);
     grow(c, s.lk, s.nl, s.lcap, s.nl + nl);
     *off = s.n;
     if (loff) *loff = s.nl;
+    svdw_region r;
+    memset(&r, 0, sizeof r);
+    r.phase = phase;
+    r.off = s.n;
+    r.n = n;
+    r.loff = s.nl;
+    r.nl = nl;
+    r.rows = rows ? rows : 1;
+    snprintf(r.tag, sizeof r.tag, "%s", tag);
+    c->layout.push_back(r);
     s.n += n;
     s.nl += nl;
 }
@@ -613,7 +629,8 @@ static void stage_own(svdw_ctx* c, uint32_t phase, const PB& pb, uint32_t nelem,
 static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, uint32_t cols,
                           const char* tag, uint64_t* loff_out = nullptr) {
     uint64_t off = 0, loff = 0;
-    append(c, phase, (uint64_t)nelem * pb.a.C, (uint64_t)nelem * pb.a.L, &off, &loff);
+    append(c, phase, (uint64_t)nelem * pb.a.C, (uint64_t)nelem * pb.a.L, &off, &loff, tag,
+           cols ? nelem / cols : nelem);
     stage_own(c, phase, pb, nelem, cols, off, loff);
     if (loff_out) *loff_out = loff;
     stage_launch(c, phase, pb, nelem, cols, off, loff, tag);
@@ -635,7 +652,7 @@ static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, ui
     REQUIRE(rows >= 1 && cols >= 1, "ZkMatrix::new: empty matrix");
     REQUIRE(data || c->dry, "null data");
     uint64_t n = (uint64_t)rows * cols, off;
-    append(c, phase, n, 0, &off, nullptr);
+    append(c, phase, n, 0, &off, nullptr, "load", rows);
     if (!c->dry) {
         const double* src = data;
         if (!on_device) {
@@ -996,7 +1013,7 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
     REQUIRE(a.cols == b.rows, "honest_prover_mat_mul: a.num_col != b.num_rows");
     const uint32_t N = a.rows, M = b.cols;
     uint64_t off;
-    append(c, phase, (uint64_t)N * M, 0, &off, nullptr);
+    append(c, phase, (uint64_t)N * M, 0, &off, nullptr, "product", N);
     svdw_mat cs{phase, N, M, off, (int64_t)M, 1};
     if (c->gemm_log) c->gemm_log->push_back(off);
     uint64_t sr0 = 0, sr1 = N;                            // shard: rows of c_s computed here
@@ -1063,7 +1080,7 @@ static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, cons
                             WScaled w, int na) {
     const uint32_t R = a.rows, L = a.cols;
     uint64_t off;
-    append(c, phase, (uint64_t)R * (3ull * L + 1), 0, &off, nullptr);
+    append(c, phase, (uint64_t)R * (3ull * L + 1), 0, &off, nullptr, "scan", R);
     uint64_t r0 = 0, r1 = R;
     if (sharded(c)) {
         REQUIRE(c->scan_impl >= 3, "row sharding needs scan_impl >= 3");
@@ -1198,7 +1215,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     uint32_t dmax = 0;
     auto scan_append = [&](const svdw_mat& a) {
         uint64_t off;
-        append(c, phase, (uint64_t)a.rows * (3ull * a.cols + 1), 0, &off, nullptr);
+        append(c, phase, (uint64_t)a.rows * (3ull * a.cols + 1), 0, &off, nullptr, "scan", a.rows);
         return svdw_vec{phase, a.rows, off + 3ull * a.cols, (int64_t)(3ull * a.cols + 1)};
     };
     // pass 1: the cell layout, in the reference's order
@@ -1212,12 +1229,13 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         pl.emplace_back(c->LB);
         Plan& p = pl.back();
         p.one.cell(p.one.K(fr_from_u64(1)));                  // load_witness(F::ONE)
-        append(c, phase, p.one.a.C, 0, &p.one_off, &p.one_loff);
+        append(c, phase, p.one.a.C, 0, &p.one_off, &p.one_loff, "load_cell");
         stage_own(c, phase, p.one, 1, 1, p.one_off, p.one_loff);
         if (d > 1) {                                          // v_i = mul(v_{i-1}, init_rand)
             uint8_t prev = p.pows.load(0), cur = p.pows.load(1);
             p.pows.cell(p.pows.K(0)); p.pows.cell(prev); p.pows.cell(p.pows.K(gamma)); p.pows.cell(cur);
-            append(c, phase, (uint64_t)(d - 1) * p.pows.a.C, 0, &p.pows_off, &p.pows_loff);
+            append(c, phase, (uint64_t)(d - 1) * p.pows.a.C, 0, &p.pows_off, &p.pows_loff,
+                   "verify_mul_gamma_pows");
             stage_own(c, phase, p.pows, d - 1, 1, p.pows_off, p.pows_loff);
         }
         p.csv = scan_append(cs);
@@ -1235,7 +1253,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         uint8_t x = p.eq.load(0), y = p.eq.load(1);           // is_equal per row (result unused)
         p.eq.g_is_equal(x, y);
         append(c, phase, (uint64_t)a.rows * p.eq.a.C, (uint64_t)a.rows * p.eq.a.L, &p.eq_off,
-               &p.eq_loff);
+               &p.eq_loff, "verify_mul_is_equal", a.rows);
         stage_own(c, phase, p.eq, a.rows, 1, p.eq_off, p.eq_loff);
     }
     if (c->dry) return;
@@ -1902,6 +1920,13 @@ int svdw_set_shard(svdw_ctx* c, uint32_t rank, uint32_t world) {
         c->shard_rank = rank;
         c->shard_world = world;
         c->owned.clear();
+    });
+}
+int svdw_layout(const svdw_ctx* c, svdw_region* out, uint64_t cap, uint64_t* n) {
+    return guarded([&] {
+        REQUIRE(c && n, "null argument");
+        *n = c->layout.size();
+        for (uint64_t i = 0; i < cap && i < c->layout.size(); ++i) out[i] = c->layout[i];
     });
 }
 int svdw_shard_segments(const svdw_ctx* c, svdw_segment* out, uint64_t cap, uint64_t* n) {

@@ -19,7 +19,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import (Counts, DivScale, InputDims, KStat, Mat, Params, Payload, Segment, SvdConfig, SvdwError,
+from ._lib import (Counts, DivScale, InputDims, KStat, Mat, Params, Payload, Region, Segment, SvdConfig, SvdwError,
                    Vec, check, lib)
 
 P_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
@@ -139,6 +139,16 @@ class Context:
         buf = (Segment * max(n.value, 1))()
         check(lib().svdw_shard_segments(self._h, buf, n.value, ct.byref(n)))
         return [(s.phase, s.lookup, s.off, s.n) for s in buf[:n.value]]
+
+    def layout(self) -> list:
+        """Virtual layout of the last witness (svdw_layout): dicts with phase, off,
+        n, loff, nl, rows, tag for every appended region, in append order."""
+        n = ct.c_uint64()
+        check(lib().svdw_layout(self._h, None, 0, ct.byref(n)))
+        buf = (Region * max(n.value, 1))()
+        check(lib().svdw_layout(self._h, buf, n.value, ct.byref(n)))
+        return [{"phase": r.phase, "off": r.off, "n": r.n, "loff": r.loff, "nl": r.nl,
+                 "rows": r.rows, "tag": r.tag.decode()} for r in buf[:n.value]]
 
     def profile(self, on: bool = True, prefix: str = "") -> None:
         """Record HIP events around kernel launches (names starting with `prefix`)."""

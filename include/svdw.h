@@ -256,6 +256,20 @@ typedef struct {
     uint64_t off, n;    /* cells [off, off + n) */
 } svdw_segment;
 int svdw_set_shard(svdw_ctx* ctx, uint32_t rank, uint32_t world);
+/* Virtual layout of the last witness: every cell region in append order (the
+ * order halo2-base's Context receives them), tagged with the gadget / function
+ * that appended it. rows > 1: the region is `rows` equal runs of cells, one per
+ * row of a row-parallel stage (the unit of svdw_set_shard). Works on planning
+ * contexts. Up to cap regions into out; *n = total count. */
+typedef struct {
+    uint32_t phase;
+    uint32_t _pad;
+    uint64_t off, n;      /* advice cells [off, off + n) */
+    uint64_t loff, nl;    /* lookup cells [loff, loff + nl) */
+    uint64_t rows;
+    char tag[40];
+} svdw_region;
+int svdw_layout(const svdw_ctx* ctx, svdw_region* out, uint64_t cap, uint64_t* n);
 /* Up to cap segments of the last witness into out; *n = total count. */
 int svdw_shard_segments(const svdw_ctx* ctx, svdw_segment* out, uint64_t cap, uint64_t* n);
 

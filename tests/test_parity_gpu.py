@@ -338,3 +338,48 @@ def test_device_inputs_parity(gpu_ctx_factory, fused, N, M, P):
     hs.svd_witness(ctx, dm, du, dv, dd, g)
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
     _assert_streams(ctx, a0, l0, a1)
+
+
+# Regions of a witness that the C oracle's sampled mode (row_lim) truncates to
+# their first row_lim rows; every other region it computes in full.
+_ROW_LIMITED = {"check_mat_entries_bounded", "mat_times_diag_mat", "product", "check_mat_diff",
+                "scan", "verify_mul_is_equal"}
+
+
+@pytest.mark.parametrize("N,M,P,row_lim", [(1024, 1024, 63, 64), (512, 512, 32, 128),
+                                           (2048, 1024, 32, 24)])
+def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim):
+    """BASELINE config sizes (1024^2 P=63 = the bench workload, 512^2 P=32,
+    2048x1024 P=32): the GPU computes the whole witness; the C oracle computes
+    the first row_lim rows of every row-parallel region and all other regions
+    in full. Walking the engine's layout table (svdw_layout), every cell the
+    oracle computed must equal the GPU's cell at its full-witness offset: the
+    loads, d checks and gamma powers entirely, the first row_lim rows of every
+    bound / product / diff / scan / is_equal region."""
+    import halo2_svd041_amd as hs
+    m, u, d, v = gen_svd_input(N, M, seed=N + M + P)
+    g = gamma_for(N * M)
+    ctx = gpu_ctx_factory(P)
+    hs.svd_witness(ctx, m, u, v, d, g)
+    ctx.sync()
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g, row_lim=row_lim)
+    want = {(0, 0): a0, (0, 1): l0, (1, 0): a1}
+    pos = {k: 0 for k in want}
+    compared = 0
+    for r in ctx.layout():
+        ph, rows = r["phase"], r["rows"]
+        keep = min(rows, row_lim) if r["tag"] in _ROW_LIMITED else rows
+        for lk, off, n in ((0, r["off"], r["n"]), (1, r["loff"], r["nl"])):
+            if not n or (ph, lk) not in want:
+                continue
+            take = n // rows * keep
+            got = (ctx.lookups if lk else ctx.advice)(ph, off, take)
+            ref = want[(ph, lk)][pos[(ph, lk)]:pos[(ph, lk)] + take]
+            bad = np.nonzero(np.any(got != ref, axis=1))[0]
+            assert bad.size == 0, f"{r['tag']} phase {ph} {'lookup' if lk else 'advice'}: " \
+                                  f"{bad.size} of {take} cells differ, first at {bad[:6]}"
+            pos[(ph, lk)] += take
+            compared += take
+    for k, w in want.items():                      # the walk consumed every oracle cell
+        assert pos[k] == w.shape[0], (k, pos[k], w.shape[0])
+    assert compared > 0
