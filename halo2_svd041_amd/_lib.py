@@ -120,6 +120,10 @@ SIGNATURES = {
     "svdw_rescale_matrix": (_i32, [_P, ct.POINTER(Mat), ct.POINTER(DivScale), ct.POINTER(Mat)]),
     "svdw_zkvector_inner_product": (_i32, [_P, _u32, ct.POINTER(Vec), ct.POINTER(Vec),
                                            ct.POINTER(DivScale), ct.POINTER(Vec)]),
+    "svdw_zkvector_norm_square": (_i32, [_P, _u32, ct.POINTER(Vec), ct.POINTER(DivScale),
+                                         ct.POINTER(Vec)]),
+    "svdw_zkvector_dist_square": (_i32, [_P, _u32, ct.POINTER(Vec), ct.POINTER(Vec),
+                                         ct.POINTER(DivScale), ct.POINTER(Vec)]),
     "svdw_zkvector_mul": (_i32, [_P, _u32, ct.POINTER(Vec), ct.POINTER(Mat), ct.POINTER(DivScale),
                                  ct.POINTER(Vec)]),
     "svdw_honest_prover_mat_mul": (_i32, [_P, _u32, ct.POINTER(Mat), ct.POINTER(Mat),

@@ -787,6 +787,25 @@ static svdw_vec zkvector_inner_product(svdw_ctx* c, uint32_t phase, const svdw_v
     uint64_t off = run_stage(c, phase, pb, 1, 1, "signed_div_scale");
     return svdw_vec{phase, 1, off + C - 4, 1};
 }
+// ZkVector::_norm_square (src/matrix/mod.rs:112-119): self.inner_product(self).
+static svdw_vec zkvector_norm_square(svdw_ctx* c, uint32_t phase, const svdw_vec& self, DivScale d) {
+    return zkvector_inner_product(c, phase, self, self, d);
+}
+// ZkVector::_dist_square (src/matrix/mod.rs:135-148): diff_i = qsub(self_i, x_i)
+// (FixedPointChip041::qsub = gate.sub [ext, inferred as for entries_in_desc_order]:
+// cells [a - b, b, 1, a]), then diff._norm_square.
+static svdw_vec zkvector_dist_square(svdw_ctx* c, uint32_t phase, const svdw_vec& self,
+                                     const svdw_vec& x, DivScale d) {
+    REQUIRE(self.len == x.len && x.len >= 1, "ZkVector::_dist_square: length mismatch");
+    PB sb(c->LB);
+    sb.a.view[0] = view_of(c, mat_of_vec(self));
+    sb.a.view[1] = view_of(c, mat_of_vec(x));
+    uint8_t a = sb.load(0), b = sb.load(1);
+    sb.g_sub(a, b);
+    const uint64_t soff = run_stage(c, phase, sb, self.len, 1, "qsub");
+    const svdw_vec diff{phase, self.len, soff, 4};
+    return zkvector_norm_square(c, phase, diff, d);
+}
 // ZkVector::mul (src/matrix/mod.rs:169-182): inner_product with each row of a
 // (one row scan + one stage per row; config-1 plumbing, not the hot path).
 static svdw_vec zkvector_mul(svdw_ctx* c, uint32_t phase, const svdw_vec& self, const svdw_mat& a,
@@ -1811,6 +1830,29 @@ int svdw_zkvector_inner_product(svdw_ctx* c, uint32_t phase, const svdw_vec* sel
         const DivScale d = div_scale_of(c, cfg);
         pregrow(c, [&](svdw_ctx* y) { zkvector_inner_product(y, phase, *self, *x, d); });
         *out = zkvector_inner_product(c, phase, *self, *x, d);
+    });
+}
+int svdw_zkvector_norm_square(svdw_ctx* c, uint32_t phase, const svdw_vec* self,
+                              const svdw_div_scale* cfg, svdw_vec* out) {
+    return guarded([&] {
+        REQUIRE(c && self && out, "null argument");
+        REQUIRE(phase < 2, "phase must be 0 or 1");
+        check_vec(c, *self);
+        const DivScale d = div_scale_of(c, cfg);
+        pregrow(c, [&](svdw_ctx* y) { zkvector_norm_square(y, phase, *self, d); });
+        *out = zkvector_norm_square(c, phase, *self, d);
+    });
+}
+int svdw_zkvector_dist_square(svdw_ctx* c, uint32_t phase, const svdw_vec* self, const svdw_vec* x,
+                              const svdw_div_scale* cfg, svdw_vec* out) {
+    return guarded([&] {
+        REQUIRE(c && self && x && out, "null argument");
+        REQUIRE(phase < 2, "phase must be 0 or 1");
+        check_vec(c, *self);
+        check_vec(c, *x);
+        const DivScale d = div_scale_of(c, cfg);
+        pregrow(c, [&](svdw_ctx* y) { zkvector_dist_square(y, phase, *self, *x, d); });
+        *out = zkvector_dist_square(c, phase, *self, *x, d);
     });
 }
 int svdw_zkvector_mul(svdw_ctx* c, uint32_t phase, const svdw_vec* self, const svdw_mat* a,

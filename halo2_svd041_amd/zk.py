@@ -277,6 +277,23 @@ class ZkVector:
                                                 ct.byref(x.vec), ct.byref(cfg), ct.byref(out)))
         return ZkVector(self.ctx, out)
 
+    def _norm_square(self, phase: int = 0, shift_bits: int = 0, num_bits: int = 0) -> "ZkVector":
+        """ZkVector::_norm_square (src/matrix/mod.rs:112-119): 1-element vector."""
+        out = Vec()
+        cfg = DivScale(shift_bits, num_bits)
+        check(lib().svdw_zkvector_norm_square(self.ctx.handle, phase, ct.byref(self.vec),
+                                              ct.byref(cfg), ct.byref(out)))
+        return ZkVector(self.ctx, out)
+
+    def _dist_square(self, x: "ZkVector", phase: int = 0, shift_bits: int = 0,
+                     num_bits: int = 0) -> "ZkVector":
+        """ZkVector::_dist_square (src/matrix/mod.rs:135-148): 1-element vector."""
+        out = Vec()
+        cfg = DivScale(shift_bits, num_bits)
+        check(lib().svdw_zkvector_dist_square(self.ctx.handle, phase, ct.byref(self.vec),
+                                              ct.byref(x.vec), ct.byref(cfg), ct.byref(out)))
+        return ZkVector(self.ctx, out)
+
     def mul(self, a: ZkMatrix, phase: int = 0, shift_bits: int = 0,
             num_bits: int = 0) -> "ZkVector":
         """ZkVector::mul (src/matrix/mod.rs:169-182): a . self, rescaled."""

@@ -145,6 +145,14 @@ int svdw_rescale_matrix(svdw_ctx* ctx, const svdw_mat* c_s, const svdw_div_scale
  * then signed_div_scale; out = 1-element vector. */
 int svdw_zkvector_inner_product(svdw_ctx* ctx, uint32_t phase, const svdw_vec* self,
                                 const svdw_vec* x, const svdw_div_scale* cfg, svdw_vec* out);
+/* ZkVector::_norm_square (src/matrix/mod.rs:112-119) = inner_product(self, self);
+ * ZkVector::_dist_square (src/matrix/mod.rs:135-148): per-entry qsub (gate.sub)
+ * then _norm_square of the differences. norm / dist add qsqrt, whose chip
+ * (zk_fixed_point_chip, git HEAD) is not available: not provided. */
+int svdw_zkvector_norm_square(svdw_ctx* ctx, uint32_t phase, const svdw_vec* self,
+                              const svdw_div_scale* cfg, svdw_vec* out);
+int svdw_zkvector_dist_square(svdw_ctx* ctx, uint32_t phase, const svdw_vec* self,
+                              const svdw_vec* x, const svdw_div_scale* cfg, svdw_vec* out);
 /* ZkVector::mul (src/matrix/mod.rs:169-182): inner_product with every row of a. */
 int svdw_zkvector_mul(svdw_ctx* ctx, uint32_t phase, const svdw_vec* self, const svdw_mat* a,
                       const svdw_div_scale* cfg, svdw_vec* out);

@@ -416,6 +416,19 @@ def zkvector_inner_product(ctx, rc, vec, x, p: int, shift_bits: int = 0, num_bit
     return signed_div_scale(ctx, rc, res_s, p, shift_bits, num_bits)[0]
 
 
+def zkvector_norm_square(ctx, rc, vec, p: int, shift_bits: int = 0, num_bits: int = 0) -> AV:
+    """ZkVector::_norm_square (src/matrix/mod.rs:112-119): self.inner_product(self)."""
+    return zkvector_inner_product(ctx, rc, vec, vec, p, shift_bits, num_bits)
+
+
+def zkvector_dist_square(ctx, rc, vec, x, p: int, shift_bits: int = 0, num_bits: int = 0) -> AV:
+    """ZkVector::_dist_square (src/matrix/mod.rs:135-148): diff_i = fpchip.qsub(self_i,
+    x_i) [ext; gate.sub, as in entries_in_desc_order], then diff._norm_square."""
+    assert len(vec) == len(x)
+    diff = [gate_sub(ctx, E(a), E(b)) for a, b in zip(vec, x)]
+    return zkvector_norm_square(ctx, rc, diff, p, shift_bits, num_bits)
+
+
 def zkvector_mul(ctx, rc, vec, a, p: int, shift_bits: int = 0, num_bits: int = 0) -> List[AV]:
     """ZkVector::mul (src/matrix/mod.rs:169-182): inner_product with each row of a."""
     assert len(a[0]) == len(vec)

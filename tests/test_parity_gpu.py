@@ -383,3 +383,56 @@ def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim):
     for k, w in want.items():                      # the walk consumed every oracle cell
         assert pos[k] == w.shape[0], (k, pos[k], w.shape[0])
     assert compared > 0
+
+
+def _zkvector_inputs(N, M):
+    """src/matrix/test_matrix.rs:51-97 (test_zkvector's deterministic inputs, M = 4
+    there). Longer vectors repeat the first 8 entries' pattern (i -> i % 8) so
+    every product stays inside signed_div_scale's |x| < 2^(3P) domain."""
+    A = [[i + (j % 8) / 10.0 for j in range(M)] for i in range(N)]
+    k = [i % 8 for i in range(M)]
+    v1 = [(i + (i * i + 1) / 10.0) if i % 2 == 0 else (-i + (i * i + 1) / 10.0) for i in k]
+    v2 = [((1.0 + i ** 3) / 10.0) * (1 if i % 2 == 0 else -1) for i in k]
+    return A, v1, v2
+
+
+@pytest.mark.parametrize("N,M,P,LB", [(5, 4, 32, 12), (5, 64, 32, 19)])
+def test_zkvector_parity(gpu_ctx_factory, N, M, P, LB):
+    """BASELINE config 1 (test_zkvector, src/matrix/test_matrix.rs:39-198, with a
+    64-entry variant): inner_product, _norm_square, _dist_square and mul through
+    the ABI on the reference's inputs; every advice / lookup cell equals the
+    oracle's, its constraint checker passes, and the dequantised results are
+    within fixed-point error of the f64 values the reference prints (norm and
+    dist add qsqrt, not provided: chip source unavailable)."""
+    import halo2_svd041_amd as hs
+    import pyoracle as po
+    A, v1, v2 = _zkvector_inputs(N, M)
+    ctx = gpu_ctx_factory(P, LB)
+    za = hs.ZkMatrix.new(ctx, np.array(A))
+    z1, z2 = hs.ZkVector.new(ctx, np.array(v1)), hs.ZkVector.new(ctx, np.array(v2))
+    ip = z1.inner_product(z2)
+    ns1, ns2 = z1._norm_square(), z2._norm_square()
+    ds = z1._dist_square(z2)
+    u1, u2 = z1.mul(za), z2.mul(za)
+    o = po.Context(phase=0)
+    rc = po.RangeChip(LB)
+    oa = po.zkmatrix_new(o, P, A)
+    o1, o2 = po.zkvector_new(o, P, v1), po.zkvector_new(o, P, v2)
+    oip = po.zkvector_inner_product(o, rc, o1, o2, P)
+    ons1, ons2 = po.zkvector_norm_square(o, rc, o1, P), po.zkvector_norm_square(o, rc, o2, P)
+    ods = po.zkvector_dist_square(o, rc, o1, o2, P)
+    ou1, ou2 = po.zkvector_mul(o, rc, o1, oa, P), po.zkvector_mul(o, rc, o2, oa, P)
+    assert po.check_constraints(o, LB) == []
+    assert _ints(ctx.advice(0)) == o.advice
+    assert _ints(ctx.lookups(0)) == o.lookups
+    deq = lambda x: po.to_signed(x) / 2.0 ** P   # noqa: E731
+    for got, want, f64 in ((ip, oip, sum(a * b for a, b in zip(v1, v2))),
+                           (ns1, ons1, sum(a * a for a in v1)), (ns2, ons2, sum(b * b for b in v2)),
+                           (ds, ods, sum((a - b) ** 2 for a, b in zip(v1, v2)))):
+        assert _ints(got.values()) == [want.value]
+        assert abs(deq(want.value) - f64) <= 1e-6 * max(1.0, abs(f64))
+    for got, want, vec in ((u1, ou1, v1), (u2, ou2, v2)):
+        assert _ints(got.values()) == [e.value for e in want]
+        for i in range(N):
+            f64 = sum(A[i][j] * vec[j] for j in range(M))
+            assert abs(deq(want[i].value) - f64) <= 1e-6 * max(1.0, abs(f64))
