@@ -337,6 +337,7 @@ struct svdw_ctx {
     int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
     bool fused_quantize = true;             // "fused_quantize": m, u, v, d in one launch
+    bool d_checks_aside = true;             // "d_checks_aside": d checks on st2 behind the products
     int phase1_overlap = 1;                 // "phase1_overlap": 0 off, 1 on st2 behind the
                                             // GEMMs, 2 on st3 from quantization on
     bool prelaunched = false;               // this witness's products were queued on st2
@@ -1468,8 +1469,19 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         c->prelaunched = true;
     };
     if (c->prelaunch_at == 0) prelaunch();
-    entries_less_than(c, d, max_bits);
-    entries_in_desc_order(c, d, max_bits);
+    {
+        // The d checks (three latency-bound stages over r elements) depend on d
+        // only: with the products queued ahead they go behind them on st2, off
+        // the cell stream, which starts on the u / v bounds at once.
+        struct Swap {
+            svdw_ctx* c;
+            bool on;
+            Swap(svdw_ctx* cc, bool o) : c(cc), on(o) { if (on) std::swap(c->st, c->st2); }
+            ~Swap() { if (on) std::swap(c->st, c->st2); }
+        } sw(c, c->prelaunched && c->d_checks_aside);
+        entries_less_than(c, d, max_bits);
+        entries_in_desc_order(c, d, max_bits);
+    }
     if (c->prelaunch_at == 1) prelaunch();
     BigU unit = big_from_u128(((unsigned __int128)1 << P) + 1);
     check_mat_entries_bounded(c, u, unit);
@@ -2017,6 +2029,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                 hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
                 c->st2 = s;
             }
+        } else if (n == "d_checks_aside") {
+            c->d_checks_aside = value != 0;
         } else if (n == "fused_quantize") {
             c->fused_quantize = value != 0;
         } else if (n == "stage_priority") {

@@ -334,6 +334,41 @@ __device__ __forceinline__ void make_half(const SlotOp op, uint32_t h, uint32_t*
     *m = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// a * b mod p for canonical a, b. Fast path when both signed representatives
+// (x or x - p) are below 2^128 in magnitude -- quantized cells always are (the
+// u128 saturation of ZkMatrix::new), e.g. mat_times_diag_mat's u_ij * d_j:
+// an exact 4 x 4-word product (< 2^256 < 6p), a quotient-estimate reduction and
+// a conditional negation instead of two full Montgomery products.
+__device__ __forceinline__ Fr fr_mul_any(const Fr& a, const Fr& b) {
+    Fr na, nb;
+    sub256(na, fr_p(), a);                              // p - a
+    sub256(nb, fr_p(), b);
+    const bool sa = a.w[7] != 0, sb = b.w[7] != 0;     // top word set: the negative side
+    uint32_t ma[4], mb[4], hi = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        ma[i] = sa ? na.w[i] : a.w[i];
+        mb[i] = sb ? nb.w[i] : b.w[i];
+    }
+#pragma unroll
+    for (int i = 4; i < 8; ++i) hi |= (sa ? na.w[i] : a.w[i]) | (sb ? nb.w[i] : b.w[i]);
+    if (__any(hi != 0)) {                               // some lane out of range: generic
+        if (hi) return fr_mul(a, b);
+    }
+    uint32_t t[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[i + j] = mac32(ma[i], mb[j], t[i + j], c);
+        t[i + 4] = c;
+    }
+    const Fr r = reduce9(t);                            // < 2^256 -> mod p
+    return (sa != sb) ? fr_neg(r) : r;
+}
+
 // Phase A for one element: run the stage's micro-ops, values into myV (LDS).
 __device__ __forceinline__ void element_program(const StageArgs& a, uint32_t e, uint32_t* myV,
                                                 const uint32_t* sK, const MicroOp* sMo,
@@ -362,7 +397,7 @@ __device__ __forceinline__ void element_program(const StageArgs& a, uint32_t e, 
                 lds_put(dst, fr_sub(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
                 break;
             case MO_MUL:
-                lds_put(dst, fr_mul(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
+                lds_put(dst, fr_mul_any(lds_get(myV + op.a * VW), lds_get(myV + op.b * VW)));
                 break;
             case MO_LIMBSHL: {
                 const Fr sv = lds_get(myV + op.a * VW);
