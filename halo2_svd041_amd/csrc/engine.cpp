@@ -640,7 +640,19 @@ static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, u
 static svdw_vec put_cell(svdw_ctx* c, uint32_t phase, const Fr& v) {   // load_witness/load_constant
     PB pb(c->LB);
     pb.cell(pb.K(v));
-    uint64_t off = run_stage(c, phase, pb, 1, 1, "load_cell");
+    // Inside svd_witness (products queued ahead), a one-cell launch on the cell
+    // stream would wait for a free CU behind the scans on st2 (15-35 us on the
+    // critical path); it depends on nothing, so it goes on st2 itself.
+    const bool aside = c->prelaunched && c->d_checks_aside && !c->dry;
+    if (aside) std::swap(c->st, c->st2);
+    uint64_t off = 0;
+    try {
+        off = run_stage(c, phase, pb, 1, 1, "load_cell");
+    } catch (...) {
+        if (aside) std::swap(c->st, c->st2);
+        throw;
+    }
+    if (aside) std::swap(c->st, c->st2);
     return svdw_vec{phase, 1, off, 1};
 }
 
@@ -719,7 +731,8 @@ static void check_mat_entries_bounded(svdw_ctx* c, const svdw_mat& a, const BigU
 }
 // check_mat_diff on arbitrary views (a may be zero-padded, b may be diagonal).
 static void check_mat_diff_views(svdw_ctx* c, uint32_t phase, const DView& a, const DView& b,
-                                 uint32_t rows, uint32_t cols, const BigU& tol) {
+                                 uint32_t rows, uint32_t cols, const BigU& tol,
+                                 const Fr* diag_val = nullptr) {
     PB pb(c->LB);
     pb.a.view[0] = a;
     pb.a.view[1] = b;
@@ -729,17 +742,22 @@ static void check_mat_diff_views(svdw_ctx* c, uint32_t phase, const DView& a, co
     // pad / diag constants referenced by the views
     pb.a.view[0].pad_k = pb.kidx(fr_zero());
     pb.a.view[1].pad_k = pb.kidx(fr_zero());
+    if (diag_val) pb.a.view[1].diag_k = pb.kidx(*diag_val);
     run_stage(c, phase, pb, rows * cols, cols, "check_mat_diff");
 }
-static void check_mat_id(svdw_ctx* c, const svdw_mat& a, const svdw_vec& sid, const BigU& tol) {
+// sid_val: the scalar's value when the host knows it (svd_witness's q^2): the
+// stage then takes it as a constant and does not read sid's cell, which may
+// still be in flight on another stream.
+static void check_mat_id(svdw_ctx* c, const svdw_mat& a, const svdw_vec& sid, const BigU& tol,
+                         const Fr* sid_val = nullptr) {
     put_cell(c, a.phase, fr_zero());                      // let zero = ctx.load_constant(F::ZERO)
     DView b;
     memset(&b, 0, sizeof b);
-    b.mode = VIEW_DIAG;
-    b.ptr = c->dry ? nullptr : cellp(c, sid.phase, sid.off);
+    b.mode = sid_val ? VIEW_DIAGK : VIEW_DIAG;
+    b.ptr = c->dry || sid_val ? nullptr : cellp(c, sid.phase, sid.off);
     b.rows = a.rows;
     b.cols = a.cols;
-    check_mat_diff_views(c, a.phase, view_of(c, a), b, a.rows, a.cols, tol);
+    check_mat_diff_views(c, a.phase, view_of(c, a), b, a.rows, a.cols, tol, sid_val);
 }
 static svdw_mat mat_times_diag_mat(svdw_ctx* c, const svdw_mat& a, const svdw_vec& v) {
     REQUIRE(v.len <= a.cols, "mat_times_diag_mat: v longer than a's rows");
@@ -1509,11 +1527,12 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     BigU es = scale_err(err_svd, P), eu = scale_err(err_u, P);
     check_mat_diff_views(c, m.phase, udv, view_of(c, mvt), N, M, es);
     Fr q = pow2_fr(P);
-    svdw_vec q2 = put_cell(c, m.phase, fr_mul(q, q));
+    const Fr qq = fr_mul(q, q);
+    svdw_vec q2 = put_cell(c, m.phase, qq);
     svdw_mat uut = honest_prover_mat_mul(c, m.phase, u, ut, bu, bu);
-    check_mat_id(c, uut, q2, eu);
+    check_mat_id(c, uut, q2, eu, &qq);
     svdw_mat vvt = honest_prover_mat_mul(c, m.phase, v, vt, bv, bv);
-    check_mat_id(c, vvt, q2, eu);
+    check_mat_id(c, vvt, q2, eu, &qq);
     return svdw_svd_payload{ut, vt, mvt, uut, vvt};
 }
 static void check_svd_phase1(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u, const svdw_mat& v,
@@ -1620,6 +1639,9 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     }
     c->wait_before_cs.clear();
     if (p1_overlap) stream_dep(c, p1s, c->st);
+    // st2 also carries the d checks and single cells queued aside (and, with
+    // phase 1 on st3, nothing else joins it): join it too
+    if (c->prelaunched && !c->dry && !(p1_overlap && p1s == c->st2)) stream_dep(c, c->st2, c->st);
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
 }
 

@@ -386,7 +386,10 @@ __device__ __forceinline__ void element_program(const StageArgs& a, uint32_t e, 
                     lds_put(dst, pf1);
                 } else {
                     const DView vw = sVw[op.a];
-                    lds_put(dst, view_load(vw, lds_get(sK + vw.pad_k * VW), i, j));
+                    if (vw.mode == VIEW_DIAGK)
+                        lds_put(dst, lds_get(sK + (i == j ? vw.diag_k : vw.pad_k) * VW));
+                    else
+                        lds_put(dst, view_load(vw, lds_get(sK + vw.pad_k * VW), i, j));
                 }
                 break;
             }

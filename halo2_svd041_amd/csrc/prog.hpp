@@ -24,7 +24,9 @@ namespace svdw {
 // Matrix view over canonical Fr cells: X(i, j) = ptr[i*rs + j*cs] for
 // i < rows && j < cols, else K[pad_k]. mode DIAG: X(i,j) = i==j ? *ptr : K[pad_k]
 // (check_mat_id's implicit scalar_id * Id matrix, src/matrix/mod.rs:461-483).
-enum : uint32_t { VIEW_STRIDED = 0, VIEW_DIAG = 1 };
+// mode DIAGK: X(i,j) = i==j ? K[diag_k] : K[pad_k] (the same matrix when the
+// diagonal scalar is a constant the host knows: no read of its cell).
+enum : uint32_t { VIEW_STRIDED = 0, VIEW_DIAG = 1, VIEW_DIAGK = 2 };
 struct DView {
     const Fr* ptr;
     int64_t rs, cs;
