@@ -1452,7 +1452,10 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         svdw_mat ut = u, vt = v;
         std::swap(ut.rows, ut.cols); std::swap(ut.rs, ut.cs);
         std::swap(vt.rows, vt.cols); std::swap(vt.rs, vt.cs);
-        stream_dep(c, c->st, c->st2);                      // loads of m, u, v done
+        // loads of m, u, v done: the quantization event when svd_witness recorded
+        // one (the cell stream may already hold later stages), else st's position
+        if (c->bits_pending) hipck(hipStreamWaitEvent(c->st2, c->ev_bits, 0), "hipStreamWaitEvent");
+        else stream_dep(c, c->st, c->st2);
         const svdw_mat A[3] = {m, u, v}, B[3] = {vt, ut, vt};
         const uint32_t ba[3] = {known_bits[0], known_bits[1], known_bits[2]};
         const uint32_t bb[3] = {known_bits[2], known_bits[1], known_bits[2]};
@@ -1496,7 +1499,8 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
             bool on;
             Swap(svdw_ctx* cc, bool o) : c(cc), on(o) { if (on) std::swap(c->st, c->st2); }
             ~Swap() { if (on) std::swap(c->st, c->st2); }
-        } sw(c, c->prelaunched && c->d_checks_aside);
+        } sw(c, c->d_checks_aside && c->overlap && known_bits && !c->dry && c->bits_pending);
+        if (sw.on) hipck(hipStreamWaitEvent(c->st, c->ev_bits, 0), "hipStreamWaitEvent");  // d loaded
         entries_less_than(c, d, max_bits);
         entries_in_desc_order(c, d, max_bits);
     }
