@@ -64,6 +64,12 @@ class Segment(ct.Structure):
                 ("n", ct.c_uint64)]
 
 
+class CheckResult(ct.Structure):
+    _fields_ = [("gates_checked", ct.c_uint64), ("gate_failures", ct.c_uint64),
+                ("lookups_checked", ct.c_uint64), ("lookup_failures", ct.c_uint64),
+                ("copies_checked", ct.c_uint64), ("copy_failures", ct.c_uint64)]
+
+
 class Region(ct.Structure):
     _fields_ = [("phase", ct.c_uint32), ("_pad", ct.c_uint32), ("off", ct.c_uint64),
                 ("n", ct.c_uint64), ("loff", ct.c_uint64), ("nl", ct.c_uint64),
@@ -146,6 +152,7 @@ SIGNATURES = {
     "svdw_parse_svd_input": (_i32, [ct.c_char_p, _u64, _i32, ct.POINTER(InputDims), _P, _P, _P, _P]),
     "svdw_shard_segments": (_i32, [_P, ct.POINTER(Segment), _u64, _u64p]),
     "svdw_layout": (_i32, [_P, ct.POINTER(Region), _u64, _u64p]),
+    "svdw_check_gates": (_i32, [_P, ct.POINTER(CheckResult)]),
     "svdw_profile_collect": (_i32, [_P, ct.POINTER(KStat), _u32, ct.POINTER(_u32)]),
     "svdw_plan_svd": (_i32, [_u32, _u32, _u32, _u32, ct.POINTER(SvdConfig), ct.POINTER(Counts)]),
 }

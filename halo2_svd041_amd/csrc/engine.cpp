@@ -126,7 +126,25 @@ static Fr fr_from_words(const uint64_t w[4]) { return big_to_fr(big_from_words(w
 struct PB {
     StageArgs a;
     uint32_t lb;
-    explicit PB(uint32_t lookup_bits) : lb(lookup_bits) { memset(&a, 0, sizeof(a)); }
+    // What MockProver checks on an element's C cells (svdw_check_gates), as
+    // check words (kernels.hpp CHK_*): the offsets where halo2-base's
+    // assign_region enables a basic gate a + b*c = d, and the copy constraints
+    // -- a value's later cells against its first cell, a loaded value's first
+    // cell against its source cell (view), range_check's last running sum
+    // against the checked value (RangeChip::range_check's constrain_equal).
+    std::vector<uint32_t> chk;
+    int8_t vload[kMaxV];      // view a value was loaded from (-1: computed)
+    int16_t fullc[kMaxV];     // first cell holding the value in full (-1: none)
+    void gate(uint32_t at) { chk.push_back(chk_gate(at)); }
+    void copy_of(uint8_t v, uint32_t at) {    // cell `at` must equal value v's cell
+        if (fullc[v] >= 0) chk.push_back(chk_copy((uint32_t)fullc[v], at));
+        else if (vload[v] >= 0) chk.push_back(chk_view((uint32_t)vload[v], at));
+    }
+    explicit PB(uint32_t lookup_bits) : lb(lookup_bits) {
+        memset(&a, 0, sizeof(a));
+        memset(vload, -1, sizeof vload);
+        for (auto& f : fullc) f = -1;
+    }
 
     uint8_t newv() {
         if (a.nv >= (uint32_t)kMaxV) fail(SVDW_ERANGE, "stage needs too many element values");
@@ -151,7 +169,12 @@ struct PB {
     }
     void cell(uint8_t src, uint32_t lo = 0, uint32_t nbits = 0) {
         if (a.C >= (uint32_t)kMaxAdv) fail(SVDW_ERANGE, "stage has too many cells per element (raise lookup_bits)");
-        a.adv[a.C++] = slot(src, lo, nbits);
+        const SlotOp s = slot(src, lo, nbits);
+        if (src < KSRC && s.lo == 0 && s.nbits == 0) {      // the value itself: a copy or its first cell
+            copy_of(src, a.C);
+            if (fullc[src] < 0) fullc[src] = (int16_t)a.C;
+        }
+        a.adv[a.C++] = s;
     }
     void look(uint8_t src, uint32_t lo = 0, uint32_t nbits = 0) {
         if (a.L >= (uint32_t)kMaxLk) fail(SVDW_ERANGE, "stage has too many lookups per element (raise lookup_bits)");
@@ -161,6 +184,7 @@ struct PB {
     uint8_t load(int view_idx) {
         uint8_t v = newv();
         op(MO_LOAD, v, (uint8_t)view_idx, 0);
+        vload[v] = (int8_t)view_idx;
         return v;
     }
     uint8_t addk(uint8_t x, const Fr& k) {
@@ -171,23 +195,27 @@ struct PB {
     // --- GateChip
     uint8_t g_add_k(uint8_t x, const Fr& k) {       // add(x, Constant(k)): [x, k, 1, x+k]
         uint8_t t = addk(x, k);
+        gate(a.C);
         cell(x); cell(K(k)); cell(K(1)); cell(t);
         return t;
     }
     uint8_t g_sub_k(uint8_t x, const Fr& k) {       // sub(x, Constant(k)): [x-k, k, 1, x]
         uint8_t d = addk(x, fr_neg(k));
+        gate(a.C);
         cell(d); cell(K(k)); cell(K(1)); cell(x);
         return d;
     }
     uint8_t g_sub(uint8_t x, uint8_t y) {           // sub: [x-y, y, 1, x]
         uint8_t d = newv();
         op(MO_SUB, d, x, y);
+        gate(a.C);
         cell(d); cell(y); cell(K(1)); cell(x);
         return d;
     }
     uint8_t g_mul(uint8_t x, uint8_t y) {           // mul: [0, x, y, x*y]
         uint8_t m = newv();
         op(MO_MUL, m, x, y);
+        gate(a.C);
         cell(K(0)); cell(x); cell(y); cell(m);
         return m;
     }
@@ -197,6 +225,8 @@ struct PB {
         uint8_t inv = newv();
         (void)inv;
         op(MO_ISZERO, z, d, 0);
+        gate(a.C);
+        gate(a.C + 4);
         cell(z); cell(d); cell((uint8_t)(z + 1)); cell(K(1));
         cell(K(0)); cell(d); cell(z); cell(K(0));
     }
@@ -218,15 +248,18 @@ struct PB {
                 if (i == 0) {
                     cell(src, slo, snb);
                 } else {
+                    gate(a.C - 1);                  // [s_(i-1), l_i, 2^(i lb), s_i]
                     cell(src, slo, snb);
                     cell(K(pow2_fr(lo)));
                     cell(v, 0, (i + 1) * lb);    // running sum = v mod 2^((i+1) lb)
+                    if (i + 1 == n && n * lb < 256) copy_of(v, a.C - 1);   // constrain_equal(a, sum)
                 }
                 look(src, slo, snb);
                 lsrc = src; llo = slo; lnb = snb;
             }
         }
         if (rem == 1) {                             // assert_bit: [0, l, l, l]
+            gate(a.C);
             cell(K(0)); cell(lsrc, llo, lnb); cell(lsrc, llo, lnb); cell(lsrc, llo, lnb);
         } else if (rem > 1) {                       // mul(last, 2^(lb-rem)), looked up
             const uint32_t sh = lb - rem;
@@ -234,6 +267,7 @@ struct PB {
             if (n == 1) op(MO_FDBL, m, v, (uint8_t)sh);
             else if ((n - 1) * lb >= 256) op(MO_ADDK, m, v, kidx(fr_zero()));   // unreachable in practice
             else op(MO_LIMBSHL, m, v, (uint8_t)sh, (uint16_t)((n - 1) * lb), (uint16_t)lb);
+            gate(a.C);
             cell(K(0)); cell(lsrc, llo, lnb); cell(K(pow2_fr(sh))); cell(m);
             look(m);
         }
@@ -243,6 +277,8 @@ struct PB {
         Fr pw = pow2_fr(bits), bf = big_to_fr(b);
         uint8_t t3 = addk(x, pw);                  // a + 2^bits
         uint8_t t2 = addk(t3, fr_neg(bf));         // a + 2^bits - b
+        gate(a.C);
+        gate(a.C + 3);
         cell(t2); cell(K(bf)); cell(K(1)); cell(t3); cell(K(fr_neg(pw))); cell(K(1)); cell(x);
         range_check(t2, bits);
     }
@@ -258,6 +294,7 @@ struct PB {
         op(MO_SHR, q, t, 0, (uint16_t)p);
         uint8_t r = newv();
         op(MO_LIMBSHL, r, t, 0, 0, (uint16_t)p);
+        gate(a.C);
         cell(r); cell(K(pow2_fr(p))); cell(q); cell(t);
         check_big_less_than_safe(q, big_add_u32(big_pow2(nb - p), 1));
         check_big_less_than_safe(r, big_pow2(p));
@@ -297,7 +334,7 @@ struct svdw_ctx {
     hipStream_t st = nullptr;
     uint32_t P = 32, LB = 19;
     Stream ph[2];
-    DBuf f64in, digA, digB, digC, w1c, w1m, w2c, w2m, bits, gpc, gpm, crtR, gbits;
+    DBuf f64in, digA, digB, digC, w1c, w1m, w2c, w2m, bits, gpc, gpm, crtR, gbits, chk, chkg;
     DBuf wbc[kMaxScanJobs], wbs[kMaxScanJobs];   // b.v per batched verify_mul (canonical, scaled)
     // gamma^j cache (canonical gpc / Montgomery gpm), shared by verify_mul calls
     Fr gp_gamma{};
@@ -363,6 +400,9 @@ struct svdw_ctx {
     };
     std::vector<PreGemm> pre;               // GEMMs launched ahead on st2, in append order
     std::vector<svdw_region> layout;        // every appended region of the current witness
+    // per region: gate offsets within one element's cells and cells per element
+    // (program regions; empty otherwise; svdw_check_gates)
+    std::vector<RegionChecks> layout_chk;
     std::vector<uint64_t>* gemm_log = nullptr;   // dry run: offsets of honest_prover_mat_mul
     std::vector<hipEvent_t> deps;           // dependency events (no timing)
     size_t dep_next = 0;
@@ -430,6 +470,7 @@ static void own(svdw_ctx* c, uint32_t phase, bool lookup, uint64_t off, uint64_t
 static void clear_streams(svdw_ctx* c) {
     c->owned.clear();
     c->layout.clear();
+    c->layout_chk.clear();
     c->bits_pending = false;
     for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
     c->mbits.clear();
@@ -516,6 +557,7 @@ static void append(svdw_ctx* c, uint32_t phase, uint64_t n, uint64_t nl, uint64_
     r.rows = rows ? rows : 1;
     snprintf(r.tag, sizeof r.tag, "%s", tag);
     c->layout.push_back(r);
+    c->layout_chk.emplace_back();
     s.n += n;
     s.nl += nl;
 }
@@ -627,11 +669,40 @@ static void stage_own(svdw_ctx* c, uint32_t phase, const PB& pb, uint32_t nelem,
     own(c, phase, false, off + r0 * cw * pb.a.C, (r1 - r0) * cw * pb.a.C);
     own(c, phase, true, loff + r0 * cw * pb.a.L, (r1 - r0) * cw * pb.a.L);
 }
+// the last appended region is `nelem` copies of pb's program: record its gates
+// (views: the source cells as (phase, offset), strided views into the cell
+// streams only -- the streams may move before the check)
+static void note_gates(svdw_ctx* c, const PB& pb, uint32_t cols = 1, size_t reg = ~size_t(0)) {
+    RegionChecks& r = reg == ~size_t(0) ? c->layout_chk.back() : c->layout_chk.at(reg);
+    r.words = pb.chk;
+    r.unit = pb.a.C;
+    r.cols = cols ? cols : 1;
+    for (int k = 0; k < kMaxViews; ++k) {
+        const DView& v = pb.a.view[k];
+        RegionChecks::Src& s = r.src[k];
+        s.phase = -1;
+        if (!v.ptr || v.mode != VIEW_STRIDED) continue;
+        for (int p = 0; p < 2; ++p) {
+            const Fr* base = c->ph[p].adv;
+            if (base && v.ptr >= base && v.ptr < base + c->ph[p].n) {
+                s = RegionChecks::Src{p, (uint64_t)(v.ptr - base), v.rs, v.cs, v.rows, v.cols};
+                break;
+            }
+        }
+    }
+    // a view word whose source is not in the streams (host-known constants,
+    // the gamma powers buffer) is dropped
+    std::vector<uint32_t> keep;
+    for (uint32_t w : r.words)
+        if (chk_kind(w) != CHK_VIEW || r.src[chk_a(w)].phase >= 0) keep.push_back(w);
+    r.words.swap(keep);
+}
 static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, uint32_t cols,
                           const char* tag, uint64_t* loff_out = nullptr) {
     uint64_t off = 0, loff = 0;
     append(c, phase, (uint64_t)nelem * pb.a.C, (uint64_t)nelem * pb.a.L, &off, &loff, tag,
            cols ? nelem / cols : nelem);
+    note_gates(c, pb, cols);
     stage_own(c, phase, pb, nelem, cols, off, loff);
     if (loff_out) *loff_out = loff;
     stage_launch(c, phase, pb, nelem, cols, off, loff, tag);
@@ -1245,6 +1316,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     struct Plan {
         PB one, pows, eq;
         uint64_t one_off = 0, one_loff = 0, pows_off = 0, pows_loff = 0, eq_off = 0, eq_loff = 0;
+        size_t eq_reg = 0;                // its layout region (views noted at launch)
         svdw_vec csv{}, bv{}, abv{};
         explicit Plan(uint32_t lb) : one(lb), pows(lb), eq(lb) {}
     };
@@ -1271,9 +1343,11 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         stage_own(c, phase, p.one, 1, 1, p.one_off, p.one_loff);
         if (d > 1) {                                          // v_i = mul(v_{i-1}, init_rand)
             uint8_t prev = p.pows.load(0), cur = p.pows.load(1);
+            p.pows.gate(0);                               // mul(v_(i-1), init_rand)
             p.pows.cell(p.pows.K(0)); p.pows.cell(prev); p.pows.cell(p.pows.K(gamma)); p.pows.cell(cur);
             append(c, phase, (uint64_t)(d - 1) * p.pows.a.C, 0, &p.pows_off, &p.pows_loff,
                    "verify_mul_gamma_pows");
+            note_gates(c, p.pows);
             stage_own(c, phase, p.pows, d - 1, 1, p.pows_off, p.pows_loff);
         }
         p.csv = scan_append(cs);
@@ -1292,6 +1366,8 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         p.eq.g_is_equal(x, y);
         append(c, phase, (uint64_t)a.rows * p.eq.a.C, (uint64_t)a.rows * p.eq.a.L, &p.eq_off,
                &p.eq_loff, "verify_mul_is_equal", a.rows);
+        note_gates(c, p.eq);
+        p.eq_reg = c->layout_chk.size() - 1;
         stage_own(c, phase, p.eq, a.rows, 1, p.eq_off, p.eq_loff);
     }
     if (c->dry) return;
@@ -1385,6 +1461,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         Plan& p = pl[i];
         p.eq.a.view[0] = view_of(c, mat_of_vec(p.csv));
         p.eq.a.view[1] = view_of(c, mat_of_vec(p.abv));
+        note_gates(c, p.eq, 1, p.eq_reg);
         stage_launch(c, phase, p.eq, vm[i].a.rows, 1, p.eq_off, p.eq_loff, "verify_mul_is_equal");
     }
 }
@@ -1691,7 +1768,7 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             (void)hipStreamSynchronize(c->st2);
             if (c->st3) (void)hipStreamSynchronize(c->st3);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
-            for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->w1c, &c->w1m, &c->w2c, &c->w2m,
+            for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->w1c, &c->w1m, &c->w2c, &c->w2m,
                             &c->bits, &c->gpc, &c->gpm, &c->crtR, &c->gbits})
                 if (b->p) (void)hipFree(b->p);
             for (auto& b : c->gps) if (b.p) (void)hipFree(b.p);
@@ -2000,6 +2077,59 @@ int svdw_set_shard(svdw_ctx* c, uint32_t rank, uint32_t world) {
         c->shard_rank = rank;
         c->shard_world = world;
         c->owned.clear();
+    });
+}
+int svdw_check_gates(svdw_ctx* c, svdw_check_result* out) {
+    return guarded([&] {
+        REQUIRE(c && out, "null argument");
+        REQUIRE(!c->dry, "svdw_check_gates needs a device context");
+        REQUIRE(!sharded(c), "svdw_check_gates: the witness of a sharded context is partial");
+        sync(c);
+        memset(out, 0, sizeof *out);
+        ensure_buf(c, c->chk, 6 * sizeof(unsigned long long));
+        unsigned long long* cnt = (unsigned long long*)c->chk.p;
+        hipck(hipMemsetAsync(cnt, 0, 6 * sizeof(unsigned long long), c->st), "hipMemsetAsync");
+        std::vector<uint32_t> scan_w;
+        for (size_t k = 0; k < c->layout.size(); ++k) {
+            const svdw_region& r = c->layout[k];
+            const RegionChecks& rc = c->layout_chk[k];
+            if (r.nl)
+                hipck(launch_check_lookups(c->ph[r.phase].lk + r.loff, r.nl, c->LB, cnt + 2, c->st),
+                      "k_check_lookups");
+            const std::vector<uint32_t>* w = &rc.words;
+            uint64_t unit = rc.unit;
+            uint32_t cols = rc.cols;
+            if (!strcmp(r.tag, "scan") && r.rows) {         // rows [0, a0, v0, s0, a1, v1, s1, ...]
+                unit = r.n / r.rows;
+                cols = 1;
+                scan_w.clear();
+                for (uint64_t q = 0; q + 3 < unit; q += 3) scan_w.push_back(chk_gate((uint32_t)q));
+                w = &scan_w;
+            }
+            if (w->empty() || !unit || !r.n) continue;
+            ChkView v[kMaxViews];
+            for (int q = 0; q < kMaxViews; ++q) {
+                const RegionChecks::Src& s = rc.src[q];
+                v[q] = s.phase < 0 ? ChkView{nullptr, 0, 0, 0, 0}
+                                   : ChkView{c->ph[s.phase].adv + s.off, s.rs, s.cs, s.rows, s.cols};
+            }
+            ensure_buf(c, c->chkg, w->size() * sizeof(uint32_t));
+            hipck(hipMemcpyAsync(c->chkg.p, w->data(), w->size() * sizeof(uint32_t),
+                                 hipMemcpyHostToDevice, c->st), "H2D");
+            hipck(launch_check_cells(c->ph[r.phase].adv + r.off, r.n / unit, (uint32_t)unit, cols,
+                                     (const uint32_t*)c->chkg.p, (uint32_t)w->size(), v[0], v[1], cnt,
+                                     c->st), "k_check_cells");
+            hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");   // chkg is reused
+        }
+        unsigned long long h[6];
+        hipck(hipMemcpyAsync(h, cnt, sizeof h, hipMemcpyDeviceToHost, c->st), "D2H");
+        hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
+        out->gates_checked = h[0];
+        out->gate_failures = h[1];
+        out->lookups_checked = h[2];
+        out->lookup_failures = h[3];
+        out->copies_checked = h[4];
+        out->copy_failures = h[5];
     });
 }
 int svdw_layout(const svdw_ctx* c, svdw_region* out, uint64_t cap, uint64_t* n) {

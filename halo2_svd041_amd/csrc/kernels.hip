@@ -1392,6 +1392,82 @@ hipError_t launch_gemm_mont(const DView& A, const DView& B, uint32_t N, uint32_t
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------- checker
+// svdw_check_gates: the MockProver-style constraint check of a generated
+// witness on the device (halo2-base's basic gate q * (a + b*c - d) = 0 at every
+// enabled offset, and the lookup table [0, 2^lb)); copy constraints are not
+// checked here. One thread per (unit, gate); counts via one atomic per wave.
+__device__ __forceinline__ void wave_count(bool valid, bool bad, unsigned long long* c) {
+    const uint64_t nv = __popcll(__ballot(valid)), nb = __popcll(__ballot(bad));
+    if ((threadIdx.x & 63) == 0) {
+        if (nv) atomicAdd(c, (unsigned long long)nv);
+        if (nb) atomicAdd(c + 1, (unsigned long long)nb);
+    }
+}
+__global__ __launch_bounds__(256) void k_check_cells(const Fr* __restrict__ adv, uint64_t nunits,
+                                                     uint32_t unit, uint32_t cols,
+                                                     const uint32_t* __restrict__ words, uint32_t nw,
+                                                     ChkView v0, ChkView v1, unsigned long long* cnt) {
+    const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool gate = false, gbad = false, copy = false, cbad = false;
+    if (idx < nunits * nw) {
+        const uint64_t u = idx / nw;
+        const uint32_t w = words[idx - u * nw];
+        const Fr* q = adv + u * unit;
+        if (chk_kind(w) == CHK_GATE) {
+            const Fr* g = q + w;
+            gate = true;
+            gbad = !fr_eq(fr_add(ld_fr(g), fr_mul(ld_fr(g + 1), ld_fr(g + 2))), ld_fr(g + 3));
+        } else if (chk_kind(w) == CHK_COPY) {
+            copy = true;
+            cbad = !fr_eq(ld_fr(q + chk_a(w)), ld_fr(q + chk_b(w)));
+        } else {
+            const ChkView v = chk_a(w) ? v1 : v0;
+            const uint64_t i = u / cols, j = u - i * cols;
+            if (v.ptr && i < v.rows && j < v.cols) {
+                copy = true;
+                cbad = !fr_eq(ld_fr(v.ptr + (int64_t)i * v.rs + (int64_t)j * v.cs), ld_fr(q + chk_b(w)));
+            }
+        }
+    }
+    wave_count(gate, gbad, cnt);
+    wave_count(copy, cbad, cnt + 4);
+}
+hipError_t launch_check_cells(const Fr* adv, uint64_t nunits, uint32_t unit, uint32_t cols,
+                              const uint32_t* words, uint32_t nw, ChkView v0, ChkView v1,
+                              unsigned long long* cnt, hipStream_t st) {
+    const uint64_t n = nunits * nw;
+    if (!n) return hipSuccess;
+    if ((n + 255) / 256 > 0x7fffffffull || !cols) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_check_cells, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, adv,
+                       nunits, unit, cols, words, nw, v0, v1, cnt);
+    return hipGetLastError();
+}
+__global__ __launch_bounds__(256) void k_check_lookups(const Fr* __restrict__ lk, uint64_t n,
+                                                       uint32_t lb, unsigned long long* cnt) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool valid = i < n;
+    bool bad = false;
+    if (valid) {
+        const Fr v = ld_fr(lk + i);
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            const int keep = (int)lb - 32 * w;
+            const uint32_t m = keep >= 32 ? 0u : (keep <= 0 ? 0xffffffffu : ~((1u << keep) - 1u));
+            bad |= (v.w[w] & m) != 0;
+        }
+    }
+    wave_count(valid, bad, cnt);
+}
+hipError_t launch_check_lookups(const Fr* lk, uint64_t n, uint32_t lb, unsigned long long* cnt,
+                                hipStream_t st) {
+    if (!n) return hipSuccess;
+    if ((n + 255) / 256 > 0x7fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_check_lookups, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, lk, n,
+                       lb, cnt);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------ vectors
 __global__ void k_vec_prep(const DView w, uint32_t L, Fr* wc, Fr* ws, Fr* wsn, const Fr f) {
     uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;

@@ -45,6 +45,42 @@ struct QuantSegs {
     uint32_t nseg;
 };
 hipError_t launch_quantize_multi(const QuantSegs& q, int precision_bits, hipStream_t st);
+// Witness checker (svdw_check_gates). A region is `nunits` repetitions of a
+// `unit`-cell block (element u = row u / cols, column u % cols); check words:
+//   CHK_GATE g      a + b*c = d on cells g..g+3
+//   CHK_COPY i, j   cell i == cell j
+//   CHK_VIEW k, j   view k's cell of the element == cell j (not counted outside the view)
+// cnt[0..1] += gates checked / failed, cnt[4..5] += copies checked / failed;
+// lookups: every cell < 2^lb -> cnt[0] += n, cnt[1] += failed.
+enum : uint32_t { CHK_GATE = 0, CHK_COPY = 1, CHK_VIEW = 2 };
+constexpr uint32_t chk_gate(uint32_t g) { return g; }
+constexpr uint32_t chk_copy(uint32_t i, uint32_t j) { return (CHK_COPY << 30) | (i << 15) | j; }
+constexpr uint32_t chk_view(uint32_t k, uint32_t j) { return (CHK_VIEW << 30) | (k << 15) | j; }
+constexpr uint32_t chk_kind(uint32_t w) { return w >> 30; }
+constexpr uint32_t chk_a(uint32_t w) { return (w >> 15) & 0x7fff; }
+constexpr uint32_t chk_b(uint32_t w) { return w & 0x7fff; }
+struct ChkView {
+    const Fr* ptr;   // null: no view
+    int64_t rs, cs;
+    uint32_t rows, cols;
+};
+// the checks of one layout region (engine side)
+struct RegionChecks {
+    struct Src {
+        int phase;     // -1: none
+        uint64_t off;
+        int64_t rs, cs;
+        uint32_t rows, cols;
+    };
+    std::vector<uint32_t> words;
+    uint32_t unit = 0, cols = 1;
+    Src src[kMaxViews] = {{-1, 0, 0, 0, 0, 0}, {-1, 0, 0, 0, 0, 0}};
+};
+hipError_t launch_check_cells(const Fr* adv, uint64_t nunits, uint32_t unit, uint32_t cols,
+                              const uint32_t* words, uint32_t nw, ChkView v0, ChkView v1,
+                              unsigned long long* cnt, hipStream_t st);
+hipError_t launch_check_lookups(const Fr* lk, uint64_t n, uint32_t lb, unsigned long long* cnt,
+                                hipStream_t st);
 static constexpr int kMaxBitSegs = 8;
 struct BitSegs {
     uint32_t begin[kMaxBitSegs];

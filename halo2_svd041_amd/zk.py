@@ -19,7 +19,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import (Counts, DivScale, InputDims, KStat, Mat, Params, Payload, Region, Segment, SvdConfig, SvdwError,
+from ._lib import (CheckResult, Counts, DivScale, InputDims, KStat, Mat, Params, Payload, Region, Segment, SvdConfig, SvdwError,
                    Vec, check, lib)
 
 P_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
@@ -149,6 +149,14 @@ class Context:
         check(lib().svdw_layout(self._h, buf, n.value, ct.byref(n)))
         return [{"phase": r.phase, "off": r.off, "n": r.n, "loff": r.loff, "nl": r.nl,
                  "rows": r.rows, "tag": r.tag.decode()} for r in buf[:n.value]]
+
+    def check_gates(self) -> dict:
+        """Device constraint check of the last witness (svdw_check_gates)."""
+        r = CheckResult()
+        check(lib().svdw_check_gates(self._h, ct.byref(r)))
+        return {"gates_checked": r.gates_checked, "gate_failures": r.gate_failures,
+                "lookups_checked": r.lookups_checked, "lookup_failures": r.lookup_failures,
+                "copies_checked": r.copies_checked, "copy_failures": r.copy_failures}
 
     def profile(self, on: bool = True, prefix: str = "") -> None:
         """Record HIP events around kernel launches (names starting with `prefix`)."""

@@ -278,6 +278,23 @@ typedef struct {
     char tag[40];
 } svdw_region;
 int svdw_layout(const svdw_ctx* ctx, svdw_region* out, uint64_t cap, uint64_t* n);
+
+/* Constraint check of the last witness on the device, the MockProver-style
+ * verification of an (unsharded) context: every halo2-base basic gate
+ * a + b*c = d at the offsets the reference's gadgets enable (assign_region's
+ * gate offsets; the row-scan inner products), every lookup cell against the
+ * [0, 2^lookup_bits) table, and the copy constraints of the gadget blocks: a
+ * value's repeated cells, a loaded operand against its source cell, and
+ * range_check's last running sum against the checked value. Not checked: the
+ * copies of the row scans' operands and of constant cells. An honest witness
+ * has no failures; an SVD that violates a bound fails range-check copies
+ * (README.md:93 "matrix-wrong", from P = 42 on). */
+typedef struct {
+    uint64_t gates_checked, gate_failures;
+    uint64_t lookups_checked, lookup_failures;
+    uint64_t copies_checked, copy_failures;
+} svdw_check_result;
+int svdw_check_gates(svdw_ctx* ctx, svdw_check_result* out);
 /* Up to cap segments of the last witness into out; *n = total count. */
 int svdw_shard_segments(const svdw_ctx* ctx, svdw_segment* out, uint64_t cap, uint64_t* n);
 

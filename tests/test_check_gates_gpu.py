@@ -1,0 +1,124 @@
+"""svdw_check_gates: the device constraint checker of a generated witness.
+
+The counts are compared with the Python oracle's MockProver-style layout
+(oracle/pyoracle.py Context.gates / lookup list, check_constraints): the same
+number of basic gates and lookups is checked, and the same gates fail. The
+known-answer behaviour is README.md:93 (`matrix` verifies, `matrix-wrong` does
+not) as the oracle pins it (tests/test_oracle_pins.py::test_kat_matrix_wrong).
+"""
+import numpy as np
+import pytest
+
+from conftest import gamma_for, gen_svd_input
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_counts(w):
+    import pyoracle as po
+    gates = len(w.ctx0.gates) + len(w.ctx1.gates)
+    looks = len(w.ctx0.lookups) + len(w.ctx1.lookups)
+    bad = po.check_constraints(w.ctx0, 19) + po.check_constraints(w.ctx1, 19)
+    return (gates, looks, sum(b.startswith("gate@") for b in bad),
+            sum(b.startswith("lookup@") for b in bad), sum(b.startswith("copy") for b in bad))
+
+
+@pytest.mark.parametrize("N,M,P", [(4, 4, 32), (6, 5, 63), (5, 7, 42), (1, 1, 32)])
+def test_honest_counts_match_oracle(gpu_ctx_factory, N, M, P):
+    import halo2_svd041_amd as hs
+    import pyoracle as po
+    m, u, d, v = gen_svd_input(N, M, seed=N * 7 + M + P)
+    g = gamma_for(P)
+    ctx = gpu_ctx_factory(P)
+    hs.svd_witness(ctx, m, u, v, d, g)
+    r = ctx.check_gates()
+    w = po.svd_witness(m.tolist(), u.tolist(), v.tolist(), d.tolist(), P, 19, gamma=g)
+    gates, looks, gbad, lbad, cbad = _oracle_counts(w)
+    assert (gbad, lbad, cbad) == (0, 0, 0)
+    assert r["copies_checked"] > 0 and r["copy_failures"] == 0, r
+    r.pop("copies_checked"), r.pop("copy_failures")
+    assert r == {"gates_checked": gates, "gate_failures": 0, "lookups_checked": looks,
+                 "lookup_failures": 0}, (r, gates, looks)
+
+
+@pytest.mark.parametrize("P,expect_fail", [(32, False), (42, True), (63, True)])
+def test_matrix_wrong_fails_gates(gpu_ctx_factory, P, expect_fail):
+    """input-creator.py:46-49 perturbation (m[i][j] += 1e-7): the SVD no longer
+    satisfies its bounds at P >= 42 -- in the oracle, as range-check copy
+    constraints (the last running sum != the checked value); the device checker
+    finds failing copies exactly when the oracle does, and the same gates and
+    lookups."""
+    import halo2_svd041_amd as hs
+    import pyoracle as po
+    m, u, d, v = gen_svd_input(6, 6, seed=11)
+    m = m.copy()
+    m[2][3] += 1e-7
+    ctx = gpu_ctx_factory(P)
+    hs.svd_witness(ctx, m, u, v, d, 3)
+    r = ctx.check_gates()
+    w = po.svd_witness(m.tolist(), u.tolist(), v.tolist(), d.tolist(), P, 19, gamma=3)
+    gates, looks, gbad, lbad, cbad = _oracle_counts(w)
+    assert (cbad > 0) == expect_fail
+    assert (r["copy_failures"] > 0) == expect_fail, r
+    assert (r["gates_checked"], r["gate_failures"]) == (gates, gbad)
+    assert (r["lookups_checked"], r["lookup_failures"]) == (looks, lbad)
+
+
+def test_tampered_cells_detected(gpu_ctx_factory):
+    """One advice cell + 1 inside a gadget region, one lookup cell set to 2^19:
+    each is caught, and restoring it makes the witness pass again."""
+    import torch
+    import halo2_svd041_amd as hs
+    from halo2_svd041_amd.collect import stream_tensors
+    m, u, d, v = gen_svd_input(16, 16, seed=4)
+    ctx = gpu_ctx_factory(63)
+    hs.svd_witness(ctx, m, u, v, d, 9)
+    assert ctx.check_gates()["gate_failures"] == 0
+    st = stream_tensors(ctx, torch.device("cuda", 0))
+    bounded = [r for r in ctx.layout() if r["tag"] == "check_mat_entries_bounded"][0]
+    idx = bounded["off"] + bounded["n"] // 2
+    cell = st[(0, 0)][idx].clone()
+    st[(0, 0)][idx, 0] ^= 1
+    torch.cuda.synchronize()
+    r = ctx.check_gates()
+    assert r["gate_failures"] + r["copy_failures"] >= 1 and r["lookup_failures"] == 0, r
+    st[(0, 0)][idx] = cell
+    st[(0, 1)][5] = 0
+    st[(0, 1)][5, 2] = 8                            # 2^19: outside the [0, 2^19) table
+    torch.cuda.synchronize()
+    r = ctx.check_gates()
+    assert r["gate_failures"] == 0 and r["lookup_failures"] == 1, r
+
+
+def test_unsorted_singular_values_fail(gpu_ctx_factory):
+    """d not in descending order: entries_in_desc_order's range check of
+    d_i - d_(i+1) < 0 fails (a copy across regions: desc_order_range reads the
+    subtraction's cell) -- in the oracle and on the device."""
+    import halo2_svd041_amd as hs
+    import pyoracle as po
+    m, u, d, v = gen_svd_input(5, 5, seed=3)
+    d = d.copy()
+    d[1], d[2] = d[2], d[1]
+    ctx = gpu_ctx_factory(32)
+    hs.svd_witness(ctx, m, u, v, d, 3)
+    r = ctx.check_gates()
+    w = po.svd_witness(m.tolist(), u.tolist(), v.tolist(), d.tolist(), 32, 19, gamma=3)
+    gates, looks, gbad, lbad, cbad = _oracle_counts(w)
+    assert cbad > 0
+    assert r["copy_failures"] > 0, r
+    assert (r["gate_failures"], r["lookup_failures"]) == (gbad, lbad), r
+
+
+@pytest.mark.parametrize("N,M,P", [(1024, 1024, 63), (2048, 1024, 32)])
+def test_full_size_honest_witness_satisfies(gpu_ctx_factory, N, M, P):
+    """BASELINE sizes: every basic gate and lookup of the whole witness holds
+    (~10^9 gates at 1024^2 P=63), and the gate count equals the closed form of
+    a small witness scaled by the layout (checked: > half the advice cells / 4)."""
+    import halo2_svd041_amd as hs
+    m, u, d, v = gen_svd_input(N, M, seed=N + M + P)
+    ctx = gpu_ctx_factory(P)
+    cnt = hs.svd_witness(ctx, m, u, v, d, gamma_for(N * M))
+    r = ctx.check_gates()
+    assert r["gate_failures"] == 0 and r["lookup_failures"] == 0 and r["copy_failures"] == 0, r
+    assert r["lookups_checked"] == cnt["lookup0"] + cnt["lookup1"]
+    assert r["gates_checked"] * 4 > (cnt["advice0"] + cnt["advice1"]) // 2, (r, cnt)
