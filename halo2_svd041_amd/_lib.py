@@ -70,6 +70,13 @@ class CheckResult(ct.Structure):
                 ("copies_checked", ct.c_uint64), ("copy_failures", ct.c_uint64)]
 
 
+class PhysParams(ct.Structure):
+    _fields_ = [("k", ct.c_uint32), ("minimum_rows", ct.c_uint32), ("max_rows", ct.c_uint64),
+                ("num_advice", ct.c_uint32 * 2), ("columns_used", ct.c_uint32 * 2),
+                ("num_lookup_advice", ct.c_uint32 * 2), ("num_fixed", ct.c_uint32),
+                ("constants", ct.c_uint64)]
+
+
 class Region(ct.Structure):
     _fields_ = [("phase", ct.c_uint32), ("_pad", ct.c_uint32), ("off", ct.c_uint64),
                 ("n", ct.c_uint64), ("loff", ct.c_uint64), ("nl", ct.c_uint64),
@@ -153,6 +160,10 @@ SIGNATURES = {
     "svdw_shard_segments": (_i32, [_P, ct.POINTER(Segment), _u64, _u64p]),
     "svdw_layout": (_i32, [_P, ct.POINTER(Region), _u64, _u64p]),
     "svdw_check_gates": (_i32, [_P, ct.POINTER(CheckResult)]),
+    "svdw_physical_layout": (_i32, [_P, _u32, _u32, ct.POINTER(PhysParams)]),
+    "svdw_break_points": (_i32, [_P, _u32, _u64p, _u64, _u64p]),
+    "svdw_assign_columns": (_i32, [_P, _u32, _P, _P, _P]),
+    "svdw_check_physical": (_i32, [_P, _u32, _P, _P, _u32, ct.POINTER(CheckResult)]),
     "svdw_profile_collect": (_i32, [_P, ct.POINTER(KStat), _u32, ct.POINTER(_u32)]),
     "svdw_plan_svd": (_i32, [_u32, _u32, _u32, _u32, ct.POINTER(SvdConfig), ct.POINTER(Counts)]),
 }

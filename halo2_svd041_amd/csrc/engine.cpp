@@ -16,6 +16,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -133,6 +135,7 @@ struct PB {
     // cell against its source cell (view), range_check's last running sum
     // against the checked value (RangeChip::range_check's constrain_equal).
     std::vector<uint32_t> chk;
+    bool kconst = true;       // its constant-source cells are halo2-base Constants
     int8_t vload[kMaxV];      // view a value was loaded from (-1: computed)
     int16_t fullc[kMaxV];     // first cell holding the value in full (-1: none)
     void gate(uint32_t at) { chk.push_back(chk_gate(at)); }
@@ -403,6 +406,18 @@ struct svdw_ctx {
     // per region: gate offsets within one element's cells and cells per element
     // (program regions; empty otherwise; svdw_check_gates)
     std::vector<RegionChecks> layout_chk;
+    // distinct constant cell values (halo2-base Constant / load_constant):
+    // the fixed-column count of svdw_physical_layout
+    std::set<std::array<uint32_t, 8>> consts;
+    // svdw_physical_layout's plan: per phase, the virtual index of each advice
+    // column's row 0 and each full column's break point
+    struct Phys {
+        bool valid = false;
+        uint32_t k = 0, min_rows = 0;
+        uint64_t R = 0;
+        std::vector<uint64_t> start[2], bp[2];
+    } phys;
+    DBuf gateq[2];
     std::vector<uint64_t>* gemm_log = nullptr;   // dry run: offsets of honest_prover_mat_mul
     std::vector<hipEvent_t> deps;           // dependency events (no timing)
     size_t dep_next = 0;
@@ -471,6 +486,8 @@ static void clear_streams(svdw_ctx* c) {
     c->owned.clear();
     c->layout.clear();
     c->layout_chk.clear();
+    c->consts.clear();
+    c->phys.valid = false;
     c->bits_pending = false;
     for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
     c->mbits.clear();
@@ -543,6 +560,7 @@ static void append(svdw_ctx* c, uint32_t phase, uint64_t n, uint64_t nl, uint64_
                    uint64_t* loff, const char* tag, uint64_t rows = 1) {
     REQUIRE(phase < 2, "phase must be 0 or 1");
     Stream& s = c->ph[phase];
+    c->phys.valid = false;
     grow(c, s.adv, s.n, s.cap, s.n + n);
     grow(c, s.lk, s.nl, s.lcap, s.nl + nl);
     *off = s.n;
@@ -669,11 +687,19 @@ static void stage_own(svdw_ctx* c, uint32_t phase, const PB& pb, uint32_t nelem,
     own(c, phase, false, off + r0 * cw * pb.a.C, (r1 - r0) * cw * pb.a.C);
     own(c, phase, true, loff + r0 * cw * pb.a.L, (r1 - r0) * cw * pb.a.L);
 }
+static void note_const(svdw_ctx* c, const Fr& v) {
+    std::array<uint32_t, 8> w;
+    for (int i = 0; i < 8; ++i) w[i] = v.w[i];
+    c->consts.insert(w);
+}
 // the last appended region is `nelem` copies of pb's program: record its gates
 // (views: the source cells as (phase, offset), strided views into the cell
 // streams only -- the streams may move before the check)
 static void note_gates(svdw_ctx* c, const PB& pb, uint32_t cols = 1, size_t reg = ~size_t(0)) {
     RegionChecks& r = reg == ~size_t(0) ? c->layout_chk.back() : c->layout_chk.at(reg);
+    if (pb.kconst)
+        for (uint32_t q = 0; q < pb.a.C; ++q)
+            if (pb.a.adv[q].src >= KSRC) note_const(c, pb.a.K[pb.a.adv[q].src - KSRC]);
     r.words = pb.chk;
     r.unit = pb.a.C;
     r.cols = cols ? cols : 1;
@@ -708,8 +734,9 @@ static uint64_t run_stage(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, u
     stage_launch(c, phase, pb, nelem, cols, off, loff, tag);
     return off;
 }
-static svdw_vec put_cell(svdw_ctx* c, uint32_t phase, const Fr& v) {   // load_witness/load_constant
-    PB pb(c->LB);
+static svdw_vec put_cell(svdw_ctx* c, uint32_t phase, const Fr& v, bool constant = false) {
+    PB pb(c->LB);                                          // load_witness / load_constant
+    pb.kconst = constant;
     pb.cell(pb.K(v));
     // Inside svd_witness (products queued ahead), a one-cell launch on the cell
     // stream would wait for a free CU behind the scans on st2 (15-35 us on the
@@ -821,7 +848,7 @@ static void check_mat_diff_views(svdw_ctx* c, uint32_t phase, const DView& a, co
 // still be in flight on another stream.
 static void check_mat_id(svdw_ctx* c, const svdw_mat& a, const svdw_vec& sid, const BigU& tol,
                          const Fr* sid_val = nullptr) {
-    put_cell(c, a.phase, fr_zero());                      // let zero = ctx.load_constant(F::ZERO)
+    put_cell(c, a.phase, fr_zero(), true);                // let zero = ctx.load_constant(F::ZERO)
     DView b;
     memset(&b, 0, sizeof b);
     b.mode = sid_val ? VIEW_DIAGK : VIEW_DIAG;
@@ -1283,7 +1310,7 @@ static void verify_mul_legacy(svdw_ctx* c, uint32_t phase, const svdw_mat& a, co
     const uint32_t d = cs.cols, n = a.rows, k = a.cols;
     ensure_gamma_vec(c, d, gamma);
     const Fr* gpc = (const Fr*)c->gpc.p;
-    put_cell(c, phase, fr_from_u64(1));                    // load_witness(F::ONE)
+    put_cell(c, phase, fr_from_u64(1), true);              // load_witness(F::ONE) + assert_is_const
     if (d > 1) {                                          // v_i = mul(v_{i-1}, init_rand)
         PB pb(c->LB);
         DView w;
@@ -1294,7 +1321,10 @@ static void verify_mul_legacy(svdw_ctx* c, uint32_t phase, const svdw_mat& a, co
         pb.a.view[1] = w;
         if (!c->dry) pb.a.view[1].ptr = gpc + 1;
         uint8_t prev = pb.load(0), cur = pb.load(1);
+        pb.gate(0);
         pb.cell(pb.K(0)); pb.cell(prev); pb.cell(pb.K(gamma)); pb.cell(cur);
+        pb.kconst = false;                                // gamma is a cell, not a Constant
+        note_const(c, fr_zero());
         run_stage(c, phase, pb, d - 1, 1, "verify_mul_gamma_pows");
     }
     const int na_cs = scan_na(c, cs), na_b = scan_na(c, b), na_a = scan_na(c, a);
@@ -1326,6 +1356,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     auto scan_append = [&](const svdw_mat& a) {
         uint64_t off;
         append(c, phase, (uint64_t)a.rows * (3ull * a.cols + 1), 0, &off, nullptr, "scan", a.rows);
+        note_const(c, fr_zero());                             // inner_product's Constant(0)
         return svdw_vec{phase, a.rows, off + 3ull * a.cols, (int64_t)(3ull * a.cols + 1)};
     };
     // pass 1: the cell layout, in the reference's order
@@ -1340,10 +1371,13 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         Plan& p = pl.back();
         p.one.cell(p.one.K(fr_from_u64(1)));                  // load_witness(F::ONE)
         append(c, phase, p.one.a.C, 0, &p.one_off, &p.one_loff, "load_cell");
+        note_const(c, fr_from_u64(1));                        // assert_is_const(one, 1)
         stage_own(c, phase, p.one, 1, 1, p.one_off, p.one_loff);
         if (d > 1) {                                          // v_i = mul(v_{i-1}, init_rand)
             uint8_t prev = p.pows.load(0), cur = p.pows.load(1);
             p.pows.gate(0);                               // mul(v_(i-1), init_rand)
+            p.pows.kconst = false;                        // gamma is a cell, not a Constant
+            note_const(c, fr_zero());
             p.pows.cell(p.pows.K(0)); p.pows.cell(prev); p.pows.cell(p.pows.K(gamma)); p.pows.cell(cur);
             append(c, phase, (uint64_t)(d - 1) * p.pows.a.C, 0, &p.pows_off, &p.pows_loff,
                    "verify_mul_gamma_pows");
@@ -1593,7 +1627,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     if (r == M) {
         udv = view_of(c, mat_times_diag_mat(c, u, d));
     } else {
-        put_cell(c, 0 + u.phase, fr_zero());              // zero padding constant
+        put_cell(c, 0 + u.phase, fr_zero(), true);        // zero padding constant
         svdw_mat ud = mat_times_diag_mat(c, u, d);
         udv = view_of(c, ud);
         udv.cols = r;                                     // columns >= N read as 0
@@ -1609,7 +1643,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     check_mat_diff_views(c, m.phase, udv, view_of(c, mvt), N, M, es);
     Fr q = pow2_fr(P);
     const Fr qq = fr_mul(q, q);
-    svdw_vec q2 = put_cell(c, m.phase, qq);
+    svdw_vec q2 = put_cell(c, m.phase, qq, true);
     svdw_mat uut = honest_prover_mat_mul(c, m.phase, u, ut, bu, bu);
     check_mat_id(c, uut, q2, eu, &qq);
     svdw_mat vvt = honest_prover_mat_mul(c, m.phase, v, vt, bv, bv);
@@ -1768,7 +1802,7 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             (void)hipStreamSynchronize(c->st2);
             if (c->st3) (void)hipStreamSynchronize(c->st3);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
-            for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->w1c, &c->w1m, &c->w2c, &c->w2m,
+            for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1], &c->w1c, &c->w1m, &c->w2c, &c->w2m,
                             &c->bits, &c->gpc, &c->gpm, &c->crtR, &c->gbits})
                 if (b->p) (void)hipFree(b->p);
             for (auto& b : c->gps) if (b.p) (void)hipFree(b.p);
@@ -1867,7 +1901,10 @@ int svdw_load_witness(svdw_ctx* c, uint32_t phase, const uint64_t value[4], svdw
     });
 }
 int svdw_load_constant(svdw_ctx* c, uint32_t phase, const uint64_t value[4], svdw_vec* out) {
-    return svdw_load_witness(c, phase, value, out);   // same cell value; constancy is a prover fact
+    return guarded([&] {
+        REQUIRE(c && value && out, "null argument");
+        *out = put_cell(c, phase, fr_from_words(value), true);
+    });
 }
 int svdw_entries_less_than(svdw_ctx* c, const svdw_vec* d, uint32_t max_bits) {
     return guarded([&] {
@@ -2128,6 +2165,183 @@ int svdw_check_gates(svdw_ctx* c, svdw_check_result* out) {
         out->gate_failures = h[1];
         out->lookups_checked = h[2];
         out->lookup_failures = h[3];
+        out->copies_checked = h[4];
+        out->copy_failures = h[5];
+    });
+}
+// ------------------------------------------------- physical layout
+// Virtual -> physical assignment of a phase's cells (halo2-base 0.4.1, recalled;
+// oracle/pyoracle.py physical_layout): basic-gate advice columns of max_rows =
+// 2^k - minimum_rows usable rows. A column ends at a cell whose gate would
+// cross max_rows (q && row + 4 > max_rows) or at row max_rows - 1; that cell is
+// repeated at row 0 of the next column (copy-constrained) and its selector is
+// enabled there only.
+namespace {
+struct GateIndex {               // q(i): does a basic gate start at virtual cell i
+    struct Reg {
+        uint64_t off, n, unit;
+        bool scan;
+        std::vector<uint8_t> bit;    // per unit offset (program regions)
+    };
+    std::vector<Reg> regs;       // ascending offsets
+    GateIndex(const svdw_ctx* c, uint32_t phase) {
+        for (size_t k = 0; k < c->layout.size(); ++k) {
+            const svdw_region& r = c->layout[k];
+            if (r.phase != phase || !r.n) continue;
+            if (!strcmp(r.tag, "scan") && r.rows) {
+                regs.push_back(Reg{r.off, r.n, r.n / r.rows, true, {}});
+                continue;
+            }
+            const RegionChecks& rc = c->layout_chk[k];
+            Reg g{r.off, r.n, rc.unit, false, std::vector<uint8_t>(rc.unit, 0)};
+            bool any = false;
+            for (uint32_t w : rc.words)
+                if (chk_kind(w) == CHK_GATE) g.bit[w] = 1, any = true;
+            if (any && rc.unit) regs.push_back(std::move(g));
+        }
+    }
+    bool q(uint64_t i) const {
+        auto it = std::upper_bound(regs.begin(), regs.end(), i,
+                                   [](uint64_t x, const Reg& r) { return x < r.off; });
+        if (it == regs.begin()) return false;
+        const Reg& r = *--it;
+        if (i >= r.off + r.n) return false;
+        const uint64_t o = (i - r.off) % r.unit;
+        return r.scan ? (o % 3 == 0 && o + 3 < r.unit) : r.bit[o] != 0;
+    }
+};
+}  // namespace
+int svdw_physical_layout(svdw_ctx* c, uint32_t k, uint32_t minimum_rows, svdw_physical_params* out) {
+    return guarded([&] {
+        REQUIRE(c && out, "null argument");
+        REQUIRE(k >= 3 && k <= 40, "svdw_physical_layout: k out of range");
+        REQUIRE(!sharded(c), "svdw_physical_layout: the witness of a sharded context is partial");
+        REQUIRE((1ull << k) > (uint64_t)minimum_rows + 4, "svdw_physical_layout: minimum_rows >= 2^k - 4");
+        const uint64_t R = (1ull << k) - minimum_rows;
+        auto& P = c->phys;
+        P.valid = false;
+        P.k = k;
+        P.min_rows = minimum_rows;
+        P.R = R;
+        memset(out, 0, sizeof *out);
+        out->k = k;
+        out->minimum_rows = minimum_rows;
+        out->max_rows = R;
+        for (uint32_t ph = 0; ph < 2; ++ph) {
+            const uint64_t T = c->ph[ph].n, TL = c->ph[ph].nl;
+            P.start[ph].clear();
+            P.bp[ph].clear();
+            const GateIndex gi(c, ph);
+            for (uint64_t s = 0; T && true;) {
+                P.start[ph].push_back(s);
+                // the first of rows R-3, R-2 (gate crossing max_rows) or R-1 (last row)
+                uint64_t r = R - 3;
+                for (; r < R - 1; ++r)
+                    if (s + r < T && gi.q(s + r)) break;
+                if (s + r >= T) break;                     // the phase ends in this column
+                P.bp[ph].push_back(r);
+                s += r;
+            }
+            out->num_advice[ph] = (uint32_t)((T + R - 1) / R);
+            out->columns_used[ph] = (uint32_t)P.start[ph].size();
+            out->num_lookup_advice[ph] = (uint32_t)((TL + R - 1) / R);
+        }
+        out->constants = c->consts.size();
+        out->num_fixed = (uint32_t)((c->consts.size() + (1ull << k) - 1) >> k);
+        P.valid = true;
+    });
+}
+int svdw_break_points(const svdw_ctx* c, uint32_t phase, uint64_t* out, uint64_t cap, uint64_t* n) {
+    return guarded([&] {
+        REQUIRE(c && n && phase < 2, "bad argument");
+        REQUIRE(c->phys.valid, "svdw_break_points: call svdw_physical_layout after the witness");
+        const auto& b = c->phys.bp[phase];
+        *n = b.size();
+        for (uint64_t i = 0; i < cap && i < b.size() && out; ++i) out[i] = b[i];
+    });
+}
+int svdw_assign_columns(svdw_ctx* c, uint32_t phase, void* advice, uint8_t* selectors, void* lookup) {
+    return guarded([&] {
+        REQUIRE(c && phase < 2, "bad argument");
+        REQUIRE(!c->dry, "svdw_assign_columns needs a device context");
+        REQUIRE(c->phys.valid, "svdw_assign_columns: call svdw_physical_layout after the witness");
+        sync(c);
+        const auto& P = c->phys;
+        const uint64_t rows = 1ull << P.k, T = c->ph[phase].n, TL = c->ph[phase].nl;
+        const size_t ncols = P.start[phase].size();
+        REQUIRE(ncols <= (T + P.R - 1) / P.R,
+                "NOT ENOUGH ADVICE COLUMNS IN PHASE (columns_used > num_advice: raise k)");
+        if (selectors && T) {                              // q bits of the virtual stream
+            const GateIndex gi(c, phase);
+            const uint64_t nw = (T + 31) / 32;
+            ensure_buf(c, c->gateq[phase], nw * 4);
+            uint32_t* qb = (uint32_t*)c->gateq[phase].p;
+            hipck(hipMemsetAsync(qb, 0, nw * 4, c->st), "hipMemsetAsync");
+            for (const auto& r : gi.regs) {
+                std::vector<uint8_t> bits(r.unit);
+                for (uint64_t o = 0; o < r.unit; ++o)
+                    bits[o] = r.scan ? (o % 3 == 0 && o + 3 < r.unit) : r.bit[o];
+                ensure_buf(c, c->chkg, r.unit);
+                hipck(hipMemcpyAsync(c->chkg.p, bits.data(), r.unit, hipMemcpyHostToDevice, c->st), "H2D");
+                hipck(launch_gate_bits(qb, r.off, r.n, r.unit, (const uint8_t*)c->chkg.p, c->st),
+                      "k_gate_bits");
+                hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");   // chkg is reused
+            }
+        }
+        for (size_t col = 0; col < ncols; ++col) {
+            const uint64_t s = P.start[phase][col];
+            const bool last = col + 1 == ncols;
+            const uint64_t len = last ? T - s : P.bp[phase][col] + 1;
+            if (advice) {
+                Fr* dst = (Fr*)advice + col * rows;
+                hipck(hipMemcpyAsync(dst, c->ph[phase].adv + s, len * sizeof(Fr), hipMemcpyDeviceToDevice,
+                                     c->st), "D2D");
+                if (len < rows)
+                    hipck(hipMemsetAsync(dst + len, 0, (rows - len) * sizeof(Fr), c->st), "hipMemsetAsync");
+            }
+            if (selectors)
+                hipck(launch_selectors(selectors + col * rows, (const uint32_t*)c->gateq[phase].p, s, len,
+                                       rows, !last, c->st), "k_selectors");
+        }
+        if (lookup) {
+            const uint64_t nl = (TL + P.R - 1) / P.R;
+            for (uint64_t col = 0; col < nl; ++col) {
+                const uint64_t s = col * P.R, len = std::min(P.R, TL - s);
+                Fr* dst = (Fr*)lookup + col * rows;
+                hipck(hipMemcpyAsync(dst, c->ph[phase].lk + s, len * sizeof(Fr), hipMemcpyDeviceToDevice,
+                                     c->st), "D2D");
+                hipck(hipMemsetAsync(dst + len, 0, (rows - len) * sizeof(Fr), c->st), "hipMemsetAsync");
+            }
+        }
+        hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
+    });
+}
+int svdw_check_physical(svdw_ctx* c, uint32_t phase, const void* advice, const uint8_t* selectors,
+                        uint32_t ncols, svdw_check_result* out) {
+    return guarded([&] {
+        REQUIRE(c && advice && selectors && out && phase < 2, "bad argument");
+        REQUIRE(!c->dry, "svdw_check_physical needs a device context");
+        REQUIRE(c->phys.valid, "svdw_check_physical: call svdw_physical_layout first");
+        memset(out, 0, sizeof *out);
+        ensure_buf(c, c->chk, 6 * sizeof(unsigned long long));
+        unsigned long long* cnt = (unsigned long long*)c->chk.p;
+        hipck(hipMemsetAsync(cnt, 0, 6 * sizeof(unsigned long long), c->st), "hipMemsetAsync");
+        hipck(launch_check_physical((const Fr*)advice, selectors, 1ull << c->phys.k, ncols, cnt, c->st),
+              "k_check_physical");
+        const auto& bp = c->phys.bp[phase];
+        const uint32_t nb = (uint32_t)std::min<uint64_t>(bp.size(), ncols ? ncols - 1 : 0);
+        if (nb) {
+            ensure_buf(c, c->chkg, nb * sizeof(uint64_t));
+            hipck(hipMemcpyAsync(c->chkg.p, bp.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, c->st),
+                  "H2D");
+            hipck(launch_check_breaks((const Fr*)advice, 1ull << c->phys.k, (const uint64_t*)c->chkg.p, nb,
+                                      cnt + 4, c->st), "k_check_breaks");
+        }
+        unsigned long long h[6];
+        hipck(hipMemcpyAsync(h, cnt, sizeof h, hipMemcpyDeviceToHost, c->st), "D2H");
+        hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
+        out->gates_checked = h[0];
+        out->gate_failures = h[1];
         out->copies_checked = h[4];
         out->copy_failures = h[5];
     });

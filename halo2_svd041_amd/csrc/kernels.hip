@@ -1443,6 +1443,94 @@ hipError_t launch_check_cells(const Fr* adv, uint64_t nunits, uint32_t unit, uin
                        nunits, unit, cols, words, nw, v0, v1, cnt);
     return hipGetLastError();
 }
+__global__ __launch_bounds__(256) void k_gate_bits(uint32_t* qb, uint64_t off, uint64_t n,
+                                                   uint64_t unit, const uint8_t* __restrict__ ubits) {
+    const uint64_t w = off / 32 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w * 32 >= off + n) return;
+    uint32_t bits = 0;
+    const uint64_t i0 = w * 32;
+    uint64_t o = i0 >= off ? (i0 - off) % unit : 0;
+    for (int b = 0; b < 32; ++b) {
+        const uint64_t i = i0 + b;
+        if (i >= off && i < off + n) {
+            if (ubits[o]) bits |= 1u << b;
+            if (++o == unit) o = 0;
+        }
+    }
+    if (bits) atomicOr(qb + w, bits);
+}
+hipError_t launch_gate_bits(uint32_t* qb, uint64_t off, uint64_t n, uint64_t unit, const uint8_t* ubits,
+                            hipStream_t st) {
+    if (!n) return hipSuccess;
+    if (!unit) return hipErrorInvalidValue;
+    const uint64_t nw = (off + n + 31) / 32 - off / 32;
+    hipLaunchKernelGGL(k_gate_bits, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, st, qb, off, n, unit,
+                       ubits);
+    return hipGetLastError();
+}
+// 4 selector bytes per thread
+__global__ __launch_bounds__(256) void k_selectors(uint8_t* q, const uint32_t* __restrict__ qb,
+                                                   uint64_t start, uint64_t len, uint64_t rows,
+                                                   bool clear_last) {
+    const uint64_t r0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (r0 >= rows) return;
+    uint32_t v = 0;
+    for (int b = 0; b < 4; ++b) {
+        const uint64_t r = r0 + b;
+        if (r < len && !(clear_last && r + 1 == len)) {
+            const uint64_t i = start + r;
+            v |= ((qb[i >> 5] >> (i & 31)) & 1u) << (8 * b);
+        }
+    }
+    *reinterpret_cast<uint32_t*>(q + r0) = v;
+}
+hipError_t launch_selectors(uint8_t* q, const uint32_t* qb, uint64_t start, uint64_t len, uint64_t rows,
+                            bool clear_last, hipStream_t st) {
+    if ((rows & 3) || ((uintptr_t)q & 3)) return hipErrorInvalidValue;
+    if (len && !qb) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_selectors, dim3((unsigned)((rows / 4 + 255) / 256)), dim3(256), 0, st, q, qb, start,
+                       len, rows, clear_last);
+    return hipGetLastError();
+}
+__global__ __launch_bounds__(256) void k_check_physical(const Fr* __restrict__ cols,
+                                                        const uint8_t* __restrict__ q, uint64_t rows,
+                                                        uint32_t ncols, unsigned long long* cnt) {
+    const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool gate = false, gbad = false;
+    if (idx < rows * ncols) {
+        const uint64_t col = idx / rows, r = idx - col * rows;
+        const Fr* g = cols + idx;
+        if (q[idx]) {
+            gate = true;
+            gbad = r + 3 >= rows ||
+                   !fr_eq(fr_add(ld_fr(g), fr_mul(ld_fr(g + 1), ld_fr(g + 2))), ld_fr(g + 3));
+        }
+    }
+    wave_count(gate, gbad, cnt);
+}
+// the break cell of column c (row bp[c]) == row 0 of column c + 1
+__global__ void k_check_breaks(const Fr* __restrict__ cols, uint64_t rows, const uint64_t* __restrict__ bp,
+                               uint32_t nb, unsigned long long* cnt) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    bool bad = false;
+    if (c < nb) bad = bp[c] >= rows || !fr_eq(ld_fr(cols + c * rows + bp[c]), ld_fr(cols + (c + 1) * rows));
+    wave_count(c < nb, bad, cnt);
+}
+hipError_t launch_check_breaks(const Fr* cols, uint64_t rows, const uint64_t* bp, uint32_t nb,
+                               unsigned long long* cnt, hipStream_t st) {
+    if (!nb) return hipSuccess;
+    hipLaunchKernelGGL(k_check_breaks, dim3((nb + 255) / 256), dim3(256), 0, st, cols, rows, bp, nb, cnt);
+    return hipGetLastError();
+}
+hipError_t launch_check_physical(const Fr* cols, const uint8_t* q, uint64_t rows, uint32_t ncols,
+                                 unsigned long long* cnt, hipStream_t st) {
+    const uint64_t n = rows * ncols;
+    if (!n) return hipSuccess;
+    if ((n + 255) / 256 > 0x7fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_check_physical, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cols, q, rows,
+                       ncols, cnt);
+    return hipGetLastError();
+}
 __global__ __launch_bounds__(256) void k_check_lookups(const Fr* __restrict__ lk, uint64_t n,
                                                        uint32_t lb, unsigned long long* cnt) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -79,6 +79,19 @@ struct RegionChecks {
 hipError_t launch_check_cells(const Fr* adv, uint64_t nunits, uint32_t unit, uint32_t cols,
                               const uint32_t* words, uint32_t nw, ChkView v0, ChkView v1,
                               unsigned long long* cnt, hipStream_t st);
+// Physical layout (svdw_assign_columns): qb |= the gate-start bits of a region
+// (`unit`-periodic pattern ubits[unit]); a column's selector bytes from the bits
+// (the last row of a full column cleared); the basic gate at every enabled
+// (column, row), and each break cell against row 0 of the next column
+// (cnt[0..1] gates, cnt[4..5] copies).
+hipError_t launch_gate_bits(uint32_t* qb, uint64_t off, uint64_t n, uint64_t unit, const uint8_t* ubits,
+                            hipStream_t st);
+hipError_t launch_selectors(uint8_t* q, const uint32_t* qb, uint64_t start, uint64_t len, uint64_t rows,
+                            bool clear_last, hipStream_t st);
+hipError_t launch_check_physical(const Fr* cols, const uint8_t* q, uint64_t rows, uint32_t ncols,
+                                 unsigned long long* cnt, hipStream_t st);
+hipError_t launch_check_breaks(const Fr* cols, uint64_t rows, const uint64_t* bp, uint32_t nb,
+                               unsigned long long* cnt, hipStream_t st);
 hipError_t launch_check_lookups(const Fr* lk, uint64_t n, uint32_t lb, unsigned long long* cnt,
                                 hipStream_t st);
 static constexpr int kMaxBitSegs = 8;

@@ -19,7 +19,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import (CheckResult, Counts, DivScale, InputDims, KStat, Mat, Params, Payload, Region, Segment, SvdConfig, SvdwError,
+from ._lib import (CheckResult, PhysParams, Counts, DivScale, InputDims, KStat, Mat, Params, Payload, Region, Segment, SvdConfig, SvdwError,
                    Vec, check, lib)
 
 P_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
@@ -62,6 +62,8 @@ class Context:
     def __init__(self, device: int = 0, precision_bits: int = 32, lookup_bits: int = 19):
         self.precision_bits = precision_bits
         self.lookup_bits = lookup_bits
+        self.device = device
+        self._phys = None
         self._h = ct.c_void_p()
         p = Params(device, precision_bits, lookup_bits)
         check(lib().svdw_ctx_create(ct.byref(p), ct.byref(self._h)))
@@ -156,6 +158,47 @@ class Context:
         check(lib().svdw_check_gates(self._h, ct.byref(r)))
         return {"gates_checked": r.gates_checked, "gate_failures": r.gate_failures,
                 "lookups_checked": r.lookups_checked, "lookup_failures": r.lookup_failures,
+                "copies_checked": r.copies_checked, "copy_failures": r.copy_failures}
+
+    def physical_layout(self, k: int, minimum_rows: int = 20) -> dict:
+        """Virtual -> physical layout plan of the last witness (svdw_physical_layout)."""
+        p = PhysParams()
+        check(lib().svdw_physical_layout(self._h, k, minimum_rows, ct.byref(p)))
+        self._phys = {"k": p.k, "minimum_rows": p.minimum_rows, "max_rows": p.max_rows,
+                "num_advice": list(p.num_advice), "columns_used": list(p.columns_used),
+                "num_lookup_advice": list(p.num_lookup_advice), "num_fixed": p.num_fixed,
+                "constants": p.constants}
+        return dict(self._phys)
+
+    def break_points(self, phase: int) -> list:
+        n = ct.c_uint64()
+        check(lib().svdw_break_points(self._h, phase, None, 0, ct.byref(n)))
+        buf = (ct.c_uint64 * max(n.value, 1))()
+        check(lib().svdw_break_points(self._h, phase, buf, n.value, ct.byref(n)))
+        return list(buf[:n.value])
+
+    def assign_columns(self, phase: int, device=None):
+        """(advice [cols, 2^k, 32] u8, selectors [cols, 2^k] u8, lookup [nl, 2^k, 32] u8)
+        torch tensors on the device, filled by svdw_assign_columns."""
+        import torch
+        p = self._phys
+        if p is None:
+            raise RuntimeError("call physical_layout() after the witness first")
+        dev = device or torch.device("cuda", self.device)
+        rows = 1 << p["k"]
+        nc, nl = p["columns_used"][phase], p["num_lookup_advice"][phase]
+        adv = torch.empty((nc, rows, 32), dtype=torch.uint8, device=dev)
+        sel = torch.empty((nc, rows), dtype=torch.uint8, device=dev)
+        lk = torch.empty((nl, rows, 32), dtype=torch.uint8, device=dev)
+        check(lib().svdw_assign_columns(self._h, phase, adv.data_ptr() if nc else None,
+                                        sel.data_ptr() if nc else None, lk.data_ptr() if nl else None))
+        return adv, sel, lk
+
+    def check_physical(self, phase: int, adv, sel) -> dict:
+        r = CheckResult()
+        check(lib().svdw_check_physical(self._h, phase, adv.data_ptr(), sel.data_ptr(), adv.shape[0],
+                                        ct.byref(r)))
+        return {"gates_checked": r.gates_checked, "gate_failures": r.gate_failures,
                 "copies_checked": r.copies_checked, "copy_failures": r.copy_failures}
 
     def profile(self, on: bool = True, prefix: str = "") -> None:

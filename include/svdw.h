@@ -295,6 +295,36 @@ typedef struct {
     uint64_t copies_checked, copy_failures;
 } svdw_check_result;
 int svdw_check_gates(svdw_ctx* ctx, svdw_check_result* out);
+
+/* Virtual -> physical layout of the last witness (the
+ * halo2-base 0.4.1 keygen assignment, restated from memory -- parity unpinned,
+ * see DESIGN.md): basic-gate advice columns of max_rows = 2^k - minimum_rows
+ * usable rows (BaseCircuitBuilder::calculate_params, src/scaffold/mod.rs:245-247
+ * MINIMUM_ROWS default 20). A column breaks at the cell whose gate would cross
+ * max_rows, or at row max_rows - 1; the break cell is repeated at row 0 of the
+ * next column and its selector enabled there only. Lookup cells fill lookup
+ * advice columns max_rows at a time. num_advice is calculate_params' estimate
+ * ceil(cells / max_rows); columns_used is what the assignment needs (more than
+ * num_advice: the reference's keygen panics "NOT ENOUGH ADVICE COLUMNS"). */
+typedef struct {
+    uint32_t k, minimum_rows;
+    uint64_t max_rows;
+    uint32_t num_advice[2], columns_used[2], num_lookup_advice[2];
+    uint32_t num_fixed;
+    uint64_t constants;    /* distinct constant cell values (fixed column cells) */
+} svdw_physical_params;
+int svdw_physical_layout(svdw_ctx* ctx, uint32_t k, uint32_t minimum_rows, svdw_physical_params* out);
+/* each column but the last: the row of its break cell (halo2-base break_points) */
+int svdw_break_points(const svdw_ctx* ctx, uint32_t phase, uint64_t* out, uint64_t cap, uint64_t* n);
+/* Materialise phase `phase` on the device, column-major, 2^k rows per column
+ * (rows past the used ones zero): advice = columns_used x 2^k cells, selectors
+ * = columns_used x 2^k q_enable bytes, lookup = num_lookup_advice x 2^k cells;
+ * any may be NULL. Fails with SVDW_ERANGE when columns_used > num_advice. */
+int svdw_assign_columns(svdw_ctx* ctx, uint32_t phase, void* advice, uint8_t* selectors, void* lookup);
+/* The basic gate at every enabled (column, row) of assigned columns, and each
+ * break cell against row 0 of the next column (copies_*). */
+int svdw_check_physical(svdw_ctx* ctx, uint32_t phase, const void* advice, const uint8_t* selectors,
+                        uint32_t ncols, svdw_check_result* out);
 /* Up to cap segments of the last witness into out; *n = total count. */
 int svdw_shard_segments(const svdw_ctx* ctx, svdw_segment* out, uint64_t cap, uint64_t* n);
 

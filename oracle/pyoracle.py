@@ -554,6 +554,56 @@ def check_constraints(ctx: Context, lookup_bits: int) -> List[str]:
     return bad
 
 
+# ---------------------------------------------------------------------------
+# Virtual -> physical layout
+# ---------------------------------------------------------------------------
+# Restated from halo2-base 0.4.1 [ext, not on disk; recalled, parity unpinned]:
+# BaseCircuitBuilder::calculate_params (max_rows = 2^k - minimum_rows, columns =
+# ceil(cells / max_rows), called from src/utils/executor.rs:48-55 and
+# src/scaffold/mod.rs:245-247 with MINIMUM_ROWS default 20), the keygen
+# assignment of a phase's virtual cells to basic-gate advice columns (a column
+# breaks at a cell whose gate would cross max_rows, or at row max_rows - 1; the
+# break cell is repeated at row 0 of the next column, copy-constrained, and its
+# selector is enabled only there), and the lookup-advice chunking (lookup cells
+# in order, max_rows per column).
+@dataclass
+class Physical:
+    k: int
+    max_rows: int
+    num_advice: int                 # calculate_params' estimate
+    columns: List[List[int]]        # advice column values (used rows only)
+    selectors: List[List[int]]      # q_enable per used row
+    break_points: List[int]         # per column but the last: the row of its last cell
+    lookup_columns: List[List[int]]
+    num_lookup_advice: int
+    num_fixed: int
+
+
+def physical_layout(ctx: Context, k: int, minimum_rows: int = 20) -> Physical:
+    R = (1 << k) - minimum_rows
+    assert R >= 4
+    q = set(ctx.gates)
+    cols, sels, bps = [[]], [[]], []
+    row = 0
+    for i, v in enumerate(ctx.advice):
+        cols[-1].append(v)
+        sels[-1].append(0)
+        if (i in q and row + 4 > R) or row >= R - 1:
+            bps.append(row)
+            row = 0
+            cols.append([v])
+            sels.append([0])
+        if i in q:
+            sels[-1][row] = 1
+        row += 1
+    if not ctx.advice:
+        cols, sels = [], []
+    lk = [ctx.lookups[j:j + R] for j in range(0, len(ctx.lookups), R)]
+    distinct = len({c % P_MOD for _, c in ctx.consts})
+    return Physical(k, R, -(-len(ctx.advice) // R), cols, sels, bps, lk,
+                    -(-len(ctx.lookups) // R), -(-distinct // (1 << k)))
+
+
 def cells_to_bytes(vals: Sequence[int]) -> bytes:
     """Canonical little-endian 32-byte cells (halo2curves Fr::to_repr)."""
     return b"".join(int(x).to_bytes(32, "little") for x in vals)
