@@ -49,8 +49,9 @@ def main():
             del adv, sel, lk
         t = min(ts)
         rows = 1 << a.k
-        moved = (2 * ctx.advice_len(ph) * 32 + 2 * ctx.lookup_len(ph) * 32 +
-                 (p["columns_used"][ph] * rows) * 33 + p["num_lookup_advice"][ph] * rows * 32)
+        # read the virtual streams once, write every column in full (cells + q bytes)
+        moved = ((ctx.advice_len(ph) + ctx.lookup_len(ph)) * 32 +
+                 p["columns_used"][ph] * rows * 33 + p["num_lookup_advice"][ph] * rows * 32)
         res["phases"][ph] = {"ms": round(t * 1e3, 3), "bytes": moved,
                              "GB_per_s": round(moved / t / 1e9, 1)}
     print(json.dumps(res))
