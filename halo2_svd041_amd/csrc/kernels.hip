@@ -253,7 +253,7 @@ __device__ __forceinline__ void stream_cells_inc(uint4* __restrict__ out, uint32
                                                  uint32_t magic, const uint32_t* sK,
                                                  const uint32_t* sV, uint32_t nv) {
     const uint32_t h = threadIdx.x & 1, step = blockDim.x >> 1;
-    const uint32_t dq = step / C, dr = step - dq * C, ev = nv * VW;
+    const uint32_t dq = step / C, dr = step - dq * C, ev = stage_elem_words(nv);
     uint32_t hc0 = threadIdx.x;
     if (ALIGN) {
         // misalignment of the region start in half-cells (even: cells are 32 B aligned)
@@ -288,7 +288,7 @@ __device__ __forceinline__ void stream_cells_desc(uint4* __restrict__ out, uint3
                                                   uint32_t magic, const uint32_t* smem,
                                                   uint32_t vbase0, uint32_t nv) {
     const uint32_t h = threadIdx.x & 1, step = blockDim.x >> 1;
-    const uint32_t dq = step / C, dr = step - dq * C, ev = nv * VW;
+    const uint32_t dq = step / C, dr = step - dq * C, ev = stage_elem_words(nv);
     uint32_t hc0 = threadIdx.x;
     if (ALIGN) {
         const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) >> 4) & (blockDim.x - 1);
@@ -475,7 +475,7 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     uint32_t* sK = smem;
     uint32_t* sV = sK + kMaxK * VW;
     const uint32_t E = a.E ? a.E : kStageElems;
-    SlotOp* sAdv = reinterpret_cast<SlotOp*>(sV + E * nv * VW);
+    SlotOp* sAdv = reinterpret_cast<SlotOp*>(sV + E * stage_elem_words(nv));
     SlotOp* sLk = sAdv + kMaxAdv;
     MicroOp* sMo = reinterpret_cast<MicroOp*>(sLk + kMaxLk);
     DView* sVw = reinterpret_cast<DView*>(sMo + kMaxMicro);
@@ -523,7 +523,7 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     // ---- phase A: per-element micro-ops (constants / ops / views read from LDS:
     // dynamic indexing into the by-value kernel argument would go to scratch)
     if (tid < ne && !(a.flags & (STAGE_PROBE_NOA | STAGE_PROBE_CONST)))
-        element_program(a, e, sV + tid * nv * VW, sK, sMo, sVw, pf0, in0, pf1, in1);
+        element_program(a, e, sV + tid * stage_elem_words(nv), sK, sMo, sVw, pf0, in0, pf1, in1);
     __syncthreads();
 
     // ---- phase B: advice cells, then lookup cells

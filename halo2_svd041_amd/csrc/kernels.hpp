@@ -25,7 +25,7 @@ struct ScanBatch {
     uint32_t njobs;
 };
 
-// Elements per block of the generic stage kernel (= block size; LDS: E * nv * 32 B).
+// Elements per block of the generic stage kernel (= block size; LDS: E * (nv * 32 + 16) B).
 static constexpr int kStageElems = 256;
 
 // ZkMatrix::new / ZkVector::new quantization (f64 -> Fr) of n contiguous values.

@@ -105,11 +105,17 @@ constexpr uint32_t half_desc(uint32_t off, uint32_t r, bool elem) {
 }
 static constexpr uint32_t kStageLdsPad = 64;   // over-read slack after the last table
 
+// LDS words per element in a stage block: nv values of 8 words + 4 words of
+// padding. Phase A reads / writes a value with ds_read/write_b128 at lane stride
+// stage_elem_words(nv); a stride of 4 (mod 8) words puts the 16 lanes of one
+// b128 pass on 16 distinct 4-bank groups (nv * 8 alone: 2- to 16-way conflicts).
+constexpr uint32_t stage_elem_words(uint32_t nv) { return nv * 8 + 4; }
+
 // Dynamic LDS of a stage block: constants, E elements' values, slot / micro-op
 // tables, views, and per (slot, half) descriptors (4 B) + masks (16 B) for the
 // C + L slots (constexpr: host and device).
 constexpr uint32_t stage_lds_bytes(uint32_t nv, uint32_t E, uint32_t CL = kMaxAdv + kMaxLk) {
-    return kMaxK * 32 + E * nv * 32 + (kMaxAdv + kMaxLk) * 4 + kMaxMicro * 8 + kMaxViews * 48 +
+    return kMaxK * 32 + E * stage_elem_words(nv) * 4 + (kMaxAdv + kMaxLk) * 4 + kMaxMicro * 8 + kMaxViews * 48 +
            CL * 2 * 20 + kStageLdsPad;
 }
 
