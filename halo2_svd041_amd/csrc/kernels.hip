@@ -1686,7 +1686,10 @@ template <int T, int NA>
 __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
     static_assert(256 % T == 0, "T divides the block");
     constexpr uint32_t TPR = 256 / T;                     // threads staged per round
-    __shared__ __attribute__((aligned(16))) uint32_t stage[3 * 256 * 8];
+    // a staging thread's 3T cells, padded by 16 B: a lane stride of 6T + 1
+    // (odd) 16 B units keeps each b128 store pass on distinct bank groups
+    constexpr uint32_t RS = 6 * T + 1;
+    __shared__ __attribute__((aligned(16))) uint4 stage[TPR * RS];
     __shared__ U9 wtot[4], wpre[4];
     __shared__ Fr carry_s;
     ScanJob J = B.job[0];
@@ -1760,7 +1763,7 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
                     const uint32_t j = j0 + i;
                     const Fr w = j < L ? ld_fr(wc + j) : zero;
                     const Fr si = reduce9(u9_add(loc[i], pre).w);
-                    uint4* st3 = reinterpret_cast<uint4*>(stage + ((tid % TPR) * T + i) * 24);
+                    uint4* st3 = stage + (tid % TPR) * RS + i * 6;
                     st3[0] = make_uint4(a[i].w[0], a[i].w[1], a[i].w[2], a[i].w[3]);
                     st3[1] = make_uint4(a[i].w[4], a[i].w[5], a[i].w[6], a[i].w[7]);
                     st3[2] = make_uint4(w.w[0], w.w[1], w.w[2], w.w[3]);
@@ -1772,8 +1775,7 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
             __syncthreads();
             const uint32_t ncell = 3 * min(256u, L - t0);
             uint4* o = reinterpret_cast<uint4*>(rowout + 1 + 3ull * t0);
-            const uint4* sv = reinterpret_cast<const uint4*>(stage);
-            for (uint32_t hc = tid; hc < 2 * ncell; hc += 256) o[hc] = sv[hc];
+            for (uint32_t hc = tid; hc < 2 * ncell; hc += 256) o[hc] = stage[hc + hc / (6 * T)];
             __syncthreads();
         }
     }
