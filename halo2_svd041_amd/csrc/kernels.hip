@@ -1145,7 +1145,14 @@ hipError_t launch_to_residues(const DView& x, uint32_t rows, uint32_t kdim, uint
 }
 
 static constexpr int CT = 128;     // CRT GEMM block tile (4 waves of 64 x 64)
-static constexpr int CROW = 80;    // LDS bytes per staged row (64 + 16 pad)
+// Staged operand rows are 64 B (one k-chunk) with the four 16 B parts XOR-swizzled
+// by (row >> 2) & 3: the staging stores (4 rows x 4 parts per 16 lanes) and the
+// fragment reads (16 rows x 1 part) both land on 16 distinct 4-bank groups.
+static constexpr int CROW = 64;
+static constexpr int CTS = 144;    // epilogue tile row stride (B): rows 4 apart in distinct banks
+__device__ __forceinline__ uint32_t crt_lds(uint32_t row, uint32_t part) {
+    return row * CROW + 16u * (part ^ ((row >> 2) & 3u));
+}
 
 // One (128 x 128 tile, modulus) per block: residues of C mod m_k as bytes
 // R[k][row][rpad_m]. SYM: A == B, upper tiles only.
@@ -1159,7 +1166,8 @@ __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar
     const int n = crt_nmod(*bits_a, *bits_b, lk);
     const int mod = blockIdx.y;
     if (mod >= n) return;
-    __shared__ __attribute__((aligned(16))) uint8_t S[2 * CT * CROW];
+    constexpr int kS = 2 * CT * CROW > CT * CTS ? 2 * CT * CROW : CT * CTS;
+    __shared__ __attribute__((aligned(16))) uint8_t S[kS];
     uint8_t* As = S;
     uint8_t* Bs = S + CT * CROW;
     uint32_t bi, bj;
@@ -1194,19 +1202,19 @@ __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar
     const uint32_t frow = lane & 15, fk = (lane >> 4) * 16;
     gload(0);
     for (uint32_t kc = 0; kc < kcn; ++kc) {
-        *reinterpret_cast<uint4*>(As + r0 * CROW + part * 16) = ra0;
-        *reinterpret_cast<uint4*>(As + r1 * CROW + part * 16) = ra1;
-        *reinterpret_cast<uint4*>(Bs + r0 * CROW + part * 16) = rb0;
-        *reinterpret_cast<uint4*>(Bs + r1 * CROW + part * 16) = rb1;
+        *reinterpret_cast<uint4*>(As + crt_lds(r0, part)) = ra0;
+        *reinterpret_cast<uint4*>(As + crt_lds(r1, part)) = ra1;
+        *reinterpret_cast<uint4*>(Bs + crt_lds(r0, part)) = rb0;
+        *reinterpret_cast<uint4*>(Bs + crt_lds(r1, part)) = rb1;
         __syncthreads();
         if (kc + 1 < kcn) gload(kc + 1);                      // next chunk in flight
         v4i af[4], bf[4];
 #pragma unroll
         for (int a = 0; a < 4; ++a)
-            af[a] = *reinterpret_cast<const v4i*>(As + (wr * 64 + a * 16 + frow) * CROW + fk);
+            af[a] = *reinterpret_cast<const v4i*>(As + crt_lds(wr * 64 + a * 16 + frow, fk >> 4));
 #pragma unroll
         for (int b = 0; b < 4; ++b)
-            bf[b] = *reinterpret_cast<const v4i*>(Bs + (wc * 64 + b * 16 + frow) * CROW + fk);
+            bf[b] = *reinterpret_cast<const v4i*>(Bs + crt_lds(wc * 64 + b * 16 + frow, fk >> 4));
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -1232,7 +1240,7 @@ __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar
                 r -= r >= m ? m : 0;
                 const uint32_t tr = wr * 64 + a * 16 + (lane >> 4) * 4 + reg;
                 const uint32_t tc = wc * 64 + b * 16 + (lane & 15);
-                T[tr * CT + tc] = (uint8_t)r;
+                T[tr * CTS + tc] = (uint8_t)r;
             }
     __syncthreads();
     uint8_t* Rp = R + ((uint64_t)mod * rpad_a + bi * CT) * (uint64_t)rpad_b + bj * CT;
@@ -1240,7 +1248,7 @@ __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar
     for (int q = 0; q < 4; ++q) {
         const uint32_t e = tid + q * 256, tr = e >> 3, c16 = (e & 7) * 16;
         *reinterpret_cast<uint4*>(Rp + (uint64_t)tr * rpad_b + c16) =
-            *reinterpret_cast<const uint4*>(T + tr * CT + c16);
+            *reinterpret_cast<const uint4*>(T + tr * CTS + c16);
     }
 }
 
