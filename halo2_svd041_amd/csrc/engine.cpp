@@ -2116,11 +2116,28 @@ int svdw_set_shard(svdw_ctx* c, uint32_t rank, uint32_t world) {
         c->owned.clear();
     });
 }
+// The parts of [off, off + n) of a phase's advice (lookup) stream this context
+// holds: all of it, or for a row-sharded rank the intersection with its owned
+// segments (whole row blocks).
+static std::vector<std::pair<uint64_t, uint64_t>> held(const svdw_ctx* c, uint32_t phase, bool lookup,
+                                                       uint64_t off, uint64_t n) {
+    std::vector<std::pair<uint64_t, uint64_t>> out;
+    if (!n) return out;
+    if (!sharded(c)) {
+        out.emplace_back(off, n);
+        return out;
+    }
+    for (const auto& o : c->owned) {
+        if (o.phase != phase || (o.lookup != 0) != lookup) continue;
+        const uint64_t b = std::max(off, o.off), e = std::min(off + n, o.off + o.n);
+        if (b < e) out.emplace_back(b, e - b);
+    }
+    return out;
+}
 int svdw_check_gates(svdw_ctx* c, svdw_check_result* out) {
     return guarded([&] {
         REQUIRE(c && out, "null argument");
         REQUIRE(!c->dry, "svdw_check_gates needs a device context");
-        REQUIRE(!sharded(c), "svdw_check_gates: the witness of a sharded context is partial");
         sync(c);
         memset(out, 0, sizeof *out);
         ensure_buf(c, c->chk, 6 * sizeof(unsigned long long));
@@ -2130,8 +2147,8 @@ int svdw_check_gates(svdw_ctx* c, svdw_check_result* out) {
         for (size_t k = 0; k < c->layout.size(); ++k) {
             const svdw_region& r = c->layout[k];
             const RegionChecks& rc = c->layout_chk[k];
-            if (r.nl)
-                hipck(launch_check_lookups(c->ph[r.phase].lk + r.loff, r.nl, c->LB, cnt + 2, c->st),
+            for (const auto& sg : held(c, r.phase, true, r.loff, r.nl))
+                hipck(launch_check_lookups(c->ph[r.phase].lk + sg.first, sg.second, c->LB, cnt + 2, c->st),
                       "k_check_lookups");
             const std::vector<uint32_t>* w = &rc.words;
             uint64_t unit = rc.unit;
@@ -2150,12 +2167,18 @@ int svdw_check_gates(svdw_ctx* c, svdw_check_result* out) {
                 v[q] = s.phase < 0 ? ChkView{nullptr, 0, 0, 0, 0}
                                    : ChkView{c->ph[s.phase].adv + s.off, s.rs, s.cs, s.rows, s.cols};
             }
+            const auto segs = held(c, r.phase, false, r.off, r.n);
+            if (segs.empty()) continue;
             ensure_buf(c, c->chkg, w->size() * sizeof(uint32_t));
             hipck(hipMemcpyAsync(c->chkg.p, w->data(), w->size() * sizeof(uint32_t),
                                  hipMemcpyHostToDevice, c->st), "H2D");
-            hipck(launch_check_cells(c->ph[r.phase].adv + r.off, r.n / unit, (uint32_t)unit, cols,
-                                     (const uint32_t*)c->chkg.p, (uint32_t)w->size(), v[0], v[1], cnt,
-                                     c->st), "k_check_cells");
+            for (const auto& sg : segs) {
+                if ((sg.first - r.off) % unit || sg.second % unit)
+                    fail(SVDW_EINVAL, "svdw_check_gates: owned segment is not whole elements");
+                hipck(launch_check_cells(c->ph[r.phase].adv + sg.first, (sg.first - r.off) / unit,
+                                         sg.second / unit, (uint32_t)unit, cols, (const uint32_t*)c->chkg.p,
+                                         (uint32_t)w->size(), v[0], v[1], cnt, c->st), "k_check_cells");
+            }
             hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");   // chkg is reused
         }
         unsigned long long h[6];

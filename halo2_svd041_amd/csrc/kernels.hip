@@ -1412,7 +1412,7 @@ __device__ __forceinline__ void wave_count(bool valid, bool bad, unsigned long l
         if (nb) atomicAdd(c + 1, (unsigned long long)nb);
     }
 }
-__global__ __launch_bounds__(256) void k_check_cells(const Fr* __restrict__ adv, uint64_t nunits,
+__global__ __launch_bounds__(256) void k_check_cells(const Fr* __restrict__ adv, uint64_t u0, uint64_t nunits,
                                                      uint32_t unit, uint32_t cols,
                                                      const uint32_t* __restrict__ words, uint32_t nw,
                                                      ChkView v0, ChkView v1, unsigned long long* cnt) {
@@ -1431,7 +1431,7 @@ __global__ __launch_bounds__(256) void k_check_cells(const Fr* __restrict__ adv,
             cbad = !fr_eq(ld_fr(q + chk_a(w)), ld_fr(q + chk_b(w)));
         } else {
             const ChkView v = chk_a(w) ? v1 : v0;
-            const uint64_t i = u / cols, j = u - i * cols;
+            const uint64_t i = (u0 + u) / cols, j = (u0 + u) - i * cols;
             if (v.ptr && i < v.rows && j < v.cols) {
                 copy = true;
                 cbad = !fr_eq(ld_fr(v.ptr + (int64_t)i * v.rs + (int64_t)j * v.cs), ld_fr(q + chk_b(w)));
@@ -1441,13 +1441,13 @@ __global__ __launch_bounds__(256) void k_check_cells(const Fr* __restrict__ adv,
     wave_count(gate, gbad, cnt);
     wave_count(copy, cbad, cnt + 4);
 }
-hipError_t launch_check_cells(const Fr* adv, uint64_t nunits, uint32_t unit, uint32_t cols,
+hipError_t launch_check_cells(const Fr* adv, uint64_t u0, uint64_t nunits, uint32_t unit, uint32_t cols,
                               const uint32_t* words, uint32_t nw, ChkView v0, ChkView v1,
                               unsigned long long* cnt, hipStream_t st) {
     const uint64_t n = nunits * nw;
     if (!n) return hipSuccess;
     if ((n + 255) / 256 > 0x7fffffffull || !cols) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_check_cells, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, adv,
+    hipLaunchKernelGGL(k_check_cells, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, adv, u0,
                        nunits, unit, cols, words, nw, v0, v1, cnt);
     return hipGetLastError();
 }

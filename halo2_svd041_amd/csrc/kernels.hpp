@@ -76,7 +76,8 @@ struct RegionChecks {
     uint32_t unit = 0, cols = 1;
     Src src[kMaxViews] = {{-1, 0, 0, 0, 0, 0}, {-1, 0, 0, 0, 0, 0}};
 };
-hipError_t launch_check_cells(const Fr* adv, uint64_t nunits, uint32_t unit, uint32_t cols,
+// (u0: index in the region of the first unit at adv, for the view rows / columns)
+hipError_t launch_check_cells(const Fr* adv, uint64_t u0, uint64_t nunits, uint32_t unit, uint32_t cols,
                               const uint32_t* words, uint32_t nw, ChkView v0, ChkView v1,
                               unsigned long long* cnt, hipStream_t st);
 // Physical layout (svdw_assign_columns): qb |= the gate-start bits of a region

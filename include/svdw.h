@@ -288,7 +288,9 @@ int svdw_layout(const svdw_ctx* ctx, svdw_region* out, uint64_t cap, uint64_t* n
  * range_check's last running sum against the checked value. Not checked: the
  * copies of the row scans' operands and of constant cells. An honest witness
  * has no failures; an SVD that violates a bound fails range-check copies
- * (README.md:93 "matrix-wrong", from P = 42 on). */
+ * (README.md:93 "matrix-wrong", from P = 42 on). A row-sharded context
+ * (svdw_set_shard) checks the cells it owns (svdw_shard_segments): summed over
+ * the ranks, the counts equal those of the unsharded witness. */
 typedef struct {
     uint64_t gates_checked, gate_failures;
     uint64_t lookups_checked, lookup_failures;

@@ -122,3 +122,32 @@ def test_full_size_honest_witness_satisfies(gpu_ctx_factory, N, M, P):
     assert r["gate_failures"] == 0 and r["lookup_failures"] == 0 and r["copy_failures"] == 0, r
     assert r["lookups_checked"] == cnt["lookup0"] + cnt["lookup1"]
     assert r["gates_checked"] * 4 > (cnt["advice0"] + cnt["advice1"]) // 2, (r, cnt)
+
+
+@pytest.mark.parametrize("N,M,P,world,wrong", [(40, 28, 63, 2, False), (33, 45, 32, 4, False),
+                                               (12, 12, 63, 3, True), (1024, 1024, 63, 8, False)])
+def test_sharded_check_sums_to_whole(gpu_ctx_factory, N, M, P, world, wrong):
+    """Row-sharded contexts (one per rank, here on one GPU in turn): each checks
+    the cells it owns; the per-rank counts add up to the unsharded check's, and
+    so do the failures of a matrix-wrong witness."""
+    import halo2_svd041_amd as hs
+    m, u, d, v = gen_svd_input(N, M, seed=N + M + world)
+    if wrong:
+        m = m.copy()
+        m[2][3] += 1e-7
+    g = gamma_for(world)
+    whole = gpu_ctx_factory(P)
+    hs.svd_witness(whole, m, u, v, d, g)
+    want = whole.check_gates()
+    whole.close()
+    tot = dict.fromkeys(want, 0)
+    for rank in range(world):
+        ctx = gpu_ctx_factory(P)
+        ctx.set_shard(rank, world)
+        hs.svd_witness(ctx, m, u, v, d, g)
+        r = ctx.check_gates()
+        for k in tot:
+            tot[k] += r[k]
+        ctx.close()
+    assert tot == want, (tot, want)
+    assert (want["copy_failures"] > 0) == wrong, want
