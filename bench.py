@@ -155,6 +155,8 @@ def main():
                     help="--shard rows: also time reassembling the witness after each step "
                          "(RCCL point-to-point gather to rank 0, or all-gather by segment "
                          "broadcasts), reported beside the witness-only value")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the untimed device constraint check of the last witness")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine tuning option name=value (svdw_set_option), repeatable")
     args = ap.parse_args()
@@ -255,6 +257,21 @@ def main():
                  "reassembly_ms": round(extra * 1e3, 4),
                  "moved_GB_per_step": round(moved_all * 32 / 1e9 / (2 if mode == "gather" else world), 3)}
 
+    # Untimed: the device constraint checker over the last witness (svdw_check_gates;
+    # a row-sharded rank checks the rows it owns), summed over the ranks.
+    check = None
+    if not args.no_check:
+        r = ctx.check_gates()
+        keys = sorted(r)
+        vals = [float(r[k]) for k in keys]
+        if dist is not None:
+            t = torch.tensor(vals, dtype=torch.float64,
+                             device=dev if backend == "nccl" else torch.device("cpu"))
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            vals = t.tolist()
+        check = {k: int(x) for k, x in zip(keys, vals)}
+        check["ok"] = check["gate_failures"] + check["copy_failures"] + check["lookup_failures"] == 0
+
     cells_step = cnt["advice0"] + cnt["advice1"]
     elapsed, cells_all = reduce_over_ranks(elapsed, cells_step, dist,
                                            dev if backend == "nccl" else torch.device("cpu"))
@@ -308,6 +325,8 @@ def main():
                                   "stats": stats}, indent=1), file=sys.stderr)
         if reasm is not None:
             out["reassembly"] = reasm
+        if check is not None:
+            out["witness_check"] = check
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(m, u, v, d, args.p, args.lb, g, args.cpu_rows)
         print(json.dumps(out), flush=True)
