@@ -1733,8 +1733,12 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     // Mode 1 on a row-sharded rank becomes mode 2: there the products are only a
     // row block, the st2 chain (products + phase 1) is the critical path and the
     // operand-only scans fit beside the products (tools/shard_sim.py, 8 ranks:
-    // 0.62 -> 0.54 ms); unsharded, mode 2 costs ~2 %.
-    const int p1mode = c->phase1_overlap == 1 && sharded(c) ? 2 : c->phase1_overlap;
+    // 0.62 -> 0.54 ms). So does a small witness (max(N, M) < 1024), where the
+    // st2 chain is also the critical path (tools/ab.py: 512^2 P=32 0.559 ->
+    // 0.454 ms, 768^2 P=63 1.328 -> 1.272 ms); from 1024 on it is neutral to
+    // 1 % slower.
+    const bool p1_small = std::max(N, M) < 1024;
+    const int p1mode = c->phase1_overlap == 1 && (sharded(c) || p1_small) ? 2 : c->phase1_overlap;
     const bool p1_overlap = p1mode && c->prelaunched && !c->dry;
     if (p1_overlap && p1mode == 2 && !c->st3)   // created on first use
         hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
