@@ -436,3 +436,41 @@ def test_zkvector_parity(gpu_ctx_factory, N, M, P, LB):
         for i in range(N):
             f64 = sum(A[i][j] * vec[j] for j in range(M))
             assert abs(deq(want[i].value) - f64) <= 1e-6 * max(1.0, abs(f64))
+
+
+@pytest.mark.parametrize("N,M,LB,seed", [(5, 5, 12, 0), (5, 5, 19, 1), (64, 48, 19, 2)])
+def test_field_mat_times_vec_parity(gpu_ctx_factory, N, M, LB, seed):
+    """test_field_mat_times_vec (src/matrix/test_matrix.rs:201-265; P=32, entries
+    uniform in (-100, 100), seeded here where the reference uses thread_rng):
+    ZkMatrix::new, ZkVector::new, field_mat_vec_mul, then signed_div_scale of
+    every entry (as rescale_matrix of the N x 1 result). Every cell equals the
+    oracle's, its constraint checker and the device checker pass, and the
+    dequantised results are within fixed-point error of the f64 product the
+    reference prints."""
+    import halo2_svd041_amd as hs
+    import pyoracle as po
+    from halo2_svd041_amd._lib import Mat
+    P = 32
+    rs = np.random.RandomState(seed)
+    A = rs.uniform(-100.0, 100.0, (N, M))
+    v1 = rs.uniform(-100.0, 100.0, M)
+    ctx = gpu_ctx_factory(P, LB)
+    za, zv = hs.ZkMatrix.new(ctx, A), hs.ZkVector.new(ctx, v1)
+    s = hs.field_mat_vec_mul(ctx, za, zv)
+    col = hs.ZkMatrix(ctx, Mat(s.vec.phase, s.vec.len, 1, s.vec.off, s.vec.stride, 1))
+    q = hs.ZkMatrix.rescale_matrix(ctx, col)
+    o = po.Context(phase=0)
+    rc = po.RangeChip(LB)
+    oa, ov = po.zkmatrix_new(o, P, A.tolist()), po.zkvector_new(o, P, v1.tolist())
+    os_ = po.field_mat_vec_mul(o, oa, ov)
+    oq = [po.signed_div_scale(o, rc, x, P)[0] for x in os_]
+    assert po.check_constraints(o, LB) == []
+    assert _ints(ctx.advice(0)) == o.advice
+    assert _ints(ctx.lookups(0)) == o.lookups
+    got = _ints(q.values().reshape(-1, 4))
+    assert got == [x.value for x in oq]
+    r = ctx.check_gates()
+    assert r["gate_failures"] + r["copy_failures"] + r["lookup_failures"] == 0, r
+    f64 = A @ v1
+    for i in range(N):
+        assert abs(po.to_signed(oq[i].value) / 2.0 ** P - f64[i]) <= 1e-6 * max(1.0, abs(f64[i]))
