@@ -6,6 +6,7 @@ long as the step, the step is host-bound (launch overhead), not GPU-bound.
     python tools/hosttime.py
 """
 import sys, time, os
+WORLD = int(os.environ.get("HT_WORLD", "1"))   # >1: time rank 0 of a row-sharded witness
 sys.path.insert(0, os.getcwd())
 import numpy as np, torch
 import halo2_svd041_amd as hs
@@ -15,6 +16,8 @@ for N in (512, 1024):
     dev = torch.device("cuda", 0)
     dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev) for x in (m, u, v, d))
     ctx = hs.Context(device=0, precision_bits=32 if N == 512 else 63, lookup_bits=19)
+    if WORLD > 1:
+        ctx.set_shard(0, WORLD)
     for _ in range(3): hs.svd_witness(ctx, dm, du, dv, dd, gamma_for(0))
     ctx.sync()
     ts = []
