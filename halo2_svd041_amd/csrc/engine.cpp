@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <array>
+#include <functional>
 #include <set>
 #include <stdexcept>
 #include <string>
@@ -381,6 +382,10 @@ struct svdw_ctx {
     int phase1_overlap = 1;                 // "phase1_overlap": 0 off, 1 on st2 behind the
                                             // GEMMs, 2 on st3 from quantization on
     bool prelaunched = false;               // this witness's products were queued on st2
+    int p1_at = -1;                         // "p1_at": phase 1 on st3 (mode 2) enqueued after
+                                            // phase-0 stage 0 / 1 / 2 (the u, v bounds), 3: at the
+                                            // end; -1: 0 on a row-sharded rank, else 1
+    std::function<void(const svdw_svd_payload&)> early_p1;   // that enqueue (svd_witness)
     std::vector<hipEvent_t> gemm_done;      // their completion events (this witness)
     std::vector<hipEvent_t> wait_before_cs; // verify_mul_many: wait before the c_s scans
     // Row-block sharding of one witness: this context computes the
@@ -1616,10 +1621,30 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         entries_in_desc_order(c, d, max_bits);
     }
     if (c->prelaunch_at == 1) prelaunch();
+    // svd_witness's phase 1 on the third stream, enqueued as soon as the products
+    // are (their offsets from the dry replay give the payload): with only the
+    // first phase-0 stages queued ahead of it, the third stream starts early
+    // instead of after the host has queued all of phase 0.
+    auto early_phase1 = [&](int at) {
+        const int p1_at = c->p1_at >= 0 ? c->p1_at : (sharded(c) ? 0 : 1);
+        if (!c->early_p1 || p1_at != at || !c->prelaunched || c->pre.size() != 3) return;
+        svdw_mat t_u = u, t_v = v;
+        std::swap(t_u.rows, t_u.cols); std::swap(t_u.rs, t_u.cs);
+        std::swap(t_v.rows, t_v.cols); std::swap(t_v.rs, t_v.cs);
+        const svdw_svd_payload pl{t_u, t_v, svdw_mat{m.phase, N, M, c->pre[0].off, (int64_t)M, 1},
+                                  svdw_mat{m.phase, N, N, c->pre[1].off, (int64_t)N, 1},
+                                  svdw_mat{m.phase, M, M, c->pre[2].off, (int64_t)M, 1}};
+        auto f = std::move(c->early_p1);
+        c->early_p1 = nullptr;
+        f(pl);
+    };
+    early_phase1(0);
     BigU unit = big_from_u128(((unsigned __int128)1 << P) + 1);
     check_mat_entries_bounded(c, u, unit);
+    early_phase1(1);
     if (c->prelaunch_at == 2) prelaunch();
     check_mat_entries_bounded(c, v, unit);
+    early_phase1(2);
     svdw_mat ut = u, vt = v;
     std::swap(ut.rows, ut.cols); std::swap(ut.rs, ut.cs);
     std::swap(vt.rows, vt.cols); std::swap(vt.rs, vt.cs);
@@ -1721,15 +1746,13 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         c->bits_pending = true;
         c->qmat[0] = zm; c->qmat[1] = zu; c->qmat[2] = zv;
     }
-    svdw_svd_payload pl =
-        check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits, dbits, true);
-    fetch_bits(c);
-    // Phase 1 needs only the products (already queued on st2), the quantized
-    // operands and gamma: run it on st2 behind the GEMMs, concurrently with the
-    // HBM-bound phase-0 checks still on st (its row scans are VALU-bound), and
-    // join the streams afterwards.
+    // Phase 1 needs only the products (queued on st2 by check_svd_phase0), the
+    // quantized operands and gamma: run it on st2 behind the GEMMs, concurrently
+    // with the HBM-bound phase-0 checks still on st (its row scans are
+    // VALU-bound), and join the streams afterwards.
     // Mode 2: on a third stream that starts after quantization; the b.g and
-    // a.(b.g) scans run at once, the c_s.g scans wait for the products.
+    // a.(b.g) scans run at once, the c_s.g scans wait for the products; queued
+    // from inside check_svd_phase0 right after its first stage (p1_at).
     // Mode 1 on a row-sharded rank becomes mode 2: there the products are only a
     // row block, the st2 chain (products + phase 1) is the critical path and the
     // operand-only scans fit beside the products (tools/shard_sim.py, 8 ranks:
@@ -1739,24 +1762,40 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     // 1 % slower.
     const bool p1_small = std::max(N, M) < 1024;
     const int p1mode = c->phase1_overlap == 1 && (sharded(c) || p1_small) ? 2 : c->phase1_overlap;
+    bool p1_queued = false;
+    auto queue_phase1 = [&](const svdw_svd_payload& pl, bool overlap) {
+        fetch_bits(c);
+        const bool p1_overlap = p1mode && overlap;
+        if (p1_overlap && p1mode == 2 && !c->st3)   // created on first use
+            hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
+        hipStream_t p1s = p1mode == 2 ? c->st3 : c->st2;
+        if (p1_overlap && p1s == c->st3) {
+            hipck(hipStreamWaitEvent(c->st3, c->ev_bits, 0), "hipStreamWaitEvent");
+            c->wait_before_cs = c->gemm_done;
+        }
+        {
+            struct Swap {
+                svdw_ctx* c;
+                hipStream_t* other;
+                Swap(svdw_ctx* cc, hipStream_t* o) : c(cc), other(o) { if (other) std::swap(c->st, *other); }
+                ~Swap() { if (other) std::swap(c->st, *other); }
+            } sw(c, p1_overlap ? (p1s == c->st3 ? &c->st3 : &c->st2) : nullptr);
+            check_svd_phase1(c, zm, zu, zv, pl, gamma);
+        }
+        c->wait_before_cs.clear();
+        p1_queued = true;
+    };
+    struct Clear {
+        svdw_ctx* c;
+        ~Clear() { c->early_p1 = nullptr; }
+    } clr{c};
+    if (p1mode == 2 && !c->dry) c->early_p1 = [&](const svdw_svd_payload& pl) { queue_phase1(pl, true); };
+    svdw_svd_payload pl =
+        check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits, dbits, true);
+    c->early_p1 = nullptr;
     const bool p1_overlap = p1mode && c->prelaunched && !c->dry;
-    if (p1_overlap && p1mode == 2 && !c->st3)   // created on first use
-        hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
     hipStream_t p1s = p1mode == 2 ? c->st3 : c->st2;
-    if (p1_overlap && p1s == c->st3) {
-        hipck(hipStreamWaitEvent(c->st3, c->ev_bits, 0), "hipStreamWaitEvent");
-        c->wait_before_cs = c->gemm_done;
-    }
-    {
-        struct Swap {
-            svdw_ctx* c;
-            hipStream_t* other;
-            Swap(svdw_ctx* cc, hipStream_t* o) : c(cc), other(o) { if (other) std::swap(c->st, *other); }
-            ~Swap() { if (other) std::swap(c->st, *other); }
-        } sw(c, p1_overlap ? (p1s == c->st3 ? &c->st3 : &c->st2) : nullptr);
-        check_svd_phase1(c, zm, zu, zv, pl, gamma);
-    }
-    c->wait_before_cs.clear();
+    if (!p1_queued) queue_phase1(pl, p1_overlap);
     if (p1_overlap) stream_dep(c, p1s, c->st);
     // st2 also carries the d checks and single cells queued aside (and, with
     // phase 1 on st3, nothing else joins it): join it too
@@ -2493,6 +2532,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "prelaunch_at") {
             REQUIRE(value >= 0 && value <= 2, "prelaunch_at: 0, 1 or 2");
             c->prelaunch_at = (int)value;
+        } else if (n == "p1_at") {
+            REQUIRE(value >= -1 && value <= 3, "p1_at: -1 (auto), 0, 1, 2 or 3");
+            c->p1_at = (int)value;
         } else if (n == "scan_impl") {
             REQUIRE(value >= 1 && value <= 5, "scan_impl: 1..5");
             c->scan_impl = (int)value;

@@ -30,7 +30,8 @@ def parse_variant(s):
 
 DEFAULTS = {"gemm_impl": 0, "scan_impl": 4, "overlap": 1, "prelaunch_at": 0, "gemm_priority": 0,
             "gemm_rt": 1, "gemm_crt": 1, "stage_elems": 256, "phase1_overlap": 1, "stage_probe": 0,
-            "stage_align": 1, "cu_split": 0, "stage_inc": 0, "stage_priority": 0, "fused_quantize": 1, "d_checks_aside": 1}
+            "stage_align": 1, "cu_split": 0, "stage_inc": 0, "stage_priority": 0, "fused_quantize": 1, "d_checks_aside": 1,
+            "p1_at": -1}
 # pseudo-option "prof": event profiler during the timed steps (0 off, 1 all, 2 k_stage only)
 PROF_PREFIX = {1: "", 2: "k_stage"}
 
