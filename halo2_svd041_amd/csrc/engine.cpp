@@ -384,7 +384,8 @@ struct svdw_ctx {
     bool prelaunched = false;               // this witness's products were queued on st2
     int p1_at = -1;                         // "p1_at": phase 1 on st3 (mode 2) enqueued after
                                             // phase-0 stage 0 / 1 / 2 (the u, v bounds), 3: at the
-                                            // end; -1: 0 on a row-sharded rank, else 1
+                                            // end; -1: auto (tools/shard_sim.py --opt p1_at=):
+                                            // 0 on a rank of >= 4, 3 of 2-3, else 1
     std::function<void(const svdw_svd_payload&)> early_p1;   // that enqueue (svd_witness)
     std::vector<hipEvent_t> gemm_done;      // their completion events (this witness)
     std::vector<hipEvent_t> wait_before_cs; // verify_mul_many: wait before the c_s scans
@@ -1626,7 +1627,8 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     // first phase-0 stages queued ahead of it, the third stream starts early
     // instead of after the host has queued all of phase 0.
     auto early_phase1 = [&](int at) {
-        const int p1_at = c->p1_at >= 0 ? c->p1_at : (sharded(c) ? 0 : 1);
+        const int p1_at = c->p1_at >= 0 ? c->p1_at
+                                         : (!sharded(c) ? 1 : (c->shard_world >= 4 ? 0 : 3));
         if (!c->early_p1 || p1_at != at || !c->prelaunched || c->pre.size() != 3) return;
         svdw_mat t_u = u, t_v = v;
         std::swap(t_u.rows, t_u.cols); std::swap(t_u.rs, t_u.cs);

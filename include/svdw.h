@@ -212,7 +212,8 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   on, its c_s scans waiting for the products / after phase 0; 1 acts as 2 on
  *   a row-sharded context and when max(N, M) < 1024); "p1_at" -1 | 0 | 1 | 2 | 3
  *   (with phase 1 on the third stream: queued after the first 0 / 1 / 2
- *   phase-0 stages, 3 after all of phase 0; -1: 0 on a row-sharded rank, else 1); "prelaunch_at" 0 | 1 | 2 (how many phase-0 stages
+ *   phase-0 stages, 3 after all of phase 0; -1: 0 on a rank of a >= 4-way shard, 3 of a
+ *   2-3-way shard, else 1); "prelaunch_at" 0 | 1 | 2 (how many phase-0 stages
  *   are queued before them); "gemm_priority" 0 | 1 (second stream priority:
  *   default | high); "stage_priority" 0 | 1 (cell stream priority);
  *   "cu_split" 0 | multiple of 8 (CUs masked to the second stream, the rest to
