@@ -319,6 +319,15 @@ def main():
                 roof["standalone"] = {k: solo[k] for k in ("achieved", "frac", "avg_launch_ms")}
                 roof["standalone"]["note"] = ("same kernel, one extra untimed step with the "
                                               "streams serialised (no concurrent products/scans)")
+            # SURVEY.md §8(d) stage (i): the whole step against HBM, algorithmic
+            # bytes = 32 B per advice + lookup cell + 8 B per f64 input entry
+            if not rows_mode:
+                step_bytes = (32 * (cells_step + cnt["lookup0"] + cnt["lookup1"])
+                              + 8 * (N * M + N * N + M * M + min(N, M)))
+                ach = step_bytes / (elapsed / args.steps) / 1e9
+                roof["step"] = {"bytes": step_bytes, "achieved": round(ach, 1),
+                                "frac": round(ach / roof["peak"], 4),
+                                "note": "whole witness per step (all kernels, both streams)"}
             out["roofline"] = roof
             if args.breakdown:
                 print(json.dumps({"ms_per_step_by_kernel": breakdown,
