@@ -95,6 +95,16 @@ int main(int argc, char** argv) {
     printf("advice0[0] = %016llx%016llx%016llx%016llx (m[0][0]=%.17g)\n",
            (unsigned long long)cell[3], (unsigned long long)cell[2],
            (unsigned long long)cell[1], (unsigned long long)cell[0], m[0]);
+    /* README.md:93: "SVD should verify on matrix but fail on matrix-wrong" */
+    svdw_check_result chk;
+    CHECK(svdw_check_gates(ctx, &chk));
+    const int ok = chk.gate_failures + chk.copy_failures + chk.lookup_failures == 0;
+    printf("constraints: %llu gates (%llu failed), %llu copies (%llu failed), %llu lookups "
+           "(%llu failed): SVD %s\n",
+           (unsigned long long)chk.gates_checked, (unsigned long long)chk.gate_failures,
+           (unsigned long long)chk.copies_checked, (unsigned long long)chk.copy_failures,
+           (unsigned long long)chk.lookups_checked, (unsigned long long)chk.lookup_failures,
+           ok ? "verifies" : "does NOT verify");
     CHECK(svdw_ctx_destroy(ctx));
     free(u); free(v); free(m); free(d);
     return 0;
