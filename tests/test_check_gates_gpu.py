@@ -182,3 +182,19 @@ def test_readme_kat_on_reference_files(gpu_ctx_factory, name, P):
     assert (r["gate_failures"], r["lookup_failures"]) == (gbad, lbad) == (0, 0), r
     assert (r["copy_failures"] > 0) == (cbad > 0), (r, cbad)
     assert (cbad > 0) == ("wrong" in name and P >= 42)
+
+
+@pytest.mark.parametrize("P,expect_fail", [(63, True), (32, False)])
+def test_full_size_matrix_wrong(gpu_ctx_factory, P, expect_fail):
+    """README.md:93 at the bench size (1024^2): input-creator.py's perturbation
+    of one entry by 1e-7 fails the check at P=63 and, the reference weakness
+    SURVEY.md §4 notes, not at P=32 (its tolerance exceeds 1e-7 there)."""
+    import halo2_svd041_amd as hs
+    m, u, d, v = gen_svd_input(1024, 1024, seed=77)
+    m = m.copy()
+    m[512][300] += 1e-7
+    ctx = gpu_ctx_factory(P)
+    hs.svd_witness(ctx, m, u, v, d, gamma_for(5))
+    r = ctx.check_gates()
+    assert r["gate_failures"] == 0 and r["lookup_failures"] == 0, r
+    assert (r["copy_failures"] > 0) == expect_fail, r
