@@ -124,6 +124,10 @@ def test_modular_api_matches_whole_witness(gpu_ctx_factory):
     hs.check_svd_phase1(ctx, zm, zu, zv, pl, g)
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
     _assert_streams(ctx, a0, l0, a1)
+    whole = gpu_ctx_factory(P)                   # the device checker sees the same witness
+    hs.svd_witness(whole, m, u, v, d, g)
+    r, rw = ctx.check_gates(), whole.check_gates()
+    assert r == rw and r["gate_failures"] + r["copy_failures"] + r["lookup_failures"] == 0, (r, rw)
 
 
 @pytest.mark.parametrize("impl", ["mfma", "valu"])
