@@ -1175,6 +1175,16 @@ __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar
         uint32_t b = blockIdx.x, r = 0, rowlen = tiles_m;
         while (b >= rowlen) { b -= rowlen; ++r; --rowlen; }
         bi = r; bj = r + b;
+    } else if ((gridDim.x & 7) == 0 && (gridDim.x / tiles_m) % 2 == 0) {
+        // Blocks b and b + 8 share an XCD (and its L2): give each XCD a contiguous
+        // run of the tiles in 2-row groups (a 2 x 4 block of tiles at 1024^2), so
+        // an XCD reads 2 row tiles of A and 4 column tiles of B per modulus
+        // instead of all 8 row tiles of A.
+        const uint32_t per = gridDim.x >> 3;
+        const uint32_t t = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+        const uint32_t grp = t / (2 * tiles_m), w = t - grp * 2 * tiles_m;
+        bi = grp * 2 + (w & 1);
+        bj = w >> 1;
     } else {
         bi = blockIdx.x / tiles_m;
         bj = blockIdx.x % tiles_m;
