@@ -1415,49 +1415,61 @@ hipError_t launch_gemm_mont(const DView& A, const DView& B, uint32_t N, uint32_t
 // witness on the device (halo2-base's basic gate q * (a + b*c - d) = 0 at every
 // enabled offset, and the lookup table [0, 2^lb)); copy constraints are not
 // checked here. One thread per (unit, gate); counts via one atomic per wave.
-__device__ __forceinline__ void wave_count(bool valid, bool bad, unsigned long long* c) {
-    const uint64_t nv = __popcll(__ballot(valid)), nb = __popcll(__ballot(bad));
-    if ((threadIdx.x & 63) == 0) {
-        if (nv) atomicAdd(c, (unsigned long long)nv);
-        if (nb) atomicAdd(c + 1, (unsigned long long)nb);
-    }
+// Checker kernels: grid-stride, per-thread counts reduced in LDS, one global
+// atomic per block and counter (per-wave atomics on one address serialise).
+__device__ __forceinline__ void block_flush(const uint32_t (&v)[4], unsigned long long* c0,
+                                            unsigned long long* c1) {
+    __shared__ unsigned long long s[4];
+    if (threadIdx.x < 4) s[threadIdx.x] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (v[k]) atomicAdd(&s[k], (unsigned long long)v[k]);
+    __syncthreads();
+    if (threadIdx.x < 2 && c0 && s[threadIdx.x]) atomicAdd(c0 + threadIdx.x, s[threadIdx.x]);
+    if (threadIdx.x >= 2 && threadIdx.x < 4 && c1 && s[threadIdx.x])
+        atomicAdd(c1 + threadIdx.x - 2, s[threadIdx.x]);
+}
+static inline unsigned check_grid(uint64_t n) {
+    const uint64_t b = (n + 255) / 256;
+    return (unsigned)(b < 4096 ? b : 4096);
 }
 __global__ __launch_bounds__(256) void k_check_cells(const Fr* __restrict__ adv, uint64_t u0, uint64_t nunits,
                                                      uint32_t unit, uint32_t cols,
                                                      const uint32_t* __restrict__ words, uint32_t nw,
                                                      ChkView v0, ChkView v1, unsigned long long* cnt) {
-    const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool gate = false, gbad = false, copy = false, cbad = false;
-    if (idx < nunits * nw) {
+    uint32_t v[4] = {0, 0, 0, 0};   // gates checked / failed, copies checked / failed
+    const uint64_t n = nunits * nw;
+    for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+         idx += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t u = idx / nw;
         const uint32_t w = words[idx - u * nw];
         const Fr* q = adv + u * unit;
         if (chk_kind(w) == CHK_GATE) {
             const Fr* g = q + w;
-            gate = true;
-            gbad = !fr_eq(fr_add(ld_fr(g), fr_mul(ld_fr(g + 1), ld_fr(g + 2))), ld_fr(g + 3));
+            ++v[0];
+            v[1] += !fr_eq(fr_add(ld_fr(g), fr_mul(ld_fr(g + 1), ld_fr(g + 2))), ld_fr(g + 3));
         } else if (chk_kind(w) == CHK_COPY) {
-            copy = true;
-            cbad = !fr_eq(ld_fr(q + chk_a(w)), ld_fr(q + chk_b(w)));
+            ++v[2];
+            v[3] += !fr_eq(ld_fr(q + chk_a(w)), ld_fr(q + chk_b(w)));
         } else {
-            const ChkView v = chk_a(w) ? v1 : v0;
+            const ChkView vw = chk_a(w) ? v1 : v0;
             const uint64_t i = (u0 + u) / cols, j = (u0 + u) - i * cols;
-            if (v.ptr && i < v.rows && j < v.cols) {
-                copy = true;
-                cbad = !fr_eq(ld_fr(v.ptr + (int64_t)i * v.rs + (int64_t)j * v.cs), ld_fr(q + chk_b(w)));
+            if (vw.ptr && i < vw.rows && j < vw.cols) {
+                ++v[2];
+                v[3] += !fr_eq(ld_fr(vw.ptr + (int64_t)i * vw.rs + (int64_t)j * vw.cs), ld_fr(q + chk_b(w)));
             }
         }
     }
-    wave_count(gate, gbad, cnt);
-    wave_count(copy, cbad, cnt + 4);
+    block_flush(v, cnt, cnt + 4);
 }
 hipError_t launch_check_cells(const Fr* adv, uint64_t u0, uint64_t nunits, uint32_t unit, uint32_t cols,
                               const uint32_t* words, uint32_t nw, ChkView v0, ChkView v1,
                               unsigned long long* cnt, hipStream_t st) {
     const uint64_t n = nunits * nw;
     if (!n) return hipSuccess;
-    if ((n + 255) / 256 > 0x7fffffffull || !cols) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_check_cells, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, adv, u0,
+    if (!cols) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_check_cells, dim3(check_grid(n)), dim3(256), 0, st, adv, u0,
                        nunits, unit, cols, words, nw, v0, v1, cnt);
     return hipGetLastError();
 }
@@ -1513,26 +1525,29 @@ hipError_t launch_selectors(uint8_t* q, const uint32_t* qb, uint64_t start, uint
 __global__ __launch_bounds__(256) void k_check_physical(const Fr* __restrict__ cols,
                                                         const uint8_t* __restrict__ q, uint64_t rows,
                                                         uint32_t ncols, unsigned long long* cnt) {
-    const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool gate = false, gbad = false;
-    if (idx < rows * ncols) {
+    uint32_t v[4] = {0, 0, 0, 0};
+    const uint64_t n = rows * ncols;
+    for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+         idx += (uint64_t)gridDim.x * blockDim.x) {
+        if (!q[idx]) continue;
         const uint64_t col = idx / rows, r = idx - col * rows;
         const Fr* g = cols + idx;
-        if (q[idx]) {
-            gate = true;
-            gbad = r + 3 >= rows ||
-                   !fr_eq(fr_add(ld_fr(g), fr_mul(ld_fr(g + 1), ld_fr(g + 2))), ld_fr(g + 3));
-        }
+        ++v[0];
+        v[1] += r + 3 >= rows ||
+                !fr_eq(fr_add(ld_fr(g), fr_mul(ld_fr(g + 1), ld_fr(g + 2))), ld_fr(g + 3));
     }
-    wave_count(gate, gbad, cnt);
+    block_flush(v, cnt, nullptr);
 }
 // the break cell of column c (row bp[c]) == row 0 of column c + 1
-__global__ void k_check_breaks(const Fr* __restrict__ cols, uint64_t rows, const uint64_t* __restrict__ bp,
-                               uint32_t nb, unsigned long long* cnt) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    bool bad = false;
-    if (c < nb) bad = bp[c] >= rows || !fr_eq(ld_fr(cols + c * rows + bp[c]), ld_fr(cols + (c + 1) * rows));
-    wave_count(c < nb, bad, cnt);
+__global__ __launch_bounds__(256) void k_check_breaks(const Fr* __restrict__ cols, uint64_t rows,
+                                                      const uint64_t* __restrict__ bp, uint32_t nb,
+                                                      unsigned long long* cnt) {
+    uint32_t v[4] = {0, 0, 0, 0};
+    for (uint32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < nb; c += gridDim.x * blockDim.x) {
+        ++v[0];
+        v[1] += bp[c] >= rows || !fr_eq(ld_fr(cols + c * rows + bp[c]), ld_fr(cols + (c + 1) * rows));
+    }
+    block_flush(v, cnt, nullptr);
 }
 hipError_t launch_check_breaks(const Fr* cols, uint64_t rows, const uint64_t* bp, uint32_t nb,
                                unsigned long long* cnt, hipStream_t st) {
@@ -1544,32 +1559,33 @@ hipError_t launch_check_physical(const Fr* cols, const uint8_t* q, uint64_t rows
                                  unsigned long long* cnt, hipStream_t st) {
     const uint64_t n = rows * ncols;
     if (!n) return hipSuccess;
-    if ((n + 255) / 256 > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_check_physical, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, cols, q, rows,
+    hipLaunchKernelGGL(k_check_physical, dim3(check_grid(n)), dim3(256), 0, st, cols, q, rows,
                        ncols, cnt);
     return hipGetLastError();
 }
 __global__ __launch_bounds__(256) void k_check_lookups(const Fr* __restrict__ lk, uint64_t n,
                                                        uint32_t lb, unsigned long long* cnt) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool valid = i < n;
-    bool bad = false;
-    if (valid) {
-        const Fr v = ld_fr(lk + i);
+    uint32_t v[4] = {0, 0, 0, 0};
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const Fr x = ld_fr(lk + i);
+        bool bad = false;
 #pragma unroll
         for (int w = 0; w < 8; ++w) {
             const int keep = (int)lb - 32 * w;
             const uint32_t m = keep >= 32 ? 0u : (keep <= 0 ? 0xffffffffu : ~((1u << keep) - 1u));
-            bad |= (v.w[w] & m) != 0;
+            bad |= (x.w[w] & m) != 0;
         }
+        ++v[0];
+        v[1] += bad;
     }
-    wave_count(valid, bad, cnt);
+    block_flush(v, cnt, nullptr);
 }
 hipError_t launch_check_lookups(const Fr* lk, uint64_t n, uint32_t lb, unsigned long long* cnt,
                                 hipStream_t st) {
     if (!n) return hipSuccess;
     if ((n + 255) / 256 > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_check_lookups, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, lk, n,
+    hipLaunchKernelGGL(k_check_lookups, dim3(check_grid(n)), dim3(256), 0, st, lk, n,
                        lb, cnt);
     return hipGetLastError();
 }

@@ -19,7 +19,7 @@ rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.
 if [ $rc -ne 0 ]; then exit $rc; fi
 if [ "${PROF:-0}" = "1" ]; then
   export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 bench.py --n $N --steps 5 --warmup 2 --no-cpu-baseline --no-profile > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 bench.py --n $N --steps 5 --warmup 2 --no-cpu-baseline --no-profile --no-check > gpurun_out/prof_bench.json 2> gpurun_out/prof_bench.err
   rc=$?; echo "rocprof rc=$rc"; find gpurun_out/prof_$TAG -name "*stats*" | head
 fi
 exit $rc
