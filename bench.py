@@ -1,24 +1,39 @@
 #!/usr/bin/env python3
 """bench.py — SVD-verify witness generation throughput (advice cells / s).
 
-One step = the whole witness of examples/svd_example.rs:98-200 for one
-N x M matrix (ZkMatrix::new m,u,v + ZkVector::new d, check_svd_phase0 into
-phase 0, check_svd_phase1 into phase 1), f64 inputs resident in HBM when the
-clock starts, complete advice + lookup streams resident in HBM when it stops.
+Workloads (BASELINE.json configs):
+  svd        (default) one step = the whole witness of examples/svd_example.rs:98-200
+             for one N x M matrix (ZkMatrix::new m,u,v + ZkVector::new d,
+             check_svd_phase0 into phase 0, check_svd_phase1 into phase 1).
+             1 GPU: configs[3]'s shape 1024 x 1024, PRECISION_BITS=63.
+             --n 512 --p 32: configs[2]; --n 2048 --m 1024 --p 32: configs[4].
+  verify_mul the README.md:32-46 recipe: ZkMatrix::new a, b; c_s =
+             honest_prover_mat_mul(a, b) in phase 0; verify_mul(a, b, c_s, gamma)
+             in phase 1 (configs[1]: 256 x 256, PRECISION_BITS=32).
+f64 inputs are resident in HBM when the clock starts, the complete advice +
+lookup streams are resident in HBM when it stops. Every step draws a fresh
+gamma (sha256(seed, step) mod p), as a prover gets a fresh challenge per witness.
 
-Default workload: BASELINE.json configs[3] shape (1024 x 1024, PRECISION_BITS=63,
-LOOKUP_BITS=19) on one GPU. With --gpus N (torch.distributed.run, one rank per
-GPU) every rank generates its own matrix (independent objects, no data-path
-collective): weak scaling, value = cells of all ranks / max-over-ranks time.
+Multi-GPU: `--gpus N` without a torch.distributed environment starts N ranks
+itself (a torch.distributed.run child process; this process never touches the
+GPU) and exits with its status. One rank per GPU:
+  --shard rows      (default for N > 1, configs[3]) one matrix row-block sharded
+                    over the ranks (svdw_set_shard): strong scaling, the witness
+                    stays sharded-resident; --gather root|all also times its
+                    reassembly over RCCL, reported beside the witness-only value.
+  --shard replicas  (configs[4]) one matrix per rank, no data-path collective:
+                    weak scaling, value = cells of all ranks / max-over-ranks time.
+--dry rehearses the launch and the rank logic on CPU (gloo, the engine's dry
+planner instead of a device): no GPU, timings are host planning only.
 
 Output: ONE JSON line on rank 0 (driver contract), including
-  roofline     dominant kernel (k_stage, the cell-program stage kernel), from
-               HIP events the engine records around each of its launches on
-               its own stream during the timed steps (svdw_profile_*; only that
-               kernel is bracketed, so the clock sees two event packets per
-               stage launch and nothing else),
-  cpu_baseline the single-threaded C oracle (oracle/svdw_oracle.c, a port of
-               the reference algorithm) on a bounded row sample, rank 0 only.
+  roofline     dominant kernel, from HIP events the engine records around each
+               of its launches on its own stream during the timed steps
+               (svdw_profile_*; filtered by --profile-prefix),
+  cpu_baseline the single-threaded C oracle (oracle/svdw_oracle.c, a port of the
+               reference algorithm) on a bounded sample of the same workload, in a
+               child process pinned to core 0 (taskset -c 0) that runs to
+               completion before this process first touches the GPU; rank 0, N=1.
 """
 from __future__ import annotations
 
@@ -26,6 +41,9 @@ import argparse
 import hashlib
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
 import time
 
@@ -49,8 +67,19 @@ def gen_input(N, M, seed):
     return m, U, D, V
 
 
+def gen_matmul_input(N, K, M, seed):
+    """README.md:32-46 recipe operands: a (N x K), b (K x M), entries U(-1, 1)."""
+    rs = np.random.RandomState(seed)
+    return rs.uniform(-1, 1, size=(N, K)), rs.uniform(-1, 1, size=(K, M))
+
+
 def gamma_for(seed) -> int:
     return int.from_bytes(hashlib.sha256(f"svdw-gamma-{seed}".encode()).digest(), "little") % P_MOD
+
+
+def step_gammas(seed, steps, offset=0):
+    """A fresh challenge per witness (the RLC gamma of svd_example.rs:181-184)."""
+    return [gamma_for(f"{seed}-{offset + i}") for i in range(steps)]
 
 
 def roofline_from_profile(stats, steps):
@@ -100,7 +129,7 @@ def reduce_over_ranks(elapsed, cells_step, dist, device):
     return float(t.item()), float(c.item())
 
 
-def pmc_traffic(kernel, N, M, P, LB):
+def pmc_traffic(kernel, workload, N, M, P, LB):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
     summary of this exact workload (profiles/*_pmc_summary.json, written by
     tools/pmc_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE passes)."""
@@ -112,23 +141,132 @@ def pmc_traffic(kernel, N, M, P, LB):
                 s = json.load(fh)
         except (OSError, ValueError):
             continue
-        if s.get("config") == want and kernel in s.get("kernels", {}):
+        if (s.get("config") == want and s.get("workload", "svd") == workload
+                and kernel in s.get("kernels", {})):
             return s["kernels"][kernel]["traffic_per_launch"], os.path.relpath(f, ROOT)
     return None, None
 
 
-def cpu_baseline(m, u, v, d, P, LB, g, rows):
+# ----------------------------------------------------------------- CPU baseline
+def cpu_info():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(),
+            "affinity": len(os.sched_getaffinity(0))}
+
+
+def cpu_baseline_run(spec):
+    """The C oracle on a bounded sample of the workload (runs in the child)."""
     sys.path.insert(0, ORACLE_DIR)
     import corc  # oracle/ — the checker / reported baseline only
-    t0 = time.perf_counter()
-    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, LB, g, row_lim=rows)
-    dt = time.perf_counter() - t0
-    cells = a0.shape[0] + a1.shape[0]
+    if spec["workload"] == "svd":
+        m, u, d, v = gen_input(spec["N"], spec["M"], spec["seed"])
+        g = step_gammas(spec["seed"], 1)[0]
+        t0 = time.perf_counter()
+        a0, l0, a1 = corc.svd_witness(m, u, v, d, spec["P"], spec["LB"], g, row_lim=spec["rows"])
+        dt = time.perf_counter() - t0
+        cells = a0.shape[0] + a1.shape[0]
+        sample = (f"oracle/svdw_oracle.c single thread, same {spec['N']}x{spec['M']} P={spec['P']} "
+                  f"witness restricted to rows [0,{spec['rows']}) of every row-parallel stage "
+                  f"(+ all loads and d checks): {cells} advice cells in {dt:.2f} s")
+    else:
+        a, b = gen_matmul_input(spec["N"], spec["N"], spec["M"], spec["seed"])
+        g = step_gammas(spec["seed"], 1)[0]
+        t0 = time.perf_counter()
+        a0, a1 = corc.verify_mul_witness(a, b, spec["P"], g)
+        dt = time.perf_counter() - t0
+        cells = a0.shape[0] + a1.shape[0]
+        sample = (f"oracle/svdw_oracle.c single thread, the whole {spec['N']}x{spec['N']} . "
+                  f"{spec['N']}x{spec['M']} P={spec['P']} verify_mul witness (loads, naive "
+                  f"i-j-k Fr GEMM, Freivalds rows): {cells} advice cells in {dt:.2f} s")
     return {"value": round(cells / dt, 1), "unit": "advice cells/s", "cores": 1, "kind": "port",
-            "sample": (f"oracle/svdw_oracle.c single thread, same {m.shape[0]}x{m.shape[1]} P={P} "
-                       f"witness restricted to rows [0,{rows}) of every row-parallel stage "
-                       f"(+ all loads and d checks): {cells} advice cells in {dt:.2f} s"),
-            "seconds": round(dt, 3)}
+            "sample": sample, "seconds": round(dt, 3), **cpu_info()}
+
+
+def cpu_baseline_child(spec):
+    """Runs the baseline in a fresh process pinned to core 0 (taskset -c 0) and
+    waits for it; called before this process touches the GPU."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", json.dumps(spec)]
+    if shutil.which("taskset"):
+        cmd = ["taskset", "-c", "0"] + cmd
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        return {"error": r.stderr.strip()[-400:]}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["pinning"] = "taskset -c 0" if cmd[0] == "taskset" else "none"
+    return out
+
+
+# ----------------------------------------------------------------- launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` outside torch.distributed: run N ranks as a child
+    torch.distributed.run process (this process never initialises the GPU and
+    never execs) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)]
+    env = dict(os.environ)
+    # the ranks read this process's arguments from the environment (torchrun's
+    # own parser would claim abbreviations such as --n)
+    env["BENCH_ARGV"] = json.dumps(sys.argv[1:])
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+# ----------------------------------------------------------------- workloads
+class SvdWorkload:
+    def __init__(self, hs, ctx, args, N, M, rank, rows_mode, dev):
+        import torch
+        self.hs, self.ctx = hs, ctx
+        m, u, d, v, _ = rank_workload(args.seed, 0 if rows_mode else rank, N, M)
+        self.host = (m, u, v, d)
+        if dev is None:                       # dry planner: host arrays
+            self.inp = (m, u, v, d)
+        else:
+            self.inp = tuple(torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev)
+                             for x in (m, u, v, d))
+
+    def step(self, gamma):
+        return self.hs.svd_witness(self.ctx, *self.inp, gamma)
+
+
+class VerifyMulWorkload:
+    """README.md:32-46 as one step: loads of a and b, c_s = a * b (phase 0),
+    verify_mul(a, b, c_s, gamma) (phase 1)."""
+
+    def __init__(self, hs, ctx, args, N, M, rank, rows_mode, dev):
+        import torch
+        self.hs, self.ctx = hs, ctx
+        a, b = gen_matmul_input(N, N, M, args.seed + rank)
+        self.host = (a, b)
+        self.inp = (a, b) if dev is None else tuple(
+            torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev) for x in (a, b))
+
+    def step(self, gamma):
+        hs, ctx = self.hs, self.ctx
+        ctx.reset()
+        za = hs.ZkMatrix.new(ctx, self.inp[0])
+        zb = hs.ZkMatrix.new(ctx, self.inp[1])
+        cs = hs.honest_prover_mat_mul(ctx, za, zb)
+        hs.ZkMatrix.verify_mul(ctx, za, zb, cs, gamma)
+        return {"advice0": ctx.advice_len(0), "advice1": ctx.advice_len(1),
+                "lookup0": ctx.lookup_len(0), "lookup1": ctx.lookup_len(1)}
 
 
 def main():
@@ -136,96 +274,134 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--workload", choices=["svd", "verify_mul"], default="svd")
+    ap.add_argument("--n", type=int, default=None, help="rows (default 1024 svd, 256 verify_mul)")
     ap.add_argument("--m", type=int, default=None)
-    ap.add_argument("--p", type=int, default=63)
+    ap.add_argument("--p", type=int, default=None, help="PRECISION_BITS (default 63 svd, 32 verify_mul)")
     ap.add_argument("--lb", type=int, default=19)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-rows", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-child", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--no-profile", action="store_true",
                     help="skip the engine's event profiler in the timed region")
-    ap.add_argument("--profile-prefix", default="k_stage",
-                    help="kernel-name prefix the timed-region profiler records ('' = all)")
+    ap.add_argument("--profile-prefix", default=None,
+                    help="kernel-name prefix the timed-region profiler records "
+                         "(default k_stage for svd, all kernels for verify_mul)")
     ap.add_argument("--breakdown", action="store_true", help="print per-kernel ms/step to stderr")
-    ap.add_argument("--shard", choices=["replicas", "rows"], default="replicas",
-                    help="N>1: one matrix per rank (weak scaling, default) or one matrix "
-                         "row-block sharded over the ranks (strong scaling, BASELINE config 4)")
+    ap.add_argument("--shard", choices=["replicas", "rows"], default=None,
+                    help="N>1: one matrix row-block sharded over the ranks (default; strong "
+                         "scaling, BASELINE config 4) or one matrix per rank (weak scaling, "
+                         "config 5)")
     ap.add_argument("--gather", choices=["none", "root", "all"], default="none",
                     help="--shard rows: also time reassembling the witness after each step "
-                         "(RCCL point-to-point gather to rank 0, or all-gather by segment "
-                         "broadcasts), reported beside the witness-only value")
+                         "(RCCL gather to rank 0 or all-gather), reported beside the "
+                         "witness-only value")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the untimed device constraint check of the last witness")
+    ap.add_argument("--dry", action="store_true",
+                    help="CPU rehearsal: gloo + the engine's dry planner, no GPU")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine tuning option name=value (svdw_set_option), repeatable")
-    args = ap.parse_args()
-    N = args.n
-    M = args.m or N
+    argv = json.loads(os.environ["BENCH_ARGV"]) if "BENCH_ARGV" in os.environ else None
+    args = ap.parse_args(argv)
 
+    if args.cpu_baseline_child is not None:
+        print(json.dumps(cpu_baseline_run(json.loads(args.cpu_baseline_child))), flush=True)
+        return 0
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus)
+
+    svd = args.workload == "svd"
+    N = args.n or (1024 if svd else 256)
+    M = args.m or N
+    P = args.p or (63 if svd else 32)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    shard = args.shard or ("rows" if world > 1 and svd else "replicas")
+    rows_mode = shard == "rows" and world > 1
+    if rows_mode and not svd:
+        raise SystemExit("bench.py: --shard rows is the SVD witness's row-block sharding")
+
+    # CPU baseline first, in a pinned child, before this process touches the GPU
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry:
+        cpu = cpu_baseline_child({"workload": args.workload, "N": N, "M": M, "P": P,
+                                  "LB": args.lb, "seed": args.seed, "rows": args.cpu_rows})
+        try:
+            os.sched_setaffinity(0, set(os.sched_getaffinity(0)) - {0} or {0})
+        except OSError:
+            pass
+
     import torch
-    # Rehearsal on fewer GPUs than ranks (e.g. a 1-GPU box): BENCH_DIST_BACKEND=gloo
-    # and ranks share devices round-robin. Timings are then not per-GPU numbers.
-    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % max(torch.cuda.device_count(), 1)
+    backend = "gloo" if args.dry else os.environ.get("BENCH_DIST_BACKEND", "nccl")
     dist = None
+    dev = None
+    if not args.dry:
+        # Rehearsal on fewer GPUs than ranks (BENCH_DIST_BACKEND=gloo): ranks share
+        # devices round-robin; timings are then not per-GPU numbers.
+        if backend != "nccl":
+            local = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist  # noqa: F811
-        torch.cuda.set_device(local)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(local)
+        assert dist.get_world_size() == world == args.gpus
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     import halo2_svd041_amd as hs
-
-    rows_mode = args.shard == "rows" and world > 1
-    m, u, d, v, g = rank_workload(args.seed, 0 if rows_mode else rank, N, M)
-    dev = torch.device("cuda", local)
-    dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev)
-                      for x in (m, u, v, d))
-    torch.cuda.synchronize()
-    ctx = hs.Context(device=local, precision_bits=args.p, lookup_bits=args.lb)
+    ctx = hs.Context(device=-1 if args.dry else local, precision_bits=P, lookup_bits=args.lb)
     for kv in args.opt:
         name, _, val = kv.partition("=")
         ctx.set_option(name, int(val))
     if rows_mode:
         ctx.set_shard(rank, world)
+    wl = (SvdWorkload if svd else VerifyMulWorkload)(hs, ctx, args, N, M, rank, rows_mode, dev)
 
-    for _ in range(args.warmup):
-        cnt = hs.svd_witness(ctx, dm, du, dv, dd, g)
-    ctx.sync()
+    def sync():
+        if not args.dry:
+            ctx.sync()
+            torch.cuda.synchronize()
 
-    if not args.no_profile:
-        ctx.profile(True, args.profile_prefix)
+    warm_g = step_gammas(args.seed, args.warmup, offset=10 ** 6)
+    gammas = step_gammas(args.seed, args.steps)
+    for g in warm_g:
+        cnt = wl.step(g)
+    sync()
+
+    profile = not args.no_profile and not args.dry
+    prefix = args.profile_prefix if args.profile_prefix is not None else ("k_stage" if svd else "")
+    if profile:
+        ctx.profile(True, prefix)
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        cnt = hs.svd_witness(ctx, dm, du, dv, dd, g)
-    ctx.sync()
-    torch.cuda.synchronize()
+    for g in gammas:
+        cnt = wl.step(g)
+    sync()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    stats = ctx.profile_collect() if not args.no_profile else []
+    stats = ctx.profile_collect() if profile else []
+    cells_step = cnt["advice0"] + cnt["advice1"]
 
-    # The same kernel alone on the GPU (one untimed step with both streams
+    # The same kernel alone on the GPU (one untimed step with the streams
     # serialised): its intrinsic rate, reported beside the contended in-step rate.
     solo = None
-    if not args.no_profile and not rows_mode:
+    if profile and svd and not rows_mode:
         ctx.set_option("overlap", 0)
         ctx.set_option("phase1_overlap", 0)
-        ctx.profile(True, args.profile_prefix)
-        hs.svd_witness(ctx, dm, du, dv, dd, g)
-        ctx.sync()
+        ctx.profile(True, prefix)
+        wl.step(gammas[-1])
+        sync()
         solo_stats = ctx.profile_collect()
         ctx.profile(False)
         ctx.set_option("overlap", 1)
@@ -234,53 +410,55 @@ def main():
             _, solo, _ = roofline_from_profile(solo_stats, 1)
 
     reasm = None
-    if rows_mode and args.gather != "none":
+    if rows_mode and args.gather != "none" and not args.dry:
         # witness + reassembly per step, timed like the witness-only loop
         from halo2_svd041_amd import collect
         mode = "gather" if args.gather == "root" else "all_gather"
-        collect.reassemble(ctx, rank, world, mode)        # warm the communicator
+        plan = collect.plan(ctx, rank, world, mode)
+        collect.reassemble(ctx, plan)                    # warm the communicator
         dist.barrier()
-        torch.cuda.synchronize()
+        sync()
         t1 = time.perf_counter()
-        moved = 0
-        for _ in range(args.steps):
-            hs.svd_witness(ctx, dm, du, dv, dd, g)
-            moved = collect.reassemble(ctx, rank, world, mode)["cells"]
-        torch.cuda.synchronize()
+        for g in gammas:
+            wl.step(g)
+            collect.reassemble(ctx, plan)
+        sync()
         dist.barrier()
         el2 = time.perf_counter() - t1
-        el2, moved_all = reduce_over_ranks(el2, moved, dist, dev if backend == "nccl"
-                                           else torch.device("cpu"))
-        extra = el2 / args.steps - elapsed / args.steps
-        reasm = {"mode": mode, "ms_per_step_with_reassembly": round(el2 / args.steps * 1e3, 4),
+        el2, _ = reduce_over_ranks(el2, 0, dist, red_dev)
+        reasm = {"mode": mode, "collectives_per_step": plan.collectives,
+                 "ms_per_step_with_reassembly": round(el2 / args.steps * 1e3, 4),
                  "value_with_reassembly": round(cells_step * args.steps / el2, 1),
-                 "reassembly_ms": round(extra * 1e3, 4),
-                 "moved_GB_per_step": round(moved_all * 32 / 1e9 / (2 if mode == "gather" else world), 3)}
+                 "reassembly_ms": round((el2 - elapsed) / args.steps * 1e3, 4),
+                 "moved_GB_per_step": round(plan.moved_cells * 32 / 1e9, 3)}
 
     # Untimed: the device constraint checker over the last witness (svdw_check_gates;
     # a row-sharded rank checks the rows it owns), summed over the ranks.
     check = None
-    if not args.no_check:
+    if not args.no_check and not args.dry:
         r = ctx.check_gates()
         keys = sorted(r)
         vals = [float(r[k]) for k in keys]
         if dist is not None:
-            t = torch.tensor(vals, dtype=torch.float64,
-                             device=dev if backend == "nccl" else torch.device("cpu"))
+            t = torch.tensor(vals, dtype=torch.float64, device=red_dev)
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
             vals = t.tolist()
         check = {k: int(x) for k, x in zip(keys, vals)}
         check["ok"] = check["gate_failures"] + check["copy_failures"] + check["lookup_failures"] == 0
 
-    cells_step = cnt["advice0"] + cnt["advice1"]
-    elapsed, cells_all = reduce_over_ranks(elapsed, cells_step, dist,
-                                           dev if backend == "nccl" else torch.device("cpu"))
+    elapsed, cells_all = reduce_over_ranks(elapsed, cells_step, dist, red_dev)
     if rows_mode:
         cells_all = float(cells_step)        # one witness, split over the ranks
-    total_cells = cells_all * args.steps
-    value = total_cells / elapsed
+    value = cells_all * args.steps / elapsed
 
     if rank == 0:
+        if svd:
+            workload = (f"svd_verify_witness N={N} M={M} PRECISION_BITS={P} LOOKUP_BITS={args.lb}, "
+                        + ("one matrix row-sharded over the GPUs" if rows_mode
+                           else "one matrix per GPU"))
+        else:
+            workload = (f"verify_mul (README.md:32-46 recipe) a {N}x{N} . b {N}x{M} "
+                        f"PRECISION_BITS={P}, one product per GPU")
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -293,25 +471,26 @@ def main():
             "scaling": "strong" if rows_mode else "weak",
             "vs_baseline": None,
             "dtype": "bn254_fr (u32 limbs; exact multi-modular int8 MFMA GEMM)",
-            "data": "synthetic (input-creator.py recipe, seeded; gamma = sha256 mod p)",
+            "data": ("dry planner rehearsal on CPU (no GPU: timings are host planning only)"
+                     if args.dry else
+                     "synthetic (input-creator.py recipe, seeded; fresh gamma = sha256 mod p "
+                     "per step)"),
             "config": {
-                "workload": (f"svd_verify_witness N={N} M={M} PRECISION_BITS={args.p} "
-                             f"LOOKUP_BITS={args.lb}, "
-                             + ("one matrix row-sharded over the GPUs" if rows_mode
-                                else "one matrix per GPU")),
-                "N": N, "M": M, "precision_bits": args.p, "lookup_bits": args.lb,
-                "advice_cells_per_matrix": cells_step,
-                "lookup_cells_per_matrix": cnt["lookup0"] + cnt["lookup1"],
+                "workload": workload,
+                "N": N, "M": M, "precision_bits": P, "lookup_bits": args.lb,
+                "advice_cells_per_step": cells_step,
+                "lookup_cells_per_step": cnt["lookup0"] + cnt["lookup1"],
                 "parallelism": (f"row blocks x{world} of one matrix (witness kept sharded; "
                                 f"reassembly timed separately with --gather)"
                                 if rows_mode else f"replicas x{world} (no data-path collective)"),
+                "ranks": world,
+                "backend": backend if world > 1 else None,
             },
         }
         if stats:
             kname, roof, breakdown = roofline_from_profile(stats, args.steps)
-            # the committed PMC summary is for the whole witness on one GPU
-            traffic, src = (None, None) if rows_mode else pmc_traffic(kname, N, M, args.p,
-                                                                         args.lb)
+            traffic, src = (None, None) if rows_mode else pmc_traffic(
+                kname, args.workload, N, M, P, args.lb)
             if traffic is not None:
                 roof["traffic"] = traffic
                 roof["traffic_source"] = src
@@ -322,12 +501,12 @@ def main():
             # SURVEY.md §8(d) stage (i): the whole step against HBM, algorithmic
             # bytes = 32 B per advice + lookup cell + 8 B per f64 input entry
             if not rows_mode:
-                step_bytes = (32 * (cells_step + cnt["lookup0"] + cnt["lookup1"])
-                              + 8 * (N * M + N * N + M * M + min(N, M)))
+                nin = (N * M + N * N + M * M + min(N, M)) if svd else (N * N + N * M)
+                step_bytes = 32 * (cells_step + cnt["lookup0"] + cnt["lookup1"]) + 8 * nin
                 ach = step_bytes / (elapsed / args.steps) / 1e9
                 roof["step"] = {"bytes": step_bytes, "achieved": round(ach, 1),
                                 "frac": round(ach / roof["peak"], 4),
-                                "note": "whole witness per step (all kernels, both streams)"}
+                                "note": "whole witness per step (all kernels, all streams)"}
             out["roofline"] = roof
             if args.breakdown:
                 print(json.dumps({"ms_per_step_by_kernel": breakdown,
@@ -336,13 +515,16 @@ def main():
             out["reassembly"] = reasm
         if check is not None:
             out["witness_check"] = check
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(m, u, v, d, args.p, args.lb, g, args.cpu_rows)
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
+            if "value" in cpu:
+                out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 1)
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -64,6 +64,7 @@ class Context:
         self.lookup_bits = lookup_bits
         self.device = device
         self._phys = None
+        self.last_svd = None
         self._h = ct.c_void_p()
         p = Params(device, precision_bits, lookup_bits)
         check(lib().svdw_ctx_create(ct.byref(p), ct.byref(self._h)))
@@ -478,6 +479,7 @@ def svd_witness(ctx: Context, m, u, v, d, gamma: int, cfg: SvdConfigPy = SvdConf
             raise SvdwError(-1, "svd_witness: shapes must be m NxM, u NxN, v MxM, d min(N,M)")
         check(lib().svdw_svd_witness(ctx.handle, *[a.ctypes.data for a in arrs], N, M, 0,
                                      ct.byref(cfgc), g.ctypes.data, ct.byref(cnt)))
+    ctx.last_svd = (int(N), int(M), cfg)        # for collect.plan (shard segment replay)
     return cnt.as_dict()
 
 

@@ -37,6 +37,11 @@ def lib():
             ct.c_size_t,
             ct.POINTER(u64p), ct.POINTER(ct.c_size_t), ct.POINTER(u64p), ct.POINTER(ct.c_size_t),
             ct.POINTER(u64p), ct.POINTER(ct.c_size_t)]
+        L.orc_verify_mul_witness.restype = ct.c_int
+        L.orc_verify_mul_witness.argtypes = [
+            ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_size_t, ct.c_size_t, ct.c_size_t, ct.c_int,
+            ct.c_void_p, ct.POINTER(u64p), ct.POINTER(ct.c_size_t), ct.POINTER(u64p),
+            ct.POINTER(ct.c_size_t)]
         L.orc_free.argtypes = [ct.c_void_p]
         L.orc_err_calc.argtypes = [ct.c_int, ct.c_size_t, ct.c_double, ct.c_double, ct.c_double,
                                    ct.POINTER(ct.c_double), ct.POINTER(ct.c_double)]
@@ -86,6 +91,28 @@ def svd_witness(m, u, v, d, p: int, lb: int, gamma: int, max_norm=100.0, eps_svd
     if rc != 0:
         raise ValueError(f"orc_svd_witness failed: {rc}")
     return _take(a0, n0.value), _take(l0, nl0.value), _take(a1, n1.value)
+
+
+def verify_mul_witness(a, b, p: int, gamma: int, b_wrong=None):
+    """README.md:32-46 recipe: phase-0 loads of a, b (and b_wrong), c_s = a * (b_wrong
+    or b); phase-1 verify_mul(a, b, c_s, gamma). Returns (advice0, advice1)."""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    bw = None if b_wrong is None else np.ascontiguousarray(b_wrong, dtype=np.float64)
+    n, k = a.shape
+    k2, m = b.shape
+    if k2 != k or (bw is not None and bw.shape != b.shape):
+        raise ValueError("verify_mul_witness: shape mismatch")
+    g = int_to_limbs(gamma)
+    a0, a1 = ct.POINTER(ct.c_uint64)(), ct.POINTER(ct.c_uint64)()
+    n0, n1 = ct.c_size_t(), ct.c_size_t()
+    rc = lib().orc_verify_mul_witness(a.ctypes.data, b.ctypes.data,
+                                      None if bw is None else bw.ctypes.data, n, k, m, p,
+                                      g.ctypes.data, ct.byref(a0), ct.byref(n0), ct.byref(a1),
+                                      ct.byref(n1))
+    if rc != 0:
+        raise ValueError(f"orc_verify_mul_witness failed: {rc}")
+    return _take(a0, n0.value), _take(a1, n1.value)
 
 
 def err_calc(p, size, max_norm=100.0, eps_svd=1e-10, eps_u=1e-10):

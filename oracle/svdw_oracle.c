@@ -428,6 +428,33 @@ int orc_svd_witness(const double *m, const double *u, const double *v, const dou
     return 0;
 }
 
+/*
+ * Matrix-multiplication recipe of README.md:32-46 (BASELINE config 2): phase 0
+ * loads a (n x k) and b (k x m) with ZkMatrix::new (src/matrix/mod.rs:230-252),
+ * then c_s = honest_prover_mat_mul(a, b) (:546-568); phase 1 runs
+ * verify_mul(a, b, c_s, gamma) (:299-342). A dishonest prover is modelled by
+ * bw != NULL: a third matrix (k x m) is loaded after b and c_s = a * bw, so
+ * every row whose Freivalds sums differ gets non-trivial is_equal cells.
+ */
+int orc_verify_mul_witness(const double *a, const double *b, const double *bw, size_t n,
+                           size_t k, size_t m, int p, const uint64_t gamma_c[4],
+                           uint64_t **adv0, size_t *n0, uint64_t **adv1, size_t *n1) {
+    if (p < 1 || p > 63 || !n || !k || !m) return -1;
+    octx c0; ctx_init(&c0, 19);
+    omat za = orc_load_mat(&c0, a, n, k, p);
+    omat zb = orc_load_mat(&c0, b, k, m, p);
+    omat zw = zb;
+    if (bw) zw = orc_load_mat(&c0, bw, k, m, p);
+    omat cs = honest_prover_mat_mul(&c0, za, zw, (size_t)-1);
+    octx c1; ctx_init(&c1, 19);
+    verify_mul(&c1, &c0, za, zb, cs, fe_from_canon(gamma_c), (size_t)-1);
+    out_cells(&c0, adv0, n0, NULL, NULL);
+    out_cells(&c1, adv1, n1, NULL, NULL);
+    ctx_free(&c0); ctx_free(&c1);
+    free(za.idx); free(zb.idx); if (bw) free(zw.idx); free(cs.idx);
+    return 0;
+}
+
 void orc_free(void *p) { free(p); }
 
 /* Field KAT helpers for tests: canonical in/out. */

@@ -45,19 +45,19 @@ def _worker(rank, world, port, mode, shape, out):
         cnt = hs.svd_witness(ctx, m, u, v, d, 99)
         sizes = {(0, 0): cnt["advice0"], (1, 0): cnt["advice1"],
                  (0, 1): cnt["lookup0"], (1, 1): cnt["lookup1"]}
-        segs = collect.all_segments(ctx.shard_segments(), rank, world)
+        plan = collect.plan(ctx, rank, world, mode)          # planner replay, no exchange
+        segs = plan.segments
         streams = {k: torch.zeros((n, 32), dtype=torch.uint8) for k, n in sizes.items()}
         for owner, ph, lk, off, n in segs:                    # this rank's own cells only
             if owner == rank:
                 streams[(ph, lk)][off:off + n] = _expected((ph, lk), sizes[(ph, lk)])[off:off + n]
-        if mode == "gather":
-            moved = collect.gather(streams, segs, rank, root=0)
-        else:
-            moved = collect.all_gather(streams, segs)
+        calls0 = collect.stats["collective_calls"]
+        moved = collect.exchange(streams, plan)
+        calls = collect.stats["collective_calls"] - calls0
         ok = {}
         for k, n in sizes.items():
             ok[k] = bool(torch.equal(streams[k], _expected(k, n)))
-        out[rank] = (ok, moved, len(segs))
+        out[rank] = (ok, moved, len(segs), calls, len(plan.sends) + len(plan.recvs))
         ctx.close()
     finally:
         dist.destroy_process_group()
@@ -71,8 +71,10 @@ def test_reassembly_gloo(mode, world, shape):
     out = mgr.dict()
     mp.spawn(_worker, args=(world, port, mode, shape, out), nprocs=world, join=True)
     for rank in range(world):
-        ok, moved, nseg = out[rank]
+        ok, moved, nseg, calls, nops = out[rank]
         assert nseg >= world
+        # one grouped exchange per reassembly, whatever the segment count
+        assert calls == (1 if nops else 0)
         if mode == "all_gather" or rank == 0:
             assert all(ok.values()), (rank, ok)
         else:                                        # non-roots keep their own rows only

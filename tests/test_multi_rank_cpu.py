@@ -56,3 +56,21 @@ def test_single_rank_reduce_is_identity():
     sys.path.insert(0, ROOT)
     import bench
     assert bench.reduce_over_ranks(0.5, 1234, None, None) == (0.5, 1234.0)
+
+
+@pytest.mark.parametrize("extra", [[], ["--shard", "replicas"]])
+def test_bench_gpus_flag_launches_ranks(extra):
+    """`bench.py --gpus 2` outside torch.distributed starts two ranks itself (a
+    torch.distributed.run child); --dry rehearses them on CPU (gloo + planner)."""
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry",
+                        "--n", "32", "--steps", "2", "--warmup", "1"] + extra,
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout                 # rank 0 prints one JSON line
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["ranks"] == 2
+    assert out["scaling"] == ("weak" if extra else "strong")
+    assert out["config"]["backend"] == "gloo"

@@ -1,0 +1,96 @@
+"""BASELINE config 2: the matrix-multiplication recipe of README.md:32-46 as a
+standalone workload -- phase 0 ZkMatrix::new(a), ZkMatrix::new(b),
+c_s = honest_prover_mat_mul(a, b); phase 1 ZkMatrix::verify_mul(a, b, c_s, gamma)
+(src/matrix/mod.rs:230-252, 546-568, 299-342).
+
+CPU: the C oracle's recipe (oracle/svdw_oracle.c orc_verify_mul_witness) is pinned
+against the Python restatement, honest and dishonest, and its cell counts against
+the closed form of README.md:51 (~9 N^2 for verify_mul).
+GPU: the full advice streams of the engine (modular C ABI) at 256 x 256, P=32
+equal the C oracle's, for an honest c_s and for a c_s computed from a perturbed b
+(then every is_equal row carries a non-zero difference and its inverse).
+"""
+import numpy as np
+import pytest
+
+import corc
+import pyoracle as po
+from conftest import P_MOD, gamma_for
+
+
+def _inputs(n, k, m, seed):
+    rs = np.random.RandomState(seed)
+    a = rs.uniform(-1, 1, (n, k))
+    b = rs.uniform(-1, 1, (k, m))
+    bw = b.copy()
+    bw[k // 2, m // 3] += 0.5              # one wrong entry of b: c_s wrong in one column
+    return a, b, bw
+
+
+def _ints(cells):
+    c = cells.astype(object)
+    return [int(r[0]) | int(r[1]) << 64 | int(r[2]) << 128 | int(r[3]) << 192 for r in c]
+
+
+def vm_cells(n, k, m):
+    """Phase-1 cells of verify_mul."""
+    return 1 + 4 * (m - 1) + n * (3 * m + 1) + k * (3 * m + 1) + n * (3 * k + 1) + 12 * n
+
+
+@pytest.mark.parametrize("wrong", [False, True])
+@pytest.mark.parametrize("n,k,m,P", [(5, 7, 4, 32), (6, 6, 6, 63), (1, 3, 1, 42)])
+def test_c_oracle_recipe_matches_python(n, k, m, P, wrong):
+    a, b, bw = _inputs(n, k, m, seed=n * 100 + k * 10 + m)
+    g = gamma_for(n + k + m)
+    c0, c1 = corc.verify_mul_witness(a, b, P, g, b_wrong=bw if wrong else None)
+    o0, o1, orlc = po.Context(phase=0), po.Context(phase=1), po.Context(phase=1)
+    oa = po.zkmatrix_new(o0, P, a.tolist())
+    ob = po.zkmatrix_new(o0, P, b.tolist())
+    ow = po.zkmatrix_new(o0, P, bw.tolist()) if wrong else ob
+    ocs = po.honest_prover_mat_mul(o0, oa, ow)
+    po.verify_mul(o1, oa, ob, ocs, po.load_witness(orlc, g))
+    assert _ints(c0) == o0.advice
+    assert _ints(c1) == o1.advice
+    assert len(c0) == n * k + k * m * (2 if wrong else 1) + n * m
+    assert len(c1) == vm_cells(n, k, m)
+
+
+def test_verify_mul_is_about_9n2_at_256():
+    n = 256
+    assert abs(vm_cells(n, n, n) / n ** 2 - 9) < 0.1          # README.md:51
+
+
+def _is_equal_diffs(a1, n, k, m):
+    """The n is_equal blocks close the phase-1 stream: [d, b, 1, a, z, d, inv, 1, 0, d, z, 0]."""
+    blocks = _ints(a1[len(a1) - 12 * n:])
+    return [(blk[0], blk[4], blk[6]) for blk in (blocks[12 * i:12 * i + 12] for i in range(n))]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wrong", [False, True])
+def test_config2_verify_mul_256_full_stream(gpu_ctx_factory, wrong):
+    """BASELINE config 2 at full size: 256 x 256, PRECISION_BITS=32, bit-exact vs CPU."""
+    import halo2_svd041_amd as hs
+    n = k = m = 256
+    P = 32
+    a, b, bw = _inputs(n, k, m, seed=2)
+    g = gamma_for(2)
+    ctx = gpu_ctx_factory(P)
+    za, zb = hs.ZkMatrix.new(ctx, a), hs.ZkMatrix.new(ctx, b)
+    zw = hs.ZkMatrix.new(ctx, bw) if wrong else zb
+    cs = hs.honest_prover_mat_mul(ctx, za, zw)
+    hs.ZkMatrix.verify_mul(ctx, za, zb, cs, g)
+    c0, c1 = corc.verify_mul_witness(a, b, P, g, b_wrong=bw if wrong else None)
+    g0, g1 = ctx.advice(0), ctx.advice(1)
+    assert g0.shape == c0.shape and g1.shape == c1.shape
+    assert np.array_equal(g0, c0), "phase-0 advice differs from the C oracle"
+    assert np.array_equal(g1, c1), "phase-1 advice differs from the C oracle"
+    diffs = _is_equal_diffs(g1, n, k, m)
+    if wrong:
+        # a[i][k/2] != 0 for every row: every Freivalds row differs, is_zero = 0,
+        # and the witness carries the inverse of the difference
+        assert all(d != 0 and z == 0 and d * inv % P_MOD == 1 for d, z, inv in diffs)
+    else:
+        assert all(d == 0 and z == 1 for d, z, inv in diffs)
+    chk = ctx.check_gates()
+    assert chk["gate_failures"] == 0 and chk["lookup_failures"] == 0 and chk["copy_failures"] == 0
