@@ -338,13 +338,21 @@ struct svdw_ctx {
     hipStream_t st = nullptr;
     uint32_t P = 32, LB = 19;
     Stream ph[2];
-    DBuf f64in, digA, digB, digC, w1c, w1m, w2c, w2m, bits, gpc, gpm, crtR, gbits, chk, chkg;
-    DBuf wbc[kMaxScanJobs], wbs[kMaxScanJobs];   // b.v per batched verify_mul (canonical, scaled)
-    // gamma^j cache (canonical gpc / Montgomery gpm), shared by verify_mul calls
+    DBuf f64in, digA, digB, digC, w1c, w1t, w2c, w2t, bits, gpc, gtab, crtR, gbits, chk, chkg;
+    DBuf wbc[kMaxScanJobs], wbt[kMaxScanJobs];   // b.v per batched verify_mul (canonical, table)
+    // gamma^j (canonical gpc, scaled table gtab, kernels.hpp kTabSlots) of the
+    // current verify_mul calls: recomputed for every witness (a fresh challenge
+    // each time). svd_witness queues it first thing on a side stream (gp_ev).
     Fr gp_gamma{};
     uint32_t gp_len = 0;
-    DBuf gps[9];                            // gamma powers * 2^(32 na), valid if gps_ok bit na
-    uint32_t gps_ok = 0;
+    hipEvent_t gp_ev = nullptr;             // gamma_prep queued ahead (svd_witness)
+    // Device bit-length words of matrices written in this witness (svd_witness:
+    // quantized m, u, v at dbitw[0..2]): the row scans decide their operand
+    // width on the device from these (NaSpec), so the host never waits for them.
+    struct DevBits { svdw_mat m; int16_t word; };
+    std::vector<DevBits> dwords;
+    const unsigned* dbitw = nullptr;
+    bool scan_na_host = false;              // "scan_na_host": host reads the bounds (A/B)
     // Known magnitude bounds of matrices written in this witness: cell (i, j) of
     // `m` satisfies |signed value| < 2^bits. Cleared with the streams.
     struct MatBits { svdw_mat m; uint32_t bits; };
@@ -502,6 +510,8 @@ static void clear_streams(svdw_ctx* c) {
     for (auto& s : c->ph) { s.n = 0; s.nl = 0; }
     c->mbits.clear();
     c->prods.clear();
+    c->dwords.clear();
+    c->dbitw = nullptr;
 }
 // RAII: brackets one kernel launch with HIP events on the context stream.
 struct ProfScope {
@@ -1206,29 +1216,67 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
     return cs;
 }
 // Words of the small operand for the row-scan products: |signed a| < 2^(32 na)
-// when a's bound is known (scan_impl 4 / 5), else 8 (full Montgomery product).
+// when a's bound is known to the host (scan_impl 4 / 5), else 8 (full Montgomery).
 static int scan_na(const svdw_ctx* c, const svdw_mat& a) {
     if (c->scan_impl < 4) return 8;
     const uint32_t b = bits_of(c, a);
     if (b == ~0u || b > 192) return 8;
     return std::max(1, (int)((b + 31) / 32));
 }
-// Factor f with mont_mul(w, f) = w * 2^(32 na) mod p (na = 8: Montgomery form).
-static Fr scale_factor(int na) {
-    if (na >= 8) return fr_r2();
-    Fr x = fr_zero();
-    x.w[na] = 1;                                          // 2^(32 na) < p for na <= 6
-    return mont_mul(x, fr_r2());
+// The same bound as the device sees it: a quantized matrix's bit-length word, or
+// a product of two of them (bits_a + bits_b + lk); wa = -1: unknown.
+static NaSpec scan_spec(const svdw_ctx* c, const svdw_mat& a) {
+    auto word = [&](const svdw_mat& m) -> int16_t {
+        for (auto& r : c->dwords)
+            if (same_cells(r.m, m)) return r.word;
+        return -1;
+    };
+    const int16_t w = word(a);
+    if (w >= 0) return NaSpec{w, -1, 0, 0};
+    for (auto& p : c->prods)
+        if (same_cells(p.cs, a)) {
+            const int16_t wa = word(p.a), wb = word(p.b);
+            if (wa >= 0 && wb >= 0) return NaSpec{wa, wb, (uint16_t)p.lk, 0};
+        }
+    return NaSpec{-1, -1, 0, 0};
 }
-// Scaled copies of a vector: ws = w * 2^(32 na) mod p (see scan_na) and, for
-// na < 8, wn = -ws.
-struct WScaled {
-    const Fr* ws;
-    const Fr* wn;
-};
-// field_mat_vec_mul with the vector given as canonical + scaled copies.
+// A scan job's bound for the device: host-known bits as a constant (wa = -2,
+// bits in lk), else its device words (scan_spec).
+static NaSpec job_spec(const svdw_ctx* c, const svdw_mat& a) {
+    const uint32_t b = bits_of(c, a);
+    if (b != ~0u) return NaSpec{-2, -1, (uint16_t)std::min(b, 65535u), 0};
+    return scan_spec(c, a);
+}
+// na of a batch of scans: host-known (1..8), or 0 = decided on the device from
+// the jobs' specs (job_spec), so the host needs no operand bounds
+static int batch_na_host(const svdw_ctx* c, const svdw_mat* ms, int n) {
+    if (c->scan_impl == 3) return 8;
+    if (c->scan_impl < 3) return 8;
+    int na = 1;
+    bool host = true, dev = c->scan_impl >= 4 && c->dbitw && !c->scan_na_host;
+    for (int i = 0; i < n; ++i) {
+        if (bits_of(c, ms[i]) != ~0u) na = std::max(na, scan_na(c, ms[i]));
+        else host = false;
+        if (job_spec(c, ms[i]).wa == -1) dev = false;
+    }
+    if (host) return na;
+    return dev ? 0 : 8;
+}
+// mont_mul(w, f[s]) = slot s of w's scaled table: w * 2^(32 (s + 1)) for s < 6,
+// w's Montgomery form for s = 6 (kernels.hpp kTabSlots)
+static ScaleTab scale_tab() {
+    ScaleTab t;
+    for (int s = 0; s < kTabSlots - 1; ++s) {
+        Fr x = fr_zero();
+        x.w[s + 1] = 1;                                    // 2^(32 (s + 1)) < p
+        t.f[s] = mont_mul(x, fr_r2());
+    }
+    t.f[kTabSlots - 1] = fr_r2();
+    return t;
+}
+// field_mat_vec_mul with the vector given as canonical copy + scaled table.
 static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const Fr* wc,
-                            WScaled w, int na) {
+                            const Fr* tab, int na) {
     const uint32_t R = a.rows, L = a.cols;
     uint64_t off;
     append(c, phase, (uint64_t)R * (3ull * L + 1), 0, &off, nullptr, "scan", R);
@@ -1240,61 +1288,39 @@ static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, cons
     }
     if (!c->dry) {
         ProfScope ps(c, c->st, a.cs == 1 ? "k_matvec_scan:rows" : "k_matvec_scan:cols", 32.0 * (double)R * (4.0 * L + 1) + 64.0 * L, (double)R * L);
-        hipck(launch_matvec_scan(view_of(c, a), (uint32_t)r0, (uint32_t)r1, L, wc, w.ws, w.wn,
+        hipck(launch_matvec_scan(view_of(c, a), (uint32_t)r0, (uint32_t)r1, L, wc, tab,
                                  cellp(c, phase, off + r0 * (3ull * L + 1)), c->scan_impl, na,
                                  c->st), "k_matvec_scan");
     }
     return svdw_vec{phase, R, off + 3ull * L, (int64_t)(3ull * L + 1)};
 }
-// canonical copy into bc, scaled copies into bm ([0, len): ws, [len, 2 len): -ws)
-static WScaled vec_prep(svdw_ctx* c, const svdw_vec& v, DBuf& bc, DBuf& bm, int na) {
-    ensure_buf(c, bc, (size_t)v.len * sizeof(Fr));
-    ensure_buf(c, bm, 2 * (size_t)v.len * sizeof(Fr));
-    Fr* ws = (Fr*)bm.p;
-    Fr* wn = na < 8 && ws ? ws + v.len : nullptr;
-    if (!c->dry)
-        hipck(launch_vec_prep(view_of(c, svdw_mat{v.phase, 1, v.len, v.off, 0, v.stride}), v.len,
-                              (Fr*)bc.p, ws, wn, scale_factor(na), c->st), "k_vec_prep");
-    return WScaled{ws, wn};
+// canonical copy into bc, scaled table into bt
+static const Fr* vec_prep_view(svdw_ctx* c, const DView& w, uint32_t len, DBuf& bc, DBuf& bt) {
+    ensure_buf(c, bc, (size_t)len * sizeof(Fr));
+    ensure_buf(c, bt, tab_len(len) * sizeof(Fr));
+    if (!c->dry) {
+        ProfScope ps(c, c->st, "k_vec_prep", 32.0 * len * (2 + tab_len(1)), 0);
+        hipck(launch_vec_prep(w, len, (Fr*)bc.p, (Fr*)bt.p, scale_tab(), c->st), "k_vec_prep");
+    }
+    return (const Fr*)bt.p;
+}
+static const Fr* vec_prep(svdw_ctx* c, const svdw_vec& v, DBuf& bc, DBuf& bt) {
+    return vec_prep_view(c, view_of(c, svdw_mat{v.phase, 1, v.len, v.off, 0, v.stride}), v.len, bc, bt);
 }
 // the same from a device vector of len canonical values
-static WScaled vec_prep_ptr(svdw_ctx* c, const Fr* src, uint32_t len, DBuf& bc, DBuf& bm, int na) {
-    ensure_buf(c, bc, (size_t)len * sizeof(Fr));
-    ensure_buf(c, bm, 2 * (size_t)len * sizeof(Fr));
-    Fr* ws = (Fr*)bm.p;
-    Fr* wn = na < 8 && ws ? ws + len : nullptr;
-    if (!c->dry) {
-        DView w;
-        memset(&w, 0, sizeof w);
-        w.ptr = src;
-        w.rs = 0; w.cs = 1; w.rows = 1; w.cols = len;
-        hipck(launch_vec_prep(w, len, (Fr*)bc.p, ws, wn, scale_factor(na), c->st), "k_vec_prep");
-    }
-    return WScaled{ws, wn};
+static const Fr* vec_prep_ptr(svdw_ctx* c, const Fr* src, uint32_t len, DBuf& bc, DBuf& bt) {
+    DView w;
+    memset(&w, 0, sizeof w);
+    w.ptr = src;
+    w.rs = 0; w.cs = 1; w.rows = 1; w.cols = len;
+    return vec_prep_view(c, w, len, bc, bt);
 }
 static svdw_vec field_mat_vec_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a,
                                   const svdw_vec& v) {
     REQUIRE(a.cols == v.len, "field_mat_vec_mul: a[0].len() != v.len()");
     const int na = scan_na(c, a);
-    const WScaled w = vec_prep(c, v, c->w1c, c->w1m, na);
-    return matvec_rows(c, phase, a, (const Fr*)c->w1c.p, w, na);
-}
-// gamma powers scaled for `na` (cached with the gamma vector)
-static WScaled gamma_scaled(svdw_ctx* c, int na) {
-    if (na >= 8) return WScaled{(const Fr*)c->gpm.p, nullptr};
-    const uint32_t len = c->gp_len;
-    if (!c->dry && !(c->gps_ok >> na & 1)) {
-        ensure_buf(c, c->gps[na], 2 * (size_t)len * sizeof(Fr));
-        DView w;
-        memset(&w, 0, sizeof w);
-        w.ptr = (const Fr*)c->gpc.p;
-        w.rs = 0; w.cs = 1; w.rows = 1; w.cols = len;
-        hipck(launch_vec_prep(w, len, nullptr, (Fr*)c->gps[na].p, (Fr*)c->gps[na].p + len,
-                              scale_factor(na), c->st), "k_vec_prep");
-        c->gps_ok |= 1u << na;
-    }
-    const Fr* ws = (const Fr*)c->gps[na].p;
-    return WScaled{ws, ws ? ws + len : nullptr};
+    const Fr* tab = vec_prep(c, v, c->w1c, c->w1t);
+    return matvec_rows(c, phase, a, (const Fr*)c->w1c.p, tab, na);
 }
 // ZkMatrix::verify_mul (src/matrix/mod.rs:251-282) for several (a, b, c_s) triples
 // with one gamma: cells are appended exactly as consecutive verify_mul calls
@@ -1304,17 +1330,45 @@ static WScaled gamma_scaled(svdw_ctx* c, int na) {
 struct VMul {
     svdw_mat a, b, cs;
 };
-static void ensure_gamma_vec(svdw_ctx* c, uint32_t d, const Fr& gamma) {
-    // v = (1, g, g^2, ...) canonical + Montgomery, cached per (gamma, length)
-    if (c->dry || (c->gp_len >= d && fr_eq(c->gp_gamma, gamma))) return;
-    const uint32_t len = std::max(d, c->gp_len);
+// v = (1, g, g^2, ...): canonical (gpc) + scaled table (gtab), on stream s. The
+// powers come from three host-side Montgomery tables (g^a, g^(16 b), g^(256 c)):
+// three products per element on the device instead of a square-and-multiply chain.
+static void gamma_prep(svdw_ctx* c, uint32_t d, const Fr& gamma, hipStream_t s) {
+    if (c->dry) return;
+    const uint32_t len = std::max(d, 1u);
+    REQUIRE((len + 255) / 256 <= (uint32_t)kGammaTab - 32, "verify_mul: vector too long");
     ensure_buf(c, c->gpc, (size_t)len * sizeof(Fr));
-    ensure_buf(c, c->gpm, (size_t)len * sizeof(Fr));
-    ProfScope ps(c, c->st, "k_gamma_vec", 64.0 * len, 0);
-    hipck(launch_gamma_vec(gamma, len, (Fr*)c->gpc.p, (Fr*)c->gpm.p, c->st), "k_gamma_vec");
-    c->gp_len = len;
+    ensure_buf(c, c->gtab, tab_len(len) * sizeof(Fr));
+    GammaTab g;
+    memset(&g, 0, sizeof g);
+    const Fr one = fr_to_mont(fr_from_u64(1)), gm = fr_to_mont(gamma);
+    g.t[0] = one;
+    for (int i = 1; i < 16; ++i) g.t[i] = mont_mul(g.t[i - 1], gm);
+    const Fr g16 = mont_mul(g.t[15], gm);
+    g.t[16] = one;
+    for (int i = 1; i < 16; ++i) g.t[16 + i] = mont_mul(g.t[15 + i], g16);
+    const Fr g256 = mont_mul(g.t[31], g16);
+    g.nhi = (len + 255) / 256;
+    g.t[32] = one;
+    for (uint32_t i = 1; i < g.nhi; ++i) g.t[32 + i] = mont_mul(g.t[31 + i], g256);
+    {
+        ProfScope ps(c, s, "k_gamma_prep", 32.0 * len * (1 + tab_len(1)), 0);
+        hipck(launch_gamma_prep(g, len, (Fr*)c->gpc.p, (Fr*)c->gtab.p, scale_tab(), s),
+              "k_gamma_prep");
+    }
     c->gp_gamma = gamma;
-    c->gps_ok = 0;
+    c->gp_len = len;
+}
+// gamma vector for verify_mul on c->st: the one queued ahead when it matches,
+// else prepared here
+static void ensure_gamma_vec(svdw_ctx* c, uint32_t d, const Fr& gamma) {
+    if (c->dry) return;
+    if (c->gp_ev && c->gp_len >= d && fr_eq(c->gp_gamma, gamma)) {
+        hipck(hipStreamWaitEvent(c->st, c->gp_ev, 0), "hipStreamWaitEvent");
+        return;
+    }
+    gamma_prep(c, d, gamma, c->st);
+    c->gp_ev = nullptr;
 }
 // ZkMatrix::verify_mul, one call at a time (scan_impl 1 / 2)
 static void verify_mul_legacy(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svdw_mat& b,
@@ -1322,7 +1376,7 @@ static void verify_mul_legacy(svdw_ctx* c, uint32_t phase, const svdw_mat& a, co
     REQUIRE(a.cols == b.rows, "verify_mul: a.num_col != b.num_rows");
     REQUIRE(cs.rows == a.rows, "verify_mul: c_s.len() != a.num_rows");
     REQUIRE(cs.cols == b.cols, "verify_mul: c_s[0].len() != b.num_col");
-    const uint32_t d = cs.cols, n = a.rows, k = a.cols;
+    const uint32_t d = cs.cols, n = a.rows;
     ensure_gamma_vec(c, d, gamma);
     const Fr* gpc = (const Fr*)c->gpc.p;
     put_cell(c, phase, fr_from_u64(1), true);              // load_witness(F::ONE) + assert_is_const
@@ -1342,12 +1396,11 @@ static void verify_mul_legacy(svdw_ctx* c, uint32_t phase, const svdw_mat& a, co
         note_const(c, fr_zero());
         run_stage(c, phase, pb, d - 1, 1, "verify_mul_gamma_pows");
     }
-    const int na_cs = scan_na(c, cs), na_b = scan_na(c, b), na_a = scan_na(c, a);
-    svdw_vec csv = matvec_rows(c, phase, cs, gpc, gamma_scaled(c, na_cs), na_cs);
-    svdw_vec bv = matvec_rows(c, phase, b, gpc, gamma_scaled(c, na_b), na_b);
-    const WScaled w2 = vec_prep(c, bv, c->w2c, c->w2m, na_a);
-    svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, w2, na_a);
-    (void)k;
+    const Fr* gtab = (const Fr*)c->gtab.p;
+    svdw_vec csv = matvec_rows(c, phase, cs, gpc, gtab, scan_na(c, cs));
+    svdw_vec bv = matvec_rows(c, phase, b, gpc, gtab, scan_na(c, b));
+    const Fr* t2 = vec_prep(c, bv, c->w2c, c->w2t);
+    svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, t2, scan_na(c, a));
     PB pb(c->LB);                                         // is_equal per row (unconstrained result)
     pb.a.view[0] = view_of(c, mat_of_vec(csv));
     pb.a.view[1] = view_of(c, mat_of_vec(abv));
@@ -1423,6 +1476,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     // pass 2: launches
     ensure_gamma_vec(c, dmax, gamma);
     const Fr* gpc = (const Fr*)c->gpc.p;
+    const Fr* gtab = (const Fr*)c->gtab.p;
     for (int i = 0; i < n; ++i) {
         Plan& p = pl[i];
         const uint32_t d = vm[i].cs.cols;
@@ -1438,74 +1492,86 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
             stage_launch(c, phase, p.pows, d - 1, 1, p.pows_off, p.pows_loff, "verify_mul_gamma_pows");
         }
     }
-    auto run_batch = [&](const char* name, auto mat_of, auto vec_of, auto wc_of, auto ws_of, int na) {
+    const int T = c->scan_impl == 5 ? 4 : c->scan_impl == 3 ? 1 : 2;
+    // operand widths per batch: host-known, or read on the device (na 0)
+    auto batch_na = [&](auto mat_of) {
+        svdw_mat ms[kMaxScanJobs];
+        for (int i = 0; i < n; ++i) ms[i] = mat_of(i);
+        return batch_na_host(c, ms, n);
+    };
+    auto run_batch = [&](const char* name, auto mat_of, auto vec_of, auto wc_of, auto tab_of, int na) {
         ScanBatch sb;
         memset(&sb, 0, sizeof sb);
         double bytes = 0, ops = 0;
         for (int i = 0; i < n; ++i) {
             const svdw_mat a = mat_of(i);
             const svdw_vec v = vec_of(i);
-            const WScaled w = ws_of(i);
             uint64_t r0 = 0, r1 = a.rows;                 // shard: this rank's rows
             const uint64_t rowc = 3ull * a.cols + 1, base = v.off - 3ull * a.cols;
             if (sharded(c)) shard_rows(c, a.rows, &r0, &r1);
-            sb.job[i] = ScanJob{view_of(c, a), wc_of(i), w.ws, w.wn,
-                                cellp(c, phase, base + r0 * rowc), a.cols, (uint32_t)(r1 - r0), 0,
-                                (uint32_t)r0};
-            bytes += 32.0 * a.rows * (4.0 * a.cols + 1) + 64.0 * a.cols;
-            ops += (double)a.rows * a.cols;
+            sb.job[i] = ScanJob{view_of(c, a), wc_of(i), tab_of(i), cellp(c, phase, base + r0 * rowc),
+                                a.cols, (uint32_t)(r1 - r0), 0, (uint32_t)r0, job_spec(c, a)};
+            bytes += 32.0 * (r1 - r0) * (4.0 * a.cols + 1) + 64.0 * a.cols;
+            ops += (double)(r1 - r0) * a.cols;
         }
         sb.njobs = n;
-        const int T = c->scan_impl == 5 ? 4 : c->scan_impl == 3 ? 1 : 2;
+        sb.bitw = c->dbitw;
         ProfScope ps(c, c->st, name, bytes, ops);
         hipck(launch_scan_batch(sb, T, T == 1 ? 8 : na, c->st), "k_matvec_scan");
-    };
-    auto group_na = [&](auto mat_of) {
-        int na = 1;
-        for (int i = 0; i < n; ++i) na = std::max(na, scan_na(c, mat_of(i)));
-        return c->scan_impl == 3 ? 8 : na;
     };
     auto cs_of = [&](int i) { return vm[i].cs; };
     auto b_of = [&](int i) { return vm[i].b; };
     auto a_of = [&](int i) { return vm[i].a; };
-    const int na_cs = group_na(cs_of), na_b = group_na(b_of), na_a = group_na(a_of);
-    const WScaled g_cs = gamma_scaled(c, na_cs);
-    const WScaled g_b = gamma_scaled(c, na_b);
+    const int na_cs = batch_na(cs_of), na_b = batch_na(b_of), na_a = batch_na(a_of);
     auto gc = [&](int) { return gpc; };
+    auto gt = [&](int) { return gtab; };
     // launch order != append order: the b and a.(b.g) scans need only the
     // operands, the c_s scans wait for the products when those run elsewhere
-    run_batch("k_matvec_scan:b", b_of, [&](int i) { return pl[i].bv; }, gc,
-              [&](int) { return g_b; }, na_b);
-    WScaled wb[kMaxScanJobs];
+    run_batch("k_matvec_scan:b", b_of, [&](int i) { return pl[i].bv; }, gc, gt, na_b);
+    // b.g of job i: the b scan of the first job with the same b (m.v^T and
+    // v.v^T share v^T) serves every later job with it
+    int src[kMaxScanJobs];
+    for (int i = 0; i < n; ++i) {
+        src[i] = i;
+        for (int k = 0; k < i; ++k)
+            if (vm[k].b.phase == vm[i].b.phase && vm[k].b.off == vm[i].b.off &&
+                vm[k].b.rows == vm[i].b.rows && vm[k].b.cols == vm[i].b.cols &&
+                vm[k].b.rs == vm[i].b.rs && vm[k].b.cs == vm[i].b.cs) { src[i] = k; break; }
+    }
+    const Fr* wt[kMaxScanJobs];
     if (sharded(c)) {
         // only this rank's rows of the b.g scans exist: every entry of b.g comes
-        // from the values-only mat-vec instead (all n products in one launch)
+        // from the values-only mat-vec instead (the distinct b's in one launch)
         ScanBatch vb;
         memset(&vb, 0, sizeof vb);
+        int nv = 0, slot[kMaxScanJobs];
         for (int i = 0; i < n; ++i) {
+            if (src[i] != i) { slot[i] = slot[src[i]]; continue; }
             const svdw_mat b = vm[i].b;
-            ensure_buf(c, c->bvfull[i], (size_t)b.rows * sizeof(Fr));
-            vb.job[i] = ScanJob{view_of(c, b), nullptr, g_b.ws, g_b.wn, (Fr*)c->bvfull[i].p,
-                                b.cols, b.rows, 0, 0};
+            ensure_buf(c, c->bvfull[nv], (size_t)b.rows * sizeof(Fr));
+            vb.job[nv] = ScanJob{view_of(c, b), nullptr, gtab, (Fr*)c->bvfull[nv].p, b.cols, b.rows,
+                                 0, 0, job_spec(c, b)};
+            slot[i] = nv++;
         }
-        vb.njobs = n;
-        ProfScope ps(c, c->st, "k_matvec_values", 0, 0);
-        hipck(launch_matvec_values(vb, na_b, c->st), "k_matvec_values");
-    }
-    for (int i = 0; i < n; ++i) {
-        if (sharded(c)) {
-            const svdw_mat b = vm[i].b;
-            wb[i] = vec_prep_ptr(c, (const Fr*)c->bvfull[i].p, b.rows, c->wbc[i], c->wbs[i], na_a);
-        } else {
-            wb[i] = vec_prep(c, pl[i].bv, c->wbc[i], c->wbs[i], na_a);
+        vb.njobs = nv;
+        vb.bitw = c->dbitw;
+        {
+            ProfScope ps(c, c->st, "k_matvec_values", 0, 0);
+            hipck(launch_matvec_values(vb, na_b, c->st), "k_matvec_values");
         }
+        for (int i = 0; i < n; ++i)
+            wt[i] = src[i] != i ? wt[src[i]]
+                                : vec_prep_ptr(c, (const Fr*)c->bvfull[slot[i]].p, vm[i].b.rows,
+                                               c->wbc[i], c->wbt[i]);
+    } else {
+        for (int i = 0; i < n; ++i)
+            wt[i] = src[i] != i ? wt[src[i]] : vec_prep(c, pl[i].bv, c->wbc[i], c->wbt[i]);
     }
     run_batch("k_matvec_scan:a", a_of, [&](int i) { return pl[i].abv; },
-              [&](int i) { return (const Fr*)c->wbc[i].p; }, [&](int i) { return wb[i]; }, na_a);
+              [&](int i) { return (const Fr*)c->wbc[src[i]].p; }, [&](int i) { return wt[i]; }, na_a);
     for (hipEvent_t ev : c->wait_before_cs)
         hipck(hipStreamWaitEvent(c->st, ev, 0), "hipStreamWaitEvent");
-    run_batch("k_matvec_scan:cs", cs_of, [&](int i) { return pl[i].csv; }, gc,
-              [&](int) { return g_cs; }, na_cs);
+    run_batch("k_matvec_scan:cs", cs_of, [&](int i) { return pl[i].csv; }, gc, gt, na_cs);
     for (int i = 0; i < n; ++i) {
         Plan& p = pl[i];
         p.eq.a.view[0] = view_of(c, mat_of_vec(p.csv));
@@ -1737,6 +1803,14 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
             grow(c, c->ph[p].lk, 0, c->ph[p].lcap, c->plan_val[2 * p + 1]);
         }
     }
+    c->gp_ev = nullptr;
+    if (!c->dry) {
+        // gamma^j depends on gamma only: queue it first, on its own stream, so it
+        // runs beside quantization instead of on the phase-1 chain
+        if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
+        gamma_prep(c, std::max(N, M), gamma, c->st3);
+        c->gp_ev = stream_dep(c, c->st3, nullptr);
+    }
     unsigned* dbits = nullptr;
     const uint32_t nbm = (uint32_t)(((uint64_t)N * M + 255) / 256);
     const uint32_t nbu = (uint32_t)(((uint64_t)N * N + 255) / 256);
@@ -1772,6 +1846,9 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         hipck(hipEventRecord(c->ev_bits, c->st), "hipEventRecord");
         c->bits_pending = true;
         c->qmat[0] = zm; c->qmat[1] = zu; c->qmat[2] = zv;
+        // the same words for the device-side choices (row-scan operand widths)
+        c->dbitw = dbits;
+        c->dwords = {{zm, 0}, {zu, 1}, {zv, 2}};
     }
     // Phase 1 needs only the products (queued on st2 by check_svd_phase0), the
     // quantized operands and gamma: run it on st2 behind the GEMMs, concurrently
@@ -1791,7 +1868,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     const int p1mode = c->phase1_overlap == 1 && (sharded(c) || p1_small) ? 2 : c->phase1_overlap;
     bool p1_queued = false;
     auto queue_phase1 = [&](const svdw_svd_payload& pl, bool overlap) {
-        fetch_bits(c);
+        if (c->scan_na_host) fetch_bits(c);       // A/B: operand widths read on the host
         const bool p1_overlap = p1mode && overlap;
         if (p1_overlap && p1mode == 2 && !c->st3)   // created on first use
             hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
@@ -1872,13 +1949,12 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             (void)hipStreamSynchronize(c->st2);
             if (c->st3) (void)hipStreamSynchronize(c->st3);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
-            for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1], &c->w1c, &c->w1m, &c->w2c, &c->w2m,
-                            &c->bits, &c->gpc, &c->gpm, &c->crtR, &c->gbits})
+            for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1], &c->w1c, &c->w1t, &c->w2c, &c->w2t,
+                            &c->bits, &c->gpc, &c->gtab, &c->crtR, &c->gbits})
                 if (b->p) (void)hipFree(b->p);
-            for (auto& b : c->gps) if (b.p) (void)hipFree(b.p);
             for (int i = 0; i < kMaxScanJobs; ++i) {
                 if (c->wbc[i].p) (void)hipFree(c->wbc[i].p);
-                if (c->wbs[i].p) (void)hipFree(c->wbs[i].p);
+                if (c->wbt[i].p) (void)hipFree(c->wbt[i].p);
                 if (c->bvfull[i].p) (void)hipFree(c->bvfull[i].p);
             }
             if (c->hbits) (void)hipHostFree(c->hbits);
@@ -2567,6 +2643,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->scan_impl = (int)value;
         } else if (n == "overlap") {
             c->overlap = value != 0;
+        } else if (n == "scan_na_host") {           // A/B: row-scan widths read on the host
+            c->scan_na_host = value != 0;
         } else {
             fail(SVDW_EINVAL, "unknown option " + n);
         }

@@ -1591,34 +1591,49 @@ hipError_t launch_check_lookups(const Fr* lk, uint64_t n, uint32_t lb, unsigned 
 }
 
 // ------------------------------------------------------------ vectors
-__global__ void k_vec_prep(const DView w, uint32_t L, Fr* wc, Fr* ws, Fr* wsn, const Fr f) {
-    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= L) return;
-    Fr zero = fr_zero();
-    Fr v = view_load(w, zero, 0, j);
-    if (wc) st_fr(wc + j, v);
-    const Fr s = mont_mul(v, f);
-    st_fr(ws + j, s);
-    if (wsn) st_fr(wsn + j, fr_neg(s));
+// grid (ceil(L / 256), 1 + kTabSlots): y = 0 the canonical copy, y = 1 + s the
+// table slot s (one Montgomery product per thread).
+__device__ __forceinline__ void tab_store(Fr* wc, Fr* tab, uint32_t L, uint32_t j, uint32_t y,
+                                          const Fr& v, const ScaleTab& f) {
+    if (y == 0) {
+        if (wc) st_fr(wc + j, v);
+        return;
+    }
+    const uint32_t s = y - 1;
+    const Fr x = mont_mul(v, f.f[s]);
+    Fr* base = tab + 2ull * s * L;
+    st_fr(base + j, x);
+    if (s < kTabSlots - 1) st_fr(base + L + j, fr_neg(x));
 }
-hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* wc, Fr* ws, Fr* wsn, const Fr& f,
+__global__ __launch_bounds__(256) void k_vec_prep(const DView w, uint32_t L, Fr* wc, Fr* tab,
+                                                  const ScaleTab f) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= L) return;
+    const Fr v = view_load(w, fr_zero(), 0, j);
+    tab_store(wc, tab, L, j, blockIdx.y, v, f);
+}
+hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* wc, Fr* tab, const ScaleTab& f,
                            hipStream_t st) {
     if (!L) return hipSuccess;
-    hipLaunchKernelGGL(k_vec_prep, dim3((L + 255) / 256), dim3(256), 0, st, w, L, wc, ws, wsn, f);
+    hipLaunchKernelGGL(k_vec_prep, dim3((L + 255) / 256, 1 + kTabSlots), dim3(256), 0, st, w, L, wc,
+                       tab, f);
     return hipGetLastError();
 }
-__global__ void k_gamma_vec(const Fr g, uint32_t L, int nbits, Fr* wc, Fr* wm) {
-    uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+// g^j from the host's three Montgomery tables (depth: three products, then the
+// slot's): no per-element square-and-multiply chain.
+__global__ __launch_bounds__(256) void k_gamma_prep(const GammaTab g, uint32_t L, Fr* wc, Fr* tab,
+                                                    const ScaleTab f) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= L) return;
-    Fr v = fr_pow_u64(g, j, nbits);
-    st_fr(wc + j, v);
-    st_fr(wm + j, fr_to_mont(v));
+    const Fr vm = mont_mul(mont_mul(g.t[j & 15], g.t[16 + ((j >> 4) & 15)]), g.t[32 + (j >> 8)]);
+    tab_store(wc, tab, L, j, blockIdx.y, fr_from_mont(vm), f);
 }
-hipError_t launch_gamma_vec(const Fr& g, uint32_t L, Fr* wc, Fr* wm, hipStream_t st) {
+hipError_t launch_gamma_prep(const GammaTab& g, uint32_t L, Fr* wc, Fr* tab, const ScaleTab& f,
+                             hipStream_t st) {
     if (!L) return hipSuccess;
-    int nbits = 1;
-    while (nbits < 32 && (L - 1) >> nbits) ++nbits;
-    hipLaunchKernelGGL(k_gamma_vec, dim3((L + 255) / 256), dim3(256), 0, st, g, L, nbits, wc, wm);
+    if ((L + 255) / 256 > g.nhi || g.nhi > (uint32_t)kGammaTab - 32) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_gamma_prep, dim3((L + 255) / 256, 1 + kTabSlots), dim3(256), 0, st, g, L,
+                       wc, tab, f);
     return hipGetLastError();
 }
 
@@ -1716,6 +1731,72 @@ __device__ __forceinline__ U9 wave_scan_u9(U9 s) {
 // One launch serves up to kMaxScanJobs independent scans (blocks [blk0, blk0 + rows)
 // of the grid belong to job q), so the scans of several verify_mul calls share
 // one wave of blocks.
+// Words of the small operand from a bit bound (host: scan_na): 8 = full Montgomery.
+__device__ __forceinline__ int na_of_bits(uint32_t b) {
+    if (b > 192) return 8;
+    return b ? (int)((b + 31) / 32) : 1;
+}
+__device__ __forceinline__ int spec_na(const NaSpec& sp, const unsigned* __restrict__ W) {
+    if (sp.wa == -2) return na_of_bits(sp.lk);            // host-known bound
+    if (sp.wa < 0 || !W) return 8;
+    uint32_t b = W[sp.wa];
+    if (sp.wb >= 0) b += W[sp.wb] + sp.lk;
+    return na_of_bits(b);
+}
+// the launch's na: the template's, or (NA = 0) the max over the jobs' specs
+template <int NA>
+__device__ __forceinline__ int batch_na(const ScanBatch& B) {
+    if constexpr (NA != 0) {
+        return NA;
+    } else {
+        int na = 1;
+#pragma unroll
+        for (int q = 0; q < kMaxScanJobs; ++q)
+            if ((uint32_t)q < B.njobs) na = max(na, spec_na(B.job[q].spec, B.bitw));
+        return na;
+    }
+}
+__device__ __forceinline__ const Fr* tab_slot(const Fr* tab, uint32_t L, int na) {
+    return tab + 2ull * (na >= 8 ? kTabSlots - 1 : na - 1) * L;
+}
+// a_j * w_j: |signed a| < 2^(32 NA): a negative value p - x has a non-zero top
+// word; multiply |a| (NA words) by w * 2^(32 NA) or by its negation. NA = 8:
+// Montgomery product with w's Montgomery form.
+template <int NA>
+__device__ __forceinline__ Fr scan_prod(const Fr& a, const Fr* __restrict__ wm,
+                                        const Fr* __restrict__ wn, uint32_t j) {
+    if constexpr (NA == 8) {
+        return mont_mul(a, ld_fr(wm + j));
+    } else {
+        const bool neg = a.w[7] != 0;
+        Fr mag = fr_zero();
+        uint32_t br = 0;
+#pragma unroll
+        for (int q = 0; q < NA; ++q) {
+            const uint32_t t = subb32(p_word(q), a.w[q], br);
+            mag.w[q] = neg ? t : a.w[q];
+        }
+        return mont_mul_small<NA>(mag, ld_fr((neg ? wn : wm) + j));
+    }
+}
+template <int NA>
+__device__ __forceinline__ Fr scan_prod_rt(int na, const Fr& a, const Fr* __restrict__ wm,
+                                           const Fr* __restrict__ wn, uint32_t j) {
+    if constexpr (NA != 0) {
+        return scan_prod<NA>(a, wm, wn, j);
+    } else {
+        switch (na) {          // uniform over the launch
+        case 1: return scan_prod<1>(a, wm, wn, j);
+        case 2: return scan_prod<2>(a, wm, wn, j);
+        case 3: return scan_prod<3>(a, wm, wn, j);
+        case 4: return scan_prod<4>(a, wm, wn, j);
+        case 5: return scan_prod<5>(a, wm, wn, j);
+        case 6: return scan_prod<6>(a, wm, wn, j);
+        default: return scan_prod<8>(a, wm, wn, j);
+        }
+    }
+}
+
 template <int T, int NA>
 __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
     static_assert(256 % T == 0, "T divides the block");
@@ -1732,9 +1813,10 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
         if ((uint32_t)q < B.njobs && blockIdx.x >= B.job[q].blk0) J = B.job[q];
     const DView& A = J.A;
     const uint32_t L = J.L;
+    const int na = batch_na<NA>(B);
     const Fr* __restrict__ wc = J.wc;
-    const Fr* __restrict__ wm = J.ws;
-    const Fr* __restrict__ wn = J.wsn;
+    const Fr* __restrict__ wm = tab_slot(J.tab, L, na);
+    const Fr* __restrict__ wn = wm + L;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t lb = blockIdx.x - J.blk0;
     const uint32_t rb = (J.blk0 & 7) ? lb : scan_row(lb, J.rows), r = J.r_begin + rb;
@@ -1751,21 +1833,7 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
         for (int i = 0; i < T; ++i) {
             const uint32_t j = j0 + i;
             a[i] = j < L ? view_load(A, zero, r, j) : zero;
-            if constexpr (NA == 8) {
-                s[i] = j < L ? mont_mul(a[i], ld_fr(wm + j)) : zero;
-            } else {
-                // |signed a| < 2^(32 NA): a negative value p - x has a non-zero top
-                // word; multiply |a| (NA words) by w or by the pre-negated -w
-                const bool neg = a[i].w[7] != 0;
-                Fr mag = zero;
-                uint32_t br = 0;
-#pragma unroll
-                for (int q = 0; q < NA; ++q) {
-                    const uint32_t t = subb32(p_word(q), a[i].w[q], br);
-                    mag.w[q] = neg ? t : a[i].w[q];
-                }
-                s[i] = j < L ? mont_mul_small<NA>(mag, ld_fr((neg ? wn : wm) + j)) : zero;
-            }
+            s[i] = j < L ? scan_prod_rt<NA>(na, a[i], wm, wn, j) : zero;
         }
         // local inclusive sums (< T p), the wave scan and the prefixes stay
         // unreduced (exact, < 2^265); each output is reduced once
@@ -1938,8 +2006,9 @@ __global__ __launch_bounds__(256) void k_matvec_values(const ScanBatch B) {
         if ((uint32_t)q < B.njobs && blockIdx.x >= B.job[q].blk0) J = B.job[q];
     const DView& A = J.A;
     const uint32_t L = J.L;
-    const Fr* __restrict__ wm = J.ws;
-    const Fr* __restrict__ wn = J.wsn;
+    const int na = batch_na<NA>(B);
+    const Fr* __restrict__ wm = tab_slot(J.tab, L, na);
+    const Fr* __restrict__ wn = wm + L;
     Fr* __restrict__ out = J.out;
     // rows dealt XCD-contiguously (as the scans): a transposed b's neighbouring
     // rows are neighbouring columns, one 128 B line per 4 rows in one L2
@@ -1949,20 +2018,7 @@ __global__ __launch_bounds__(256) void k_matvec_values(const ScanBatch B) {
     U9 acc = u9_from(zero);
     for (uint32_t j = tid; j < L; j += 256) {
         const Fr a = view_load(A, zero, r, j);
-        Fr s;
-        if constexpr (NA == 8) {
-            s = mont_mul(a, ld_fr(wm + j));
-        } else {
-            const bool neg = a.w[7] != 0;
-            Fr mag = zero;
-            uint32_t br = 0;
-#pragma unroll
-            for (int q = 0; q < NA; ++q) {
-                const uint32_t t = subb32(p_word(q), a.w[q], br);
-                mag.w[q] = neg ? t : a.w[q];
-            }
-            s = mont_mul_small<NA>(mag, ld_fr((neg ? wn : wm) + j));
-        }
+        const Fr s = scan_prod_rt<NA>(na, a, wm, wn, j);
         acc = u9_add(acc, u9_from(s));                     // <= 2^13 terms of < p: < 2^267
     }
     part[tid] = acc;
@@ -1985,6 +2041,7 @@ hipError_t launch_matvec_values(const ScanBatch& b0, int na, hipStream_t st) {
     if (!blocks) return hipSuccess;
     const dim3 g(blocks), blk(256);
     switch (na) {
+    case 0: hipLaunchKernelGGL(k_matvec_values<0>, g, blk, 0, st, b); break;
     case 1: hipLaunchKernelGGL(k_matvec_values<1>, g, blk, 0, st, b); break;
     case 2: hipLaunchKernelGGL(k_matvec_values<2>, g, blk, 0, st, b); break;
     case 3: hipLaunchKernelGGL(k_matvec_values<3>, g, blk, 0, st, b); break;
@@ -2000,6 +2057,7 @@ template <int T>
 static void launch_scan_t(const ScanBatch& b, int na, dim3 g, hipStream_t st) {
     const dim3 blk(256);
     switch (na) {
+    case 0: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 0>), g, blk, 0, st, b); break;
     case 1: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 1>), g, blk, 0, st, b); break;
     case 2: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 2>), g, blk, 0, st, b); break;
     case 3: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 3>), g, blk, 0, st, b); break;
@@ -2028,9 +2086,10 @@ hipError_t launch_scan_batch(const ScanBatch& b0, int T, int na, hipStream_t st)
     return hipGetLastError();
 }
 hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
-                              const Fr* wc, const Fr* wm, const Fr* wn, Fr* out, int impl, int na,
+                              const Fr* wc, const Fr* tab, Fr* out, int impl, int na,
                               hipStream_t st) {
     if (r_end <= r_begin || !L) return hipSuccess;
+    const Fr* wm = tab + 2ull * (kTabSlots - 1) * L;    // Montgomery slot (impls 1, 2)
     if (impl == 1)
         hipLaunchKernelGGL(k_matvec_scan_v1, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L,
                            wc, wm, out);
@@ -2038,7 +2097,8 @@ hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, 
         ScanBatch b;
         memset(&b, 0, sizeof b);
         b.njobs = 1;
-        b.job[0] = ScanJob{A, wc, wm, wn, out, L, r_end - r_begin, 0, r_begin};
+        b.job[0] = ScanJob{A, wc, tab, out, L, r_end - r_begin, 0, r_begin, NaSpec{-1, -1, 0, 0}};
+        b.bitw = nullptr;
         return launch_scan_batch(b, impl == 3 ? 1 : impl == 4 ? 2 : 4, impl == 3 ? 8 : na, st);
     } else
         hipLaunchKernelGGL(k_matvec_scan, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L, wc,

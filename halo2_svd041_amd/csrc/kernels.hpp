@@ -8,21 +8,46 @@
 
 namespace svdw {
 
+// Row-scan operand width decided on the device: a job's matrix has |signed
+// entries| < 2^bits with bits = W[wa] (ZkMatrix::new cells whose bit-length
+// maximum is device word W[wa]) or W[wa] + W[wb] + lk (a product c_s = a * b
+// with K <= 2^lk, like bits_of on the host); wa < 0: unknown (na = 8).
+struct NaSpec {
+    int16_t wa, wb;
+    uint16_t lk, _r;
+};
+// Scaled-vector table of a length-L vector w: kTabSlots slots of 2L cells.
+// Slot s < 6 (na = s + 1): w * 2^(32 na) mod p at [2sL, 2sL + L) and its
+// negation at [2sL + L, 2sL + 2L); slot 6: w in Montgomery form at [12L, 13L).
+static constexpr int kTabSlots = 7;
+constexpr uint64_t tab_len(uint64_t L) { return 2ull * kTabSlots * L; }
+// factors per slot: mont_mul(w, f[s]) is slot s's entry for a canonical w
+struct ScaleTab {
+    Fr f[kTabSlots];
+};
 // One row scan of a batched launch: rows [r_begin, r_begin + rows) of A (L
-// columns) against w, row i's 3L+1 cells at out + i*(3L+1). blk0 is set by
-// launch_scan_batch.
+// columns) against w (canonical wc, scaled table tab), row i's 3L+1 cells at
+// out + i*(3L+1). blk0 is set by launch_scan_batch.
 struct ScanJob {
     DView A;
     const Fr* wc;
-    const Fr* ws;
-    const Fr* wsn;   // -ws (na < 8)
+    const Fr* tab;
     Fr* out;
     uint32_t L, rows, blk0, r_begin;
+    NaSpec spec;
 };
 static constexpr int kMaxScanJobs = 4;
 struct ScanBatch {
     ScanJob job[kMaxScanJobs];
     uint32_t njobs;
+    const unsigned* bitw;     // device bit-length words of the NaSpecs (na = 0 launches)
+};
+// gamma powers from host-side Montgomery tables: g^j = t[j & 15] t[16 + (j >> 4 & 15)]
+// t[32 + (j >> 8)] (j < 256 * nhi)
+static constexpr int kGammaTab = 96;
+struct GammaTab {
+    Fr t[kGammaTab];
+    uint32_t nhi;
 };
 
 // Elements per block of the generic stage kernel (= block size; LDS: E * (nv * 32 + 16) B).
@@ -156,29 +181,29 @@ hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint3
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
                            const unsigned* bits_b, uint32_t lk, hipStream_t st);
 static constexpr int kCrtMaxResidues = 40;   // = kCrtMaxMod (crt_tables.hpp)
-// w vector (len L) from a view (row 0 / col j of a 1 x L view) -> canonical copy
-// (w_canon nullable), w_scaled = mont_mul(w, f) (f = R^2: Montgomery form) and
-// its negation (w_neg nullable).
-hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* w_scaled, Fr* w_neg,
-                           const Fr& f, hipStream_t st);
-// w_j = gamma^j, j < L.
-hipError_t launch_gamma_vec(const Fr& gamma, uint32_t L, Fr* w_canon, Fr* w_mont, hipStream_t st);
+// w (len L) from a view (row 0 / col j of a 1 x L view) -> canonical copy
+// (w_canon nullable) and its scaled table (ScaleTab f: see kTabSlots).
+hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* tab, const ScaleTab& f,
+                           hipStream_t st);
+// w_j = gamma^j, j < L (L <= 256 * (kGammaTab - 32)): canonical copy and scaled table.
+hipError_t launch_gamma_prep(const GammaTab& g, uint32_t L, Fr* w_canon, Fr* tab, const ScaleTab& f,
+                             hipStream_t st);
 // Freivalds inner-product rows (GateChip::inner_product, 1+3L cells per row) for
 // rows [r_begin, r_end) of A (R x L); row r's cells at out + (r - r_begin)*(3L+1).
 // impl 1: one term per thread, shuffle scan, LDS-staged coalesced stores; 2: four
 // terms per thread, direct stores; 3: DPP scan; 4 / 5: DPP scan, two / four terms per
-// thread and small-operand products when na < 8 (|signed A| < 2^(32 na), w_scaled =
-// w * 2^(32 na)); impls 1-3 and na = 8 take w_scaled in Montgomery form.
+// thread and small-operand products when na < 8 (|signed A| < 2^(32 na), the
+// table's slot na - 1); impls 1-3 and na = 8 use the table's Montgomery slot.
 hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
-                              const Fr* w_canon, const Fr* w_scaled, const Fr* w_neg, Fr* out,
-                              int impl, int na, hipStream_t st);
-// out[r] = sum_j A(r, j) w_j mod p, r < R, L <= 8192 (values of the scans' last
-// cells without the cells); w_scaled / w_neg as for the scans with the same na.
-// out[r] = sum_j A(r, j) w_j per job (job.ws / job.wsn = w scaled / negated as
-// in the scans, job.out = the values, rows [0, job.rows)); one launch for all jobs.
+                              const Fr* w_canon, const Fr* tab, Fr* out, int impl, int na,
+                              hipStream_t st);
+// out[r] = sum_j A(r, j) w_j per job (job.tab = w's scaled table, job.out = the
+// values, rows [0, job.rows)); one launch for all jobs. na as for the scans
+// (0: from the jobs' NaSpecs and b.bitw on the device).
 hipError_t launch_matvec_values(const ScanBatch& b, int na, hipStream_t st);
 // Up to kMaxScanJobs DPP row scans in one launch (T terms per thread: 1, 2, 4;
-// na as above, shared by every job: each job's w_scaled = w * 2^(32 na)).
+// na shared by every job; na = 0: the max over the jobs' NaSpecs, read on the
+// device from b.bitw, so the host needs no operand bounds).
 hipError_t launch_scan_batch(const ScanBatch& b, int T, int na, hipStream_t st);
 
 }  // namespace svdw

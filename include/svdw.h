@@ -226,7 +226,9 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   "scan_impl" 4 | 1 | 2 | 3 | 5 (row-scan kernel: 1 shuffle scan, 2 four
  *   terms/thread direct stores, 3 DPP scan, 4 / 5 DPP scan with two / four
  *   terms per thread, unreduced partial sums and small-operand products where
- *   bounds are known).
+ *   bounds are known); "scan_na_host" 0 | 1 (row-scan operand widths inside
+ *   svdw_svd_witness: read on the device from the quantization's bit-length
+ *   words, or 1: read back by the host first, the round-1 behaviour).
  * Timing probe (NOT bit-identical, for A/B measurements only): "stage_probe"
  *   0 | 1 (skip the stage programs) | 2 (store a constant instead of cells). */
 int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);

@@ -172,7 +172,8 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                                   {"phase1_overlap": 0}, {"phase1_overlap": 2},
                                   {"stage_align": 0}, {"stage_align": 0, "stage_elems": 64},
                                   {"overlap": 0}, {"stage_inc": 1}, {"stage_priority": 1},
-                                  {"gemm_priority": 1}, {"cu_split": 64}, {"fused_quantize": 0}, {"d_checks_aside": 0}])
+                                  {"gemm_priority": 1}, {"cu_split": 64}, {"fused_quantize": 0}, {"d_checks_aside": 0},
+                                  {"scan_na_host": 1}, {"scan_impl": 5, "phase1_overlap": 2}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
