@@ -1276,7 +1276,7 @@ static ScaleTab scale_tab() {
 }
 // field_mat_vec_mul with the vector given as canonical copy + scaled table.
 static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const Fr* wc,
-                            const Fr* tab, int na) {
+                            const Fr* tab, uint32_t tl, int na) {
     const uint32_t R = a.rows, L = a.cols;
     uint64_t off;
     append(c, phase, (uint64_t)R * (3ull * L + 1), 0, &off, nullptr, "scan", R);
@@ -1288,7 +1288,7 @@ static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, cons
     }
     if (!c->dry) {
         ProfScope ps(c, c->st, a.cs == 1 ? "k_matvec_scan:rows" : "k_matvec_scan:cols", 32.0 * (double)R * (4.0 * L + 1) + 64.0 * L, (double)R * L);
-        hipck(launch_matvec_scan(view_of(c, a), (uint32_t)r0, (uint32_t)r1, L, wc, tab,
+        hipck(launch_matvec_scan(view_of(c, a), (uint32_t)r0, (uint32_t)r1, L, wc, tab, tl,
                                  cellp(c, phase, off + r0 * (3ull * L + 1)), c->scan_impl, na,
                                  c->st), "k_matvec_scan");
     }
@@ -1320,7 +1320,7 @@ static svdw_vec field_mat_vec_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a
     REQUIRE(a.cols == v.len, "field_mat_vec_mul: a[0].len() != v.len()");
     const int na = scan_na(c, a);
     const Fr* tab = vec_prep(c, v, c->w1c, c->w1t);
-    return matvec_rows(c, phase, a, (const Fr*)c->w1c.p, tab, na);
+    return matvec_rows(c, phase, a, (const Fr*)c->w1c.p, tab, v.len, na);
 }
 // ZkMatrix::verify_mul (src/matrix/mod.rs:251-282) for several (a, b, c_s) triples
 // with one gamma: cells are appended exactly as consecutive verify_mul calls
@@ -1397,10 +1397,10 @@ static void verify_mul_legacy(svdw_ctx* c, uint32_t phase, const svdw_mat& a, co
         run_stage(c, phase, pb, d - 1, 1, "verify_mul_gamma_pows");
     }
     const Fr* gtab = (const Fr*)c->gtab.p;
-    svdw_vec csv = matvec_rows(c, phase, cs, gpc, gtab, scan_na(c, cs));
-    svdw_vec bv = matvec_rows(c, phase, b, gpc, gtab, scan_na(c, b));
+    svdw_vec csv = matvec_rows(c, phase, cs, gpc, gtab, c->gp_len, scan_na(c, cs));
+    svdw_vec bv = matvec_rows(c, phase, b, gpc, gtab, c->gp_len, scan_na(c, b));
     const Fr* t2 = vec_prep(c, bv, c->w2c, c->w2t);
-    svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, t2, scan_na(c, a));
+    svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, t2, bv.len, scan_na(c, a));
     PB pb(c->LB);                                         // is_equal per row (unconstrained result)
     pb.a.view[0] = view_of(c, mat_of_vec(csv));
     pb.a.view[1] = view_of(c, mat_of_vec(abv));
@@ -1499,7 +1499,8 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         for (int i = 0; i < n; ++i) ms[i] = mat_of(i);
         return batch_na_host(c, ms, n);
     };
-    auto run_batch = [&](const char* name, auto mat_of, auto vec_of, auto wc_of, auto tab_of, int na) {
+    auto run_batch = [&](const char* name, auto mat_of, auto vec_of, auto wc_of, auto tab_of,
+                         auto tl_of, int na) {
         ScanBatch sb;
         memset(&sb, 0, sizeof sb);
         double bytes = 0, ops = 0;
@@ -1509,7 +1510,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
             uint64_t r0 = 0, r1 = a.rows;                 // shard: this rank's rows
             const uint64_t rowc = 3ull * a.cols + 1, base = v.off - 3ull * a.cols;
             if (sharded(c)) shard_rows(c, a.rows, &r0, &r1);
-            sb.job[i] = ScanJob{view_of(c, a), wc_of(i), tab_of(i), cellp(c, phase, base + r0 * rowc),
+            sb.job[i] = ScanJob{view_of(c, a), wc_of(i), tab_of(i), tl_of(i), cellp(c, phase, base + r0 * rowc),
                                 a.cols, (uint32_t)(r1 - r0), 0, (uint32_t)r0, job_spec(c, a)};
             bytes += 32.0 * (r1 - r0) * (4.0 * a.cols + 1) + 64.0 * a.cols;
             ops += (double)(r1 - r0) * a.cols;
@@ -1527,7 +1528,8 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     auto gt = [&](int) { return gtab; };
     // launch order != append order: the b and a.(b.g) scans need only the
     // operands, the c_s scans wait for the products when those run elsewhere
-    run_batch("k_matvec_scan:b", b_of, [&](int i) { return pl[i].bv; }, gc, gt, na_b);
+    auto gl = [&](int) { return c->gp_len; };            // the gamma table's length (>= every d)
+    run_batch("k_matvec_scan:b", b_of, [&](int i) { return pl[i].bv; }, gc, gt, gl, na_b);
     // b.g of job i: the b scan of the first job with the same b (m.v^T and
     // v.v^T share v^T) serves every later job with it
     int src[kMaxScanJobs];
@@ -1549,7 +1551,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
             if (src[i] != i) { slot[i] = slot[src[i]]; continue; }
             const svdw_mat b = vm[i].b;
             ensure_buf(c, c->bvfull[nv], (size_t)b.rows * sizeof(Fr));
-            vb.job[nv] = ScanJob{view_of(c, b), nullptr, gtab, (Fr*)c->bvfull[nv].p, b.cols, b.rows,
+            vb.job[nv] = ScanJob{view_of(c, b), nullptr, gtab, c->gp_len, (Fr*)c->bvfull[nv].p, b.cols, b.rows,
                                  0, 0, job_spec(c, b)};
             slot[i] = nv++;
         }
@@ -1568,10 +1570,11 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
             wt[i] = src[i] != i ? wt[src[i]] : vec_prep(c, pl[i].bv, c->wbc[i], c->wbt[i]);
     }
     run_batch("k_matvec_scan:a", a_of, [&](int i) { return pl[i].abv; },
-              [&](int i) { return (const Fr*)c->wbc[src[i]].p; }, [&](int i) { return wt[i]; }, na_a);
+              [&](int i) { return (const Fr*)c->wbc[src[i]].p; }, [&](int i) { return wt[i]; },
+              [&](int i) { return vm[i].b.rows; }, na_a);
     for (hipEvent_t ev : c->wait_before_cs)
         hipck(hipStreamWaitEvent(c->st, ev, 0), "hipStreamWaitEvent");
-    run_batch("k_matvec_scan:cs", cs_of, [&](int i) { return pl[i].csv; }, gc, gt, na_cs);
+    run_batch("k_matvec_scan:cs", cs_of, [&](int i) { return pl[i].csv; }, gc, gt, gl, na_cs);
     for (int i = 0; i < n; ++i) {
         Plan& p = pl[i];
         p.eq.a.view[0] = view_of(c, mat_of_vec(p.csv));

@@ -1815,8 +1815,8 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
     const uint32_t L = J.L;
     const int na = batch_na<NA>(B);
     const Fr* __restrict__ wc = J.wc;
-    const Fr* __restrict__ wm = tab_slot(J.tab, L, na);
-    const Fr* __restrict__ wn = wm + L;
+    const Fr* __restrict__ wm = tab_slot(J.tab, J.tl, na);
+    const Fr* __restrict__ wn = wm + J.tl;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t lb = blockIdx.x - J.blk0;
     const uint32_t rb = (J.blk0 & 7) ? lb : scan_row(lb, J.rows), r = J.r_begin + rb;
@@ -2007,8 +2007,8 @@ __global__ __launch_bounds__(256) void k_matvec_values(const ScanBatch B) {
     const DView& A = J.A;
     const uint32_t L = J.L;
     const int na = batch_na<NA>(B);
-    const Fr* __restrict__ wm = tab_slot(J.tab, L, na);
-    const Fr* __restrict__ wn = wm + L;
+    const Fr* __restrict__ wm = tab_slot(J.tab, J.tl, na);
+    const Fr* __restrict__ wn = wm + J.tl;
     Fr* __restrict__ out = J.out;
     // rows dealt XCD-contiguously (as the scans): a transposed b's neighbouring
     // rows are neighbouring columns, one 128 B line per 4 rows in one L2
@@ -2033,7 +2033,7 @@ hipError_t launch_matvec_values(const ScanBatch& b0, int na, hipStream_t st) {
     ScanBatch b = b0;
     uint32_t blocks = 0;
     for (uint32_t q = 0; q < b.njobs; ++q) {
-        if (b.job[q].L > 8192) return hipErrorInvalidValue;
+        if (b.job[q].L > 8192 || b.job[q].tl < b.job[q].L) return hipErrorInvalidValue;
         b.job[q].blk0 = blocks;
         blocks += b.job[q].L ? b.job[q].rows : 0;
         if (!b.job[q].L) b.job[q].rows = 0;
@@ -2071,6 +2071,7 @@ hipError_t launch_scan_batch(const ScanBatch& b0, int T, int na, hipStream_t st)
     ScanBatch b = b0;
     uint32_t blocks = 0;
     for (uint32_t q = 0; q < b.njobs; ++q) {
+        if (b.job[q].tl < b.job[q].L) return hipErrorInvalidValue;
         b.job[q].blk0 = blocks;
         blocks += b.job[q].L ? b.job[q].rows : 0;
         if (!b.job[q].L) b.job[q].rows = 0;
@@ -2086,10 +2087,11 @@ hipError_t launch_scan_batch(const ScanBatch& b0, int T, int na, hipStream_t st)
     return hipGetLastError();
 }
 hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
-                              const Fr* wc, const Fr* tab, Fr* out, int impl, int na,
-                              hipStream_t st) {
+                              const Fr* wc, const Fr* tab, uint32_t tl, Fr* out, int impl,
+                              int na, hipStream_t st) {
     if (r_end <= r_begin || !L) return hipSuccess;
-    const Fr* wm = tab + 2ull * (kTabSlots - 1) * L;    // Montgomery slot (impls 1, 2)
+    if (tl < L) return hipErrorInvalidValue;
+    const Fr* wm = tab + 2ull * (kTabSlots - 1) * tl;    // Montgomery slot (impls 1, 2)
     if (impl == 1)
         hipLaunchKernelGGL(k_matvec_scan_v1, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L,
                            wc, wm, out);
@@ -2097,7 +2099,7 @@ hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, 
         ScanBatch b;
         memset(&b, 0, sizeof b);
         b.njobs = 1;
-        b.job[0] = ScanJob{A, wc, tab, out, L, r_end - r_begin, 0, r_begin, NaSpec{-1, -1, 0, 0}};
+        b.job[0] = ScanJob{A, wc, tab, tl, out, L, r_end - r_begin, 0, r_begin, NaSpec{-1, -1, 0, 0}};
         b.bitw = nullptr;
         return launch_scan_batch(b, impl == 3 ? 1 : impl == 4 ? 2 : 4, impl == 3 ? 8 : na, st);
     } else

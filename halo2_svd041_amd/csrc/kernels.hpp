@@ -32,6 +32,7 @@ struct ScanJob {
     DView A;
     const Fr* wc;
     const Fr* tab;
+    uint32_t tl;     // the table's length (slot stride, >= L: gamma tables serve shorter scans)
     Fr* out;
     uint32_t L, rows, blk0, r_begin;
     NaSpec spec;
@@ -195,8 +196,8 @@ hipError_t launch_gamma_prep(const GammaTab& g, uint32_t L, Fr* w_canon, Fr* tab
 // thread and small-operand products when na < 8 (|signed A| < 2^(32 na), the
 // table's slot na - 1); impls 1-3 and na = 8 use the table's Montgomery slot.
 hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
-                              const Fr* w_canon, const Fr* tab, Fr* out, int impl, int na,
-                              hipStream_t st);
+                              const Fr* w_canon, const Fr* tab, uint32_t tl, Fr* out, int impl,
+                              int na, hipStream_t st);
 // out[r] = sum_j A(r, j) w_j per job (job.tab = w's scaled table, job.out = the
 // values, rows [0, job.rows)); one launch for all jobs. na as for the scans
 // (0: from the jobs' NaSpecs and b.bitw on the device).
