@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <array>
 #include <functional>
 #include <set>
@@ -333,6 +334,10 @@ struct Stream {
     uint64_t nl = 0, lcap = 0;
 };
 struct svdw_ctx {
+    // SVDW_HOST_TRACE=1: host-side timestamps of svd_witness's enqueue points on
+    // stderr (µs since the call started), to find host waits inside a call
+    bool host_trace = false;
+    std::chrono::steady_clock::time_point ht0;
     int device = -1;
     bool dry = true;
     hipStream_t st = nullptr;
@@ -492,6 +497,11 @@ static void fetch_bits(svdw_ctx* c) {
     }
 }
 static bool sharded(const svdw_ctx* c) { return c->shard_world > 1; }
+static void host_mark(svdw_ctx* c, const char* what) {
+    if (!c->host_trace || c->dry) return;
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - c->ht0).count();
+    fprintf(stderr, "[svdw host] %9.1f us  %s\n", us, what);
+}
 // rows of a row-parallel stage (R rows) that this rank computes / owns
 static void shard_rows(const svdw_ctx* c, uint64_t R, uint64_t* r0, uint64_t* r1) {
     *r0 = R * c->shard_rank / c->shard_world;
@@ -1693,6 +1703,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
             c->gemm_done.push_back(c->pre.back().ev);
         }
         c->prelaunched = true;
+        host_mark(c, "products queued");
     };
     if (c->prelaunch_at == 0) prelaunch();
     {
@@ -1708,6 +1719,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         if (sw.on) hipck(hipStreamWaitEvent(c->st, c->ev_bits, 0), "hipStreamWaitEvent");  // d loaded
         entries_less_than(c, d, max_bits);
         entries_in_desc_order(c, d, max_bits);
+        host_mark(c, "d checks queued");
     }
     if (c->prelaunch_at == 1) prelaunch();
     // svd_witness's phase 1 on the third stream, enqueued as soon as the products
@@ -1731,9 +1743,11 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     early_phase1(0);
     BigU unit = big_from_u128(((unsigned __int128)1 << P) + 1);
     check_mat_entries_bounded(c, u, unit);
+    host_mark(c, "bounds(u) queued");
     early_phase1(1);
     if (c->prelaunch_at == 2) prelaunch();
     check_mat_entries_bounded(c, v, unit);
+    host_mark(c, "bounds(v) queued");
     early_phase1(2);
     svdw_mat ut = u, vt = v;
     std::swap(ut.rows, ut.cols); std::swap(ut.rs, ut.cs);
@@ -1755,7 +1769,9 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     }
     svdw_mat mvt = honest_prover_mat_mul(c, m.phase, m, vt, bm, bv);
     BigU es = scale_err(err_svd, P), eu = scale_err(err_u, P);
+    host_mark(c, "u.d queued");
     check_mat_diff_views(c, m.phase, udv, view_of(c, mvt), N, M, es);
+    host_mark(c, "diff queued");
     Fr q = pow2_fr(P);
     const Fr qq = fr_mul(q, q);
     svdw_vec q2 = put_cell(c, m.phase, qq, true);
@@ -1763,6 +1779,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     check_mat_id(c, uut, q2, eu, &qq);
     svdw_mat vvt = honest_prover_mat_mul(c, m.phase, v, vt, bv, bv);
     check_mat_id(c, vvt, q2, eu, &qq);
+    host_mark(c, "ids queued");
     return svdw_svd_payload{ut, vt, mvt, uut, vvt};
 }
 static void check_svd_phase1(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u, const svdw_mat& v,
@@ -1784,6 +1801,8 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
                                const svdw_svd_config& cfg, const Fr& gamma) {
     REQUIRE(N >= 1 && M >= 1, "empty matrix");
     const uint32_t r = std::min(N, M);
+    c->ht0 = std::chrono::steady_clock::now();
+    host_mark(c, "svd_witness start");
     clear_streams(c);
     c->dep_next = 0;
     c->prelaunched = false;
@@ -1813,6 +1832,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
         gamma_prep(c, std::max(N, M), gamma, c->st3);
         c->gp_ev = stream_dep(c, c->st3, nullptr);
+        host_mark(c, "gamma_prep queued");
     }
     unsigned* dbits = nullptr;
     const uint32_t nbm = (uint32_t)(((uint64_t)N * M + 255) / 256);
@@ -1852,6 +1872,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         // the same words for the device-side choices (row-scan operand widths)
         c->dbitw = dbits;
         c->dwords = {{zm, 0}, {zu, 1}, {zv, 2}};
+        host_mark(c, "quantize + bits queued");
     }
     // Phase 1 needs only the products (queued on st2 by check_svd_phase0), the
     // quantized operands and gamma: run it on st2 behind the GEMMs, concurrently
@@ -1891,6 +1912,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         }
         c->wait_before_cs.clear();
         p1_queued = true;
+        host_mark(c, "phase 1 (early) queued");
     };
     struct Clear {
         svdw_ctx* c;
@@ -1902,11 +1924,14 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     c->early_p1 = nullptr;
     const bool p1_overlap = p1mode && c->prelaunched && !c->dry;
     hipStream_t p1s = p1mode == 2 ? c->st3 : c->st2;
+    host_mark(c, "phase 0 queued");
     if (!p1_queued) queue_phase1(pl, p1_overlap);
+    host_mark(c, "phase 1 queued");
     if (p1_overlap) stream_dep(c, p1s, c->st);
     // st2 also carries the d checks and single cells queued aside (and, with
     // phase 1 on st3, nothing else joins it): join it too
     if (c->prelaunched && !c->dry && !(p1_overlap && p1s == c->st2)) stream_dep(c, c->st2, c->st);
+    host_mark(c, "svd_witness end");
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
 }
 
@@ -1927,6 +1952,7 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
         c->LB = p->lookup_bits;
         c->device = p->device;
         c->dry = p->device < 0;
+        if (const char* h = getenv("SVDW_HOST_TRACE")) c->host_trace = atoi(h) != 0;
         if (const char* g = getenv("SVDW_GEMM"))
             c->gemm_impl = (!strcmp(g, "valu") || !strcmp(g, "dot4")) ? SVDW_GEMM_VALU : SVDW_GEMM_MFMA;
         if (!c->dry) {

@@ -66,6 +66,28 @@ int main() {
         printf("launch %d: host %.1f us, event elapsed %s %.4f ms, a[0] %.3f\n", it,
                std::chrono::duration<double, std::micro>(h1 - h0).count(), hipGetErrorString(e), ms, av);
     }
+    // the same with external event-record nodes (hipEventRecordExternal)
+    {
+        hipGraph_t gx;
+        hipGraphExec_t xx;
+        CK(hipStreamBeginCapture(s1, hipStreamCaptureModeRelaxed));
+        hipLaunchKernelGGL(k_fill, dim3(n / 256), dim3(256), 0, s1, a, n, 1.f, g);
+        CK(hipEventRecordWithFlags(t0, s1, hipEventRecordExternal));
+        hipLaunchKernelGGL(k_spin, dim3(n / 256), dim3(256), 0, s1, a, n, 2000);
+        CK(hipEventRecordWithFlags(t1, s1, hipEventRecordExternal));
+        CK(hipStreamEndCapture(s1, &gx));
+        size_t nx = 0;
+        CK(hipGraphGetNodes(gx, nullptr, &nx));
+        printf("external-record graph nodes: %zu\n", nx);
+        CK(hipGraphInstantiate(&xx, gx, nullptr, nullptr, 0));
+        for (int it = 0; it < 3; ++it) {
+            CK(hipGraphLaunch(xx, s1));
+            CK(hipStreamSynchronize(s1));
+            float ms = -1;
+            hipError_t e = hipEventElapsedTime(&ms, t0, t1);
+            printf("external launch %d: elapsed %s %.4f ms\n", it, hipGetErrorString(e), ms);
+        }
+    }
     // 40-kernel, 3-stream workload: eager enqueue vs graph replay (host + wall)
     {
         hipStream_t s3;
