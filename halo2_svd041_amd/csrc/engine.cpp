@@ -391,6 +391,9 @@ struct svdw_ctx {
     int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
     bool fused_quantize = true;             // "fused_quantize": m, u, v, d in one launch
+    bool res_f64 = true;                    // "res_f64": CRT residue planes of m, u, v from the
+                                            // f64 inputs, one launch (else from the cells)
+    const double* svd_f64[3] = {nullptr, nullptr, nullptr};   // device f64 m, u, v of svd_witness
     bool d_checks_aside = true;             // "d_checks_aside": d checks on st2 behind the products
     int phase1_overlap = 1;                 // "phase1_overlap": 0 off, 1 on st2 behind the
                                             // GEMMs, 2 on st3 from quantization on
@@ -1621,6 +1624,75 @@ static BigU scale_err(double err, uint32_t p) {
     return big_from_u128((unsigned __int128)x);
 }
 
+// The three products of check_svd_phase0 (A[g] * B[g], B = transposes) on st2
+// from residue planes built in one k_residues_f64 launch over svd_witness's f64
+// inputs: m (this rank's rows) into digA, v into digB (covering m.v^T and
+// v.v^T), u into digC. Planes of v and u carry 128 rows of slack so a row block
+// (sharded rank) reads its A tiles as a slice of the full planes. log[g]: the
+// products' stream offsets (dry replay); W: the device bit-length words of m, u, v.
+static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const svdw_mat (&B)[3],
+                                   const std::vector<uint64_t>& log, uint32_t phase,
+                                   const unsigned* W) {
+    const uint32_t N = A[0].rows, M = A[0].cols;
+    auto clog2 = [](uint32_t k) { uint32_t l = 0; while ((1ull << l) < k) ++l; return l; };
+    auto ceil_to = [](uint32_t x, uint32_t a) { return (x + a - 1) / a * a; };
+    const uint32_t lkM = clog2(M), lkN = clog2(N), kpM = ceil_to(M, 64), kpN = ceil_to(N, 64);
+    uint64_t rr0[3], rr1[3];
+    for (int g = 0; g < 3; ++g) {
+        rr0[g] = 0; rr1[g] = A[g].rows;
+        if (sharded(c)) shard_rows(c, A[g].rows, &rr0[g], &rr1[g]);
+    }
+    const uint32_t rows_m = (uint32_t)(rr1[0] - rr0[0]);
+    const uint32_t rp_m = ceil_to(std::max(rows_m, 1u), 128), rp_v = ceil_to(M, 128) + 128,
+                   rp_u = ceil_to(N, 128) + 128;
+    ensure_buf(c, c->digA, (size_t)kCrtMaxResidues * rp_m * kpM);
+    ensure_buf(c, c->digB, (size_t)kCrtMaxResidues * rp_v * kpM);
+    ensure_buf(c, c->digC, (size_t)kCrtMaxResidues * rp_u * kpN);
+    ensure_buf(c, c->crtR, (size_t)kCrtMaxResidues * ceil_to(std::max(N, M), 128) *
+                               ceil_to(std::max(N, M), 128));
+    ResSegs q;
+    memset(&q, 0, sizeof q);
+    auto seg = [&](const double* in, uint32_t rows, uint32_t cols, uint32_t rp, uint32_t kp,
+                   DBuf& out, std::initializer_list<std::array<int, 3>> pairs) {
+        ResSeg& g = q.seg[q.nseg++];
+        g.in = in; g.out = (uint32_t*)out.p;
+        g.rows = rows; g.cols = cols; g.ld = cols; g.rows_pad = rp; g.kw = kp / 4;
+        g.wa[0] = g.wa[1] = g.wb[0] = g.wb[1] = -1;
+        int k = 0;
+        for (auto& pr : pairs) { g.wa[k] = (int16_t)pr[0]; g.wb[k] = (int16_t)pr[1]; g.lk[k] = (uint32_t)pr[2]; ++k; }
+    };
+    if (rows_m) seg(c->svd_f64[0] + rr0[0] * M, rows_m, M, rp_m, kpM, c->digA, {{0, 2, (int)lkM}});
+    seg(c->svd_f64[2], M, M, rp_v, kpM, c->digB, {{0, 2, (int)lkM}, {2, 2, (int)lkM}});
+    seg(c->svd_f64[1], N, N, rp_u, kpN, c->digC, {{1, 1, (int)lkN}});
+    {
+        ProfScope ps(c, c->st2, "k_residues_f64",
+                     8.0 * ((double)rows_m * M + (double)M * M + (double)N * N), 0);
+        hipck(launch_residues_f64(q, W, (int)c->P, c->st2), "k_residues_f64");
+    }
+    const uint8_t* P[3] = {(const uint8_t*)c->digA.p, (const uint8_t*)c->digC.p,
+                           (const uint8_t*)c->digB.p};                 // A planes of m, u, v
+    const uint32_t stride[3] = {rp_m, rp_u, rp_v}, kp[3] = {kpM, kpN, kpM}, lk[3] = {lkM, lkN, lkM};
+    const int wa[3] = {0, 1, 2}, wb[3] = {2, 1, 2};
+    for (int g = 0; g < 3; ++g) {
+        const uint32_t rows = (uint32_t)(rr1[g] - rr0[g]), cols = B[g].cols;
+        Fr* out = cellp(c, phase, log[g] + rr0[g] * cols);
+        if (rows) {
+            const bool sym = !sharded(c) && g > 0;          // u.u^T, v.v^T: upper tiles + mirror
+            const uint8_t* Bp = g == 0 ? (const uint8_t*)c->digB.p : P[g];
+            const uint32_t bs = g == 0 ? rp_v : stride[g];
+            // a row block of u / v is a slice of the full planes (m's are this rank's rows)
+            const uint8_t* Ap = P[g] + (g == 0 ? 0 : rr0[g] * (uint64_t)kp[g]);
+            ProfScope ps(c, c->st2, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * rows * cols,
+                         (double)rows * cols * A[g].cols);
+            hipck(launch_gemm_crt(sym, Ap, Bp, rows, cols, stride[g], bs, kp[g], (uint8_t*)c->crtR.p,
+                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], c->st2),
+                  "k_gemm_crt");
+        }
+        c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
+        c->gemm_done.push_back(c->pre.back().ev);
+    }
+}
+
 // check_svd_phase0
 static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u,
                                          const svdw_mat& v, const svdw_vec& d, double err_svd,
@@ -1647,6 +1719,11 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         // waits for the operand bit lengths.
         const bool on_device = dev_bits && c->gemm_impl == SVDW_GEMM_MFMA && c->gemm_rt;
         if (!on_device) fetch_bits(c);
+        // residue planes straight from svd_witness's f64 inputs (one launch for m,
+        // u and v) when they are on the device and the CRT path applies
+        const bool from_f64 = on_device && dev_quantized && c->res_f64 && c->gemm_crt &&
+                              c->svd_f64[0] && c->svd_f64[1] && c->svd_f64[2] && N <= 8192 &&
+                              M <= 8192;
         std::vector<uint64_t> key = {n0[0], n0[1], nl0[0], nl0[1], d.phase, d.len, d.off,
                                      (uint64_t)d.stride, f64_key(err_svd), f64_key(err_u), max_bits_d};
         for (const svdw_mat* x : {&m, &u, &v})
@@ -1679,6 +1756,12 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
                                  dev_bits ? dev_bits + 2 : nullptr};
         const unsigned* sa[3] = {sl[0], sl[1], sl[2]};
         const unsigned* sb[3] = {sl[2], sl[1], sl[2]};
+        if (from_f64) {
+            prelaunch_products_f64(c, A, B, log, m.phase, dev_bits);
+            c->prelaunched = true;
+            host_mark(c, "products queued");
+            return;
+        }
         bool vplanes = false;                            // v's planes built (digB) on this rank
         for (int g = 0; g < 3; ++g) {
             // shard: rows [r0, r1) of the product only
@@ -1919,6 +2002,11 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         ~Clear() { c->early_p1 = nullptr; }
     } clr{c};
     if (p1mode == 2 && !c->dry) c->early_p1 = [&](const svdw_svd_payload& pl) { queue_phase1(pl, true); };
+    struct F64 {
+        svdw_ctx* c;
+        ~F64() { c->svd_f64[0] = c->svd_f64[1] = c->svd_f64[2] = nullptr; }
+    } f64clr{c};
+    if (on_device && !c->dry) { c->svd_f64[0] = m; c->svd_f64[1] = u; c->svd_f64[2] = v; }
     svdw_svd_payload pl =
         check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits, dbits, true);
     c->early_p1 = nullptr;
@@ -2655,6 +2743,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "phase1_overlap") {
             REQUIRE(value >= 0 && value <= 2, "phase1_overlap: 0, 1 or 2");
             c->phase1_overlap = (int)value;
+        } else if (n == "res_f64") {
+            c->res_f64 = value != 0;
         } else if (n == "gemm_crt") {
             REQUIRE(value == 0 || value == 1, "gemm_crt: 0 or 1");
             c->gemm_crt = (int)value;

@@ -1055,29 +1055,12 @@ __device__ __forceinline__ int crt_nmod(uint32_t ba, uint32_t bb, uint32_t lk) {
     return 0;
 }
 
-// NH 16-bit halves of |x| per element (|x| < 2^(16 NH)); moduli loop unrolled
-// so the table loads are scalar and hoisted.
+// Balanced residues of 4 consecutive-k elements (16-bit halves h of |x|, sign
+// neg) for moduli k < n, one u32 word (4 x int8) per plane at o[k * plane].
+// Moduli loop unrolled so the table loads are scalar and hoisted.
 template <int NH>
-__device__ __forceinline__ void residues_body(const DView& x, uint32_t rows, uint32_t kdim,
-                                              uint32_t rows_pad, uint32_t kw,
-                                              uint32_t* __restrict__ out, int n, uint32_t row,
-                                              uint32_t kg, const Fr& half) {
-    const Fr zero = fr_zero();
-    uint32_t h[4][NH];
-    bool neg[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-        const uint32_t kk = kg * 4 + t;
-        Fr v = zero;
-        if (row < rows && kk < kdim) v = view_load(x, zero, row, kk);
-        Fr tmp;
-        neg[t] = sub256(tmp, half, v) != 0;
-        const Fr mag = neg[t] ? fr_sub(zero, v) : v;
-#pragma unroll
-        for (int j = 0; j < NH; ++j) h[t][j] = (mag.w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-    }
-    uint32_t* o = out + (uint64_t)row * kw + kg;
-    const uint64_t plane = (uint64_t)rows_pad * kw;
+__device__ __forceinline__ void residues_emit(const uint32_t (&h)[4][8], const bool (&neg)[4],
+                                              uint32_t* __restrict__ o, uint64_t plane, int n) {
     for (int k = 0; k < n; ++k) {
         const int m = (int)c_crt_mod[k];
         const float inv = c_crt_invf[k];
@@ -1098,6 +1081,28 @@ __device__ __forceinline__ void residues_body(const DView& x, uint32_t rows, uin
         }
         o[k * plane] = word;
     }
+}
+// NH 16-bit halves of |x| per element (|x| < 2^(16 NH)) from canonical Fr cells.
+template <int NH>
+__device__ __forceinline__ void residues_body(const DView& x, uint32_t rows, uint32_t kdim,
+                                              uint32_t rows_pad, uint32_t kw,
+                                              uint32_t* __restrict__ out, int n, uint32_t row,
+                                              uint32_t kg, const Fr& half) {
+    const Fr zero = fr_zero();
+    uint32_t h[4][8];
+    bool neg[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const uint32_t kk = kg * 4 + t;
+        Fr v = zero;
+        if (row < rows && kk < kdim) v = view_load(x, zero, row, kk);
+        Fr tmp;
+        neg[t] = sub256(tmp, half, v) != 0;
+        const Fr mag = neg[t] ? fr_sub(zero, v) : v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[t][j] = j < NH ? (mag.w[j >> 1] >> (16 * (j & 1))) & 0xffffu : 0u;
+    }
+    residues_emit<NH>(h, neg, out + (uint64_t)row * kw + kg, (uint64_t)rows_pad * kw, n);
 }
 // Balanced residue planes: out[k][row][kpad] int8 (= u32 words of 4 consecutive
 // k), k < n; rows >= `rows` and columns >= kdim are zero.
@@ -1144,6 +1149,84 @@ hipError_t launch_to_residues(const DView& x, uint32_t rows, uint32_t kdim, uint
     return hipGetLastError();
 }
 
+// |x_q| and sign of ZkMatrix::new's quantization (quantize_body: round half away
+// of |x| 2^P, u128 saturation, NaN -> 0, sign(x) < 0 -> p - x_q) as 16-bit halves.
+__device__ __forceinline__ void quantized_halves(double x, double scale, uint32_t (&h)[8], bool& neg) {
+    neg = signbit(x) && !isnan(x);
+    const double s = round(fabs(x) * scale);
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (s >= 340282366920938463463374607431768211456.0) {
+        w[0] = w[1] = w[2] = w[3] = 0xffffffffu;
+    } else if (s > 0.0) {
+        const uint64_t bits = __double_as_longlong(s);
+        const int e = (int)((bits >> 52) & 0x7ff) - 1075;
+        const uint64_t mant = (bits & 0xfffffffffffffull) | (1ull << 52);
+        const unsigned __int128 v = e >= 0 ? ((unsigned __int128)mant << e) : (unsigned __int128)(mant >> -e);
+        w[0] = (uint32_t)v; w[1] = (uint32_t)(v >> 32);
+        w[2] = (uint32_t)(v >> 64); w[3] = (uint32_t)(v >> 96);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h[j] = (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+}
+// Residue planes straight from the f64 inputs of svd_witness (what k_to_residues
+// computes from the quantized cells, without reading the 32 B cells back): up to
+// kMaxResSegs matrices in one launch, segment s covering blocks [blk0[s], blk0[s+1]).
+__global__ __launch_bounds__(256) void k_residues_f64(const ResSegs q, const unsigned* __restrict__ W,
+                                                      double scale) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxResSegs; ++k) s += (uint32_t)k < q.nseg && blockIdx.x >= q.blk0[k];
+    const ResSeg g = q.seg[s];
+    int n = 0;
+    uint32_t bmax = 0;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+        if (g.wa[p] >= 0) {
+            const uint32_t ba = W[g.wa[p]], bb = W[g.wb[p]];
+            const int np = crt_nmod(ba, bb, g.lk[p]);
+            if (!np) return;                                   // too wide: no CRT product
+            n = max(n, np);
+            bmax = max(bmax, max(ba, bb));
+        }
+    if (!n) return;
+    const uint64_t idx = (uint64_t)(blockIdx.x - q.blk0[s]) * blockDim.x + threadIdx.x;
+    if (idx >= (uint64_t)g.rows_pad * g.kw) return;
+    const uint32_t row = (uint32_t)(idx / g.kw), kg = (uint32_t)(idx % g.kw);
+    uint32_t h[4][8];
+    bool neg[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const uint32_t kk = kg * 4 + t;
+        const double x = row < g.rows && kk < g.cols ? g.in[(uint64_t)row * g.ld + kk] : 0.0;
+        quantized_halves(x, scale, h[t], neg[t]);
+    }
+    uint32_t* o = g.out + (uint64_t)row * g.kw + kg;
+    const uint64_t plane = (uint64_t)g.rows_pad * g.kw;
+    if (bmax <= 64)
+        residues_emit<4>(h, neg, o, plane, n);
+    else if (bmax <= 96)
+        residues_emit<6>(h, neg, o, plane, n);
+    else
+        residues_emit<8>(h, neg, o, plane, n);
+}
+hipError_t launch_residues_f64(const ResSegs& q0, const unsigned* W, int precision_bits,
+                               hipStream_t st) {
+    ResSegs q = q0;
+    if (!q.nseg || q.nseg > (uint32_t)kMaxResSegs) return hipErrorInvalidValue;
+    uint32_t blocks = 0;
+    for (uint32_t k = 0; k < q.nseg; ++k) {
+        ResSeg& g = q.seg[k];
+        if (g.kw * 4 < g.cols || g.rows_pad < g.rows || g.ld < g.cols) return hipErrorInvalidValue;
+        q.blk0[k] = blocks;
+        blocks += (uint32_t)(((uint64_t)g.rows_pad * g.kw + 255) / 256);
+    }
+    q.blk0[q.nseg] = blocks;
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_residues_f64, dim3(blocks), dim3(256), 0, st, q, W,
+                       (double)(1ull << precision_bits));
+    return hipGetLastError();
+}
+
 static constexpr int CT = 128;     // CRT GEMM block tile (4 waves of 64 x 64)
 // Staged operand rows are 64 B (one k-chunk) with the four 16 B parts XOR-swizzled
 // by (row >> 2) & 3: the staging stores (4 rows x 4 parts per 16 lanes) and the
@@ -1156,11 +1239,14 @@ __device__ __forceinline__ uint32_t crt_lds(uint32_t row, uint32_t part) {
 
 // One (128 x 128 tile, modulus) per block: residues of C mod m_k as bytes
 // R[k][row][rpad_m]. SYM: A == B, upper tiles only.
+// Ar / Br: planes of astride / bstride rows (a row block of a larger operand is
+// its planes from row r0 on with the full operand's stride); R is
+// [mod][tiles_a * CT][tiles_m * CT].
 template <bool SYM>
 __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar,
-                                                  const uint8_t* __restrict__ Br, uint32_t rpad_a,
-                                                  uint32_t rpad_b, uint32_t kpad, uint32_t tiles_m,
-                                                  uint8_t* __restrict__ R,
+                                                  const uint8_t* __restrict__ Br, uint32_t astride,
+                                                  uint32_t bstride, uint32_t kpad, uint32_t tiles_a,
+                                                  uint32_t tiles_m, uint8_t* __restrict__ R,
                                                   const unsigned* __restrict__ bits_a,
                                                   const unsigned* __restrict__ bits_b, uint32_t lk) {
     const int n = crt_nmod(*bits_a, *bits_b, lk);
@@ -1191,8 +1277,8 @@ __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar
     }
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t wr = wave >> 1, wc = wave & 1;
-    const uint8_t* Ap = Ar + ((uint64_t)mod * rpad_a + bi * CT) * kpad;
-    const uint8_t* Bp = Br + ((uint64_t)mod * rpad_b + bj * CT) * kpad;
+    const uint8_t* Ap = Ar + ((uint64_t)mod * astride + bi * CT) * kpad;
+    const uint8_t* Bp = Br + ((uint64_t)mod * bstride + bj * CT) * kpad;
     // staging map: 512 x 16 B per operand chunk; thread -> (row, part) for q = tid, tid + 256
     const uint32_t r0 = tid >> 2, r1 = (tid + 256) >> 2, part = tid & 3;
     uint4 ra0, ra1, rb0, rb1;
@@ -1253,11 +1339,12 @@ __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar
                 T[tr * CTS + tc] = (uint8_t)r;
             }
     __syncthreads();
-    uint8_t* Rp = R + ((uint64_t)mod * rpad_a + bi * CT) * (uint64_t)rpad_b + bj * CT;
+    const uint32_t rpa = tiles_a * CT, rpb = tiles_m * CT;
+    uint8_t* Rp = R + ((uint64_t)mod * rpa + bi * CT) * (uint64_t)rpb + bj * CT;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t e = tid + q * 256, tr = e >> 3, c16 = (e & 7) * 16;
-        *reinterpret_cast<uint4*>(Rp + (uint64_t)tr * rpad_b + c16) =
+        *reinterpret_cast<uint4*>(Rp + (uint64_t)tr * rpb + c16) =
             *reinterpret_cast<const uint4*>(T + tr * CTS + c16);
     }
 }
@@ -1357,22 +1444,24 @@ __global__ __launch_bounds__(256) void k_crt_combine(const uint8_t* __restrict__
 }
 
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
-                           uint32_t rpad_a, uint32_t rpad_b, uint32_t kpad, uint8_t* R, Fr* out,
+                           uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
                            const unsigned* bits_b, uint32_t lk, hipStream_t st) {
-    if (rpad_a % CT || rpad_b % CT || kpad % 64) return hipErrorInvalidValue;
-    const uint32_t ta = rpad_a / CT, tb = rpad_b / CT;
+    const uint32_t ta = (N + CT - 1) / CT, tb = (M + CT - 1) / CT;
+    // every staged row (tiles x CT) lies inside its operand's planes
+    if (kpad % 64 || astride < ta * CT || bstride < tb * CT) return hipErrorInvalidValue;
+    const uint32_t rpa = ta * CT, rpb = tb * CT;           // R: [mod][rpa][rpb]
     const uint32_t sa = (N + MT - 1) / MT, sb = (M + MT - 1) / MT;
     if (sym) {
-        if (N != M || rpad_a != rpad_b) return hipErrorInvalidValue;
+        if (N != M || astride != bstride) return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_gemm_crt<true>, dim3(ta * (ta + 1) / 2, kCrtMaxMod), dim3(256), 0, st,
-                           Ar, Ar, rpad_a, rpad_b, kpad, ta, R, bits_a, bits_b, lk);
-        hipLaunchKernelGGL(k_crt_combine<true>, dim3(sa * (sa + 1) / 2), dim3(256), 0, st, R, rpad_a,
-                           rpad_b, N, M, sa, out, ors, ocs, bits_a, bits_b, lk);
+                           Ar, Ar, astride, bstride, kpad, ta, ta, R, bits_a, bits_b, lk);
+        hipLaunchKernelGGL(k_crt_combine<true>, dim3(sa * (sa + 1) / 2), dim3(256), 0, st, R, rpa,
+                           rpb, N, M, sa, out, ors, ocs, bits_a, bits_b, lk);
     } else {
         hipLaunchKernelGGL(k_gemm_crt<false>, dim3(ta * tb, kCrtMaxMod), dim3(256), 0, st, Ar, Br,
-                           rpad_a, rpad_b, kpad, tb, R, bits_a, bits_b, lk);
-        hipLaunchKernelGGL(k_crt_combine<false>, dim3(sa * sb), dim3(256), 0, st, R, rpad_a, rpad_b,
+                           astride, bstride, kpad, ta, tb, R, bits_a, bits_b, lk);
+        hipLaunchKernelGGL(k_crt_combine<false>, dim3(sa * sb), dim3(256), 0, st, R, rpa, rpb,
                            N, M, sb, out, ors, ocs, bits_a, bits_b, lk);
     }
     return hipGetLastError();

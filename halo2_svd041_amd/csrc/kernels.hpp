@@ -175,10 +175,31 @@ hipError_t launch_to_residues(const DView& x, uint32_t rows, uint32_t kdim, uint
                               uint32_t kpad, uint32_t* out, const unsigned* bits_a,
                               const unsigned* bits_b, uint32_t lk, hipStream_t st,
                               const unsigned* bits_c = nullptr);
-// c_s = A * Bt from residue planes Ar (rows_pad rpad_a) and Br (rpad_b); R is
-// the residue scratch [kCrtMaxResidues][rpad_a][rpad_b] bytes.
+// Residue planes of up to kMaxResSegs f64 matrices (row-major, row pitch ld),
+// each as k_to_residues would build them from its quantized cells: planes
+// [n][rows_pad][kw] u32 words (4 x int8 per word, kw * 4 >= cols), rows >= rows
+// and k >= cols zero; n = max over the segment's pairs p (wa[p] >= 0) of the CRT
+// modulus count of a product with operand bits W[wa[p]], W[wb[p]] and K <= 2^lk[p].
+static constexpr int kMaxResSegs = 4;
+struct ResSeg {
+    const double* in;
+    uint32_t* out;
+    uint32_t rows, cols, ld, rows_pad, kw;
+    int16_t wa[2], wb[2];
+    uint32_t lk[2];
+};
+struct ResSegs {
+    ResSeg seg[kMaxResSegs];
+    uint32_t blk0[kMaxResSegs + 1];   // set by the launcher
+    uint32_t nseg;
+};
+hipError_t launch_residues_f64(const ResSegs& q, const unsigned* W, int precision_bits,
+                               hipStream_t st);
+// c_s = A * Bt from residue planes Ar (plane stride astride rows, from the A rows'
+// first row) and Br (bstride): N x M, tiles of 128 rows / columns read from each;
+// R is the residue scratch [kCrtMaxResidues][ceil128(N)][ceil128(M)] bytes.
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
-                           uint32_t rpad_a, uint32_t rpad_b, uint32_t kpad, uint8_t* R, Fr* out,
+                           uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
                            const unsigned* bits_b, uint32_t lk, hipStream_t st);
 static constexpr int kCrtMaxResidues = 40;   // = kCrtMaxMod (crt_tables.hpp)

@@ -326,23 +326,80 @@ def test_rescale_and_inner_product_parity(gpu_ctx_factory, P, LB, S, NB, elems):
     assert _ints(y.values()) == [e.value for e in oy]
 
 
+def _on_device(*xs):
+    import torch
+    dev = torch.device("cuda", 0)
+    return [torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev) for x in xs]
+
+
+@pytest.mark.parametrize("res", [1, 0])
 @pytest.mark.parametrize("fused", [1, 0])
 @pytest.mark.parametrize("N,M,P", [(130, 97, 63), (64, 200, 32)])
-def test_device_inputs_parity(gpu_ctx_factory, fused, N, M, P):
+def test_device_inputs_parity(gpu_ctx_factory, fused, res, N, M, P):
     """The bench path: m, u, v, d already resident in HBM (torch float64 CUDA
-    tensors), quantized in one fused launch (or four), witness vs the oracle."""
-    import torch
+    tensors), quantized in one fused launch (or four); the CRT residue planes of
+    m, u, v built from the f64 inputs in one launch (res 1) or from the
+    quantized cells (res 0); witness vs the oracle."""
     import halo2_svd041_amd as hs
     m, u, d, v = gen_svd_input(N, M, seed=N * M)
     g = gamma_for(N + M)
     ctx = gpu_ctx_factory(P)
     ctx.set_option("fused_quantize", fused)
-    dev = torch.device("cuda", 0)
-    dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev)
-                      for x in (m, u, v, d))
+    ctx.set_option("res_f64", res)
+    dm, du, dv, dd = _on_device(m, u, v, d)
     hs.svd_witness(ctx, dm, du, dv, dd, g)
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
     _assert_streams(ctx, a0, l0, a1)
+
+
+@pytest.mark.parametrize("P", [32, 63])
+def test_device_garbage_inputs_parity(gpu_ctx_factory, P):
+    """Quantization edges through the f64 residue planes (device inputs): -0.0,
+    ties, saturation to 2^128 - 1, +-inf, NaN, in the GEMM operands m, u, v."""
+    import halo2_svd041_amd as hs
+    rs = np.random.RandomState(12)
+    N, M = 7, 6
+    m = rs.standard_normal((N, M)) * 50
+    u = rs.standard_normal((N, N))
+    v = rs.standard_normal((M, M))
+    d = np.abs(rs.standard_normal(min(N, M)))
+    m[0, 0] = -0.0
+    m[0, 1] = 0.5 / 2 ** 32
+    m[0, 2] = -1.5 / 2 ** 32
+    m[1, 0] = 3.0e19 if P == 63 else 1e30     # saturates to 2^128 - 1
+    m[1, 1] = -np.inf
+    m[1, 2] = np.nan
+    u[2, 3] = np.inf
+    v[3, 1] = -2.5 / 2 ** P
+    g = gamma_for(98)
+    ctx = gpu_ctx_factory(P)
+    hs.svd_witness(ctx, *_on_device(m, u, v, d), g)
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+    _assert_streams(ctx, a0, l0, a1)
+
+
+@pytest.mark.parametrize("N,M,P,world", [(40, 33, 63, 2), (33, 40, 32, 3), (70, 70, 63, 8),
+                                         (130, 97, 63, 3), (97, 130, 42, 5)])
+def test_row_sharded_device_inputs_parity(gpu_ctx_factory, N, M, P, world):
+    """Row-sharded ranks with device-resident inputs (the config-4 bench path):
+    each rank's A operand planes are a row slice of the full f64 residue planes
+    (u, v) or its own rows of m; the union of the owned cells is the oracle's
+    witness."""
+    import halo2_svd041_amd as hs
+    m, u, d, v = gen_svd_input(N, M, seed=N * M + 7 * world)
+    g = gamma_for(world + 40)
+    dm, du, dv, dd = _on_device(m, u, v, d)
+    ctxs = []
+    for rank in range(world):
+        ctx = gpu_ctx_factory(P)
+        ctx.set_shard(rank, world)
+        counts = hs.svd_witness(ctx, dm, du, dv, dd, g)
+        ctxs.append(ctx)
+    got = _reassemble(ctxs, counts)
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+    for key, want in (((0, 0), a0), ((1, 0), a1), ((0, 1), l0)):
+        bad = np.nonzero(np.any(got[key] != want, axis=1))[0]
+        assert bad.size == 0, f"{key}: {bad.size} cells differ, first at {bad[:8]}"
 
 
 # Regions of a witness that the C oracle's sampled mode (row_lim) truncates to
@@ -351,9 +408,9 @@ _ROW_LIMITED = {"check_mat_entries_bounded", "mat_times_diag_mat", "product", "c
                 "scan", "verify_mul_is_equal"}
 
 
-@pytest.mark.parametrize("N,M,P,row_lim", [(1024, 1024, 63, 64), (512, 512, 32, 128),
-                                           (2048, 1024, 32, 24)])
-def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim):
+@pytest.mark.parametrize("N,M,P,row_lim,device", [(1024, 1024, 63, 64, False), (512, 512, 32, 128, False),
+                                                  (2048, 1024, 32, 24, False), (1024, 1024, 63, 32, True)])
+def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device):
     """BASELINE config sizes (1024^2 P=63 = the bench workload, 512^2 P=32,
     2048x1024 P=32): the GPU computes the whole witness; the C oracle computes
     the first row_lim rows of every row-parallel region and all other regions
@@ -365,7 +422,10 @@ def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim):
     m, u, d, v = gen_svd_input(N, M, seed=N + M + P)
     g = gamma_for(N * M)
     ctx = gpu_ctx_factory(P)
-    hs.svd_witness(ctx, m, u, v, d, g)
+    if device:                                    # the bench path (inputs resident in HBM)
+        hs.svd_witness(ctx, *_on_device(m, u, v, d), g)
+    else:
+        hs.svd_witness(ctx, m, u, v, d, g)
     ctx.sync()
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g, row_lim=row_lim)
     want = {(0, 0): a0, (0, 1): l0, (1, 0): a1}
