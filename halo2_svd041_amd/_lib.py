@@ -64,6 +64,11 @@ class Segment(ct.Structure):
                 ("n", ct.c_uint64)]
 
 
+class EqCheck(ct.Structure):
+    _fields_ = [("copies_checked", ct.c_uint64), ("copy_failures", ct.c_uint64),
+                ("consts_checked", ct.c_uint64), ("const_failures", ct.c_uint64)]
+
+
 class CheckResult(ct.Structure):
     _fields_ = [("gates_checked", ct.c_uint64), ("gate_failures", ct.c_uint64),
                 ("lookups_checked", ct.c_uint64), ("lookup_failures", ct.c_uint64),
@@ -164,6 +169,8 @@ SIGNATURES = {
     "svdw_break_points": (_i32, [_P, _u32, _u64p, _u64, _u64p]),
     "svdw_assign_columns": (_i32, [_P, _u32, _P, _P, _P]),
     "svdw_check_physical": (_i32, [_P, _u32, _P, _P, _u32, ct.POINTER(CheckResult)]),
+    "svdw_equalities": (_i32, [_P, _u32, _P, _u64, _u64p, _P, _u64, _u64p]),
+    "svdw_check_equalities": (_i32, [_P, _u32, _P, _P, ct.POINTER(EqCheck)]),
     "svdw_profile_collect": (_i32, [_P, ct.POINTER(KStat), _u32, ct.POINTER(_u32)]),
     "svdw_plan_svd": (_i32, [_u32, _u32, _u32, _u32, ct.POINTER(SvdConfig), ct.POINTER(Counts)]),
 }

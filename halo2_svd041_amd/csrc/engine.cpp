@@ -137,6 +137,15 @@ struct PB {
     // cell against its source cell (view), range_check's last running sum
     // against the checked value (RangeChip::range_check's constrain_equal).
     std::vector<uint32_t> chk;
+    // halo2-base's equality records of an element's cells (svdw_equalities), in
+    // assign order: a Constant cell's (cell, value), an Existing cell's (source
+    // cell, cell), range_check's constrain_equal(a, last running sum) -- as eq
+    // words (kernels.hpp EQ_*): a constant slot, an earlier cell of the element,
+    // the element's cell of a view (RegionChecks::esrc), or an external cell
+    std::vector<uint32_t> eq;
+    int kext = -1;            // constant slot holding an external cell's value (init_rand)
+    bool vsrc[kMaxViews] = {true, true};   // false: the view holds values produced here
+    static constexpr int EQ_AUTO = -1, EQ_WIT = -2;
     bool kconst = true;       // its constant-source cells are halo2-base Constants
     int8_t vload[kMaxV];      // view a value was loaded from (-1: computed)
     int16_t fullc[kMaxV];     // first cell holding the value in full (-1: none)
@@ -172,9 +181,29 @@ struct PB {
         if (nbits >= 256) nbits = 0;
         return SlotOp{src, (uint8_t)lo, (uint8_t)nbits, 0};
     }
-    void cell(uint8_t src, uint32_t lo = 0, uint32_t nbits = 0) {
+    // cell `at` holds a copy of value v (QuantumCell::Existing of v's cell)
+    void eq_of_value(uint8_t v, uint32_t at) {
+        if (vload[v] >= 0 && vsrc[vload[v]]) eq.push_back(eq_word(EQ_VIEW, (uint32_t)vload[v], at));
+        else if (fullc[v] >= 0) eq.push_back(eq_word(EQ_LOCAL, (uint32_t)fullc[v], at));
+    }
+    // eqk: EQ_AUTO -- a Constant for a constant slot (kconst), the external cell
+    // for kext, an Existing copy for a value's full cell seen before (or loaded
+    // from a source view), else a Witness; EQ_WIT: a Witness; >= 0: an Existing
+    // copy of the element's cell eqk (range_check's last limb)
+    void cell(uint8_t src, uint32_t lo = 0, uint32_t nbits = 0, int eqk = EQ_AUTO) {
         if (a.C >= (uint32_t)kMaxAdv) fail(SVDW_ERANGE, "stage has too many cells per element (raise lookup_bits)");
         const SlotOp s = slot(src, lo, nbits);
+        if (eqk >= 0) {
+            eq.push_back(eq_word(EQ_LOCAL, (uint32_t)eqk, a.C));
+        } else if (eqk == EQ_AUTO) {
+            if (src >= KSRC) {
+                const int k = src - KSRC;
+                if (k == kext) eq.push_back(eq_word(EQ_EXT, 0, a.C));
+                else if (kconst) eq.push_back(eq_word(EQ_CONST, (uint32_t)k, a.C));
+            } else if (s.lo == 0 && s.nbits == 0) {
+                eq_of_value(src, a.C);
+            }
+        }
         if (src < KSRC && s.lo == 0 && s.nbits == 0) {      // the value itself: a copy or its first cell
             copy_of(src, a.C);
             if (fullc[src] < 0) fullc[src] = (int16_t)a.C;
@@ -242,6 +271,7 @@ struct PB {
         const uint32_t n = (bits + lb - 1) / lb, rem = bits % lb;
         uint8_t lsrc = v;
         uint32_t llo = 0, lnb = 0;
+        int lastc = EQ_AUTO;                        // the last limb's cell (n > 1)
         if (n == 1) {
             look(v);
         } else {
@@ -251,13 +281,16 @@ struct PB {
                 uint32_t slo = lo, snb = lb;
                 if (lo >= 256) { src = K(0); slo = 0; snb = 0; }
                 if (i == 0) {
-                    cell(src, slo, snb);
+                    lastc = (int)a.C;
+                    cell(src, slo, snb, EQ_WIT);   // limbs are witnesses
                 } else {
                     gate(a.C - 1);                  // [s_(i-1), l_i, 2^(i lb), s_i]
-                    cell(src, slo, snb);
+                    lastc = (int)a.C;
+                    cell(src, slo, snb, EQ_WIT);
                     cell(K(pow2_fr(lo)));
-                    cell(v, 0, (i + 1) * lb);    // running sum = v mod 2^((i+1) lb)
+                    cell(v, 0, (i + 1) * lb, EQ_WIT);   // running sum = v mod 2^((i+1) lb)
                     if (i + 1 == n && n * lb < 256) copy_of(v, a.C - 1);   // constrain_equal(a, sum)
+                    if (i + 1 == n) eq_of_value(v, a.C - 1);
                 }
                 look(src, slo, snb);
                 lsrc = src; llo = slo; lnb = snb;
@@ -265,7 +298,7 @@ struct PB {
         }
         if (rem == 1) {                             // assert_bit: [0, l, l, l]
             gate(a.C);
-            cell(K(0)); cell(lsrc, llo, lnb); cell(lsrc, llo, lnb); cell(lsrc, llo, lnb);
+            cell(K(0)); cell(lsrc, llo, lnb, lastc); cell(lsrc, llo, lnb, lastc); cell(lsrc, llo, lnb, lastc);
         } else if (rem > 1) {                       // mul(last, 2^(lb-rem)), looked up
             const uint32_t sh = lb - rem;
             uint8_t m = newv();
@@ -273,7 +306,7 @@ struct PB {
             else if ((n - 1) * lb >= 256) op(MO_ADDK, m, v, kidx(fr_zero()));   // unreachable in practice
             else op(MO_LIMBSHL, m, v, (uint8_t)sh, (uint16_t)((n - 1) * lb), (uint16_t)lb);
             gate(a.C);
-            cell(K(0)); cell(lsrc, llo, lnb); cell(K(pow2_fr(sh))); cell(m);
+            cell(K(0)); cell(lsrc, llo, lnb, lastc); cell(K(pow2_fr(sh))); cell(m);
             look(m);
         }
     }
@@ -398,6 +431,8 @@ struct svdw_ctx {
     int phase1_overlap = 1;                 // "phase1_overlap": 0 off, 1 on st2 behind the
                                             // GEMMs, 2 on st3 from quantization on
     bool prelaunched = false;               // this witness's products were queued on st2
+    uint32_t hold_us = 0;                   // "hold_us": timing aid, st spins this long first
+    Fr ext_gamma{};                          // init_rand of the last verify_mul (equality source 2)
     int p1_at = -1;                         // "p1_at": phase 1 on st3 (mode 2) enqueued after
                                             // phase-0 stage 0 / 1 / 2 (the u, v bounds), 3: at the
                                             // end; -1: auto (tools/shard_sim.py --opt p1_at=):
@@ -493,6 +528,9 @@ static uint32_t bits_of(const svdw_ctx* c, const svdw_mat& m) {
 static void fetch_bits(svdw_ctx* c) {
     if (!c->bits_pending) return;
     hipck(hipEventSynchronize(c->ev_bits), "hipEventSynchronize");
+    // the words are final once the event has fired: read them now (no copy is
+    // queued on st per witness, the device-side consumers read the words directly)
+    hipck(hipMemcpy(c->hbits, c->dbitw, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost), "D2H");
     c->bits_pending = false;
     for (int i = 0; i < 3; ++i) {
         c->qbits[i] = c->hbits[i];
@@ -634,10 +672,16 @@ static void pregrow(svdw_ctx* c, F&& fn) {
 }
 
 // --------------------------------------------------------------- views
+// A dry context has no streams: its views carry a placeholder pointer that
+// view_source decodes to (phase, offset) (never dereferenced: nothing launches).
+static constexpr uintptr_t kDryBase = (uintptr_t)1 << 44;
+static const Fr* dry_ptr(uint32_t phase, uint64_t off) {
+    return reinterpret_cast<const Fr*>(kDryBase * (phase + 1) + off * sizeof(Fr));
+}
 static DView view_of(svdw_ctx* c, const svdw_mat& m) {
     DView v;
     memset(&v, 0, sizeof v);
-    v.ptr = c->dry ? nullptr : cellp(c, m.phase, m.off);
+    v.ptr = c->dry ? dry_ptr(m.phase, m.off) : cellp(c, m.phase, m.off);
     v.rs = m.rs;
     v.cs = m.cs;
     v.rows = m.rows;
@@ -733,11 +777,58 @@ static void note_const(svdw_ctx* c, const Fr& v) {
 // the last appended region is `nelem` copies of pb's program: record its gates
 // (views: the source cells as (phase, offset), strided views into the cell
 // streams only -- the streams may move before the check)
+// (phase, offset) of a view's cell 0 in the cell streams (dry placeholders too)
+static bool view_source(const svdw_ctx* c, const Fr* ptr, uint32_t* phase, uint64_t* off) {
+    if (!ptr) return false;
+    if (c->dry) {
+        const uintptr_t x = reinterpret_cast<uintptr_t>(ptr);
+        if (x < kDryBase || x >= 3 * kDryBase) return false;
+        *phase = (uint32_t)(x / kDryBase - 1);
+        *off = (x % kDryBase) / sizeof(Fr);
+        return true;
+    }
+    for (uint32_t p = 0; p < 2; ++p) {
+        const Fr* base = c->ph[p].adv;
+        if (base && ptr >= base && ptr < base + c->ph[p].n) {
+            *phase = p;
+            *off = (uint64_t)(ptr - base);
+            return true;
+        }
+    }
+    return false;
+}
+// equality source of a matrix / a vector chain (RegionChecks::EqSrc)
+static RegionChecks::EqSrc eqsrc_mat(const svdw_mat& m) {
+    RegionChecks::EqSrc e;
+    e.kind = EQS_MAT;
+    e.phase = m.phase; e.off = m.off; e.rs = m.rs; e.cs = m.cs; e.rows = m.rows; e.cols = m.cols;
+    return e;
+}
+static RegionChecks::EqSrc eqsrc_chain(uint32_t first_phase, uint64_t first, uint32_t phase,
+                                       uint64_t base, int64_t stride) {
+    RegionChecks::EqSrc e;
+    e.kind = EQS_CHAIN;
+    e.first_phase = first_phase; e.first = first; e.phase = phase; e.off = base; e.rs = stride;
+    return e;
+}
+static RegionChecks::EqSrc eqsrc_vec(const svdw_vec& v) {   // cells v.off + t v.stride
+    return eqsrc_chain(v.phase, v.off, v.phase, v.off + v.stride, v.stride);
+}
 static void note_gates(svdw_ctx* c, const PB& pb, uint32_t cols = 1, size_t reg = ~size_t(0)) {
     RegionChecks& r = reg == ~size_t(0) ? c->layout_chk.back() : c->layout_chk.at(reg);
+    r.eq = pb.eq;
+    r.eqk.assign(pb.a.K, pb.a.K + pb.a.nk);
+    for (int k = 0; k < kMaxViews; ++k) {             // the loaded values' source cells
+        const DView& v = pb.a.view[k];
+        uint32_t ph;
+        uint64_t off;
+        if (v.mode == VIEW_STRIDED && view_source(c, v.ptr, &ph, &off))
+            r.esrc[k] = eqsrc_mat(svdw_mat{ph, v.rows, v.cols, off, v.rs, v.cs});
+    }
     if (pb.kconst)
         for (uint32_t q = 0; q < pb.a.C; ++q)
-            if (pb.a.adv[q].src >= KSRC) note_const(c, pb.a.K[pb.a.adv[q].src - KSRC]);
+            if (pb.a.adv[q].src >= KSRC && pb.a.adv[q].src - KSRC != pb.kext)
+                note_const(c, pb.a.K[pb.a.adv[q].src - KSRC]);
     r.words = pb.chk;
     r.unit = pb.a.C;
     r.cols = cols ? cols : 1;
@@ -866,9 +957,15 @@ static void check_mat_entries_bounded(svdw_ctx* c, const svdw_mat& a, const BigU
     run_stage(c, a.phase, pb, a.rows * a.cols, a.cols, "check_mat_entries_bounded");
 }
 // check_mat_diff on arbitrary views (a may be zero-padded, b may be diagonal).
+// a cell of the streams, for equality sources (phase -1: none)
+struct EqCell {
+    int phase = -1;
+    uint64_t off = 0;
+};
 static void check_mat_diff_views(svdw_ctx* c, uint32_t phase, const DView& a, const DView& b,
                                  uint32_t rows, uint32_t cols, const BigU& tol,
-                                 const Fr* diag_val = nullptr) {
+                                 const Fr* diag_val = nullptr, EqCell pad_a = {},
+                                 EqCell pad_b = {}, EqCell diag_b = {}) {
     PB pb(c->LB);
     pb.a.view[0] = a;
     pb.a.view[1] = b;
@@ -880,20 +977,31 @@ static void check_mat_diff_views(svdw_ctx* c, uint32_t phase, const DView& a, co
     pb.a.view[1].pad_k = pb.kidx(fr_zero());
     if (diag_val) pb.a.view[1].diag_k = pb.kidx(*diag_val);
     run_stage(c, phase, pb, rows * cols, cols, "check_mat_diff");
+    // equality sources of the padded / diagonal entries: the zero padding
+    // constant (check_svd_phase0), check_mat_id's zero and scalar_id cells
+    RegionChecks& r = c->layout_chk.back();
+    if (pad_a.phase >= 0) { r.esrc[0].pad_phase = pad_a.phase; r.esrc[0].pad_off = pad_a.off; }
+    if (b.mode != VIEW_STRIDED) {
+        r.esrc[1] = RegionChecks::EqSrc();
+        r.esrc[1].kind = EQS_MAT;                         // no strided part: pad or diagonal
+    }
+    if (pad_b.phase >= 0) { r.esrc[1].pad_phase = pad_b.phase; r.esrc[1].pad_off = pad_b.off; }
+    if (diag_b.phase >= 0) { r.esrc[1].diag_phase = diag_b.phase; r.esrc[1].diag_off = diag_b.off; }
 }
 // sid_val: the scalar's value when the host knows it (svd_witness's q^2): the
 // stage then takes it as a constant and does not read sid's cell, which may
 // still be in flight on another stream.
 static void check_mat_id(svdw_ctx* c, const svdw_mat& a, const svdw_vec& sid, const BigU& tol,
                          const Fr* sid_val = nullptr) {
-    put_cell(c, a.phase, fr_zero(), true);                // let zero = ctx.load_constant(F::ZERO)
+    const svdw_vec zero = put_cell(c, a.phase, fr_zero(), true);   // ctx.load_constant(F::ZERO)
     DView b;
     memset(&b, 0, sizeof b);
     b.mode = sid_val ? VIEW_DIAGK : VIEW_DIAG;
     b.ptr = c->dry || sid_val ? nullptr : cellp(c, sid.phase, sid.off);
     b.rows = a.rows;
     b.cols = a.cols;
-    check_mat_diff_views(c, a.phase, view_of(c, a), b, a.rows, a.cols, tol, sid_val);
+    check_mat_diff_views(c, a.phase, view_of(c, a), b, a.rows, a.cols, tol, sid_val, EqCell{},
+                         EqCell{(int)zero.phase, zero.off}, EqCell{(int)sid.phase, sid.off});
 }
 static svdw_mat mat_times_diag_mat(svdw_ctx* c, const svdw_mat& a, const svdw_vec& v) {
     REQUIRE(v.len <= a.cols, "mat_times_diag_mat: v longer than a's rows");
@@ -1288,11 +1396,20 @@ static ScaleTab scale_tab() {
     return t;
 }
 // field_mat_vec_mul with the vector given as canonical copy + scaled table.
+// the equality sources of an inner-product row region: a's row i, the vector w
+static void note_scan(svdw_ctx* c, const svdw_mat& a, const RegionChecks::EqSrc& w) {
+    RegionChecks& r = c->layout_chk.back();
+    r.scan = true;
+    r.unit = 3 * a.cols + 1;
+    r.esrc[0] = eqsrc_mat(a);
+    r.esrc[1] = w;
+}
 static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const Fr* wc,
-                            const Fr* tab, uint32_t tl, int na) {
+                            const Fr* tab, uint32_t tl, int na, const RegionChecks::EqSrc& wsrc) {
     const uint32_t R = a.rows, L = a.cols;
     uint64_t off;
     append(c, phase, (uint64_t)R * (3ull * L + 1), 0, &off, nullptr, "scan", R);
+    note_scan(c, a, wsrc);
     uint64_t r0 = 0, r1 = R;
     if (sharded(c)) {
         REQUIRE(c->scan_impl >= 3, "row sharding needs scan_impl >= 3");
@@ -1333,7 +1450,7 @@ static svdw_vec field_mat_vec_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a
     REQUIRE(a.cols == v.len, "field_mat_vec_mul: a[0].len() != v.len()");
     const int na = scan_na(c, a);
     const Fr* tab = vec_prep(c, v, c->w1c, c->w1t);
-    return matvec_rows(c, phase, a, (const Fr*)c->w1c.p, tab, v.len, na);
+    return matvec_rows(c, phase, a, (const Fr*)c->w1c.p, tab, v.len, na, eqsrc_vec(v));
 }
 // ZkMatrix::verify_mul (src/matrix/mod.rs:251-282) for several (a, b, c_s) triples
 // with one gamma: cells are appended exactly as consecutive verify_mul calls
@@ -1390,11 +1507,15 @@ static void verify_mul_legacy(svdw_ctx* c, uint32_t phase, const svdw_mat& a, co
     REQUIRE(cs.rows == a.rows, "verify_mul: c_s.len() != a.num_rows");
     REQUIRE(cs.cols == b.cols, "verify_mul: c_s[0].len() != b.num_col");
     const uint32_t d = cs.cols, n = a.rows;
+    c->ext_gamma = gamma;
     ensure_gamma_vec(c, d, gamma);
     const Fr* gpc = (const Fr*)c->gpc.p;
-    put_cell(c, phase, fr_from_u64(1), true);              // load_witness(F::ONE) + assert_is_const
+    const svdw_vec one = put_cell(c, phase, fr_from_u64(1), true);   // load_witness(F::ONE) + assert_is_const
+    uint64_t pows_off = 0;
     if (d > 1) {                                          // v_i = mul(v_{i-1}, init_rand)
         PB pb(c->LB);
+        pb.kext = pb.kidx(gamma);                         // gamma: a cell of the RLC context
+        pb.vsrc[1] = false;
         DView w;
         memset(&w, 0, sizeof w);
         w.ptr = gpc;
@@ -1405,25 +1526,30 @@ static void verify_mul_legacy(svdw_ctx* c, uint32_t phase, const svdw_mat& a, co
         uint8_t prev = pb.load(0), cur = pb.load(1);
         pb.gate(0);
         pb.cell(pb.K(0)); pb.cell(prev); pb.cell(pb.K(gamma)); pb.cell(cur);
-        pb.kconst = false;                                // gamma is a cell, not a Constant
         note_const(c, fr_zero());
-        run_stage(c, phase, pb, d - 1, 1, "verify_mul_gamma_pows");
+        pows_off = run_stage(c, phase, pb, d - 1, 1, "verify_mul_gamma_pows");
+        c->layout_chk.back().esrc[0] = eqsrc_chain(one.phase, one.off, phase, pows_off + 3, 4);
     }
+    const RegionChecks::EqSrc gsrc = eqsrc_chain(one.phase, one.off, phase, pows_off + 3, 4);
     const Fr* gtab = (const Fr*)c->gtab.p;
-    svdw_vec csv = matvec_rows(c, phase, cs, gpc, gtab, c->gp_len, scan_na(c, cs));
-    svdw_vec bv = matvec_rows(c, phase, b, gpc, gtab, c->gp_len, scan_na(c, b));
+    svdw_vec csv = matvec_rows(c, phase, cs, gpc, gtab, c->gp_len, scan_na(c, cs), gsrc);
+    svdw_vec bv = matvec_rows(c, phase, b, gpc, gtab, c->gp_len, scan_na(c, b), gsrc);
     const Fr* t2 = vec_prep(c, bv, c->w2c, c->w2t);
-    svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, t2, bv.len, scan_na(c, a));
+    svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, t2, bv.len, scan_na(c, a),
+                               eqsrc_vec(bv));
     PB pb(c->LB);                                         // is_equal per row (unconstrained result)
     pb.a.view[0] = view_of(c, mat_of_vec(csv));
     pb.a.view[1] = view_of(c, mat_of_vec(abv));
     uint8_t x = pb.load(0), y = pb.load(1);
     pb.g_is_equal(x, y);
     run_stage(c, phase, pb, n, 1, "verify_mul_is_equal");
+    c->layout_chk.back().esrc[0] = eqsrc_mat(mat_of_vec(csv));
+    c->layout_chk.back().esrc[1] = eqsrc_mat(mat_of_vec(abv));
 }
 
 static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, const Fr& gamma) {
     REQUIRE(n >= 1 && n <= kMaxScanJobs, "internal: verify_mul batch size");
+    c->ext_gamma = gamma;
     struct Plan {
         PB one, pows, eq;
         uint64_t one_off = 0, one_loff = 0, pows_off = 0, pows_loff = 0, eq_off = 0, eq_loff = 0;
@@ -1434,9 +1560,10 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     std::vector<Plan> pl;
     pl.reserve(n);
     uint32_t dmax = 0;
-    auto scan_append = [&](const svdw_mat& a) {
+    auto scan_append = [&](const svdw_mat& a, const RegionChecks::EqSrc& w) {
         uint64_t off;
         append(c, phase, (uint64_t)a.rows * (3ull * a.cols + 1), 0, &off, nullptr, "scan", a.rows);
+        note_scan(c, a, w);
         note_const(c, fr_zero());                             // inner_product's Constant(0)
         return svdw_vec{phase, a.rows, off + 3ull * a.cols, (int64_t)(3ull * a.cols + 1)};
     };
@@ -1452,22 +1579,26 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         Plan& p = pl.back();
         p.one.cell(p.one.K(fr_from_u64(1)));                  // load_witness(F::ONE)
         append(c, phase, p.one.a.C, 0, &p.one_off, &p.one_loff, "load_cell");
-        note_const(c, fr_from_u64(1));                        // assert_is_const(one, 1)
+        note_gates(c, p.one);                                 // assert_is_const(one, 1)
         stage_own(c, phase, p.one, 1, 1, p.one_off, p.one_loff);
         if (d > 1) {                                          // v_i = mul(v_{i-1}, init_rand)
             uint8_t prev = p.pows.load(0), cur = p.pows.load(1);
             p.pows.gate(0);                               // mul(v_(i-1), init_rand)
-            p.pows.kconst = false;                        // gamma is a cell, not a Constant
+            p.pows.kext = p.pows.kidx(gamma);             // gamma: a cell of the RLC context
+            p.pows.vsrc[1] = false;                       // v_i: produced here
             note_const(c, fr_zero());
             p.pows.cell(p.pows.K(0)); p.pows.cell(prev); p.pows.cell(p.pows.K(gamma)); p.pows.cell(cur);
             append(c, phase, (uint64_t)(d - 1) * p.pows.a.C, 0, &p.pows_off, &p.pows_loff,
                    "verify_mul_gamma_pows");
             note_gates(c, p.pows);
+            // v_(i-1): the `one` cell, then the previous mul's output
+            c->layout_chk.back().esrc[0] = eqsrc_chain(phase, p.one_off, phase, p.pows_off + 3, 4);
             stage_own(c, phase, p.pows, d - 1, 1, p.pows_off, p.pows_loff);
         }
-        p.csv = scan_append(cs);
-        p.bv = scan_append(b);
-        p.abv = scan_append(a);
+        const RegionChecks::EqSrc gsrc = eqsrc_chain(phase, p.one_off, phase, p.pows_off + 3, 4);
+        p.csv = scan_append(cs, gsrc);
+        p.bv = scan_append(b, gsrc);
+        p.abv = scan_append(a, eqsrc_vec(p.bv));
         if (sharded(c)) {                                 // this rank's rows of the three scans
             for (const auto& sv : {std::make_pair(cs, p.csv), std::make_pair(b, p.bv),
                                    std::make_pair(a, p.abv)}) {
@@ -1483,6 +1614,8 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
                &p.eq_loff, "verify_mul_is_equal", a.rows);
         note_gates(c, p.eq);
         p.eq_reg = c->layout_chk.size() - 1;
+        c->layout_chk.back().esrc[0] = eqsrc_mat(mat_of_vec(p.csv));
+        c->layout_chk.back().esrc[1] = eqsrc_mat(mat_of_vec(p.abv));
         stage_own(c, phase, p.eq, a.rows, 1, p.eq_off, p.eq_loff);
     }
     if (c->dry) return;
@@ -1836,10 +1969,12 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     std::swap(ut.rows, ut.cols); std::swap(ut.rs, ut.cs);
     std::swap(vt.rows, vt.cols); std::swap(vt.rs, vt.cs);
     DView udv;
+    EqCell udpad;
     if (r == M) {
         udv = view_of(c, mat_times_diag_mat(c, u, d));
     } else {
-        put_cell(c, 0 + u.phase, fr_zero(), true);        // zero padding constant
+        const svdw_vec z = put_cell(c, 0 + u.phase, fr_zero(), true);   // zero padding constant
+        udpad = EqCell{(int)z.phase, z.off};
         svdw_mat ud = mat_times_diag_mat(c, u, d);
         udv = view_of(c, ud);
         udv.cols = r;                                     // columns >= N read as 0
@@ -1853,7 +1988,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     svdw_mat mvt = honest_prover_mat_mul(c, m.phase, m, vt, bm, bv);
     BigU es = scale_err(err_svd, P), eu = scale_err(err_u, P);
     host_mark(c, "u.d queued");
-    check_mat_diff_views(c, m.phase, udv, view_of(c, mvt), N, M, es);
+    check_mat_diff_views(c, m.phase, udv, view_of(c, mvt), N, M, es, nullptr, udpad);
     host_mark(c, "diff queued");
     Fr q = pow2_fr(P);
     const Fr qq = fr_mul(q, q);
@@ -1909,6 +2044,11 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         }
     }
     c->gp_ev = nullptr;
+    if (!c->dry && c->hold_us) {       // every stream of the step waits for st's hold
+        hipck(launch_hold(c->hold_us, c->st), "k_hold");
+        if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
+        stream_dep(c, c->st, c->st3);
+    }
     if (!c->dry) {
         // gamma^j depends on gamma only: queue it first, on its own stream, so it
         // runs beside quantization instead of on the phase-1 chain
@@ -1947,8 +2087,6 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         seg.begin[2] = nbm + nbu;
         seg.begin[3] = nbm + nbu + nbv;
         hipck(launch_bits_reduce(dbits + 64, seg, 3, dbits, c->st), "k_bits_reduce");
-        hipck(hipMemcpyAsync(c->hbits, dbits, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, c->st),
-              "D2H");
         hipck(hipEventRecord(c->ev_bits, c->st), "hipEventRecord");
         c->bits_pending = true;
         c->qmat[0] = zm; c->qmat[1] = zu; c->qmat[2] = zv;
@@ -2021,6 +2159,82 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     if (c->prelaunched && !c->dry && !(p1_overlap && p1s == c->st2)) stream_dep(c, c->st2, c->st);
     host_mark(c, "svd_witness end");
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
+}
+
+// ------------------------------------------------------ equality lists
+// halo2-base's equality records of phase `phase` (svdw_equalities), in assign
+// order, from the layout table: per region its element program's eq words
+// (PB::eq) or the inner-product row pattern, with the source cells of the
+// loaded values (RegionChecks::esrc). copies: (source | store << 62,
+// destination) pairs, store 2 = the external init_rand cell; consts: (cell,
+// 4 canonical words).
+static uint64_t eq_src_cell(const RegionChecks::EqSrc& e, uint64_t i, uint64_t j, uint64_t t) {
+    if (e.kind == EQS_CHAIN) {
+        if (t == 0) return e.first | (uint64_t)e.first_phase << 62;
+        return (e.off + (t - 1) * (uint64_t)e.rs) | (uint64_t)e.phase << 62;
+    }
+    if (e.kind == EQS_MAT) {
+        if (e.diag_phase >= 0 && i == j) return e.diag_off | (uint64_t)e.diag_phase << 62;
+        if (i < e.rows && j < e.cols)
+            return (uint64_t)((int64_t)e.off + (int64_t)i * e.rs + (int64_t)j * e.cs) | (uint64_t)e.phase << 62;
+        if (e.pad_phase >= 0) return e.pad_off | (uint64_t)e.pad_phase << 62;
+    }
+    fail(SVDW_EINVAL, "svdw_equalities: a region's copy source is not in the cell streams");
+    return 0;
+}
+static void eq_lists(const svdw_ctx* c, uint32_t phase, std::vector<uint64_t>* copies,
+                     std::vector<uint64_t>* consts) {
+    auto konst = [&](uint64_t dst, const Fr& v) {
+        consts->push_back(dst);
+        for (int w = 0; w < 4; ++w) consts->push_back((uint64_t)v.w[2 * w] | (uint64_t)v.w[2 * w + 1] << 32);
+    };
+    const uint64_t me = (uint64_t)phase << 62;
+    for (size_t k = 0; k < c->layout.size(); ++k) {
+        const svdw_region& r = c->layout[k];
+        const RegionChecks& rc = c->layout_chk[k];
+        if (r.phase != phase || !r.n) continue;
+        if (rc.scan) {                                    // [C(0), E(a_j), E(v_j), W(s_j), ...]
+            const uint64_t R = r.rows, unit = r.n / R, L = (unit - 1) / 3;
+            for (uint64_t i = 0; i < R; ++i) {
+                const uint64_t base = r.off + i * unit;
+                konst(base, fr_zero());
+                for (uint64_t j = 0; j < L; ++j) {
+                    copies->push_back(eq_src_cell(rc.esrc[0], i, j, 0));
+                    copies->push_back(base + 1 + 3 * j);
+                    copies->push_back(eq_src_cell(rc.esrc[1], 0, 0, j));
+                    copies->push_back(base + 2 + 3 * j);
+                }
+            }
+            continue;
+        }
+        if (rc.eq.empty() || !rc.unit) continue;
+        const uint64_t unit = rc.unit, nel = r.n / unit, cols = rc.cols ? rc.cols : 1;
+        for (uint64_t e = 0; e < nel; ++e) {
+            const uint64_t base = r.off + e * unit, i = e / cols, j = e % cols;
+            for (uint32_t w : rc.eq) {
+                const uint32_t a = eq_a(w), at = eq_slot(w);
+                switch (eq_kind(w)) {
+                case EQ_CONST: konst(base + at, rc.eqk.at(a)); break;
+                case EQ_LOCAL: copies->push_back((base + a) | me); copies->push_back(base + at); break;
+                case EQ_VIEW:
+                    copies->push_back(eq_src_cell(rc.esrc[a], i, j, i));
+                    copies->push_back(base + at);
+                    break;
+                default:                                  // EQ_EXT
+                    copies->push_back(2ull << 62); copies->push_back(base + at); break;
+                }
+            }
+        }
+    }
+}
+// virtual cell -> column-major physical index (the first placement of a break cell)
+static uint64_t phys_index(const svdw_ctx* c, uint32_t phase, uint64_t v) {
+    const auto& st = c->phys.start[phase];
+    size_t col = std::upper_bound(st.begin(), st.end(), v) - st.begin();
+    REQUIRE(col > 0, "internal: cell before column 0");
+    --col;
+    if (col > 0 && v == st[col]) --col;                   // break cell: its row in the column before
+    return ((uint64_t)col << c->phys.k) + (v - st[col]);
 }
 
 // ================================================================== C ABI
@@ -2632,6 +2846,71 @@ int svdw_check_physical(svdw_ctx* c, uint32_t phase, const void* advice, const u
         out->copy_failures = h[5];
     });
 }
+int svdw_equalities(const svdw_ctx* c, uint32_t phase, uint64_t* copies, uint64_t copies_cap,
+                    uint64_t* n_copies, uint64_t* consts, uint64_t consts_cap, uint64_t* n_consts) {
+    return guarded([&] {
+        REQUIRE(c && phase < 2 && n_copies && n_consts, "bad argument");
+        std::vector<uint64_t> cp, cs;
+        eq_lists(c, phase, &cp, &cs);
+        *n_copies = cp.size() / 2;
+        *n_consts = cs.size() / 5;
+        if (copies) memcpy(copies, cp.data(), std::min<uint64_t>(copies_cap, cp.size() / 2) * 16);
+        if (consts) memcpy(consts, cs.data(), std::min<uint64_t>(consts_cap, cs.size() / 5) * 40);
+    });
+}
+int svdw_check_equalities(svdw_ctx* c, uint32_t phase, const void* columns0, const void* columns1,
+                          svdw_eq_check* out) {
+    return guarded([&] {
+        REQUIRE(c && phase < 2 && out, "bad argument");
+        REQUIRE(!c->dry, "svdw_check_equalities needs a device context");
+        const bool phys = columns0 || columns1;
+        REQUIRE(!phys || (c->phys.valid && (phase == 0 ? columns0 != nullptr : columns0 && columns1)),
+                "svdw_check_equalities: physical columns need svdw_physical_layout and phase 0's "
+                "columns (and phase 1's for phase 1)");
+        memset(out, 0, sizeof *out);
+        std::vector<uint64_t> cp, cs;
+        eq_lists(c, phase, &cp, &cs);
+        if (phys) {
+            for (size_t i = 0; i < cp.size(); i += 2) {
+                const uint32_t sp = (uint32_t)(cp[i] >> 62);
+                if (sp < 2) cp[i] = phys_index(c, sp, cp[i] & ((1ull << 62) - 1)) | (uint64_t)sp << 62;
+                cp[i + 1] = phys_index(c, phase, cp[i + 1]);
+            }
+            for (size_t i = 0; i < cs.size(); i += 5) cs[i] = phys_index(c, phase, cs[i]);
+        }
+        const Fr* s0 = phys ? (const Fr*)columns0 : c->ph[0].adv;
+        const Fr* s1 = phys ? (const Fr*)columns1 : c->ph[1].adv;
+        const Fr* dst = phase ? s1 : s0;
+        sync(c);
+        ensure_buf(c, c->chk, 6 * sizeof(unsigned long long));
+        unsigned long long* cnt = (unsigned long long*)c->chk.p;
+        hipck(hipMemsetAsync(cnt, 0, 6 * sizeof(unsigned long long), c->st), "hipMemsetAsync");
+        // upload in chunks through chkg (stream-ordered; the buffer is reused)
+        const size_t chunk = (size_t)1 << 22;
+        for (size_t i = 0; i < cp.size(); i += 2 * chunk) {
+            const size_t n = std::min(chunk, (cp.size() - i) / 2);
+            ensure_buf(c, c->chkg, n * 16);
+            hipck(hipMemcpyAsync(c->chkg.p, cp.data() + i, n * 16, hipMemcpyHostToDevice, c->st), "H2D");
+            hipck(launch_check_copies(s0, s1, dst, (const uint64_t*)c->chkg.p, n, c->ext_gamma, cnt,
+                                      c->st), "k_check_copies");
+            hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
+        }
+        for (size_t i = 0; i < cs.size(); i += 5 * chunk) {
+            const size_t n = std::min(chunk, (cs.size() - i) / 5);
+            ensure_buf(c, c->chkg, n * 40);
+            hipck(hipMemcpyAsync(c->chkg.p, cs.data() + i, n * 40, hipMemcpyHostToDevice, c->st), "H2D");
+            hipck(launch_check_consts(dst, (const uint64_t*)c->chkg.p, n, cnt + 2, c->st), "k_check_consts");
+            hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
+        }
+        unsigned long long h[4];
+        hipck(hipMemcpyAsync(h, cnt, sizeof h, hipMemcpyDeviceToHost, c->st), "D2H");
+        hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
+        out->copies_checked = h[0];
+        out->copy_failures = h[1];
+        out->consts_checked = h[2];
+        out->const_failures = h[3];
+    });
+}
 int svdw_layout(const svdw_ctx* c, svdw_region* out, uint64_t cap, uint64_t* n) {
     return guarded([&] {
         REQUIRE(c && n, "null argument");
@@ -2743,6 +3022,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "phase1_overlap") {
             REQUIRE(value >= 0 && value <= 2, "phase1_overlap: 0, 1 or 2");
             c->phase1_overlap = (int)value;
+        } else if (n == "hold_us") {         // timing aid: GPU-only schedule of a witness
+            REQUIRE(value >= 0 && value <= 100000, "hold_us: 0..100000");
+            c->hold_us = (uint32_t)value;
         } else if (n == "res_f64") {
             c->res_f64 = value != 0;
         } else if (n == "gemm_crt") {

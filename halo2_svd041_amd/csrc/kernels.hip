@@ -151,6 +151,16 @@ __global__ __launch_bounds__(256) void k_bits_reduce(const unsigned* __restrict_
     __syncthreads();
     if (threadIdx.x == 0) out[s] = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
 }
+// Timing aid ("hold_us"): one wave spinning ~us microseconds on the device clock
+// (s_memrealtime, 100 MHz) so the host finishes enqueueing before the step runs.
+__global__ void k_hold(uint64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+hipError_t launch_hold(uint32_t us, hipStream_t st) {
+    hipLaunchKernelGGL(k_hold, dim3(1), dim3(64), 0, st, (uint64_t)us * 100u);
+    return hipGetLastError();
+}
 hipError_t launch_bits_reduce(const unsigned* blockmax, const BitSegs& seg, uint32_t nseg,
                               unsigned* out, hipStream_t st) {
     if (!nseg || nseg >= (uint32_t)kMaxBitSegs) return hipErrorInvalidValue;
@@ -1669,6 +1679,55 @@ __global__ __launch_bounds__(256) void k_check_lookups(const Fr* __restrict__ lk
         v[1] += bad;
     }
     block_flush(v, cnt, nullptr);
+}
+// Equality lists (svdw_check_equalities) on cell stores: pair i = (source | its
+// store << 62, destination); store 2 is the external value `ext` (init_rand).
+// Constants: 5 words per record, (destination, canonical value).
+__global__ __launch_bounds__(256) void k_check_copies(const Fr* __restrict__ s0, const Fr* __restrict__ s1,
+                                                      const Fr* __restrict__ dst,
+                                                      const uint64_t* __restrict__ pairs, uint64_t n,
+                                                      const Fr ext, unsigned long long* cnt) {
+    uint32_t v[4] = {0, 0, 0, 0};
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t src = pairs[2 * i], d = pairs[2 * i + 1];
+        const uint32_t st = (uint32_t)(src >> 62);
+        const uint64_t so = src & ((1ull << 62) - 1);
+        const Fr a = st == 2 ? ext : ld_fr((st ? s1 : s0) + so);
+        const Fr b = ld_fr(dst + d);
+        ++v[0];
+        v[1] += !fr_eq(a, b);
+    }
+    block_flush(v, cnt, nullptr);
+}
+__global__ __launch_bounds__(256) void k_check_consts(const Fr* __restrict__ dst,
+                                                      const uint64_t* __restrict__ recs, uint64_t n,
+                                                      unsigned long long* cnt) {
+    uint32_t v[4] = {0, 0, 0, 0};
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t* r = recs + 5 * i;
+        const Fr b = ld_fr(dst + r[0]);
+        Fr k;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) { k.w[2 * w] = (uint32_t)r[1 + w]; k.w[2 * w + 1] = (uint32_t)(r[1 + w] >> 32); }
+        ++v[0];
+        v[1] += !fr_eq(k, b);
+    }
+    block_flush(v, cnt, nullptr);
+}
+hipError_t launch_check_copies(const Fr* s0, const Fr* s1, const Fr* dst, const uint64_t* pairs,
+                               uint64_t n, const Fr& ext, unsigned long long* cnt, hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_check_copies, dim3(check_grid(n)), dim3(256), 0, st, s0, s1, dst, pairs, n,
+                       ext, cnt);
+    return hipGetLastError();
+}
+hipError_t launch_check_consts(const Fr* dst, const uint64_t* recs, uint64_t n,
+                               unsigned long long* cnt, hipStream_t st) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_check_consts, dim3(check_grid(n)), dim3(256), 0, st, dst, recs, n, cnt);
+    return hipGetLastError();
 }
 hipError_t launch_check_lookups(const Fr* lk, uint64_t n, uint32_t lb, unsigned long long* cnt,
                                 hipStream_t st) {

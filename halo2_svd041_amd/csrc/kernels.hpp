@@ -101,7 +101,34 @@ struct RegionChecks {
     std::vector<uint32_t> words;
     uint32_t unit = 0, cols = 1;
     Src src[kMaxViews] = {{-1, 0, 0, 0, 0, 0}, {-1, 0, 0, 0, 0, 0}};
+    // ---- equality lists (svdw_equalities): halo2-base's copy / constant
+    // equalities of the region, per element in assign order (eq words, below),
+    // with the source cells of the element's loaded values per view (esrc)
+    std::vector<uint32_t> eq;
+    struct EqSrc {
+        int kind = 0;                 // EQS_NONE / EQS_MAT / EQS_CHAIN
+        uint32_t phase = 0;           // EQS_MAT: cell (i, j) = off + i rs + j cs inside rows x cols,
+        uint64_t off = 0;             //   else `pad`; diag >= 0 phase: (i == i) -> diag, else pad
+        int64_t rs = 0, cs = 0;
+        uint32_t rows = 0, cols = 0;
+        int pad_phase = -1, diag_phase = -1;
+        uint64_t pad_off = 0, diag_off = 0;
+        // EQS_CHAIN (vector, index t = the element's row i, or the scan term j):
+        // t == 0 -> (first_phase, first), else (phase, off + (t - 1) * rs)
+        uint32_t first_phase = 0;
+        uint64_t first = 0;
+    } esrc[kMaxViews];
+    std::vector<Fr> eqk;              // the program's constants (EQ_CONST values)
+    bool scan = false;                // inner_product rows: [C(0), E(a_j), E(v_j), W(s_j), ...],
+                                      // a = esrc[0] (row i, term j), v = esrc[1] (term j)
 };
+// equality words of an element program: kind << 24 | a << 12 | slot
+enum : uint32_t { EQ_CONST = 0, EQ_LOCAL = 1, EQ_VIEW = 2, EQ_EXT = 3 };
+enum : int { EQS_NONE = 0, EQS_MAT = 1, EQS_CHAIN = 2 };
+constexpr uint32_t eq_word(uint32_t kind, uint32_t a, uint32_t slot) { return kind << 24 | a << 12 | slot; }
+constexpr uint32_t eq_kind(uint32_t w) { return w >> 24; }
+constexpr uint32_t eq_a(uint32_t w) { return (w >> 12) & 0xfff; }
+constexpr uint32_t eq_slot(uint32_t w) { return w & 0xfff; }
 // (u0: index in the region of the first unit at adv, for the view rows / columns)
 hipError_t launch_check_cells(const Fr* adv, uint64_t u0, uint64_t nunits, uint32_t unit, uint32_t cols,
                               const uint32_t* words, uint32_t nw, ChkView v0, ChkView v1,
@@ -119,12 +146,20 @@ hipError_t launch_check_physical(const Fr* cols, const uint8_t* q, uint64_t rows
                                  unsigned long long* cnt, hipStream_t st);
 hipError_t launch_check_breaks(const Fr* cols, uint64_t rows, const uint64_t* bp, uint32_t nb,
                                unsigned long long* cnt, hipStream_t st);
+// Equality lists: cnt[0..1] += pairs checked / failing (source store from the
+// top two bits: s0, s1, or 2 = ext), constants checked / failing.
+hipError_t launch_check_copies(const Fr* s0, const Fr* s1, const Fr* dst, const uint64_t* pairs,
+                               uint64_t n, const Fr& ext, unsigned long long* cnt, hipStream_t st);
+hipError_t launch_check_consts(const Fr* dst, const uint64_t* recs, uint64_t n,
+                               unsigned long long* cnt, hipStream_t st);
 hipError_t launch_check_lookups(const Fr* lk, uint64_t n, uint32_t lb, unsigned long long* cnt,
                                 hipStream_t st);
 static constexpr int kMaxBitSegs = 8;
 struct BitSegs {
     uint32_t begin[kMaxBitSegs];
 };
+// Timing aid: a one-wave kernel spinning `us` microseconds on the device clock.
+hipError_t launch_hold(uint32_t us, hipStream_t st);
 hipError_t launch_bits_reduce(const unsigned* blockmax, const BitSegs& seg, uint32_t nseg,
                               unsigned* out, hipStream_t st);
 // k_maxbits grid bound (= words written to `out`).

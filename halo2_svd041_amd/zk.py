@@ -19,7 +19,7 @@ from typing import Optional
 
 import numpy as np
 
-from ._lib import (CheckResult, PhysParams, Counts, DivScale, InputDims, KStat, Mat, Params, Payload, Region, Segment, SvdConfig, SvdwError,
+from ._lib import (CheckResult, EqCheck, PhysParams, Counts, DivScale, InputDims, KStat, Mat, Params, Payload, Region, Segment, SvdConfig, SvdwError,
                    Vec, check, lib)
 
 P_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
@@ -201,6 +201,34 @@ class Context:
                                         ct.byref(r)))
         return {"gates_checked": r.gates_checked, "gate_failures": r.gate_failures,
                 "copies_checked": r.copies_checked, "copy_failures": r.copy_failures}
+
+    def equalities(self, phase: int):
+        """Copy-constraint lists of the last witness (svdw_equalities), in assign
+        order: copies (n, 3) uint64 [source phase (2: init_rand), source cell,
+        destination cell], consts: list of (cell, value int)."""
+        nc, nk = ct.c_uint64(), ct.c_uint64()
+        check(lib().svdw_equalities(self._h, phase, None, 0, ct.byref(nc), None, 0, ct.byref(nk)))
+        cp = np.zeros((max(nc.value, 1), 2), dtype=np.uint64)
+        ks = np.zeros((max(nk.value, 1), 5), dtype=np.uint64)
+        check(lib().svdw_equalities(self._h, phase, cp.ctypes.data, nc.value, ct.byref(nc),
+                                    ks.ctypes.data, nk.value, ct.byref(nk)))
+        cp, ks = cp[:nc.value], ks[:nk.value]
+        out = np.empty((cp.shape[0], 3), dtype=np.uint64)
+        out[:, 0] = cp[:, 0] >> np.uint64(62)
+        out[:, 1] = cp[:, 0] & np.uint64((1 << 62) - 1)
+        out[:, 2] = cp[:, 1]
+        consts = [(int(r[0]), words_to_int(r[1:])) for r in ks]
+        return out, consts
+
+    def check_equalities(self, phase: int, columns0=None, columns1=None) -> dict:
+        """Device check of the equality records (svdw_check_equalities) on the
+        cell streams, or on assigned physical columns (torch tensors)."""
+        r = EqCheck()
+        p0 = columns0.data_ptr() if columns0 is not None else None
+        p1 = columns1.data_ptr() if columns1 is not None else None
+        check(lib().svdw_check_equalities(self._h, phase, p0, p1, ct.byref(r)))
+        return {"copies_checked": r.copies_checked, "copy_failures": r.copy_failures,
+                "consts_checked": r.consts_checked, "const_failures": r.const_failures}
 
     def profile(self, on: bool = True, prefix: str = "") -> None:
         """Record HIP events around kernel launches (names starting with `prefix`)."""

@@ -332,6 +332,30 @@ int svdw_assign_columns(svdw_ctx* ctx, uint32_t phase, void* advice, uint8_t* se
  * break cell against row 0 of the next column (copies_*). */
 int svdw_check_physical(svdw_ctx* ctx, uint32_t phase, const void* advice, const uint8_t* selectors,
                         uint32_t ncols, svdw_check_result* out);
+/* Copy-constraint (equality) lists of phase `phase` of the last witness: the
+ * records halo2-base 0.4.1's copy manager holds after the same calls, in assign
+ * order -- every QuantumCell::Existing cell against its source cell, every
+ * Constant cell (and assert_is_const) against its value, range_check's
+ * constrain_equal(a, last running sum) -- so keygen / MockProver can run on
+ * the engine's columns. Replaces Context's copy manager (advice_equalities,
+ * constant_equalities) consumed by raw_synthesize_phase0/1
+ * (src/utils/executor.rs:100-102,116-118; src/scaffold/mod.rs:93-106).
+ * copies: 2 words per record, (source cell | source phase << 62, destination
+ * cell of `phase`); source phase 2 = the external init_rand cell of verify_mul
+ * (RLC context). consts: 5 words per record, (cell, 4 canonical LE words).
+ * Works on dry (planner) contexts. Null buffers: counts only. */
+int svdw_equalities(const svdw_ctx* ctx, uint32_t phase, uint64_t* copies, uint64_t copies_cap,
+                    uint64_t* n_copies, uint64_t* consts, uint64_t consts_cap, uint64_t* n_consts);
+typedef struct {
+    uint64_t copies_checked, copy_failures;
+    uint64_t consts_checked, const_failures;
+} svdw_eq_check;
+/* Check every equality record of `phase` on the device: on the virtual cell
+ * streams (columns0 = columns1 = NULL), or on assigned physical columns
+ * (svdw_assign_columns output of phase 0, and of phase 1 for phase 1), each
+ * cell at its first placement. External sources compare with the last init_rand. */
+int svdw_check_equalities(svdw_ctx* ctx, uint32_t phase, const void* columns0, const void* columns1,
+                          svdw_eq_check* out);
 /* Up to cap segments of the last witness into out; *n = total count. */
 int svdw_shard_segments(const svdw_ctx* ctx, svdw_segment* out, uint64_t cap, uint64_t* n);
 
