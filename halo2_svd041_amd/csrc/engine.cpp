@@ -433,6 +433,9 @@ struct svdw_ctx {
     bool prelaunched = false;               // this witness's products were queued on st2
     uint32_t hold_us = 0;                   // "hold_us": timing aid, st spins this long first
     Fr ext_gamma{};                          // init_rand of the last verify_mul (equality source 2)
+    uint64_t ext_off = 0;                    // its cell in the RLC context
+    bool rlc_prefix = false;                 // "rlc_prefix": svd_witness's phase 1 starts with the
+                                             // ctx_gate cells of load_rlc_cache(.., 1)
     int p1_at = -1;                         // "p1_at": phase 1 on st3 (mode 2) enqueued after
                                             // phase-0 stage 0 / 1 / 2 (the u, v bounds), 3: at the
                                             // end; -1: auto (tools/shard_sim.py --opt p1_at=):
@@ -555,6 +558,7 @@ static void clear_streams(svdw_ctx* c) {
     c->owned.clear();
     c->layout.clear();
     c->layout_chk.clear();
+    c->ext_off = 0;
     c->consts.clear();
     c->phys.valid = false;
     c->bits_pending = false;
@@ -2030,10 +2034,11 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     if (!c->dry) {
         // exact sizes from the dry planner: no growth copies inside the step
         const std::vector<uint64_t> key = {N, M, cfg.max_bits_d, f64_key(cfg.max_norm),
-                                           f64_key(cfg.eps_svd), f64_key(cfg.eps_u)};
+                                           f64_key(cfg.eps_svd), f64_key(cfg.eps_u), c->rlc_prefix};
         if (key != c->plan_key) {
             svdw_ctx plan;
             plan.P = c->P; plan.LB = c->LB;
+            plan.rlc_prefix = c->rlc_prefix;
             svd_witness(&plan, nullptr, nullptr, nullptr, nullptr, N, M, false, cfg, gamma);
             c->plan_key = key;
             c->plan_val = {plan.ph[0].n, plan.ph[0].nl, plan.ph[1].n, plan.ph[1].nl};
@@ -2042,6 +2047,18 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
             grow(c, c->ph[p].adv, 0, c->ph[p].cap, c->plan_val[2 * p]);
             grow(c, c->ph[p].lk, 0, c->ph[p].lcap, c->plan_val[2 * p + 1]);
         }
+    }
+    // examples/svd_example.rs:183-184 run rlc.load_rlc_cache((ctx_gate, ctx_rlc), gate, 1)
+    // on the phase-1 pair before check_svd_phase1. As recalled from axiom-eth's
+    // RlcChip (un-vendored; parity unpinned), an empty cache loads gamma as
+    // compute_rlc_fixed_len(ctx_rlc, [one, zero]) with one = ctx_gate.load_constant(1),
+    // zero = ctx_gate.load_zero(): two constant cells at the head of ctx_gate (the
+    // stream here); [E(one), E(zero), W(gamma)] go to ctx_rlc, whose cell 2 is init_rand.
+    c->ext_off = 0;
+    if (c->rlc_prefix) {
+        put_cell(c, 1, fr_from_u64(1), true);
+        put_cell(c, 1, fr_zero(), true);
+        c->ext_off = 2;
     }
     c->gp_ev = nullptr;
     if (!c->dry && c->hold_us) {       // every stream of the step waits for st's hold
@@ -2220,8 +2237,8 @@ static void eq_lists(const svdw_ctx* c, uint32_t phase, std::vector<uint64_t>* c
                     copies->push_back(eq_src_cell(rc.esrc[a], i, j, i));
                     copies->push_back(base + at);
                     break;
-                default:                                  // EQ_EXT
-                    copies->push_back(2ull << 62); copies->push_back(base + at); break;
+                default:                                  // EQ_EXT: init_rand's RLC cell
+                    copies->push_back(c->ext_off | 2ull << 62); copies->push_back(base + at); break;
                 }
             }
         }
@@ -3025,6 +3042,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "hold_us") {         // timing aid: GPU-only schedule of a witness
             REQUIRE(value >= 0 && value <= 100000, "hold_us: 0..100000");
             c->hold_us = (uint32_t)value;
+        } else if (n == "rlc_prefix") {
+            c->rlc_prefix = value != 0;
         } else if (n == "res_f64") {
             c->res_f64 = value != 0;
         } else if (n == "gemm_crt") {

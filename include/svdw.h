@@ -228,9 +228,17 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   terms per thread, unreduced partial sums and small-operand products where
  *   bounds are known); "scan_na_host" 0 | 1 (row-scan operand widths inside
  *   svdw_svd_witness: read on the device from the quantization's bit-length
- *   words, or 1: read back by the host first, the round-1 behaviour).
- * Timing probe (NOT bit-identical, for A/B measurements only): "stage_probe"
- *   0 | 1 (skip the stage programs) | 2 (store a constant instead of cells). */
+ *   words, or 1: read back by the host first, the round-1 behaviour);
+ *   "res_f64" 1 | 0 (svd_witness with inputs in HBM: the CRT residue planes of
+ *   m, u, v built from the f64 inputs in one launch, or from the quantized cells).
+ * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:
+ *   phase 1 starts with the two ctx_gate constant cells [1, 0] that
+ *   examples/svd_example.rs:183's rlc.load_rlc_cache(.., 1) appends as recalled
+ *   from axiom-eth's RlcChip, parity unpinned; init_rand is then RLC cell 2).
+ * Timing aids (NOT bit-identical, for A/B measurements only): "stage_probe"
+ *   0 | 1 (skip the stage programs) | 2 (store a constant instead of cells);
+ *   "hold_us" 0 | us (svd_witness: the step's streams wait behind a kernel
+ *   spinning that long, so the GPU schedule is measured without host gaps). */
 int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);
 
 /* ----------------------------------------------------------- profiling */

@@ -514,9 +514,21 @@ class SvdWitness:
     err_u: float
 
 
+def load_rlc_cache_1(ctx_gate: Context, rlc: Context, gamma: int) -> AV:
+    """rlc.load_rlc_cache((ctx_gate, ctx_rlc), gate, 1) then gamma_pow_cached()[0]
+    (examples/svd_example.rs:183-184), as recalled from axiom-eth's RlcChip
+    (un-vendored crate; PARITY UNPINNED): an empty cache loads gamma as
+    compute_rlc_fixed_len(ctx_rlc, [one, zero]) = one * gamma + zero, with
+    one = ctx_gate.load_constant(1) and zero = ctx_gate.load_zero() (a constant);
+    the RLC trace [E(one), E(zero), W(gamma)] lives in ctx_rlc."""
+    one = load_constant(ctx_gate, 1)
+    zero = load_constant(ctx_gate, 0)
+    return rlc.get(assign_region(rlc, [E(one), E(zero), W(gamma)], []) + 2)
+
+
 def svd_witness(m, u, v, d, p: int, lookup_bits: int, gamma: int,
                 max_norm: float = 100.0, eps_svd: float = 1e-10, eps_u: float = 1e-10,
-                max_bits_d: int = 30) -> SvdWitness:
+                max_bits_d: int = 30, rlc_prefix: bool = False) -> SvdWitness:
     rc = RangeChip(lookup_bits)
     ctx0 = Context(phase=0)
     zm = zkmatrix_new(ctx0, p, m)
@@ -526,8 +538,8 @@ def svd_witness(m, u, v, d, p: int, lookup_bits: int, gamma: int,
     err_svd, err_u = err_calc(p, max(len(m), len(m[0])), max_norm, eps_svd, eps_u)
     pl = check_svd_phase0(ctx0, rc, p, zm, zu, zv, zd, err_svd, err_u, max_bits_d)
     rlc = Context(phase=1)
-    g = load_witness(rlc, gamma)
     ctx1 = Context(phase=1)
+    g = load_rlc_cache_1(ctx1, rlc, gamma) if rlc_prefix else load_witness(rlc, gamma)
     check_svd_phase1(ctx1, zm, zu, zv, pl, g)
     return SvdWitness(ctx0, ctx1, err_svd, err_u)
 

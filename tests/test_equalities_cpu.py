@@ -18,7 +18,7 @@ from conftest import gamma_for, gen_svd_input
 def _oracle_lists(w, octx):
     def phase_of(av):
         return 0 if av.ctx is w.ctx0 else (1 if av.ctx is w.ctx1 else 2)
-    copies = [(phase_of(a), a.idx if phase_of(a) < 2 else 0, dst) for a, dst in octx.copies]
+    copies = [(phase_of(a), a.idx, dst) for a, dst in octx.copies]
     consts = [(i, v % po.P_MOD) for i, v in octx.consts]
     return copies, consts
 
@@ -106,4 +106,25 @@ def test_rescale_and_inner_product_equalities(P, LB):
     ocp, oks = _oracle_lists(W, o0)
     assert [tuple(int(v) for v in r) for r in cp] == ocp
     assert ks == oks
+    ctx.close()
+
+
+@pytest.mark.parametrize("N,M,P", [(4, 4, 32), (5, 3, 63)])
+def test_rlc_prefix_equalities(N, M, P):
+    """rlc_prefix: load_rlc_cache(.., 1)'s two ctx_gate constants head phase 1
+    and init_rand is RLC cell 2 (recalled axiom-eth construction, parity
+    unpinned): the lists shift with the stream and still match the oracle."""
+    m, u, d, v = gen_svd_input(N, M, seed=3)
+    g = gamma_for(9)
+    ctx = hs.Context(device=-1, precision_bits=P, lookup_bits=19)
+    ctx.set_option("rlc_prefix", 1)
+    hs.svd_witness(ctx, m, u, v, d, g)
+    w = po.svd_witness(m.tolist(), u.tolist(), v.tolist(), d.tolist(), P, 19, gamma=g, rlc_prefix=True)
+    for ph, octx in ((0, w.ctx0), (1, w.ctx1)):
+        cp, ks = ctx.equalities(ph)
+        ocp, oks = _oracle_lists(w, octx)
+        assert [tuple(int(x) for x in r) for r in cp] == ocp, ph
+        assert ks == oks, ph
+    _, ks1 = ctx.equalities(1)
+    assert ks1[:2] == [(0, 1), (1, 0)]
     ctx.close()

@@ -73,6 +73,22 @@ def test_golden_known_answers(path):
             assert exp["constraints_satisfied"], exp
 
 
+@pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
+def test_rlc_prefix_golden_consistent(path):
+    """The rlc_prefix phase-1 digests (tests/golden/add_rlc_digests.py: the Python
+    oracle's load_rlc_cache(.., 1) restatement, parity unpinned) are the two
+    ctx_gate constants [1, 0] followed by the C oracle's phase-1 stream."""
+    case = _load(path)
+    g = int(case["gamma"])
+    for exp in case["expected"]:
+        m, u, v, d = _inputs(case, exp["input"])
+        _, _, a1 = corc.svd_witness(m, u, v, d, exp["precision_bits"], case["lookup_bits"], g)
+        head = np.array([[1, 0, 0, 0], [0, 0, 0, 0]], dtype=np.uint64)
+        both = np.concatenate([head, a1])
+        assert both.shape[0] == exp["advice1_rlc"]
+        assert _sha(both) == exp["sha256_advice1_rlc"]
+
+
 def test_serde_parse_mode_changes_p63_witness():
     """serde_json default parsing differs by 1 ulp on some values; at P=63 the
     quantized cells (hence the digests) differ, at P=32 they typically do not."""
@@ -95,6 +111,23 @@ def test_engine_matches_golden(gpu_ctx_factory, path):
         assert _sha(ctx.advice(0)) == exp["sha256_advice0"]
         assert _sha(ctx.lookups(0)) == exp["sha256_lookup0"]
         assert _sha(ctx.advice(1)) == exp["sha256_advice1"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
+def test_engine_rlc_prefix_golden(gpu_ctx_factory, path):
+    """rlc_prefix on: the engine's phase-1 stream (with load_rlc_cache's two
+    ctx_gate cells) matches the golden digest; phase 0 is unchanged."""
+    import halo2_svd041_amd as hs
+    case = _load(path)
+    g = int(case["gamma"])
+    for exp in case["expected"]:
+        m, u, v, d = _inputs(case, exp["input"])
+        ctx = gpu_ctx_factory(exp["precision_bits"], case["lookup_bits"])
+        ctx.set_option("rlc_prefix", 1)
+        hs.svd_witness(ctx, m, u, v, d, g)
+        assert _sha(ctx.advice(0)) == exp["sha256_advice0"]
+        assert _sha(ctx.advice(1)) == exp["sha256_advice1_rlc"]
 
 
 @pytest.mark.gpu
