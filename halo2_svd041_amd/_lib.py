@@ -170,6 +170,9 @@ SIGNATURES = {
     "svdw_assign_columns": (_i32, [_P, _u32, _P, _P, _P]),
     "svdw_check_physical": (_i32, [_P, _u32, _P, _P, _u32, ct.POINTER(CheckResult)]),
     "svdw_equalities": (_i32, [_P, _u32, _P, _u64, _u64p, _P, _u64, _u64p]),
+    "svdw_zkvector_norm": (_i32, [_P, _u32, ct.POINTER(Vec), ct.POINTER(DivScale), _u32, ct.POINTER(Vec)]),
+    "svdw_zkvector_dist": (_i32, [_P, _u32, ct.POINTER(Vec), ct.POINTER(Vec), ct.POINTER(DivScale), _u32,
+                                  ct.POINTER(Vec)]),
     "svdw_check_equalities": (_i32, [_P, _u32, _P, _P, ct.POINTER(EqCheck)]),
     "svdw_profile_collect": (_i32, [_P, ct.POINTER(KStat), _u32, ct.POINTER(_u32)]),
     "svdw_plan_svd": (_i32, [_u32, _u32, _u32, _u32, ct.POINTER(SvdConfig), ct.POINTER(Counts)]),

@@ -346,6 +346,33 @@ struct PB {
         uint8_t q = div_mod_pow2(t, p, nb);
         return g_sub_k(q, pow2_fr(s - p));
     }
+    // FixedPointChip041::qsqrt (ZkVector::norm / dist, src/matrix/mod.rs:124-131,
+    // 156-164), parameterised (the chip's source is unavailable: PARITY UNPINNED;
+    // oracle/pyoracle.py qsqrt): y = floor(sqrt(a 2^P)) for a fixed-point a in
+    // [0, 2^nbits), as load_witness(y) with range_check(y, ny), t = mul(a, 2^P),
+    // d = sub(t, mul(y, y)) and f = sub(mul(y, 2), d), both range-checked on nd
+    // bits: 0 <= t - y^2 <= 2y, i.e. y^2 <= t < (y + 1)^2.
+    uint8_t qsqrt(uint8_t x, uint32_t p, uint32_t nbits) {
+        const uint32_t ny = (nbits + p + 1) / 2 + 1, nd = ny + 1;
+        uint8_t t = newv();
+        op(MO_FDBL, t, x, (uint8_t)p);                   // a 2^P (< 2^254: an integer)
+        uint8_t y = newv();
+        op(MO_ISQRT, y, t, 0);
+        cell(y);                                          // load_witness(y)
+        range_check(y, ny);
+        gate(a.C);
+        cell(K(0)); cell(x); cell(K(pow2_fr(p))); cell(t);   // mul(a, 2^P)
+        uint8_t y2 = g_mul(y, y);
+        uint8_t d = g_sub(t, y2);
+        range_check(d, nd);
+        uint8_t e = newv();
+        op(MO_FDBL, e, y, 1);
+        gate(a.C);
+        cell(K(0)); cell(y); cell(K(2)); cell(e);          // mul(y, 2)
+        uint8_t f = g_sub(e, d);
+        range_check(f, nd);
+        return y;
+    }
     // check_abs_less_than (src/matrix/mod.rs:425-435)
     void check_abs_less_than(uint8_t x, const BigU& bnd) {
         if (big_is_zero(bnd)) fail(SVDW_EINVAL, "check_abs_less_than: bound must be >= 1");
@@ -1025,7 +1052,7 @@ struct DivScale {
 static DivScale div_scale_of(const svdw_ctx* c, const svdw_div_scale* cfg) {
     DivScale d;
     d.s = cfg && cfg->shift_bits ? cfg->shift_bits : 3 * c->P;
-    d.nb = cfg && cfg->num_bits ? cfg->num_bits : d.s + 1;
+    d.nb = cfg && cfg->num_bits ? cfg->num_bits : 4 * c->P + 1;   // the reference's cell counts (svdw.h)
     REQUIRE(d.s >= c->P && d.s < 254 && d.nb > d.s && d.nb <= 253 && d.nb - c->P <= 200,
             "signed_div_scale: need P <= shift_bits < num_bits <= 253, num_bits - P <= 200");
     return d;
@@ -1061,6 +1088,16 @@ static svdw_vec zkvector_norm_square(svdw_ctx* c, uint32_t phase, const svdw_vec
 // ZkVector::_dist_square (src/matrix/mod.rs:135-148): diff_i = qsub(self_i, x_i)
 // (FixedPointChip041::qsub = gate.sub [ext, inferred as for entries_in_desc_order]:
 // cells [a - b, b, 1, a]), then diff._norm_square.
+// qsqrt of a one-element vector (ZkVector::norm / dist's final step)
+static svdw_vec qsqrt_vec(svdw_ctx* c, uint32_t phase, const svdw_vec& a, uint32_t nbits) {
+    const uint32_t nb = nbits ? nbits : 2 * c->P;
+    REQUIRE(nb >= 1 && nb + c->P <= 250, "qsqrt: need 1 <= sqrt_bits, sqrt_bits + P <= 250");
+    PB pb(c->LB);
+    pb.a.view[0] = view_of(c, mat_of_vec(a));
+    pb.qsqrt(pb.load(0), c->P, nb);
+    uint64_t off = run_stage(c, phase, pb, 1, 1, "qsqrt");
+    return svdw_vec{phase, 1, off, 1};                   // y: the gadget's first cell
+}
 static svdw_vec zkvector_dist_square(svdw_ctx* c, uint32_t phase, const svdw_vec& self,
                                      const svdw_vec& x, DivScale d) {
     REQUIRE(self.len == x.len && x.len >= 1, "ZkVector::_dist_square: length mismatch");
@@ -2487,6 +2524,33 @@ int svdw_zkvector_norm_square(svdw_ctx* c, uint32_t phase, const svdw_vec* self,
         const DivScale d = div_scale_of(c, cfg);
         pregrow(c, [&](svdw_ctx* y) { zkvector_norm_square(y, phase, *self, d); });
         *out = zkvector_norm_square(c, phase, *self, d);
+    });
+}
+int svdw_zkvector_norm(svdw_ctx* c, uint32_t phase, const svdw_vec* self, const svdw_div_scale* cfg,
+                       uint32_t sqrt_bits, svdw_vec* out) {
+    return guarded([&] {
+        REQUIRE(c && self && out, "null argument");
+        REQUIRE(phase < 2, "phase must be 0 or 1");
+        check_vec(c, *self);
+        const DivScale d = div_scale_of(c, cfg);
+        auto f = [&](svdw_ctx* x) { return qsqrt_vec(x, phase, zkvector_norm_square(x, phase, *self, d), sqrt_bits); };
+        pregrow(c, f);
+        *out = f(c);
+    });
+}
+int svdw_zkvector_dist(svdw_ctx* c, uint32_t phase, const svdw_vec* self, const svdw_vec* x,
+                       const svdw_div_scale* cfg, uint32_t sqrt_bits, svdw_vec* out) {
+    return guarded([&] {
+        REQUIRE(c && self && x && out, "null argument");
+        REQUIRE(phase < 2, "phase must be 0 or 1");
+        check_vec(c, *self);
+        check_vec(c, *x);
+        const DivScale d = div_scale_of(c, cfg);
+        auto f = [&](svdw_ctx* y) {
+            return qsqrt_vec(y, phase, zkvector_dist_square(y, phase, *self, *x, d), sqrt_bits);
+        };
+        pregrow(c, f);
+        *out = f(c);
     });
 }
 int svdw_zkvector_dist_square(svdw_ctx* c, uint32_t phase, const svdw_vec* self, const svdw_vec* x,

@@ -460,6 +460,38 @@ __device__ __forceinline__ void element_program(const StageArgs& a, uint32_t e, 
                 lds_put(dst, fr_pow_u64(lds_get(sK + op.a * VW), x, x ? 64 - __clzll(x) : 1));
                 break;
             }
+            case MO_ISQRT: {
+                // bit by bit from 2^127 down: keep the bit when (y | b)^2 <= v
+                const Fr v = lds_get(myV + op.a * VW);
+                uint32_t y[4] = {0u, 0u, 0u, 0u};
+                for (int bit = 127; bit >= 0; --bit) {
+                    uint32_t c[4] = {y[0], y[1], y[2], y[3]};
+                    c[bit >> 5] |= 1u << (bit & 31);
+                    uint32_t sq[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        uint64_t carry = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const uint64_t t = (uint64_t)c[i] * c[j] + sq[i + j] + carry;
+                            sq[i + j] = (uint32_t)t;
+                            carry = t >> 32;
+                        }
+                        sq[i + 4] = (uint32_t)carry;
+                    }
+                    bool le = true;                     // sq <= v (lexicographic from the top word)
+                    bool decided = false;
+#pragma unroll
+                    for (int w = 7; w >= 0; --w) {
+                        if (!decided && sq[w] != v.w[w]) { le = sq[w] < v.w[w]; decided = true; }
+                    }
+                    if (le) { y[0] = c[0]; y[1] = c[1]; y[2] = c[2]; y[3] = c[3]; }
+                }
+                Fr r = fr_zero();
+                r.w[0] = y[0]; r.w[1] = y[1]; r.w[2] = y[2]; r.w[3] = y[3];
+                lds_put(dst, r);
+                break;
+            }
             case MO_SHR: {
                 const uint32_t* s = myV + op.a * VW;    // words straight from LDS
                 const uint32_t q = op.p0 >> 5, r = op.p0 & 31;

@@ -46,6 +46,7 @@ enum : uint8_t {
     MO_ISZERO,       // V[dst] = (V[a]==0), V[dst+1] = V[a]==0 ? 1 : V[a]^-1
     MO_POWK,         // V[dst] = K[a] ^ (e + p0)                         (verify_mul's gamma powers)
     MO_SHR,          // V[dst] = V[a] >> p0 (canonical value, full width; div_mod quotients)
+    MO_ISQRT,        // V[dst] = floor(sqrt(V[a])) of the canonical value as an integer (< 2^256)
 };
 struct MicroOp {
     uint8_t op, dst, a, b;
@@ -68,8 +69,8 @@ static constexpr uint32_t STAGE_INC = 512;       // phase B decoding slot ops pe
 
 static constexpr int kMaxViews = 2;
 static constexpr int kMaxMicro = 16;
-static constexpr int kMaxAdv = 112;
-static constexpr int kMaxLk = 32;
+static constexpr int kMaxAdv = 160;
+static constexpr int kMaxLk = 48;
 static constexpr int kMaxK = 32;
 static constexpr int kMaxV = 12;
 

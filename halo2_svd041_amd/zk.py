@@ -365,6 +365,25 @@ class ZkVector:
                                               ct.byref(cfg), ct.byref(out)))
         return ZkVector(self.ctx, out)
 
+    def norm(self, phase: int = 0, shift_bits: int = 0, num_bits: int = 0,
+             sqrt_bits: int = 0) -> "ZkVector":
+        """ZkVector::norm (src/matrix/mod.rs:124-131): qsqrt(_norm_square); qsqrt is
+        the parameterised construction of svdw_zkvector_norm (parity unpinned)."""
+        out = Vec()
+        cfg = DivScale(shift_bits, num_bits)
+        check(lib().svdw_zkvector_norm(self.ctx.handle, phase, ct.byref(self.vec), ct.byref(cfg),
+                                       sqrt_bits, ct.byref(out)))
+        return ZkVector(self.ctx, out)
+
+    def dist(self, x: "ZkVector", phase: int = 0, shift_bits: int = 0, num_bits: int = 0,
+             sqrt_bits: int = 0) -> "ZkVector":
+        """ZkVector::dist (src/matrix/mod.rs:156-164): qsqrt(_dist_square(x))."""
+        out = Vec()
+        cfg = DivScale(shift_bits, num_bits)
+        check(lib().svdw_zkvector_dist(self.ctx.handle, phase, ct.byref(self.vec), ct.byref(x.vec),
+                                       ct.byref(cfg), sqrt_bits, ct.byref(out)))
+        return ZkVector(self.ctx, out)
+
     def _dist_square(self, x: "ZkVector", phase: int = 0, shift_bits: int = 0,
                      num_bits: int = 0) -> "ZkVector":
         """ZkVector::_dist_square (src/matrix/mod.rs:135-148): 1-element vector."""

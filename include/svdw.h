@@ -132,7 +132,13 @@ int svdw_mat_times_diag_mat(svdw_ctx* ctx, const svdw_mat* a, const svdw_vec* v,
  * (div_mod = [r, 2^P, q, t] + check_big_less_than_safe(q, 2^NB/2^P + 1)
  *  + check_big_less_than_safe(r, 2^P)), i.e. floor(x / 2^P) for |x| < 2^S.
  * Zero fields (or a null pointer) select S = 3P (the domain rescale_matrix's
- * doc states, src/matrix/mod.rs:350-353) and NB = S + 1. */
+ * doc states, src/matrix/mod.rs:350-353) and NB = 4P + 1 (NB = S + 1 is the
+ * tightest sound choice). NB = 4P + 1 is the choice that reproduces the
+ * reference's own cell counts: 90 cells per element at P = 32, LOOKUP_BITS = 12
+ * ("#CONSTRAINTS = 90", src/matrix/mod.rs:102; "~94 (when lookup_bits = 12)",
+ * :348) and 60-90 for P = 32 across LOOKUP_BITS 12-24, more for P > 32
+ * (README.md:51: "60N^2 - 100N^2, depends on LB; higher for P>32"); NB = 3P + 1
+ * gives 72 at P = 32, LB = 12. Both stay parity unpinned. */
 typedef struct {
     uint32_t shift_bits;
     uint32_t num_bits;
@@ -147,12 +153,22 @@ int svdw_zkvector_inner_product(svdw_ctx* ctx, uint32_t phase, const svdw_vec* s
                                 const svdw_vec* x, const svdw_div_scale* cfg, svdw_vec* out);
 /* ZkVector::_norm_square (src/matrix/mod.rs:112-119) = inner_product(self, self);
  * ZkVector::_dist_square (src/matrix/mod.rs:135-148): per-entry qsub (gate.sub)
- * then _norm_square of the differences. norm / dist add qsqrt, whose chip
- * (zk_fixed_point_chip, git HEAD) is not available: not provided. */
+ * then _norm_square of the differences. */
 int svdw_zkvector_norm_square(svdw_ctx* ctx, uint32_t phase, const svdw_vec* self,
                               const svdw_div_scale* cfg, svdw_vec* out);
 int svdw_zkvector_dist_square(svdw_ctx* ctx, uint32_t phase, const svdw_vec* self,
                               const svdw_vec* x, const svdw_div_scale* cfg, svdw_vec* out);
+/* ZkVector::norm / dist (src/matrix/mod.rs:124-131, 156-164): _norm_square /
+ * _dist_square then FixedPointChip041::qsqrt. The chip (zk_fixed_point_chip,
+ * git HEAD) is not available, so qsqrt is a parameterised, constraint-checked
+ * construction, PARITY UNPINNED: y = floor(sqrt(a 2^P)) for a in [0, 2^B)
+ * (B = sqrt_bits, 0 -> 2P): load_witness(y), range_check(y, ny), t = mul(a, 2^P),
+ * d = sub(t, mul(y, y)), range_check(d, ny + 1), f = sub(mul(y, 2), d),
+ * range_check(f, ny + 1), ny = ceil((B + P) / 2) + 1; out = the y cell. */
+int svdw_zkvector_norm(svdw_ctx* ctx, uint32_t phase, const svdw_vec* self, const svdw_div_scale* cfg,
+                       uint32_t sqrt_bits, svdw_vec* out);
+int svdw_zkvector_dist(svdw_ctx* ctx, uint32_t phase, const svdw_vec* self, const svdw_vec* x,
+                       const svdw_div_scale* cfg, uint32_t sqrt_bits, svdw_vec* out);
 /* ZkVector::mul (src/matrix/mod.rs:169-182): inner_product with every row of a. */
 int svdw_zkvector_mul(svdw_ctx* ctx, uint32_t phase, const svdw_vec* self, const svdw_mat* a,
                       const svdw_div_scale* cfg, svdw_vec* out);

@@ -368,10 +368,12 @@ def verify_mul(ctx, a, b, c_s, init_rand: AV) -> None:
 # ---------------------------------------------------------------------------
 def div_scale_defaults(p: int, shift_bits: int = 0, num_bits: int = 0):
     """Default constants: the input domain |x| < 2^(3P) that rescale_matrix's
-    doc comment states (src/matrix/mod.rs:350-353): shift 2^(3P), div_mod on
-    3P+1 bits."""
+    doc comment states (src/matrix/mod.rs:350-353): shift 2^(3P); div_mod on
+    4P+1 bits, the width that reproduces the reference's own counts (90 cells
+    per element at P=32, LB=12: src/matrix/mod.rs:102 "#CONSTRAINTS = 90",
+    :348 "~94"; README.md:51 60-100 N^2; include/svdw.h svdw_div_scale)."""
     s = shift_bits or 3 * p
-    nb = num_bits or s + 1
+    nb = num_bits or 4 * p + 1
     assert p <= s < 254 and s < nb <= 253 and nb - p <= 200
     return s, nb
 
@@ -419,6 +421,35 @@ def zkvector_inner_product(ctx, rc, vec, x, p: int, shift_bits: int = 0, num_bit
 def zkvector_norm_square(ctx, rc, vec, p: int, shift_bits: int = 0, num_bits: int = 0) -> AV:
     """ZkVector::_norm_square (src/matrix/mod.rs:112-119): self.inner_product(self)."""
     return zkvector_inner_product(ctx, rc, vec, vec, p, shift_bits, num_bits)
+
+
+def qsqrt(ctx, rc: RangeChip, a: AV, p: int, sqrt_bits: int = 0) -> AV:
+    """FixedPointChip041::qsqrt [ext, PARITY UNPINNED: the chip's source is not
+    available offline] as the engine's parameterised construction (include/svdw.h
+    svdw_zkvector_norm): y = floor(sqrt(a 2^P)) for a in [0, 2^B), B = sqrt_bits
+    or 2P; y^2 <= a 2^P < (y + 1)^2 enforced by two range-checked differences."""
+    nb = sqrt_bits or 2 * p
+    ny = (nb + p + 1) // 2 + 1
+    y = load_witness(ctx, math.isqrt(a.value * (1 << p)))
+    rc.range_check(ctx, y, ny)
+    t = gate_mul(ctx, E(a), C(1 << p))
+    y2 = gate_mul(ctx, E(y), E(y))
+    d = gate_sub(ctx, E(t), E(y2))
+    rc.range_check(ctx, d, ny + 1)
+    e = gate_mul(ctx, E(y), C(2))
+    f = gate_sub(ctx, E(e), E(d))
+    rc.range_check(ctx, f, ny + 1)
+    return y
+
+
+def zkvector_norm(ctx, rc, vec, p: int, shift_bits: int = 0, num_bits: int = 0, sqrt_bits: int = 0) -> AV:
+    """ZkVector::norm (src/matrix/mod.rs:124-131): qsqrt(_norm_square)."""
+    return qsqrt(ctx, rc, zkvector_norm_square(ctx, rc, vec, p, shift_bits, num_bits), p, sqrt_bits)
+
+
+def zkvector_dist(ctx, rc, vec, x, p: int, shift_bits: int = 0, num_bits: int = 0, sqrt_bits: int = 0) -> AV:
+    """ZkVector::dist (src/matrix/mod.rs:156-164): qsqrt(_dist_square(x))."""
+    return qsqrt(ctx, rc, zkvector_dist_square(ctx, rc, vec, x, p, shift_bits, num_bits), p, sqrt_bits)
 
 
 def zkvector_dist_square(ctx, rc, vec, x, p: int, shift_bits: int = 0, num_bits: int = 0) -> AV:

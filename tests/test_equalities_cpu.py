@@ -93,12 +93,16 @@ def test_rescale_and_inner_product_equalities(P, LB):
     hs.ZkMatrix.rescale_matrix(ctx, cs)
     zx, zy = hs.ZkVector.new(ctx, x), hs.ZkVector.new(ctx, y)
     zx.inner_product(zy)
+    zx.norm()
+    zx.dist(zy)
     o0 = po.Context(phase=0)
     rc = po.RangeChip(LB)
     oa, ob = po.zkmatrix_new(o0, P, A.tolist()), po.zkmatrix_new(o0, P, B.tolist())
     po.rescale_matrix(o0, rc, po.honest_prover_mat_mul(o0, oa, ob), P)
     ox, oy = po.zkvector_new(o0, P, x.tolist()), po.zkvector_new(o0, P, y.tolist())
     po.zkvector_inner_product(o0, rc, ox, oy, P)         # zx.inner_product(zy): self = x
+    po.zkvector_norm(o0, rc, ox, P)
+    po.zkvector_dist(o0, rc, ox, oy, P)
 
     class W:
         ctx0, ctx1 = o0, None

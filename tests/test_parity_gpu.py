@@ -286,7 +286,8 @@ def _ints(cells):
 
 @pytest.mark.parametrize("P,LB,S,NB,elems", [(32, 12, 0, 0, 256), (32, 19, 0, 0, 256), (63, 19, 0, 0, 256),
                                             (42, 16, 100, 110, 256), (40, 19, 120, 0, 256),
-                                            (32, 12, 0, 0, 64), (63, 19, 0, 0, 128)])
+                                            (32, 12, 0, 0, 64), (63, 19, 0, 0, 128), (63, 12, 0, 0, 64),
+                                            (32, 12, 96, 97, 64)])
 def test_rescale_and_inner_product_parity(gpu_ctx_factory, P, LB, S, NB, elems):
     """rescale_matrix / ZkVector::inner_product / ZkVector::mul through the ABI vs
     the oracle's parameterised signed_div_scale (chip layout parity unpinned:
@@ -464,11 +465,12 @@ def _zkvector_inputs(N, M):
 @pytest.mark.parametrize("N,M,P,LB", [(5, 4, 32, 12), (5, 64, 32, 19)])
 def test_zkvector_parity(gpu_ctx_factory, N, M, P, LB):
     """BASELINE config 1 (test_zkvector, src/matrix/test_matrix.rs:39-198, with a
-    64-entry variant): inner_product, _norm_square, _dist_square and mul through
-    the ABI on the reference's inputs; every advice / lookup cell equals the
-    oracle's, its constraint checker passes, and the dequantised results are
-    within fixed-point error of the f64 values the reference prints (norm and
-    dist add qsqrt, not provided: chip source unavailable)."""
+    64-entry variant): inner_product, _norm_square, _dist_square, norm, dist and
+    mul through the ABI on the reference's inputs; every advice / lookup cell
+    equals the oracle's, its constraint checker passes, and the dequantised
+    results are within fixed-point error of the f64 values the reference prints
+    (norm / dist: qsqrt is the parameterised construction of include/svdw.h,
+    parity unpinned -- the chip's source is unavailable)."""
     import halo2_svd041_amd as hs
     import pyoracle as po
     A, v1, v2 = _zkvector_inputs(N, M)
@@ -479,6 +481,7 @@ def test_zkvector_parity(gpu_ctx_factory, N, M, P, LB):
     ns1, ns2 = z1._norm_square(), z2._norm_square()
     ds = z1._dist_square(z2)
     u1, u2 = z1.mul(za), z2.mul(za)
+    n1, n2, dd = z1.norm(), z2.norm(), z1.dist(z2)
     o = po.Context(phase=0)
     rc = po.RangeChip(LB)
     oa = po.zkmatrix_new(o, P, A)
@@ -487,13 +490,17 @@ def test_zkvector_parity(gpu_ctx_factory, N, M, P, LB):
     ons1, ons2 = po.zkvector_norm_square(o, rc, o1, P), po.zkvector_norm_square(o, rc, o2, P)
     ods = po.zkvector_dist_square(o, rc, o1, o2, P)
     ou1, ou2 = po.zkvector_mul(o, rc, o1, oa, P), po.zkvector_mul(o, rc, o2, oa, P)
+    on1, on2 = po.zkvector_norm(o, rc, o1, P), po.zkvector_norm(o, rc, o2, P)
+    odd = po.zkvector_dist(o, rc, o1, o2, P)
     assert po.check_constraints(o, LB) == []
     assert _ints(ctx.advice(0)) == o.advice
     assert _ints(ctx.lookups(0)) == o.lookups
     deq = lambda x: po.to_signed(x) / 2.0 ** P   # noqa: E731
     for got, want, f64 in ((ip, oip, sum(a * b for a, b in zip(v1, v2))),
                            (ns1, ons1, sum(a * a for a in v1)), (ns2, ons2, sum(b * b for b in v2)),
-                           (ds, ods, sum((a - b) ** 2 for a, b in zip(v1, v2)))):
+                           (ds, ods, sum((a - b) ** 2 for a, b in zip(v1, v2))),
+                           (n1, on1, sum(a * a for a in v1) ** 0.5), (n2, on2, sum(b * b for b in v2) ** 0.5),
+                           (dd, odd, sum((a - b) ** 2 for a, b in zip(v1, v2)) ** 0.5)):
         assert _ints(got.values()) == [want.value]
         assert abs(deq(want.value) - f64) <= 1e-6 * max(1.0, abs(f64))
     for got, want, vec in ((u1, ou1, v1), (u2, ou2, v2)):
