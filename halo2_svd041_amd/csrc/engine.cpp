@@ -450,6 +450,10 @@ struct svdw_ctx {
     int prelaunch_at = 0;                   // "prelaunch_at": GEMMs queued before stage 0/1/2
     int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
+    int gemm_kc = 4;                        // "gemm_kc": 64-k chunks per LDS round of the CRT GEMM (1 / 4)
+    bool gemm_batched = false;              // this witness's products went out as one batch
+    int gemm_batch = -1;                    // "gemm_batch": svd_witness's three products in one launch
+                                            // (1), one by one (0), or -1: batched on row-sharded ranks
     bool fused_quantize = true;             // "fused_quantize": m, u, v, d in one launch
     bool res_f64 = true;                    // "res_f64": CRT residue planes of m, u, v from the
                                             // f64 inputs, one launch (else from the cells)
@@ -512,8 +516,24 @@ struct svdw_ctx {
     std::vector<uint64_t>* gemm_log = nullptr;   // dry run: offsets of honest_prover_mat_mul
     std::vector<hipEvent_t> deps;           // dependency events (no timing)
     size_t dep_next = 0;
+    // Stage batches (BatchScope, "stage_batch"): stage launches on a stream with
+    // an open batch are collected and issued as k_stage_multi launches when the
+    // scope closes, when a stage reads cells a pending stage writes, or before
+    // anything else is recorded or launched on that stream.
+    struct Pending {
+        StageArgs a;
+        std::string name;
+        double bytes;
+    };
+    struct Batch {
+        hipStream_t st;
+        std::vector<Pending> progs;
+    };
+    std::vector<Batch> batches;
+    bool stage_batch = true;
 };
 
+static void flush_batch(svdw_ctx* c, hipStream_t s);
 static void sync(svdw_ctx* c) {
     if (c->dry) return;
     hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
@@ -530,6 +550,7 @@ static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
         c->deps.push_back(e);
     }
     hipEvent_t e = c->deps[c->dep_next++];
+    flush_batch(c, from);
     hipck(hipEventRecord(e, from), "hipEventRecord");
     if (to) hipck(hipStreamWaitEvent(to, e, 0), "hipStreamWaitEvent");
     return e;
@@ -612,8 +633,10 @@ struct ProfScope {
         return e;
     }
     hipStream_t s = nullptr;
-    ProfScope(svdw_ctx* cc, hipStream_t ss, const std::string& name, double bytes, double ops)
+    ProfScope(svdw_ctx* cc, hipStream_t ss, const std::string& name, double bytes, double ops,
+              bool batch = false)
         : c(cc), s(ss) {
+        if (!batch) flush_batch(c, s);      // earlier batched stages go first
         if (!c->prof || c->dry) return;
         if (!c->prof_filter.empty() && name.compare(0, c->prof_filter.size(), c->prof_filter) != 0)
             return;
@@ -779,12 +802,79 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     a.ldiv_magic = magic(a.L);
     uint32_t loads = 0;
     for (uint32_t i = 0; i < a.nmo; ++i) loads += a.mo[i].op == MO_LOAD;
+    const double bytes = 32.0 * (ee - eb) * ((double)a.C + a.L + loads);
+    for (auto& b : c->batches) {
+        if (b.st != c->st || !stage_multi_fits(a)) continue;
+        // a stage reading cells that a pending stage writes starts a new launch
+        bool dep = false;
+        for (const auto& q : b.progs) {
+            const char* w0 = reinterpret_cast<const char*>(q.a.out_adv);
+            const char* w1 = w0 + sizeof(Fr) * (uint64_t)q.a.e_end * q.a.C;
+            for (int k = 0; k < kMaxViews; ++k) {
+                const DView& v = a.view[k];
+                if (!v.ptr || v.mode == VIEW_DIAGK) continue;
+                // the view's cells lie within [lo, hi) of ptr (signed strides, in cells)
+                const int64_t dr = (int64_t)(v.rows ? v.rows - 1 : 0) * v.rs,
+                              dc = (int64_t)(v.cols ? v.cols - 1 : 0) * v.cs;
+                const int64_t lo = std::min<int64_t>(dr, 0) + std::min<int64_t>(dc, 0),
+                              hi = std::max<int64_t>(dr, 0) + std::max<int64_t>(dc, 0) + 1;
+                const char* p = reinterpret_cast<const char*>(v.ptr);
+                if (p + lo * (int64_t)sizeof(Fr) < w1 && p + hi * (int64_t)sizeof(Fr) > w0) dep = true;
+            }
+        }
+        if (dep) flush_batch(c, c->st);
+        b.progs.push_back({a, std::string("k_stage:") + tag, bytes});
+        return;
+    }
     {
-        ProfScope ps(c, c->st, std::string("k_stage:") + tag,
-                     32.0 * (ee - eb) * ((double)a.C + a.L + loads), 0);
+        ProfScope ps(c, c->st, std::string("k_stage:") + tag, bytes, 0);
         hipck(launch_stage(a, c->st), "k_stage");
     }
 }
+// Issue a stream's pending batched stages (k_stage_multi; one program: k_stage).
+static void flush_batch(svdw_ctx* c, hipStream_t s) {
+    for (auto& b : c->batches) {
+        if (b.st != s || b.progs.empty()) continue;
+        std::vector<const StageArgs*> ps;
+        double bytes = 0;
+        for (const auto& q : b.progs) {
+            ps.push_back(&q.a);
+            bytes += q.bytes;
+        }
+        const std::string name = b.progs.size() == 1 ? b.progs[0].name : "k_stage:multi";
+        std::vector<svdw_ctx::Pending> progs;
+        progs.swap(b.progs);                 // (cleared before launching: no re-entry)
+        ProfScope pr(c, s, name, bytes, 0, true);
+        hipck(launch_stage_multi(ps.data(), (int)ps.size(), s), "k_stage_multi");
+    }
+}
+// RAII: stage launches on the current stream between construction and end()
+// are batched (k_stage_multi); nested scopes on the same stream join the outer
+// one. Without end() (an exception) the pending stages are dropped.
+struct BatchScope {
+    svdw_ctx* c;
+    hipStream_t st = nullptr;
+    bool mine = false;
+    explicit BatchScope(svdw_ctx* cc) : c(cc) {
+        if (c->dry || !c->stage_batch) return;
+        for (auto& b : c->batches)
+            if (b.st == c->st) return;
+        st = c->st;
+        c->batches.push_back({st, {}});
+        mine = true;
+    }
+    void end() {
+        if (!mine) return;
+        flush_batch(c, st);
+        close();
+    }
+    void close() {
+        for (size_t i = 0; i < c->batches.size(); ++i)
+            if (c->batches[i].st == st) { c->batches.erase(c->batches.begin() + i); break; }
+        mine = false;
+    }
+    ~BatchScope() { if (mine) close(); }
+};
 // shard ownership of a stage's cells: this rank's rows (single cells: the last rank)
 static void stage_own(svdw_ctx* c, uint32_t phase, const PB& pb, uint32_t nelem, uint32_t cols,
                       uint64_t off, uint64_t loff) {
@@ -1229,7 +1319,7 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
             ProfScope ps(c, s, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * N * M,
                          (double)N * M * K);
             hipck(launch_gemm_crt(sym, Ar, Br, N, M, rpa, sym ? rpa : rpb,
-                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s),
+                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s, c->gemm_kc),
                   "k_gemm_crt");
         }
         if (!quantized)
@@ -1664,20 +1754,24 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     ensure_gamma_vec(c, dmax, gamma);
     const Fr* gpc = (const Fr*)c->gpc.p;
     const Fr* gtab = (const Fr*)c->gtab.p;
-    for (int i = 0; i < n; ++i) {
-        Plan& p = pl[i];
-        const uint32_t d = vm[i].cs.cols;
-        stage_launch(c, phase, p.one, 1, 1, p.one_off, p.one_loff, "load_cell");
-        if (d > 1) {
-            DView w;
-            memset(&w, 0, sizeof w);
-            w.ptr = gpc;
-            w.rs = 1; w.cs = 0; w.rows = d; w.cols = 1;
-            p.pows.a.view[0] = w;
-            p.pows.a.view[1] = w;
-            p.pows.a.view[1].ptr = gpc + 1;
-            stage_launch(c, phase, p.pows, d - 1, 1, p.pows_off, p.pows_loff, "verify_mul_gamma_pows");
+    {
+        BatchScope bs(c);                                 // the one cells and gamma powers: one launch
+        for (int i = 0; i < n; ++i) {
+            Plan& p = pl[i];
+            const uint32_t d = vm[i].cs.cols;
+            stage_launch(c, phase, p.one, 1, 1, p.one_off, p.one_loff, "load_cell");
+            if (d > 1) {
+                DView w;
+                memset(&w, 0, sizeof w);
+                w.ptr = gpc;
+                w.rs = 1; w.cs = 0; w.rows = d; w.cols = 1;
+                p.pows.a.view[0] = w;
+                p.pows.a.view[1] = w;
+                p.pows.a.view[1].ptr = gpc + 1;
+                stage_launch(c, phase, p.pows, d - 1, 1, p.pows_off, p.pows_loff, "verify_mul_gamma_pows");
+            }
         }
+        bs.end();
     }
     const int T = c->scan_impl == 5 ? 4 : c->scan_impl == 3 ? 1 : 2;
     // operand widths per batch: host-known, or read on the device (na 0)
@@ -1762,6 +1856,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     for (hipEvent_t ev : c->wait_before_cs)
         hipck(hipStreamWaitEvent(c->st, ev, 0), "hipStreamWaitEvent");
     run_batch("k_matvec_scan:cs", cs_of, [&](int i) { return pl[i].csv; }, gc, gt, gl, na_cs);
+    BatchScope bs(c);                                     // the is_equal rows: one launch
     for (int i = 0; i < n; ++i) {
         Plan& p = pl[i];
         p.eq.a.view[0] = view_of(c, mat_of_vec(p.csv));
@@ -1769,6 +1864,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         note_gates(c, p.eq, 1, p.eq_reg);
         stage_launch(c, phase, p.eq, vm[i].a.rows, 1, p.eq_off, p.eq_loff, "verify_mul_is_equal");
     }
+    bs.end();
 }
 static void verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svdw_mat& b,
                        const svdw_mat& cs, const Fr& gamma) {
@@ -1847,6 +1943,57 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
                            (const uint8_t*)c->digB.p};                 // A planes of m, u, v
     const uint32_t stride[3] = {rp_m, rp_u, rp_v}, kp[3] = {kpM, kpN, kpM}, lk[3] = {lkM, lkN, lkM};
     const int wa[3] = {0, 1, 2}, wb[3] = {2, 1, 2};
+    if (c->gemm_batch > 0 || (c->gemm_batch < 0 && sharded(c))) {
+        // the three products in one GEMM launch and one combine launch (each its
+        // own residue scratch): one step of the st2 chain instead of three
+        CrtBatch b;
+        memset(&b, 0, sizeof b);
+        b.kc = c->gemm_kc;
+        size_t rbytes[3], rtot = 0;
+        for (int g = 0; g < 3; ++g) {
+            rbytes[g] = (size_t)kCrtMaxResidues * ceil_to(std::max<uint32_t>((uint32_t)(rr1[g] - rr0[g]), 1), 128) *
+                        ceil_to(B[g].cols, 128);
+            rtot += rbytes[g];
+        }
+        ensure_buf(c, c->crtR, rtot);
+        size_t roff = 0;
+        double bytes = 0, ops = 0;
+        for (int g = 0; g < 3; ++g) {
+            const uint32_t rows = (uint32_t)(rr1[g] - rr0[g]), cols = B[g].cols;
+            if (rows) {
+                const bool sym = !sharded(c) && g > 0;
+                CrtJob& q = b.job[b.njobs++];
+                q.Ar = P[g] + (g == 0 ? 0 : rr0[g] * (uint64_t)kp[g]);
+                q.Br = g == 0 ? (const uint8_t*)c->digB.p : P[g];
+                q.R = (uint8_t*)c->crtR.p + roff;
+                q.out = cellp(c, phase, log[g] + rr0[g] * cols);
+                q.bits_a = W + wa[g];
+                q.bits_b = W + wb[g];
+                q.ors = cols;
+                q.ocs = 1;
+                q.astride = stride[g];
+                q.bstride = g == 0 ? rp_v : stride[g];
+                q.kpad = kp[g];
+                q.N = rows;
+                q.M = cols;
+                q.lk = lk[g];
+                q.sym = sym;
+                bytes += 32.0 * rows * cols;
+                ops += (double)rows * cols * A[g].cols;
+            }
+            roff += rbytes[g];
+        }
+        c->gemm_batched = true;
+        if (b.njobs) {
+            ProfScope ps(c, c->st2, "k_gemm_crt:multi", bytes, ops);
+            hipck(launch_gemm_crt_multi(b, c->st2), "k_gemm_crt_multi");
+        }
+        for (int g = 0; g < 3; ++g) {
+            c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
+            c->gemm_done.push_back(c->pre.back().ev);
+        }
+        return;
+    }
     for (int g = 0; g < 3; ++g) {
         const uint32_t rows = (uint32_t)(rr1[g] - rr0[g]), cols = B[g].cols;
         Fr* out = cellp(c, phase, log[g] + rr0[g] * cols);
@@ -1859,7 +2006,7 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
             ProfScope ps(c, c->st2, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * rows * cols,
                          (double)rows * cols * A[g].cols);
             hipck(launch_gemm_crt(sym, Ap, Bp, rows, cols, stride[g], bs, kp[g], (uint8_t*)c->crtR.p,
-                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], c->st2),
+                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], c->st2, c->gemm_kc),
                   "k_gemm_crt");
         }
         c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
@@ -1974,8 +2121,10 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
             ~Swap() { if (on) std::swap(c->st, c->st2); }
         } sw(c, c->d_checks_aside && c->overlap && known_bits && !c->dry && c->bits_pending);
         if (sw.on) hipck(hipStreamWaitEvent(c->st, c->ev_bits, 0), "hipStreamWaitEvent");  // d loaded
+        BatchScope bs(c);                   // (desc_order_range reads desc_order_sub: two launches)
         entries_less_than(c, d, max_bits);
         entries_in_desc_order(c, d, max_bits);
+        bs.end();
         host_mark(c, "d checks queued");
     }
     if (c->prelaunch_at == 1) prelaunch();
@@ -1998,14 +2147,18 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         f(pl);
     };
     early_phase1(0);
+    // The u, v bounds and u.d read only the loaded matrices: one launch when
+    // batched (stage_batch), after which phase 1 is queued (p1_at 1 or 2).
+    BatchScope bs(c);
+    const bool batched = bs.mine;
     BigU unit = big_from_u128(((unsigned __int128)1 << P) + 1);
     check_mat_entries_bounded(c, u, unit);
     host_mark(c, "bounds(u) queued");
-    early_phase1(1);
+    if (!batched) early_phase1(1);
     if (c->prelaunch_at == 2) prelaunch();
     check_mat_entries_bounded(c, v, unit);
     host_mark(c, "bounds(v) queued");
-    early_phase1(2);
+    if (!batched) early_phase1(2);
     svdw_mat ut = u, vt = v;
     std::swap(ut.rows, ut.cols); std::swap(ut.rs, ut.cs);
     std::swap(vt.rows, vt.cols); std::swap(vt.rs, vt.cs);
@@ -2021,11 +2174,20 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         udv.cols = r;                                     // columns >= N read as 0
     }
     udv.rows = N;
+    bs.end();
+    if (batched) {
+        host_mark(c, "bounds(u), bounds(v), u.d queued");
+        early_phase1(1);
+        early_phase1(2);
+    }
     uint32_t bm = ~0u, bu = ~0u, bv = ~0u;
     if (known_bits && c->pre.empty()) {                  // products not launched ahead
         fetch_bits(c);
         bm = known_bits[0]; bu = known_bits[1]; bv = known_bits[2];
     }
+    // products batched (one completion point): diff and the two ids in one launch
+    BatchScope bs2(c);
+    if (!c->gemm_batched) bs2.close();
     svdw_mat mvt = honest_prover_mat_mul(c, m.phase, m, vt, bm, bv);
     BigU es = scale_err(err_svd, P), eu = scale_err(err_u, P);
     host_mark(c, "u.d queued");
@@ -2038,6 +2200,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     check_mat_id(c, uut, q2, eu, &qq);
     svdw_mat vvt = honest_prover_mat_mul(c, m.phase, v, vt, bv, bv);
     check_mat_id(c, vvt, q2, eu, &qq);
+    bs2.end();
     host_mark(c, "ids queued");
     return svdw_svd_payload{ut, vt, mvt, uut, vvt};
 }
@@ -2065,6 +2228,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     clear_streams(c);
     c->dep_next = 0;
     c->prelaunched = false;
+    c->gemm_batched = false;
     c->gemm_done.clear();
     c->wait_before_cs.clear();
     c->pre.clear();
@@ -2141,6 +2305,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         seg.begin[2] = nbm + nbu;
         seg.begin[3] = nbm + nbu + nbv;
         hipck(launch_bits_reduce(dbits + 64, seg, 3, dbits, c->st), "k_bits_reduce");
+        flush_batch(c, c->st);
         hipck(hipEventRecord(c->ev_bits, c->st), "hipEventRecord");
         c->bits_pending = true;
         c->qmat[0] = zm; c->qmat[1] = zu; c->qmat[2] = zv;
@@ -2317,7 +2482,7 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipHostMalloc((void**)&c->hbits, 64 * sizeof(uint32_t),
                                                hipHostMallocDefault);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bits, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bits, hipEventDisableTiming | hipEventReleaseToDevice);
             if (e != hipSuccess) {
                 delete c;
                 fail(SVDW_EDEVICE, std::string("HIP device init failed: ") + hipGetErrorString(e));
@@ -3025,9 +3190,11 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "stage_align") {
             c->stage_flags = (c->stage_flags & ~STAGE_ALIGN) | (value ? STAGE_ALIGN : 0);
         } else if (n == "stage_probe") {             // timing probe, wrong cells (tools/ab.py)
-            REQUIRE(value >= 0 && value <= 2, "stage_probe: 0 off, 1 skip phase A, 2 constant stores");
-            c->stage_flags = (c->stage_flags & ~(STAGE_PROBE_NOA | STAGE_PROBE_CONST)) |
-                             (value == 1 ? STAGE_PROBE_NOA : value == 2 ? STAGE_PROBE_CONST : 0);
+            REQUIRE(value >= 0 && value <= 3,
+                    "stage_probe: 0 off, 1 skip phase A, 2 constant stores, 3 constant stores, no loads");
+            c->stage_flags = (c->stage_flags & ~(STAGE_PROBE_NOA | STAGE_PROBE_CONST | STAGE_PROBE_NOLD)) |
+                             (value == 1 ? STAGE_PROBE_NOA : value == 2 ? STAGE_PROBE_CONST
+                              : value == 3 ? (STAGE_PROBE_CONST | STAGE_PROBE_NOLD) : 0);
         } else if (n == "gemm_priority") {
             // second (GEMM) stream priority: 0 normal, 1 high
             REQUIRE(value == 0 || value == 1, "gemm_priority: 0 or 1");
@@ -3113,6 +3280,14 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "gemm_crt") {
             REQUIRE(value == 0 || value == 1, "gemm_crt: 0 or 1");
             c->gemm_crt = (int)value;
+        } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
+            c->stage_batch = value != 0;
+        } else if (n == "gemm_batch") {
+            REQUIRE(value >= -1 && value <= 1, "gemm_batch: -1 (auto), 0 or 1");
+            c->gemm_batch = (int)value;
+        } else if (n == "gemm_kc") {
+            REQUIRE(value == 1 || value == 4, "gemm_kc: 1 or 4");
+            c->gemm_kc = (int)value;
         } else if (n == "gemm_rt") {
             REQUIRE(value == 0 || value == 1, "gemm_rt: 0 or 1");
             c->gemm_rt = (int)value;

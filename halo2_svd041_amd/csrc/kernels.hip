@@ -11,6 +11,7 @@
 //  k_matvec_scan   field_mat_vec_mul rows (src/matrix/mod.rs:574-599): every
 //                  prefix sum of the row inner product is a cell -> block Fr scan
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <string.h>
 
 #include "kernels.hpp"
@@ -511,7 +512,14 @@ __device__ __forceinline__ void element_program(const StageArgs& a, uint32_t e, 
     }
     }
 
-__global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
+// One block of a stage: `a` supplies the scalar fields and the views (StageArgs
+// up to `mo`), the tables come from mo / adv / lk / K (the by-value kernel
+// argument of k_stage, or a record of a k_stage_multi batch); blk is the
+// block's index within the stage.
+__device__ __forceinline__ void stage_block(const StageArgs& a, const MicroOp* __restrict__ mo,
+                                            const SlotOp* __restrict__ adv,
+                                            const SlotOp* __restrict__ lk, const Fr* __restrict__ K,
+                                            uint32_t blk) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t nv = a.nv;
     uint32_t* sK = smem;
@@ -530,14 +538,14 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     uint32_t* sHD = reinterpret_cast<uint32_t*>(sHM + 2 * (a.C + a.L));
 
     const uint32_t tid = threadIdx.x;
-    const uint32_t e0 = a.e_begin + blockIdx.x * E;
+    const uint32_t e0 = a.e_begin + blk * E;
     const uint32_t ne = min(E, a.e_end - e0), e = e0 + tid;
 
     // Issue this thread's in-bounds strided view loads before the LDS set-up,
     // so their latency overlaps it (phase A falls back to view_load otherwise).
     Fr pf0 = fr_zero(), pf1 = fr_zero();
     bool in0 = false, in1 = false;
-    if (tid < ne) {
+    if (tid < ne && !(a.flags & STAGE_PROBE_NOLD)) {
         const uint32_t pi = e / a.cols, pj = e - pi * a.cols;
         const DView& v0 = a.view[0];
         if (v0.ptr && v0.mode == VIEW_STRIDED && pi < v0.rows && pj < v0.cols) {
@@ -551,14 +559,14 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
         }
     }
 
-    for (uint32_t k = tid; k < a.nk; k += blockDim.x) lds_put(sK + k * VW, a.K[k]);
-    for (uint32_t k = tid; k < a.C; k += blockDim.x) sAdv[k] = a.adv[k];
-    for (uint32_t k = tid; k < a.L; k += blockDim.x) sLk[k] = a.lk[k];
-    for (uint32_t k = tid; k < a.nmo; k += blockDim.x) sMo[k] = a.mo[k];
+    for (uint32_t k = tid; k < a.nk; k += blockDim.x) lds_put(sK + k * VW, K[k]);
+    for (uint32_t k = tid; k < a.C; k += blockDim.x) sAdv[k] = adv[k];
+    for (uint32_t k = tid; k < a.L; k += blockDim.x) sLk[k] = lk[k];
+    for (uint32_t k = tid; k < a.nmo; k += blockDim.x) sMo[k] = mo[k];
     if (tid < kMaxViews) sVw[tid] = a.view[tid];
     for (uint32_t k = tid; k < 2 * (a.C + a.L); k += blockDim.x) {
         const uint32_t sl = k >> 1;
-        make_half(sl < a.C ? a.adv[sl] : a.lk[sl - a.C], k & 1, sHD + k, sHM + k);
+        make_half(sl < a.C ? adv[sl] : lk[sl - a.C], k & 1, sHD + k, sHM + k);
     }
     __syncthreads();
 
@@ -595,6 +603,27 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     }
 }
 
+__global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
+    stage_block(a, a.mo, a.adv, a.lk, a.K, blockIdx.x);
+}
+
+// Several independent stages in one launch (k_stage_multi): block b runs block
+// b - blk0[p] of program p, whose compact record (stage_record, prog.hpp) is at
+// data + off[p] -- so the small stages of a witness (single cells, d checks,
+// gamma powers, is_equal rows, ...) and the phase-0 stages that read only the
+// loaded matrices share one launch (one tail, one dispatch).
+__global__ __launch_bounds__(256) void k_stage_multi(const StageMulti m) {
+    uint32_t p = 0;
+    for (uint32_t k = 1; k < m.nprog; ++k) p += blockIdx.x >= m.blk0[k];
+    const uint8_t* r = m.data + m.off[p];
+    const StageArgs& a = *reinterpret_cast<const StageArgs*>(r);      // fields up to `mo` only
+    const MicroOp* mo = reinterpret_cast<const MicroOp*>(r + kRecHead);
+    const SlotOp* adv = reinterpret_cast<const SlotOp*>(mo + a.nmo);
+    const SlotOp* lk = adv + a.C;
+    const Fr* K = reinterpret_cast<const Fr*>(lk + a.L);
+    stage_block(a, mo, adv, lk, K, blockIdx.x - m.blk0[p]);
+}
+
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     if (a.e_end <= a.e_begin) return hipSuccess;
     const uint32_t n = a.e_end - a.e_begin;
@@ -604,6 +633,59 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     const uint32_t grid = (n + E - 1) / E;
     hipLaunchKernelGGL(k_stage, dim3(grid), dim3(256), lds, st, a);
     return hipGetLastError();
+}
+bool stage_multi_fits(const StageArgs& a) {
+    return stage_record_bytes(a.nmo, a.C, a.L, a.nk) <= kMultiBytes && (a.E ? a.E : kStageElems) <= kStageElems;
+}
+hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st) {
+    StageMulti m;
+    uint32_t used = 0, blocks = 0, lds = 0;
+    m.nprog = 0;
+    const StageArgs* single = nullptr;
+    // launch what is packed (a single program as a plain k_stage launch)
+    auto flush = [&]() -> hipError_t {
+        hipError_t e = hipSuccess;
+        if (m.nprog == 1) {
+            e = launch_stage(*single, st);
+        } else if (m.nprog > 1) {
+            m.blk0[m.nprog] = blocks;
+            hipLaunchKernelGGL(k_stage_multi, dim3(blocks), dim3(256), lds, st, m);
+            e = hipGetLastError();
+        }
+        m.nprog = 0;
+        used = blocks = lds = 0;
+        return e;
+    };
+    for (int i = 0; i < n; ++i) {
+        const StageArgs& a = *progs[i];
+        if (a.e_end <= a.e_begin) continue;
+        const uint32_t E = a.E ? a.E : kStageElems;
+        if (E > kStageElems) return hipErrorInvalidValue;
+        const uint32_t rb = stage_record_bytes(a.nmo, a.C, a.L, a.nk);
+        if (rb > kMultiBytes) return hipErrorInvalidValue;
+        if (m.nprog == (uint32_t)kMaxMulti || used + rb > kMultiBytes) {
+            const hipError_t e = flush();
+            if (e != hipSuccess) return e;
+        }
+        uint8_t* r = m.data + used;
+        memcpy(r, &a, kRecHead);
+        uint8_t* q = r + kRecHead;
+        memcpy(q, a.mo, 8 * a.nmo);
+        q += 8 * a.nmo;
+        memcpy(q, a.adv, 4 * a.C);
+        q += 4 * a.C;
+        memcpy(q, a.lk, 4 * a.L);
+        q += 4 * a.L;
+        memcpy(q, a.K, 32 * a.nk);
+        m.off[m.nprog] = used;
+        m.blk0[m.nprog] = blocks;
+        ++m.nprog;
+        if (m.nprog == 1) single = &a;
+        used += rb;
+        blocks += (a.e_end - a.e_begin + E - 1) / E;
+        lds = lds > stage_lds_bytes(a.nv ? a.nv : 1, E, a.C + a.L) ? lds : stage_lds_bytes(a.nv ? a.nv : 1, E, a.C + a.L);
+    }
+    return flush();
 }
 
 // ----------------------------------------------------------------- maxbits
@@ -1269,6 +1351,18 @@ hipError_t launch_residues_f64(const ResSegs& q0, const unsigned* W, int precisi
     return hipGetLastError();
 }
 
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>): an unrolled
+// loop whose index is a compile-time constant in the body
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for_impl(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for_impl<I + 1, N>(f);
+    }
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) { static_for_impl<0, N>(f); }
+
 static constexpr int CT = 128;     // CRT GEMM block tile (4 waves of 64 x 64)
 // Staged operand rows are 64 B (one k-chunk) with the four 16 B parts XOR-swizzled
 // by (row >> 2) & 3: the staging stores (4 rows x 4 parts per 16 lanes) and the
@@ -1284,38 +1378,43 @@ __device__ __forceinline__ uint32_t crt_lds(uint32_t row, uint32_t part) {
 // Ar / Br: planes of astride / bstride rows (a row block of a larger operand is
 // its planes from row r0 on with the full operand's stride); R is
 // [mod][tiles_a * CT][tiles_m * CT].
-template <bool SYM>
-__global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar,
-                                                  const uint8_t* __restrict__ Br, uint32_t astride,
-                                                  uint32_t bstride, uint32_t kpad, uint32_t tiles_a,
-                                                  uint32_t tiles_m, uint8_t* __restrict__ R,
-                                                  const unsigned* __restrict__ bits_a,
-                                                  const unsigned* __restrict__ bits_b, uint32_t lk) {
+// KC 64-k chunks are staged per LDS round (KC = 4: 64 KiB of LDS, 16 loads of
+// 16 B in flight per thread): the K loop is bound by the global-load latency
+// per round, so K = 1024 takes 4 rounds instead of 16.
+// (block function: blk / nblk = the block's index and the block count of this
+// product's grid, mod = its modulus; the kernels below map their grids onto it)
+template <bool SYM, int KC>
+__device__ __forceinline__ void crt_gemm_block(const uint8_t* __restrict__ Ar,
+                                               const uint8_t* __restrict__ Br, uint32_t astride,
+                                               uint32_t bstride, uint32_t kpad, uint32_t tiles_a,
+                                               uint32_t tiles_m, uint8_t* __restrict__ R,
+                                               const unsigned* __restrict__ bits_a,
+                                               const unsigned* __restrict__ bits_b, uint32_t lk,
+                                               uint32_t blk, uint32_t nblk, int mod) {
     const int n = crt_nmod(*bits_a, *bits_b, lk);
-    const int mod = blockIdx.y;
     if (mod >= n) return;
-    constexpr int kS = 2 * CT * CROW > CT * CTS ? 2 * CT * CROW : CT * CTS;
+    constexpr int kS = 2 * KC * CT * CROW > CT * CTS ? 2 * KC * CT * CROW : CT * CTS;
     __shared__ __attribute__((aligned(16))) uint8_t S[kS];
     uint8_t* As = S;
-    uint8_t* Bs = S + CT * CROW;
+    uint8_t* Bs = S + KC * CT * CROW;
     uint32_t bi, bj;
     if (SYM) {
-        uint32_t b = blockIdx.x, r = 0, rowlen = tiles_m;
+        uint32_t b = blk, r = 0, rowlen = tiles_m;
         while (b >= rowlen) { b -= rowlen; ++r; --rowlen; }
         bi = r; bj = r + b;
-    } else if ((gridDim.x & 7) == 0 && (gridDim.x / tiles_m) % 2 == 0) {
+    } else if ((nblk & 7) == 0 && (nblk / tiles_m) % 2 == 0) {
         // Blocks b and b + 8 share an XCD (and its L2): give each XCD a contiguous
         // run of the tiles in 2-row groups (a 2 x 4 block of tiles at 1024^2), so
         // an XCD reads 2 row tiles of A and 4 column tiles of B per modulus
         // instead of all 8 row tiles of A.
-        const uint32_t per = gridDim.x >> 3;
-        const uint32_t t = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+        const uint32_t per = nblk >> 3;
+        const uint32_t t = (blk & 7) * per + (blk >> 3);
         const uint32_t grp = t / (2 * tiles_m), w = t - grp * 2 * tiles_m;
         bi = grp * 2 + (w & 1);
         bj = w >> 1;
     } else {
-        bi = blockIdx.x / tiles_m;
-        bj = blockIdx.x % tiles_m;
+        bi = blk / tiles_m;
+        bj = blk % tiles_m;
     }
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t wr = wave >> 1, wc = wave & 1;
@@ -1323,43 +1422,71 @@ __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar
     const uint8_t* Bp = Br + ((uint64_t)mod * bstride + bj * CT) * kpad;
     // staging map: 512 x 16 B per operand chunk; thread -> (row, part) for q = tid, tid + 256
     const uint32_t r0 = tid >> 2, r1 = (tid + 256) >> 2, part = tid & 3;
-    uint4 ra0, ra1, rb0, rb1;
-    auto gload = [&](uint32_t kc) {
-        const uint64_t ko = (uint64_t)kc * 64 + part * 16;
-        ra0 = *reinterpret_cast<const uint4*>(Ap + (uint64_t)r0 * kpad + ko);
-        ra1 = *reinterpret_cast<const uint4*>(Ap + (uint64_t)r1 * kpad + ko);
-        rb0 = *reinterpret_cast<const uint4*>(Bp + (uint64_t)r0 * kpad + ko);
-        rb1 = *reinterpret_cast<const uint4*>(Bp + (uint64_t)r1 * kpad + ko);
-    };
+    const uint32_t kcn = kpad / 64, nst = (kcn + KC - 1) / KC;
     v4i acc[4][4];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[a][b] = v4i{0, 0, 0, 0};
-    const uint32_t kcn = kpad / 64;
     const uint32_t frow = lane & 15, fk = (lane >> 4) * 16;
-    gload(0);
-    for (uint32_t kc = 0; kc < kcn; ++kc) {
-        *reinterpret_cast<uint4*>(As + crt_lds(r0, part)) = ra0;
-        *reinterpret_cast<uint4*>(As + crt_lds(r1, part)) = ra1;
-        *reinterpret_cast<uint4*>(Bs + crt_lds(r0, part)) = rb0;
-        *reinterpret_cast<uint4*>(Bs + crt_lds(r1, part)) = rb1;
+    // Staging registers per chunk as named variables, loops spelled out by macro
+    // (arrays or lambdas over them ended up in scratch). Chunk indices past the
+    // end are clamped to the last chunk, so the loads stay unconditional; those
+    // chunks are never multiplied.
+#define CRT_GLOAD(g, chunk)                                                                   \
+    {                                                                                         \
+        const uint64_t ko = (uint64_t)min((uint32_t)(chunk), kcn - 1) * 64 + part * 16;     \
+        g##a0 = *reinterpret_cast<const uint4*>(Ap + (uint64_t)r0 * kpad + ko);             \
+        g##a1 = *reinterpret_cast<const uint4*>(Ap + (uint64_t)r1 * kpad + ko);             \
+        g##b0 = *reinterpret_cast<const uint4*>(Bp + (uint64_t)r0 * kpad + ko);             \
+        g##b1 = *reinterpret_cast<const uint4*>(Bp + (uint64_t)r1 * kpad + ko);             \
+    }
+#define CRT_LSTORE(g, c)                                                                      \
+    {                                                                                         \
+        uint8_t* Ac = As + (c) * CT * CROW;                                                   \
+        uint8_t* Bc = Bs + (c) * CT * CROW;                                                   \
+        *reinterpret_cast<uint4*>(Ac + crt_lds(r0, part)) = g##a0;                            \
+        *reinterpret_cast<uint4*>(Ac + crt_lds(r1, part)) = g##a1;                            \
+        *reinterpret_cast<uint4*>(Bc + crt_lds(r0, part)) = g##b0;                            \
+        *reinterpret_cast<uint4*>(Bc + crt_lds(r1, part)) = g##b1;                            \
+    }
+#define CRT_MMA(c)                                                                            \
+    {                                                                                         \
+        const uint8_t* Ac = As + (c) * CT * CROW;                                             \
+        const uint8_t* Bc = Bs + (c) * CT * CROW;                                             \
+        v4i af[4], bf[4];                                                                     \
+        _Pragma("unroll") for (int a = 0; a < 4; ++a)                                         \
+            af[a] = *reinterpret_cast<const v4i*>(Ac + crt_lds(wr * 64 + a * 16 + frow, fk >> 4)); \
+        _Pragma("unroll") for (int b = 0; b < 4; ++b)                                         \
+            bf[b] = *reinterpret_cast<const v4i*>(Bc + crt_lds(wc * 64 + b * 16 + frow, fk >> 4)); \
+        _Pragma("unroll") for (int a = 0; a < 4; ++a)                                         \
+            _Pragma("unroll") for (int b = 0; b < 4; ++b)                                     \
+                acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0); \
+    }
+    uint4 s0a0, s0a1, s0b0, s0b1, s1a0, s1a1, s1b0, s1b1;
+    uint4 s2a0, s2a1, s2b0, s2b1, s3a0, s3a1, s3b0, s3b1;
+    CRT_GLOAD(s0, 0);
+    if constexpr (KC == 4) { CRT_GLOAD(s1, 1); CRT_GLOAD(s2, 2); CRT_GLOAD(s3, 3); }
+    for (uint32_t st = 0; st < nst; ++st) {
+        const uint32_t c0 = st * KC;
+        CRT_LSTORE(s0, 0);
+        if constexpr (KC == 4) { CRT_LSTORE(s1, 1); CRT_LSTORE(s2, 2); CRT_LSTORE(s3, 3); }
         __syncthreads();
-        if (kc + 1 < kcn) gload(kc + 1);                      // next chunk in flight
-        v4i af[4], bf[4];
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-            af[a] = *reinterpret_cast<const v4i*>(As + crt_lds(wr * 64 + a * 16 + frow, fk >> 4));
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-            bf[b] = *reinterpret_cast<const v4i*>(Bs + crt_lds(wc * 64 + b * 16 + frow, fk >> 4));
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
+        if (st + 1 < nst) {                                   // next round in flight
+            CRT_GLOAD(s0, c0 + KC);
+            if constexpr (KC == 4) { CRT_GLOAD(s1, c0 + 5); CRT_GLOAD(s2, c0 + 6); CRT_GLOAD(s3, c0 + 7); }
+        }
+        CRT_MMA(0);
+        if constexpr (KC == 4) {
+            if (c0 + 1 < kcn) CRT_MMA(1);
+            if (c0 + 2 < kcn) CRT_MMA(2);
+            if (c0 + 3 < kcn) CRT_MMA(3);
+        }
         __syncthreads();
     }
+#undef CRT_GLOAD
+#undef CRT_LSTORE
+#undef CRT_MMA
     // residues -> 128 x 128 byte tile in LDS -> 128 B rows
     const int m = (int)c_crt_mod[mod];
     const float inv = c_crt_invf[mod];
@@ -1391,26 +1518,55 @@ __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar
     }
 }
 
+template <bool SYM, int KC>
+__global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar,
+                                                  const uint8_t* __restrict__ Br, uint32_t astride,
+                                                  uint32_t bstride, uint32_t kpad, uint32_t tiles_a,
+                                                  uint32_t tiles_m, uint8_t* __restrict__ R,
+                                                  const unsigned* __restrict__ bits_a,
+                                                  const unsigned* __restrict__ bits_b, uint32_t lk) {
+    crt_gemm_block<SYM, KC>(Ar, Br, astride, bstride, kpad, tiles_a, tiles_m, R, bits_a, bits_b, lk,
+                            blockIdx.x, gridDim.x, (int)blockIdx.y);
+}
+// The products of a CrtBatch in one launch: grid.x covers every job's tile
+// blocks (job j from blk0[j], multiples of 8 so the XCD mapping holds), grid.y
+// the moduli.
+template <int KC>
+__global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
+    uint32_t j = 0;
+    for (uint32_t k = 1; k < b.njobs; ++k) j += blockIdx.x >= b.job[k].blk0;
+    const CrtJob& q = b.job[j];
+    const uint32_t blk = blockIdx.x - q.blk0;
+    if (blk >= q.nblk) return;                    // padding to a multiple of 8
+    if (q.sym)
+        crt_gemm_block<true, KC>(q.Ar, q.Ar, q.astride, q.astride, q.kpad, q.tiles_a, q.tiles_a, q.R,
+                                 q.bits_a, q.bits_b, q.lk, blk, q.nblk, (int)blockIdx.y);
+    else
+        crt_gemm_block<false, KC>(q.Ar, q.Br, q.astride, q.bstride, q.kpad, q.tiles_a, q.tiles_m, q.R,
+                                  q.bits_a, q.bits_b, q.lk, blk, q.nblk, (int)blockIdx.y);
+}
+
 // C from its n residues, written as canonical Fr to out[i*ors + j*ocs]; one
 // 32 x 32 tile per block (SYM: upper tiles, mirrored through LDS).
 template <bool SYM>
-__global__ __launch_bounds__(256) void k_crt_combine(const uint8_t* __restrict__ R, uint32_t rpad_a,
-                                                     uint32_t rpad_b, uint32_t N, uint32_t M,
-                                                     uint32_t tiles_m, Fr* __restrict__ out,
-                                                     int64_t ors, int64_t ocs,
-                                                     const unsigned* __restrict__ bits_a,
-                                                     const unsigned* __restrict__ bits_b, uint32_t lk) {
+__device__ __forceinline__ void crt_combine_block(const uint8_t* __restrict__ R, uint32_t rpad_a,
+                                                  uint32_t rpad_b, uint32_t N, uint32_t M,
+                                                  uint32_t tiles_m, Fr* __restrict__ out,
+                                                  int64_t ors, int64_t ocs,
+                                                  const unsigned* __restrict__ bits_a,
+                                                  const unsigned* __restrict__ bits_b, uint32_t lk,
+                                                  uint32_t blk) {
     const int n = crt_nmod(*bits_a, *bits_b, lk);
     if (!n) return;
     __shared__ __attribute__((aligned(16))) uint8_t Ts[MT * MT * 32];
     uint32_t bi, bj;
     if (SYM) {
-        uint32_t b = blockIdx.x, r = 0, rowlen = tiles_m;
+        uint32_t b = blk, r = 0, rowlen = tiles_m;
         while (b >= rowlen) { b -= rowlen; ++r; --rowlen; }
         bi = r; bj = r + b;
     } else {
-        bi = blockIdx.x / tiles_m;
-        bj = blockIdx.x % tiles_m;
+        bi = blk / tiles_m;
+        bj = blk % tiles_m;
     }
     const uint32_t tid = threadIdx.x;
     const uint32_t i0 = bi * MT, j0 = bj * MT;
@@ -1485,10 +1641,63 @@ __global__ __launch_bounds__(256) void k_crt_combine(const uint8_t* __restrict__
     }
 }
 
+template <bool SYM>
+__global__ __launch_bounds__(256) void k_crt_combine(const uint8_t* __restrict__ R, uint32_t rpad_a,
+                                                     uint32_t rpad_b, uint32_t N, uint32_t M,
+                                                     uint32_t tiles_m, Fr* __restrict__ out,
+                                                     int64_t ors, int64_t ocs,
+                                                     const unsigned* __restrict__ bits_a,
+                                                     const unsigned* __restrict__ bits_b, uint32_t lk) {
+    crt_combine_block<SYM>(R, rpad_a, rpad_b, N, M, tiles_m, out, ors, ocs, bits_a, bits_b, lk, blockIdx.x);
+}
+__global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b) {
+    uint32_t j = 0;
+    for (uint32_t k = 1; k < b.njobs; ++k) j += blockIdx.x >= b.job[k].cblk0;
+    const CrtJob& q = b.job[j];
+    const uint32_t blk = blockIdx.x - q.cblk0;
+    const uint32_t rpa = q.tiles_a * CT, rpb = (q.sym ? q.tiles_a : q.tiles_m) * CT;
+    if (q.sym)
+        crt_combine_block<true>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
+                                q.bits_b, q.lk, blk);
+    else
+        crt_combine_block<false>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
+                                 q.bits_b, q.lk, blk);
+}
+
+hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
+    CrtBatch b = b0;
+    if (b.njobs < 1 || b.njobs > (uint32_t)kMaxCrtJobs) return hipErrorInvalidValue;
+    uint32_t blocks = 0, cblocks = 0;
+    for (uint32_t j = 0; j < b.njobs; ++j) {
+        CrtJob& q = b.job[j];
+        q.tiles_a = (q.N + CT - 1) / CT;
+        q.tiles_m = q.sym ? q.tiles_a : (q.M + CT - 1) / CT;
+        if (q.kpad % 64 || q.astride < q.tiles_a * CT || (!q.sym && q.bstride < q.tiles_m * CT))
+            return hipErrorInvalidValue;
+        if (q.sym && q.N != q.M) return hipErrorInvalidValue;
+        q.nblk = q.sym ? q.tiles_a * (q.tiles_a + 1) / 2 : q.tiles_a * q.tiles_m;
+        q.blk0 = blocks;
+        blocks += (q.nblk + 7) / 8 * 8;
+        const uint32_t sa = (q.N + MT - 1) / MT, sb = (q.M + MT - 1) / MT;
+        q.ctiles_m = q.sym ? sa : sb;
+        q.cblk0 = cblocks;
+        cblocks += q.sym ? sa * (sa + 1) / 2 : sa * sb;
+    }
+    if (b.kc == 4)
+        hipLaunchKernelGGL(k_gemm_crt_multi<4>, dim3(blocks, kCrtMaxMod), dim3(256), 0, st, b);
+    else
+        hipLaunchKernelGGL(k_gemm_crt_multi<1>, dim3(blocks, kCrtMaxMod), dim3(256), 0, st, b);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_crt_combine_multi, dim3(cblocks), dim3(256), 0, st, b);
+    return hipGetLastError();
+}
+
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st) {
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st, int kc) {
+    if (kc != 1 && kc != 4) return hipErrorInvalidValue;
     const uint32_t ta = (N + CT - 1) / CT, tb = (M + CT - 1) / CT;
     // every staged row (tiles x CT) lies inside its operand's planes
     if (kpad % 64 || astride < ta * CT || bstride < tb * CT) return hipErrorInvalidValue;
@@ -1496,13 +1705,21 @@ hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint3
     const uint32_t sa = (N + MT - 1) / MT, sb = (M + MT - 1) / MT;
     if (sym) {
         if (N != M || astride != bstride) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_gemm_crt<true>, dim3(ta * (ta + 1) / 2, kCrtMaxMod), dim3(256), 0, st,
-                           Ar, Ar, astride, bstride, kpad, ta, ta, R, bits_a, bits_b, lk);
+        if (kc == 4)
+            hipLaunchKernelGGL((k_gemm_crt<true, 4>), dim3(ta * (ta + 1) / 2, kCrtMaxMod), dim3(256), 0, st,
+                               Ar, Ar, astride, bstride, kpad, ta, ta, R, bits_a, bits_b, lk);
+        else
+            hipLaunchKernelGGL((k_gemm_crt<true, 1>), dim3(ta * (ta + 1) / 2, kCrtMaxMod), dim3(256), 0, st,
+                               Ar, Ar, astride, bstride, kpad, ta, ta, R, bits_a, bits_b, lk);
         hipLaunchKernelGGL(k_crt_combine<true>, dim3(sa * (sa + 1) / 2), dim3(256), 0, st, R, rpa,
                            rpb, N, M, sa, out, ors, ocs, bits_a, bits_b, lk);
     } else {
-        hipLaunchKernelGGL(k_gemm_crt<false>, dim3(ta * tb, kCrtMaxMod), dim3(256), 0, st, Ar, Br,
-                           astride, bstride, kpad, ta, tb, R, bits_a, bits_b, lk);
+        if (kc == 4)
+            hipLaunchKernelGGL((k_gemm_crt<false, 4>), dim3(ta * tb, kCrtMaxMod), dim3(256), 0, st, Ar, Br,
+                               astride, bstride, kpad, ta, tb, R, bits_a, bits_b, lk);
+        else
+            hipLaunchKernelGGL((k_gemm_crt<false, 1>), dim3(ta * tb, kCrtMaxMod), dim3(256), 0, st, Ar, Br,
+                               astride, bstride, kpad, ta, tb, R, bits_a, bits_b, lk);
         hipLaunchKernelGGL(k_crt_combine<false>, dim3(sa * sb), dim3(256), 0, st, R, rpa, rpb,
                            N, M, sb, out, ors, ocs, bits_a, bits_b, lk);
     }

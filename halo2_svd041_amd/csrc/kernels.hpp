@@ -166,6 +166,11 @@ hipError_t launch_bits_reduce(const unsigned* blockmax, const BitSegs& seg, uint
 static constexpr uint32_t kMaxBitBlocks = 2048;
 // Generic cell-program stage over elements [a.e_begin, a.e_end).
 hipError_t launch_stage(const StageArgs& a, hipStream_t st);
+// Independent stages (no stage reads another's cells) in as few k_stage_multi
+// launches as their records fit (stage_record_bytes, kMultiBytes); n >= 1.
+hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st);
+// does the record of `a` fit one k_stage_multi launch?
+bool stage_multi_fits(const StageArgs& a);
 // max over the view of bit-length(|signed(x)|): out[b] = max of block b
 // (min(ceil(rows * cols / 256), kMaxBitBlocks) blocks).
 hipError_t launch_maxbits(const DView& v, uint32_t rows, uint32_t cols, unsigned* out,
@@ -236,8 +241,31 @@ hipError_t launch_residues_f64(const ResSegs& q, const unsigned* W, int precisio
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st);
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st, int kc = 4);
 static constexpr int kCrtMaxResidues = 40;   // = kCrtMaxMod (crt_tables.hpp)
+// Several CRT products in one GEMM launch and one combine launch (a row-sharded
+// rank's three products of check_svd_phase0). Per job the caller sets Ar, Br,
+// astride, bstride, kpad, R (its own residue scratch), out, ors, ocs, N, M,
+// bits_a, bits_b, lk and sym (A == B: upper tiles + mirror); the launcher
+// fills the tile and block fields.
+static constexpr int kMaxCrtJobs = 3;
+struct CrtJob {
+    const uint8_t* Ar;
+    const uint8_t* Br;
+    uint8_t* R;
+    Fr* out;
+    const unsigned* bits_a;
+    const unsigned* bits_b;
+    int64_t ors, ocs;
+    uint32_t astride, bstride, kpad, N, M, lk, sym;
+    uint32_t tiles_a, tiles_m, nblk, blk0, ctiles_m, cblk0;
+};
+struct CrtBatch {
+    CrtJob job[kMaxCrtJobs];
+    uint32_t njobs;
+    int kc;
+};
+hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st);
 // w (len L) from a view (row 0 / col j of a 1 x L view) -> canonical copy
 // (w_canon nullable) and its scaled table (ScaleTab f: see kTabSlots).
 hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* tab, const ScaleTab& f,

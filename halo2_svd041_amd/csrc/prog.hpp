@@ -14,6 +14,7 @@
 // Range-check limbs are bit windows of the canonical value, and the running
 // sums of the limb inner product are `value mod 2^(i*LB)`.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #include "fr.hpp"
@@ -66,6 +67,7 @@ static constexpr uint32_t STAGE_PROBE_NOA = 64;
 static constexpr uint32_t STAGE_PROBE_CONST = 128;
 static constexpr uint32_t STAGE_ALIGN = 256;     // 4 KiB-aligned block store windows
 static constexpr uint32_t STAGE_INC = 512;       // phase B decoding slot ops per half-cell (A/B reference)
+static constexpr uint32_t STAGE_PROBE_NOLD = 1024;  // timing probe: no view loads either (with CONST)
 
 static constexpr int kMaxViews = 2;
 static constexpr int kMaxMicro = 16;
@@ -93,6 +95,26 @@ struct StageArgs {
     Fr K[kMaxK];
 };
 static_assert(sizeof(StageArgs) < 4096, "kernel argument block too large");
+
+// A batch of independent stages in one launch (k_stage_multi). Each program is
+// a compact record in `data`: StageArgs up to `mo` (scalar fields and views,
+// kRecHead bytes), then its nmo micro-ops, C + L slot ops and nk constants.
+// Program p runs blocks [blk0[p], blk0[p + 1]).
+static constexpr uint32_t kRecHead = (uint32_t)offsetof(StageArgs, mo);
+static_assert(kRecHead % 8 == 0, "record head keeps 8-byte alignment");
+constexpr uint32_t stage_record_bytes(uint32_t nmo, uint32_t C, uint32_t L, uint32_t nk) {
+    return (kRecHead + 8 * nmo + 4 * (C + L) + 32 * nk + 7) / 8 * 8;
+}
+static constexpr int kMaxMulti = 16;
+static constexpr uint32_t kMultiBytes = 3712;
+struct StageMulti {
+    uint32_t nprog;
+    uint32_t blk0[kMaxMulti + 1];
+    uint32_t off[kMaxMulti];
+    uint32_t _pad;
+    alignas(8) uint8_t data[kMultiBytes];
+};
+static_assert(sizeof(StageMulti) < 4096, "kernel argument block too large");
 
 // Phase-B half-cell descriptor (one per slot and half, built per block in LDS):
 // output words [4h, 4h+4) of a cell are alignbit(x[i+1], x[i], r) & mask[i]
