@@ -450,8 +450,11 @@ struct svdw_ctx {
     int prelaunch_at = 0;                   // "prelaunch_at": GEMMs queued before stage 0/1/2
     int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
-    int gemm_kc = 4;                        // "gemm_kc": 64-k chunks per LDS round of the CRT GEMM (1 / 4)
+    int gemm_kc = 1;                        // "gemm_kc": 64-k chunks per LDS round of the CRT GEMM (1 / 4;
+                                            // 4 needs 64 KiB of LDS and starves beside the stage blocks)
     bool gemm_batched = false;              // this witness's products went out as one batch
+    int res_first = -1;                     // "res_first": cell stream waits for the residue planes
+                                            // (1), not (0), -1: on row-sharded ranks
     int gemm_batch = -1;                    // "gemm_batch": svd_witness's three products in one launch
                                             // (1), one by one (0), or -1: batched on row-sharded ranks
     bool fused_quantize = true;             // "fused_quantize": m, u, v, d in one launch
@@ -855,11 +858,12 @@ struct BatchScope {
     svdw_ctx* c;
     hipStream_t st = nullptr;
     bool mine = false;
-    explicit BatchScope(svdw_ctx* cc) : c(cc) {
+    explicit BatchScope(svdw_ctx* cc, hipStream_t on = nullptr) : c(cc) {
         if (c->dry || !c->stage_batch) return;
+        if (!on) on = c->st;
         for (auto& b : c->batches)
-            if (b.st == c->st) return;
-        st = c->st;
+            if (b.st == on) return;
+        st = on;
         c->batches.push_back({st, {}});
         mine = true;
     }
@@ -1007,15 +1011,24 @@ static svdw_vec put_cell(svdw_ctx* c, uint32_t phase, const Fr& v, bool constant
 // ----------------------------------------------------- reference functions
 // qs: collect the quantization into one k_quantize_multi launch (device inputs
 // only) instead of launching it here.
+// own_rows_only (row-sharded svd_witness, m): quantize only this rank's rows,
+// the only rows of the matrix any of its stages read.
 static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, uint32_t rows,
                              uint32_t cols, bool on_device, unsigned* blockmax = nullptr,
-                             QuantSegs* qs = nullptr) {
+                             QuantSegs* qs = nullptr, bool own_rows_only = false) {
     REQUIRE(rows >= 1 && cols >= 1, "ZkMatrix::new: empty matrix");
     REQUIRE(data || c->dry, "null data");
     uint64_t n = (uint64_t)rows * cols, off;
     append(c, phase, n, 0, &off, nullptr, "load", rows);
-    if (!c->dry) {
-        const double* src = data;
+    uint64_t q0 = 0;                                      // first quantized value
+    if (own_rows_only && sharded(c) && on_device && qs) {
+        uint64_t r0, r1;
+        shard_rows(c, rows, &r0, &r1);
+        q0 = r0 * cols;
+        n = (r1 - r0) * cols;
+    }
+    if (!c->dry && n) {
+        const double* src = data + q0;
         if (!on_device) {
             ensure_buf(c, c->f64in, n * sizeof(double));
             hipck(hipMemcpyAsync(c->f64in.p, data, n * sizeof(double), hipMemcpyHostToDevice, c->st),
@@ -1025,7 +1038,7 @@ static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, ui
         if (qs && on_device && qs->nseg < (uint32_t)kMaxQuantSegs) {
             const uint32_t k = qs->nseg++;
             qs->in[k] = src;
-            qs->out[k] = cellp(c, phase, off);
+            qs->out[k] = cellp(c, phase, off + q0);
             qs->blockmax[k] = blockmax;
             qs->n[k] = n;
             qs->blk0[k + 1] = qs->blk0[k] + (uint32_t)((n + 255) / 256);
@@ -1939,6 +1952,9 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
                      8.0 * ((double)rows_m * M + (double)M * M + (double)N * N), 0);
         hipck(launch_residues_f64(q, W, (int)c->P, c->st2), "k_residues_f64");
     }
+    // res_first: the cell stream waits for the residue planes, which then run
+    // alone instead of beside the first (HBM-saturating) stages
+    if (c->res_first > 0 || (c->res_first < 0 && sharded(c))) stream_dep(c, c->st2, c->st);
     const uint8_t* P[3] = {(const uint8_t*)c->digA.p, (const uint8_t*)c->digC.p,
                            (const uint8_t*)c->digB.p};                 // A planes of m, u, v
     const uint32_t stride[3] = {rp_m, rp_u, rp_v}, kp[3] = {kpM, kpN, kpM}, lk[3] = {lkM, lkN, lkM};
@@ -1988,9 +2004,10 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
             ProfScope ps(c, c->st2, "k_gemm_crt:multi", bytes, ops);
             hipck(launch_gemm_crt_multi(b, c->st2), "k_gemm_crt_multi");
         }
+        const hipEvent_t done = stream_dep(c, c->st2, nullptr);   // one completion point
         for (int g = 0; g < 3; ++g) {
-            c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
-            c->gemm_done.push_back(c->pre.back().ev);
+            c->pre.push_back({log[g], done});
+            c->gemm_done.push_back(done);
         }
         return;
     }
@@ -2110,6 +2127,10 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         host_mark(c, "products queued");
     };
     if (c->prelaunch_at == 0) prelaunch();
+    // what goes aside on st2 (d checks, single constant cells) is read by no
+    // later kernel: batched until the end of phase 0 (two launches)
+    BatchScope aside(c, c->st2);
+    if (!(c->prelaunched && c->d_checks_aside)) aside.close();
     {
         // The d checks (three latency-bound stages over r elements) depend on d
         // only: with the products queued ahead they go behind them on st2, off
@@ -2201,6 +2222,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     svdw_mat vvt = honest_prover_mat_mul(c, m.phase, v, vt, bv, bv);
     check_mat_id(c, vvt, q2, eu, &qq);
     bs2.end();
+    aside.end();
     host_mark(c, "ids queued");
     return svdw_svd_payload{ut, vt, mvt, uut, vvt};
 }
@@ -2276,7 +2298,10 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         host_mark(c, "gamma_prep queued");
     }
     unsigned* dbits = nullptr;
-    const uint32_t nbm = (uint32_t)(((uint64_t)N * M + 255) / 256);
+    // m: only this rank's rows are quantized on a row-sharded rank (zkmatrix_new)
+    uint64_t mr0 = 0, mr1 = N;
+    if (sharded(c) && on_device && c->fused_quantize) shard_rows(c, N, &mr0, &mr1);
+    const uint32_t nbm = (uint32_t)(((mr1 - mr0) * M + 255) / 256);
     const uint32_t nbu = (uint32_t)(((uint64_t)N * N + 255) / 256);
     const uint32_t nbv = (uint32_t)(((uint64_t)M * M + 255) / 256);
     if (!c->dry) {
@@ -2287,7 +2312,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     QuantSegs qs;
     memset(&qs, 0, sizeof qs);
     QuantSegs* qp = c->fused_quantize ? &qs : nullptr;
-    svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device, dbits ? dbits + 64 : nullptr, qp);
+    svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device, dbits ? dbits + 64 : nullptr, qp, true);
     svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device, dbits ? dbits + 64 + nbm : nullptr, qp);
     svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device, dbits ? dbits + 64 + nbm + nbu : nullptr, qp);
     svdw_mat zdm = zkmatrix_new(c, 0, d, r, 1, on_device, nullptr, qp);
@@ -3282,6 +3307,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_crt = (int)value;
         } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
             c->stage_batch = value != 0;
+        } else if (n == "res_first") {
+            REQUIRE(value >= -1 && value <= 1, "res_first: -1 (auto), 0 or 1");
+            c->res_first = (int)value;
         } else if (n == "gemm_batch") {
             REQUIRE(value >= -1 && value <= 1, "gemm_batch: -1 (auto), 0 or 1");
             c->gemm_batch = (int)value;

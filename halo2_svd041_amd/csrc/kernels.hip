@@ -1572,9 +1572,10 @@ __device__ __forceinline__ void crt_combine_block(const uint8_t* __restrict__ R,
     const uint32_t i0 = bi * MT, j0 = bj * MT;
     const int off = n * (n - 1) / 2;
     const uint64_t plane = (uint64_t)rpad_a * rpad_b;
-    // four elements per thread (rows tr0 + 8 q, one column), interleaved for ILP
-    const uint32_t tc = tid & 31, tr0 = tid >> 5;
-    const uint8_t* rp = R + (uint64_t)(i0 + tr0) * rpad_b + j0 + tc;
+    // four elements per thread (one row, columns tc0 .. tc0 + 3: one 4-byte load
+    // per modulus), interleaved for ILP
+    const uint32_t tc0 = (tid & 7) * 4, tr = tid >> 3;
+    const uint32_t* rp = reinterpret_cast<const uint32_t*>(R + (uint64_t)(i0 + tr) * rpad_b + j0 + tc0);
     // 16 accumulators per element, one per 16-bit limb of ep: r (8 bit) x limb
     // (16 bit) < 2^24, n <= 40 terms plus q x nmp stay below 2^31 -> no carries
     uint32_t acc[4][16];
@@ -1587,8 +1588,9 @@ __device__ __forceinline__ void crt_combine_block(const uint8_t* __restrict__ R,
     }
     for (int k = 0; k < n; ++k) {
         uint32_t r[4];
+        const uint32_t w4 = rp[(uint64_t)k * (plane >> 2)];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) r[q] = rp[k * plane + (uint64_t)q * 8 * rpad_b];
+        for (int q = 0; q < 4; ++q) r[q] = (w4 >> (8 * q)) & 0xffu;
         const double fr = c_crt_frac[off + k];
 #pragma unroll
         for (int q = 0; q < 4; ++q) s[q] = fma((double)r[q], fr, s[q]);
@@ -1617,7 +1619,7 @@ __device__ __forceinline__ void crt_combine_block(const uint8_t* __restrict__ R,
         }
         x[8] = (uint32_t)t;
         const Fr v = reduce9(x);
-        const uint32_t tr = tr0 + 8 * q;
+        const uint32_t tc = tc0 + q;
         uint4* dst = reinterpret_cast<uint4*>(Ts + (tr * MT + tc) * 32);
         dst[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
         dst[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);

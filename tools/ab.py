@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--variant", action="append", default=[])
+    ap.add_argument("--top", type=int, default=8, help="kernels listed per variant")
     a = ap.parse_args()
     import torch
     import halo2_svd041_amd as hs
@@ -90,7 +91,7 @@ def main():
         med = statistics.median(res[name])
         print(f"{name:12s} median {med:.4f} ms  min {min(res[name]):.4f}  -> {cells / med / 1e6:.2f} Gcells/s"
               f"  samples {' '.join(f'{x:.3f}' for x in sorted(res[name]))}")
-        top = sorted(kern[name].items(), key=lambda kv: -statistics.median(kv[1]))[:8]
+        top = sorted(kern[name].items(), key=lambda kv: -statistics.median(kv[1]))[:a.top]
         print("   " + "  ".join(f"{k}={statistics.median(vv):.3f}" for k, vv in top))
     print(json.dumps({n: statistics.median(r) for n, r in res.items()}))
 
