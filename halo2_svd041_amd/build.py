@@ -11,8 +11,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libsvdw.so")
-SOURCES = ["kernels.hip", "engine.cpp"]
-HEADERS = ["fr.hpp", "prog.hpp", "kernels.hpp", "crt_tables.hpp", "ingest.hpp"]
+SOURCES = ["kernels.hip", "ingest_dev.hip", "engine.cpp"]
+HEADERS = ["fr.hpp", "prog.hpp", "kernels.hpp", "crt_tables.hpp", "ingest.hpp", "ingest_dev.hpp"]
 ARCH = os.environ.get("SVDW_OFFLOAD_ARCH", "gfx950")
 
 

@@ -26,6 +26,7 @@
 
 #include "../../include/svdw.h"
 #include "ingest.hpp"
+#include "ingest_dev.hpp"
 #include "kernels.hpp"
 
 using namespace svdw;
@@ -534,6 +535,8 @@ struct svdw_ctx {
     };
     std::vector<Batch> batches;
     bool stage_batch = true;
+    // device ingest (svdw_parse_svd_input_device) scratch
+    DBuf ing_x, ing_e, ing_c, ing_p10, ing_val, ing_npos, ing_nd, ing_rpos, ing_kpos, ing_err, ing_q;
 };
 
 static void flush_batch(svdw_ctx* c, hipStream_t s);
@@ -2853,6 +2856,196 @@ int svdw_parse_svd_input(const char* text, uint64_t len, int mode, svdw_input_di
             {m, &in.m}, {u, &in.u}, {d, &in.d}, {v, &in.v}};
         for (const auto& o : outs)
             if (o.first) memcpy(o.first, o.second->v.data(), o.second->v.size() * sizeof(double));
+    });
+}
+// Device ingest of data/matrix.in (ingest_dev.hip): three passes over the text
+// on the device, then the few top-level keys and the arrays' number ranges on
+// the host (small reads), then a device check of depths, separators and row
+// lengths of m, u, v, d and device-to-device copies of their values.
+namespace {
+struct DevText {                  // small host reads of the device text
+    svdw_ctx* c;
+    const uint8_t* t;
+    uint64_t n;
+    std::vector<uint8_t> get(uint64_t at, uint64_t len) {
+        len = std::min(len, at < n ? n - at : 0);
+        std::vector<uint8_t> b(len);
+        if (len) hipck(hipMemcpy(b.data(), t + at, len, hipMemcpyDeviceToHost), "D2H");
+        return b;
+    }
+    // the string starting with the quote at `at`: its content (escapes as the
+    // host parser reads them) and the position just past the closing quote
+    bool str(uint64_t at, std::string* s, uint64_t* end) {
+        uint64_t p = at + 1;
+        bool esc = false;
+        for (;;) {
+            std::vector<uint8_t> b = get(p, 256);
+            if (b.empty()) return false;
+            for (size_t k = 0; k < b.size(); ++k, ++p) {
+                if (esc) { s->push_back((char)b[k]); esc = false; continue; }
+                if (b[k] == '\\') { esc = true; continue; }
+                if (b[k] == '"') { *end = p + 1; return true; }
+                s->push_back((char)b[k]);
+            }
+        }
+    }
+    int next_nonws(uint64_t at) {
+        for (;;) {
+            std::vector<uint8_t> b = get(at, 256);
+            if (b.empty()) return -1;
+            for (uint8_t x : b)
+                if (!(x == ' ' || x == '\n' || x == '\r' || x == '\t')) return x;
+            at += b.size();
+        }
+    }
+};
+}  // namespace
+int svdw_parse_svd_input_device(svdw_ctx* c, const void* text, uint64_t len, int mode,
+                                svdw_input_dims* dims, double* m, double* u, double* d, double* v) {
+    namespace ig = svdw_ingest_dev;
+    return guarded([&] {
+        REQUIRE(c && text && dims, "null argument");
+        REQUIRE(!c->dry, "device ingest needs a device context");
+        REQUIRE(mode == SVDW_PARSE_SERDE,
+                "device ingest: serde mode only (correct rounding: svdw_parse_svd_input)");
+        REQUIRE(len > 0, "svd input: empty text");
+        const uint8_t* t = (const uint8_t*)text;
+        const uint64_t nc64 = (len + ig::kChunk - 1) / ig::kChunk;
+        REQUIRE(nc64 < (1ull << 31), "svd input: text too large");
+        const uint32_t nc = (uint32_t)nc64;
+        hipStream_t s = c->st;
+        sync(c);
+        if (!c->ing_p10.p) {                       // serde's POW10 table (correctly rounded 10^k)
+            std::vector<double> p10(309);
+            char buf[16];
+            for (int i = 0; i <= 308; ++i) { snprintf(buf, sizeof buf, "1e%d", i); p10[i] = strtod(buf, nullptr); }
+            ensure_buf(c, c->ing_p10, sizeof(double) * 309);
+            hipck(hipMemcpy(c->ing_p10.p, p10.data(), sizeof(double) * 309, hipMemcpyHostToDevice), "H2D");
+        }
+        ensure_buf(c, c->ing_x, sizeof(ig::Xfer) * nc);
+        ensure_buf(c, c->ing_e, sizeof(ig::Entry) * (nc + 1));
+        ensure_buf(c, c->ing_c, sizeof(ig::Counts) * (nc + 1));
+        ig::Xfer* X = (ig::Xfer*)c->ing_x.p;
+        ig::Entry* E = (ig::Entry*)c->ing_e.p;
+        ig::Counts* C = (ig::Counts*)c->ing_c.p;
+        hipck(ig::launch_pass1(t, len, X, s), "ingest pass 1");
+        hipck(ig::launch_scan1(X, nc, E, s), "ingest scan 1");
+        hipck(ig::launch_pass2(t, len, E, C, s), "ingest pass 2");
+        hipck(ig::launch_scan2(C, nc, s), "ingest scan 2");
+        ig::Entry fin;
+        ig::Counts tot;
+        hipck(hipMemcpyAsync(&fin, E + nc, sizeof fin, hipMemcpyDeviceToHost, s), "D2H");
+        hipck(hipMemcpyAsync(&tot, C + nc, sizeof tot, hipMemcpyDeviceToHost, s), "D2H");
+        hipck(hipStreamSynchronize(s), "hipStreamSynchronize");
+        REQUIRE(fin.state == 0, "svd input: unterminated string");
+        REQUIRE(fin.depth == 0, "svd input: unbalanced brackets");
+        const uint32_t nn = tot.num, nr = tot.row, nk = tot.key;
+        ensure_buf(c, c->ing_val, sizeof(double) * std::max(nn, 1u));
+        ensure_buf(c, c->ing_npos, sizeof(uint64_t) * std::max(nn, 1u));
+        ensure_buf(c, c->ing_nd, std::max(nn, 1u));
+        ensure_buf(c, c->ing_rpos, sizeof(uint64_t) * std::max(nr, 1u));
+        ensure_buf(c, c->ing_kpos, sizeof(uint64_t) * std::max(nk, 1u));
+        ensure_buf(c, c->ing_err, sizeof(uint64_t) * 264);
+        unsigned long long* slist = (unsigned long long*)c->ing_err.p;          // [0] count, [1..255]
+        unsigned long long* verr = slist + 256;
+        hipck(hipMemsetAsync(slist, 0, sizeof(uint64_t), s), "memset");
+        hipck(hipMemsetAsync(verr, 0xff, sizeof(uint64_t), s), "memset");
+        hipck(ig::launch_pass3(t, len, E, C, (const double*)c->ing_p10.p, (double*)c->ing_val.p,
+                               (uint64_t*)c->ing_npos.p, (uint8_t*)c->ing_nd.p, (uint64_t*)c->ing_rpos.p,
+                               (uint64_t*)c->ing_kpos.p, slist, s), "ingest pass 3");
+        std::vector<uint64_t> kpos(nk), sl(256);
+        if (nk) hipck(hipMemcpyAsync(kpos.data(), c->ing_kpos.p, sizeof(uint64_t) * nk, hipMemcpyDeviceToHost, s), "D2H");
+        hipck(hipMemcpyAsync(sl.data(), slist, sizeof(uint64_t) * 256, hipMemcpyDeviceToHost, s), "D2H");
+        hipck(hipStreamSynchronize(s), "hipStreamSynchronize");
+        auto at = [](uint64_t p) { return " (at byte " + std::to_string(p) + ")"; };
+        // members: depth-1 strings followed by ':' are keys (host parser: str, ws, ':')
+        DevText dt{c, t, len};
+        struct Member { uint64_t pos; std::string key; };
+        std::vector<Member> mem;
+        for (uint32_t j = 0; j < nk; ++j) {
+            std::string k;
+            uint64_t end = 0;
+            REQUIRE(dt.str(kpos[j], &k, &end), "svd input: unterminated string" + at(kpos[j]));
+            const int nx = dt.next_nonws(end);
+            // a key follows '{' or ','; a string value follows ':' and is not followed by ':'
+            std::vector<uint8_t> back = dt.get(kpos[j] >= 256 ? kpos[j] - 256 : 0, kpos[j] >= 256 ? 256 : kpos[j]);
+            int pv = 0;
+            for (size_t q = back.size(); q-- > 0;)
+                if (!(back[q] == ' ' || back[q] == '\n' || back[q] == '\r' || back[q] == '\t')) { pv = back[q]; break; }
+            if (pv == ':') {
+                REQUIRE(nx != ':', "svd input: expected ',' or '}'" + at(end));
+                continue;
+            }
+            REQUIRE(nx == ':', "svd input: expected ':'" + at(end));
+            mem.push_back({kpos[j], k});
+        }
+        const uint64_t nsl = sl[0];
+        REQUIRE(nsl <= 255, "svd input: too many structural irregularities for the device parser");
+        for (const char* want : {"m", "u", "v", "d"}) {
+            int cnt = 0;
+            for (const auto& x : mem) cnt += x.key == want;
+            REQUIRE(cnt <= 1, std::string("svd input: duplicate key \"") + want + "\"");
+            REQUIRE(cnt == 1, "svd input: missing one of the keys m, u, v, d");
+        }
+        // number / row-open ranges of every member
+        std::vector<uint64_t> q;
+        for (const auto& x : mem) q.push_back(x.pos);
+        q.push_back(len);
+        ensure_buf(c, c->ing_q, (sizeof(uint64_t) + 2 * sizeof(uint32_t)) * q.size());
+        uint32_t* rg = (uint32_t*)((uint64_t*)c->ing_q.p + q.size());
+        hipck(hipMemcpyAsync(c->ing_q.p, q.data(), sizeof(uint64_t) * q.size(), hipMemcpyHostToDevice, s), "H2D");
+        hipck(ig::launch_ranges((const uint64_t*)c->ing_npos.p, nn, (const uint64_t*)c->ing_rpos.p, nr,
+                                (const uint64_t*)c->ing_q.p, (uint32_t)q.size(), rg, s), "ingest ranges");
+        std::vector<uint32_t> r(2 * q.size());
+        hipck(hipMemcpyAsync(r.data(), rg, sizeof(uint32_t) * r.size(), hipMemcpyDeviceToHost, s), "D2H");
+        hipck(hipStreamSynchronize(s), "hipStreamSynchronize");
+        for (uint64_t k = 0; k < nsl; ++k) {       // structural errors: object level, or inside m/u/v/d
+            const uint64_t p = sl[1 + k] & ~(1ull << 63);
+            REQUIRE(!(sl[1 + k] >> 63), "svd input: malformed JSON object" + at(p));
+            for (size_t j = 0; j < mem.size(); ++j) {
+                const bool known = mem[j].key == "m" || mem[j].key == "u" || mem[j].key == "v" || mem[j].key == "d";
+                REQUIRE(!(known && p >= q[j] && p < q[j + 1]), "svd input: malformed array" + at(p));
+            }
+        }
+        struct Arr { uint32_t lo, hi, r0, rows, cols; };
+        auto arr = [&](const char* key, bool matrix) {
+            size_t j = 0;
+            while (mem[j].key != key) ++j;
+            Arr a{r[2 * j], r[2 * j + 2], r[2 * j + 1], r[2 * j + 3] - r[2 * j + 1], 0};
+            const uint32_t total = a.hi - a.lo;
+            if (matrix) {
+                REQUIRE(a.rows >= 1, "svd input: m, u, v must be matrices and d a vector");
+                REQUIRE(total % a.rows == 0, std::string("svd input: ragged matrix rows (") + key + ")");
+                a.cols = total / a.rows;
+            } else {
+                REQUIRE(a.rows == 0, "svd input: m, u, v must be matrices and d a vector");
+                a.cols = total;
+            }
+            hipck(ig::launch_validate((const uint8_t*)c->ing_nd.p, a.lo, a.hi, matrix ? 3 : 2,
+                                      (const uint64_t*)c->ing_npos.p, nn, (const uint64_t*)c->ing_rpos.p,
+                                      a.r0, a.rows, a.cols, verr, s), "ingest validate");
+            return a;
+        };
+        const Arr am = arr("m", true), au = arr("u", true), av = arr("v", true), ad = arr("d", false);
+        unsigned long long ve = 0;
+        hipck(hipMemcpyAsync(&ve, verr, sizeof ve, hipMemcpyDeviceToHost, s), "D2H");
+        hipck(hipStreamSynchronize(s), "hipStreamSynchronize");
+        if (ve != ~0ull) {
+            static const char* what[] = {"", "expected a number", "significand beyond u64 (serde's overflow path is not emulated)",
+                                         "number out of range", "expected ',' or ']'", "unexpected nesting",
+                                         "ragged matrix rows"};
+            const uint32_t code = (uint32_t)(ve >> 48);
+            fail(SVDW_EINVAL, std::string("svd input: ") + (code < 7 ? what[code] : "malformed") +
+                              at(ve & ((1ull << 48) - 1)));
+        }
+        *dims = svdw_input_dims{am.rows, am.cols, au.rows, au.cols, av.rows, av.cols, ad.cols};
+        const std::pair<double*, const Arr*> outs[4] = {{m, &am}, {u, &au}, {d, &ad}, {v, &av}};
+        for (const auto& o : outs)
+            if (o.first && o.second->hi > o.second->lo)
+                hipck(hipMemcpyAsync(o.first, (const double*)c->ing_val.p + o.second->lo,
+                                     sizeof(double) * (o.second->hi - o.second->lo), hipMemcpyDeviceToDevice, s),
+                      "D2D");
+        hipck(hipStreamSynchronize(s), "hipStreamSynchronize");
     });
 }
 int svdw_set_shard(svdw_ctx* c, uint32_t rank, uint32_t world) {

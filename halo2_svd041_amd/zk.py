@@ -554,6 +554,38 @@ def parse_svd_input(src, mode: str = "serde") -> dict:
     return {"m": m, "u": u, "d": d, "v": v}
 
 
+def parse_svd_input_device(ctx: "Context", src):
+    """parse_svd_input on the device (svdw_parse_svd_input_device, serde mode):
+    the text (a path, bytes, str, or a uint8 torch tensor already on the
+    context's device) is staged to HBM and parsed there; returns device f64
+    torch tensors m, u, d, v, ready for svd_witness (on_device)."""
+    import torch
+    dev = torch.device("cuda", ctx.device)
+    if isinstance(src, torch.Tensor):
+        t = src.to(dev, dtype=torch.uint8).contiguous()
+    else:
+        if isinstance(src, (bytes, bytearray)):
+            text = bytes(src)
+        elif isinstance(src, str) and src.lstrip().startswith("{"):
+            text = src.encode()
+        else:
+            with open(src, "rb") as fh:
+                text = fh.read()
+        t = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(dev)
+    dims = InputDims()
+    n = t.numel()
+    check(lib().svdw_parse_svd_input_device(ctx._h, t.data_ptr(), n, 0, ct.byref(dims),
+                                            None, None, None, None))
+    out = {"m": torch.empty((dims.m_rows, dims.m_cols), dtype=torch.float64, device=dev),
+           "u": torch.empty((dims.u_rows, dims.u_cols), dtype=torch.float64, device=dev),
+           "v": torch.empty((dims.v_rows, dims.v_cols), dtype=torch.float64, device=dev),
+           "d": torch.empty(dims.d_len, dtype=torch.float64, device=dev)}
+    check(lib().svdw_parse_svd_input_device(ctx._h, t.data_ptr(), n, 0, ct.byref(dims),
+                                            out["m"].data_ptr(), out["u"].data_ptr(),
+                                            out["d"].data_ptr(), out["v"].data_ptr()))
+    return out
+
+
 def plan_svd(N: int, M: int, precision_bits: int, lookup_bits: int,
              cfg: SvdConfigPy = SvdConfigPy()) -> dict:
     """Closed-form cell counts (no device)."""

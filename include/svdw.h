@@ -398,6 +398,14 @@ typedef struct {
 } svdw_input_dims;
 int svdw_parse_svd_input(const char* text, uint64_t len, int mode, svdw_input_dims* dims,
                          double* m, double* u, double* d, double* v);
+/* The same parse of text already in device memory, on the context's device
+ * (serde mode only): m, u, d, v are DEVICE pointers (null: dims only), ready for
+ * svdw_svd_witness(on_device = 1). Replaces examples/svd_example.rs:326-330
+ * (read_to_string + serde_json::from_str) for a file staged to HBM; the values
+ * are identical to svdw_parse_svd_input's (SVDW_PARSE_SERDE) on every input, and
+ * malformed text is rejected (SVDW_EINVAL). Synchronous. */
+int svdw_parse_svd_input_device(svdw_ctx* ctx, const void* text, uint64_t len, int mode,
+                                svdw_input_dims* dims, double* m, double* u, double* d, double* v);
 
 /* Closed-form cell counts of svdw_svd_witness without touching a device. */
 int svdw_plan_svd(uint32_t N, uint32_t M, uint32_t precision_bits, uint32_t lookup_bits,

@@ -9,6 +9,6 @@ TMP=$(mktemp -d)
 git -C "$ROOT" archive "$REV" halo2_svd041_amd/csrc include | tar -x -C "$TMP"
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -Wno-unused-function \
   -I"$TMP/include" -o "$ROOT/halo2_svd041_amd/libsvdw_base.so" \
-  "$TMP/halo2_svd041_amd/csrc/kernels.hip" "$TMP/halo2_svd041_amd/csrc/engine.cpp"
+  $(ls "$TMP"/halo2_svd041_amd/csrc/*.hip) "$TMP/halo2_svd041_amd/csrc/engine.cpp"
 rm -rf "$TMP"
 echo "built libsvdw_base.so from $REV"
