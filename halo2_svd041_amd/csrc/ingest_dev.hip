@@ -16,7 +16,32 @@
 
 namespace svdw_ingest_dev {
 
-static constexpr int kThreads = 256, kPer = kChunk / kThreads;   // 8 bytes per thread
+static constexpr int kThreads = 256, kPer = kChunk / kThreads;   // 16 bytes per thread
+static constexpr uint32_t kHalo = 256;   // bytes staged before and after a chunk
+
+// The text as a block sees it: its chunk and halos staged in LDS (coalesced
+// 16-byte loads), anything further out (long tokens or whitespace runs) read
+// from global memory.
+struct Txt {
+    const uint8_t* g;
+    const uint8_t* s;
+    uint64_t lo, hi;
+    __device__ __forceinline__ uint8_t operator[](uint64_t i) const { return i >= lo && i < hi ? s[i - lo] : g[i]; }
+};
+__device__ __forceinline__ Txt stage(const uint8_t* g, uint64_t n, uint8_t* sw) {
+    const uint64_t c0 = (uint64_t)blockIdx.x * kChunk;
+    const uint64_t lo = c0 >= kHalo ? c0 - kHalo : 0, hi = min(n, c0 + kChunk + kHalo);
+    for (uint64_t k = threadIdx.x; 16 * k < hi - lo; k += blockDim.x) {
+        const uint64_t off = lo + 16 * k;
+        if (off + 16 <= hi && ((reinterpret_cast<uintptr_t>(g) + off) & 15) == 0) {
+            *reinterpret_cast<uint4*>(sw + 16 * k) = *reinterpret_cast<const uint4*>(g + off);
+        } else {
+            for (uint64_t b = off; b < off + 16 && b < hi; ++b) sw[b - lo] = g[b];
+        }
+    }
+    __syncthreads();
+    return Txt{g, sw, lo, hi};
+}
 static_assert(kPer * kThreads == (int)kChunk, "chunk = threads x bytes per thread");
 
 __device__ __forceinline__ bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
@@ -38,22 +63,32 @@ __device__ __forceinline__ Xfer compose(const Xfer& a, const Xfer& b) {
     return r;
 }
 // a '"' at i ends a string only after an even run of backslashes (ingest.hpp str())
-__device__ __forceinline__ bool escaped(const uint8_t* t, uint64_t i) {
+__device__ __forceinline__ bool escaped(const Txt& t, uint64_t i) {
     uint64_t k = 0;
     while (k < i && t[i - 1 - k] == '\\') ++k;
     return k & 1;
 }
-__device__ __forceinline__ Xfer byte_xfer(const uint8_t* t, uint64_t i) {
-    const uint8_t c = t[i];
+__device__ __forceinline__ Xfer byte_xfer(const Txt& t, uint64_t i, uint8_t c) {
     if (c == '"') return Xfer{1 | ((escaped(t, i) ? 1 : 0) << 1), 0, 0};
     if (c == '[' || c == '{') return Xfer{2, 1, 0};
     if (c == ']' || c == '}') return Xfer{2, -1, 0};
     return xid();
 }
-__device__ __forceinline__ Xfer thread_xfer(const uint8_t* t, uint64_t n, uint64_t b0) {
+// Four bytes of the text from i (4-aligned): one LDS read inside the staged
+// window (past the end: spaces).
+__device__ __forceinline__ uint32_t word_at(const Txt& t, uint64_t n, uint64_t i) {
+    if (i >= t.lo && i + 4 <= t.hi) return *reinterpret_cast<const uint32_t*>(t.s + (i - t.lo));
+    uint32_t x = 0;
+    for (int b = 0; b < 4; ++b) x |= (uint32_t)(i + b < n ? t[i + b] : ' ') << (8 * b);
+    return x;
+}
+__device__ __forceinline__ Xfer thread_xfer(const Txt& t, uint64_t n, uint64_t b0) {
     Xfer x = xid();
-    for (int k = 0; k < kPer; ++k)
-        if (b0 + k < n) x = compose(x, byte_xfer(t, b0 + k));
+    for (int wi = 0; wi < kPer / 4; ++wi) {
+        const uint32_t w = word_at(t, n, b0 + 4 * wi);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) x = compose(x, byte_xfer(t, b0 + 4 * wi + b, (uint8_t)(w >> (8 * b))));
+    }
     return x;
 }
 // block-wide exclusive scan (in order) of the threads' transfers
@@ -72,11 +107,13 @@ __device__ __forceinline__ Xfer block_excl(Xfer x, Xfer* sx) {
     return r;
 }
 
-__global__ __launch_bounds__(kThreads) void k_pass1(const uint8_t* __restrict__ t, uint64_t n,
+__global__ __launch_bounds__(kThreads) void k_pass1(const uint8_t* __restrict__ text, uint64_t n,
                                                     Xfer* __restrict__ cx) {
     __shared__ Xfer sx[kThreads];
+    __shared__ __attribute__((aligned(16))) uint8_t sw[kChunk + 2 * kHalo];
+    const Txt t = stage(text, n, sw);
     const uint64_t b0 = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kPer;
-    Xfer x = thread_xfer(t, n, b0);
+    const Xfer x = thread_xfer(t, n, b0);
     const Xfer pre = block_excl(x, sx);
     if (threadIdx.x == kThreads - 1) cx[blockIdx.x] = compose(pre, x);
 }
@@ -108,7 +145,7 @@ __global__ __launch_bounds__(1024) void k_scan1(const Xfer* __restrict__ cx, uin
 }
 
 // This thread's entry (state, depth) inside its chunk.
-__device__ __forceinline__ Entry thread_entry(const uint8_t* t, uint64_t n, const Entry* entry,
+__device__ __forceinline__ Entry thread_entry(const Txt& t, uint64_t n, const Entry* entry,
                                               Xfer* sx, uint64_t b0) {
     const Xfer pre = block_excl(thread_xfer(t, n, b0), sx);
     const Entry e = entry[blockIdx.x];
@@ -118,12 +155,10 @@ __device__ __forceinline__ Entry thread_entry(const uint8_t* t, uint64_t n, cons
 struct Kinds {
     bool num, row, key;
 };
-__device__ __forceinline__ Kinds kinds(const uint8_t* t, uint64_t i, int st, int dp) {
+__device__ __forceinline__ Kinds kinds(uint8_t c, uint8_t p, int st, int dp) {
     Kinds k{false, false, false};
     if (st) return k;
-    const uint8_t c = t[i];
     if (num_char(c)) {
-        const uint8_t p = i ? t[i - 1] : ' ';
         k.num = !num_char(p) && !is_alpha(p);         // (not the 'e' of true / false)
     } else if (c == '[') {
         k.row = dp == 2;
@@ -132,24 +167,33 @@ __device__ __forceinline__ Kinds kinds(const uint8_t* t, uint64_t i, int st, int
     }
     return k;
 }
-__device__ __forceinline__ void advance(const uint8_t* t, uint64_t i, int& st, int& dp) {
-    const Xfer x = byte_xfer(t, i);
+__device__ __forceinline__ void advance(const Txt& t, uint64_t i, uint8_t c, int& st, int& dp) {
+    const Xfer x = byte_xfer(t, i, c);
     dp += st ? x.d1 : x.d0;
     st = fstate(x, st);
 }
 
-__global__ __launch_bounds__(kThreads) void k_pass2(const uint8_t* __restrict__ t, uint64_t n,
+__global__ __launch_bounds__(kThreads) void k_pass2(const uint8_t* __restrict__ text, uint64_t n,
                                                     const Entry* __restrict__ entry,
                                                     Counts* __restrict__ cc) {
     __shared__ Xfer sx[kThreads];
     __shared__ uint32_t sn[kThreads], sr[kThreads], sk[kThreads];
+    __shared__ __attribute__((aligned(16))) uint8_t sw[kChunk + 2 * kHalo];
+    const Txt t = stage(text, n, sw);
     const uint64_t b0 = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kPer;
     Entry e = thread_entry(t, n, entry, sx, b0);
     uint32_t cn = 0, cr = 0, ck = 0;
-    for (int k = 0; k < kPer && b0 + k < n; ++k) {
-        const Kinds kd = kinds(t, b0 + k, e.state, e.depth);
-        cn += kd.num; cr += kd.row; ck += kd.key;
-        advance(t, b0 + k, e.state, e.depth);
+    uint8_t p = b0 ? t[b0 - 1] : ' ';
+    for (int wi = 0; wi < kPer / 4; ++wi) {
+        const uint32_t w = word_at(t, n, b0 + 4 * wi);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint8_t c = (uint8_t)(w >> (8 * b));
+            const Kinds kd = kinds(c, p, e.state, e.depth);
+            cn += kd.num; cr += kd.row; ck += kd.key;
+            advance(t, b0 + 4 * wi + b, c, e.state, e.depth);
+            p = c;
+        }
     }
     sn[threadIdx.x] = cn; sr[threadIdx.x] = cr; sk[threadIdx.x] = ck;
     __syncthreads();
@@ -189,7 +233,7 @@ __global__ __launch_bounds__(1024) void k_scan2(Counts* __restrict__ cc, uint32_
 }
 
 // The previous non-whitespace byte before i (0 at the start).
-__device__ __forceinline__ uint8_t prev_nonws(const uint8_t* t, uint64_t i, uint64_t* at = nullptr) {
+__device__ __forceinline__ uint8_t prev_nonws(const Txt& t, uint64_t i, uint64_t* at = nullptr) {
     while (i > 0) {
         const uint8_t c = t[--i];
         if (!is_ws(c)) {
@@ -202,7 +246,7 @@ __device__ __forceinline__ uint8_t prev_nonws(const uint8_t* t, uint64_t i, uint
 
 // One number token at i (ingest.hpp Parser::number, kParseSerde). Returns the
 // error code (0: ok) and the value.
-__device__ __forceinline__ uint32_t parse_number(const uint8_t* t, uint64_t n, uint64_t i,
+__device__ __forceinline__ uint32_t parse_number(const Txt& t, uint64_t n, uint64_t i,
                                                  const double* __restrict__ pow10, double* out,
                                                  uint64_t* end) {
     uint64_t p = i;
@@ -270,7 +314,7 @@ __device__ __forceinline__ uint32_t parse_number(const uint8_t* t, uint64_t n, u
 // host keeps when it lies inside m, u, v or d; unknown members may hold
 // anything). Object level (depth 0 / 1): the members' syntax (2: always an
 // error). 0: fine.
-__device__ __forceinline__ uint32_t struct_bad(const uint8_t* t, uint64_t i, int dp) {
+__device__ __forceinline__ uint32_t struct_bad(const Txt& t, uint64_t i, int dp) {
     const uint8_t c = t[i];
     if (is_ws(c)) return 0;
     const uint8_t p = prev_nonws(t, i);
@@ -295,7 +339,19 @@ __device__ __forceinline__ uint32_t struct_bad(const uint8_t* t, uint64_t i, int
     return 2;
 }
 
-__global__ __launch_bounds__(kThreads) void k_pass3(const uint8_t* __restrict__ t, uint64_t n,
+// Bytes of a walk that need a check against their neighbours: number tokens
+// (parse + separators) and structural bytes outside strings (struct_bad).
+__device__ __forceinline__ bool struct_candidate(uint8_t c, int dp) {
+    return !is_ws(c) && !(dp >= 2 && num_char(c));
+}
+__device__ __forceinline__ int8_t clamp_depth(int dp) { return (int8_t)max(-1, min(dp, 127)); }
+
+// Pass 3 walks each thread's bytes twice: counting, then writing row-open and
+// key positions and collecting the block's number tokens and structural bytes
+// (chunk offset, depth) in LDS in document order; the numbers are then parsed
+// and the structural bytes checked one item per thread (a per-byte walk would
+// run every thread's number parse on the whole wave).
+__global__ __launch_bounds__(kThreads) void k_pass3(const uint8_t* __restrict__ text, uint64_t n,
                                                     const Entry* __restrict__ entry,
                                                     const Counts* __restrict__ off,
                                                     const double* __restrict__ pow10,
@@ -304,61 +360,94 @@ __global__ __launch_bounds__(kThreads) void k_pass3(const uint8_t* __restrict__ 
                                                     uint64_t* __restrict__ rpos, uint64_t* __restrict__ kpos,
                                                     unsigned long long* __restrict__ err) {
     __shared__ Xfer sx[kThreads];
-    __shared__ uint32_t sn[kThreads], sr[kThreads], sk[kThreads];
-    const uint64_t b0 = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kPer;
+    __shared__ uint32_t sn[kThreads], sr[kThreads], sk[kThreads], ss[kThreads];
+    __shared__ __attribute__((aligned(16))) uint8_t sw[kChunk + 2 * kHalo];
+    // a number token takes >= 2 bytes with its separator: <= kChunk / 2 per chunk
+    __shared__ uint16_t lnum[kChunk / 2];
+    __shared__ int8_t lnd[kChunk / 2];
+    __shared__ uint16_t lst[kChunk];
+    __shared__ int8_t lsd[kChunk];
+    const Txt t = stage(text, n, sw);
+    const uint64_t c0 = (uint64_t)blockIdx.x * kChunk;
+    const uint64_t b0 = c0 + (uint64_t)threadIdx.x * kPer;
     const Entry e0 = thread_entry(t, n, entry, sx, b0);
-    // this thread's counts, then their exclusive scan within the block
+    const uint8_t p0 = b0 ? t[b0 - 1] : ' ';
     Entry e = e0;
-    uint32_t cn = 0, cr = 0, ck = 0;
-    for (int k = 0; k < kPer && b0 + k < n; ++k) {
-        const Kinds kd = kinds(t, b0 + k, e.state, e.depth);
-        cn += kd.num; cr += kd.row; ck += kd.key;
-        advance(t, b0 + k, e.state, e.depth);
+    uint32_t cn = 0, cr = 0, ck = 0, cs = 0;
+    uint8_t p = p0;
+    for (int wi = 0; wi < kPer / 4; ++wi) {
+        const uint32_t w = word_at(t, n, b0 + 4 * wi);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint64_t i = b0 + 4 * wi + b;
+            const uint8_t c = (uint8_t)(w >> (8 * b));
+            const Kinds kd = kinds(c, p, e.state, e.depth);
+            cn += kd.num; cr += kd.row; ck += kd.key;
+            cs += !e.state && i < n && struct_candidate(c, e.depth);
+            advance(t, i, c, e.state, e.depth);
+            p = c;
+        }
     }
-    sn[threadIdx.x] = cn; sr[threadIdx.x] = cr; sk[threadIdx.x] = ck;
+    sn[threadIdx.x] = cn; sr[threadIdx.x] = cr; sk[threadIdx.x] = ck; ss[threadIdx.x] = cs;
     __syncthreads();
     for (int s = 1; s < kThreads; s <<= 1) {
-        const uint32_t a = (int)threadIdx.x >= s ? sn[threadIdx.x - s] : 0u;
-        const uint32_t b = (int)threadIdx.x >= s ? sr[threadIdx.x - s] : 0u;
-        const uint32_t c = (int)threadIdx.x >= s ? sk[threadIdx.x - s] : 0u;
+        const bool on = (int)threadIdx.x >= s;
+        const uint32_t a = on ? sn[threadIdx.x - s] : 0u, b = on ? sr[threadIdx.x - s] : 0u,
+                       c = on ? sk[threadIdx.x - s] : 0u, d = on ? ss[threadIdx.x - s] : 0u;
         __syncthreads();
-        sn[threadIdx.x] += a; sr[threadIdx.x] += b; sk[threadIdx.x] += c;
+        sn[threadIdx.x] += a; sr[threadIdx.x] += b; sk[threadIdx.x] += c; ss[threadIdx.x] += d;
         __syncthreads();
     }
+    const uint32_t nb = sn[kThreads - 1], sb = ss[kThreads - 1];
     const Counts o = off[blockIdx.x];
-    uint32_t in = o.num + sn[threadIdx.x] - cn, ir = o.row + sr[threadIdx.x] - cr,
-             ik = o.key + sk[threadIdx.x] - ck;
+    uint32_t jn = sn[threadIdx.x] - cn, js = ss[threadIdx.x] - cs;
+    uint32_t ir = o.row + sr[threadIdx.x] - cr, ik = o.key + sk[threadIdx.x] - ck;
     e = e0;
-    for (int k = 0; k < kPer && b0 + k < n; ++k) {
-        const uint64_t i = b0 + k;
-        const Kinds kd = kinds(t, i, e.state, e.depth);
-        if (kd.num) {
-            double v = 0.0;
-            uint64_t end = i;
-            uint32_t code = parse_number(t, n, i, pow10, &v, &end);
-            if (!code && e.depth >= 2) {
-                // separators: after '[' or ',', before ',' or ']'
-                const uint8_t p = prev_nonws(t, i);
-                uint64_t q = end;
-                while (q < n && is_ws(t[q])) ++q;
-                const uint8_t nx = q < n ? t[q] : 0;
-                if (!(p == '[' || p == ',') || !(nx == ',' || nx == ']')) code = (uint32_t)kErrSeparator;
-            }
-            val[in] = v;
-            npos[in] = i;
-            ndepth[in] = (uint8_t)(code ? 0x80u | code : (uint32_t)min(e.depth, 127));
-            ++in;
+    p = p0;
+    for (int wi = 0; wi < kPer / 4; ++wi) {
+        const uint32_t w = word_at(t, n, b0 + 4 * wi);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint64_t i = b0 + 4 * wi + b;
+            const uint8_t c = (uint8_t)(w >> (8 * b));
+            const Kinds kd = kinds(c, p, e.state, e.depth);
+            if (kd.num) { lnum[jn] = (uint16_t)(i - c0); lnd[jn] = clamp_depth(e.depth); ++jn; }
+            if (kd.row) rpos[ir++] = i;
+            if (kd.key) kpos[ik++] = i;
+            if (!e.state && i < n && struct_candidate(c, e.depth)) { lst[js] = (uint16_t)(i - c0); lsd[js] = clamp_depth(e.depth); ++js; }
+            advance(t, i, c, e.state, e.depth);
+            p = c;
         }
-        if (kd.row) rpos[ir++] = i;
-        if (kd.key) kpos[ik++] = i;
-        const uint32_t bad = e.state ? 0u : struct_bad(t, i, e.depth);
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < nb; j += kThreads) {
+        const uint64_t i = c0 + lnum[j];
+        const int dp = lnd[j];
+        double v = 0.0;
+        uint64_t end = i;
+        uint32_t code = parse_number(t, n, i, pow10, &v, &end);
+        if (!code && dp >= 2) {
+            // separators: after '[' or ',', before ',' or ']'
+            const uint8_t p = prev_nonws(t, i);
+            uint64_t q = end;
+            while (q < n && is_ws(t[q])) ++q;
+            const uint8_t nx = q < n ? t[q] : 0;
+            if (!(p == '[' || p == ',') || !(nx == ',' || nx == ']')) code = (uint32_t)kErrSeparator;
+        }
+        const uint32_t at = o.num + j;
+        val[at] = v;
+        npos[at] = i;
+        ndepth[at] = (uint8_t)(code ? 0x80u | code : (uint32_t)max(dp, 0));
+    }
+    for (uint32_t j = threadIdx.x; j < sb; j += kThreads) {
+        const uint64_t i = c0 + lst[j];
+        const uint32_t bad = struct_bad(t, i, lsd[j]);
         if (bad) {
             // structural errors: position list (bit 63: object level, always an
             // error; else the host keeps those inside m, u, v, d)
             const unsigned long long slot = atomicAdd(err, 1ull);
             if (slot < 255) err[1 + slot] = i | (bad == 2 ? (1ull << 63) : 0ull);
         }
-        advance(t, i, e.state, e.depth);
     }
 }
 

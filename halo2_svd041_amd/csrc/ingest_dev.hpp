@@ -11,7 +11,7 @@
 
 namespace svdw_ingest_dev {
 
-static constexpr uint32_t kChunk = 2048;   // bytes per block (256 threads x 8)
+static constexpr uint32_t kChunk = 4096;   // bytes per block (256 threads x 16)
 // 2-state transfer of a byte range: f = the string state after the range for
 // entry state 0 (outside) / 1 (inside a string) as bits 0 / 1; d0 / d1 = the
 // bracket depth change for each entry state.
