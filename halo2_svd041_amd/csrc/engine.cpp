@@ -454,7 +454,7 @@ struct svdw_ctx {
     int gemm_kc = 1;                        // "gemm_kc": 64-k chunks per LDS round of the CRT GEMM (1 / 4;
                                             // 4 needs 64 KiB of LDS and starves beside the stage blocks)
     bool gemm_batched = false;              // this witness's products went out as one batch
-    int res_first = -1;                     // "res_first": cell stream waits for the residue planes
+    int res_first = 0;                      // "res_first": cell stream waits for the residue planes
                                             // (1), not (0), -1: on row-sharded ranks
     int gemm_batch = -1;                    // "gemm_batch": svd_witness's three products in one launch
                                             // (1), one by one (0), or -1: batched on row-sharded ranks

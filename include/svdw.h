@@ -246,13 +246,22 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   svdw_svd_witness: read on the device from the quantization's bit-length
  *   words, or 1: read back by the host first, the round-1 behaviour);
  *   "res_f64" 1 | 0 (svd_witness with inputs in HBM: the CRT residue planes of
- *   m, u, v built from the f64 inputs in one launch, or from the quantized cells).
+ *   m, u, v built from the f64 inputs in one launch, or from the quantized cells);
+ *   "stage_batch" 1 | 0 (independent stages share k_stage_multi launches: the
+ *   u / v bounds and u.d, the d checks and constant cells, verify_mul's one cells
+ *   and gamma powers, the is_equal rows; split automatically where a stage reads
+ *   cells a pending one writes); "gemm_batch" -1 | 0 | 1 (svd_witness's three
+ *   products in one GEMM and one combine launch: -1 on row-sharded contexts);
+ *   "gemm_kc" 1 | 4 (64-k chunks per LDS round of the CRT GEMM); "res_first"
+ *   0 | 1 | -1 (the cell stream waits for the residue planes; -1: on row-sharded
+ *   contexts; measured slower, kept for A/B).
  * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:
  *   phase 1 starts with the two ctx_gate constant cells [1, 0] that
  *   examples/svd_example.rs:183's rlc.load_rlc_cache(.., 1) appends as recalled
  *   from axiom-eth's RlcChip, parity unpinned; init_rand is then RLC cell 2).
  * Timing aids (NOT bit-identical, for A/B measurements only): "stage_probe"
- *   0 | 1 (skip the stage programs) | 2 (store a constant instead of cells);
+ *   0 | 1 (skip the stage programs) | 2 (store a constant instead of cells) |
+ *   3 (constant stores, no view loads either);
  *   "hold_us" 0 | us (svd_witness: the step's streams wait behind a kernel
  *   spinning that long, so the GPU schedule is measured without host gaps). */
 int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);
