@@ -495,6 +495,7 @@ struct svdw_ctx {
     // second stream: GEMMs overlap the HBM-bound stages; third: phase 1
     hipStream_t st2 = nullptr;
     hipStream_t st3 = nullptr;
+    hipStream_t st_cell = nullptr;          // the cell stream proper (st is swapped at times)
     bool overlap = true;
     struct PreGemm {
         uint64_t off;
@@ -646,7 +647,9 @@ struct ProfScope {
         if (!c->prof || c->dry) return;
         if (!c->prof_filter.empty() && name.compare(0, c->prof_filter.size(), c->prof_filter) != 0)
             return;
-        svdw_ctx::Rec r{name, bytes, ops, ev(c), ev(c)};
+        // launches on the cell stream (the phase-0 critical path of svd_witness)
+        // are tagged, so a bench can report their rate beside the all-stream average
+        svdw_ctx::Rec r{s == c->st_cell ? name + "@cell" : name, bytes, ops, ev(c), ev(c)};
         hipck(hipEventRecord(r.e0, s), "hipEventRecord");
         c->recs.push_back(r);
         idx = (long)c->recs.size() - 1;
@@ -2507,6 +2510,7 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
         if (!c->dry) {
             hipError_t e = hipSetDevice(p->device);
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
+            c->st_cell = c->st;
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipHostMalloc((void**)&c->hbits, 64 * sizeof(uint32_t),
                                                hipHostMallocDefault);
@@ -3450,6 +3454,7 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                     hipck(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
                 hipck(hipStreamDestroy(c->st), "hipStreamDestroy");
                 c->st = s;
+                c->st_cell = s;
             }
         } else if (n == "cu_split") {
             // Give the second stream (products, phase 1) `value` CUs of its own and
@@ -3483,6 +3488,7 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                 hipck(hipStreamDestroy(c->st), "hipStreamDestroy");
                 hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
                 c->st = s1;
+                c->st_cell = s1;
                 c->st2 = s2;
             }
         } else if (n == "phase1_overlap") {
