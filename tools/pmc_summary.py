@@ -62,6 +62,19 @@ def main():
         out["kernels"][k] = {"dispatches": n, "read_bytes_per_launch": round(fb),
                              "write_bytes_per_launch": round(wb),
                              "traffic_per_launch": round(fb + wb)}
+    # bench.py's event profiler aggregates every stage launch (k_stage and the
+    # batched k_stage_multi) under "k_stage": the same aggregate per launch here
+    parts = {k: v for k, v in out["kernels"].items() if k.startswith("k_stage")}
+    if len(parts) > 1:
+        n = sum(v["dispatches"] for v in parts.values())
+        rd = sum(v["read_bytes_per_launch"] * v["dispatches"] for v in parts.values())
+        wr = sum(v["write_bytes_per_launch"] * v["dispatches"] for v in parts.values())
+        if "k_stage" in out["kernels"]:
+            out["kernels"]["k_stage_single"] = out["kernels"].pop("k_stage")
+        out["kernels"]["k_stage"] = {"dispatches": n, "read_bytes_per_launch": round(rd / n),
+                                     "write_bytes_per_launch": round(wr / n),
+                                     "traffic_per_launch": round((rd + wr) / n),
+                                     "aggregate_of": sorted(parts)}
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
     for k, v in sorted(out["kernels"].items(), key=lambda kv: -kv[1]["traffic_per_launch"] * kv[1]["dispatches"]):
