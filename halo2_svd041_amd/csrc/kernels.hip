@@ -1181,26 +1181,25 @@ __device__ __forceinline__ int crt_nmod(uint32_t ba, uint32_t bb, uint32_t lk) {
 
 // Balanced residues of 4 consecutive-k elements (16-bit halves h of |x|, sign
 // neg) for moduli k < n, one u32 word (4 x int8) per plane at o[k * plane].
-// Moduli loop unrolled so the table loads are scalar and hoisted.
+// The table loads are per-modulus (scalar); s mod m uses mul_hi, no fp32 quotient.
 template <int NH>
 __device__ __forceinline__ void residues_emit(const uint32_t (&h)[4][8], const bool (&neg)[4],
                                               uint32_t* __restrict__ o, uint64_t plane, int n) {
     for (int k = 0; k < n; ++k) {
-        const int m = (int)c_crt_mod[k];
-        const float inv = c_crt_invf[k];
+        const uint32_t m = c_crt_mod[k], magic = c_crt_magic[k], bias = c_crt_bias[k];
         uint32_t word = 0;
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             uint32_t s = 0;
 #pragma unroll
             for (int j = 0; j < NH; ++j) s = __umul24(h[t][j], c_crt_pow16[k][j]) + s;   // < 2^27
-            // quotient from fp32 (off by at most one for m >= 71), 24-bit products
-            const int q = (int)((float)s * inv);
-            int r = (int)s - __mul24(q, m);
-            r += r < 0 ? m : 0;
-            r -= r >= m ? m : 0;
-            if (neg[t] && r) r = m - r;
-            if (2 * r >= m) r -= m;                            // balanced: [-128, 127]
+            // -x: bias - s (bias a multiple of m, >= 2^27), still < 2^28
+            s = neg[t] ? bias - s : s;
+            // s mod m: the quotient from mul_hi by ceil(2^32 / m) is exact or one
+            // too large (s < 2^28, m <= 256)
+            int r = (int)(s - __umulhi(s, magic) * m);
+            r += r < 0 ? (int)m : 0;
+            if (2 * r >= (int)m) r -= (int)m;                  // balanced: [-128, 127]
             word |= ((uint32_t)r & 0xffu) << (8 * t);
         }
         o[k * plane] = word;
