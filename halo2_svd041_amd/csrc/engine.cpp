@@ -536,6 +536,7 @@ struct svdw_ctx {
     };
     std::vector<Batch> batches;
     bool stage_batch = true;
+    bool stage_persist = false;             // "stage_persist": resident stage blocks walk the chunks
     // device ingest (svdw_parse_svd_input_device) scratch
     DBuf ing_x, ing_e, ing_c, ing_p10, ing_val, ing_npos, ing_nd, ing_rpos, ing_kpos, ing_err, ing_q;
 };
@@ -837,7 +838,12 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     }
     {
         ProfScope ps(c, c->st, std::string("k_stage:") + tag, bytes, 0);
-        hipck(launch_stage(a, c->st), "k_stage");
+        if (c->stage_persist && stage_multi_fits(a)) {
+            const StageArgs* one = &a;
+            hipck(launch_stage_multi(&one, 1, c->st, true), "k_stage");
+        } else {
+            hipck(launch_stage(a, c->st), "k_stage");
+        }
     }
 }
 // Issue a stream's pending batched stages (k_stage_multi; one program: k_stage).
@@ -854,7 +860,7 @@ static void flush_batch(svdw_ctx* c, hipStream_t s) {
         std::vector<svdw_ctx::Pending> progs;
         progs.swap(b.progs);                 // (cleared before launching: no re-entry)
         ProfScope pr(c, s, name, bytes, 0, true);
-        hipck(launch_stage_multi(ps.data(), (int)ps.size(), s), "k_stage_multi");
+        hipck(launch_stage_multi(ps.data(), (int)ps.size(), s, c->stage_persist), "k_stage_multi");
     }
 }
 // RAII: stage launches on the current stream between construction and end()
@@ -3509,6 +3515,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "res_first") {
             REQUIRE(value >= -1 && value <= 1, "res_first: -1 (auto), 0 or 1");
             c->res_first = (int)value;
+        } else if (n == "stage_persist") {
+            c->stage_persist = value != 0;
         } else if (n == "gemm_batch") {
             REQUIRE(value >= -1 && value <= 1, "gemm_batch: -1 (auto), 0 or 1");
             c->gemm_batch = (int)value;

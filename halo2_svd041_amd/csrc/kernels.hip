@@ -512,99 +512,161 @@ __device__ __forceinline__ void element_program(const StageArgs& a, uint32_t e, 
     }
     }
 
-// One block of a stage: `a` supplies the scalar fields and the views (StageArgs
-// up to `mo`), the tables come from mo / adv / lk / K (the by-value kernel
-// argument of k_stage, or a record of a k_stage_multi batch); blk is the
-// block's index within the stage.
-__device__ __forceinline__ void stage_block(const StageArgs& a, const MicroOp* __restrict__ mo,
-                                            const SlotOp* __restrict__ adv,
-                                            const SlotOp* __restrict__ lk, const Fr* __restrict__ K,
-                                            uint32_t blk) {
+// LDS carve of a stage block (the same for every block of a program):
+// constants | element values | slot ops | micro-ops | views | half descriptors.
+struct StageLds {
+    uint32_t* sK;
+    uint32_t* sV;
+    SlotOp* sAdv;
+    SlotOp* sLk;
+    MicroOp* sMo;
+    DView* sVw;
+    uint4* sHM;
+    uint32_t* sHD;
+};
+__device__ __forceinline__ StageLds stage_lds(const StageArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    const uint32_t nv = a.nv;
-    uint32_t* sK = smem;
-    uint32_t* sV = sK + kMaxK * VW;
+    StageLds L;
+    L.sK = smem;
+    L.sV = L.sK + kMaxK * VW;
     const uint32_t E = a.E ? a.E : kStageElems;
-    SlotOp* sAdv = reinterpret_cast<SlotOp*>(sV + E * stage_elem_words(nv));
-    SlotOp* sLk = sAdv + kMaxAdv;
-    MicroOp* sMo = reinterpret_cast<MicroOp*>(sLk + kMaxLk);
-    DView* sVw = reinterpret_cast<DView*>(sMo + kMaxMicro);
+    L.sAdv = reinterpret_cast<SlotOp*>(L.sV + E * stage_elem_words(a.nv));
+    L.sLk = L.sAdv + kMaxAdv;
+    L.sMo = reinterpret_cast<MicroOp*>(L.sLk + kMaxLk);
+    L.sVw = reinterpret_cast<DView*>(L.sMo + kMaxMicro);
     // (stage_lds_bytes counts 48 B per view, >= sizeof(DView) + the alignment slack)
     static_assert(sizeof(DView) <= 40, "DView grew: recheck stage_lds_bytes");
     // (word offsets from smem, not integer casts: a cast pointer would lose its
     // LDS address space and every table read would become a flat load)
-    const uint32_t hm_off = ((uint32_t)(reinterpret_cast<uint32_t*>(sVw + kMaxViews) - smem) + 3u) & ~3u;
-    uint4* sHM = reinterpret_cast<uint4*>(smem + hm_off);
-    uint32_t* sHD = reinterpret_cast<uint32_t*>(sHM + 2 * (a.C + a.L));
-
+    const uint32_t hm_off = ((uint32_t)(reinterpret_cast<uint32_t*>(L.sVw + kMaxViews) - smem) + 3u) & ~3u;
+    L.sHM = reinterpret_cast<uint4*>(smem + hm_off);
+    L.sHD = reinterpret_cast<uint32_t*>(L.sHM + 2 * (a.C + a.L));
+    return L;
+}
+// A block's tables: constants, slot ops, micro-ops, views and the per (slot,
+// half) descriptors and masks (no barrier).
+__device__ __forceinline__ void stage_setup(const StageArgs& a, const StageLds& L,
+                                            const MicroOp* __restrict__ mo, const SlotOp* __restrict__ adv,
+                                            const SlotOp* __restrict__ lk, const Fr* __restrict__ K) {
     const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < a.nk; k += blockDim.x) lds_put(L.sK + k * VW, K[k]);
+    for (uint32_t k = tid; k < a.C; k += blockDim.x) L.sAdv[k] = adv[k];
+    for (uint32_t k = tid; k < a.L; k += blockDim.x) L.sLk[k] = lk[k];
+    for (uint32_t k = tid; k < a.nmo; k += blockDim.x) L.sMo[k] = mo[k];
+    if (tid < kMaxViews) L.sVw[tid] = a.view[tid];
+    for (uint32_t k = tid; k < 2 * (a.C + a.L); k += blockDim.x) {
+        const uint32_t sl = k >> 1;
+        make_half(sl < a.C ? adv[sl] : lk[sl - a.C], k & 1, L.sHD + k, L.sHM + k);
+    }
+}
+// This thread's in-bounds strided view loads of block blk's element.
+struct Prefetch {
+    Fr v0, v1;
+    bool in0, in1;
+};
+__device__ __forceinline__ Prefetch stage_loads(const StageArgs& a, uint32_t blk) {
+    const uint32_t E = a.E ? a.E : kStageElems;
     const uint32_t e0 = a.e_begin + blk * E;
-    const uint32_t ne = min(E, a.e_end - e0), e = e0 + tid;
-
-    // Issue this thread's in-bounds strided view loads before the LDS set-up,
-    // so their latency overlaps it (phase A falls back to view_load otherwise).
-    Fr pf0 = fr_zero(), pf1 = fr_zero();
-    bool in0 = false, in1 = false;
-    if (tid < ne && !(a.flags & STAGE_PROBE_NOLD)) {
+    const uint32_t ne = min(E, a.e_end - e0), e = e0 + threadIdx.x;
+    Prefetch f{fr_zero(), fr_zero(), false, false};
+    if (threadIdx.x < ne && !(a.flags & STAGE_PROBE_NOLD)) {
         const uint32_t pi = e / a.cols, pj = e - pi * a.cols;
         const DView& v0 = a.view[0];
         if (v0.ptr && v0.mode == VIEW_STRIDED && pi < v0.rows && pj < v0.cols) {
-            pf0 = ld_fr(v0.ptr + (int64_t)pi * v0.rs + (int64_t)pj * v0.cs);
-            in0 = true;
+            f.v0 = ld_fr(v0.ptr + (int64_t)pi * v0.rs + (int64_t)pj * v0.cs);
+            f.in0 = true;
         }
         const DView& v1 = a.view[1];
         if (v1.ptr && v1.mode == VIEW_STRIDED && pi < v1.rows && pj < v1.cols) {
-            pf1 = ld_fr(v1.ptr + (int64_t)pi * v1.rs + (int64_t)pj * v1.cs);
-            in1 = true;
+            f.v1 = ld_fr(v1.ptr + (int64_t)pi * v1.rs + (int64_t)pj * v1.cs);
+            f.in1 = true;
         }
     }
-
-    for (uint32_t k = tid; k < a.nk; k += blockDim.x) lds_put(sK + k * VW, K[k]);
-    for (uint32_t k = tid; k < a.C; k += blockDim.x) sAdv[k] = adv[k];
-    for (uint32_t k = tid; k < a.L; k += blockDim.x) sLk[k] = lk[k];
-    for (uint32_t k = tid; k < a.nmo; k += blockDim.x) sMo[k] = mo[k];
-    if (tid < kMaxViews) sVw[tid] = a.view[tid];
-    for (uint32_t k = tid; k < 2 * (a.C + a.L); k += blockDim.x) {
-        const uint32_t sl = k >> 1;
-        make_half(sl < a.C ? adv[sl] : lk[sl - a.C], k & 1, sHD + k, sHM + k);
-    }
-    __syncthreads();
-
+    return f;
+}
+// Phase A and phase B of block blk (tables set up; one barrier in between).
+__device__ __forceinline__ void stage_chunk(const StageArgs& a, const StageLds& L, uint32_t blk,
+                                            const Prefetch& f) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    const uint32_t nv = a.nv, tid = threadIdx.x;
+    const uint32_t E = a.E ? a.E : kStageElems;
+    const uint32_t e0 = a.e_begin + blk * E;
+    const uint32_t ne = min(E, a.e_end - e0), e = e0 + tid;
     // ---- phase A: per-element micro-ops (constants / ops / views read from LDS:
     // dynamic indexing into the by-value kernel argument would go to scratch)
     if (tid < ne && !(a.flags & (STAGE_PROBE_NOA | STAGE_PROBE_CONST)))
-        element_program(a, e, sV + tid * stage_elem_words(nv), sK, sMo, sVw, pf0, in0, pf1, in1);
+        element_program(a, e, L.sV + tid * stage_elem_words(nv), L.sK, L.sMo, L.sVw, f.v0, f.in0, f.v1, f.in1);
     __syncthreads();
 
     // ---- phase B: advice cells, then lookup cells
     uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
     uint4* outL = a.L ? reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L) : nullptr;
     if (a.flags & STAGE_PROBE_CONST) {
-        const uint4 z = make_uint4(pf0.w[0] ^ pf1.w[0], 0, 0, 0);
+        const uint4 z = make_uint4(f.v0.w[0] ^ f.v1.w[0], 0, 0, 0);
         for (uint32_t hc = tid; hc < 2 * ne * a.C; hc += blockDim.x) outA[hc] = z;
         if (a.L)
             for (uint32_t hc = tid; hc < 2 * ne * a.L; hc += blockDim.x) outL[hc] = z;
     } else if (a.flags & STAGE_INC) {
-        stream_cells_inc<true>(outA, 2 * ne * a.C, sAdv, a.C, a.cdiv_magic, sK, sV, nv);
-        if (a.L) stream_cells_inc<true>(outL, 2 * ne * a.L, sLk, a.L, a.ldiv_magic, sK, sV, nv);
+        stream_cells_inc<true>(outA, 2 * ne * a.C, L.sAdv, a.C, a.cdiv_magic, L.sK, L.sV, nv);
+        if (a.L) stream_cells_inc<true>(outL, 2 * ne * a.L, L.sLk, a.L, a.ldiv_magic, L.sK, L.sV, nv);
     } else {
-        const uint32_t vb0 = (uint32_t)(sV - smem);
+        const uint32_t vb0 = (uint32_t)(L.sV - smem);
         if (a.flags & STAGE_ALIGN) {
-            stream_cells_desc<true>(outA, 2 * ne * a.C, sHD, sHM, a.C, a.cdiv_magic, smem, vb0, nv);
+            stream_cells_desc<true>(outA, 2 * ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv);
             if (a.L)
-                stream_cells_desc<true>(outL, 2 * ne * a.L, sHD + 2 * a.C, sHM + 2 * a.C, a.L,
+                stream_cells_desc<true>(outL, 2 * ne * a.L, L.sHD + 2 * a.C, L.sHM + 2 * a.C, a.L,
                                         a.ldiv_magic, smem, vb0, nv);
         } else {
-            stream_cells_desc<false>(outA, 2 * ne * a.C, sHD, sHM, a.C, a.cdiv_magic, smem, vb0, nv);
+            stream_cells_desc<false>(outA, 2 * ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv);
             if (a.L)
-                stream_cells_desc<false>(outL, 2 * ne * a.L, sHD + 2 * a.C, sHM + 2 * a.C, a.L,
+                stream_cells_desc<false>(outL, 2 * ne * a.L, L.sHD + 2 * a.C, L.sHM + 2 * a.C, a.L,
                                          a.ldiv_magic, smem, vb0, nv);
         }
     }
 }
 
+// One block of a stage: `a` supplies the scalar fields and the views (StageArgs
+// up to `mo`), the tables come from mo / adv / lk / K (the by-value kernel
+// argument of k_stage, or a record of a k_stage_multi batch); blk is the
+// block's index within the stage. The view loads are issued before the table
+// set-up so their latency overlaps it.
+__device__ __forceinline__ void stage_block(const StageArgs& a, const MicroOp* __restrict__ mo,
+                                            const SlotOp* __restrict__ adv,
+                                            const SlotOp* __restrict__ lk, const Fr* __restrict__ K,
+                                            uint32_t blk) {
+    const StageLds L = stage_lds(a);
+    const Prefetch f = stage_loads(a, blk);
+    stage_setup(a, L, mo, adv, lk, K);
+    __syncthreads();
+    stage_chunk(a, L, blk, f);
+}
+
 __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
     stage_block(a, a.mo, a.adv, a.lk, a.K, blockIdx.x);
+}
+
+// the program of batch block g (m.blk0 ascending)
+__device__ __forceinline__ uint32_t multi_prog(const StageMulti& m, uint32_t g) {
+    uint32_t p = 0;
+    for (uint32_t k = 1; k < m.nprog; ++k) p += g >= m.blk0[k];
+    return p;
+}
+struct Rec {
+    const StageArgs* a;
+    const MicroOp* mo;
+    const SlotOp* adv;
+    const SlotOp* lk;
+    const Fr* K;
+};
+__device__ __forceinline__ Rec multi_rec(const StageMulti& m, uint32_t p) {
+    const uint8_t* r = m.data + m.off[p];
+    Rec q;
+    q.a = reinterpret_cast<const StageArgs*>(r);                     // fields up to `mo` only
+    q.mo = reinterpret_cast<const MicroOp*>(r + kRecHead);
+    q.adv = reinterpret_cast<const SlotOp*>(q.mo + q.a->nmo);
+    q.lk = q.adv + q.a->C;
+    q.K = reinterpret_cast<const Fr*>(q.lk + q.a->L);
+    return q;
 }
 
 // Several independent stages in one launch (k_stage_multi): block b runs block
@@ -613,15 +675,30 @@ __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
 // gamma powers, is_equal rows, ...) and the phase-0 stages that read only the
 // loaded matrices share one launch (one tail, one dispatch).
 __global__ __launch_bounds__(256) void k_stage_multi(const StageMulti m) {
-    uint32_t p = 0;
-    for (uint32_t k = 1; k < m.nprog; ++k) p += blockIdx.x >= m.blk0[k];
-    const uint8_t* r = m.data + m.off[p];
-    const StageArgs& a = *reinterpret_cast<const StageArgs*>(r);      // fields up to `mo` only
-    const MicroOp* mo = reinterpret_cast<const MicroOp*>(r + kRecHead);
-    const SlotOp* adv = reinterpret_cast<const SlotOp*>(mo + a.nmo);
-    const SlotOp* lk = adv + a.C;
-    const Fr* K = reinterpret_cast<const Fr*>(lk + a.L);
-    stage_block(a, mo, adv, lk, K, blockIdx.x - m.blk0[p]);
+    const uint32_t p = multi_prog(m, blockIdx.x);
+    const Rec q = multi_rec(m, p);
+    stage_block(*q.a, q.mo, q.adv, q.lk, q.K, blockIdx.x - m.blk0[p]);
+}
+// Persistent form ("stage_persist"): a grid of resident blocks walks the batch's
+// blocks round-robin (g = blockIdx.x, + gridDim.x, ...: the same write front as
+// one block per chunk) and sets its tables up only when the program changes,
+// instead of once per 256 elements.
+__global__ __launch_bounds__(256) void k_stage_multi_p(const StageMulti m) {
+    const uint32_t total = m.blk0[m.nprog];
+    uint32_t cur = ~0u;
+    for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
+        const uint32_t p = multi_prog(m, g);
+        const Rec q = multi_rec(m, p);
+        const StageLds L = stage_lds(*q.a);
+        const Prefetch f = stage_loads(*q.a, g - m.blk0[p]);
+        if (p != cur) {
+            stage_setup(*q.a, L, q.mo, q.adv, q.lk, q.K);
+            cur = p;
+        }
+        __syncthreads();                    // tables ready; the previous chunk's phase B done
+        stage_chunk(*q.a, L, g - m.blk0[p], f);
+        __syncthreads();                    // phase B done before the next phase A / set-up
+    }
 }
 
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
@@ -637,7 +714,25 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
 bool stage_multi_fits(const StageArgs& a) {
     return stage_record_bytes(a.nmo, a.C, a.L, a.nk) <= kMultiBytes && (a.E ? a.E : kStageElems) <= kStageElems;
 }
-hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st) {
+// resident k_stage_multi_p blocks for `lds` bytes of dynamic LDS (cached)
+static uint32_t persist_grid(uint32_t lds) {
+    static uint32_t cu = 0;
+    static uint32_t last_lds = ~0u, last = 0;
+    if (!cu) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+        cu = (uint32_t)prop.multiProcessorCount;
+    }
+    if (lds != last_lds) {
+        int nb = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_stage_multi_p, 256, lds) != hipSuccess) return 0;
+        last_lds = lds;
+        last = (uint32_t)std::max(nb, 1) * cu;
+    }
+    return last;
+}
+hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st, bool persist) {
     StageMulti m;
     uint32_t used = 0, blocks = 0, lds = 0;
     m.nprog = 0;
@@ -645,7 +740,12 @@ hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t 
     // launch what is packed (a single program as a plain k_stage launch)
     auto flush = [&]() -> hipError_t {
         hipError_t e = hipSuccess;
-        if (m.nprog == 1) {
+        const uint32_t pg = persist && m.nprog ? persist_grid(lds) : 0;
+        if (pg && blocks > pg) {
+            m.blk0[m.nprog] = blocks;
+            hipLaunchKernelGGL(k_stage_multi_p, dim3(pg), dim3(256), lds, st, m);
+            e = hipGetLastError();
+        } else if (m.nprog == 1) {
             e = launch_stage(*single, st);
         } else if (m.nprog > 1) {
             m.blk0[m.nprog] = blocks;

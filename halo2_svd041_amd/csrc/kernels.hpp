@@ -168,7 +168,9 @@ static constexpr uint32_t kMaxBitBlocks = 2048;
 hipError_t launch_stage(const StageArgs& a, hipStream_t st);
 // Independent stages (no stage reads another's cells) in as few k_stage_multi
 // launches as their records fit (stage_record_bytes, kMultiBytes); n >= 1.
-hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st);
+// persist: a resident grid walks the blocks (k_stage_multi_p) when there are
+// more blocks than fit at once.
+hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st, bool persist = false);
 // does the record of `a` fit one k_stage_multi launch?
 bool stage_multi_fits(const StageArgs& a);
 // max over the view of bit-length(|signed(x)|): out[b] = max of block b

@@ -173,7 +173,10 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                                   {"stage_align": 0}, {"stage_align": 0, "stage_elems": 64},
                                   {"overlap": 0}, {"stage_inc": 1}, {"stage_priority": 1},
                                   {"gemm_priority": 1}, {"cu_split": 64}, {"fused_quantize": 0}, {"d_checks_aside": 0},
-                                  {"scan_na_host": 1}, {"scan_impl": 5, "phase1_overlap": 2}])
+                                  {"scan_na_host": 1}, {"scan_impl": 5, "phase1_overlap": 2},
+                                  {"stage_batch": 0}, {"gemm_batch": 1}, {"gemm_kc": 4},
+                                  {"gemm_batch": 1, "gemm_kc": 4}, {"res_first": 1}, {"stage_persist": 1},
+                                  {"stage_persist": 1, "stage_batch": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
@@ -546,3 +549,24 @@ def test_field_mat_times_vec_parity(gpu_ctx_factory, N, M, LB, seed):
     f64 = A @ v1
     for i in range(N):
         assert abs(po.to_signed(oq[i].value) / 2.0 ** P - f64[i]) <= 1e-6 * max(1.0, abs(f64[i]))
+
+
+@pytest.mark.parametrize("shape,P", [((512, 384), 32), ((300, 700), 63)])
+def test_persistent_stages_match_default(gpu_ctx_factory, shape, P):
+    """stage_persist: resident blocks walking the chunks (k_stage_multi_p, used
+    once a stage has more blocks than fit at once) give the default witness
+    bit for bit, batched and unbatched."""
+    import halo2_svd041_amd as hs
+    N, M = shape
+    m, u, d, v = gen_svd_input(N, M, seed=21)
+    g = gamma_for(21)
+    ref = gpu_ctx_factory(P)
+    hs.svd_witness(ref, m, u, v, d, g)
+    want = [ref.advice(0), ref.lookups(0), ref.advice(1)]
+    for batch in (1, 0):
+        ctx = gpu_ctx_factory(P)
+        ctx.set_option("stage_persist", 1)
+        ctx.set_option("stage_batch", batch)
+        hs.svd_witness(ctx, m, u, v, d, g)
+        for w, got in zip(want, [ctx.advice(0), ctx.lookups(0), ctx.advice(1)]):
+            assert np.array_equal(w, got)
