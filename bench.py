@@ -459,7 +459,15 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.SUM)
             vals = t.tolist()
         check = {k: int(x) for k, x in zip(keys, vals)}
-        check["ok"] = check["gate_failures"] + check["copy_failures"] + check["lookup_failures"] == 0
+        bad = check["gate_failures"] + check["copy_failures"] + check["lookup_failures"]
+        if not rows_mode:
+            # every copy-constraint (equality) record, generated and checked on the
+            # device (svdw_check_equalities): scan operands and constants included
+            eq = [ctx.check_equalities(ph) for ph in (0, 1)]
+            for k in ("copies_checked", "copy_failures", "consts_checked", "const_failures"):
+                check["equality_" + k] = sum(int(x[k]) for x in eq)
+            bad += check["equality_copy_failures"] + check["equality_const_failures"]
+        check["ok"] = bad == 0
 
     elapsed, cells_all = reduce_over_ranks(elapsed, cells_step, dist, red_dev)
     if rows_mode:

@@ -539,6 +539,8 @@ struct svdw_ctx {
     bool stage_persist = false;             // "stage_persist": resident stage blocks walk the chunks
     // device ingest (svdw_parse_svd_input_device) scratch
     DBuf ing_x, ing_e, ing_c, ing_p10, ing_val, ing_npos, ing_nd, ing_rpos, ing_kpos, ing_err, ing_q;
+    // device equality records (eq_gen_device)
+    DBuf eq_cp, eq_ks, eq_reg, eq_w, eq_k, eq_err, eq_st;
 };
 
 static void flush_batch(svdw_ctx* c, hipStream_t s);
@@ -2483,6 +2485,83 @@ static void eq_lists(const svdw_ctx* c, uint32_t phase, std::vector<uint64_t>* c
         }
     }
 }
+// The same records generated on the device (k_eq_records) into c->eq_cp /
+// c->eq_ks: per region its record counts are closed-form (elements x copy /
+// constant words, or rows x 2L copies + rows constants for a scan), so every
+// work item writes at a fixed offset and the order is eq_lists' order.
+static EqSrcDev eqsrc_dev(const RegionChecks::EqSrc& e) {
+    EqSrcDev d;
+    memset(&d, 0, sizeof d);
+    d.kind = e.kind; d.phase = (int32_t)e.phase; d.pad_phase = e.pad_phase; d.diag_phase = e.diag_phase;
+    d.first_phase = (int32_t)e.first_phase; d.off = e.off; d.pad_off = e.pad_off; d.diag_off = e.diag_off;
+    d.first = e.first; d.rs = e.rs; d.cs = e.cs; d.rows = e.rows; d.cols = e.cols;
+    return d;
+}
+static void eq_gen_device(svdw_ctx* c, uint32_t phase, uint64_t* n_copies, uint64_t* n_consts) {
+    std::vector<EqRegionDev> regs;
+    std::vector<uint32_t> words;
+    std::vector<Fr> konst;
+    uint64_t items = 0, nc = 0, nk = 0;
+    for (size_t k = 0; k < c->layout.size(); ++k) {
+        const svdw_region& r = c->layout[k];
+        const RegionChecks& rc = c->layout_chk[k];
+        if (r.phase != phase || !r.n) continue;
+        EqRegionDev d;
+        memset(&d, 0, sizeof d);
+        d.off = r.off;
+        d.item0 = items;
+        d.copy0 = nc;
+        d.const0 = nk;
+        d.src[0] = eqsrc_dev(rc.esrc[0]);
+        d.src[1] = eqsrc_dev(rc.esrc[1]);
+        if (rc.scan) {
+            const uint64_t R = r.rows, unit = r.n / R, L = (unit - 1) / 3;
+            REQUIRE(L >= 1, "internal: empty scan rows");
+            d.scan = 1; d.unit = (uint32_t)unit; d.L = (uint32_t)L;
+            d.nitems = R * L;
+            nc += R * 2 * L;
+            nk += R;
+        } else {
+            if (rc.eq.empty() || !rc.unit) continue;
+            const uint64_t nel = r.n / rc.unit;
+            d.unit = rc.unit;
+            d.cols = rc.cols ? rc.cols : 1;
+            d.w0 = (uint32_t)words.size();
+            d.nw = (uint32_t)rc.eq.size();
+            d.k0 = (uint32_t)konst.size();
+            for (uint32_t w : rc.eq) (eq_kind(w) == EQ_CONST ? d.nkw : d.ncw) += 1;
+            words.insert(words.end(), rc.eq.begin(), rc.eq.end());
+            konst.insert(konst.end(), rc.eqk.begin(), rc.eqk.end());
+            d.nitems = nel;
+            nc += nel * d.ncw;
+            nk += nel * d.nkw;
+        }
+        items += d.nitems;
+        regs.push_back(d);
+    }
+    *n_copies = nc;
+    *n_consts = nk;
+    ensure_buf(c, c->eq_cp, std::max<uint64_t>(nc, 1) * 16);
+    ensure_buf(c, c->eq_ks, std::max<uint64_t>(nk, 1) * 40);
+    ensure_buf(c, c->eq_reg, std::max<size_t>(regs.size(), 1) * sizeof(EqRegionDev));
+    ensure_buf(c, c->eq_w, std::max<size_t>(words.size(), 1) * 4);
+    ensure_buf(c, c->eq_k, std::max<size_t>(konst.size(), 1) * sizeof(Fr));
+    ensure_buf(c, c->eq_err, 4);
+    hipStream_t s = c->st;
+    if (!regs.empty())
+        hipck(hipMemcpyAsync(c->eq_reg.p, regs.data(), regs.size() * sizeof(EqRegionDev), hipMemcpyHostToDevice, s), "H2D");
+    if (!words.empty()) hipck(hipMemcpyAsync(c->eq_w.p, words.data(), words.size() * 4, hipMemcpyHostToDevice, s), "H2D");
+    if (!konst.empty())
+        hipck(hipMemcpyAsync(c->eq_k.p, konst.data(), konst.size() * sizeof(Fr), hipMemcpyHostToDevice, s), "H2D");
+    hipck(hipMemsetAsync(c->eq_err.p, 0, 4, s), "memset");
+    hipck(launch_eq_records((const EqRegionDev*)c->eq_reg.p, (uint32_t)regs.size(), items, (const uint32_t*)c->eq_w.p,
+                            (const Fr*)c->eq_k.p, phase, c->ext_off, (uint64_t*)c->eq_cp.p, (uint64_t*)c->eq_ks.p,
+                            (unsigned*)c->eq_err.p, s), "k_eq_records");
+    unsigned err = 0;
+    hipck(hipMemcpyAsync(&err, c->eq_err.p, 4, hipMemcpyDeviceToHost, s), "D2H");
+    hipck(hipStreamSynchronize(s), "hipStreamSynchronize");
+    REQUIRE(!err, "svdw_equalities: a region's copy source is not in the cell streams");
+}
 // virtual cell -> column-major physical index (the first placement of a break cell)
 static uint64_t phys_index(const svdw_ctx* c, uint32_t phase, uint64_t v) {
     const auto& st = c->phys.start[phase];
@@ -3324,6 +3403,16 @@ int svdw_equalities(const svdw_ctx* c, uint32_t phase, uint64_t* copies, uint64_
                     uint64_t* n_copies, uint64_t* consts, uint64_t consts_cap, uint64_t* n_consts) {
     return guarded([&] {
         REQUIRE(c && phase < 2 && n_copies && n_consts, "bad argument");
+        if (!c->dry) {                       // generated on the device, copied out up to the caps
+            svdw_ctx* m = const_cast<svdw_ctx*>(c);
+            sync(m);
+            eq_gen_device(m, phase, n_copies, n_consts);
+            if (copies && copies_cap)
+                hipck(hipMemcpy(copies, m->eq_cp.p, std::min(copies_cap, *n_copies) * 16, hipMemcpyDeviceToHost), "D2H");
+            if (consts && consts_cap)
+                hipck(hipMemcpy(consts, m->eq_ks.p, std::min(consts_cap, *n_consts) * 40, hipMemcpyDeviceToHost), "D2H");
+            return;
+        }
         std::vector<uint64_t> cp, cs;
         eq_lists(c, phase, &cp, &cs);
         *n_copies = cp.size() / 2;
@@ -3342,40 +3431,29 @@ int svdw_check_equalities(svdw_ctx* c, uint32_t phase, const void* columns0, con
                 "svdw_check_equalities: physical columns need svdw_physical_layout and phase 0's "
                 "columns (and phase 1's for phase 1)");
         memset(out, 0, sizeof *out);
-        std::vector<uint64_t> cp, cs;
-        eq_lists(c, phase, &cp, &cs);
-        if (phys) {
-            for (size_t i = 0; i < cp.size(); i += 2) {
-                const uint32_t sp = (uint32_t)(cp[i] >> 62);
-                if (sp < 2) cp[i] = phys_index(c, sp, cp[i] & ((1ull << 62) - 1)) | (uint64_t)sp << 62;
-                cp[i + 1] = phys_index(c, phase, cp[i + 1]);
-            }
-            for (size_t i = 0; i < cs.size(); i += 5) cs[i] = phys_index(c, phase, cs[i]);
+        sync(c);
+        uint64_t nc = 0, nk = 0;
+        eq_gen_device(c, phase, &nc, &nk);
+        if (phys) {                          // records onto the assigned columns
+            const auto& s0 = c->phys.start[0];
+            const auto& s1 = c->phys.start[1];
+            ensure_buf(c, c->eq_st, (s0.size() + s1.size() + 1) * sizeof(uint64_t));
+            uint64_t* st = (uint64_t*)c->eq_st.p;
+            if (!s0.empty()) hipck(hipMemcpyAsync(st, s0.data(), s0.size() * 8, hipMemcpyHostToDevice, c->st), "H2D");
+            if (!s1.empty())
+                hipck(hipMemcpyAsync(st + s0.size(), s1.data(), s1.size() * 8, hipMemcpyHostToDevice, c->st), "H2D");
+            hipck(launch_eq_phys((uint64_t*)c->eq_cp.p, nc, (uint64_t*)c->eq_ks.p, nk, st, (uint32_t)s0.size(),
+                                 st + s0.size(), (uint32_t)s1.size(), phase, c->phys.k, c->st), "k_eq_phys");
         }
         const Fr* s0 = phys ? (const Fr*)columns0 : c->ph[0].adv;
         const Fr* s1 = phys ? (const Fr*)columns1 : c->ph[1].adv;
         const Fr* dst = phase ? s1 : s0;
-        sync(c);
         ensure_buf(c, c->chk, 6 * sizeof(unsigned long long));
         unsigned long long* cnt = (unsigned long long*)c->chk.p;
         hipck(hipMemsetAsync(cnt, 0, 6 * sizeof(unsigned long long), c->st), "hipMemsetAsync");
-        // upload in chunks through chkg (stream-ordered; the buffer is reused)
-        const size_t chunk = (size_t)1 << 22;
-        for (size_t i = 0; i < cp.size(); i += 2 * chunk) {
-            const size_t n = std::min(chunk, (cp.size() - i) / 2);
-            ensure_buf(c, c->chkg, n * 16);
-            hipck(hipMemcpyAsync(c->chkg.p, cp.data() + i, n * 16, hipMemcpyHostToDevice, c->st), "H2D");
-            hipck(launch_check_copies(s0, s1, dst, (const uint64_t*)c->chkg.p, n, c->ext_gamma, cnt,
-                                      c->st), "k_check_copies");
-            hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
-        }
-        for (size_t i = 0; i < cs.size(); i += 5 * chunk) {
-            const size_t n = std::min(chunk, (cs.size() - i) / 5);
-            ensure_buf(c, c->chkg, n * 40);
-            hipck(hipMemcpyAsync(c->chkg.p, cs.data() + i, n * 40, hipMemcpyHostToDevice, c->st), "H2D");
-            hipck(launch_check_consts(dst, (const uint64_t*)c->chkg.p, n, cnt + 2, c->st), "k_check_consts");
-            hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
-        }
+        hipck(launch_check_copies(s0, s1, dst, (const uint64_t*)c->eq_cp.p, nc, c->ext_gamma, cnt, c->st),
+              "k_check_copies");
+        hipck(launch_check_consts(dst, (const uint64_t*)c->eq_ks.p, nk, cnt + 2, c->st), "k_check_consts");
         unsigned long long h[4];
         hipck(hipMemcpyAsync(h, cnt, sizeof h, hipMemcpyDeviceToHost, c->st), "D2H");
         hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");

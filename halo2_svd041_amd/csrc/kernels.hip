@@ -2073,6 +2073,117 @@ hipError_t launch_check_copies(const Fr* s0, const Fr* s1, const Fr* dst, const 
                        ext, cnt);
     return hipGetLastError();
 }
+// the copy source of a region's view (engine.cpp eq_src_cell, same cases)
+__device__ __forceinline__ uint64_t eq_src_dev(const EqSrcDev& e, uint64_t i, uint64_t j, uint64_t t,
+                                               unsigned* err) {
+    if (e.kind == 2) {                          // EQS_CHAIN
+        if (t == 0) return e.first | (uint64_t)e.first_phase << 62;
+        return (e.off + (t - 1) * (uint64_t)e.rs) | (uint64_t)e.phase << 62;
+    }
+    if (e.kind == 1) {                          // EQS_MAT
+        if (e.diag_phase >= 0 && i == j) return e.diag_off | (uint64_t)e.diag_phase << 62;
+        if (i < e.rows && j < e.cols)
+            return (uint64_t)((int64_t)e.off + (int64_t)i * e.rs + (int64_t)j * e.cs) | (uint64_t)e.phase << 62;
+        if (e.pad_phase >= 0) return e.pad_off | (uint64_t)e.pad_phase << 62;
+    }
+    atomicOr(err, 1u);
+    return 0;
+}
+__global__ __launch_bounds__(256) void k_eq_records(const EqRegionDev* __restrict__ R, uint32_t nreg,
+                                                    uint64_t nitems, const uint32_t* __restrict__ words,
+                                                    const Fr* __restrict__ konst, uint32_t phase,
+                                                    uint64_t ext_off, uint64_t* __restrict__ copies,
+                                                    uint64_t* __restrict__ consts, unsigned* __restrict__ err) {
+    const uint64_t me = (uint64_t)phase << 62;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < nitems;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t lo = 0, hi = nreg;                 // region: the last with item0 <= g
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (R[mid].item0 <= g) lo = mid; else hi = mid;
+        }
+        const EqRegionDev& r = R[lo];
+        const uint64_t e = g - r.item0;
+        if (r.scan) {                               // [C(0), E(a_j), E(v_j), W(s_j), ...]
+            const uint64_t i = e / r.L, j = e - i * r.L, base = r.off + i * r.unit;
+            if (j == 0) {
+                uint64_t* k = consts + 5 * (r.const0 + i);
+                k[0] = base;
+                k[1] = k[2] = k[3] = k[4] = 0;
+            }
+            uint64_t* c = copies + 2 * (r.copy0 + 2 * (i * r.L + j));
+            c[0] = eq_src_dev(r.src[0], i, j, 0, err);
+            c[1] = base + 1 + 3 * j;
+            c[2] = eq_src_dev(r.src[1], 0, 0, j, err);
+            c[3] = base + 2 + 3 * j;
+            continue;
+        }
+        const uint64_t base = r.off + e * r.unit, i = e / r.cols, j = e - i * r.cols;
+        uint64_t* c = copies + 2 * (r.copy0 + e * r.ncw);
+        uint64_t* k = consts + 5 * (r.const0 + e * r.nkw);
+        for (uint32_t q = 0; q < r.nw; ++q) {
+            const uint32_t w = words[r.w0 + q], a = eq_a(w), at = eq_slot(w);
+            switch (eq_kind(w)) {
+            case EQ_CONST: {
+                const Fr v = konst[r.k0 + a];
+                k[0] = base + at;
+                for (int t = 0; t < 4; ++t) k[1 + t] = (uint64_t)v.w[2 * t] | (uint64_t)v.w[2 * t + 1] << 32;
+                k += 5;
+                break;
+            }
+            case EQ_LOCAL: c[0] = (base + a) | me; c[1] = base + at; c += 2; break;
+            case EQ_VIEW: c[0] = eq_src_dev(r.src[a], i, j, i, err); c[1] = base + at; c += 2; break;
+            default: c[0] = ext_off | 2ull << 62; c[1] = base + at; c += 2; break;   // init_rand
+            }
+        }
+    }
+}
+__device__ __forceinline__ uint64_t phys_dev(const uint64_t* st, uint32_t ncol, uint32_t k, uint64_t v) {
+    uint32_t lo = 0, hi = ncol;                     // upper_bound(st, v) - 1
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (st[mid] <= v) lo = mid + 1; else hi = mid;
+    }
+    uint32_t col = lo ? lo - 1 : 0;
+    if (col > 0 && v == st[col]) --col;             // break cell: its row in the column before
+    return ((uint64_t)col << k) + (v - st[col]);
+}
+__global__ __launch_bounds__(256) void k_eq_phys(uint64_t* __restrict__ copies, uint64_t nc,
+                                                 uint64_t* __restrict__ consts, uint64_t nk,
+                                                 const uint64_t* __restrict__ s0, uint32_t n0,
+                                                 const uint64_t* __restrict__ s1, uint32_t n1, uint32_t phase,
+                                                 uint32_t k) {
+    const uint64_t* sp = phase ? s1 : s0;
+    const uint32_t np = phase ? n1 : n0;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < nc + nk;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        if (g < nc) {
+            const uint64_t src = copies[2 * g];
+            const uint32_t st = (uint32_t)(src >> 62);
+            if (st < 2)
+                copies[2 * g] = phys_dev(st ? s1 : s0, st ? n1 : n0, k, src & ((1ull << 62) - 1)) | (uint64_t)st << 62;
+            copies[2 * g + 1] = phys_dev(sp, np, k, copies[2 * g + 1]);
+        } else {
+            consts[5 * (g - nc)] = phys_dev(sp, np, k, consts[5 * (g - nc)]);
+        }
+    }
+}
+hipError_t launch_eq_records(const EqRegionDev* regions, uint32_t nreg, uint64_t nitems,
+                             const uint32_t* words, const Fr* konst, uint32_t phase, uint64_t ext_off,
+                             uint64_t* copies, uint64_t* consts, unsigned* err, hipStream_t st) {
+    if (!nitems || !nreg) return hipSuccess;
+    hipLaunchKernelGGL(k_eq_records, dim3(check_grid(nitems)), dim3(256), 0, st, regions, nreg, nitems, words,
+                       konst, phase, ext_off, copies, consts, err);
+    return hipGetLastError();
+}
+hipError_t launch_eq_phys(uint64_t* copies, uint64_t nc, uint64_t* consts, uint64_t nk,
+                          const uint64_t* start0, uint32_t ncol0, const uint64_t* start1, uint32_t ncol1,
+                          uint32_t phase, uint32_t k, hipStream_t st) {
+    if (!nc && !nk) return hipSuccess;
+    hipLaunchKernelGGL(k_eq_phys, dim3(check_grid(nc + nk)), dim3(256), 0, st, copies, nc, consts, nk, start0,
+                       ncol0, start1, ncol1, phase, k);
+    return hipGetLastError();
+}
 hipError_t launch_check_consts(const Fr* dst, const uint64_t* recs, uint64_t n,
                                unsigned long long* cnt, hipStream_t st) {
     if (!n) return hipSuccess;

@@ -154,6 +154,32 @@ hipError_t launch_check_consts(const Fr* dst, const uint64_t* recs, uint64_t n,
                                unsigned long long* cnt, hipStream_t st);
 hipError_t launch_check_lookups(const Fr* lk, uint64_t n, uint32_t lb, unsigned long long* cnt,
                                 hipStream_t st);
+// Equality records on the device (svdw_equalities / svdw_check_equalities): one
+// work item per element of a program region (its eq words in order) or per
+// (row, term) of an inner-product scan region; records land at closed-form
+// offsets, so the lists come out in the host's assign order.
+struct EqSrcDev {
+    int32_t kind, phase, pad_phase, diag_phase, first_phase, _r;
+    uint64_t off, pad_off, diag_off, first;
+    int64_t rs, cs;
+    uint32_t rows, cols;
+};
+struct EqRegionDev {
+    uint64_t off, nitems, item0, copy0, const0;
+    uint32_t scan, unit, cols, L;
+    uint32_t w0, nw, ncw, nkw, k0, _r;
+    EqSrcDev src[2];
+};
+// copies: (source | store << 62, destination) pairs; consts: (cell, 4 words);
+// err: set to 1 when a copy source lies outside the cell streams.
+hipError_t launch_eq_records(const EqRegionDev* regions, uint32_t nreg, uint64_t nitems,
+                             const uint32_t* words, const Fr* konst, uint32_t phase, uint64_t ext_off,
+                             uint64_t* copies, uint64_t* consts, unsigned* err, hipStream_t st);
+// virtual cell -> column-major physical index, in place over the records
+// (svdw_assign_columns' layout: start[phase][col] = the column's first cell)
+hipError_t launch_eq_phys(uint64_t* copies, uint64_t nc, uint64_t* consts, uint64_t nk,
+                          const uint64_t* start0, uint32_t ncol0, const uint64_t* start1, uint32_t ncol1,
+                          uint32_t phase, uint32_t k, hipStream_t st);
 static constexpr int kMaxBitSegs = 8;
 struct BitSegs {
     uint32_t begin[kMaxBitSegs];

@@ -85,3 +85,46 @@ def test_shifted_columns_are_caught(gpu_ctx_factory):
     c0[0, [1, 2]] = c0[0, [2, 1]]          # m[0][1], m[0][2]: sources of phase-1 scan copies
     torch.cuda.synchronize()
     assert fails() > 0
+
+
+@pytest.mark.parametrize("N,M,P,rlc", [(6, 5, 63, 0), (33, 40, 32, 1), (128, 96, 63, 0)])
+def test_device_records_equal_planner_lists(gpu_ctx_factory, N, M, P, rlc):
+    """svdw_equalities on a device context generates the records on the GPU
+    (k_eq_records); they equal the dry planner's host lists record for record
+    (the lists tests/test_equalities_cpu.py pins against the oracle)."""
+    import numpy as np
+    import halo2_svd041_amd as hs
+    m, u, d, v = gen_svd_input(N, M, seed=N + 7 * M + P)
+    g = gamma_for(N + M)
+    ctx = gpu_ctx_factory(P)
+    ctx.set_option("rlc_prefix", rlc)
+    hs.svd_witness(ctx, m, u, v, d, g)
+    with hs.Context(device=-1, precision_bits=P, lookup_bits=19) as dry:
+        dry.set_option("rlc_prefix", rlc)
+        hs.svd_witness(dry, m, u, v, d, g)
+        for ph in (0, 1):
+            cp_d, ks_d = ctx.equalities(ph)
+            cp_h, ks_h = dry.equalities(ph)
+            assert np.array_equal(cp_d, cp_h), ph
+            assert ks_d == ks_h, ph
+
+
+def test_full_size_equalities_on_device(gpu_ctx_factory):
+    """1024^2 P=63 (29 M + 19 M copy records, 76 M constants): generated and
+    checked on the device, every record holds."""
+    import time
+    import torch
+    import halo2_svd041_amd as hs
+    from bench import gen_input
+    m, u, d, v = gen_input(1024, 1024, 0)
+    dev = torch.device("cuda", 0)
+    tm = [torch.tensor(x, dtype=torch.float64, device=dev) for x in (m, u, v, d)]
+    ctx = gpu_ctx_factory(63)
+    hs.svd_witness(ctx, *tm, gamma_for(1))
+    t0 = time.perf_counter()
+    r = [ctx.check_equalities(ph) for ph in (0, 1)]
+    dt = time.perf_counter() - t0
+    assert r[0]["copies_checked"] > 20_000_000 and r[0]["consts_checked"] > 50_000_000
+    assert all(x["copy_failures"] == 0 and x["const_failures"] == 0 for x in r), r
+    print(f"\nequality records at 1024^2: {sum(x['copies_checked'] + x['consts_checked'] for x in r) / 1e6:.1f} M "
+          f"generated and checked on the device in {dt * 1e3:.1f} ms")
