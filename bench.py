@@ -274,14 +274,9 @@ class VerifyMulWorkload:
             torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev) for x in (a, b))
 
     def step(self, gamma):
-        hs, ctx = self.hs, self.ctx
-        ctx.reset()
-        za = hs.ZkMatrix.new(ctx, self.inp[0])
-        zb = hs.ZkMatrix.new(ctx, self.inp[1])
-        cs = hs.honest_prover_mat_mul(ctx, za, zb)
-        hs.ZkMatrix.verify_mul(ctx, za, zb, cs, gamma)
-        return {"advice0": ctx.advice_len(0), "advice1": ctx.advice_len(1),
-                "lookup0": ctx.lookup_len(0), "lookup1": ctx.lookup_len(1)}
+        # the four modular calls in one (svdw_verify_mul_witness: same cells,
+        # tests/test_verify_mul_config.py; no host waits between them)
+        return self.hs.verify_mul_witness(self.ctx, *self.inp, gamma)
 
 
 def main():
@@ -480,8 +475,8 @@ def main():
                         + ("one matrix row-sharded over the GPUs" if rows_mode
                            else "one matrix per GPU"))
         else:
-            workload = (f"verify_mul (README.md:32-46 recipe) a {N}x{N} . b {N}x{M} "
-                        f"PRECISION_BITS={P}, one product per GPU")
+            workload = (f"verify_mul (README.md:32-46 recipe, svdw_verify_mul_witness) a {N}x{N} . "
+                        f"b {N}x{M} PRECISION_BITS={P}, one product per GPU")
         out = {
             "metric": METRIC,
             "value": round(value, 1),

@@ -2419,6 +2419,81 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
 }
 
+// README.md:32-46 as one call: ZkMatrix::new(a), ZkMatrix::new(b), c_s =
+// honest_prover_mat_mul(a, b) into phase 0, verify_mul(a, b, c_s, gamma) into
+// phase 1 -- the modular calls' cells, enqueued without host waits: a and b
+// quantized in one launch, the GEMM's modulus count and the row scans' operand
+// widths decided on the device from the bit-length words, gamma^j prepared
+// first on the side stream.
+static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double* b, uint32_t N,
+                                      uint32_t K, uint32_t M, bool on_device, const Fr& gamma) {
+    REQUIRE(N >= 1 && K >= 1 && M >= 1, "empty matrix");
+    REQUIRE(!sharded(c), "verify_mul_witness: not for row-sharded contexts");
+    clear_streams(c);
+    c->dep_next = 0;
+    c->prelaunched = false;
+    c->gemm_batched = false;
+    c->gemm_done.clear();
+    c->wait_before_cs.clear();
+    c->pre.clear();
+    if (!c->dry) {
+        const std::vector<uint64_t> key = {0x766d77ull, N, K, M};      // sizes from the dry plan
+        if (key != c->plan_key) {
+            svdw_ctx plan;
+            plan.P = c->P; plan.LB = c->LB;
+            verify_mul_witness(&plan, nullptr, nullptr, N, K, M, false, gamma);
+            c->plan_key = key;
+            c->plan_val = {plan.ph[0].n, plan.ph[0].nl, plan.ph[1].n, plan.ph[1].nl};
+        }
+        for (int p = 0; p < 2; ++p) {
+            grow(c, c->ph[p].adv, 0, c->ph[p].cap, c->plan_val[2 * p]);
+            grow(c, c->ph[p].lk, 0, c->ph[p].lcap, c->plan_val[2 * p + 1]);
+        }
+    }
+    c->ext_off = 0;
+    c->gp_ev = nullptr;
+    unsigned* dbits = nullptr;
+    const uint32_t nba = (uint32_t)(((uint64_t)N * K + 255) / 256), nbb = (uint32_t)(((uint64_t)K * M + 255) / 256);
+    if (!c->dry) {
+        if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
+        gamma_prep(c, M, gamma, c->st3);
+        c->gp_ev = stream_dep(c, c->st3, nullptr);
+        ensure_buf(c, c->bits, (64 + nba + nbb) * sizeof(unsigned));
+        dbits = (unsigned*)c->bits.p;
+    }
+    QuantSegs qs;
+    memset(&qs, 0, sizeof qs);
+    QuantSegs* qp = c->fused_quantize && on_device ? &qs : nullptr;
+    const svdw_mat za = zkmatrix_new(c, 0, a, N, K, on_device, dbits ? dbits + 64 : nullptr, qp);
+    const svdw_mat zb = zkmatrix_new(c, 0, b, K, M, on_device, dbits ? dbits + 64 + nba : nullptr, qp);
+    if (qs.nseg) {
+        ProfScope ps(c, c->st, "k_quantize", 40.0 * ((double)N * K + (double)K * M), 0);
+        hipck(launch_quantize_multi(qs, (int)c->P, c->st), "k_quantize_multi");
+    }
+    if (!c->dry) {
+        BitSegs seg{};
+        seg.begin[0] = 0;
+        seg.begin[1] = nba;
+        seg.begin[2] = nba + nbb;
+        hipck(launch_bits_reduce(dbits + 64, seg, 2, dbits, c->st), "k_bits_reduce");
+        c->dbitw = dbits;
+        c->dwords = {{za, 0}, {zb, 1}};
+    }
+    // c_s = a * b (honest_prover_mat_mul's cells), the CRT GEMM sized on the device
+    uint64_t off;
+    append(c, 0, (uint64_t)N * M, 0, &off, nullptr, "product", N);
+    const svdw_mat cs{0, N, M, off, (int64_t)M, 1};
+    {
+        uint32_t lk = 0;
+        while ((1ull << lk) < K) ++lk;
+        c->prods.push_back({cs, za, zb, lk});
+    }
+    if (!c->dry) gemm_exec(c, c->st, za, zb, cellp(c, 0, off), ~0u, ~0u, dbits, dbits + 1, true);
+    const VMul vm{za, zb, cs};
+    verify_mul_many(c, 1, &vm, 1, gamma);
+    return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
+}
+
 // ------------------------------------------------------ equality lists
 // halo2-base's equality records of phase `phase` (svdw_equalities), in assign
 // order, from the layout table: per region its element program's eq words
@@ -2925,6 +3000,15 @@ int svdw_svd_witness(svdw_ctx* c, const double* m, const double* u, const double
         REQUIRE(c && cfg && gamma, "null argument");
         REQUIRE(c->dry || (m && u && v && d), "null input matrix");
         svdw_counts k = svd_witness(c, m, u, v, d, N, M, on_device != 0, *cfg, fr_from_words(gamma));
+        if (counts) *counts = k;
+    });
+}
+int svdw_verify_mul_witness(svdw_ctx* c, const double* a, const double* b, uint32_t N, uint32_t K,
+                            uint32_t M, int on_device, const uint64_t gamma[4], svdw_counts* counts) {
+    return guarded([&] {
+        REQUIRE(c && gamma, "null argument");
+        REQUIRE(c->dry || (a && b), "null input matrix");
+        svdw_counts k = verify_mul_witness(c, a, b, N, K, M, on_device != 0, fr_from_words(gamma));
         if (counts) *counts = k;
     });
 }

@@ -530,6 +530,28 @@ def svd_witness(ctx: Context, m, u, v, d, gamma: int, cfg: SvdConfigPy = SvdConf
     return cnt.as_dict()
 
 
+def verify_mul_witness(ctx: Context, a, b, gamma: int) -> dict:
+    """The README.md:32-46 recipe in one call (svdw_verify_mul_witness): loads
+    of a and b, c_s = a * b in phase 0, verify_mul(a, b, c_s, gamma) in phase 1.
+    Inputs: numpy arrays or contiguous float64 torch tensors on the device."""
+    cnt = Counts()
+    g = int_to_words(int(gamma) % P_MOD)
+    dps = [_device_ptr(x) for x in (a, b)]
+    if all(p is not None for p in dps):
+        (N, K), M = a.shape, b.shape[1]
+        if b.shape[0] != K:
+            raise SvdwError(-1, "verify_mul_witness: a.num_col != b.num_rows")
+        check(lib().svdw_verify_mul_witness(ctx.handle, *dps, N, K, M, 1, g.ctypes.data, ct.byref(cnt)))
+    else:
+        arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (a, b)]
+        (N, K), M = arrs[0].shape, arrs[1].shape[1]
+        if arrs[1].shape[0] != K:
+            raise SvdwError(-1, "verify_mul_witness: a.num_col != b.num_rows")
+        check(lib().svdw_verify_mul_witness(ctx.handle, arrs[0].ctypes.data, arrs[1].ctypes.data, N, K, M, 0,
+                                            g.ctypes.data, ct.byref(cnt)))
+    return cnt.as_dict()
+
+
 def parse_svd_input(src, mode: str = "serde") -> dict:
     """Arrays m, u, d, v of the example's input file (data/matrix.in; a path,
     bytes or str), parsed natively like serde_json's default float path

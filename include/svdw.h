@@ -204,6 +204,14 @@ int svdw_check_svd_phase1(svdw_ctx* ctx, const svdw_mat* m, const svdw_mat* u, c
 int svdw_svd_witness(svdw_ctx* ctx, const double* m, const double* u, const double* v,
                      const double* d, uint32_t N, uint32_t M, int on_device,
                      const svdw_svd_config* cfg, const uint64_t gamma[4], svdw_counts* counts);
+/* The README.md:32-46 recipe as one call (BASELINE config 2): reset,
+ * ZkMatrix::new(a) (N x K), ZkMatrix::new(b) (K x M), c_s =
+ * honest_prover_mat_mul(a, b) into phase 0, ZkMatrix::verify_mul(a, b, c_s,
+ * gamma) (src/matrix/mod.rs:299-342) into phase 1; the same cells as those four
+ * modular calls, without host waits. a, b row-major f64 (device memory if
+ * on_device). */
+int svdw_verify_mul_witness(svdw_ctx* ctx, const double* a, const double* b, uint32_t N, uint32_t K,
+                            uint32_t M, int on_device, const uint64_t gamma[4], svdw_counts* counts);
 /* Exact integer GEMM of honest_prover_mat_mul (the integer sum of quantized
  * products, reduced mod p once). Matrix-core paths (SVDW_GEMM_MFMA, default):
  *   - multi-modular / CRT (option "gemm_crt" 1, default): balanced residues

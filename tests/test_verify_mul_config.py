@@ -94,3 +94,40 @@ def test_config2_verify_mul_256_full_stream(gpu_ctx_factory, wrong):
         assert all(d == 0 and z == 1 for d, z, inv in diffs)
     chk = ctx.check_gates()
     assert chk["gate_failures"] == 0 and chk["lookup_failures"] == 0 and chk["copy_failures"] == 0
+
+
+def test_fused_recipe_plans_like_the_modular_calls():
+    """svdw_verify_mul_witness appends exactly the modular calls' cells (dry planner)."""
+    import halo2_svd041_amd as hs
+    for n, k, m, P in ((5, 7, 4, 32), (33, 17, 40, 63), (256, 256, 256, 32)):
+        a, b, _ = _inputs(n, k, m, seed=n + k)
+        with hs.Context(device=-1, precision_bits=P, lookup_bits=19) as c1, \
+                hs.Context(device=-1, precision_bits=P, lookup_bits=19) as c2:
+            got = hs.verify_mul_witness(c1, a, b, 7)
+            za, zb = hs.ZkMatrix.new(c2, a), hs.ZkMatrix.new(c2, b)
+            hs.ZkMatrix.verify_mul(c2, za, zb, hs.honest_prover_mat_mul(c2, za, zb), 7)
+            assert got == {"advice0": c2.advice_len(0), "advice1": c2.advice_len(1),
+                           "lookup0": c2.lookup_len(0), "lookup1": c2.lookup_len(1)}
+            assert got["advice1"] == vm_cells(n, k, m)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k,m,P,dev", [(256, 256, 256, 32, True), (256, 256, 256, 32, False),
+                                         (45, 130, 37, 63, True), (1, 1, 1, 32, True)])
+def test_fused_verify_mul_witness_full_stream(gpu_ctx_factory, n, k, m, P, dev):
+    """The one-call recipe (svdw_verify_mul_witness: device-decided GEMM moduli and
+    row-scan widths, no host waits) against the C oracle, full advice streams."""
+    import torch
+    import halo2_svd041_amd as hs
+    a, b, _ = _inputs(n, k, m, seed=n + 3 * m)
+    g = gamma_for(n + m)
+    ctx = gpu_ctx_factory(P)
+    if dev:
+        ta, tb = (torch.tensor(x, dtype=torch.float64, device="cuda:0") for x in (a, b))
+        hs.verify_mul_witness(ctx, ta, tb, g)
+    else:
+        hs.verify_mul_witness(ctx, a, b, g)
+    c0, c1 = corc.verify_mul_witness(a, b, P, g)
+    assert np.array_equal(ctx.advice(0), c0) and np.array_equal(ctx.advice(1), c1)
+    chk = ctx.check_gates()
+    assert chk["gate_failures"] == 0 and chk["lookup_failures"] == 0 and chk["copy_failures"] == 0
