@@ -309,6 +309,8 @@ def main():
                          "witness-only value")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the untimed device constraint check of the last witness")
+    ap.add_argument("--no-ingest", action="store_true",
+                    help="skip the untimed device parse of the input as data/matrix.in text")
     ap.add_argument("--dry", action="store_true",
                     help="CPU rehearsal: gloo + the engine's dry planner, no GPU")
     ap.add_argument("--opt", action="append", default=[],
@@ -406,10 +408,11 @@ def main():
     # The same kernel alone on the GPU (one untimed step with the streams
     # serialised): its intrinsic rate, reported beside the contended in-step rate.
     solo = None
+    gemm = None
     if profile and svd and not rows_mode:
         ctx.set_option("overlap", 0)
         ctx.set_option("phase1_overlap", 0)
-        ctx.profile(True, prefix)
+        ctx.profile(True, "")
         wl.step(gammas[-1])
         sync()
         solo_stats = ctx.profile_collect()
@@ -417,7 +420,16 @@ def main():
         ctx.set_option("overlap", 1)
         ctx.set_option("phase1_overlap", 1)
         if solo_stats:
-            _, solo, _ = roofline_from_profile(solo_stats, 1)
+            _, solo, _ = roofline_from_profile([x for x in solo_stats if x["name"].startswith(prefix)], 1)
+            # SURVEY.md §8(d) stage (ii): the exact field GEMMs (N M^2 + N^3 + M^3
+            # MACs) -- residue planes, int8 matrix-core GEMMs, CRT -- alone on the GPU
+            gms = sum(x["total_ms"] for x in solo_stats
+                      if x["name"].split("@")[0].startswith(("k_to_residues", "k_residues", "k_gemm", "k_crt")))
+            macs = float(N) * M * M + float(N) ** 3 + float(M) ** 3
+            if gms > 0:
+                gemm = {"field_macs_per_step": macs, "ms": round(gms, 4),
+                        "field_GMAC_s": round(macs / (gms * 1e-3) / 1e9, 1),
+                        "note": "exact Fr GEMMs (residues + int8 MFMA GEMMs + CRT), streams serialised"}
 
     reasm = None
     if rows_mode and args.gather != "none" and not args.dry:
@@ -463,6 +475,35 @@ def main():
                 check["equality_" + k] = sum(int(x[k]) for x in eq)
             bad += check["equality_copy_failures"] + check["equality_const_failures"]
         check["ok"] = bad == 0
+
+    # Untimed: the same input as data/matrix.in text (json.dump(indent=4), as
+    # input-creator.py writes it) parsed on the device (svdw_parse_svd_input_device)
+    ingest = None
+    if svd and world == 1 and not args.dry and not args.no_ingest:
+        m, u, v, d = wl.host
+        text = json.dumps({"m": m.tolist(), "u": u.tolist(), "d": d.tolist(), "v": v.tolist()},
+                          indent=4).encode()
+        tt = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(dev)
+        hs.parse_svd_input_device(ctx, tt)
+        ts = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            parsed = hs.parse_svd_input_device(ctx, tt)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        tdev = sorted(ts)[1]
+        t0 = time.perf_counter()
+        host = hs.parse_svd_input(text, "serde")
+        thost = time.perf_counter() - t0
+        same = all(np.array_equal(parsed[k].cpu().numpy().view(np.uint64), host[k].view(np.uint64))
+                   for k in ("m", "u", "v", "d"))
+        ingest = {"text_MB": round(len(text) / 1e6, 1), "device_parse_ms": round(tdev * 1e3, 3),
+                  "device_GB_s": round(len(text) / tdev / 1e9, 1), "host_parse_ms": round(thost * 1e3, 1),
+                  "bit_identical_to_host_parse": bool(same),
+                  "note": "untimed; serde_json's default float path (1 ulp off correct rounding on ~10 % "
+                          "of values, as the reference reads data/matrix.in), text resident in HBM"}
+        del tt, parsed
 
     elapsed, cells_all = reduce_over_ranks(elapsed, cells_step, dist, red_dev)
     if rows_mode:
@@ -532,6 +573,10 @@ def main():
             if args.breakdown:
                 print(json.dumps({"ms_per_step_by_kernel": breakdown,
                                   "stats": stats}, indent=1), file=sys.stderr)
+        if gemm is not None:
+            out["field_gemm"] = gemm
+        if ingest is not None:
+            out["ingest"] = ingest
         if reasm is not None:
             out["reassembly"] = reasm
         if check is not None:
