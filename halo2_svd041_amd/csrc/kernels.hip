@@ -1749,7 +1749,12 @@ __global__ __launch_bounds__(256) void k_crt_combine(const uint8_t* __restrict__
                                                      int64_t ors, int64_t ocs,
                                                      const unsigned* __restrict__ bits_a,
                                                      const unsigned* __restrict__ bits_b, uint32_t lk) {
-    crt_combine_block<SYM>(R, rpad_a, rpad_b, N, M, tiles_m, out, ors, ocs, bits_a, bits_b, lk, blockIdx.x);
+    // Blocks b and b + 8 share an XCD: give each XCD a contiguous run of the
+    // (row-major) tile sequence, so the 32-byte row pieces that neighbouring
+    // tiles read from the same 128-byte lines of R come through one L2.
+    const uint32_t g = gridDim.x, b = blockIdx.x;
+    const uint32_t blk = (g & 7) == 0 ? (b & 7) * (g >> 3) + (b >> 3) : b;
+    crt_combine_block<SYM>(R, rpad_a, rpad_b, N, M, tiles_m, out, ors, ocs, bits_a, bits_b, lk, blk);
 }
 __global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b) {
     uint32_t j = 0;
