@@ -454,6 +454,7 @@ struct svdw_ctx {
     int gemm_kc = 1;                        // "gemm_kc": 64-k chunks per LDS round of the CRT GEMM (1 / 4;
                                             // 4 needs 64 KiB of LDS and starves beside the stage blocks)
     bool gemm_batched = false;              // this witness's products went out as one batch
+    bool gemm_xm = true;                    // "gemm_xm": CRT GEMM units (modulus, half) placed per XCD
     int res_first = 0;                      // "res_first": cell stream waits for the residue planes
                                             // (1), not (0), -1: on row-sharded ranks
     int gemm_batch = -1;                    // "gemm_batch": svd_witness's three products in one launch
@@ -1346,7 +1347,7 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
             ProfScope ps(c, s, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * N * M,
                          (double)N * M * K);
             hipck(launch_gemm_crt(sym, Ar, Br, N, M, rpa, sym ? rpa : rpb,
-                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s, c->gemm_kc),
+                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s, c->gemm_kc, c->gemm_xm),
                   "k_gemm_crt");
         }
         if (!quantized)
@@ -2037,7 +2038,8 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
             ProfScope ps(c, c->st2, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * rows * cols,
                          (double)rows * cols * A[g].cols);
             hipck(launch_gemm_crt(sym, Ap, Bp, rows, cols, stride[g], bs, kp[g], (uint8_t*)c->crtR.p,
-                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], c->st2, c->gemm_kc),
+                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], c->st2, c->gemm_kc,
+                                  c->gemm_xm),
                   "k_gemm_crt");
         }
         c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
@@ -3677,6 +3679,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "res_first") {
             REQUIRE(value >= -1 && value <= 1, "res_first: -1 (auto), 0 or 1");
             c->res_first = (int)value;
+        } else if (n == "gemm_xm") {
+            c->gemm_xm = value != 0;
         } else if (n == "stage_persist") {
             c->stage_persist = value != 0;
         } else if (n == "gemm_batch") {

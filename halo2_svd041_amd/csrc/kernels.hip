@@ -1627,6 +1627,27 @@ __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar
     crt_gemm_block<SYM, KC>(Ar, Br, astride, bstride, kpad, tiles_a, tiles_m, R, bits_a, bits_b, lk,
                             blockIdx.x, gridDim.x, (int)blockIdx.y);
 }
+// Modulus-major XCD placement (1-D grid): work unit u = (modulus u / 2, half
+// u % 2 of its tiles) runs entirely on XCD u % 8 (workgroup L goes to XCD
+// L % 8), so each XCD streams a modulus's residue planes through its own L2
+// once per half instead of every XCD re-reading strips of every plane; the 38
+// units of 19 moduli balance over the 8 XCDs. tpu: tiles per unit.
+template <bool SYM, int KC>
+__global__ __launch_bounds__(256) void k_gemm_crt_xm(const uint8_t* __restrict__ Ar,
+                                                     const uint8_t* __restrict__ Br, uint32_t astride,
+                                                     uint32_t bstride, uint32_t kpad, uint32_t tiles_a,
+                                                     uint32_t tiles_m, uint8_t* __restrict__ R,
+                                                     const unsigned* __restrict__ bits_a,
+                                                     const unsigned* __restrict__ bits_b, uint32_t lk,
+                                                     uint32_t ntiles, uint32_t tpu) {
+    const uint32_t L = blockIdx.x, k = L >> 3;
+    const uint32_t u = (L & 7) + 8 * (k / tpu), t = k % tpu;
+    const uint32_t tile = (u & 1) * tpu + t;
+    if (tile >= ntiles) return;
+    // nblk = 1: plain row-major tile decode (no in-modulus XCD remap)
+    crt_gemm_block<SYM, KC>(Ar, Br, astride, bstride, kpad, tiles_a, tiles_m, R, bits_a, bits_b, lk, tile,
+                            1, (int)(u >> 1));
+}
 // The products of a CrtBatch in one launch: grid.x covers every job's tile
 // blocks (job j from blk0[j], multiples of 8 so the XCD mapping holds), grid.y
 // the moduli.
@@ -1802,13 +1823,34 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st, int kc) {
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st, int kc, bool xm) {
     if (kc != 1 && kc != 4) return hipErrorInvalidValue;
+    xm = xm && kc == 1;
     const uint32_t ta = (N + CT - 1) / CT, tb = (M + CT - 1) / CT;
     // every staged row (tiles x CT) lies inside its operand's planes
     if (kpad % 64 || astride < ta * CT || bstride < tb * CT) return hipErrorInvalidValue;
     const uint32_t rpa = ta * CT, rpb = tb * CT;           // R: [mod][rpa][rpb]
     const uint32_t sa = (N + MT - 1) / MT, sb = (M + MT - 1) / MT;
+    if (xm) {
+        const uint32_t ntiles = sym ? ta * (ta + 1) / 2 : ta * tb, tpu = (ntiles + 1) / 2;
+        const uint32_t grid = 8 * tpu * ((2 * kCrtMaxMod + 7) / 8);
+        if (sym && (N != M || astride != bstride)) return hipErrorInvalidValue;
+        if (sym)
+            hipLaunchKernelGGL((k_gemm_crt_xm<true, 1>), dim3(grid), dim3(256), 0, st, Ar, Ar, astride, bstride,
+                               kpad, ta, ta, R, bits_a, bits_b, lk, ntiles, tpu);
+        else
+            hipLaunchKernelGGL((k_gemm_crt_xm<false, 1>), dim3(grid), dim3(256), 0, st, Ar, Br, astride, bstride,
+                               kpad, ta, tb, R, bits_a, bits_b, lk, ntiles, tpu);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        if (sym)
+            hipLaunchKernelGGL(k_crt_combine<true>, dim3(sa * (sa + 1) / 2), dim3(256), 0, st, R, rpa,
+                               rpb, N, M, sa, out, ors, ocs, bits_a, bits_b, lk);
+        else
+            hipLaunchKernelGGL(k_crt_combine<false>, dim3(sa * sb), dim3(256), 0, st, R, rpa, rpb,
+                               N, M, sb, out, ors, ocs, bits_a, bits_b, lk);
+        return hipGetLastError();
+    }
     if (sym) {
         if (N != M || astride != bstride) return hipErrorInvalidValue;
         if (kc == 4)

@@ -269,7 +269,8 @@ hipError_t launch_residues_f64(const ResSegs& q, const unsigned* W, int precisio
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st, int kc = 4);
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st, int kc = 4,
+                           bool xm = false);
 static constexpr int kCrtMaxResidues = 40;   // = kCrtMaxMod (crt_tables.hpp)
 // Several CRT products in one GEMM launch and one combine launch (a row-sharded
 // rank's three products of check_svd_phase0). Per job the caller sets Ar, Br,

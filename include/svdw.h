@@ -260,7 +260,9 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   and gamma powers, the is_equal rows; split automatically where a stage reads
  *   cells a pending one writes); "gemm_batch" -1 | 0 | 1 (svd_witness's three
  *   products in one GEMM and one combine launch: -1 on row-sharded contexts);
- *   "gemm_kc" 1 | 4 (64-k chunks per LDS round of the CRT GEMM); "res_first"
+ *   "gemm_kc" 1 | 4 (64-k chunks per LDS round of the CRT GEMM); "gemm_xm"
+ *   1 | 0 (unbatched CRT GEMMs: XCD-major modulus placement, so each residue
+ *   plane is read through two XCDs' L2 rather than all eight); "res_first"
  *   0 | 1 | -1 (the cell stream waits for the residue planes; -1: on row-sharded
  *   contexts; measured slower, kept for A/B).
  * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:

@@ -176,7 +176,7 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                                   {"scan_na_host": 1}, {"scan_impl": 5, "phase1_overlap": 2},
                                   {"stage_batch": 0}, {"gemm_batch": 1}, {"gemm_kc": 4},
                                   {"gemm_batch": 1, "gemm_kc": 4}, {"res_first": 1}, {"stage_persist": 1},
-                                  {"stage_persist": 1, "stage_batch": 0}])
+                                  {"stage_persist": 1, "stage_batch": 0}, {"gemm_xm": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
