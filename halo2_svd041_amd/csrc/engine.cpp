@@ -467,6 +467,11 @@ struct svdw_ctx {
     int phase1_overlap = 1;                 // "phase1_overlap": 0 off, 1 on st2 behind the
                                             // GEMMs, 2 on st3 from quantization on
     bool prelaunched = false;               // this witness's products were queued on st2
+    int prod_cell = -1;                     // "prod_cell": svd_witness's products (residues, GEMM,
+                                            // combine) on the cell stream and the u / v bounds and
+                                            // u.d beside them on st2 (1), not (0); -1: on row-sharded
+                                            // ranks, where the product chain is the critical path
+    bool prod_on_cell = false;              // this witness's products went on the cell stream
     uint32_t hold_us = 0;                   // "hold_us": timing aid, st spins this long first
     Fr ext_gamma{};                          // init_rand of the last verify_mul (equality source 2)
     uint64_t ext_off = 0;                    // its cell in the RLC context
@@ -501,6 +506,7 @@ struct svdw_ctx {
     struct PreGemm {
         uint64_t off;
         hipEvent_t ev;
+        hipStream_t st;                     // the stream it was launched on
     };
     std::vector<PreGemm> pre;               // GEMMs launched ahead on st2, in append order
     std::vector<svdw_region> layout;        // every appended region of the current witness
@@ -1472,7 +1478,9 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
     if (c->dry) return cs;
     if (!c->pre.empty()) {
         if (c->pre.front().off != off) fail(SVDW_EDEVICE, "internal: pre-launched GEMM offset mismatch");
-        hipck(hipStreamWaitEvent(c->st, c->pre.front().ev, 0), "hipStreamWaitEvent");
+        // (launched on this very stream: already ordered)
+        if (c->pre.front().st != c->st)
+            hipck(hipStreamWaitEvent(c->st, c->pre.front().ev, 0), "hipStreamWaitEvent");
         c->pre.erase(c->pre.begin());
         return cs;
     }
@@ -1930,7 +1938,7 @@ static BigU scale_err(double err, uint32_t p) {
 // products' stream offsets (dry replay); W: the device bit-length words of m, u, v.
 static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const svdw_mat (&B)[3],
                                    const std::vector<uint64_t>& log, uint32_t phase,
-                                   const unsigned* W) {
+                                   const unsigned* W, hipStream_t pst) {
     const uint32_t N = A[0].rows, M = A[0].cols;
     auto clog2 = [](uint32_t k) { uint32_t l = 0; while ((1ull << l) < k) ++l; return l; };
     auto ceil_to = [](uint32_t x, uint32_t a) { return (x + a - 1) / a * a; };
@@ -1963,13 +1971,14 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
     seg(c->svd_f64[2], M, M, rp_v, kpM, c->digB, {{0, 2, (int)lkM}, {2, 2, (int)lkM}});
     seg(c->svd_f64[1], N, N, rp_u, kpN, c->digC, {{1, 1, (int)lkN}});
     {
-        ProfScope ps(c, c->st2, "k_residues_f64",
+        ProfScope ps(c, pst, "k_residues_f64",
                      8.0 * ((double)rows_m * M + (double)M * M + (double)N * N), 0);
-        hipck(launch_residues_f64(q, W, (int)c->P, c->st2), "k_residues_f64");
+        hipck(launch_residues_f64(q, W, (int)c->P, pst), "k_residues_f64");
     }
     // res_first: the cell stream waits for the residue planes, which then run
     // alone instead of beside the first (HBM-saturating) stages
-    if (c->res_first > 0 || (c->res_first < 0 && sharded(c))) stream_dep(c, c->st2, c->st);
+    if (pst != c->st && (c->res_first > 0 || (c->res_first < 0 && sharded(c))))
+        stream_dep(c, pst, c->st);
     const uint8_t* P[3] = {(const uint8_t*)c->digA.p, (const uint8_t*)c->digC.p,
                            (const uint8_t*)c->digB.p};                 // A planes of m, u, v
     const uint32_t stride[3] = {rp_m, rp_u, rp_v}, kp[3] = {kpM, kpN, kpM}, lk[3] = {lkM, lkN, lkM};
@@ -2016,12 +2025,12 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
         }
         c->gemm_batched = true;
         if (b.njobs) {
-            ProfScope ps(c, c->st2, "k_gemm_crt:multi", bytes, ops);
-            hipck(launch_gemm_crt_multi(b, c->st2), "k_gemm_crt_multi");
+            ProfScope ps(c, pst, "k_gemm_crt:multi", bytes, ops);
+            hipck(launch_gemm_crt_multi(b, pst), "k_gemm_crt_multi");
         }
-        const hipEvent_t done = stream_dep(c, c->st2, nullptr);   // one completion point
+        const hipEvent_t done = stream_dep(c, pst, nullptr);   // one completion point
         for (int g = 0; g < 3; ++g) {
-            c->pre.push_back({log[g], done});
+            c->pre.push_back({log[g], done, pst});
             c->gemm_done.push_back(done);
         }
         return;
@@ -2035,14 +2044,14 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
             const uint32_t bs = g == 0 ? rp_v : stride[g];
             // a row block of u / v is a slice of the full planes (m's are this rank's rows)
             const uint8_t* Ap = P[g] + (g == 0 ? 0 : rr0[g] * (uint64_t)kp[g]);
-            ProfScope ps(c, c->st2, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * rows * cols,
+            ProfScope ps(c, pst, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * rows * cols,
                          (double)rows * cols * A[g].cols);
             hipck(launch_gemm_crt(sym, Ap, Bp, rows, cols, stride[g], bs, kp[g], (uint8_t*)c->crtR.p,
-                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], c->st2, c->gemm_kc,
+                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], pst, c->gemm_kc,
                                   c->gemm_xm),
                   "k_gemm_crt");
         }
-        c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
+        c->pre.push_back({log[g], stream_dep(c, pst, nullptr), pst});
         c->gemm_done.push_back(c->pre.back().ev);
     }
 }
@@ -2100,8 +2109,15 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         std::swap(vt.rows, vt.cols); std::swap(vt.rs, vt.cs);
         // loads of m, u, v done: the quantization event when svd_witness recorded
         // one (the cell stream may already hold later stages), else st's position
-        if (c->bits_pending) hipck(hipStreamWaitEvent(c->st2, c->ev_bits, 0), "hipStreamWaitEvent");
-        else stream_dep(c, c->st, c->st2);
+        // products on the cell stream (prod_cell): already behind the loads there
+        c->prod_on_cell = from_f64 && c->prelaunch_at == 0 && c->d_checks_aside && c->bits_pending &&
+                          (c->prod_cell > 0 || (c->prod_cell < 0 && sharded(c)));
+        if (c->prod_on_cell) {
+        } else if (c->bits_pending) {
+            hipck(hipStreamWaitEvent(c->st2, c->ev_bits, 0), "hipStreamWaitEvent");
+        } else {
+            stream_dep(c, c->st, c->st2);
+        }
         const svdw_mat A[3] = {m, u, v}, B[3] = {vt, ut, vt};
         const uint32_t ba[3] = {known_bits[0], known_bits[1], known_bits[2]};
         const uint32_t bb[3] = {known_bits[2], known_bits[1], known_bits[2]};
@@ -2111,7 +2127,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         const unsigned* sa[3] = {sl[0], sl[1], sl[2]};
         const unsigned* sb[3] = {sl[2], sl[1], sl[2]};
         if (from_f64) {
-            prelaunch_products_f64(c, A, B, log, m.phase, dev_bits);
+            prelaunch_products_f64(c, A, B, log, m.phase, dev_bits, c->prod_on_cell ? c->st : c->st2);
             c->prelaunched = true;
             host_mark(c, "products queued");
             return;
@@ -2136,7 +2152,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
             else
                 gemm_exec(c, c->st2, Ag, B[g], outg, ba[g], bb[g]);
             if (g == 0 && r1 > r0 && on_device) vplanes = true;
-            c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr)});
+            c->pre.push_back({log[g], stream_dep(c, c->st2, nullptr), c->st2});
             c->gemm_done.push_back(c->pre.back().ev);
         }
         c->prelaunched = true;
@@ -2186,8 +2202,13 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     early_phase1(0);
     // The u, v bounds and u.d read only the loaded matrices: one launch when
     // batched (stage_batch), after which phase 1 is queued (p1_at 1 or 2).
+    // With the products on the cell stream they go on st2 instead (behind the
+    // d checks, in the same batch), and the cell stream waits for them before
+    // the diff, by when they are done.
+    const bool pc = c->prod_on_cell && c->prelaunched;
+    if (pc) std::swap(c->st, c->st2);
     BatchScope bs(c);
-    const bool batched = bs.mine;
+    const bool batched = bs.mine || pc;
     BigU unit = big_from_u128(((unsigned __int128)1 << P) + 1);
     check_mat_entries_bounded(c, u, unit);
     host_mark(c, "bounds(u) queued");
@@ -2212,6 +2233,10 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     }
     udv.rows = N;
     bs.end();
+    if (pc) {
+        std::swap(c->st, c->st2);
+        stream_dep(c, c->st2, c->st);                   // (flushes st2's batch first)
+    }
     if (batched) {
         host_mark(c, "bounds(u), bounds(v), u.d queued");
         early_phase1(1);
@@ -2266,6 +2291,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     clear_streams(c);
     c->dep_next = 0;
     c->prelaunched = false;
+    c->prod_on_cell = false;
     c->gemm_batched = false;
     c->gemm_done.clear();
     c->wait_before_cs.clear();
@@ -2434,6 +2460,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     clear_streams(c);
     c->dep_next = 0;
     c->prelaunched = false;
+    c->prod_on_cell = false;
     c->gemm_batched = false;
     c->gemm_done.clear();
     c->wait_before_cs.clear();
@@ -3604,6 +3631,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                 hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
                 c->st2 = s;
             }
+        } else if (n == "prod_cell") {
+            REQUIRE(value >= -1 && value <= 1, "prod_cell: -1, 0 or 1");
+            c->prod_cell = (int)value;
         } else if (n == "d_checks_aside") {
             c->d_checks_aside = value != 0;
         } else if (n == "fused_quantize") {

@@ -1279,53 +1279,59 @@ __device__ __forceinline__ int crt_nmod(uint32_t ba, uint32_t bb, uint32_t lk) {
     return 0;
 }
 
-// Balanced residues of 4 consecutive-k elements (16-bit halves h of |x|, sign
-// neg) for moduli k < n, one u32 word (4 x int8) per plane at o[k * plane].
-// The table loads are per-modulus (scalar); s mod m uses mul_hi, no fp32 quotient.
-template <int NH>
-__device__ __forceinline__ void residues_emit(const uint32_t (&h)[4][8], const bool (&neg)[4],
+// Balanced residues bal = ((x + h) mod m) - h, h = floor(m / 2), in [-128, 127],
+// of 4 consecutive-k elements x = +-|x| for moduli k < n: one u32 word (4 x
+// int8) per plane at o[k * plane]. w: NW u32 words of |x| (< 2^(32 NW)); nm:
+// all ones for x < 0. The sign costs one xor per word, since -|x| = ~|x| + 1 -
+// 2^(32 NW), plus the AND of the modulus' (1 - 2^(32 NW)) mod m; the sum of the
+// bytes times 256^i mod m is one v_dot4_u32_u8 per word and stays < 2^20,
+// where the mul_hi quotient by ceil(2^32 / m) is exact.
+template <int NW>
+__device__ __forceinline__ void residues_emit(const uint32_t (&w)[4][4], const uint32_t (&nm)[4],
                                               uint32_t* __restrict__ o, uint64_t plane, int n) {
+    uint32_t x[4][NW];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < NW; ++j) x[t][j] = w[t][j] ^ nm[t];
     for (int k = 0; k < n; ++k) {
-        const uint32_t m = c_crt_mod[k], magic = c_crt_magic[k], bias = c_crt_bias[k];
-        uint32_t word = 0;
+        const uint32_t m = c_crt_mod[k], magic = c_crt_magic[k], h = m >> 1,
+                       cn = c_crt_negc[NW - 2][k];
+        uint32_t bal[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            uint32_t s = 0;
+            uint32_t s0 = nm[t] & cn;
 #pragma unroll
-            for (int j = 0; j < NH; ++j) s = __umul24(h[t][j], c_crt_pow16[k][j]) + s;   // < 2^27
-            // -x: bias - s (bias a multiple of m, >= 2^27), still < 2^28
-            s = neg[t] ? bias - s : s;
-            // s mod m: the quotient from mul_hi by ceil(2^32 / m) is exact or one
-            // too large (s < 2^28, m <= 256)
-            int r = (int)(s - __umulhi(s, magic) * m);
-            r += r < 0 ? (int)m : 0;
-            if (2 * r >= (int)m) r -= (int)m;                  // balanced: [-128, 127]
-            word |= ((uint32_t)r & 0xffu) << (8 * t);
+            for (int j = 0; j < NW; ++j) s0 = __builtin_amdgcn_udot4(x[t][j], c_crt_p256[k][j], s0, false);
+            const uint32_t q = __umulhi(s0 + h, magic);
+            bal[t] = s0 - __umul24(q, m);                      // (x + h) mod m - h, two's complement
         }
-        o[k * plane] = word;
+        const uint32_t lo = __builtin_amdgcn_perm(bal[1], bal[0], 0x0c0c0400u),
+                       hi = __builtin_amdgcn_perm(bal[3], bal[2], 0x0c0c0400u);
+        o[k * plane] = lo | (hi << 16);
     }
 }
-// NH 16-bit halves of |x| per element (|x| < 2^(16 NH)) from canonical Fr cells.
-template <int NH>
+// NW words of |x| (|x| < 2^(32 NW)) from canonical Fr cells.
+template <int NW>
 __device__ __forceinline__ void residues_body(const DView& x, uint32_t rows, uint32_t kdim,
                                               uint32_t rows_pad, uint32_t kw,
                                               uint32_t* __restrict__ out, int n, uint32_t row,
                                               uint32_t kg, const Fr& half) {
     const Fr zero = fr_zero();
-    uint32_t h[4][8];
-    bool neg[4];
+    uint32_t w[4][4], nm[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const uint32_t kk = kg * 4 + t;
         Fr v = zero;
         if (row < rows && kk < kdim) v = view_load(x, zero, row, kk);
         Fr tmp;
-        neg[t] = sub256(tmp, half, v) != 0;
-        const Fr mag = neg[t] ? fr_sub(zero, v) : v;
+        const bool neg = sub256(tmp, half, v) != 0;
+        const Fr mag = neg ? fr_sub(zero, v) : v;
+        nm[t] = neg ? ~0u : 0u;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) h[t][j] = j < NH ? (mag.w[j >> 1] >> (16 * (j & 1))) & 0xffffu : 0u;
+        for (int j = 0; j < 4; ++j) w[t][j] = mag.w[j];
     }
-    residues_emit<NH>(h, neg, out + (uint64_t)row * kw + kg, (uint64_t)rows_pad * kw, n);
+    residues_emit<NW>(w, nm, out + (uint64_t)row * kw + kg, (uint64_t)rows_pad * kw, n);
 }
 // Balanced residue planes: out[k][row][kpad] int8 (= u32 words of 4 consecutive
 // k), k < n; rows >= `rows` and columns >= kdim are zero.
@@ -1355,11 +1361,11 @@ __global__ __launch_bounds__(256) void k_to_residues(const DView x, uint32_t row
     }
     const uint32_t bmax = max(max(*bits_a, *bits_b), bits_c ? *bits_c : 0u);
     if (bmax <= 64)
-        residues_body<4>(x, rows, kdim, rows_pad, kw, out, n, row, kg, half);
+        residues_body<2>(x, rows, kdim, rows_pad, kw, out, n, row, kg, half);
     else if (bmax <= 96)
-        residues_body<6>(x, rows, kdim, rows_pad, kw, out, n, row, kg, half);
+        residues_body<3>(x, rows, kdim, rows_pad, kw, out, n, row, kg, half);
     else
-        residues_body<8>(x, rows, kdim, rows_pad, kw, out, n, row, kg, half);
+        residues_body<4>(x, rows, kdim, rows_pad, kw, out, n, row, kg, half);
 }
 hipError_t launch_to_residues(const DView& x, uint32_t rows, uint32_t kdim, uint32_t rows_pad,
                               uint32_t kpad, uint32_t* out, const unsigned* bits_a,
@@ -1373,11 +1379,12 @@ hipError_t launch_to_residues(const DView& x, uint32_t rows, uint32_t kdim, uint
 }
 
 // |x_q| and sign of ZkMatrix::new's quantization (quantize_body: round half away
-// of |x| 2^P, u128 saturation, NaN -> 0, sign(x) < 0 -> p - x_q) as 16-bit halves.
-__device__ __forceinline__ void quantized_halves(double x, double scale, uint32_t (&h)[8], bool& neg) {
-    neg = signbit(x) && !isnan(x);
+// of |x| 2^P, u128 saturation, NaN -> 0, sign(x) < 0 -> p - x_q) as u32 words;
+// nm = all ones when x_q is negative (-0.0 included: its residues are 0 either way).
+__device__ __forceinline__ void quantized_words(double x, double scale, uint32_t (&w)[4], uint32_t& nm) {
+    nm = signbit(x) && !isnan(x) ? ~0u : 0u;
     const double s = round(fabs(x) * scale);
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    w[0] = w[1] = w[2] = w[3] = 0u;
     if (s >= 340282366920938463463374607431768211456.0) {
         w[0] = w[1] = w[2] = w[3] = 0xffffffffu;
     } else if (s > 0.0) {
@@ -1388,8 +1395,6 @@ __device__ __forceinline__ void quantized_halves(double x, double scale, uint32_
         w[0] = (uint32_t)v; w[1] = (uint32_t)(v >> 32);
         w[2] = (uint32_t)(v >> 64); w[3] = (uint32_t)(v >> 96);
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) h[j] = (w[j >> 1] >> (16 * (j & 1))) & 0xffffu;
 }
 // Residue planes straight from the f64 inputs of svd_witness (what k_to_residues
 // computes from the quantized cells, without reading the 32 B cells back): up to
@@ -1415,22 +1420,21 @@ __global__ __launch_bounds__(256) void k_residues_f64(const ResSegs q, const uns
     const uint64_t idx = (uint64_t)(blockIdx.x - q.blk0[s]) * blockDim.x + threadIdx.x;
     if (idx >= (uint64_t)g.rows_pad * g.kw) return;
     const uint32_t row = (uint32_t)(idx / g.kw), kg = (uint32_t)(idx % g.kw);
-    uint32_t h[4][8];
-    bool neg[4];
+    uint32_t w[4][4], nm[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const uint32_t kk = kg * 4 + t;
         const double x = row < g.rows && kk < g.cols ? g.in[(uint64_t)row * g.ld + kk] : 0.0;
-        quantized_halves(x, scale, h[t], neg[t]);
+        quantized_words(x, scale, w[t], nm[t]);
     }
     uint32_t* o = g.out + (uint64_t)row * g.kw + kg;
     const uint64_t plane = (uint64_t)g.rows_pad * g.kw;
     if (bmax <= 64)
-        residues_emit<4>(h, neg, o, plane, n);
+        residues_emit<2>(w, nm, o, plane, n);
     else if (bmax <= 96)
-        residues_emit<6>(h, neg, o, plane, n);
+        residues_emit<3>(w, nm, o, plane, n);
     else
-        residues_emit<8>(h, neg, o, plane, n);
+        residues_emit<4>(w, nm, o, plane, n);
 }
 hipError_t launch_residues_f64(const ResSegs& q0, const unsigned* W, int precision_bits,
                                hipStream_t st) {
@@ -1482,6 +1486,10 @@ __device__ __forceinline__ uint32_t crt_lds(uint32_t row, uint32_t part) {
 // per round, so K = 1024 takes 4 rounds instead of 16.
 // (block function: blk / nblk = the block's index and the block count of this
 // product's grid, mod = its modulus; the kernels below map their grids onto it)
+// LDS of one block (kernels declare it: two inlined variants sharing a kernel
+// would otherwise get an array each)
+template <int KC>
+constexpr int crt_lds_bytes() { return 2 * KC * CT * CROW > CT * CTS ? 2 * KC * CT * CROW : CT * CTS; }
 template <bool SYM, int KC>
 __device__ __forceinline__ void crt_gemm_block(const uint8_t* __restrict__ Ar,
                                                const uint8_t* __restrict__ Br, uint32_t astride,
@@ -1489,11 +1497,10 @@ __device__ __forceinline__ void crt_gemm_block(const uint8_t* __restrict__ Ar,
                                                uint32_t tiles_m, uint8_t* __restrict__ R,
                                                const unsigned* __restrict__ bits_a,
                                                const unsigned* __restrict__ bits_b, uint32_t lk,
-                                               uint32_t blk, uint32_t nblk, int mod) {
+                                               uint32_t blk, uint32_t nblk, int mod,
+                                               uint8_t* __restrict__ S) {
     const int n = crt_nmod(*bits_a, *bits_b, lk);
     if (mod >= n) return;
-    constexpr int kS = 2 * KC * CT * CROW > CT * CTS ? 2 * KC * CT * CROW : CT * CTS;
-    __shared__ __attribute__((aligned(16))) uint8_t S[kS];
     uint8_t* As = S;
     uint8_t* Bs = S + KC * CT * CROW;
     uint32_t bi, bj;
@@ -1624,8 +1631,9 @@ __global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar
                                                   uint32_t tiles_m, uint8_t* __restrict__ R,
                                                   const unsigned* __restrict__ bits_a,
                                                   const unsigned* __restrict__ bits_b, uint32_t lk) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes<KC>()];
     crt_gemm_block<SYM, KC>(Ar, Br, astride, bstride, kpad, tiles_a, tiles_m, R, bits_a, bits_b, lk,
-                            blockIdx.x, gridDim.x, (int)blockIdx.y);
+                            blockIdx.x, gridDim.x, (int)blockIdx.y, S);
 }
 // Modulus-major XCD placement (1-D grid): work unit u = (modulus u / 2, half
 // u % 2 of its tiles) runs entirely on XCD u % 8 (workgroup L goes to XCD
@@ -1645,8 +1653,9 @@ __global__ __launch_bounds__(256) void k_gemm_crt_xm(const uint8_t* __restrict__
     const uint32_t tile = (u & 1) * tpu + t;
     if (tile >= ntiles) return;
     // nblk = 1: plain row-major tile decode (no in-modulus XCD remap)
+    __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes<KC>()];
     crt_gemm_block<SYM, KC>(Ar, Br, astride, bstride, kpad, tiles_a, tiles_m, R, bits_a, bits_b, lk, tile,
-                            1, (int)(u >> 1));
+                            1, (int)(u >> 1), S);
 }
 // The products of a CrtBatch in one launch: grid.x covers every job's tile
 // blocks (job j from blk0[j], multiples of 8 so the XCD mapping holds), grid.y
@@ -1658,12 +1667,13 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
     const CrtJob& q = b.job[j];
     const uint32_t blk = blockIdx.x - q.blk0;
     if (blk >= q.nblk) return;                    // padding to a multiple of 8
+    __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes<KC>()];
     if (q.sym)
         crt_gemm_block<true, KC>(q.Ar, q.Ar, q.astride, q.astride, q.kpad, q.tiles_a, q.tiles_a, q.R,
-                                 q.bits_a, q.bits_b, q.lk, blk, q.nblk, (int)blockIdx.y);
+                                 q.bits_a, q.bits_b, q.lk, blk, q.nblk, (int)blockIdx.y, S);
     else
         crt_gemm_block<false, KC>(q.Ar, q.Br, q.astride, q.bstride, q.kpad, q.tiles_a, q.tiles_m, q.R,
-                                  q.bits_a, q.bits_b, q.lk, blk, q.nblk, (int)blockIdx.y);
+                                  q.bits_a, q.bits_b, q.lk, blk, q.nblk, (int)blockIdx.y, S);
 }
 
 // C from its n residues, written as canonical Fr to out[i*ors + j*ocs]; one
@@ -1675,10 +1685,9 @@ __device__ __forceinline__ void crt_combine_block(const uint8_t* __restrict__ R,
                                                   int64_t ors, int64_t ocs,
                                                   const unsigned* __restrict__ bits_a,
                                                   const unsigned* __restrict__ bits_b, uint32_t lk,
-                                                  uint32_t blk) {
+                                                  uint32_t blk, uint8_t* __restrict__ Ts) {
     const int n = crt_nmod(*bits_a, *bits_b, lk);
     if (!n) return;
-    __shared__ __attribute__((aligned(16))) uint8_t Ts[MT * MT * 32];
     uint32_t bi, bj;
     if (SYM) {
         uint32_t b = blk, r = 0, rowlen = tiles_m;
@@ -1706,21 +1715,32 @@ __device__ __forceinline__ void crt_combine_block(const uint8_t* __restrict__ R,
 #pragma unroll
         for (int w = 0; w < 16; ++w) acc[q][w] = 0;
     }
-    for (int k = 0; k < n; ++k) {
-        uint32_t r[4];
-        const uint32_t w4 = rp[(uint64_t)k * (plane >> 2)];
+    // the residue words of kU moduli are loaded together (one load per modulus
+    // and then a wait, as a plain loop compiles, puts n full memory latencies
+    // in a row); indices past n re-read the last plane and are not used
+    constexpr int kU = 8;
+    for (int k0 = 0; k0 < n; k0 += kU) {
+        uint32_t w4[kU];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) r[q] = (w4 >> (8 * q)) & 0xffu;
-        const double fr = c_crt_frac[off + k];
+        for (int i = 0; i < kU; ++i) w4[i] = rp[(uint64_t)min(k0 + i, n - 1) * (plane >> 2)];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s[q] = fma((double)r[q], fr, s[q]);
+        for (int i = 0; i < kU; ++i) {
+            const int k = k0 + i;
+            if (k >= n) break;
+            uint32_t r[4];
 #pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            const uint32_t e = c_crt_ep[off + k][w], lo = e & 0xffffu, hi = e >> 16;
+            for (int q = 0; q < 4; ++q) r[q] = (w4[i] >> (8 * q)) & 0xffu;
+            const double fr = c_crt_frac[off + k];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                acc[q][2 * w] = __umul24(r[q], lo) + acc[q][2 * w];
-                acc[q][2 * w + 1] = __umul24(r[q], hi) + acc[q][2 * w + 1];
+            for (int q = 0; q < 4; ++q) s[q] = fma((double)r[q], fr, s[q]);
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                const uint32_t e = c_crt_ep[off + k][w], lo = e & 0xffffu, hi = e >> 16;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    acc[q][2 * w] = __umul24(r[q], lo) + acc[q][2 * w];
+                    acc[q][2 * w + 1] = __umul24(r[q], hi) + acc[q][2 * w + 1];
+                }
             }
         }
     }
@@ -1775,7 +1795,8 @@ __global__ __launch_bounds__(256) void k_crt_combine(const uint8_t* __restrict__
     // tiles read from the same 128-byte lines of R come through one L2.
     const uint32_t g = gridDim.x, b = blockIdx.x;
     const uint32_t blk = (g & 7) == 0 ? (b & 7) * (g >> 3) + (b >> 3) : b;
-    crt_combine_block<SYM>(R, rpad_a, rpad_b, N, M, tiles_m, out, ors, ocs, bits_a, bits_b, lk, blk);
+    __shared__ __attribute__((aligned(16))) uint8_t Ts[MT * MT * 32];
+    crt_combine_block<SYM>(R, rpad_a, rpad_b, N, M, tiles_m, out, ors, ocs, bits_a, bits_b, lk, blk, Ts);
 }
 __global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b) {
     uint32_t j = 0;
@@ -1783,12 +1804,13 @@ __global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b) {
     const CrtJob& q = b.job[j];
     const uint32_t blk = blockIdx.x - q.cblk0;
     const uint32_t rpa = q.tiles_a * CT, rpb = (q.sym ? q.tiles_a : q.tiles_m) * CT;
+    __shared__ __attribute__((aligned(16))) uint8_t Ts[MT * MT * 32];
     if (q.sym)
         crt_combine_block<true>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
-                                q.bits_b, q.lk, blk);
+                                q.bits_b, q.lk, blk, Ts);
     else
         crt_combine_block<false>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
-                                 q.bits_b, q.lk, blk);
+                                 q.bits_b, q.lk, blk, Ts);
 }
 
 hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {

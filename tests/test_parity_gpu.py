@@ -406,6 +406,38 @@ def test_row_sharded_device_inputs_parity(gpu_ctx_factory, N, M, P, world):
         assert bad.size == 0, f"{key}: {bad.size} cells differ, first at {bad[:8]}"
 
 
+@pytest.mark.parametrize("world,opts", [(1, {"prod_cell": 1}), (1, {"prod_cell": 1, "stage_batch": 0}),
+                                        (1, {"prod_cell": 1, "p1_at": 1}), (1, {"prod_cell": 1, "hold_us": 50}),
+                                        (3, {"prod_cell": 0}), (3, {"prod_cell": 1, "stage_batch": 0}),
+                                        (4, {"prod_cell": 1, "gemm_batch": 0})])
+def test_products_on_cell_stream_parity(gpu_ctx_factory, world, opts):
+    """prod_cell: the products on the cell stream, the u / v bounds and u.d on
+    st2 beside them (default on row-sharded ranks), with device inputs (the
+    only path it applies to): bit-identical to the oracle, sharded or not."""
+    import halo2_svd041_amd as hs
+    N, M, P = 70, 53, 63
+    m, u, d, v = gen_svd_input(N, M, seed=world + 90)
+    g = gamma_for(world + 90)
+    dm, du, dv, dd = _on_device(m, u, v, d)
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+    ctxs = []
+    for rank in range(world):
+        ctx = gpu_ctx_factory(P)
+        if world > 1:
+            ctx.set_shard(rank, world)
+        for k, val in opts.items():
+            ctx.set_option(k, val)
+        counts = hs.svd_witness(ctx, dm, du, dv, dd, g)
+        ctxs.append(ctx)
+    if world == 1:
+        _assert_streams(ctxs[0], a0, l0, a1)
+        return
+    got = _reassemble(ctxs, counts)
+    for key, want in (((0, 0), a0), ((1, 0), a1), ((0, 1), l0)):
+        bad = np.nonzero(np.any(got[key] != want, axis=1))[0]
+        assert bad.size == 0, f"{key}: {bad.size} cells differ, first at {bad[:8]}"
+
+
 # Regions of a witness that the C oracle's sampled mode (row_lim) truncates to
 # their first row_lim rows; every other region it computes in full.
 _ROW_LIMITED = {"check_mat_entries_bounded", "mat_times_diag_mat", "product", "check_mat_diff",
