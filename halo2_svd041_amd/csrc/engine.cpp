@@ -457,7 +457,7 @@ struct svdw_ctx {
     bool gemm_xm = true;                    // "gemm_xm": CRT GEMM units (modulus, half) placed per XCD
     int res_first = 0;                      // "res_first": cell stream waits for the residue planes
                                             // (1), not (0), -1: on row-sharded ranks
-    int gemm_batch = -1;                    // "gemm_batch": svd_witness's three products in one launch
+    int gemm_batch = 1;                     // "gemm_batch": svd_witness's three products in one launch
                                             // (1), one by one (0), or -1: batched on row-sharded ranks
     bool fused_quantize = true;             // "fused_quantize": m, u, v, d in one launch
     bool res_f64 = true;                    // "res_f64": CRT residue planes of m, u, v from the
@@ -1983,6 +1983,8 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
                            (const uint8_t*)c->digB.p};                 // A planes of m, u, v
     const uint32_t stride[3] = {rp_m, rp_u, rp_v}, kp[3] = {kpM, kpN, kpM}, lk[3] = {lkM, lkN, lkM};
     const int wa[3] = {0, 1, 2}, wb[3] = {2, 1, 2};
+    // one launch each for the three GEMMs and combines (same box, tools/probe_opts.sh:
+    // 512^2 P=32 0.43 -> 0.41 ms, 1024^2 P=63 2.10 -> 2.07 ms; row-sharded ranks too)
     if (c->gemm_batch > 0 || (c->gemm_batch < 0 && sharded(c))) {
         // the three products in one GEMM launch and one combine launch (each its
         // own residue scratch): one step of the st2 chain instead of three

@@ -258,8 +258,10 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   "stage_batch" 1 | 0 (independent stages share k_stage_multi launches: the
  *   u / v bounds and u.d, the d checks and constant cells, verify_mul's one cells
  *   and gamma powers, the is_equal rows; split automatically where a stage reads
- *   cells a pending one writes); "gemm_batch" -1 | 0 | 1 (svd_witness's three
- *   products in one GEMM and one combine launch: -1 on row-sharded contexts);
+ *   cells a pending one writes); "gemm_batch" 1 | 0 | -1 (svd_witness's three
+ *   products in one GEMM and one combine launch; -1: on row-sharded contexts); "prod_cell" -1 | 0 | 1 (svd_witness with
+ *   device inputs: the products on the cell stream and the u / v bounds and u.d
+ *   beside them; -1 on row-sharded contexts);
  *   "gemm_kc" 1 | 4 (64-k chunks per LDS round of the CRT GEMM); "gemm_xm"
  *   1 | 0 (unbatched CRT GEMMs: XCD-major modulus placement, so each residue
  *   plane is read through two XCDs' L2 rather than all eight); "res_first"
