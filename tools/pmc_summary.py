@@ -65,7 +65,7 @@ def main():
     # bench.py's event profiler aggregates every stage launch (k_stage and the
     # batched k_stage_multi) under "k_stage": the same aggregate per launch here
     parts = {k: v for k, v in out["kernels"].items() if k.startswith("k_stage")}
-    if len(parts) > 1:
+    if parts and "k_stage" not in parts or len(parts) > 1:
         n = sum(v["dispatches"] for v in parts.values())
         rd = sum(v["read_bytes_per_launch"] * v["dispatches"] for v in parts.values())
         wr = sum(v["write_bytes_per_launch"] * v["dispatches"] for v in parts.values())
