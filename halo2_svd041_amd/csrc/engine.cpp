@@ -500,6 +500,8 @@ struct svdw_ctx {
     DBuf bvfull[kMaxScanJobs];              // shard mode: full b.g values per verify_mul
     // second stream: GEMMs overlap the HBM-bound stages; third: phase 1
     hipStream_t st2 = nullptr;
+    bool st2_hi = false;                    // st2 is the high-priority stream
+    int gemm_prio = -1;                     // "gemm_priority": -1 auto, 0 normal, 1 high
     hipStream_t st3 = nullptr;
     hipStream_t st_cell = nullptr;          // the cell stream proper (st is swapped at times)
     bool overlap = true;
@@ -571,6 +573,35 @@ static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
     hipck(hipEventRecord(e, from), "hipEventRecord");
     if (to) hipck(hipStreamWaitEvent(to, e, 0), "hipStreamWaitEvent");
     return e;
+}
+// The second stream at high or normal dispatch priority: on a change the queued
+// work drains and st2 is re-created (one second stream at a time: an idle twin
+// kept beside it measured 2.7x slower at 512^2 under bench.py's event profiler).
+static void pick_st2(svdw_ctx* c, bool hi) {
+    if (c->dry || hi == c->st2_hi) return;
+    sync(c);
+    hipStream_t s;
+    if (hi) {
+        int lo = 0, top = 0;
+        hipck(hipDeviceGetStreamPriorityRange(&lo, &top), "hipDeviceGetStreamPriorityRange");
+        hipck(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, top), "hipStreamCreateWithPriority");
+    } else {
+        hipck(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    }
+    hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
+    c->st2 = s;
+    c->st2_hi = hi;
+}
+// gemm_priority auto (-1): high for unsharded witnesses with 512 <= max(N, M)
+// < 1024, where the product chain on st2 is the critical path (the cell stream
+// idles ~40 us waiting for the combine at 512^2 P=32). bench.py lines, same box
+// (tools/check_gp2.sh): 512^2 P=32 0.424 -> 0.416 ms; 256^2 P=32 0.189 -> 0.194
+// ms (so off below 512); 1024^2 and 2048 x 1024 within 0.5 % (tools/probe_gp.sh);
+// 8-way shard rank 0.378 -> 0.383 ms (tools/probe_r02b.sh), off when sharded.
+static void apply_gemm_prio(svdw_ctx* c, uint32_t N, uint32_t M) {
+    const bool sharded_ctx = c->shard_world > 1;
+    const uint32_t mx = std::max(N, M);
+    pick_st2(c, c->gemm_prio > 0 || (c->gemm_prio < 0 && !sharded_ctx && mx >= 512 && mx < 1024));
 }
 static bool same_cells(const svdw_mat& a, const svdw_mat& b) {
     if (a.phase != b.phase || a.off != b.off) return false;
@@ -2292,6 +2323,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     host_mark(c, "svd_witness start");
     clear_streams(c);
     c->dep_next = 0;
+    if (!c->dry) apply_gemm_prio(c, N, M);
     c->prelaunched = false;
     c->prod_on_cell = false;
     c->gemm_batched = false;
@@ -3617,22 +3649,10 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                              (value == 1 ? STAGE_PROBE_NOA : value == 2 ? STAGE_PROBE_CONST
                               : value == 3 ? (STAGE_PROBE_CONST | STAGE_PROBE_NOLD) : 0);
         } else if (n == "gemm_priority") {
-            // second (GEMM) stream priority: 0 normal, 1 high
-            REQUIRE(value == 0 || value == 1, "gemm_priority: 0 or 1");
-            if (!c->dry) {
-                sync(c);
-                int lo = 0, hi = 0;
-                hipck(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
-                (void)lo;                                  // 0: the default priority
-                hipStream_t s;
-                if (value)
-                    hipck(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi),
-                          "hipStreamCreateWithPriority");
-                else
-                    hipck(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
-                hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
-                c->st2 = s;
-            }
+            // second (GEMM) stream priority: -1 auto (see apply_gemm_prio), 0 normal, 1 high
+            REQUIRE(value >= -1 && value <= 1, "gemm_priority: -1, 0 or 1");
+            c->gemm_prio = (int)value;
+            if (value >= 0) pick_st2(c, value == 1);
         } else if (n == "prod_cell") {
             REQUIRE(value >= -1 && value <= 1, "prod_cell: -1, 0 or 1");
             c->prod_cell = (int)value;
@@ -3665,6 +3685,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             // XCDs whether the mask order is XCD-major or XCD-interleaved.
             REQUIRE(value >= 0 && value % 8 == 0, "cu_split: a multiple of 8, >= 0");
             if (!c->dry) {
+                c->st2_hi = false;                // (re-created below at normal priority)
+                c->gemm_prio = 0;
                 hipDeviceProp_t prop;
                 hipck(hipGetDeviceProperties(&prop, c->device), "hipGetDeviceProperties");
                 const uint32_t ncu = (uint32_t)prop.multiProcessorCount;

@@ -238,8 +238,9 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   (with phase 1 on the third stream: queued after the first 0 / 1 / 2
  *   phase-0 stages, 3 after all of phase 0; -1: 0 on a rank of a >= 4-way shard, 3 of a
  *   2-3-way shard, else 1); "prelaunch_at" 0 | 1 | 2 (how many phase-0 stages
- *   are queued before them); "gemm_priority" 0 | 1 (second stream priority:
- *   default | high); "stage_priority" 0 | 1 (cell stream priority);
+ *   are queued before them); "gemm_priority" -1 | 0 | 1 (second stream priority:
+ *   -1 auto = high for unsharded witnesses with 512 <= max(N, M) < 1024, where
+ *   the product chain is the critical path; 0 normal; 1 high); "stage_priority" 0 | 1 (cell stream priority);
  *   "cu_split" 0 | multiple of 8 (CUs masked to the second stream, the rest to
  *   the cell stream); "fused_quantize" 1 | 0 (m, u, v, d quantized in one
  *   launch when resident in HBM);

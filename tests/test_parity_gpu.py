@@ -172,7 +172,8 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                                   {"phase1_overlap": 0}, {"phase1_overlap": 2},
                                   {"stage_align": 0}, {"stage_align": 0, "stage_elems": 64},
                                   {"overlap": 0}, {"stage_inc": 1}, {"stage_priority": 1},
-                                  {"gemm_priority": 1}, {"cu_split": 64}, {"fused_quantize": 0}, {"d_checks_aside": 0},
+                                  {"gemm_priority": 1}, {"gemm_priority": 0}, {"gemm_priority": 1, "cu_split": 64},
+                                  {"cu_split": 64}, {"fused_quantize": 0}, {"d_checks_aside": 0},
                                   {"scan_na_host": 1}, {"scan_impl": 5, "phase1_overlap": 2},
                                   {"stage_batch": 0}, {"gemm_batch": 0}, {"gemm_kc": 4},
                                   {"gemm_batch": 1, "gemm_kc": 4}, {"res_first": 1}, {"stage_persist": 1},
@@ -189,6 +190,22 @@ def test_tuning_options_parity(gpu_ctx_factory, opts):
     hs.svd_witness(ctx, m, u, v, d, g)
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
     _assert_streams(ctx, a0, l0, a1)
+
+
+def test_gemm_priority_switch_parity(gpu_ctx_factory):
+    """The auto product-stream priority (high below 1024, normal from 1024 on)
+    switches st2 between two streams across witnesses of one context; every
+    witness stays bit-identical to the oracle, whichever stream it ran on."""
+    import halo2_svd041_amd as hs
+    P = 63
+    ctx = gpu_ctx_factory(P)
+    for (N, M, seed, prio) in [(45, 37, 4, -1), (33, 52, 5, 0), (40, 40, 6, -1), (38, 29, 7, 1)]:
+        ctx.set_option("gemm_priority", prio)
+        m, u, d, v = gen_svd_input(N, M, seed=seed)
+        g = gamma_for(seed)
+        hs.svd_witness(ctx, m, u, v, d, g)
+        a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+        _assert_streams(ctx, a0, l0, a1)
 
 
 @pytest.mark.parametrize("impl", [4, 1])
