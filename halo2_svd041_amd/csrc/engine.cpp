@@ -457,6 +457,8 @@ struct svdw_ctx {
     bool gemm_xm = true;                    // "gemm_xm": CRT GEMM units (modulus, half) placed per XCD
     int res_first = 0;                      // "res_first": cell stream waits for the residue planes
                                             // (1), not (0), -1: on row-sharded ranks
+    int comb_direct = 1;                    // "comb_direct": batched CRT combine without symmetric
+                                            // jobs stores from registers, no LDS (1) or via LDS (0)
     int gemm_batch = 1;                     // "gemm_batch": svd_witness's three products in one launch
                                             // (1), one by one (0), or -1: batched on row-sharded ranks
     bool fused_quantize = true;             // "fused_quantize": m, u, v, d in one launch
@@ -2022,6 +2024,7 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
         CrtBatch b;
         memset(&b, 0, sizeof b);
         b.kc = c->gemm_kc;
+        b.direct = c->comb_direct;
         size_t rbytes[3], rtot = 0;
         for (int g = 0; g < 3; ++g) {
             rbytes[g] = (size_t)kCrtMaxResidues * ceil_to(std::max<uint32_t>((uint32_t)(rr1[g] - rr0[g]), 1), 128) *
@@ -3737,6 +3740,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_xm = value != 0;
         } else if (n == "stage_persist") {
             c->stage_persist = value != 0;
+        } else if (n == "comb_direct") {
+            c->comb_direct = value != 0;
         } else if (n == "gemm_batch") {
             REQUIRE(value >= -1 && value <= 1, "gemm_batch: -1 (auto), 0 or 1");
             c->gemm_batch = (int)value;

@@ -1678,7 +1678,7 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
 
 // C from its n residues, written as canonical Fr to out[i*ors + j*ocs]; one
 // 32 x 32 tile per block (SYM: upper tiles, mirrored through LDS).
-template <bool SYM>
+template <bool SYM, bool DIRECT = false>
 __device__ __forceinline__ void crt_combine_block(const uint8_t* __restrict__ R, uint32_t rpad_a,
                                                   uint32_t rpad_b, uint32_t N, uint32_t M,
                                                   uint32_t tiles_m, Fr* __restrict__ out,
@@ -1760,10 +1760,23 @@ __device__ __forceinline__ void crt_combine_block(const uint8_t* __restrict__ R,
         x[8] = (uint32_t)t;
         const Fr v = reduce9(x);
         const uint32_t tc = tc0 + q;
+        if (DIRECT) {
+            // straight from registers: a thread's 4 elements are 128 contiguous
+            // bytes of a row-major product (no LDS, so the blocks fit beside
+            // resident stage blocks)
+            const uint32_t row = i0 + tr, col = j0 + tc;
+            if (row < N && col < M) {
+                uint4* dst = reinterpret_cast<uint4*>(out + (int64_t)row * ors + (int64_t)col * ocs);
+                dst[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+                dst[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+            }
+            continue;
+        }
         uint4* dst = reinterpret_cast<uint4*>(Ts + (tr * MT + tc) * 32);
         dst[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
         dst[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
     }
+    if (DIRECT) return;
     __syncthreads();
     for (uint32_t q = tid; q < MT * 64; q += 256) {
         const uint32_t tr = q >> 6, hc = q & 63, tc = hc >> 1, h = hc & 1;
@@ -1813,6 +1826,18 @@ __global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b) {
                                  q.bits_b, q.lk, blk, Ts);
 }
 
+// Batches without a symmetric job (a row-sharded rank's row blocks): the same
+// combine with direct stores and no LDS ("comb_direct").
+__global__ __launch_bounds__(256) void k_crt_combine_multi_d(const CrtBatch b) {
+    uint32_t j = 0;
+    for (uint32_t k = 1; k < b.njobs; ++k) j += blockIdx.x >= b.job[k].cblk0;
+    const CrtJob& q = b.job[j];
+    const uint32_t blk = blockIdx.x - q.cblk0;
+    const uint32_t rpa = q.tiles_a * CT, rpb = q.tiles_m * CT;
+    crt_combine_block<false, true>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
+                                   q.bits_b, q.lk, blk, nullptr);
+}
+
 hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
     CrtBatch b = b0;
     if (b.njobs < 1 || b.njobs > (uint32_t)kMaxCrtJobs) return hipErrorInvalidValue;
@@ -1838,7 +1863,12 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
         hipLaunchKernelGGL(k_gemm_crt_multi<1>, dim3(blocks, kCrtMaxMod), dim3(256), 0, st, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_crt_combine_multi, dim3(cblocks), dim3(256), 0, st, b);
+    bool any_sym = false;
+    for (uint32_t j = 0; j < b.njobs; ++j) any_sym |= b.job[j].sym != 0;
+    if (b.direct && !any_sym)
+        hipLaunchKernelGGL(k_crt_combine_multi_d, dim3(cblocks), dim3(256), 0, st, b);
+    else
+        hipLaunchKernelGGL(k_crt_combine_multi, dim3(cblocks), dim3(256), 0, st, b);
     return hipGetLastError();
 }
 

@@ -293,6 +293,7 @@ struct CrtBatch {
     CrtJob job[kMaxCrtJobs];
     uint32_t njobs;
     int kc;
+    int direct;          // combine stores from registers (no LDS) when no job is symmetric
 };
 hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st);
 // w (len L) from a view (row 0 / col j of a 1 x L view) -> canonical copy
