@@ -457,8 +457,12 @@ struct svdw_ctx {
     bool gemm_xm = true;                    // "gemm_xm": CRT GEMM units (modulus, half) placed per XCD
     int res_first = 0;                      // "res_first": cell stream waits for the residue planes
                                             // (1), not (0), -1: on row-sharded ranks
-    int comb_direct = 1;                    // "comb_direct": batched CRT combine without symmetric
-                                            // jobs stores from registers, no LDS (1) or via LDS (0)
+    int comb_direct = 1;                    // "comb_direct": batched CRT combine stores from registers
+                                            // (no LDS) for batches without symmetric jobs (1), for
+                                            // every batch (2), or always via LDS (0). 2 measured
+                                            // slower (mirror stores of symmetric tiles scatter):
+                                            // 512^2 P=32 0.411-0.418 -> 0.426-0.428 ms, 1024^2
+                                            // 2.07-2.08 -> 2.08-2.09 ms (tools/probe_comb.sh)
     int gemm_batch = 1;                     // "gemm_batch": svd_witness's three products in one launch
                                             // (1), one by one (0), or -1: batched on row-sharded ranks
     bool fused_quantize = true;             // "fused_quantize": m, u, v, d in one launch
@@ -3741,7 +3745,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "stage_persist") {
             c->stage_persist = value != 0;
         } else if (n == "comb_direct") {
-            c->comb_direct = value != 0;
+            REQUIRE(value >= 0 && value <= 2, "comb_direct: 0, 1 or 2");
+            c->comb_direct = (int)value;
         } else if (n == "gemm_batch") {
             REQUIRE(value >= -1 && value <= 1, "gemm_batch: -1 (auto), 0 or 1");
             c->gemm_batch = (int)value;

@@ -1770,6 +1770,11 @@ __device__ __forceinline__ void crt_combine_block(const uint8_t* __restrict__ R,
                 dst[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
                 dst[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
             }
+            if (SYM && bi != bj && col < N && row < M) {     // mirrored tile: (col, row)
+                uint4* mir = reinterpret_cast<uint4*>(out + (int64_t)col * ors + (int64_t)row * ocs);
+                mir[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+                mir[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+            }
             continue;
         }
         uint4* dst = reinterpret_cast<uint4*>(Ts + (tr * MT + tc) * 32);
@@ -1826,16 +1831,21 @@ __global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b) {
                                  q.bits_b, q.lk, blk, Ts);
 }
 
-// Batches without a symmetric job (a row-sharded rank's row blocks): the same
-// combine with direct stores and no LDS ("comb_direct").
+// The same combine with direct stores and no LDS ("comb_direct"): 1 for batches
+// without a symmetric job (a row-sharded rank's row blocks), 2 for every batch
+// (symmetric tiles then store their mirror image element by element).
 __global__ __launch_bounds__(256) void k_crt_combine_multi_d(const CrtBatch b) {
     uint32_t j = 0;
     for (uint32_t k = 1; k < b.njobs; ++k) j += blockIdx.x >= b.job[k].cblk0;
     const CrtJob& q = b.job[j];
     const uint32_t blk = blockIdx.x - q.cblk0;
-    const uint32_t rpa = q.tiles_a * CT, rpb = q.tiles_m * CT;
-    crt_combine_block<false, true>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
-                                   q.bits_b, q.lk, blk, nullptr);
+    const uint32_t rpa = q.tiles_a * CT, rpb = (q.sym ? q.tiles_a : q.tiles_m) * CT;
+    if (q.sym)
+        crt_combine_block<true, true>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
+                                      q.bits_b, q.lk, blk, nullptr);
+    else
+        crt_combine_block<false, true>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
+                                       q.bits_b, q.lk, blk, nullptr);
 }
 
 hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
@@ -1865,7 +1875,7 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
     if (e != hipSuccess) return e;
     bool any_sym = false;
     for (uint32_t j = 0; j < b.njobs; ++j) any_sym |= b.job[j].sym != 0;
-    if (b.direct && !any_sym)
+    if (b.direct >= 2 || (b.direct == 1 && !any_sym))
         hipLaunchKernelGGL(k_crt_combine_multi_d, dim3(cblocks), dim3(256), 0, st, b);
     else
         hipLaunchKernelGGL(k_crt_combine_multi, dim3(cblocks), dim3(256), 0, st, b);

@@ -172,7 +172,7 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                                   {"phase1_overlap": 0}, {"phase1_overlap": 2},
                                   {"stage_align": 0}, {"stage_align": 0, "stage_elems": 64},
                                   {"overlap": 0}, {"stage_inc": 1}, {"stage_priority": 1},
-                                  {"gemm_priority": 1}, {"gemm_priority": 0}, {"gemm_priority": 1, "cu_split": 64},
+                                  {"gemm_priority": 1}, {"gemm_priority": 0}, {"comb_direct": 2}, {"gemm_priority": 1, "cu_split": 64},
                                   {"cu_split": 64}, {"fused_quantize": 0}, {"d_checks_aside": 0},
                                   {"scan_na_host": 1}, {"scan_impl": 5, "phase1_overlap": 2},
                                   {"stage_batch": 0}, {"gemm_batch": 0}, {"gemm_kc": 4},
@@ -427,7 +427,7 @@ def test_row_sharded_device_inputs_parity(gpu_ctx_factory, N, M, P, world):
                                         (1, {"prod_cell": 1, "p1_at": 1}), (1, {"prod_cell": 1, "hold_us": 50}),
                                         (3, {"prod_cell": 0}), (3, {"prod_cell": 1, "stage_batch": 0}),
                                         (4, {"prod_cell": 1, "gemm_batch": 0}), (1, {"gemm_batch": 0}),
-                                        (1, {"gemm_batch": 0, "gemm_xm": 0}), (3, {"comb_direct": 0}),
+                                        (1, {"gemm_batch": 0, "gemm_xm": 0}), (3, {"comb_direct": 0}), (1, {"comb_direct": 2}), (2, {"comb_direct": 2}),
                                         (5, {"comb_direct": 1, "prod_cell": 0})])
 def test_products_on_cell_stream_parity(gpu_ctx_factory, world, opts):
     """prod_cell: the products on the cell stream, the u / v bounds and u.d on
