@@ -303,10 +303,11 @@ def main():
                     help="N>1: one matrix row-block sharded over the ranks (default; strong "
                          "scaling, BASELINE config 4) or one matrix per rank (weak scaling, "
                          "config 5)")
-    ap.add_argument("--gather", choices=["none", "root", "all"], default="none",
+    ap.add_argument("--gather", choices=["auto", "none", "root", "all"], default="auto",
                     help="--shard rows: also time reassembling the witness after each step "
                          "(RCCL gather to rank 0 or all-gather), reported beside the "
-                         "witness-only value")
+                         "witness-only value as the `reassembly` record (auto: root in "
+                         "rows mode)")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the untimed device constraint check of the last witness")
     ap.add_argument("--no-ingest", action="store_true",
@@ -335,6 +336,7 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     shard = args.shard or ("rows" if world > 1 and svd else "replicas")
     rows_mode = shard == "rows" and world > 1
+    gather = args.gather if args.gather != "auto" else ("root" if rows_mode else "none")
     if rows_mode and not svd:
         raise SystemExit("bench.py: --shard rows is the SVD witness's row-block sharding")
 
@@ -432,27 +434,40 @@ def main():
                         "note": "exact Fr GEMMs (residues + int8 MFMA GEMMs + CRT), streams serialised"}
 
     reasm = None
-    if rows_mode and args.gather != "none" and not args.dry:
+    if rows_mode and gather != "none":
         # witness + reassembly per step, timed like the witness-only loop
+        # (scaling reported with and without reassembly); --dry: the
+        # same plan and grouped exchange over gloo on host buffers
         from halo2_svd041_amd import collect
-        mode = "gather" if args.gather == "root" else "all_gather"
+        mode = "gather" if gather == "root" else "all_gather"
         plan = collect.plan(ctx, rank, world, mode)
-        collect.reassemble(ctx, plan)                    # warm the communicator
+        if args.dry:
+            sizes = {(0, 0): cnt["advice0"], (1, 0): cnt["advice1"],
+                     (0, 1): cnt["lookup0"], (1, 1): cnt["lookup1"]}
+            host = {k: torch.zeros((n, 32), dtype=torch.uint8) for k, n in sizes.items()}
+            reassemble = lambda: collect.exchange(host, plan)             # noqa: E731
+        else:
+            reassemble = lambda: collect.reassemble(ctx, plan)           # noqa: E731
+        reassemble()                                     # warm the communicator
         dist.barrier()
         sync()
         t1 = time.perf_counter()
         for g in gammas:
             wl.step(g)
-            collect.reassemble(ctx, plan)
+            reassemble()
         sync()
         dist.barrier()
         el2 = time.perf_counter() - t1
         el2, _ = reduce_over_ranks(el2, 0, dist, red_dev)
-        reasm = {"mode": mode, "collectives_per_step": plan.collectives,
+        reasm = {"mode": mode, "root": 0 if mode == "gather" else None,
+                 "collectives_per_step": plan.collectives,
                  "ms_per_step_with_reassembly": round(el2 / args.steps * 1e3, 4),
                  "value_with_reassembly": round(cells_step * args.steps / el2, 1),
                  "reassembly_ms": round((el2 - elapsed) / args.steps * 1e3, 4),
-                 "moved_GB_per_step": round(plan.moved_cells * 32 / 1e9, 3)}
+                 "moved_GB_per_step": round(plan.moved_cells * 32 / 1e9, 3),
+                 "note": "witness then its stream-ordered reassembly over "
+                         + ("gloo (dry rehearsal, host buffers)" if args.dry else "RCCL")
+                         + ", max over ranks"}
 
     # Untimed: the device constraint checker over the last witness (svdw_check_gates;
     # a row-sharded rank checks the rows it owns), summed over the ranks.
@@ -505,6 +520,12 @@ def main():
                           "of values, as the reference reads data/matrix.in), text resident in HBM"}
         del tt, parsed
 
+    rank_ms = None
+    if dist is not None:
+        t = torch.zeros(world, dtype=torch.float64, device=red_dev)
+        t[rank] = elapsed / args.steps * 1e3
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        rank_ms = [round(x, 4) for x in t.tolist()]
     elapsed, cells_all = reduce_over_ranks(elapsed, cells_step, dist, red_dev)
     if rows_mode:
         cells_all = float(cells_step)        # one witness, split over the ranks
@@ -540,12 +561,30 @@ def main():
                 "advice_cells_per_step": cells_step,
                 "lookup_cells_per_step": cnt["lookup0"] + cnt["lookup1"],
                 "parallelism": (f"row blocks x{world} of one matrix (witness kept sharded; "
-                                f"reassembly timed separately with --gather)"
+                                f"its reassembly timed in the `reassembly` record)"
                                 if rows_mode else f"replicas x{world} (no data-path collective)"),
                 "ranks": world,
                 "backend": backend if world > 1 else None,
             },
         }
+        # SURVEY.md §8(d) stage (i): the whole witness against HBM, algorithmic
+        # bytes = 32 B per advice + lookup cell + 8 B per f64 input entry; with
+        # N GPUs against N x peak (the node's aggregate HBM roofline)
+        nin = (N * M + N * N + M * M + min(N, M)) if svd else (N * N + N * M)
+        step_bytes = 32 * (cells_step + cnt["lookup0"] + cnt["lookup1"]) + 8 * nin
+        ach = step_bytes / (elapsed / args.steps) / 1e9
+        peak_all = HBM_PEAK_GBS * (world if rows_mode else 1)
+        step = {"bytes": step_bytes, "achieved": round(ach, 1), "peak": peak_all,
+                "frac": round(ach / peak_all, 4),
+                "note": ("one witness row-sharded over %d GPUs: its bytes / ms_per_step / "
+                         "(%d x peak)" % (world, world)) if rows_mode else
+                        "whole witness per step (all kernels, all streams)"}
+        if rows_mode and rank_ms:
+            step["rank_ms_min"] = min(rank_ms)
+            step["rank_ms_max"] = max(rank_ms)
+            step["rank_ms"] = rank_ms
+        if world > 1 and not rows_mode:           # replicas: every rank its own witness
+            step["note"] = "each rank's whole witness per step against one GPU's peak"
         if stats:
             kname, roof, breakdown = roofline_from_profile(stats, args.steps)
             traffic, src = (None, None) if rows_mode else pmc_traffic(
@@ -560,19 +599,14 @@ def main():
                 roof["standalone"] = {k: solo[k] for k in ("achieved", "frac", "avg_launch_ms")}
                 roof["standalone"]["note"] = ("same kernel, one extra untimed step with the "
                                               "streams serialised (no concurrent products/scans)")
-            # SURVEY.md §8(d) stage (i): the whole step against HBM, algorithmic
-            # bytes = 32 B per advice + lookup cell + 8 B per f64 input entry
-            if not rows_mode:
-                nin = (N * M + N * N + M * M + min(N, M)) if svd else (N * N + N * M)
-                step_bytes = 32 * (cells_step + cnt["lookup0"] + cnt["lookup1"]) + 8 * nin
-                ach = step_bytes / (elapsed / args.steps) / 1e9
-                roof["step"] = {"bytes": step_bytes, "achieved": round(ach, 1),
-                                "frac": round(ach / roof["peak"], 4),
-                                "note": "whole witness per step (all kernels, all streams)"}
-            out["roofline"] = roof
             if args.breakdown:
                 print(json.dumps({"ms_per_step_by_kernel": breakdown,
                                   "stats": stats}, indent=1), file=sys.stderr)
+        else:                                     # (--dry / --no-profile: no kernel events)
+            roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": None, "traffic": None, "kernel": None}
+        roof["step"] = step
+        out["roofline"] = roof
         if gemm is not None:
             out["field_gemm"] = gemm
         if ingest is not None:

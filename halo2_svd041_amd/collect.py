@@ -80,13 +80,17 @@ def coalesce(segs: Sequence[Segment]) -> List[Segment]:
 _plan_cache: Dict[tuple, List[Segment]] = {}
 
 
-def planned_segments(N: int, M: int, P: int, LB: int, world: int, cfg=None) -> List[Segment]:
+def planned_segments(N: int, M: int, P: int, LB: int, world: int, cfg=None,
+                      layout_opts=None) -> List[Segment]:
     """Every rank's owned segments of a row-sharded svd_witness (N x M, P, LB)
     from the dry planner (Context(device=-1)), coalesced, in an order every
-    rank computes identically."""
+    rank computes identically. layout_opts: the engine options of the witness
+    that move cells (zk.LAYOUT_OPTIONS, e.g. rlc_prefix), replayed on the dry
+    contexts."""
     from . import zk
     cfg = cfg or zk.SvdConfigPy()
-    key = (N, M, P, LB, world, cfg.max_norm, cfg.eps_svd, cfg.eps_u, cfg.max_bits_d)
+    opts = tuple(sorted((layout_opts or {}).items()))
+    key = (N, M, P, LB, world, cfg.max_norm, cfg.eps_svd, cfg.eps_u, cfg.max_bits_d, opts)
     if key not in _plan_cache:
         r_ = min(N, M)
         m, u, v, d = np.zeros((N, M)), np.zeros((N, N)), np.zeros((M, M)), np.zeros(r_)
@@ -94,6 +98,8 @@ def planned_segments(N: int, M: int, P: int, LB: int, world: int, cfg=None) -> L
         for r in range(world):
             c = zk.Context(device=-1, precision_bits=P, lookup_bits=LB)
             try:
+                for name, val in opts:
+                    c.set_option(name, val)
                 c.set_shard(r, world)
                 zk.svd_witness(c, m, u, v, d, 1, cfg)
                 segs += [(r, ph, lk, off, n) for ph, lk, off, n in c.shard_segments() if n]
@@ -124,7 +130,8 @@ def plan(ctx, rank: int, world: int, mode: str = "gather", root: int = 0) -> Pla
     if last is None:
         raise RuntimeError("collect.plan needs a row-sharded svd_witness on this context first")
     N, M, cfg = last
-    segs = planned_segments(N, M, ctx.precision_bits, ctx.lookup_bits, world, cfg)
+    segs = planned_segments(N, M, ctx.precision_bits, ctx.lookup_bits, world, cfg,
+                            getattr(ctx, "layout_opts", None))
     mine = coalesce([(rank, ph, lk, off, n) for ph, lk, off, n in ctx.shard_segments() if n])
     if mine != [s for s in segs if s[0] == rank]:
         raise RuntimeError("collect.plan: the context's shard segments differ from the planner's")
@@ -170,12 +177,15 @@ def exchange(streams: Dict[Key, "object"], p: Plan, group=None) -> int:
 
 def reassemble(ctx, p: Plan, group=None, device=None) -> int:
     """Reassemble the last (sharded) witness of `ctx` with plan `p` (from plan()).
-    Streams are stream-ordered with the engine: the exchange starts after the
-    witness on the device without a host round trip per segment."""
+    Stream-ordered, no host wait: torch's current stream (which the RCCL
+    exchange follows) first waits on the device for the engine's queued
+    witness, and the engine's streams then wait for the exchange, so a next
+    witness cannot overwrite cells still being sent or received."""
     import torch
+    from . import zk
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device())
-    ctx.sync()
+    zk._before_torch(ctx)
     moved = exchange(stream_tensors(ctx, device), p, group)
-    torch.cuda.synchronize(device)
+    zk._after_torch(ctx)
     return moved

@@ -418,7 +418,6 @@ struct svdw_ctx {
     struct DevBits { svdw_mat m; int16_t word; };
     std::vector<DevBits> dwords;
     const unsigned* dbitw = nullptr;
-    bool scan_na_host = false;              // "scan_na_host": host reads the bounds (A/B)
     // Known magnitude bounds of matrices written in this witness: cell (i, j) of
     // `m` satisfies |signed value| < 2^bits. Cleared with the streams.
     struct MatBits { svdw_mat m; uint32_t bits; };
@@ -447,22 +446,12 @@ struct svdw_ctx {
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
     uint32_t stage_flags = STAGE_ALIGN;     // STAGE_* (svdw_set_option "stage_align", "stage_inc", ...)
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
-    int scan_impl = 4;                      // svdw_set_option "scan_impl"
     int prelaunch_at = 0;                   // "prelaunch_at": GEMMs queued before stage 0/1/2
     int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
-    int gemm_kc = 1;                        // "gemm_kc": 64-k chunks per LDS round of the CRT GEMM (1 / 4;
-                                            // 4 needs 64 KiB of LDS and starves beside the stage blocks)
     bool gemm_batched = false;              // this witness's products went out as one batch
-    bool gemm_xm = true;                    // "gemm_xm": CRT GEMM units (modulus, half) placed per XCD
     int res_first = 0;                      // "res_first": cell stream waits for the residue planes
                                             // (1), not (0), -1: on row-sharded ranks
-    int comb_direct = 1;                    // "comb_direct": batched CRT combine stores from registers
-                                            // (no LDS) for batches without symmetric jobs (1), for
-                                            // every batch (2), or always via LDS (0). 2 measured
-                                            // slower (mirror stores of symmetric tiles scatter):
-                                            // 512^2 P=32 0.411-0.418 -> 0.426-0.428 ms, 1024^2
-                                            // 2.07-2.08 -> 2.08-2.09 ms (tools/probe_comb.sh)
     int gemm_batch = 1;                     // "gemm_batch": svd_witness's three products in one launch
                                             // (1), one by one (0), or -1: batched on row-sharded ranks
     bool fused_quantize = true;             // "fused_quantize": m, u, v, d in one launch
@@ -504,12 +493,20 @@ struct svdw_ctx {
     struct Seg { uint32_t phase, lookup; uint64_t off, n; };
     std::vector<Seg> owned;
     DBuf bvfull[kMaxScanJobs];              // shard mode: full b.g values per verify_mul
+    // svd_witness's quantized matrices and their device f64 inputs (u, v): a
+    // row-sharded rank takes b.g of b = u^T, v^T from the f64 rows directly
+    // (k_colsum_f64), not from cells. Cleared at the end of the witness.
+    struct F64Src { svdw_mat m; const double* x; };
+    std::vector<F64Src> f64src;
+    DBuf colpart;                           // k_colsum_f64's per-slice partial sums
+    bool colsum = true;                     // "colsum": that path (else k_matvec_values on the cells)
     // second stream: GEMMs overlap the HBM-bound stages; third: phase 1
     hipStream_t st2 = nullptr;
     bool st2_hi = false;                    // st2 is the high-priority stream
     int gemm_prio = -1;                     // "gemm_priority": -1 auto, 0 normal, 1 high
     hipStream_t st3 = nullptr;
     hipStream_t st_cell = nullptr;          // the cell stream proper (st is swapped at times)
+    hipEvent_t xev[4] = {};                 // svdw_stream_wait / _signal (caller's stream)
     bool overlap = true;
     struct PreGemm {
         uint64_t off;
@@ -551,7 +548,6 @@ struct svdw_ctx {
     };
     std::vector<Batch> batches;
     bool stage_batch = true;
-    bool stage_persist = false;             // "stage_persist": resident stage blocks walk the chunks
     // device ingest (svdw_parse_svd_input_device) scratch
     DBuf ing_x, ing_e, ing_c, ing_p10, ing_val, ing_npos, ing_nd, ing_rpos, ing_kpos, ing_err, ing_q;
     // device equality records (eq_gen_device)
@@ -884,12 +880,7 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     }
     {
         ProfScope ps(c, c->st, std::string("k_stage:") + tag, bytes, 0);
-        if (c->stage_persist && stage_multi_fits(a)) {
-            const StageArgs* one = &a;
-            hipck(launch_stage_multi(&one, 1, c->st, true), "k_stage");
-        } else {
-            hipck(launch_stage(a, c->st), "k_stage");
-        }
+        hipck(launch_stage(a, c->st), "k_stage");
     }
 }
 // Issue a stream's pending batched stages (k_stage_multi; one program: k_stage).
@@ -906,7 +897,7 @@ static void flush_batch(svdw_ctx* c, hipStream_t s) {
         std::vector<svdw_ctx::Pending> progs;
         progs.swap(b.progs);                 // (cleared before launching: no re-entry)
         ProfScope pr(c, s, name, bytes, 0, true);
-        hipck(launch_stage_multi(ps.data(), (int)ps.size(), s, c->stage_persist), "k_stage_multi");
+        hipck(launch_stage_multi(ps.data(), (int)ps.size(), s), "k_stage_multi");
     }
 }
 // RAII: stage launches on the current stream between construction and end()
@@ -1213,7 +1204,8 @@ struct DivScale {
 static DivScale div_scale_of(const svdw_ctx* c, const svdw_div_scale* cfg) {
     DivScale d;
     d.s = cfg && cfg->shift_bits ? cfg->shift_bits : 3 * c->P;
-    d.nb = cfg && cfg->num_bits ? cfg->num_bits : 4 * c->P + 1;   // the reference's cell counts (svdw.h)
+    // the reference's cell counts (svdw.h); a shift alone >= 4P + 1 widens the div_mod
+    d.nb = cfg && cfg->num_bits ? cfg->num_bits : std::max(4 * c->P + 1, d.s + 1);
     REQUIRE(d.s >= c->P && d.s < 254 && d.nb > d.s && d.nb <= 253 && d.nb - c->P <= 200,
             "signed_div_scale: need P <= shift_bits < num_bits <= 253, num_bits - P <= 200");
     return d;
@@ -1390,7 +1382,7 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
             ProfScope ps(c, s, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * N * M,
                          (double)N * M * K);
             hipck(launch_gemm_crt(sym, Ar, Br, N, M, rpa, sym ? rpa : rpb,
-                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s, c->gemm_kc, c->gemm_xm),
+                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s),
                   "k_gemm_crt");
         }
         if (!quantized)
@@ -1541,9 +1533,8 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
     return cs;
 }
 // Words of the small operand for the row-scan products: |signed a| < 2^(32 na)
-// when a's bound is known to the host (scan_impl 4 / 5), else 8 (full Montgomery).
+// when a's bound is known to the host, else 8 (full Montgomery).
 static int scan_na(const svdw_ctx* c, const svdw_mat& a) {
-    if (c->scan_impl < 4) return 8;
     const uint32_t b = bits_of(c, a);
     if (b == ~0u || b > 192) return 8;
     return std::max(1, (int)((b + 31) / 32));
@@ -1575,10 +1566,8 @@ static NaSpec job_spec(const svdw_ctx* c, const svdw_mat& a) {
 // na of a batch of scans: host-known (1..8), or 0 = decided on the device from
 // the jobs' specs (job_spec), so the host needs no operand bounds
 static int batch_na_host(const svdw_ctx* c, const svdw_mat* ms, int n) {
-    if (c->scan_impl == 3) return 8;
-    if (c->scan_impl < 3) return 8;
     int na = 1;
-    bool host = true, dev = c->scan_impl >= 4 && c->dbitw && !c->scan_na_host;
+    bool host = true, dev = c->dbitw != nullptr;
     for (int i = 0; i < n; ++i) {
         if (bits_of(c, ms[i]) != ~0u) na = std::max(na, scan_na(c, ms[i]));
         else host = false;
@@ -1616,14 +1605,13 @@ static svdw_vec matvec_rows(svdw_ctx* c, uint32_t phase, const svdw_mat& a, cons
     note_scan(c, a, wsrc);
     uint64_t r0 = 0, r1 = R;
     if (sharded(c)) {
-        REQUIRE(c->scan_impl >= 3, "row sharding needs scan_impl >= 3");
         shard_rows(c, R, &r0, &r1);
         own(c, phase, false, off + r0 * (3ull * L + 1), (r1 - r0) * (3ull * L + 1));
     }
     if (!c->dry) {
         ProfScope ps(c, c->st, a.cs == 1 ? "k_matvec_scan:rows" : "k_matvec_scan:cols", 32.0 * (double)R * (4.0 * L + 1) + 64.0 * L, (double)R * L);
         hipck(launch_matvec_scan(view_of(c, a), (uint32_t)r0, (uint32_t)r1, L, wc, tab, tl,
-                                 cellp(c, phase, off + r0 * (3ull * L + 1)), c->scan_impl, na,
+                                 cellp(c, phase, off + r0 * (3ull * L + 1)), na,
                                  c->st), "k_matvec_scan");
     }
     return svdw_vec{phase, R, off + 3ull * L, (int64_t)(3ull * L + 1)};
@@ -1704,53 +1692,6 @@ static void ensure_gamma_vec(svdw_ctx* c, uint32_t d, const Fr& gamma) {
     gamma_prep(c, d, gamma, c->st);
     c->gp_ev = nullptr;
 }
-// ZkMatrix::verify_mul, one call at a time (scan_impl 1 / 2)
-static void verify_mul_legacy(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svdw_mat& b,
-                       const svdw_mat& cs, const Fr& gamma) {
-    REQUIRE(a.cols == b.rows, "verify_mul: a.num_col != b.num_rows");
-    REQUIRE(cs.rows == a.rows, "verify_mul: c_s.len() != a.num_rows");
-    REQUIRE(cs.cols == b.cols, "verify_mul: c_s[0].len() != b.num_col");
-    const uint32_t d = cs.cols, n = a.rows;
-    c->ext_gamma = gamma;
-    ensure_gamma_vec(c, d, gamma);
-    const Fr* gpc = (const Fr*)c->gpc.p;
-    const svdw_vec one = put_cell(c, phase, fr_from_u64(1), true);   // load_witness(F::ONE) + assert_is_const
-    uint64_t pows_off = 0;
-    if (d > 1) {                                          // v_i = mul(v_{i-1}, init_rand)
-        PB pb(c->LB);
-        pb.kext = pb.kidx(gamma);                         // gamma: a cell of the RLC context
-        pb.vsrc[1] = false;
-        DView w;
-        memset(&w, 0, sizeof w);
-        w.ptr = gpc;
-        w.rs = 1; w.cs = 0; w.rows = d; w.cols = 1;
-        pb.a.view[0] = w;
-        pb.a.view[1] = w;
-        if (!c->dry) pb.a.view[1].ptr = gpc + 1;
-        uint8_t prev = pb.load(0), cur = pb.load(1);
-        pb.gate(0);
-        pb.cell(pb.K(0)); pb.cell(prev); pb.cell(pb.K(gamma)); pb.cell(cur);
-        note_const(c, fr_zero());
-        pows_off = run_stage(c, phase, pb, d - 1, 1, "verify_mul_gamma_pows");
-        c->layout_chk.back().esrc[0] = eqsrc_chain(one.phase, one.off, phase, pows_off + 3, 4);
-    }
-    const RegionChecks::EqSrc gsrc = eqsrc_chain(one.phase, one.off, phase, pows_off + 3, 4);
-    const Fr* gtab = (const Fr*)c->gtab.p;
-    svdw_vec csv = matvec_rows(c, phase, cs, gpc, gtab, c->gp_len, scan_na(c, cs), gsrc);
-    svdw_vec bv = matvec_rows(c, phase, b, gpc, gtab, c->gp_len, scan_na(c, b), gsrc);
-    const Fr* t2 = vec_prep(c, bv, c->w2c, c->w2t);
-    svdw_vec abv = matvec_rows(c, phase, a, (const Fr*)c->w2c.p, t2, bv.len, scan_na(c, a),
-                               eqsrc_vec(bv));
-    PB pb(c->LB);                                         // is_equal per row (unconstrained result)
-    pb.a.view[0] = view_of(c, mat_of_vec(csv));
-    pb.a.view[1] = view_of(c, mat_of_vec(abv));
-    uint8_t x = pb.load(0), y = pb.load(1);
-    pb.g_is_equal(x, y);
-    run_stage(c, phase, pb, n, 1, "verify_mul_is_equal");
-    c->layout_chk.back().esrc[0] = eqsrc_mat(mat_of_vec(csv));
-    c->layout_chk.back().esrc[1] = eqsrc_mat(mat_of_vec(abv));
-}
-
 static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, const Fr& gamma) {
     REQUIRE(n >= 1 && n <= kMaxScanJobs, "internal: verify_mul batch size");
     c->ext_gamma = gamma;
@@ -1846,7 +1787,6 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         }
         bs.end();
     }
-    const int T = c->scan_impl == 5 ? 4 : c->scan_impl == 3 ? 1 : 2;
     // operand widths per batch: host-known, or read on the device (na 0)
     auto batch_na = [&](auto mat_of) {
         svdw_mat ms[kMaxScanJobs];
@@ -1872,7 +1812,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         sb.njobs = n;
         sb.bitw = c->dbitw;
         ProfScope ps(c, c->st, name, bytes, ops);
-        hipck(launch_scan_batch(sb, T, T == 1 ? 8 : na, c->st), "k_matvec_scan");
+        hipck(launch_scan_batch(sb, na, c->st), "k_matvec_scan");
     };
     auto cs_of = [&](int i) { return vm[i].cs; };
     auto b_of = [&](int i) { return vm[i].b; };
@@ -1895,7 +1835,58 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
                 vm[k].b.rs == vm[i].b.rs && vm[k].b.cs == vm[i].b.cs) { src[i] = k; break; }
     }
     const Fr* wt[kMaxScanJobs];
-    if (sharded(c)) {
+    // b = X^T of an f64 input of svd_witness: X, else null
+    auto f64_of = [&](const svdw_mat& b) -> const svdw_ctx::F64Src* {
+        if (!c->colsum || b.cols > 8192) return nullptr;
+        for (auto& s : c->f64src)
+            if (is_transpose_of(b, s.m) && s.m.rs == (int64_t)s.m.cols && s.m.cs == 1) return &s;
+        return nullptr;
+    };
+    bool all_f64 = sharded(c);
+    for (int i = 0; i < n && all_f64; ++i) all_f64 = f64_of(vm[i].b) != nullptr;
+    if (all_f64) {
+        // every entry of b.g from the f64 rows of X (quantized in registers),
+        // column-parallel and coalesced: one launch for the distinct b's, then
+        // the slices' sums folded into each vector's table (k_vec_prep_sum)
+        ColBatch cb;
+        memset(&cb, 0, sizeof cb);
+        cb.tab = gtab;
+        cb.tl = c->gp_len;
+        cb.bitw = c->dbitw;
+        int slot[kMaxScanJobs];
+        size_t poff[kMaxScanJobs], ptot = 0;
+        for (int i = 0; i < n; ++i) {
+            if (src[i] != i) { slot[i] = slot[src[i]]; continue; }
+            REQUIRE(cb.njobs < (uint32_t)kMaxColJobs, "internal: too many distinct b for k_colsum_f64");
+            const svdw_ctx::F64Src* s = f64_of(vm[i].b);
+            ColJob& j = cb.job[cb.njobs];
+            j.x = s->x;
+            j.R = s->m.rows;
+            j.C = s->m.cols;
+            j.ld = s->m.cols;
+            j.spec = job_spec(c, vm[i].b);
+            poff[cb.njobs] = ptot;
+            ptot += (size_t)colsum_slices(j.R) * j.C;
+            slot[i] = (int)cb.njobs++;
+        }
+        ensure_buf(c, c->colpart, ptot * sizeof(Fr));
+        for (uint32_t q = 0; q < cb.njobs; ++q) cb.job[q].part = (Fr*)c->colpart.p + poff[q];
+        {
+            ProfScope ps(c, c->st, "k_colsum_f64", 0, 0);
+            hipck(launch_colsum_f64(cb, (int)c->P, c->st), "k_colsum_f64");
+        }
+        for (int i = 0; i < n; ++i) {
+            if (src[i] != i) { wt[i] = wt[src[i]]; continue; }
+            const uint32_t L = vm[i].b.rows;
+            ensure_buf(c, c->wbc[i], (size_t)L * sizeof(Fr));
+            ensure_buf(c, c->wbt[i], tab_len(L) * sizeof(Fr));
+            ProfScope ps(c, c->st, "k_vec_prep", 32.0 * L * (2 + tab_len(1)), 0);
+            hipck(launch_vec_prep_sum(cb.job[slot[i]].part, colsum_slices(cb.job[slot[i]].R), L,
+                                      (Fr*)c->wbc[i].p, (Fr*)c->wbt[i].p, scale_tab(), c->st),
+                  "k_vec_prep_sum");
+            wt[i] = (const Fr*)c->wbt[i].p;
+        }
+    } else if (sharded(c)) {
         // only this rank's rows of the b.g scans exist: every entry of b.g comes
         // from the values-only mat-vec instead (the distinct b's in one launch)
         ScanBatch vb;
@@ -1941,11 +1932,6 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
 }
 static void verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svdw_mat& b,
                        const svdw_mat& cs, const Fr& gamma) {
-    if (c->scan_impl < 3) {                       // legacy per-call path (A/B only)
-        REQUIRE(!sharded(c), "row sharding needs scan_impl >= 3");
-        verify_mul_legacy(c, phase, a, b, cs, gamma);
-        return;
-    }
     VMul v{a, b, cs};
     verify_mul_many(c, phase, &v, 1, gamma);
 }
@@ -2027,8 +2013,6 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
         // own residue scratch): one step of the st2 chain instead of three
         CrtBatch b;
         memset(&b, 0, sizeof b);
-        b.kc = c->gemm_kc;
-        b.direct = c->comb_direct;
         size_t rbytes[3], rtot = 0;
         for (int g = 0; g < 3; ++g) {
             rbytes[g] = (size_t)kCrtMaxResidues * ceil_to(std::max<uint32_t>((uint32_t)(rr1[g] - rr0[g]), 1), 128) *
@@ -2087,8 +2071,7 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
             ProfScope ps(c, pst, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * rows * cols,
                          (double)rows * cols * A[g].cols);
             hipck(launch_gemm_crt(sym, Ap, Bp, rows, cols, stride[g], bs, kp[g], (uint8_t*)c->crtR.p,
-                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], pst, c->gemm_kc,
-                                  c->gemm_xm),
+                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], pst),
                   "k_gemm_crt");
         }
         c->pre.push_back({log[g], stream_dep(c, pst, nullptr), pst});
@@ -2235,6 +2218,14 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         const svdw_svd_payload pl{t_u, t_v, svdw_mat{m.phase, N, M, c->pre[0].off, (int64_t)M, 1},
                                   svdw_mat{m.phase, N, N, c->pre[1].off, (int64_t)N, 1},
                                   svdw_mat{m.phase, M, M, c->pre[2].off, (int64_t)M, 1}};
+        // the products' bounds (|c_s| < 2^(bits_a + bits_b + lk)) before
+        // honest_prover_mat_mul registers them: the c_s scans then size their
+        // operand on the device (NaSpec) instead of falling back to full
+        // Montgomery products (8-way shard rank: 81 -> 25 us)
+        auto clog2 = [](uint32_t k) { uint32_t l = 0; while ((1ull << l) < k) ++l; return l; };
+        c->prods.push_back({pl.m_times_vt, m, t_v, clog2(M)});
+        c->prods.push_back({pl.u_times_ut, u, t_u, clog2(N)});
+        c->prods.push_back({pl.v_times_vt, v, t_v, clog2(M)});
         auto f = std::move(c->early_p1);
         c->early_p1 = nullptr;
         f(pl);
@@ -2309,13 +2300,6 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
 }
 static void check_svd_phase1(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u, const svdw_mat& v,
                              const svdw_svd_payload& pl, const Fr& g) {
-    if (c->scan_impl < 3) {
-        REQUIRE(!sharded(c), "row sharding needs scan_impl >= 3");
-        verify_mul(c, 1, m, pl.v_t, pl.m_times_vt, g);
-        verify_mul(c, 1, u, pl.u_t, pl.u_times_ut, g);
-        verify_mul(c, 1, v, pl.v_t, pl.v_times_vt, g);
-        return;
-    }
     const VMul vm[3] = {{m, pl.v_t, pl.m_times_vt}, {u, pl.u_t, pl.u_times_ut},
                         {v, pl.v_t, pl.v_times_vt}};
     verify_mul_many(c, 1, vm, 3, g);
@@ -2440,7 +2424,6 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     const int p1mode = c->phase1_overlap == 1 && (sharded(c) || p1_small) ? 2 : c->phase1_overlap;
     bool p1_queued = false;
     auto queue_phase1 = [&](const svdw_svd_payload& pl, bool overlap) {
-        if (c->scan_na_host) fetch_bits(c);       // A/B: operand widths read on the host
         const bool p1_overlap = p1mode && overlap;
         if (p1_overlap && p1mode == 2 && !c->st3)   // created on first use
             hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
@@ -2469,9 +2452,15 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     if (p1mode == 2 && !c->dry) c->early_p1 = [&](const svdw_svd_payload& pl) { queue_phase1(pl, true); };
     struct F64 {
         svdw_ctx* c;
-        ~F64() { c->svd_f64[0] = c->svd_f64[1] = c->svd_f64[2] = nullptr; }
+        ~F64() {
+            c->svd_f64[0] = c->svd_f64[1] = c->svd_f64[2] = nullptr;
+            c->f64src.clear();
+        }
     } f64clr{c};
-    if (on_device && !c->dry) { c->svd_f64[0] = m; c->svd_f64[1] = u; c->svd_f64[2] = v; }
+    if (on_device && !c->dry) {
+        c->svd_f64[0] = m; c->svd_f64[1] = u; c->svd_f64[2] = v;
+        c->f64src = {{zu, u}, {zv, v}};
+    }
     svdw_svd_payload pl =
         check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits, dbits, true);
     c->early_p1 = nullptr;
@@ -2771,6 +2760,8 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             }
             if (c->hbits) (void)hipHostFree(c->hbits);
             if (c->ev_bits) (void)hipEventDestroy(c->ev_bits);
+            for (auto e : c->xev)
+                if (e) (void)hipEventDestroy(e);
             for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
             for (auto e : c->pool) (void)hipEventDestroy(e);
             for (auto e : c->deps) (void)hipEventDestroy(e);
@@ -2799,6 +2790,41 @@ int svdw_reserve(svdw_ctx* c, uint32_t phase, uint64_t na, uint64_t nl) {
         Stream& s = c->ph[phase];
         grow(c, s.adv, s.n, s.cap, na);
         grow(c, s.lk, s.nl, s.lcap, nl);
+    });
+}
+// Stream-ordered hand-off with a caller's stream (e.g. torch's current stream):
+// the context's streams wait for the work queued on `s` so far (inputs it is
+// still writing, buffers it still reads), and `s` waits for the context's
+// queued work (outputs it will read). No host wait either way.
+static hipEvent_t xevent(svdw_ctx* c, int i) {
+    if (!c->xev[i])
+        hipck(hipEventCreateWithFlags(&c->xev[i], hipEventDisableTiming), "hipEventCreate");
+    return c->xev[i];
+}
+int svdw_stream_wait(svdw_ctx* c, void* stream) {
+    return guarded([&] {
+        REQUIRE(c, "null ctx");
+        if (c->dry) return;
+        const hipStream_t s = (hipStream_t)stream;
+        const hipEvent_t e = xevent(c, 0);
+        hipck(hipEventRecord(e, s), "hipEventRecord");
+        for (hipStream_t t : {c->st, c->st2, c->st3})
+            if (t) hipck(hipStreamWaitEvent(t, e, 0), "hipStreamWaitEvent");
+    });
+}
+int svdw_stream_signal(svdw_ctx* c, void* stream) {
+    return guarded([&] {
+        REQUIRE(c, "null ctx");
+        if (c->dry) return;
+        const hipStream_t s = (hipStream_t)stream;
+        int i = 1;
+        for (hipStream_t t : {c->st, c->st2, c->st3}) {
+            if (!t) continue;
+            flush_batch(c, t);
+            const hipEvent_t e = xevent(c, i++);
+            hipck(hipEventRecord(e, t), "hipEventRecord");
+            hipck(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
+        }
     });
 }
 int svdw_sync(svdw_ctx* c) {
@@ -3580,6 +3606,10 @@ int svdw_check_equalities(svdw_ctx* c, uint32_t phase, const void* columns0, con
     return guarded([&] {
         REQUIRE(c && phase < 2 && out, "bad argument");
         REQUIRE(!c->dry, "svdw_check_equalities needs a device context");
+        // a record's source and destination cells may lie in other ranks' rows,
+        // which this context never wrote (svdw_check_gates checks a rank's own)
+        REQUIRE(!sharded(c), "svdw_check_equalities: not on a row-sharded context (its streams hold "
+                             "this rank's rows only; check the reassembled witness, or use svdw_check_gates)");
         const bool phys = columns0 || columns1;
         REQUIRE(!phys || (c->phys.valid && (phase == 0 ? columns0 != nullptr : columns0 && columns1)),
                 "svdw_check_equalities: physical columns need svdw_physical_layout and phase 0's "
@@ -3645,8 +3675,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             REQUIRE(value >= 16 && value <= 256 && value % 16 == 0,
                     "stage_elems: a multiple of 16 in [16, 256]");
             c->stage_elems = (uint32_t)value;
-        } else if (n == "stage_inc") {             // previous phase B (per-half-cell decode)
-            c->stage_flags = (c->stage_flags & ~STAGE_INC) | (value ? STAGE_INC : 0);
         } else if (n == "stage_align") {
             c->stage_flags = (c->stage_flags & ~STAGE_ALIGN) | (value ? STAGE_ALIGN : 0);
         } else if (n == "stage_probe") {             // timing probe, wrong cells (tools/ab.py)
@@ -3685,43 +3713,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                 c->st = s;
                 c->st_cell = s;
             }
-        } else if (n == "cu_split") {
-            // Give the second stream (products, phase 1) `value` CUs of its own and
-            // the cell stream the rest (0: both streams on every CU). Masks pick
-            // groups of 8 consecutive mask bits, so the split is even over the
-            // XCDs whether the mask order is XCD-major or XCD-interleaved.
-            REQUIRE(value >= 0 && value % 8 == 0, "cu_split: a multiple of 8, >= 0");
-            if (!c->dry) {
-                c->st2_hi = false;                // (re-created below at normal priority)
-                c->gemm_prio = 0;
-                hipDeviceProp_t prop;
-                hipck(hipGetDeviceProperties(&prop, c->device), "hipGetDeviceProperties");
-                const uint32_t ncu = (uint32_t)prop.multiProcessorCount;
-                REQUIRE(value < ncu && ncu % 8 == 0, "cu_split: fewer CUs than the device has");
-                hipStream_t s1 = nullptr, s2 = nullptr;
-                if (value) {
-                    const uint32_t groups = ncu / 8, g2 = (uint32_t)value / 8;
-                    std::vector<uint32_t> m1((ncu + 31) / 32, 0), m2((ncu + 31) / 32, 0);
-                    for (uint32_t g = 0; g < groups; ++g) {
-                        // g2 of the groups, spread evenly (Bresenham) over the mask
-                        const bool two = (g + 1) * g2 / groups != g * g2 / groups;
-                        for (uint32_t b = 8 * g; b < 8 * g + 8; ++b)
-                            (two ? m2 : m1)[b / 32] |= 1u << (b % 32);
-                    }
-                    hipck(hipExtStreamCreateWithCUMask(&s1, (uint32_t)m1.size(), m1.data()),
-                          "hipExtStreamCreateWithCUMask");
-                    hipck(hipExtStreamCreateWithCUMask(&s2, (uint32_t)m2.size(), m2.data()),
-                          "hipExtStreamCreateWithCUMask");
-                } else {
-                    hipck(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking), "hipStreamCreate");
-                    hipck(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking), "hipStreamCreate");
-                }
-                hipck(hipStreamDestroy(c->st), "hipStreamDestroy");
-                hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
-                c->st = s1;
-                c->st_cell = s1;
-                c->st2 = s2;
-            }
         } else if (n == "phase1_overlap") {
             REQUIRE(value >= 0 && value <= 2, "phase1_overlap: 0, 1 or 2");
             c->phase1_overlap = (int)value;
@@ -3740,19 +3731,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "res_first") {
             REQUIRE(value >= -1 && value <= 1, "res_first: -1 (auto), 0 or 1");
             c->res_first = (int)value;
-        } else if (n == "gemm_xm") {
-            c->gemm_xm = value != 0;
-        } else if (n == "stage_persist") {
-            c->stage_persist = value != 0;
-        } else if (n == "comb_direct") {
-            REQUIRE(value >= 0 && value <= 2, "comb_direct: 0, 1 or 2");
-            c->comb_direct = (int)value;
         } else if (n == "gemm_batch") {
             REQUIRE(value >= -1 && value <= 1, "gemm_batch: -1 (auto), 0 or 1");
             c->gemm_batch = (int)value;
-        } else if (n == "gemm_kc") {
-            REQUIRE(value == 1 || value == 4, "gemm_kc: 1 or 4");
-            c->gemm_kc = (int)value;
         } else if (n == "gemm_rt") {
             REQUIRE(value == 0 || value == 1, "gemm_rt: 0 or 1");
             c->gemm_rt = (int)value;
@@ -3762,13 +3743,10 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "p1_at") {
             REQUIRE(value >= -1 && value <= 3, "p1_at: -1 (auto), 0, 1, 2 or 3");
             c->p1_at = (int)value;
-        } else if (n == "scan_impl") {
-            REQUIRE(value >= 1 && value <= 5, "scan_impl: 1..5");
-            c->scan_impl = (int)value;
         } else if (n == "overlap") {
             c->overlap = value != 0;
-        } else if (n == "scan_na_host") {           // A/B: row-scan widths read on the host
-            c->scan_na_host = value != 0;
+        } else if (n == "colsum") {                 // row-sharded b.g from the f64 inputs
+            c->colsum = value != 0;
         } else {
             fail(SVDW_EINVAL, "unknown option " + n);
         }

@@ -252,46 +252,13 @@ __device__ __forceinline__ uint32_t fastdiv(uint32_t x, uint32_t d, uint32_t mag
     return d == 1 ? x : __umulhi(x, magic);
 }
 
-// Previous phase B (STAGE_INC, kept as the A/B reference of the descriptor
-// path): one half-cell per lane per iteration, each lane decoding its slot op
-// and building the masks; the (element, slot) of the lane's next cell tracked
-// incrementally (the cell index advances by blockDim/2 each step).
-// ALIGN: the block's iterations cover whole (blockDim * 16 B)-aligned address
-// windows (the first one partially), so every wave store is one aligned 1 KiB.
-template <bool ALIGN>
-__device__ __forceinline__ void stream_cells_inc(uint4* __restrict__ out, uint32_t total,
-                                                 const SlotOp* __restrict__ ops, uint32_t C,
-                                                 uint32_t magic, const uint32_t* sK,
-                                                 const uint32_t* sV, uint32_t nv) {
-    const uint32_t h = threadIdx.x & 1, step = blockDim.x >> 1;
-    const uint32_t dq = step / C, dr = step - dq * C, ev = stage_elem_words(nv);
-    uint32_t hc0 = threadIdx.x;
-    if (ALIGN) {
-        // misalignment of the region start in half-cells (even: cells are 32 B aligned)
-        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) >> 4) & (blockDim.x - 1);
-        hc0 = threadIdx.x >= mis ? threadIdx.x - mis : threadIdx.x + blockDim.x - mis;
-    }
-    uint32_t c = hc0 >> 1;
-    uint32_t el = fastdiv(c, C, magic), slot = c - el * C;
-    uint32_t vbase = el * ev;                             // LDS word offset of this element
-    for (uint32_t hc = hc0; hc < total; hc += blockDim.x) {
-        const SlotOp op = ops[slot];
-        const uint32_t* src = op.src >= KSRC ? sK + (op.src - KSRC) * VW : sV + vbase + op.src * VW;
-        out[hc] = extract_half(src, op.lo, op.nbits, h);
-        slot += dr;
-        vbase += dq * ev;
-        if (slot >= C) {
-            slot -= C;
-            vbase += ev;
-        }
-    }
-}
-
 // Phase B: per-(slot, half) descriptors and masks prepared once per block
 // (half_desc, prog.hpp), so a half-cell costs one descriptor + one mask LDS
 // read, five word reads, four alignbit and four and (no per-cell decoding,
 // clamping or mask arithmetic). The (element, slot) of the lane's next cell is
-// tracked incrementally as in stream_cells_inc; ALIGN as there.
+// tracked incrementally (the cell index advances by blockDim / 2 per step).
+// ALIGN: the block's iterations cover whole (blockDim * 16 B)-aligned address
+// windows (the first one partially), so every wave store is one aligned 1 KiB.
 template <bool ALIGN>
 __device__ __forceinline__ void stream_cells_desc(uint4* __restrict__ out, uint32_t total,
                                                   const uint32_t* __restrict__ sHD,
@@ -606,9 +573,6 @@ __device__ __forceinline__ void stage_chunk(const StageArgs& a, const StageLds& 
         for (uint32_t hc = tid; hc < 2 * ne * a.C; hc += blockDim.x) outA[hc] = z;
         if (a.L)
             for (uint32_t hc = tid; hc < 2 * ne * a.L; hc += blockDim.x) outL[hc] = z;
-    } else if (a.flags & STAGE_INC) {
-        stream_cells_inc<true>(outA, 2 * ne * a.C, L.sAdv, a.C, a.cdiv_magic, L.sK, L.sV, nv);
-        if (a.L) stream_cells_inc<true>(outL, 2 * ne * a.L, L.sLk, a.L, a.ldiv_magic, L.sK, L.sV, nv);
     } else {
         const uint32_t vb0 = (uint32_t)(L.sV - smem);
         if (a.flags & STAGE_ALIGN) {
@@ -679,28 +643,6 @@ __global__ __launch_bounds__(256) void k_stage_multi(const StageMulti m) {
     const Rec q = multi_rec(m, p);
     stage_block(*q.a, q.mo, q.adv, q.lk, q.K, blockIdx.x - m.blk0[p]);
 }
-// Persistent form ("stage_persist"): a grid of resident blocks walks the batch's
-// blocks round-robin (g = blockIdx.x, + gridDim.x, ...: the same write front as
-// one block per chunk) and sets its tables up only when the program changes,
-// instead of once per 256 elements.
-__global__ __launch_bounds__(256) void k_stage_multi_p(const StageMulti m) {
-    const uint32_t total = m.blk0[m.nprog];
-    uint32_t cur = ~0u;
-    for (uint32_t g = blockIdx.x; g < total; g += gridDim.x) {
-        const uint32_t p = multi_prog(m, g);
-        const Rec q = multi_rec(m, p);
-        const StageLds L = stage_lds(*q.a);
-        const Prefetch f = stage_loads(*q.a, g - m.blk0[p]);
-        if (p != cur) {
-            stage_setup(*q.a, L, q.mo, q.adv, q.lk, q.K);
-            cur = p;
-        }
-        __syncthreads();                    // tables ready; the previous chunk's phase B done
-        stage_chunk(*q.a, L, g - m.blk0[p], f);
-        __syncthreads();                    // phase B done before the next phase A / set-up
-    }
-}
-
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     if (a.e_end <= a.e_begin) return hipSuccess;
     const uint32_t n = a.e_end - a.e_begin;
@@ -714,25 +656,7 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
 bool stage_multi_fits(const StageArgs& a) {
     return stage_record_bytes(a.nmo, a.C, a.L, a.nk) <= kMultiBytes && (a.E ? a.E : kStageElems) <= kStageElems;
 }
-// resident k_stage_multi_p blocks for `lds` bytes of dynamic LDS (cached)
-static uint32_t persist_grid(uint32_t lds) {
-    static uint32_t cu = 0;
-    static uint32_t last_lds = ~0u, last = 0;
-    if (!cu) {
-        int dev = 0;
-        hipDeviceProp_t prop;
-        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
-        cu = (uint32_t)prop.multiProcessorCount;
-    }
-    if (lds != last_lds) {
-        int nb = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_stage_multi_p, 256, lds) != hipSuccess) return 0;
-        last_lds = lds;
-        last = (uint32_t)std::max(nb, 1) * cu;
-    }
-    return last;
-}
-hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st, bool persist) {
+hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st) {
     StageMulti m;
     uint32_t used = 0, blocks = 0, lds = 0;
     m.nprog = 0;
@@ -740,12 +664,7 @@ hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t 
     // launch what is packed (a single program as a plain k_stage launch)
     auto flush = [&]() -> hipError_t {
         hipError_t e = hipSuccess;
-        const uint32_t pg = persist && m.nprog ? persist_grid(lds) : 0;
-        if (pg && blocks > pg) {
-            m.blk0[m.nprog] = blocks;
-            hipLaunchKernelGGL(k_stage_multi_p, dim3(pg), dim3(256), lds, st, m);
-            e = hipGetLastError();
-        } else if (m.nprog == 1) {
+        if (m.nprog == 1) {
             e = launch_stage(*single, st);
         } else if (m.nprog > 1) {
             m.blk0[m.nprog] = blocks;
@@ -1477,58 +1396,25 @@ __device__ __forceinline__ uint32_t crt_lds(uint32_t row, uint32_t part) {
 }
 
 // One (128 x 128 tile, modulus) per block: residues of C mod m_k as bytes
-// R[k][row][rpad_m]. SYM: A == B, upper tiles only.
+// R[k][row][rpad_m] (tile (bi, bj) of the product; SYM: A == B).
 // Ar / Br: planes of astride / bstride rows (a row block of a larger operand is
 // its planes from row r0 on with the full operand's stride); R is
-// [mod][tiles_a * CT][tiles_m * CT].
-// KC 64-k chunks are staged per LDS round (KC = 4: 64 KiB of LDS, 16 loads of
-// 16 B in flight per thread): the K loop is bound by the global-load latency
-// per round, so K = 1024 takes 4 rounds instead of 16.
-// (block function: blk / nblk = the block's index and the block count of this
-// product's grid, mod = its modulus; the kernels below map their grids onto it)
-// LDS of one block (kernels declare it: two inlined variants sharing a kernel
-// would otherwise get an array each)
-template <int KC>
-constexpr int crt_lds_bytes() { return 2 * KC * CT * CROW > CT * CTS ? 2 * KC * CT * CROW : CT * CTS; }
-template <bool SYM, int KC>
-__device__ __forceinline__ void crt_gemm_block(const uint8_t* __restrict__ Ar,
-                                               const uint8_t* __restrict__ Br, uint32_t astride,
-                                               uint32_t bstride, uint32_t kpad, uint32_t tiles_a,
-                                               uint32_t tiles_m, uint8_t* __restrict__ R,
-                                               const unsigned* __restrict__ bits_a,
-                                               const unsigned* __restrict__ bits_b, uint32_t lk,
-                                               uint32_t blk, uint32_t nblk, int mod,
-                                               uint8_t* __restrict__ S) {
-    const int n = crt_nmod(*bits_a, *bits_b, lk);
-    if (mod >= n) return;
+// [mod][tiles_a * CT][tiles_m * CT]. One 64-k chunk per LDS round, the next
+// chunk's global loads in flight under the current chunk's MFMAs.
+constexpr int crt_lds_bytes() { return 2 * CT * CROW > CT * CTS ? 2 * CT * CROW : CT * CTS; }
+__device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, const uint8_t* __restrict__ Br,
+                                              uint32_t astride, uint32_t bstride, uint32_t kpad,
+                                              uint32_t tiles_a, uint32_t tiles_m, uint8_t* __restrict__ R,
+                                              uint32_t bi, uint32_t bj, int mod, uint8_t* __restrict__ S) {
     uint8_t* As = S;
-    uint8_t* Bs = S + KC * CT * CROW;
-    uint32_t bi, bj;
-    if (SYM) {
-        uint32_t b = blk, r = 0, rowlen = tiles_m;
-        while (b >= rowlen) { b -= rowlen; ++r; --rowlen; }
-        bi = r; bj = r + b;
-    } else if ((nblk & 7) == 0 && (nblk / tiles_m) % 2 == 0) {
-        // Blocks b and b + 8 share an XCD (and its L2): give each XCD a contiguous
-        // run of the tiles in 2-row groups (a 2 x 4 block of tiles at 1024^2), so
-        // an XCD reads 2 row tiles of A and 4 column tiles of B per modulus
-        // instead of all 8 row tiles of A.
-        const uint32_t per = nblk >> 3;
-        const uint32_t t = (blk & 7) * per + (blk >> 3);
-        const uint32_t grp = t / (2 * tiles_m), w = t - grp * 2 * tiles_m;
-        bi = grp * 2 + (w & 1);
-        bj = w >> 1;
-    } else {
-        bi = blk / tiles_m;
-        bj = blk % tiles_m;
-    }
+    uint8_t* Bs = S + CT * CROW;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t wr = wave >> 1, wc = wave & 1;
     const uint8_t* Ap = Ar + ((uint64_t)mod * astride + bi * CT) * kpad;
     const uint8_t* Bp = Br + ((uint64_t)mod * bstride + bj * CT) * kpad;
     // staging map: 512 x 16 B per operand chunk; thread -> (row, part) for q = tid, tid + 256
     const uint32_t r0 = tid >> 2, r1 = (tid + 256) >> 2, part = tid & 3;
-    const uint32_t kcn = kpad / 64, nst = (kcn + KC - 1) / KC;
+    const uint32_t kcn = kpad / 64;
     v4i acc[4][4];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -1569,25 +1455,13 @@ __device__ __forceinline__ void crt_gemm_block(const uint8_t* __restrict__ Ar,
             _Pragma("unroll") for (int b = 0; b < 4; ++b)                                     \
                 acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0); \
     }
-    uint4 s0a0, s0a1, s0b0, s0b1, s1a0, s1a1, s1b0, s1b1;
-    uint4 s2a0, s2a1, s2b0, s2b1, s3a0, s3a1, s3b0, s3b1;
+    uint4 s0a0, s0a1, s0b0, s0b1;
     CRT_GLOAD(s0, 0);
-    if constexpr (KC == 4) { CRT_GLOAD(s1, 1); CRT_GLOAD(s2, 2); CRT_GLOAD(s3, 3); }
-    for (uint32_t st = 0; st < nst; ++st) {
-        const uint32_t c0 = st * KC;
+    for (uint32_t c0 = 0; c0 < kcn; ++c0) {
         CRT_LSTORE(s0, 0);
-        if constexpr (KC == 4) { CRT_LSTORE(s1, 1); CRT_LSTORE(s2, 2); CRT_LSTORE(s3, 3); }
         __syncthreads();
-        if (st + 1 < nst) {                                   // next round in flight
-            CRT_GLOAD(s0, c0 + KC);
-            if constexpr (KC == 4) { CRT_GLOAD(s1, c0 + 5); CRT_GLOAD(s2, c0 + 6); CRT_GLOAD(s3, c0 + 7); }
-        }
+        if (c0 + 1 < kcn) CRT_GLOAD(s0, c0 + 1);             // next chunk in flight
         CRT_MMA(0);
-        if constexpr (KC == 4) {
-            if (c0 + 1 < kcn) CRT_MMA(1);
-            if (c0 + 2 < kcn) CRT_MMA(2);
-            if (c0 + 3 < kcn) CRT_MMA(3);
-        }
         __syncthreads();
     }
 #undef CRT_GLOAD
@@ -1624,56 +1498,45 @@ __device__ __forceinline__ void crt_gemm_block(const uint8_t* __restrict__ Ar,
     }
 }
 
-template <bool SYM, int KC>
-__global__ __launch_bounds__(256) void k_gemm_crt(const uint8_t* __restrict__ Ar,
-                                                  const uint8_t* __restrict__ Br, uint32_t astride,
-                                                  uint32_t bstride, uint32_t kpad, uint32_t tiles_a,
-                                                  uint32_t tiles_m, uint8_t* __restrict__ R,
-                                                  const unsigned* __restrict__ bits_a,
-                                                  const unsigned* __restrict__ bits_b, uint32_t lk) {
-    __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes<KC>()];
-    crt_gemm_block<SYM, KC>(Ar, Br, astride, bstride, kpad, tiles_a, tiles_m, R, bits_a, bits_b, lk,
-                            blockIdx.x, gridDim.x, (int)blockIdx.y, S);
-}
-// Modulus-major XCD placement (1-D grid): work unit u = (modulus u / 2, half
-// u % 2 of its tiles) runs entirely on XCD u % 8 (workgroup L goes to XCD
-// L % 8), so each XCD streams a modulus's residue planes through its own L2
-// once per half instead of every XCD re-reading strips of every plane; the 38
-// units of 19 moduli balance over the 8 XCDs. tpu: tiles per unit.
-template <bool SYM, int KC>
-__global__ __launch_bounds__(256) void k_gemm_crt_xm(const uint8_t* __restrict__ Ar,
-                                                     const uint8_t* __restrict__ Br, uint32_t astride,
-                                                     uint32_t bstride, uint32_t kpad, uint32_t tiles_a,
-                                                     uint32_t tiles_m, uint8_t* __restrict__ R,
-                                                     const unsigned* __restrict__ bits_a,
-                                                     const unsigned* __restrict__ bits_b, uint32_t lk,
-                                                     uint32_t ntiles, uint32_t tpu) {
-    const uint32_t L = blockIdx.x, k = L >> 3;
-    const uint32_t u = (L & 7) + 8 * (k / tpu), t = k % tpu;
-    const uint32_t tile = (u & 1) * tpu + t;
-    if (tile >= ntiles) return;
-    // nblk = 1: plain row-major tile decode (no in-modulus XCD remap)
-    __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes<KC>()];
-    crt_gemm_block<SYM, KC>(Ar, Br, astride, bstride, kpad, tiles_a, tiles_m, R, bits_a, bits_b, lk, tile,
-                            1, (int)(u >> 1), S);
-}
-// The products of a CrtBatch in one launch: grid.x covers every job's tile
-// blocks (job j from blk0[j], multiples of 8 so the XCD mapping holds), grid.y
-// the moduli.
-template <int KC>
+
+// The products of a CrtBatch in one launch, placed modulus-major per XCD: the
+// work units (job, modulus < the job's device-decided count n, tile) are laid
+// out job-major, modulus-major, and XCD x (blocks x, x + 8, ... on gfx950) takes
+// the x-th eighth of them in order, so an XCD streams one modulus's residue
+// planes through its own L2 while it computes that modulus's tiles, instead of
+// every XCD reading strips of every plane. Blocks past the units exit at once
+// (the grid is sized for n = kCrtMaxMod).
 __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes()];
+    uint32_t cnt[kMaxCrtJobs], total = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxCrtJobs; ++j) {
+        cnt[j] = 0;
+        if ((uint32_t)j < b.njobs)
+            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk;
+        total += cnt[j];
+    }
+    const uint32_t per = (total + 7) / 8, k = blockIdx.x >> 3;
+    if (k >= per) return;
+    uint32_t u = (blockIdx.x & 7) * per + k;
+    if (u >= total) return;
     uint32_t j = 0;
-    for (uint32_t k = 1; k < b.njobs; ++k) j += blockIdx.x >= b.job[k].blk0;
+#pragma unroll
+    for (int q = 0; q < kMaxCrtJobs - 1; ++q)
+        if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
     const CrtJob& q = b.job[j];
-    const uint32_t blk = blockIdx.x - q.blk0;
-    if (blk >= q.nblk) return;                    // padding to a multiple of 8
-    __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes<KC>()];
-    if (q.sym)
-        crt_gemm_block<true, KC>(q.Ar, q.Ar, q.astride, q.astride, q.kpad, q.tiles_a, q.tiles_a, q.R,
-                                 q.bits_a, q.bits_b, q.lk, blk, q.nblk, (int)blockIdx.y, S);
-    else
-        crt_gemm_block<false, KC>(q.Ar, q.Br, q.astride, q.bstride, q.kpad, q.tiles_a, q.tiles_m, q.R,
-                                  q.bits_a, q.bits_b, q.lk, blk, q.nblk, (int)blockIdx.y, S);
+    const uint32_t mod = u / q.nblk, t = u - mod * q.nblk;
+    uint32_t bi, bj;
+    if (q.sym) {                                       // upper tiles, row by row
+        uint32_t r = 0, rest = t, rowlen = q.tiles_a;
+        while (rest >= rowlen) { rest -= rowlen; ++r; --rowlen; }
+        bi = r; bj = r + rest;
+    } else {
+        bi = t / q.tiles_m;
+        bj = t - bi * q.tiles_m;
+    }
+    crt_gemm_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.tiles_a,
+                  q.sym ? q.tiles_a : q.tiles_m, q.R, bi, bj, (int)mod, S);
 }
 
 // C from its n residues, written as canonical Fr to out[i*ors + j*ocs]; one
@@ -1801,26 +1664,23 @@ __device__ __forceinline__ void crt_combine_block(const uint8_t* __restrict__ R,
     }
 }
 
-template <bool SYM>
-__global__ __launch_bounds__(256) void k_crt_combine(const uint8_t* __restrict__ R, uint32_t rpad_a,
-                                                     uint32_t rpad_b, uint32_t N, uint32_t M,
-                                                     uint32_t tiles_m, Fr* __restrict__ out,
-                                                     int64_t ors, int64_t ocs,
-                                                     const unsigned* __restrict__ bits_a,
-                                                     const unsigned* __restrict__ bits_b, uint32_t lk) {
-    // Blocks b and b + 8 share an XCD: give each XCD a contiguous run of the
-    // (row-major) tile sequence, so the 32-byte row pieces that neighbouring
-    // tiles read from the same 128-byte lines of R come through one L2.
-    const uint32_t g = gridDim.x, b = blockIdx.x;
-    const uint32_t blk = (g & 7) == 0 ? (b & 7) * (g >> 3) + (b >> 3) : b;
-    __shared__ __attribute__((aligned(16))) uint8_t Ts[MT * MT * 32];
-    crt_combine_block<SYM>(R, rpad_a, rpad_b, N, M, tiles_m, out, ors, ocs, bits_a, bits_b, lk, blk, Ts);
-}
-__global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b) {
+// Combine blocks of a CrtBatch (cblocks in all, job j from cblk0[j]) dealt
+// XCD-contiguously: XCD x takes a contiguous run of the row-major tile
+// sequence, so the 32-byte row pieces that neighbouring tiles read from one
+// 128-byte line of R come through the same L2.
+__device__ __forceinline__ uint32_t combine_tile(const CrtBatch& b, uint32_t cblocks, uint32_t* job) {
+    const uint32_t per = (cblocks + 7) / 8, t = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
     uint32_t j = 0;
-    for (uint32_t k = 1; k < b.njobs; ++k) j += blockIdx.x >= b.job[k].cblk0;
+    for (uint32_t k = 1; k < b.njobs; ++k) j += t >= b.job[k].cblk0;
+    *job = j;
+    return t;
+}
+__global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b, uint32_t cblocks) {
+    uint32_t j;
+    const uint32_t t = combine_tile(b, cblocks, &j);
+    if (t >= cblocks) return;
     const CrtJob& q = b.job[j];
-    const uint32_t blk = blockIdx.x - q.cblk0;
+    const uint32_t blk = t - q.cblk0;
     const uint32_t rpa = q.tiles_a * CT, rpb = (q.sym ? q.tiles_a : q.tiles_m) * CT;
     __shared__ __attribute__((aligned(16))) uint8_t Ts[MT * MT * 32];
     if (q.sym)
@@ -1830,110 +1690,77 @@ __global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b) {
         crt_combine_block<false>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
                                  q.bits_b, q.lk, blk, Ts);
 }
-
-// The same combine with direct stores and no LDS ("comb_direct"): 1 for batches
-// without a symmetric job (a row-sharded rank's row blocks), 2 for every batch
-// (symmetric tiles then store their mirror image element by element).
-__global__ __launch_bounds__(256) void k_crt_combine_multi_d(const CrtBatch b) {
-    uint32_t j = 0;
-    for (uint32_t k = 1; k < b.njobs; ++k) j += blockIdx.x >= b.job[k].cblk0;
+// The same combine with direct register stores and no LDS, for batches without
+// a symmetric job (a row-sharded rank's row blocks): the blocks then fit beside
+// resident stage blocks. (Direct stores of the mirror tiles of a symmetric job
+// scatter and measured slower: 512^2 P=32 0.411-0.418 -> 0.426-0.428 ms.)
+__global__ __launch_bounds__(256) void k_crt_combine_multi_d(const CrtBatch b, uint32_t cblocks) {
+    uint32_t j;
+    const uint32_t t = combine_tile(b, cblocks, &j);
+    if (t >= cblocks) return;
     const CrtJob& q = b.job[j];
-    const uint32_t blk = blockIdx.x - q.cblk0;
-    const uint32_t rpa = q.tiles_a * CT, rpb = (q.sym ? q.tiles_a : q.tiles_m) * CT;
-    if (q.sym)
-        crt_combine_block<true, true>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
-                                      q.bits_b, q.lk, blk, nullptr);
-    else
-        crt_combine_block<false, true>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
-                                       q.bits_b, q.lk, blk, nullptr);
+    const uint32_t rpa = q.tiles_a * CT, rpb = q.tiles_m * CT;
+    crt_combine_block<false, true>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
+                                   q.bits_b, q.lk, t - q.cblk0, nullptr);
 }
 
 hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
     CrtBatch b = b0;
     if (b.njobs < 1 || b.njobs > (uint32_t)kMaxCrtJobs) return hipErrorInvalidValue;
-    uint32_t blocks = 0, cblocks = 0;
+    uint32_t units = 0, cblocks = 0;
+    bool any_sym = false;
     for (uint32_t j = 0; j < b.njobs; ++j) {
         CrtJob& q = b.job[j];
         q.tiles_a = (q.N + CT - 1) / CT;
         q.tiles_m = q.sym ? q.tiles_a : (q.M + CT - 1) / CT;
+        // every staged row (tiles x CT) lies inside its operand's planes
         if (q.kpad % 64 || q.astride < q.tiles_a * CT || (!q.sym && q.bstride < q.tiles_m * CT))
             return hipErrorInvalidValue;
         if (q.sym && q.N != q.M) return hipErrorInvalidValue;
         q.nblk = q.sym ? q.tiles_a * (q.tiles_a + 1) / 2 : q.tiles_a * q.tiles_m;
-        q.blk0 = blocks;
-        blocks += (q.nblk + 7) / 8 * 8;
+        units += kCrtMaxMod * q.nblk;                    // upper bound: n = kCrtMaxMod
         const uint32_t sa = (q.N + MT - 1) / MT, sb = (q.M + MT - 1) / MT;
         q.ctiles_m = q.sym ? sa : sb;
         q.cblk0 = cblocks;
         cblocks += q.sym ? sa * (sa + 1) / 2 : sa * sb;
+        any_sym |= q.sym != 0;
     }
-    if (b.kc == 4)
-        hipLaunchKernelGGL(k_gemm_crt_multi<4>, dim3(blocks, kCrtMaxMod), dim3(256), 0, st, b);
-    else
-        hipLaunchKernelGGL(k_gemm_crt_multi<1>, dim3(blocks, kCrtMaxMod), dim3(256), 0, st, b);
+    hipLaunchKernelGGL(k_gemm_crt_multi, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    bool any_sym = false;
-    for (uint32_t j = 0; j < b.njobs; ++j) any_sym |= b.job[j].sym != 0;
-    if (b.direct >= 2 || (b.direct == 1 && !any_sym))
-        hipLaunchKernelGGL(k_crt_combine_multi_d, dim3(cblocks), dim3(256), 0, st, b);
+    const dim3 cg((cblocks + 7) / 8 * 8);
+    if (any_sym)
+        hipLaunchKernelGGL(k_crt_combine_multi, cg, dim3(256), 0, st, b, cblocks);
     else
-        hipLaunchKernelGGL(k_crt_combine_multi, dim3(cblocks), dim3(256), 0, st, b);
+        hipLaunchKernelGGL(k_crt_combine_multi_d, cg, dim3(256), 0, st, b, cblocks);
     return hipGetLastError();
 }
 
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st, int kc, bool xm) {
-    if (kc != 1 && kc != 4) return hipErrorInvalidValue;
-    xm = xm && kc == 1;
-    const uint32_t ta = (N + CT - 1) / CT, tb = (M + CT - 1) / CT;
-    // every staged row (tiles x CT) lies inside its operand's planes
-    if (kpad % 64 || astride < ta * CT || bstride < tb * CT) return hipErrorInvalidValue;
-    const uint32_t rpa = ta * CT, rpb = tb * CT;           // R: [mod][rpa][rpb]
-    const uint32_t sa = (N + MT - 1) / MT, sb = (M + MT - 1) / MT;
-    if (xm) {
-        const uint32_t ntiles = sym ? ta * (ta + 1) / 2 : ta * tb, tpu = (ntiles + 1) / 2;
-        const uint32_t grid = 8 * tpu * ((2 * kCrtMaxMod + 7) / 8);
-        if (sym && (N != M || astride != bstride)) return hipErrorInvalidValue;
-        if (sym)
-            hipLaunchKernelGGL((k_gemm_crt_xm<true, 1>), dim3(grid), dim3(256), 0, st, Ar, Ar, astride, bstride,
-                               kpad, ta, ta, R, bits_a, bits_b, lk, ntiles, tpu);
-        else
-            hipLaunchKernelGGL((k_gemm_crt_xm<false, 1>), dim3(grid), dim3(256), 0, st, Ar, Br, astride, bstride,
-                               kpad, ta, tb, R, bits_a, bits_b, lk, ntiles, tpu);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        if (sym)
-            hipLaunchKernelGGL(k_crt_combine<true>, dim3(sa * (sa + 1) / 2), dim3(256), 0, st, R, rpa,
-                               rpb, N, M, sa, out, ors, ocs, bits_a, bits_b, lk);
-        else
-            hipLaunchKernelGGL(k_crt_combine<false>, dim3(sa * sb), dim3(256), 0, st, R, rpa, rpb,
-                               N, M, sb, out, ors, ocs, bits_a, bits_b, lk);
-        return hipGetLastError();
-    }
-    if (sym) {
-        if (N != M || astride != bstride) return hipErrorInvalidValue;
-        if (kc == 4)
-            hipLaunchKernelGGL((k_gemm_crt<true, 4>), dim3(ta * (ta + 1) / 2, kCrtMaxMod), dim3(256), 0, st,
-                               Ar, Ar, astride, bstride, kpad, ta, ta, R, bits_a, bits_b, lk);
-        else
-            hipLaunchKernelGGL((k_gemm_crt<true, 1>), dim3(ta * (ta + 1) / 2, kCrtMaxMod), dim3(256), 0, st,
-                               Ar, Ar, astride, bstride, kpad, ta, ta, R, bits_a, bits_b, lk);
-        hipLaunchKernelGGL(k_crt_combine<true>, dim3(sa * (sa + 1) / 2), dim3(256), 0, st, R, rpa,
-                           rpb, N, M, sa, out, ors, ocs, bits_a, bits_b, lk);
-    } else {
-        if (kc == 4)
-            hipLaunchKernelGGL((k_gemm_crt<false, 4>), dim3(ta * tb, kCrtMaxMod), dim3(256), 0, st, Ar, Br,
-                               astride, bstride, kpad, ta, tb, R, bits_a, bits_b, lk);
-        else
-            hipLaunchKernelGGL((k_gemm_crt<false, 1>), dim3(ta * tb, kCrtMaxMod), dim3(256), 0, st, Ar, Br,
-                               astride, bstride, kpad, ta, tb, R, bits_a, bits_b, lk);
-        hipLaunchKernelGGL(k_crt_combine<false>, dim3(sa * sb), dim3(256), 0, st, R, rpa, rpb,
-                           N, M, sb, out, ors, ocs, bits_a, bits_b, lk);
-    }
-    return hipGetLastError();
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st) {
+    if (sym && (N != M || astride != bstride)) return hipErrorInvalidValue;
+    CrtBatch b;
+    memset(&b, 0, sizeof b);
+    b.njobs = 1;
+    CrtJob& q = b.job[0];
+    q.Ar = Ar;
+    q.Br = sym ? Ar : Br;
+    q.R = R;
+    q.out = out;
+    q.bits_a = bits_a;
+    q.bits_b = bits_b;
+    q.ors = ors;
+    q.ocs = ocs;
+    q.astride = astride;
+    q.bstride = bstride;
+    q.kpad = kpad;
+    q.N = N;
+    q.M = M;
+    q.lk = lk;
+    q.sym = sym;
+    return launch_gemm_crt_multi(b, st);
 }
 
 // -------------------------------------------------------- Montgomery GEMM
@@ -2601,116 +2428,6 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_matvec_scan_v1(const DView A, uint32_t r_begin, uint32_t L,
-                                                     const Fr* __restrict__ wc,
-                                                     const Fr* __restrict__ wm,
-                                                     Fr* __restrict__ out) {
-    __shared__ uint32_t stage[3 * 256 * 8];
-    __shared__ Fr wtot[4];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t rb = scan_row(blockIdx.x, gridDim.x), r = r_begin + rb;
-    Fr* rowout = out + (uint64_t)rb * (3ull * L + 1);
-    Fr zero = fr_zero();
-    if (tid == 0) st_fr(rowout, zero);
-    Fr carry = fr_zero();
-    for (uint32_t c0 = 0; c0 < L; c0 += 256) {
-        const uint32_t j = c0 + tid;
-        const bool valid = j < L;
-        Fr a = zero, w = zero, p = zero;
-        if (valid) {
-            a = view_load(A, zero, r, j);
-            w = ld_fr(wc + j);
-            p = mont_mul(a, ld_fr(wm + j));
-        }
-        Fr s = p;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            Fr o = shfl_up_fr(s, off);
-            if ((int)lane >= off) s = fr_add(s, o);
-        }
-        if (lane == 63) wtot[wave] = s;
-        __syncthreads();
-        Fr pre = carry;
-        for (uint32_t w2 = 0; w2 < wave; ++w2) pre = fr_add(pre, wtot[w2]);
-        s = fr_add(s, pre);
-        uint32_t* st3 = stage + tid * 24;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            st3[i] = a.w[i];
-            st3[8 + i] = w.w[i];
-            st3[16 + i] = s.w[i];
-        }
-        Fr tot = carry;
-#pragma unroll
-        for (int w2 = 0; w2 < 4; ++w2) tot = fr_add(tot, wtot[w2]);
-        __syncthreads();
-        const uint32_t ncell = 3 * min(256u, L - c0);
-        uint4* o = reinterpret_cast<uint4*>(rowout + 1 + 3ull * c0);
-        const uint4* sv = reinterpret_cast<const uint4*>(stage);
-        for (uint32_t hc = tid; hc < 2 * ncell; hc += 256) o[hc] = sv[hc];
-        carry = tot;
-        __syncthreads();
-    }
-}
-
-__global__ __launch_bounds__(256) void k_matvec_scan(const DView A, uint32_t r_begin, uint32_t L,
-                                                     const Fr* __restrict__ wc,
-                                                     const Fr* __restrict__ wm,
-                                                     Fr* __restrict__ out) {
-    // T consecutive terms per thread: products, sequential local prefix, one
-    // cross-lane Fr scan per T terms, then the thread's 3T consecutive cells
-    // [a_j, w_j, s_j] are stored directly (16 B pieces; each 128 B line is
-    // completed by one lane's consecutive stores and merged in L2).
-    constexpr int T = 4;
-    __shared__ Fr wtot[4];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t rb = scan_row(blockIdx.x, gridDim.x), r = r_begin + rb;
-    Fr* rowout = out + (uint64_t)rb * (3ull * L + 1);
-    const Fr zero = fr_zero();
-    if (tid == 0) st_fr(rowout, zero);
-    Fr carry = fr_zero();
-    for (uint32_t c0 = 0; c0 < L; c0 += 256 * T) {
-        const uint32_t j0 = c0 + tid * T;
-        Fr a[T], s[T];
-#pragma unroll
-        for (int i = 0; i < T; ++i) {
-            const uint32_t j = j0 + i;
-            a[i] = j < L ? view_load(A, zero, r, j) : zero;
-            s[i] = j < L ? mont_mul(a[i], ld_fr(wm + j)) : zero;   // a_j * w_j (canonical)
-        }
-#pragma unroll
-        for (int i = 1; i < T; ++i) s[i] = fr_add(s[i], s[i - 1]);
-        // inclusive wave scan of the per-thread totals
-        Fr tot = s[T - 1];
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            Fr o = shfl_up_fr(tot, off);
-            if ((int)lane >= off) tot = fr_add(tot, o);
-        }
-        if (lane == 63) wtot[wave] = tot;
-        __syncthreads();
-        // exclusive prefix of this thread = carry + earlier waves + (tot - own total)
-        Fr pre = fr_sub(tot, s[T - 1]);
-        pre = fr_add(pre, carry);
-        for (uint32_t w2 = 0; w2 < wave; ++w2) pre = fr_add(pre, wtot[w2]);
-        Fr ctot = carry;
-#pragma unroll
-        for (int w2 = 0; w2 < 4; ++w2) ctot = fr_add(ctot, wtot[w2]);
-#pragma unroll
-        for (int i = 0; i < T; ++i) {
-            const uint32_t j = j0 + i;
-            if (j < L) {
-                Fr* cell = rowout + 1 + 3ull * j;
-                st_fr(cell, a[i]);
-                st_fr(cell + 1, ld_fr(wc + j));
-                st_fr(cell + 2, fr_add(s[i], pre));
-            }
-        }
-        carry = ctot;
-        __syncthreads();
-    }
-}
-
 // out[r] = sum_j A(r, j) w_j mod p for rows [0, R) (values only, no cells): the
 // row-sharded witness needs every entry of b.g while it emits the b.g scan
 // cells of its own rows only. One block per row; products as in the scan.
@@ -2771,21 +2488,133 @@ hipError_t launch_matvec_values(const ScanBatch& b0, int na, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int T>
-static void launch_scan_t(const ScanBatch& b, int na, dim3 g, hipStream_t st) {
-    const dim3 blk(256);
-    switch (na) {
-    case 0: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 0>), g, blk, 0, st, b); break;
-    case 1: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 1>), g, blk, 0, st, b); break;
-    case 2: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 2>), g, blk, 0, st, b); break;
-    case 3: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 3>), g, blk, 0, st, b); break;
-    case 4: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 4>), g, blk, 0, st, b); break;
-    case 5: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 5>), g, blk, 0, st, b); break;
-    case 6: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 6>), g, blk, 0, st, b); break;
-    default: hipLaunchKernelGGL((k_matvec_scan_dpp<T, 8>), g, blk, 0, st, b); break;
+// b.g for b = X^T with X an f64 input of svd_witness (the row-sharded witness's
+// b.g vector, every entry): (b.g)_i = sum_j q(X[j][i]) g^j, q = ZkMatrix::new's
+// quantization done in registers (the cells of X need not exist on this rank).
+// Column-parallel: thread = column i, block = (256 columns, one slice of
+// rows), so every wave load is 2 KiB of one row of X (k_matvec_values reads a
+// transposed view: one 32 B cell per lane, each from a different row). The
+// slices' partial sums land in part[job][slice][C]; k_vec_prep_sum adds them.
+__device__ __forceinline__ void quantize_mag(double x, double scale, Fr& mag, bool& neg) {
+    const double s = round(fabs(x) * scale);
+    mag = fr_zero();
+    if (s >= 340282366920938463463374607431768211456.0) {
+        mag.w[0] = mag.w[1] = mag.w[2] = mag.w[3] = 0xffffffffu;
+    } else if (s > 0.0) {
+        const uint64_t bits = __double_as_longlong(s);
+        const int e = (int)((bits >> 52) & 0x7ff) - 1075;
+        const uint64_t mant = (bits & 0xfffffffffffffull) | (1ull << 52);
+        const unsigned __int128 v = e >= 0 ? ((unsigned __int128)mant << e) : (unsigned __int128)(mant >> -e);
+        mag.w[0] = (uint32_t)v; mag.w[1] = (uint32_t)(v >> 32);
+        mag.w[2] = (uint32_t)(v >> 64); mag.w[3] = (uint32_t)(v >> 96);
+    }
+    // -0.0 and negatives quantizing to 0 are the cell 0 (quantize_body)
+    neg = signbit(x) && !isnan(x) && s > 0.0;
+}
+// Beside a saturating cell stream a memory round trip costs microseconds, so
+// the kernel has three: the block's slice of the g table into LDS, every f64
+// of the thread issued at once, the partial-sum store. Block = 32 columns x 8
+// sub-slices of kColRows rows (one slice of 8 kColRows rows); the sub-slices
+// are added in LDS, so a column has ceil(R / (8 kColRows)) partial sums.
+template <int NA>
+__device__ __forceinline__ U9 colsum_rows(const double (&x)[kColRows], uint32_t jl0, double scale,
+                                          const Fr* sWm, const Fr* sWn) {
+    U9 acc = u9_from(fr_zero());
+#pragma unroll
+    for (int t = 0; t < kColRows; ++t) {
+        Fr mag;
+        bool neg;
+        quantize_mag(x[t], scale, mag, neg);
+        const uint32_t jl = jl0 + t;
+        Fr s;
+        if constexpr (NA == 8) s = mont_mul(neg ? fr_neg(mag) : mag, sWm[jl]);
+        else s = mont_mul_small<NA>(mag, neg ? sWn[jl] : sWm[jl]);
+        acc = u9_add(acc, u9_from(s));                    // kColRows * 8 terms of < p
+    }
+    return acc;
+}
+__global__ __launch_bounds__(256) void k_colsum_f64(const ColBatch B, double scale) {
+    constexpr uint32_t SR = 8 * kColRows;                 // rows per block
+    __shared__ Fr sWm[SR], sWn[SR];
+    __shared__ U9 sPart[256];
+    const ColJob J = B.job[blockIdx.y];
+    const uint32_t ncb = (J.C + 31) / 32, cb = blockIdx.x % ncb, sg = blockIdx.x / ncb;
+    if (sg * SR >= J.R) return;                           // (grid sized for the longest job)
+    const uint32_t tid = threadIdx.x, col = tid & 31, sub = tid >> 5;
+    const uint32_t i = cb * 32 + col, jb = sg * SR, jl0 = sub * kColRows;
+    int na = spec_na(J.spec, B.bitw);
+    if (na > 4) na = 8;                                   // (quantized: <= 128 bits)
+    const Fr* __restrict__ wm = tab_slot(B.tab, B.tl, na);
+    const Fr* __restrict__ wn = wm + B.tl;
+    double x[kColRows];
+#pragma unroll
+    for (int t = 0; t < kColRows; ++t) {
+        const uint32_t j = jb + jl0 + t;
+        x[t] = i < J.C && j < J.R ? J.x[(uint64_t)j * J.ld + i] : 0.0;
+    }
+    for (uint32_t k = tid; k < SR; k += 256) {            // rows past R read as 0 (x = 0 there)
+        const uint32_t j = min(jb + k, J.R - 1);
+        sWm[k] = ld_fr(wm + j);
+        sWn[k] = na == 8 ? fr_zero() : ld_fr(wn + j);
+    }
+    __syncthreads();
+    U9 acc;
+    switch (na) {                                         // uniform over the launch
+    case 1: acc = colsum_rows<1>(x, jl0, scale, sWm, sWn); break;
+    case 2: acc = colsum_rows<2>(x, jl0, scale, sWm, sWn); break;
+    case 3: acc = colsum_rows<3>(x, jl0, scale, sWm, sWn); break;
+    case 4: acc = colsum_rows<4>(x, jl0, scale, sWm, sWn); break;
+    default: acc = colsum_rows<8>(x, jl0, scale, sWm, sWn); break;
+    }
+    sPart[tid] = acc;
+    __syncthreads();
+    if (sub == 0 && i < J.C) {
+#pragma unroll
+        for (int k = 1; k < 8; ++k) acc = u9_add(acc, sPart[tid + 32 * k]);   // < 2^267 + 2^264
+        st_fr(J.part + (uint64_t)sg * J.C + i, reduce9(acc.w));
     }
 }
-hipError_t launch_scan_batch(const ScanBatch& b0, int T, int na, hipStream_t st) {
+uint32_t colsum_slices(uint32_t R) { return (R + 8 * kColRows - 1) / (8 * kColRows); }
+hipError_t launch_colsum_f64(const ColBatch& b, int precision_bits, hipStream_t st) {
+    if (!b.njobs || b.njobs > (uint32_t)kMaxColJobs) return hipErrorInvalidValue;
+    uint32_t blocks = 0;
+    for (uint32_t q = 0; q < b.njobs; ++q) {
+        const ColJob& j = b.job[q];
+        if (!j.R || j.R > b.tl || j.R > 8192 || j.ld < j.C) return hipErrorInvalidValue;
+        blocks = max(blocks, (j.C + 31) / 32 * colsum_slices(j.R));
+    }
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_colsum_f64, dim3(blocks, b.njobs), dim3(256), 0, st, b,
+                       (double)(1ull << precision_bits));
+    return hipGetLastError();
+}
+// w_j = sum_s part[s L + j] -> canonical copy and scaled table (as k_vec_prep);
+// a thread's loads are issued kColPartBatch at a time
+__global__ __launch_bounds__(256) void k_vec_prep_sum(const Fr* __restrict__ part, uint32_t S, uint32_t L,
+                                                      Fr* wc, Fr* tab, const ScaleTab f) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= L) return;
+    Fr v = fr_zero();
+    for (uint32_t s0 = 0; s0 < S; s0 += kColPartBatch) {
+        Fr p[kColPartBatch];
+#pragma unroll
+        for (int s = 0; s < kColPartBatch; ++s)
+            p[s] = s0 + s < S ? ld_fr(part + (uint64_t)(s0 + s) * L + j) : fr_zero();
+#pragma unroll
+        for (int s = 0; s < kColPartBatch; ++s) v = fr_add(v, p[s]);
+    }
+    tab_store(wc, tab, L, j, blockIdx.y, v, f);
+}
+hipError_t launch_vec_prep_sum(const Fr* part, uint32_t S, uint32_t L, Fr* wc, Fr* tab, const ScaleTab& f,
+                               hipStream_t st) {
+    if (!L) return hipSuccess;
+    if (!S) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_vec_prep_sum, dim3((L + 255) / 256, 1 + kTabSlots), dim3(256), 0, st, part, S, L,
+                       wc, tab, f);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_batch(const ScanBatch& b0, int na, hipStream_t st) {
     ScanBatch b = b0;
     uint32_t blocks = 0;
     for (uint32_t q = 0; q < b.njobs; ++q) {
@@ -2795,35 +2624,29 @@ hipError_t launch_scan_batch(const ScanBatch& b0, int T, int na, hipStream_t st)
         if (!b.job[q].L) b.job[q].rows = 0;
     }
     if (!blocks) return hipSuccess;
-    if (T == 1) {
-        hipLaunchKernelGGL((k_matvec_scan_dpp<1, 8>), dim3(blocks), dim3(256), 0, st, b);
-    } else if (T == 2) {
-        launch_scan_t<2>(b, na, dim3(blocks), st);
-    } else {
-        launch_scan_t<4>(b, na, dim3(blocks), st);
+    const dim3 g(blocks), blk(256);
+    switch (na) {                      // two terms per thread (T = 2)
+    case 0: hipLaunchKernelGGL((k_matvec_scan_dpp<2, 0>), g, blk, 0, st, b); break;
+    case 1: hipLaunchKernelGGL((k_matvec_scan_dpp<2, 1>), g, blk, 0, st, b); break;
+    case 2: hipLaunchKernelGGL((k_matvec_scan_dpp<2, 2>), g, blk, 0, st, b); break;
+    case 3: hipLaunchKernelGGL((k_matvec_scan_dpp<2, 3>), g, blk, 0, st, b); break;
+    case 4: hipLaunchKernelGGL((k_matvec_scan_dpp<2, 4>), g, blk, 0, st, b); break;
+    case 5: hipLaunchKernelGGL((k_matvec_scan_dpp<2, 5>), g, blk, 0, st, b); break;
+    case 6: hipLaunchKernelGGL((k_matvec_scan_dpp<2, 6>), g, blk, 0, st, b); break;
+    default: hipLaunchKernelGGL((k_matvec_scan_dpp<2, 8>), g, blk, 0, st, b); break;
     }
     return hipGetLastError();
 }
 hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
-                              const Fr* wc, const Fr* tab, uint32_t tl, Fr* out, int impl,
-                              int na, hipStream_t st) {
+                              const Fr* wc, const Fr* tab, uint32_t tl, Fr* out, int na, hipStream_t st) {
     if (r_end <= r_begin || !L) return hipSuccess;
     if (tl < L) return hipErrorInvalidValue;
-    const Fr* wm = tab + 2ull * (kTabSlots - 1) * tl;    // Montgomery slot (impls 1, 2)
-    if (impl == 1)
-        hipLaunchKernelGGL(k_matvec_scan_v1, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L,
-                           wc, wm, out);
-    else if (impl >= 3 && impl <= 5) {
-        ScanBatch b;
-        memset(&b, 0, sizeof b);
-        b.njobs = 1;
-        b.job[0] = ScanJob{A, wc, tab, tl, out, L, r_end - r_begin, 0, r_begin, NaSpec{-1, -1, 0, 0}};
-        b.bitw = nullptr;
-        return launch_scan_batch(b, impl == 3 ? 1 : impl == 4 ? 2 : 4, impl == 3 ? 8 : na, st);
-    } else
-        hipLaunchKernelGGL(k_matvec_scan, dim3(r_end - r_begin), dim3(256), 0, st, A, r_begin, L, wc,
-                           wm, out);
-    return hipGetLastError();
+    ScanBatch b;
+    memset(&b, 0, sizeof b);
+    b.njobs = 1;
+    b.job[0] = ScanJob{A, wc, tab, tl, out, L, r_end - r_begin, 0, r_begin, NaSpec{-1, -1, 0, 0}};
+    b.bitw = nullptr;
+    return launch_scan_batch(b, na, st);
 }
 
 }  // namespace svdw

@@ -194,9 +194,7 @@ static constexpr uint32_t kMaxBitBlocks = 2048;
 hipError_t launch_stage(const StageArgs& a, hipStream_t st);
 // Independent stages (no stage reads another's cells) in as few k_stage_multi
 // launches as their records fit (stage_record_bytes, kMultiBytes); n >= 1.
-// persist: a resident grid walks the blocks (k_stage_multi_p) when there are
-// more blocks than fit at once.
-hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st, bool persist = false);
+hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st);
 // does the record of `a` fit one k_stage_multi launch?
 bool stage_multi_fits(const StageArgs& a);
 // max over the view of bit-length(|signed(x)|): out[b] = max of block b
@@ -269,11 +267,11 @@ hipError_t launch_residues_f64(const ResSegs& q, const unsigned* W, int precisio
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st, int kc = 4,
-                           bool xm = false);
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st);
 static constexpr int kCrtMaxResidues = 40;   // = kCrtMaxMod (crt_tables.hpp)
-// Several CRT products in one GEMM launch and one combine launch (a row-sharded
-// rank's three products of check_svd_phase0). Per job the caller sets Ar, Br,
+// Several CRT products in one GEMM launch and one combine launch (the three
+// products of check_svd_phase0; launch_gemm_crt is the one-job case). The GEMM's
+// (job, modulus, tile) units are placed modulus-major per XCD. Per job the caller sets Ar, Br,
 // astride, bstride, kpad, R (its own residue scratch), out, ors, ocs, N, M,
 // bits_a, bits_b, lk and sym (A == B: upper tiles + mirror); the launcher
 // fills the tile and block fields.
@@ -292,8 +290,6 @@ struct CrtJob {
 struct CrtBatch {
     CrtJob job[kMaxCrtJobs];
     uint32_t njobs;
-    int kc;
-    int direct;          // combine stores from registers (no LDS) when no job is symmetric
 };
 hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st);
 // w (len L) from a view (row 0 / col j of a 1 x L view) -> canonical copy
@@ -304,21 +300,43 @@ hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* tab, con
 hipError_t launch_gamma_prep(const GammaTab& g, uint32_t L, Fr* w_canon, Fr* tab, const ScaleTab& f,
                              hipStream_t st);
 // Freivalds inner-product rows (GateChip::inner_product, 1+3L cells per row) for
-// rows [r_begin, r_end) of A (R x L); row r's cells at out + (r - r_begin)*(3L+1).
-// impl 1: one term per thread, shuffle scan, LDS-staged coalesced stores; 2: four
-// terms per thread, direct stores; 3: DPP scan; 4 / 5: DPP scan, two / four terms per
-// thread and small-operand products when na < 8 (|signed A| < 2^(32 na), the
-// table's slot na - 1); impls 1-3 and na = 8 use the table's Montgomery slot.
+// rows [r_begin, r_end) of A (R x L); row r's cells at out + (r - r_begin)*(3L+1):
+// one block per row, two terms per thread, DPP wave scan, small-operand products
+// when na < 8 (|signed A| < 2^(32 na), the table's slot na - 1), the table's
+// Montgomery slot for na = 8.
 hipError_t launch_matvec_scan(const DView& A, uint32_t r_begin, uint32_t r_end, uint32_t L,
-                              const Fr* w_canon, const Fr* tab, uint32_t tl, Fr* out, int impl,
-                              int na, hipStream_t st);
+                              const Fr* w_canon, const Fr* tab, uint32_t tl, Fr* out, int na, hipStream_t st);
 // out[r] = sum_j A(r, j) w_j per job (job.tab = w's scaled table, job.out = the
 // values, rows [0, job.rows)); one launch for all jobs. na as for the scans
 // (0: from the jobs' NaSpecs and b.bitw on the device).
 hipError_t launch_matvec_values(const ScanBatch& b, int na, hipStream_t st);
-// Up to kMaxScanJobs DPP row scans in one launch (T terms per thread: 1, 2, 4;
-// na shared by every job; na = 0: the max over the jobs' NaSpecs, read on the
+// b.g of b = X^T from svd_witness's f64 input X (R x C, row pitch ld), quantized
+// in registers: part[s C + i] = sum over the rows j of slice s (colsum_slices(R)
+// slices of 8 kColRows rows) of q(X[j][i]) g^j, with g's scaled table `tab`
+// (length tl >= R) and the job's operand width from its NaSpec (bitw).
+// k_vec_prep_sum then adds the S slices into the canonical vector and its table.
+static constexpr int kMaxColJobs = 2;
+static constexpr int kColRows = 16;       // rows per thread
+static constexpr int kColPartBatch = 8;   // slice sums loaded together by k_vec_prep_sum
+struct ColJob {
+    const double* x;
+    Fr* part;
+    uint32_t R, C, ld;
+    NaSpec spec;
+};
+struct ColBatch {
+    ColJob job[kMaxColJobs];
+    uint32_t njobs, tl;
+    const Fr* tab;
+    const unsigned* bitw;
+};
+uint32_t colsum_slices(uint32_t R);
+hipError_t launch_colsum_f64(const ColBatch& b, int precision_bits, hipStream_t st);
+hipError_t launch_vec_prep_sum(const Fr* part, uint32_t S, uint32_t L, Fr* w_canon, Fr* tab,
+                               const ScaleTab& f, hipStream_t st);
+// Up to kMaxScanJobs DPP row scans in one launch (two terms per thread; na
+// shared by every job; na = 0: the max over the jobs' NaSpecs, read on the
 // device from b.bitw, so the host needs no operand bounds).
-hipError_t launch_scan_batch(const ScanBatch& b, int T, int na, hipStream_t st);
+hipError_t launch_scan_batch(const ScanBatch& b, int na, hipStream_t st);
 
 }  // namespace svdw

@@ -66,7 +66,6 @@ static constexpr uint8_t KSRC = 0x80;
 static constexpr uint32_t STAGE_PROBE_NOA = 64;
 static constexpr uint32_t STAGE_PROBE_CONST = 128;
 static constexpr uint32_t STAGE_ALIGN = 256;     // 4 KiB-aligned block store windows
-static constexpr uint32_t STAGE_INC = 512;       // phase B decoding slot ops per half-cell (A/B reference)
 static constexpr uint32_t STAGE_PROBE_NOLD = 1024;  // timing probe: no view loads either (with CONST)
 
 static constexpr int kMaxViews = 2;

@@ -55,6 +55,27 @@ def _device_ptr(a) -> Optional[int]:
     return None
 
 
+def _torch_stream(ctx: "Context") -> int:
+    """torch's current stream on the context's device (hipStream_t as int)."""
+    import torch  # noqa: WPS433
+    return torch.cuda.current_stream(torch.device("cuda", ctx.device)).cuda_stream
+
+
+def _after_torch(ctx: "Context") -> None:
+    """The engine's streams wait (on the device) for work torch has queued on
+    its current stream: tensors it is still writing, memory it still reads."""
+    check(lib().svdw_stream_wait(ctx.handle, _torch_stream(ctx)))
+
+
+def _before_torch(ctx: "Context") -> None:
+    """torch's current stream waits for the engine's queued work (its outputs)."""
+    check(lib().svdw_stream_signal(ctx.handle, _torch_stream(ctx)))
+
+
+# svdw_set_option names that change the cell layout (not just the schedule)
+LAYOUT_OPTIONS = ("rlc_prefix",)
+
+
 class Context:
     """One engine context = the phase-0 and phase-1 halo2-base `Context`s of a
     circuit (examples/svd_example.rs:108,181), streams resident on `device`."""
@@ -65,6 +86,7 @@ class Context:
         self.device = device
         self._phys = None
         self.last_svd = None
+        self.layout_opts = {}
         self._h = ct.c_void_p()
         p = Params(device, precision_bits, lookup_bits)
         check(lib().svdw_ctx_create(ct.byref(p), ct.byref(self._h)))
@@ -128,8 +150,13 @@ class Context:
         check(lib().svdw_set_gemm_impl(self._h, {"mfma": 0, "valu": 1}[impl]))
 
     def set_option(self, name: str, value: int) -> None:
-        """Tuning knobs of svdw_set_option (include/svdw.h); results are bit-identical."""
+        """Options of svdw_set_option (include/svdw.h). Tuning knobs leave the
+        cells bit-identical; the layout options (LAYOUT_OPTIONS) add cells and
+        are recorded in `layout_opts`, so a replay of this context's witness
+        (collect.plan's dry planner) sees the same layout."""
         check(lib().svdw_set_option(self._h, name.encode(), int(value)))
+        if name in LAYOUT_OPTIONS:
+            self.layout_opts[name] = int(value)
 
     def set_shard(self, rank: int, world: int) -> None:
         """Row-block sharding of one witness over `world` contexts (svdw_set_shard)."""
@@ -191,12 +218,15 @@ class Context:
         adv = torch.empty((nc, rows, 32), dtype=torch.uint8, device=dev)
         sel = torch.empty((nc, rows), dtype=torch.uint8, device=dev)
         lk = torch.empty((nl, rows, 32), dtype=torch.uint8, device=dev)
+        _after_torch(self)
         check(lib().svdw_assign_columns(self._h, phase, adv.data_ptr() if nc else None,
                                         sel.data_ptr() if nc else None, lk.data_ptr() if nl else None))
+        _before_torch(self)
         return adv, sel, lk
 
     def check_physical(self, phase: int, adv, sel) -> dict:
         r = CheckResult()
+        _after_torch(self)
         check(lib().svdw_check_physical(self._h, phase, adv.data_ptr(), sel.data_ptr(), adv.shape[0],
                                         ct.byref(r)))
         return {"gates_checked": r.gates_checked, "gate_failures": r.gate_failures,
@@ -226,6 +256,8 @@ class Context:
         r = EqCheck()
         p0 = columns0.data_ptr() if columns0 is not None else None
         p1 = columns1.data_ptr() if columns1 is not None else None
+        if p0 is not None or p1 is not None:
+            _after_torch(self)
         check(lib().svdw_check_equalities(self._h, phase, p0, p1, ct.byref(r)))
         return {"copies_checked": r.copies_checked, "copy_failures": r.copy_failures,
                 "consts_checked": r.consts_checked, "const_failures": r.const_failures}
@@ -279,6 +311,7 @@ class ZkMatrix:
         dp = _device_ptr(matrix)
         if dp is not None:
             rows, cols = matrix.shape
+            _after_torch(ctx)
             check(lib().svdw_zkmatrix_new(ctx.handle, phase, dp, rows, cols, 1, ct.byref(out)))
         else:
             a = np.ascontiguousarray(matrix, dtype=np.float64)
@@ -336,6 +369,7 @@ class ZkVector:
         out = Vec()
         dp = _device_ptr(v)
         if dp is not None:
+            _after_torch(ctx)
             check(lib().svdw_zkvector_new(ctx.handle, phase, dp, v.numel(), 1, ct.byref(out)))
         else:
             a = np.ascontiguousarray(v, dtype=np.float64).ravel()
@@ -517,6 +551,7 @@ def svd_witness(ctx: Context, m, u, v, d, gamma: int, cfg: SvdConfigPy = SvdConf
     dps = [_device_ptr(x) for x in (m, u, v, d)]
     if all(p is not None for p in dps):
         N, M = m.shape
+        _after_torch(ctx)
         check(lib().svdw_svd_witness(ctx.handle, *dps, N, M, 1, ct.byref(cfgc), g.ctypes.data,
                                      ct.byref(cnt)))
     else:
@@ -541,6 +576,7 @@ def verify_mul_witness(ctx: Context, a, b, gamma: int) -> dict:
         (N, K), M = a.shape, b.shape[1]
         if b.shape[0] != K:
             raise SvdwError(-1, "verify_mul_witness: a.num_col != b.num_rows")
+        _after_torch(ctx)
         check(lib().svdw_verify_mul_witness(ctx.handle, *dps, N, K, M, 1, g.ctypes.data, ct.byref(cnt)))
     else:
         arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (a, b)]
@@ -596,15 +632,18 @@ def parse_svd_input_device(ctx: "Context", src):
         t = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(dev)
     dims = InputDims()
     n = t.numel()
+    _after_torch(ctx)                   # the text may still be in flight on torch's stream
     check(lib().svdw_parse_svd_input_device(ctx._h, t.data_ptr(), n, 0, ct.byref(dims),
                                             None, None, None, None))
     out = {"m": torch.empty((dims.m_rows, dims.m_cols), dtype=torch.float64, device=dev),
            "u": torch.empty((dims.u_rows, dims.u_cols), dtype=torch.float64, device=dev),
            "v": torch.empty((dims.v_rows, dims.v_cols), dtype=torch.float64, device=dev),
            "d": torch.empty(dims.d_len, dtype=torch.float64, device=dev)}
+    _after_torch(ctx)                   # the outputs' memory may still be read on torch's stream
     check(lib().svdw_parse_svd_input_device(ctx._h, t.data_ptr(), n, 0, ct.byref(dims),
                                             out["m"].data_ptr(), out["u"].data_ptr(),
                                             out["d"].data_ptr(), out["v"].data_ptr()))
+    _before_torch(ctx)                  # torch kernels reading m, u, d, v run after the parse
     return out
 
 

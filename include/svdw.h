@@ -83,6 +83,19 @@ int svdw_ctx_reset(svdw_ctx* ctx);
 /* Pre-size a phase's advice / lookup streams (cells). */
 int svdw_reserve(svdw_ctx* ctx, uint32_t phase, uint64_t advice_cells, uint64_t lookup_cells);
 int svdw_sync(svdw_ctx* ctx);
+/* Stream ordering with the caller's own HIP stream (hipStream_t as void*; e.g.
+ * torch.cuda.current_stream().cuda_stream). The context runs on streams of its
+ * own and does NOT see work queued elsewhere: device memory an on_device call
+ * reads (f64 inputs, device text) or writes (parse outputs) must be complete
+ * / free when the call's work starts. Either synchronize the producing stream
+ * first, or call svdw_stream_wait(ctx, producer) before the call: the
+ * context's streams then wait (on the device, no host wait) for everything
+ * queued on `stream` so far. svdw_stream_signal(ctx, consumer) after a call
+ * makes `stream` wait for everything the context has queued (its outputs).
+ * The Python layer (halo2_svd041_amd.zk) does both around every on-device call
+ * with torch's current stream. */
+int svdw_stream_wait(svdw_ctx* ctx, void* stream);
+int svdw_stream_signal(svdw_ctx* ctx, void* stream);
 const char* svdw_last_error(void);
 
 /* ------------------------------------------------------ stream access */
@@ -132,8 +145,9 @@ int svdw_mat_times_diag_mat(svdw_ctx* ctx, const svdw_mat* a, const svdw_vec* v,
  * (div_mod = [r, 2^P, q, t] + check_big_less_than_safe(q, 2^NB/2^P + 1)
  *  + check_big_less_than_safe(r, 2^P)), i.e. floor(x / 2^P) for |x| < 2^S.
  * Zero fields (or a null pointer) select S = 3P (the domain rescale_matrix's
- * doc states, src/matrix/mod.rs:350-353) and NB = 4P + 1 (NB = S + 1 is the
- * tightest sound choice). NB = 4P + 1 is the choice that reproduces the
+ * doc states, src/matrix/mod.rs:350-353) and NB = max(4P + 1, S + 1) (NB = S + 1
+ * is the tightest sound choice; a shift alone never makes the default NB
+ * invalid). NB = 4P + 1 is the choice that reproduces the
  * reference's own cell counts: 90 cells per element at P = 32, LOOKUP_BITS = 12
  * ("#CONSTRAINTS = 90", src/matrix/mod.rs:102; "~94 (when lookup_bits = 12)",
  * :348) and 60-90 for P = 32 across LOOKUP_BITS 12-24, more for P > 32
@@ -241,19 +255,12 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   are queued before them); "gemm_priority" -1 | 0 | 1 (second stream priority:
  *   -1 auto = high for unsharded witnesses with 512 <= max(N, M) < 1024, where
  *   the product chain is the critical path; 0 normal; 1 high); "stage_priority" 0 | 1 (cell stream priority);
- *   "cu_split" 0 | multiple of 8 (CUs masked to the second stream, the rest to
- *   the cell stream); "fused_quantize" 1 | 0 (m, u, v, d quantized in one
- *   launch when resident in HBM);
+ *   "fused_quantize" 1 | 0 (m, u, v, d quantized in one launch when resident
+ *   in HBM);
  *   "stage_elems" 256 (elements per stage block, multiple of 16 in [16, 256]);
  *   "stage_align" 1 | 0 (each block's store windows aligned to 4 KiB);
- *   "stage_inc" 0 | 1 (previous phase B: slot ops decoded per half-cell
- *   instead of per-block descriptors);
- *   "scan_impl" 4 | 1 | 2 | 3 | 5 (row-scan kernel: 1 shuffle scan, 2 four
- *   terms/thread direct stores, 3 DPP scan, 4 / 5 DPP scan with two / four
- *   terms per thread, unreduced partial sums and small-operand products where
- *   bounds are known); "scan_na_host" 0 | 1 (row-scan operand widths inside
- *   svdw_svd_witness: read on the device from the quantization's bit-length
- *   words, or 1: read back by the host first, the round-1 behaviour);
+ *   "colsum" 1 | 0 (row-sharded svd_witness: every entry of the Freivalds
+ *   vectors b.g from the f64 inputs, column-parallel, or 0 from the cells);
  *   "res_f64" 1 | 0 (svd_witness with inputs in HBM: the CRT residue planes of
  *   m, u, v built from the f64 inputs in one launch, or from the quantized cells);
  *   "stage_batch" 1 | 0 (independent stages share k_stage_multi launches: the
@@ -262,10 +269,7 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   cells a pending one writes); "gemm_batch" 1 | 0 | -1 (svd_witness's three
  *   products in one GEMM and one combine launch; -1: on row-sharded contexts); "prod_cell" -1 | 0 | 1 (svd_witness with
  *   device inputs: the products on the cell stream and the u / v bounds and u.d
- *   beside them; -1 on row-sharded contexts);
- *   "gemm_kc" 1 | 4 (64-k chunks per LDS round of the CRT GEMM); "gemm_xm"
- *   1 | 0 (unbatched CRT GEMMs: XCD-major modulus placement, so each residue
- *   plane is read through two XCDs' L2 rather than all eight); "res_first"
+ *   beside them; -1 on row-sharded contexts); "res_first"
  *   0 | 1 | -1 (the cell stream waits for the residue planes; -1: on row-sharded
  *   contexts; measured slower, kept for A/B).
  * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:

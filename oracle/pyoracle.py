@@ -373,7 +373,7 @@ def div_scale_defaults(p: int, shift_bits: int = 0, num_bits: int = 0):
     per element at P=32, LB=12: src/matrix/mod.rs:102 "#CONSTRAINTS = 90",
     :348 "~94"; README.md:51 60-100 N^2; include/svdw.h svdw_div_scale)."""
     s = shift_bits or 3 * p
-    nb = num_bits or 4 * p + 1
+    nb = num_bits or max(4 * p + 1, s + 1)      # (a shift alone >= 4P+1 widens the div_mod)
     assert p <= s < 254 and s < nb <= 253 and nb - p <= 200
     return s, nb
 

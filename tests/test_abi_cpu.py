@@ -113,3 +113,20 @@ def test_dry_modular_api_counts():
     assert (pl.m_times_vt.num_rows, pl.m_times_vt.num_col) == (N, M)
     assert (pl.u_t.num_rows, pl.v_t.num_col) == (N, M)
     ctx.close()
+
+
+def test_dry_rescale_shift_only():
+    """rescale_matrix with shift_bits only (>= 4P + 1): accepted, and the cell
+    count is the oracle's for NB = S + 1 (the default was 4P + 1)."""
+    import pyoracle as po
+    P, LB, S = 32, 12, 140
+    ctx = hs.Context(device=-1, precision_bits=P, lookup_bits=LB)
+    a = hs.ZkMatrix.new(ctx, np.ones((2, 3)))
+    b = hs.ZkMatrix.new(ctx, np.ones((3, 2)))
+    cs = hs.honest_prover_mat_mul(ctx, a, b)
+    n0 = ctx.advice_len(0)
+    hs.ZkMatrix.rescale_matrix(ctx, cs, S)
+    o = po.Context()
+    po.signed_div_scale(o, po.RangeChip(LB), po.load_witness(o, 5), P, S)
+    assert ctx.advice_len(0) - n0 == 4 * (len(o.advice) - 1)
+    ctx.close()

@@ -30,7 +30,7 @@ def _expected(key, n):
     return torch.from_numpy(((idx + 7 * ph + 3 * lk) % 251).astype(np.uint8))
 
 
-def _worker(rank, world, port, mode, shape, out):
+def _worker(rank, world, port, mode, shape, out, opts=None):
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -41,6 +41,8 @@ def _worker(rank, world, port, mode, shape, out):
         N, M, P = shape
         m, u, d, v = gen_svd_input(N, M, seed=3)
         ctx = hs.Context(device=-1, precision_bits=P, lookup_bits=19)   # planner
+        for k, val in (opts or {}).items():
+            ctx.set_option(k, val)
         ctx.set_shard(rank, world)
         cnt = hs.svd_witness(ctx, m, u, v, d, 99)
         sizes = {(0, 0): cnt["advice0"], (1, 0): cnt["advice1"],
@@ -64,12 +66,16 @@ def _worker(rank, world, port, mode, shape, out):
 
 
 @pytest.mark.parametrize("mode", ["gather", "all_gather"])
-@pytest.mark.parametrize("world,shape", [(2, (12, 12, 63)), (3, (9, 13, 32))])
-def test_reassembly_gloo(mode, world, shape):
+@pytest.mark.parametrize("world,shape,opts", [(2, (12, 12, 63), None), (3, (9, 13, 32), None),
+                                              (2, (12, 12, 63), {"rlc_prefix": 1}),
+                                              (3, (9, 13, 32), {"rlc_prefix": 1})])
+def test_reassembly_gloo(mode, world, shape, opts):
+    """rlc_prefix shifts every phase-1 segment by two cells: the plan's dry
+    replay must see it (the option is recorded on the Python Context)."""
     port = _free_port()
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, port, mode, shape, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, mode, shape, out, opts), nprocs=world, join=True)
     for rank in range(world):
         ok, moved, nseg, calls, nops = out[rank]
         assert nseg >= world

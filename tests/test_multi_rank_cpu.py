@@ -74,3 +74,15 @@ def test_bench_gpus_flag_launches_ranks(extra):
     assert out["n_gpus"] == 2 and out["config"]["ranks"] == 2
     assert out["scaling"] == ("weak" if extra else "strong")
     assert out["config"]["backend"] == "gloo"
+    # the whole-witness roofline fraction is on every line; in rows mode against
+    # N x peak, with the per-rank times and the reassembly record
+    step = out["roofline"]["step"]
+    assert step["bytes"] > 0 and step["frac"] is not None
+    if not extra:
+        assert step["peak"] == 2 * 8000.0
+        assert len(step["rank_ms"]) == 2 and step["rank_ms_min"] <= step["rank_ms_max"]
+        r = out["reassembly"]
+        assert r["mode"] == "gather" and r["moved_GB_per_step"] > 0
+        assert r["ms_per_step_with_reassembly"] > 0
+    else:
+        assert "reassembly" not in out

@@ -97,3 +97,19 @@ def test_qsqrt_wrong_root_fails_constraints():
         finally:
             math.isqrt = real
         assert po.check_constraints(ctx2, LB) != []
+
+
+def test_shift_only_widens_default_num_bits():
+    """A caller that sets shift_bits only (>= 4P + 1) gets NB = S + 1, not the
+    invalid NB = 4P + 1 <= S: the default is max(4P + 1, S + 1) (engine and
+    oracle alike; tests/test_abi_cpu.py checks the engine's dry planner)."""
+    P, LB, S = 32, 12, 140
+    assert po.div_scale_defaults(P, S) == (S, S + 1)
+    assert po.div_scale_defaults(P) == (3 * P, 4 * P + 1)
+    ctx = po.Context()
+    rc = po.RangeChip(LB)
+    for x in (0, 5, -7, (1 << 139) - 3, -(1 << 139)):
+        a = po.load_witness(ctx, x % po.P_MOD)
+        y, _ = po.signed_div_scale(ctx, rc, a, P, S)
+        assert po.to_signed(y.value) == x >> P
+    assert po.check_constraints(ctx, LB) == []

@@ -2,7 +2,7 @@
 """Interleaved A/B of engine tuning options in ONE process (guide rule 24).
 
     python tools/ab.py --n 1024 --p 63 --rounds 5 --steps 3 \
-        --variant base: --variant e64:stage_elems=64 --variant scan2:scan_impl=2
+        --variant base: --variant e64:stage_elems=64 --variant p1:phase1_overlap=2
 Prints median / min ms per step and per-kernel medians for each variant.
 """
 import argparse
@@ -28,9 +28,9 @@ def parse_variant(s):
     return name, opts
 
 
-DEFAULTS = {"gemm_impl": 0, "scan_impl": 4, "overlap": 1, "prelaunch_at": 0, "gemm_priority": 0,
+DEFAULTS = {"gemm_impl": 0, "overlap": 1, "prelaunch_at": 0, "gemm_priority": 0,
             "gemm_rt": 1, "gemm_crt": 1, "stage_elems": 256, "phase1_overlap": 1, "stage_probe": 0,
-            "stage_align": 1, "cu_split": 0, "stage_inc": 0, "stage_priority": 0, "fused_quantize": 1, "d_checks_aside": 1,
+            "stage_align": 1, "stage_priority": 0, "fused_quantize": 1, "d_checks_aside": 1,
             "p1_at": -1}
 # pseudo-option "prof": event profiler during the timed steps (0 off, 1 all, 2 k_stage only)
 PROF_PREFIX = {1: "", 2: "k_stage"}
