@@ -500,6 +500,8 @@ struct svdw_ctx {
     std::vector<F64Src> f64src;
     DBuf colpart;                           // k_colsum_f64's per-slice partial sums
     bool colsum = true;                     // "colsum": that path (else k_matvec_values on the cells)
+    bool prod_first = false;                // "prod_first": the first stages wait for the products
+    int gemm_lds = 0;                       // "gemm_lds": CRT GEMM tiles through LDS (1) or not (0)
     // second stream: GEMMs overlap the HBM-bound stages; third: phase 1
     hipStream_t st2 = nullptr;
     bool st2_hi = false;                    // st2 is the high-priority stream
@@ -542,9 +544,13 @@ struct svdw_ctx {
         std::string name;
         double bytes;
     };
+    // A batch holds groups issued in order, one k_stage_multi launch each: a
+    // stage joins the group after the last one holding a stage whose cells it
+    // reads, so a dependent stage (entries_in_desc_order's range checks of its
+    // subtractions) defers only itself, not the independent stages after it.
     struct Batch {
         hipStream_t st;
-        std::vector<Pending> progs;
+        std::vector<std::vector<Pending>> groups;
     };
     std::vector<Batch> batches;
     bool stage_batch = true;
@@ -857,9 +863,8 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     const double bytes = 32.0 * (ee - eb) * ((double)a.C + a.L + loads);
     for (auto& b : c->batches) {
         if (b.st != c->st || !stage_multi_fits(a)) continue;
-        // a stage reading cells that a pending stage writes starts a new launch
-        bool dep = false;
-        for (const auto& q : b.progs) {
+        // does this stage read cells that pending stage q writes?
+        auto reads = [&](const svdw_ctx::Pending& q) {
             const char* w0 = reinterpret_cast<const char*>(q.a.out_adv);
             const char* w1 = w0 + sizeof(Fr) * (uint64_t)q.a.e_end * q.a.C;
             for (int k = 0; k < kMaxViews; ++k) {
@@ -871,11 +876,16 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
                 const int64_t lo = std::min<int64_t>(dr, 0) + std::min<int64_t>(dc, 0),
                               hi = std::max<int64_t>(dr, 0) + std::max<int64_t>(dc, 0) + 1;
                 const char* p = reinterpret_cast<const char*>(v.ptr);
-                if (p + lo * (int64_t)sizeof(Fr) < w1 && p + hi * (int64_t)sizeof(Fr) > w0) dep = true;
+                if (p + lo * (int64_t)sizeof(Fr) < w1 && p + hi * (int64_t)sizeof(Fr) > w0) return true;
             }
-        }
-        if (dep) flush_batch(c, c->st);
-        b.progs.push_back({a, std::string("k_stage:") + tag, bytes});
+            return false;
+        };
+        size_t g = 0;                                     // after the last group it depends on
+        for (size_t k = 0; k < b.groups.size(); ++k)
+            for (const auto& q : b.groups[k])
+                if (reads(q)) g = k + 1;
+        if (g == b.groups.size()) b.groups.emplace_back();
+        b.groups[g].push_back({a, std::string("k_stage:") + tag, bytes});
         return;
     }
     {
@@ -886,18 +896,21 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
 // Issue a stream's pending batched stages (k_stage_multi; one program: k_stage).
 static void flush_batch(svdw_ctx* c, hipStream_t s) {
     for (auto& b : c->batches) {
-        if (b.st != s || b.progs.empty()) continue;
-        std::vector<const StageArgs*> ps;
-        double bytes = 0;
-        for (const auto& q : b.progs) {
-            ps.push_back(&q.a);
-            bytes += q.bytes;
+        if (b.st != s || b.groups.empty()) continue;
+        std::vector<std::vector<svdw_ctx::Pending>> groups;
+        groups.swap(b.groups);               // (cleared before launching: no re-entry)
+        for (const auto& grp : groups) {
+            if (grp.empty()) continue;
+            std::vector<const StageArgs*> ps;
+            double bytes = 0;
+            for (const auto& q : grp) {
+                ps.push_back(&q.a);
+                bytes += q.bytes;
+            }
+            const std::string name = grp.size() == 1 ? grp[0].name : "k_stage:multi";
+            ProfScope pr(c, s, name, bytes, 0, true);
+            hipck(launch_stage_multi(ps.data(), (int)ps.size(), s), "k_stage_multi");
         }
-        const std::string name = b.progs.size() == 1 ? b.progs[0].name : "k_stage:multi";
-        std::vector<svdw_ctx::Pending> progs;
-        progs.swap(b.progs);                 // (cleared before launching: no re-entry)
-        ProfScope pr(c, s, name, bytes, 0, true);
-        hipck(launch_stage_multi(ps.data(), (int)ps.size(), s), "k_stage_multi");
     }
 }
 // RAII: stage launches on the current stream between construction and end()
@@ -1062,9 +1075,14 @@ static svdw_vec put_cell(svdw_ctx* c, uint32_t phase, const Fr& v, bool constant
 // only) instead of launching it here.
 // own_rows_only (row-sharded svd_witness, m): quantize only this rank's rows,
 // the only rows of the matrix any of its stages read.
+// own_rows_cols (row-sharded svd_witness, square u and v, b.g from the f64
+// inputs): store only this rank's rows and its column block, the cells its
+// stages (bounds, u.d, the a and b = X^T scans) read; the bit-length maxima
+// still cover the whole matrix (the GEMM's B operand).
 static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, uint32_t rows,
                              uint32_t cols, bool on_device, unsigned* blockmax = nullptr,
-                             QuantSegs* qs = nullptr, bool own_rows_only = false) {
+                             QuantSegs* qs = nullptr, bool own_rows_only = false,
+                             bool own_rows_cols = false) {
     REQUIRE(rows >= 1 && cols >= 1, "ZkMatrix::new: empty matrix");
     REQUIRE(data || c->dry, "null data");
     uint64_t n = (uint64_t)rows * cols, off;
@@ -1090,6 +1108,12 @@ static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, ui
             qs->out[k] = cellp(c, phase, off + q0);
             qs->blockmax[k] = blockmax;
             qs->n[k] = n;
+            qs->keep[k] = QuantKeep{0, 0, 0, 0, 0};
+            if (own_rows_cols && sharded(c) && rows == cols) {
+                uint64_t r0, r1;
+                shard_rows(c, rows, &r0, &r1);
+                qs->keep[k] = QuantKeep{cols, (uint32_t)r0, (uint32_t)r1, (uint32_t)r0, (uint32_t)r1};
+            }
             qs->blk0[k + 1] = qs->blk0[k] + (uint32_t)((n + 255) / 256);
         } else {
             ProfScope ps(c, c->st, "k_quantize", 40.0 * n, 0);
@@ -1382,7 +1406,7 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
             ProfScope ps(c, s, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * N * M,
                          (double)N * M * K);
             hipck(launch_gemm_crt(sym, Ar, Br, N, M, rpa, sym ? rpa : rpb,
-                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s),
+                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s, c->gemm_lds),
                   "k_gemm_crt");
         }
         if (!quantized)
@@ -2000,8 +2024,9 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
     }
     // res_first: the cell stream waits for the residue planes, which then run
     // alone instead of beside the first (HBM-saturating) stages
-    if (pst != c->st && (c->res_first > 0 || (c->res_first < 0 && sharded(c))))
-        stream_dep(c, pst, c->st);
+    // (products on the cell stream: the stages beside them on st2 wait instead)
+    if (c->res_first > 0 || (c->res_first < 0 && sharded(c)))
+        stream_dep(c, pst, pst != c->st ? c->st : c->st2);
     const uint8_t* P[3] = {(const uint8_t*)c->digA.p, (const uint8_t*)c->digC.p,
                            (const uint8_t*)c->digB.p};                 // A planes of m, u, v
     const uint32_t stride[3] = {rp_m, rp_u, rp_v}, kp[3] = {kpM, kpN, kpM}, lk[3] = {lkM, lkN, lkM};
@@ -2013,6 +2038,7 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
         // own residue scratch): one step of the st2 chain instead of three
         CrtBatch b;
         memset(&b, 0, sizeof b);
+        b.lds = c->gemm_lds;
         size_t rbytes[3], rtot = 0;
         for (int g = 0; g < 3; ++g) {
             rbytes[g] = (size_t)kCrtMaxResidues * ceil_to(std::max<uint32_t>((uint32_t)(rr1[g] - rr0[g]), 1), 128) *
@@ -2071,7 +2097,7 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
             ProfScope ps(c, pst, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * rows * cols,
                          (double)rows * cols * A[g].cols);
             hipck(launch_gemm_crt(sym, Ap, Bp, rows, cols, stride[g], bs, kp[g], (uint8_t*)c->crtR.p,
-                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], pst),
+                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], pst, c->gemm_lds),
                   "k_gemm_crt");
         }
         c->pre.push_back({log[g], stream_dep(c, pst, nullptr), pst});
@@ -2237,6 +2263,10 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     // d checks, in the same batch), and the cell stream waits for them before
     // the diff, by when they are done.
     const bool pc = c->prod_on_cell && c->prelaunched;
+    // prod_first: the bounds and u.d wait for the products (which then run with
+    // the chip to themselves instead of beside the first stage launch)
+    if (c->prod_first && c->prelaunched && !c->gemm_done.empty() && !c->dry)
+        hipck(hipStreamWaitEvent(pc ? c->st2 : c->st, c->gemm_done.back(), 0), "hipStreamWaitEvent");
     if (pc) std::swap(c->st, c->st2);
     BatchScope bs(c);
     const bool batched = bs.mine || pc;
@@ -2380,8 +2410,11 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     memset(&qs, 0, sizeof qs);
     QuantSegs* qp = c->fused_quantize ? &qs : nullptr;
     svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device, dbits ? dbits + 64 : nullptr, qp, true);
-    svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device, dbits ? dbits + 64 + nbm : nullptr, qp);
-    svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device, dbits ? dbits + 64 + nbm + nbu : nullptr, qp);
+    // (u, v: the rank's rows and column block only, when b.g comes from the f64 inputs)
+    const bool part = sharded(c) && on_device && c->colsum && N <= 8192 && M <= 8192;   // (f64_of's bound)
+    svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device, dbits ? dbits + 64 + nbm : nullptr, qp, false, part);
+    svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device, dbits ? dbits + 64 + nbm + nbu : nullptr, qp, false,
+                               part);
     svdw_mat zdm = zkmatrix_new(c, 0, d, r, 1, on_device, nullptr, qp);
     if (qs.nseg) {
         ProfScope ps(c, c->st, "k_quantize", 40.0 * ((double)N * M + (double)N * N + (double)M * M + r), 0);
@@ -3747,6 +3780,10 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->overlap = value != 0;
         } else if (n == "colsum") {                 // row-sharded b.g from the f64 inputs
             c->colsum = value != 0;
+        } else if (n == "prod_first") {
+            c->prod_first = value != 0;
+        } else if (n == "gemm_lds") {
+            c->gemm_lds = value != 0;
         } else {
             fail(SVDW_EINVAL, "unknown option " + n);
         }

@@ -66,7 +66,8 @@ __device__ __forceinline__ uint32_t signed_bits(const Fr& x) {
 // SURVEY.md Appendix C.1]
 __device__ __forceinline__ void quantize_body(const double* __restrict__ in, uint64_t n,
                                               Fr* __restrict__ out, double scale,
-                                              unsigned* __restrict__ blockmax, uint32_t blk) {
+                                              unsigned* __restrict__ blockmax, uint32_t blk,
+                                              QuantKeep keep = QuantKeep{0, 0, 0, 0, 0}) {
     uint64_t i = (uint64_t)blk * blockDim.x + threadIdx.x;
     // bit length of |x_q| for the GEMM digit-count choice (wave max, one atomic)
     uint32_t bits = 0;
@@ -87,6 +88,10 @@ __device__ __forceinline__ void quantize_body(const double* __restrict__ in, uin
             blockmax[blk] = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
     }
     if (i >= n) return;
+    if (keep.cols) {                                  // partial store (row-sharded rank)
+        const uint32_t r = (uint32_t)(i / keep.cols), cc = (uint32_t)(i - (uint64_t)r * keep.cols);
+        if (!((r >= keep.rlo && r < keep.rhi) || (cc >= keep.clo && cc < keep.chi))) return;
+    }
     double x = in[i];
     bool neg = signbit(x) && !isnan(x);
     double s = round(fabs(x) * scale);
@@ -119,10 +124,13 @@ __global__ __launch_bounds__(256) void k_quantize_multi(const QuantSegs q, doubl
     unsigned* bm = q.blockmax[0];
     uint64_t n = q.n[0];
     uint32_t b0 = q.blk0[0];
+    QuantKeep keep = q.keep[0];
 #pragma unroll
     for (int k = 1; k < kMaxQuantSegs; ++k)      // selects, not a dynamic index into the argument
-        if (s == (uint32_t)k) { in = q.in[k]; out = q.out[k]; bm = q.blockmax[k]; n = q.n[k]; b0 = q.blk0[k]; }
-    quantize_body(in, n, out, scale, bm, blockIdx.x - b0);
+        if (s == (uint32_t)k) {
+            in = q.in[k]; out = q.out[k]; bm = q.blockmax[k]; n = q.n[k]; b0 = q.blk0[k]; keep = q.keep[k];
+        }
+    quantize_body(in, n, out, scale, bm, blockIdx.x - b0, keep);
 }
 hipError_t launch_quantize_multi(const QuantSegs& q, int p, hipStream_t st) {
     if (!q.nseg || q.nseg > (uint32_t)kMaxQuantSegs || !q.blk0[q.nseg]) return hipErrorInvalidValue;
@@ -416,8 +424,11 @@ __device__ __forceinline__ void element_program(const StageArgs& a, uint32_t e, 
                 // is_equal rows are all zero): a select would always run it
                 Fr inv = fr_from_u64(1);
                 if (__any(!z)) {
+                    // word by word: `inv = z ? inv : t` on whole structs compiled
+                    // to a select between two stack copies (scratch, 80 B / lane)
                     const Fr t = fr_inv(v);
-                    inv = z ? inv : t;
+#pragma unroll
+                    for (int w = 0; w < 8; ++w) inv.w[w] = z ? inv.w[w] : t.w[w];
                 }
                 lds_put(dst, fr_from_u64(z ? 1 : 0));
                 lds_put(dst + VW, inv);
@@ -1455,15 +1466,31 @@ __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, co
             _Pragma("unroll") for (int b = 0; b < 4; ++b)                                     \
                 acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0); \
     }
-    uint4 s0a0, s0a1, s0b0, s0b1;
+    // Four 64-k chunks in flight in registers (16 VGPRs each): beside a
+    // saturating cell stream one global round trip costs microseconds, and with
+    // a single chunk ahead every 64-k step paid one in full (43 us per tile
+    // in-step at 1024^2 against ~2 us of MFMA work).
+    uint4 s0a0, s0a1, s0b0, s0b1, s1a0, s1a1, s1b0, s1b1;
+    uint4 s2a0, s2a1, s2b0, s2b1, s3a0, s3a1, s3b0, s3b1;
     CRT_GLOAD(s0, 0);
-    for (uint32_t c0 = 0; c0 < kcn; ++c0) {
-        CRT_LSTORE(s0, 0);
-        __syncthreads();
-        if (c0 + 1 < kcn) CRT_GLOAD(s0, c0 + 1);             // next chunk in flight
-        CRT_MMA(0);
-        __syncthreads();
+    CRT_GLOAD(s1, 1);
+    CRT_GLOAD(s2, 2);
+    CRT_GLOAD(s3, 3);
+#define CRT_STEP(g, c)                                                                        \
+    if ((c) < kcn) {                                                                          \
+        CRT_LSTORE(g, 0);                                                                     \
+        __syncthreads();                                                                      \
+        if ((c) + 4 < kcn) CRT_GLOAD(g, (c) + 4);                                             \
+        CRT_MMA(0);                                                                           \
+        __syncthreads();                                                                      \
     }
+    for (uint32_t c0 = 0; c0 < kcn; c0 += 4) {
+        CRT_STEP(s0, c0)
+        CRT_STEP(s1, c0 + 1)
+        CRT_STEP(s2, c0 + 2)
+        CRT_STEP(s3, c0 + 3)
+    }
+#undef CRT_STEP
 #undef CRT_GLOAD
 #undef CRT_LSTORE
 #undef CRT_MMA
@@ -1498,6 +1525,92 @@ __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, co
     }
 }
 
+
+// The same tile without LDS (gemm_lds 0): each wave loads its own MFMA
+// fragments straight from the residue planes (rows of 64 B per k-chunk, 16 B
+// per lane; the two waves sharing a row or column strip re-read it through L1),
+// four chunks in flight in registers, no barriers, and the residues stored as
+// bytes from the accumulators. Nothing of the block's LDS or barriers then
+// competes with the stage blocks it runs beside.
+__device__ __forceinline__ void crt_gemm_tile_direct(const uint8_t* __restrict__ Ar,
+                                                     const uint8_t* __restrict__ Br, uint32_t astride,
+                                                     uint32_t bstride, uint32_t kpad, uint32_t tiles_a,
+                                                     uint32_t tiles_m, uint8_t* __restrict__ R, uint32_t bi,
+                                                     uint32_t bj, int mod) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t wr = wave >> 1, wc = wave & 1;
+    const uint32_t frow = lane & 15, fk = (lane >> 4) * 16;
+    const uint64_t kp16 = 16ull * kpad;
+    const uint8_t* Apw = Ar + ((uint64_t)mod * astride + bi * CT + wr * 64 + frow) * kpad + fk;
+    const uint8_t* Bpw = Br + ((uint64_t)mod * bstride + bj * CT + wc * 64 + frow) * kpad + fk;
+    const uint32_t kcn = kpad / 64;
+    v4i acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = v4i{0, 0, 0, 0};
+#define CRD_GLOAD(g, chunk)                                                                   \
+    {                                                                                         \
+        const uint64_t ko = (uint64_t)min((uint32_t)(chunk), kcn - 1) * 64;                  \
+        g##a0 = *reinterpret_cast<const v4i*>(Apw + ko);                                      \
+        g##a1 = *reinterpret_cast<const v4i*>(Apw + kp16 + ko);                               \
+        g##a2 = *reinterpret_cast<const v4i*>(Apw + 2 * kp16 + ko);                           \
+        g##a3 = *reinterpret_cast<const v4i*>(Apw + 3 * kp16 + ko);                           \
+        g##b0 = *reinterpret_cast<const v4i*>(Bpw + ko);                                      \
+        g##b1 = *reinterpret_cast<const v4i*>(Bpw + kp16 + ko);                               \
+        g##b2 = *reinterpret_cast<const v4i*>(Bpw + 2 * kp16 + ko);                           \
+        g##b3 = *reinterpret_cast<const v4i*>(Bpw + 3 * kp16 + ko);                           \
+    }
+#define CRD_MMA1(g, i, j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(g##a##i, g##b##j, acc[i][j], 0, 0, 0);
+#define CRD_MMA(g)                                                                            \
+    {                                                                                         \
+        CRD_MMA1(g, 0, 0) CRD_MMA1(g, 0, 1) CRD_MMA1(g, 0, 2) CRD_MMA1(g, 0, 3)               \
+        CRD_MMA1(g, 1, 0) CRD_MMA1(g, 1, 1) CRD_MMA1(g, 1, 2) CRD_MMA1(g, 1, 3)               \
+        CRD_MMA1(g, 2, 0) CRD_MMA1(g, 2, 1) CRD_MMA1(g, 2, 2) CRD_MMA1(g, 2, 3)               \
+        CRD_MMA1(g, 3, 0) CRD_MMA1(g, 3, 1) CRD_MMA1(g, 3, 2) CRD_MMA1(g, 3, 3)               \
+    }
+#define CRD_STEP(g, c)                                                                        \
+    if ((c) < kcn) {                                                                          \
+        CRD_MMA(g)                                                                            \
+        if ((c) + 4 < kcn) CRD_GLOAD(g, (c) + 4);                                             \
+    }
+    v4i s0a0, s0a1, s0a2, s0a3, s0b0, s0b1, s0b2, s0b3;
+    v4i s1a0, s1a1, s1a2, s1a3, s1b0, s1b1, s1b2, s1b3;
+    v4i s2a0, s2a1, s2a2, s2a3, s2b0, s2b1, s2b2, s2b3;
+    v4i s3a0, s3a1, s3a2, s3a3, s3b0, s3b1, s3b2, s3b3;
+    CRD_GLOAD(s0, 0);
+    CRD_GLOAD(s1, 1);
+    CRD_GLOAD(s2, 2);
+    CRD_GLOAD(s3, 3);
+    for (uint32_t c0 = 0; c0 < kcn; c0 += 4) {
+        CRD_STEP(s0, c0)
+        CRD_STEP(s1, c0 + 1)
+        CRD_STEP(s2, c0 + 2)
+        CRD_STEP(s3, c0 + 3)
+    }
+#undef CRD_STEP
+#undef CRD_MMA
+#undef CRD_MMA1
+#undef CRD_GLOAD
+    const int m = (int)c_crt_mod[mod];
+    const float inv = c_crt_invf[mod];
+    const uint32_t rpa = tiles_a * CT, rpb = tiles_m * CT;
+    uint8_t* Rp = R + ((uint64_t)mod * rpa + bi * CT + wr * 64) * (uint64_t)rpb + bj * CT + wc * 64 + (lane & 15);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                // |acc| <= 2^27: fp32 quotient off by at most one (m >= 71)
+                const int av = acc[a][b][reg];
+                const int q = (int)floorf((float)av * inv);
+                int r = av - __mul24(q, m);
+                r += r < 0 ? m : 0;
+                r -= r >= m ? m : 0;
+                Rp[(uint64_t)(a * 16 + (lane >> 4) * 4 + reg) * rpb + b * 16] = (uint8_t)r;
+            }
+}
 
 // The products of a CrtBatch in one launch, placed modulus-major per XCD: the
 // work units (job, modulus < the job's device-decided count n, tile) are laid
@@ -1538,177 +1651,110 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
     crt_gemm_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.tiles_a,
                   q.sym ? q.tiles_a : q.tiles_m, q.R, bi, bj, (int)mod, S);
 }
-
-// C from its n residues, written as canonical Fr to out[i*ors + j*ocs]; one
-// 32 x 32 tile per block (SYM: upper tiles, mirrored through LDS).
-template <bool SYM, bool DIRECT = false>
-__device__ __forceinline__ void crt_combine_block(const uint8_t* __restrict__ R, uint32_t rpad_a,
-                                                  uint32_t rpad_b, uint32_t N, uint32_t M,
-                                                  uint32_t tiles_m, Fr* __restrict__ out,
-                                                  int64_t ors, int64_t ocs,
-                                                  const unsigned* __restrict__ bits_a,
-                                                  const unsigned* __restrict__ bits_b, uint32_t lk,
-                                                  uint32_t blk, uint8_t* __restrict__ Ts) {
-    const int n = crt_nmod(*bits_a, *bits_b, lk);
-    if (!n) return;
+__global__ __launch_bounds__(256) void k_gemm_crt_multi_d(const CrtBatch b) {
+    uint32_t cnt[kMaxCrtJobs], total = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxCrtJobs; ++j) {
+        cnt[j] = 0;
+        if ((uint32_t)j < b.njobs)
+            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk;
+        total += cnt[j];
+    }
+    const uint32_t per = (total + 7) / 8, k = blockIdx.x >> 3;
+    if (k >= per) return;
+    uint32_t u = (blockIdx.x & 7) * per + k;
+    if (u >= total) return;
+    uint32_t j = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxCrtJobs - 1; ++q)
+        if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
+    const CrtJob& q = b.job[j];
+    const uint32_t mod = u / q.nblk, t = u - mod * q.nblk;
     uint32_t bi, bj;
-    if (SYM) {
-        uint32_t b = blk, r = 0, rowlen = tiles_m;
-        while (b >= rowlen) { b -= rowlen; ++r; --rowlen; }
-        bi = r; bj = r + b;
+    if (q.sym) {
+        uint32_t r = 0, rest = t, rowlen = q.tiles_a;
+        while (rest >= rowlen) { rest -= rowlen; ++r; --rowlen; }
+        bi = r; bj = r + rest;
     } else {
-        bi = blk / tiles_m;
-        bj = blk % tiles_m;
+        bi = t / q.tiles_m;
+        bj = t - bi * q.tiles_m;
     }
-    const uint32_t tid = threadIdx.x;
-    const uint32_t i0 = bi * MT, j0 = bj * MT;
+    crt_gemm_tile_direct(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad,
+                         q.tiles_a, q.sym ? q.tiles_a : q.tiles_m, q.R, bi, bj, (int)mod);
+}
+
+// C from its n residues, written as canonical Fr to out[i*ors + j*ocs]: one
+// element per thread, a block = kCombRows rows x 64 columns, so a wave reads 64
+// consecutive residue bytes per modulus (the n loads issued before the first
+// use: one memory latency, not n). C mod p = sum_k r_k E_k + q (-Mtot mod p),
+// q = floor(sum_k r_k inv_k / m_k + 1/2) in f64 (|C| < Mtot / 4 keeps it exact),
+// accumulated carry-free in 16-bit limbs, one 9-word reduction. SYM: elements
+// j >= i of the upper tiles (the GEMM computed upper and diagonal 128-tiles),
+// each also stored at (j, i).
+static constexpr uint32_t kCombRows = 4;
+__device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t tile) {
+    const int n = crt_nmod(*q.bits_a, *q.bits_b, q.lk);
+    if (!n) return;
+    const uint32_t cts = (q.M + 63) / 64, rg = tile / cts, jt = tile - rg * cts;
+    const uint32_t i = rg * kCombRows + (threadIdx.x >> 6), j = jt * 64 + (threadIdx.x & 63);
+    if (i >= q.N || j >= q.M || (q.sym && j < i)) return;
+    const uint32_t rpb = (q.sym ? q.tiles_a : q.tiles_m) * CT;
+    const uint64_t plane = (uint64_t)q.tiles_a * CT * rpb;
+    const uint8_t* __restrict__ rp = q.R + (uint64_t)i * rpb + j;
+    uint32_t r[kCrtMaxMod];
+#pragma unroll
+    for (int k = 0; k < kCrtMaxMod; ++k) r[k] = k < n ? rp[k * plane] : 0u;
     const int off = n * (n - 1) / 2;
-    const uint64_t plane = (uint64_t)rpad_a * rpad_b;
-    // four elements per thread (one row, columns tc0 .. tc0 + 3: one 4-byte load
-    // per modulus), interleaved for ILP
-    const uint32_t tc0 = (tid & 7) * 4, tr = tid >> 3;
-    const uint32_t* rp = reinterpret_cast<const uint32_t*>(R + (uint64_t)(i0 + tr) * rpad_b + j0 + tc0);
-    // 16 accumulators per element, one per 16-bit limb of ep: r (8 bit) x limb
-    // (16 bit) < 2^24, n <= 40 terms plus q x nmp stay below 2^31 -> no carries
-    uint32_t acc[4][16];
-    double s[4];
+    // 16 accumulators, one per 16-bit limb of E_k: r (8 bit) x limb (16 bit)
+    // < 2^24; n <= 40 terms plus q x nmp stay below 2^31 -> no carries
+    uint32_t acc[16];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        s[q] = 0.0;
+    for (int w = 0; w < 16; ++w) acc[w] = 0;
+    double sq = 0.0;
 #pragma unroll
-        for (int w = 0; w < 16; ++w) acc[q][w] = 0;
-    }
-    // the residue words of kU moduli are loaded together (one load per modulus
-    // and then a wait, as a plain loop compiles, puts n full memory latencies
-    // in a row); indices past n re-read the last plane and are not used
-    constexpr int kU = 8;
-    for (int k0 = 0; k0 < n; k0 += kU) {
-        uint32_t w4[kU];
-#pragma unroll
-        for (int i = 0; i < kU; ++i) w4[i] = rp[(uint64_t)min(k0 + i, n - 1) * (plane >> 2)];
-#pragma unroll
-        for (int i = 0; i < kU; ++i) {
-            const int k = k0 + i;
-            if (k >= n) break;
-            uint32_t r[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) r[q] = (w4[i] >> (8 * q)) & 0xffu;
-            const double fr = c_crt_frac[off + k];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) s[q] = fma((double)r[q], fr, s[q]);
+    for (int k = 0; k < kCrtMaxMod; ++k) {
+        if (k < n) {                                       // (uniform)
+            sq = fma((double)r[k], c_crt_frac[off + k], sq);
 #pragma unroll
             for (int w = 0; w < 8; ++w) {
-                const uint32_t e = c_crt_ep[off + k][w], lo = e & 0xffffu, hi = e >> 16;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    acc[q][2 * w] = __umul24(r[q], lo) + acc[q][2 * w];
-                    acc[q][2 * w + 1] = __umul24(r[q], hi) + acc[q][2 * w + 1];
-                }
+                const uint32_t e = c_crt_ep[off + k][w];
+                acc[2 * w] = __umul24(r[k], e & 0xffffu) + acc[2 * w];
+                acc[2 * w + 1] = __umul24(r[k], e >> 16) + acc[2 * w + 1];
             }
         }
     }
+    const uint32_t qq = (uint32_t)floor(sq + 0.5);         // < 2^14
+    uint32_t x[9];
+    uint64_t t = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t qq = (uint32_t)floor(s[q] + 0.5);   // < 2^14
-        uint32_t x[9];
-        uint64_t t = 0;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            const uint32_t e = c_crt_nmp[n][w];
-            t += (uint64_t)(__umul24(qq, e & 0xffffu) + acc[q][2 * w]) +
-                 ((uint64_t)(__umul24(qq, e >> 16) + acc[q][2 * w + 1]) << 16);
-            x[w] = (uint32_t)t;
-            t >>= 32;
-        }
-        x[8] = (uint32_t)t;
-        const Fr v = reduce9(x);
-        const uint32_t tc = tc0 + q;
-        if (DIRECT) {
-            // straight from registers: a thread's 4 elements are 128 contiguous
-            // bytes of a row-major product (no LDS, so the blocks fit beside
-            // resident stage blocks)
-            const uint32_t row = i0 + tr, col = j0 + tc;
-            if (row < N && col < M) {
-                uint4* dst = reinterpret_cast<uint4*>(out + (int64_t)row * ors + (int64_t)col * ocs);
-                dst[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
-                dst[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
-            }
-            if (SYM && bi != bj && col < N && row < M) {     // mirrored tile: (col, row)
-                uint4* mir = reinterpret_cast<uint4*>(out + (int64_t)col * ors + (int64_t)row * ocs);
-                mir[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
-                mir[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
-            }
-            continue;
-        }
-        uint4* dst = reinterpret_cast<uint4*>(Ts + (tr * MT + tc) * 32);
-        dst[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
-        dst[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+    for (int w = 0; w < 8; ++w) {
+        const uint32_t e = c_crt_nmp[n][w];
+        t += (uint64_t)(__umul24(qq, e & 0xffffu) + acc[2 * w]) +
+             ((uint64_t)(__umul24(qq, e >> 16) + acc[2 * w + 1]) << 16);
+        x[w] = (uint32_t)t;
+        t >>= 32;
     }
-    if (DIRECT) return;
-    __syncthreads();
-    for (uint32_t q = tid; q < MT * 64; q += 256) {
-        const uint32_t tr = q >> 6, hc = q & 63, tc = hc >> 1, h = hc & 1;
-        const uint32_t row = i0 + tr, col = j0 + tc;
-        if (row < N && col < M)
-            reinterpret_cast<uint4*>(out + (int64_t)row * ors + (int64_t)col * ocs)[h] =
-                reinterpret_cast<const uint4*>(Ts + (tr * MT + tc) * 32)[h];
-    }
-    if (SYM && bi != bj) {
-        for (uint32_t q = tid; q < MT * 64; q += 256) {
-            const uint32_t tc = q >> 6, hc = q & 63, tr = hc >> 1, h = hc & 1;
-            const uint32_t row = j0 + tc, col = i0 + tr;
-            if (row < M && col < N)
-                reinterpret_cast<uint4*>(out + (int64_t)row * ors + (int64_t)col * ocs)[h] =
-                    reinterpret_cast<const uint4*>(Ts + (tr * MT + tc) * 32)[h];
-        }
-    }
+    x[8] = (uint32_t)t;
+    const Fr v = reduce9(x);
+    st_fr(q.out + (int64_t)i * q.ors + (int64_t)j * q.ocs, v);
+    if (q.sym && j > i) st_fr(q.out + (int64_t)j * q.ors + (int64_t)i * q.ocs, v);
 }
-
 // Combine blocks of a CrtBatch (cblocks in all, job j from cblk0[j]) dealt
 // XCD-contiguously: XCD x takes a contiguous run of the row-major tile
-// sequence, so the 32-byte row pieces that neighbouring tiles read from one
-// 128-byte line of R come through the same L2.
-__device__ __forceinline__ uint32_t combine_tile(const CrtBatch& b, uint32_t cblocks, uint32_t* job) {
+// sequence, so the halves of a 128-byte residue line that neighbouring tiles
+// read come through the same L2.
+__global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b, uint32_t cblocks) {
     const uint32_t per = (cblocks + 7) / 8, t = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (t >= cblocks) return;
     uint32_t j = 0;
     for (uint32_t k = 1; k < b.njobs; ++k) j += t >= b.job[k].cblk0;
-    *job = j;
-    return t;
-}
-__global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b, uint32_t cblocks) {
-    uint32_t j;
-    const uint32_t t = combine_tile(b, cblocks, &j);
-    if (t >= cblocks) return;
-    const CrtJob& q = b.job[j];
-    const uint32_t blk = t - q.cblk0;
-    const uint32_t rpa = q.tiles_a * CT, rpb = (q.sym ? q.tiles_a : q.tiles_m) * CT;
-    __shared__ __attribute__((aligned(16))) uint8_t Ts[MT * MT * 32];
-    if (q.sym)
-        crt_combine_block<true>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
-                                q.bits_b, q.lk, blk, Ts);
-    else
-        crt_combine_block<false>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
-                                 q.bits_b, q.lk, blk, Ts);
-}
-// The same combine with direct register stores and no LDS, for batches without
-// a symmetric job (a row-sharded rank's row blocks): the blocks then fit beside
-// resident stage blocks. (Direct stores of the mirror tiles of a symmetric job
-// scatter and measured slower: 512^2 P=32 0.411-0.418 -> 0.426-0.428 ms.)
-__global__ __launch_bounds__(256) void k_crt_combine_multi_d(const CrtBatch b, uint32_t cblocks) {
-    uint32_t j;
-    const uint32_t t = combine_tile(b, cblocks, &j);
-    if (t >= cblocks) return;
-    const CrtJob& q = b.job[j];
-    const uint32_t rpa = q.tiles_a * CT, rpb = q.tiles_m * CT;
-    crt_combine_block<false, true>(q.R, rpa, rpb, q.N, q.M, q.ctiles_m, q.out, q.ors, q.ocs, q.bits_a,
-                                   q.bits_b, q.lk, t - q.cblk0, nullptr);
+    crt_combine_elem(b.job[j], t - b.job[j].cblk0);
 }
 
 hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
     CrtBatch b = b0;
     if (b.njobs < 1 || b.njobs > (uint32_t)kMaxCrtJobs) return hipErrorInvalidValue;
     uint32_t units = 0, cblocks = 0;
-    bool any_sym = false;
     for (uint32_t j = 0; j < b.njobs; ++j) {
         CrtJob& q = b.job[j];
         q.tiles_a = (q.N + CT - 1) / CT;
@@ -1719,31 +1765,28 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
         if (q.sym && q.N != q.M) return hipErrorInvalidValue;
         q.nblk = q.sym ? q.tiles_a * (q.tiles_a + 1) / 2 : q.tiles_a * q.tiles_m;
         units += kCrtMaxMod * q.nblk;                    // upper bound: n = kCrtMaxMod
-        const uint32_t sa = (q.N + MT - 1) / MT, sb = (q.M + MT - 1) / MT;
-        q.ctiles_m = q.sym ? sa : sb;
-        q.cblk0 = cblocks;
-        cblocks += q.sym ? sa * (sa + 1) / 2 : sa * sb;
-        any_sym |= q.sym != 0;
+        q.cblk0 = cblocks;                               // (SYM: lower tiles exit at once)
+        cblocks += (q.N + kCombRows - 1) / kCombRows * ((q.M + 63) / 64);
     }
-    hipLaunchKernelGGL(k_gemm_crt_multi, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
+    if (b.lds)
+        hipLaunchKernelGGL(k_gemm_crt_multi, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
+    else
+        hipLaunchKernelGGL(k_gemm_crt_multi_d, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const dim3 cg((cblocks + 7) / 8 * 8);
-    if (any_sym)
-        hipLaunchKernelGGL(k_crt_combine_multi, cg, dim3(256), 0, st, b, cblocks);
-    else
-        hipLaunchKernelGGL(k_crt_combine_multi_d, cg, dim3(256), 0, st, b, cblocks);
+    hipLaunchKernelGGL(k_crt_combine_multi, dim3((cblocks + 7) / 8 * 8), dim3(256), 0, st, b, cblocks);
     return hipGetLastError();
 }
 
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st) {
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st, int lds) {
     if (sym && (N != M || astride != bstride)) return hipErrorInvalidValue;
     CrtBatch b;
     memset(&b, 0, sizeof b);
     b.njobs = 1;
+    b.lds = lds;
     CrtJob& q = b.job[0];
     q.Ar = Ar;
     q.Br = sym ? Ar : Br;
@@ -2342,6 +2385,43 @@ __device__ __forceinline__ Fr scan_prod_rt(int na, const Fr& a, const Fr* __rest
     }
 }
 
+// scan_prod with the table entries already loaded (wmv = w * 2^(32 NA) or its
+// Montgomery form for NA = 8, wnv = -wmv)
+template <int NA>
+__device__ __forceinline__ Fr scan_prod_v(const Fr& a, const Fr& wmv, const Fr& wnv) {
+    if constexpr (NA == 8) {
+        return mont_mul(a, wmv);
+    } else {
+        const bool neg = a.w[7] != 0;
+        Fr mag = fr_zero(), wv;
+        uint32_t br = 0;
+#pragma unroll
+        for (int q = 0; q < NA; ++q) {
+            const uint32_t t = subb32(p_word(q), a.w[q], br);
+            mag.w[q] = neg ? t : a.w[q];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) wv.w[q] = neg ? wnv.w[q] : wmv.w[q];
+        return mont_mul_small<NA>(mag, wv);
+    }
+}
+template <int NA>
+__device__ __forceinline__ Fr scan_prod_pre(int na, const Fr& a, const Fr& wmv, const Fr& wnv) {
+    if constexpr (NA != 0) {
+        return scan_prod_v<NA>(a, wmv, wnv);
+    } else {
+        switch (na) {          // uniform over the launch
+        case 1: return scan_prod_v<1>(a, wmv, wnv);
+        case 2: return scan_prod_v<2>(a, wmv, wnv);
+        case 3: return scan_prod_v<3>(a, wmv, wnv);
+        case 4: return scan_prod_v<4>(a, wmv, wnv);
+        case 5: return scan_prod_v<5>(a, wmv, wnv);
+        case 6: return scan_prod_v<6>(a, wmv, wnv);
+        default: return scan_prod_v<8>(a, wmv, wnv);
+        }
+    }
+}
+
 template <int T, int NA>
 __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
     static_assert(256 % T == 0, "T divides the block");
@@ -2373,13 +2453,22 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
     }
     for (uint32_t c0 = 0; c0 < L; c0 += 256 * T) {
         const uint32_t j0 = c0 + tid * T;
-        Fr a[T], s[T];
+        // every load of the chunk issued together (the row operand, both table
+        // entries, the vector's canonical cell): one memory round trip per
+        // chunk instead of three dependent ones, which beside a saturating cell
+        // stream cost microseconds each
+        Fr a[T], w[T], tm[T], tn[T], s[T];
 #pragma unroll
         for (int i = 0; i < T; ++i) {
             const uint32_t j = j0 + i;
-            a[i] = j < L ? view_load(A, zero, r, j) : zero;
-            s[i] = j < L ? scan_prod_rt<NA>(na, a[i], wm, wn, j) : zero;
+            const bool in = j < L;
+            a[i] = in ? view_load(A, zero, r, j) : zero;
+            w[i] = in ? ld_fr(wc + j) : zero;
+            tm[i] = in ? ld_fr(wm + j) : zero;
+            tn[i] = in && na < 8 ? ld_fr(wn + j) : zero;
         }
+#pragma unroll
+        for (int i = 0; i < T; ++i) s[i] = j0 + i < L ? scan_prod_pre<NA>(na, a[i], tm[i], tn[i]) : zero;
         // local inclusive sums (< T p), the wave scan and the prefixes stay
         // unreduced (exact, < 2^265); each output is reduced once
         U9 loc[T];
@@ -2407,14 +2496,12 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
             if (tid / TPR == (uint32_t)q) {
 #pragma unroll
                 for (int i = 0; i < T; ++i) {
-                    const uint32_t j = j0 + i;
-                    const Fr w = j < L ? ld_fr(wc + j) : zero;
                     const Fr si = reduce9(u9_add(loc[i], pre).w);
                     uint4* st3 = stage + (tid % TPR) * RS + i * 6;
                     st3[0] = make_uint4(a[i].w[0], a[i].w[1], a[i].w[2], a[i].w[3]);
                     st3[1] = make_uint4(a[i].w[4], a[i].w[5], a[i].w[6], a[i].w[7]);
-                    st3[2] = make_uint4(w.w[0], w.w[1], w.w[2], w.w[3]);
-                    st3[3] = make_uint4(w.w[4], w.w[5], w.w[6], w.w[7]);
+                    st3[2] = make_uint4(w[i].w[0], w[i].w[1], w[i].w[2], w[i].w[3]);
+                    st3[3] = make_uint4(w[i].w[4], w[i].w[5], w[i].w[6], w[i].w[7]);
                     st3[4] = make_uint4(si.w[0], si.w[1], si.w[2], si.w[3]);
                     st3[5] = make_uint4(si.w[4], si.w[5], si.w[6], si.w[7]);
                 }

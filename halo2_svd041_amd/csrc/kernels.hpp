@@ -61,12 +61,19 @@ hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int precision_
 // Fold per-block maxima: out[s] = max(blockmax[begin[s] .. begin[s + 1])), s < nseg.
 // One launch quantizing up to 4 matrices (m, u, v, d of the SVD witness):
 // segment s covers blocks [blk0[s], blk0[s+1]) of 256 values.
+// Segment k may store only part of its cells (keep[k].cols != 0: value i is
+// element (i / cols, i % cols) and is stored when its row is in [rlo, rhi) or
+// its column in [clo, chi)); its bit-length maxima still cover every value.
 static constexpr int kMaxQuantSegs = 4;
+struct QuantKeep {
+    uint32_t cols, rlo, rhi, clo, chi;
+};
 struct QuantSegs {
     const double* in[kMaxQuantSegs];
     Fr* out[kMaxQuantSegs];
     unsigned* blockmax[kMaxQuantSegs];
     uint64_t n[kMaxQuantSegs];
+    QuantKeep keep[kMaxQuantSegs];
     uint32_t blk0[kMaxQuantSegs + 1];
     uint32_t nseg;
 };
@@ -267,7 +274,7 @@ hipError_t launch_residues_f64(const ResSegs& q, const unsigned* W, int precisio
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st);
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st, int lds = 0);
 static constexpr int kCrtMaxResidues = 40;   // = kCrtMaxMod (crt_tables.hpp)
 // Several CRT products in one GEMM launch and one combine launch (the three
 // products of check_svd_phase0; launch_gemm_crt is the one-job case). The GEMM's
@@ -285,11 +292,12 @@ struct CrtJob {
     const unsigned* bits_b;
     int64_t ors, ocs;
     uint32_t astride, bstride, kpad, N, M, lk, sym;
-    uint32_t tiles_a, tiles_m, nblk, blk0, ctiles_m, cblk0;
+    uint32_t tiles_a, tiles_m, nblk, cblk0;
 };
 struct CrtBatch {
     CrtJob job[kMaxCrtJobs];
     uint32_t njobs;
+    int lds;             // GEMM tiles staged through LDS (1) or fragments loaded per wave (0)
 };
 hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st);
 // w (len L) from a view (row 0 / col j of a 1 x L view) -> canonical copy

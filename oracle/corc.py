@@ -34,7 +34,7 @@ def lib():
         L.orc_svd_witness.argtypes = [
             ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_size_t, ct.c_size_t,
             ct.c_int, ct.c_int, ct.c_void_p, ct.c_double, ct.c_double, ct.c_double, ct.c_int,
-            ct.c_size_t,
+            ct.c_size_t, ct.c_size_t,
             ct.POINTER(u64p), ct.POINTER(ct.c_size_t), ct.POINTER(u64p), ct.POINTER(ct.c_size_t),
             ct.POINTER(u64p), ct.POINTER(ct.c_size_t)]
         L.orc_verify_mul_witness.restype = ct.c_int
@@ -73,8 +73,10 @@ def _take(ptr, n) -> np.ndarray:
 
 
 def svd_witness(m, u, v, d, p: int, lb: int, gamma: int, max_norm=100.0, eps_svd=1e-10,
-                eps_u=1e-10, max_bits_d=30, row_lim=None):
-    """Returns (advice0, lookup0, advice1) as (n,4) uint64 arrays of canonical cells."""
+                eps_u=1e-10, max_bits_d=30, row_lim=None, row_begin=0):
+    """Returns (advice0, lookup0, advice1) as (n,4) uint64 arrays of canonical cells.
+    row_lim / row_begin: only the rows [row_begin, row_begin + row_lim) of every
+    row-parallel stage (the others are computed in full)."""
     m = np.ascontiguousarray(m, dtype=np.float64)
     u = np.ascontiguousarray(u, dtype=np.float64)
     v = np.ascontiguousarray(v, dtype=np.float64)
@@ -85,7 +87,7 @@ def svd_witness(m, u, v, d, p: int, lb: int, gamma: int, max_norm=100.0, eps_svd
     n0, nl0, n1 = ct.c_size_t(), ct.c_size_t(), ct.c_size_t()
     rc = lib().orc_svd_witness(
         m.ctypes.data, u.ctypes.data, v.ctypes.data, d.ctypes.data, N, M, p, lb,
-        g.ctypes.data, max_norm, eps_svd, eps_u, max_bits_d,
+        g.ctypes.data, max_norm, eps_svd, eps_u, max_bits_d, row_begin,
         SIZE_MAX if row_lim is None else row_lim,
         ct.byref(a0), ct.byref(n0), ct.byref(l0), ct.byref(nl0), ct.byref(a1), ct.byref(n1))
     if rc != 0:

@@ -284,12 +284,15 @@ static omat transpose(omat a) {
         for (size_t j = 0; j < a.rows; ++j) AT(t, i, j) = AT(a, j, i);
     return t;
 }
-/* field_mat_mul + load_witness (src/matrix/mod.rs:510-568), rows [0, row_lim) */
-static omat honest_prover_mat_mul(octx *c, omat a, omat b, size_t row_lim) {
+/* the rows a sampled witness computes of every row-parallel stage: [rb, re) */
+typedef struct { size_t rb, re; } rwin;
+static int in_win(rwin w, size_t i) { return i >= w.rb && i < w.re; }
+/* field_mat_mul + load_witness (src/matrix/mod.rs:510-568), rows of the window */
+static omat honest_prover_mat_mul(octx *c, omat a, omat b, rwin w) {
     omat cs = mat_alloc(a.rows, b.cols);
     for (size_t i = 0; i < a.rows; ++i)
         for (size_t j = 0; j < b.cols; ++j) {
-            if (i >= row_lim) { AT(cs, i, j) = 0; continue; }
+            if (!in_win(w, i)) { AT(cs, i, j) = 0; continue; }
             fe e = fe_zero();
             for (size_t k = 0; k < a.cols; ++k)
                 e = fe_add(e, fe_mul(VAL(c, AT(a, i, k)), VAL(c, AT(b, k, j))));
@@ -297,8 +300,8 @@ static omat honest_prover_mat_mul(octx *c, omat a, omat b, size_t row_lim) {
         }
     return cs;
 }
-static void check_mat_diff_val(octx *c, omat a, const fe *bvals, omat b, size_t row_lim, big tol) {
-    for (size_t i = 0; i < a.rows && i < row_lim; ++i)
+static void check_mat_diff_val(octx *c, omat a, const fe *bvals, omat b, rwin w, big tol) {
+    for (size_t i = w.rb; i < a.rows && i < w.re; ++i)
         for (size_t j = 0; j < a.cols; ++j) {
             fe bv = bvals ? bvals[i == j ? 0 : 1] : VAL(c, AT(b, i, j));
             size_t d = g_sub(c, VAL(c, AT(a, i, j)), bv);
@@ -324,7 +327,7 @@ static void out_cells(octx *c, uint64_t **adv, size_t *na, uint64_t **lk, size_t
     }
 }
 
-static void verify_mul(octx *c, octx *c0, omat a, omat b, omat cs, fe gamma, size_t row_lim) {
+static void verify_mul(octx *c, octx *c0, omat a, omat b, omat cs, fe gamma, rwin w) {
     size_t d = cs.cols;
     fe *v = (fe *)malloc(d * sizeof(fe));
     { size_t k = push(c, fe_one()); v[0] = VAL(c, k); }      /* load_witness(1) */
@@ -333,9 +336,9 @@ static void verify_mul(octx *c, octx *c0, omat a, omat b, omat cs, fe gamma, siz
     fe *csv = (fe *)malloc(cs.rows * sizeof(fe)), *bv = (fe *)malloc(b.rows * sizeof(fe));
     fe *abv = (fe *)malloc(a.rows * sizeof(fe));
     octx tmp; ctx_init(&tmp, c->lb);
-#define IP_ROWS(M, VEC, OUT, LIM)                                              \
+#define IP_ROWS(M, VEC, OUT, W)                                                \
     for (size_t r = 0; r < (M).rows; ++r) {                                    \
-        octx *dst = r < (LIM) ? c : &tmp;                                      \
+        octx *dst = in_win((W), r) ? c : &tmp;                                 \
         tmp.n = 0;                                                             \
         fe s = fe_zero(); push(dst, fe_zero());                                \
         for (size_t j = 0; j < (M).cols; ++j) {                                \
@@ -345,29 +348,32 @@ static void verify_mul(octx *c, octx *c0, omat a, omat b, omat cs, fe gamma, siz
         }                                                                      \
         (OUT)[r] = s;                                                          \
     }
-    IP_ROWS(cs, v, csv, row_lim)
-    IP_ROWS(b, v, bv, row_lim)
-    IP_ROWS(a, bv, abv, row_lim)
+    IP_ROWS(cs, v, csv, w)
+    IP_ROWS(b, v, bv, w)
+    IP_ROWS(a, bv, abv, w)
 #undef IP_ROWS
-    for (size_t r = 0; r < a.rows && r < row_lim; ++r) g_is_equal(c, csv[r], abv[r]);
+    for (size_t r = w.rb; r < a.rows && r < w.re; ++r) g_is_equal(c, csv[r], abv[r]);
     ctx_free(&tmp);
     free(v); free(csv); free(bv); free(abv);
 }
 
 /*
  * Whole witness of examples/svd_example.rs:98-200 with the intended one-context
- * semantics. gamma: canonical 4x u64. row_lim limits every row-parallel stage
- * to its first row_lim rows (CPU-baseline sampling; SIZE_MAX = full witness).
+ * semantics. gamma: canonical 4x u64. row_begin / row_lim limit every
+ * row-parallel stage to its rows [row_begin, row_begin + row_lim) (CPU-baseline
+ * sampling, and the full-size parity of any row-sharded rank's rows; 0 /
+ * SIZE_MAX = the full witness); every other region is computed in full.
  * Outputs are malloc'd canonical cells (4 x u64 each); free with orc_free.
  */
 int orc_svd_witness(const double *m, const double *u, const double *v, const double *d,
                     size_t N, size_t M, int p, int lb, const uint64_t gamma_c[4],
                     double max_norm, double eps_svd, double eps_u, int max_bits_d,
-                    size_t row_lim,
+                    size_t row_begin, size_t row_lim,
                     uint64_t **adv0, size_t *n0, uint64_t **lk0, size_t *nl0,
                     uint64_t **adv1, size_t *n1) {
     if (p < 1 || p > 63 || lb < 1 || lb > 63 || !N || !M) return -1;
     size_t r = N < M ? N : M;
+    rwin w = {row_begin, row_lim > SIZE_MAX - row_begin ? SIZE_MAX : row_begin + row_lim};
     octx c0; ctx_init(&c0, lb);
     omat zm = orc_load_mat(&c0, m, N, M, p);
     omat zu = orc_load_mat(&c0, u, N, N, p);
@@ -384,9 +390,9 @@ int orc_svd_witness(const double *m, const double *u, const double *v, const dou
     for (size_t i = 0; i + 1 < r; ++i) dd[i] = g_sub(&c0, VAL(&c0, zd[i]), VAL(&c0, zd[i + 1]));
     for (size_t i = 0; i + 1 < r; ++i) range_check(&c0, dd[i], max_bits);
     big unit = big_u128(((u128)1 << p) + 1);
-    for (size_t i = 0; i < N && i < row_lim; ++i)
+    for (size_t i = w.rb; i < N && i < w.re; ++i)
         for (size_t j = 0; j < N; ++j) check_abs_less_than(&c0, VAL(&c0, AT(zu, i, j)), unit);
-    for (size_t i = 0; i < M && i < row_lim; ++i)
+    for (size_t i = w.rb; i < M && i < w.re; ++i)
         for (size_t j = 0; j < M; ++j) check_abs_less_than(&c0, VAL(&c0, AT(zv, i, j)), unit);
     omat ut = transpose(zu), vt = transpose(zv);
     omat ud = mat_alloc(N, M);
@@ -394,31 +400,31 @@ int orc_svd_witness(const double *m, const double *u, const double *v, const dou
     if (r != M) zero_idx = push(&c0, fe_zero());
     for (size_t i = 0; i < N; ++i) {
         for (size_t j = 0; j < r; ++j)
-            AT(ud, i, j) = i < row_lim ? g_mul(&c0, VAL(&c0, AT(zu, i, j)), VAL(&c0, zd[j])) : 0;
+            AT(ud, i, j) = in_win(w, i) ? g_mul(&c0, VAL(&c0, AT(zu, i, j)), VAL(&c0, zd[j])) : 0;
         for (size_t j = r; j < M; ++j) AT(ud, i, j) = zero_idx;
     }
-    omat mvt = honest_prover_mat_mul(&c0, zm, vt, row_lim);
+    omat mvt = honest_prover_mat_mul(&c0, zm, vt, w);
     big tol_svd = big_u128(scale_err(err_svd, p)), tol_u = big_u128(scale_err(err_u, p));
     if (!big_bits(tol_svd) || !big_bits(tol_u)) return -2;
-    check_mat_diff_val(&c0, ud, NULL, mvt, row_lim, tol_svd);
+    check_mat_diff_val(&c0, ud, NULL, mvt, w, tol_svd);
     fe q = fe_pow2((unsigned)p);
     size_t q2i = push(&c0, fe_mul(q, q)); fe q2 = VAL(&c0, q2i);
-    omat uut = honest_prover_mat_mul(&c0, zu, ut, row_lim);
+    omat uut = honest_prover_mat_mul(&c0, zu, ut, w);
     fe idv[2] = {q2, fe_zero()};
     push(&c0, fe_zero());
-    check_mat_diff_val(&c0, uut, idv, uut, row_lim, tol_u);
-    omat vvt = honest_prover_mat_mul(&c0, zv, vt, row_lim);
+    check_mat_diff_val(&c0, uut, idv, uut, w, tol_u);
+    omat vvt = honest_prover_mat_mul(&c0, zv, vt, w);
     push(&c0, fe_zero());
-    check_mat_diff_val(&c0, vvt, idv, vvt, row_lim, tol_u);
+    check_mat_diff_val(&c0, vvt, idv, vvt, w, tol_u);
 
     /* --- check_svd_phase1 (src/svd/mod.rs:127-144) --- */
     octx c1; ctx_init(&c1, lb);
     fe gamma = fe_from_canon(gamma_c);
     /* Phase-1 mat-vec rows read the phase-0 payload (cross-phase copies).
-       In sampled mode the c_s rows >= row_lim were not computed: give them 0. */
-    verify_mul(&c1, &c0, zm, vt, mvt, gamma, row_lim);
-    verify_mul(&c1, &c0, zu, ut, uut, gamma, row_lim);
-    verify_mul(&c1, &c0, zv, vt, vvt, gamma, row_lim);
+       In sampled mode the c_s rows outside the window were not computed (0). */
+    verify_mul(&c1, &c0, zm, vt, mvt, gamma, w);
+    verify_mul(&c1, &c0, zu, ut, uut, gamma, w);
+    verify_mul(&c1, &c0, zv, vt, vvt, gamma, w);
 
     out_cells(&c0, adv0, n0, lk0, nl0);
     out_cells(&c1, adv1, n1, NULL, NULL);
@@ -445,9 +451,10 @@ int orc_verify_mul_witness(const double *a, const double *b, const double *bw, s
     omat zb = orc_load_mat(&c0, b, k, m, p);
     omat zw = zb;
     if (bw) zw = orc_load_mat(&c0, bw, k, m, p);
-    omat cs = honest_prover_mat_mul(&c0, za, zw, (size_t)-1);
+    const rwin all = {0, (size_t)-1};
+    omat cs = honest_prover_mat_mul(&c0, za, zw, all);
     octx c1; ctx_init(&c1, 19);
-    verify_mul(&c1, &c0, za, zb, cs, fe_from_canon(gamma_c), (size_t)-1);
+    verify_mul(&c1, &c0, za, zb, cs, fe_from_canon(gamma_c), all);
     out_cells(&c0, adv0, n0, NULL, NULL);
     out_cells(&c1, adv1, n1, NULL, NULL);
     ctx_free(&c0); ctx_free(&c1);

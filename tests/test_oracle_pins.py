@@ -160,3 +160,25 @@ def test_field_ops_c_vs_python():
         if a:
             assert corc.fe_op("orc_fe_inv", a) == pow(a, P_MOD - 2, P_MOD)
     assert math.isclose(1.0, 1.0)
+
+
+@pytest.mark.parametrize("N,M,P,row_begin,row_lim", [(20, 20, 63, 8, 4), (17, 23, 32, 5, 6),
+                                                      (23, 17, 42, 0, 3), (12, 12, 63, 10, 9)])
+def test_oracle_row_window_is_slice_of_full(N, M, P, row_begin, row_lim):
+    """The C oracle's sampled mode with a row window (the full-size parity of a
+    row-sharded rank's rows) is exactly the full witness restricted to those
+    rows of every row-parallel region, walked through the engine's layout table
+    (dry planner)."""
+    import corc
+    import halo2_svd041_amd as hs
+    from conftest import gamma_for, gen_svd_input, walk_window
+    m, u, d, v = gen_svd_input(N, M, seed=N + M)
+    g = gamma_for(N * M)
+    full = dict(zip([(0, 0), (0, 1), (1, 0)], corc.svd_witness(m, u, v, d, P, 19, g)))
+    win = dict(zip([(0, 0), (0, 1), (1, 0)],
+                   corc.svd_witness(m, u, v, d, P, 19, g, row_lim=row_lim, row_begin=row_begin)))
+    with hs.Context(device=-1, precision_bits=P, lookup_bits=19) as dry:
+        hs.svd_witness(dry, m, u, v, d, g)
+        layout = dry.layout()
+    n = walk_window(layout, lambda ph, lk, off, k: full[(ph, lk)][off:off + k], win, row_begin, row_lim)
+    assert n > 0

@@ -450,12 +450,6 @@ def test_products_on_cell_stream_parity(gpu_ctx_factory, world, opts):
         assert bad.size == 0, f"{key}: {bad.size} cells differ, first at {bad[:8]}"
 
 
-# Regions of a witness that the C oracle's sampled mode (row_lim) truncates to
-# their first row_lim rows; every other region it computes in full.
-_ROW_LIMITED = {"check_mat_entries_bounded", "mat_times_diag_mat", "product", "check_mat_diff",
-                "scan", "verify_mul_is_equal"}
-
-
 @pytest.mark.parametrize("N,M,P,row_lim,device", [(1024, 1024, 63, 64, False), (512, 512, 32, 128, False),
                                                   (2048, 1024, 32, 24, False), (1024, 1024, 63, 32, True)])
 def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device):
@@ -467,6 +461,7 @@ def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device):
     loads, d checks and gamma powers entirely, the first row_lim rows of every
     bound / product / diff / scan / is_equal region."""
     import halo2_svd041_amd as hs
+    from conftest import walk_window
     m, u, d, v = gen_svd_input(N, M, seed=N + M + P)
     g = gamma_for(N * M)
     ctx = gpu_ctx_factory(P)
@@ -476,26 +471,40 @@ def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device):
         hs.svd_witness(ctx, m, u, v, d, g)
     ctx.sync()
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g, row_lim=row_lim)
+    get = lambda ph, lk, off, n: (ctx.lookups if lk else ctx.advice)(ph, off, n)   # noqa: E731
+    assert walk_window(ctx.layout(), get, {(0, 0): a0, (0, 1): l0, (1, 0): a1}, 0, row_lim) > 0
+
+
+@pytest.mark.parametrize("rank", [0, 3, 7])
+def test_full_size_shard_rank_parity(gpu_ctx_factory, rank):
+    """BASELINE config 4 (1024^2, P=63, row blocks over 8 GPUs), rank by rank at
+    full size, cell for cell: the rank's witness on the GPU (svdw_set_shard, the
+    bench's device-input path) against the C oracle's row window inside that
+    rank's rows ([128 rank + 40, +16) of every row-parallel region; every other
+    region in full), mapped through the layout table, on the cells the rank
+    owns (svdw_shard_segments). Together with the
+    owned-segment tiling (tests/test_shard_cpu.py) and the small-shape union
+    tests, every rank's cells are value-checked, not just rank 0's."""
+    import halo2_svd041_amd as hs
+    from conftest import walk_window
+    N, P, world, lim = 1024, 63, 8, 16
+    m, u, d, v = gen_svd_input(N, N, seed=2 * N + P)
+    g = gamma_for(N * N + 8)
+    ctx = gpu_ctx_factory(P)
+    ctx.set_shard(rank, world)
+    hs.svd_witness(ctx, *_on_device(m, u, v, d), g)
+    ctx.sync()
+    rb = N * rank // world + 40
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g, row_lim=lim, row_begin=rb)
+    # a row-sharded context writes (at least) the cells it owns: compare those
+    owned = {}
+    for ph, lk, off, n in ctx.shard_segments():
+        owned.setdefault((ph, lk), []).append((off, off + n))
+    get = lambda ph, lk, off, n: (ctx.lookups if lk else ctx.advice)(ph, off, n)   # noqa: E731
     want = {(0, 0): a0, (0, 1): l0, (1, 0): a1}
-    pos = {k: 0 for k in want}
-    compared = 0
-    for r in ctx.layout():
-        ph, rows = r["phase"], r["rows"]
-        keep = min(rows, row_lim) if r["tag"] in _ROW_LIMITED else rows
-        for lk, off, n in ((0, r["off"], r["n"]), (1, r["loff"], r["nl"])):
-            if not n or (ph, lk) not in want:
-                continue
-            take = n // rows * keep
-            got = (ctx.lookups if lk else ctx.advice)(ph, off, take)
-            ref = want[(ph, lk)][pos[(ph, lk)]:pos[(ph, lk)] + take]
-            bad = np.nonzero(np.any(got != ref, axis=1))[0]
-            assert bad.size == 0, f"{r['tag']} phase {ph} {'lookup' if lk else 'advice'}: " \
-                                  f"{bad.size} of {take} cells differ, first at {bad[:6]}"
-            pos[(ph, lk)] += take
-            compared += take
-    for k, w in want.items():                      # the walk consumed every oracle cell
-        assert pos[k] == w.shape[0], (k, pos[k], w.shape[0])
-    assert compared > 0
+    compared = walk_window(ctx.layout(), get, want, rb, lim, owned)
+    # the window's rows of every row-parallel region (all owned) were compared
+    assert compared >= 0.9 * (a1.shape[0] - 3 * (1 + 4 * (N - 1))), compared
 
 
 def _zkvector_inputs(N, M):
