@@ -119,6 +119,7 @@ SIGNATURES = {
     "svdw_sync": (_i32, [_P]),
     "svdw_stream_wait": (_i32, [_P, _P]),
     "svdw_stream_signal": (_i32, [_P, _P]),
+    "svdw_debug_trace": (_i32, [_P]),
     "svdw_last_error": (ct.c_char_p, []),
     "svdw_advice_len": (_u64, [_P, _u32]),
     "svdw_lookup_len": (_u64, [_P, _u32]),

@@ -501,7 +501,6 @@ struct svdw_ctx {
     DBuf colpart;                           // k_colsum_f64's per-slice partial sums
     bool colsum = true;                     // "colsum": that path (else k_matvec_values on the cells)
     bool prod_first = false;                // "prod_first": the first stages wait for the products
-    int gemm_lds = 0;                       // "gemm_lds": CRT GEMM tiles through LDS (1) or not (0)
     // second stream: GEMMs overlap the HBM-bound stages; third: phase 1
     hipStream_t st2 = nullptr;
     bool st2_hi = false;                    // st2 is the high-priority stream
@@ -1379,7 +1378,7 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
         // multi-modular path: residue planes, one int8 GEMM per modulus, CRT
         uint32_t lk = 0;
         while ((1ull << lk) < K) ++lk;
-        const uint32_t kpad = (K + 63) / 64 * 64;
+        const uint32_t kpad = (K + 255) / 256 * 256;      // whole groups of four 64-k chunks
         const uint32_t rpa = (N + 127) / 128 * 128, rpb = (M + 127) / 128 * 128;
         ensure_buf(c, c->crtR, (size_t)kCrtMaxResidues * rpa * (sym ? rpa : rpb));
         const uint8_t* Ar;
@@ -1406,7 +1405,7 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
             ProfScope ps(c, s, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * N * M,
                          (double)N * M * K);
             hipck(launch_gemm_crt(sym, Ar, Br, N, M, rpa, sym ? rpa : rpb,
-                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s, c->gemm_lds),
+                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s),
                   "k_gemm_crt");
         }
         if (!quantized)
@@ -1989,7 +1988,7 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
     const uint32_t N = A[0].rows, M = A[0].cols;
     auto clog2 = [](uint32_t k) { uint32_t l = 0; while ((1ull << l) < k) ++l; return l; };
     auto ceil_to = [](uint32_t x, uint32_t a) { return (x + a - 1) / a * a; };
-    const uint32_t lkM = clog2(M), lkN = clog2(N), kpM = ceil_to(M, 64), kpN = ceil_to(N, 64);
+    const uint32_t lkM = clog2(M), lkN = clog2(N), kpM = ceil_to(M, 256), kpN = ceil_to(N, 256);
     uint64_t rr0[3], rr1[3];
     for (int g = 0; g < 3; ++g) {
         rr0[g] = 0; rr1[g] = A[g].rows;
@@ -2038,7 +2037,6 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
         // own residue scratch): one step of the st2 chain instead of three
         CrtBatch b;
         memset(&b, 0, sizeof b);
-        b.lds = c->gemm_lds;
         size_t rbytes[3], rtot = 0;
         for (int g = 0; g < 3; ++g) {
             rbytes[g] = (size_t)kCrtMaxResidues * ceil_to(std::max<uint32_t>((uint32_t)(rr1[g] - rr0[g]), 1), 128) *
@@ -2097,7 +2095,7 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
             ProfScope ps(c, pst, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * rows * cols,
                          (double)rows * cols * A[g].cols);
             hipck(launch_gemm_crt(sym, Ap, Bp, rows, cols, stride[g], bs, kp[g], (uint8_t*)c->crtR.p,
-                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], pst, c->gemm_lds),
+                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], pst),
                   "k_gemm_crt");
         }
         c->pre.push_back({log[g], stream_dep(c, pst, nullptr), pst});
@@ -2859,6 +2857,9 @@ int svdw_stream_signal(svdw_ctx* c, void* stream) {
             hipck(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
         }
     });
+}
+int svdw_debug_trace(void* buf) {
+    return guarded([&] { hipck(set_debug_trace(buf), "set_debug_trace"); });
 }
 int svdw_sync(svdw_ctx* c) {
     return guarded([&] { REQUIRE(c, "null ctx"); sync(c); });
@@ -3782,8 +3783,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->colsum = value != 0;
         } else if (n == "prod_first") {
             c->prod_first = value != 0;
-        } else if (n == "gemm_lds") {
-            c->gemm_lds = value != 0;
         } else {
             fail(SVDW_EINVAL, "unknown option " + n);
         }

@@ -1401,7 +1401,8 @@ static constexpr int CT = 128;     // CRT GEMM block tile (4 waves of 64 x 64)
 // by (row >> 2) & 3: the staging stores (4 rows x 4 parts per 16 lanes) and the
 // fragment reads (16 rows x 1 part) both land on 16 distinct 4-bank groups.
 static constexpr int CROW = 64;
-static constexpr int CTS = 144;    // epilogue tile row stride (B): rows 4 apart in distinct banks
+static constexpr uint32_t kCrtTileBytes = CT * CT;             // residues of one (tile, modulus)
+static constexpr uint32_t kCombBlocksPerTile = kCrtTileBytes / 256;
 __device__ __forceinline__ uint32_t crt_lds(uint32_t row, uint32_t part) {
     return row * CROW + 16u * (part ^ ((row >> 2) & 3u));
 }
@@ -1412,13 +1413,18 @@ __device__ __forceinline__ uint32_t crt_lds(uint32_t row, uint32_t part) {
 // its planes from row r0 on with the full operand's stride); R is
 // [mod][tiles_a * CT][tiles_m * CT]. One 64-k chunk per LDS round, the next
 // chunk's global loads in flight under the current chunk's MFMAs.
-constexpr int crt_lds_bytes() { return 2 * CT * CROW > CT * CTS ? 2 * CT * CROW : CT * CTS; }
+// Software pipeline, one barrier per 64-k step: LDS is double-buffered (the
+// next chunk is stored into the other buffer while this chunk's MFMAs run from
+// fragments read before them), two chunks are in flight in registers behind
+// that, and the next step's fragment reads overlap the MFMAs still in the
+// pipe. (A single buffer with a store / barrier / read / MFMA / barrier chain
+// per step took ~1 us per step, ~16 us per tile, against ~0.1 us of MFMA.)
+constexpr int crt_lds_bytes() { return 4 * CT * CROW; }
 __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, const uint8_t* __restrict__ Br,
                                               uint32_t astride, uint32_t bstride, uint32_t kpad,
-                                              uint32_t tiles_a, uint32_t tiles_m, uint8_t* __restrict__ R,
-                                              uint32_t bi, uint32_t bj, int mod, uint8_t* __restrict__ S) {
-    uint8_t* As = S;
-    uint8_t* Bs = S + CT * CROW;
+                                              uint32_t nblk, uint32_t tile, uint8_t* __restrict__ R,
+                                              uint32_t bi, uint32_t bj, int mod, uint8_t* __restrict__ S,
+                                              uint64_t& tp1, uint64_t& tp2) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t wr = wave >> 1, wc = wave & 1;
     const uint8_t* Ap = Ar + ((uint64_t)mod * astride + bi * CT) * kpad;
@@ -1435,7 +1441,7 @@ __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, co
     // Staging registers per chunk as named variables, loops spelled out by macro
     // (arrays or lambdas over them ended up in scratch). Chunk indices past the
     // end are clamped to the last chunk, so the loads stay unconditional; those
-    // chunks are never multiplied.
+    // chunks are never stored or multiplied.
 #define CRT_GLOAD(g, chunk)                                                                   \
     {                                                                                         \
         const uint64_t ko = (uint64_t)min((uint32_t)(chunk), kcn - 1) * 64 + part * 16;     \
@@ -1444,64 +1450,83 @@ __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, co
         g##b0 = *reinterpret_cast<const uint4*>(Bp + (uint64_t)r0 * kpad + ko);             \
         g##b1 = *reinterpret_cast<const uint4*>(Bp + (uint64_t)r1 * kpad + ko);             \
     }
-#define CRT_LSTORE(g, c)                                                                      \
+#define CRT_LSTORE(g, buf)                                                                    \
     {                                                                                         \
-        uint8_t* Ac = As + (c) * CT * CROW;                                                   \
-        uint8_t* Bc = Bs + (c) * CT * CROW;                                                   \
+        uint8_t* Ac = S + (buf) * 2 * CT * CROW;                                              \
+        uint8_t* Bc = Ac + CT * CROW;                                                         \
         *reinterpret_cast<uint4*>(Ac + crt_lds(r0, part)) = g##a0;                            \
         *reinterpret_cast<uint4*>(Ac + crt_lds(r1, part)) = g##a1;                            \
         *reinterpret_cast<uint4*>(Bc + crt_lds(r0, part)) = g##b0;                            \
         *reinterpret_cast<uint4*>(Bc + crt_lds(r1, part)) = g##b1;                            \
     }
-#define CRT_MMA(c)                                                                            \
+#define CRT_FRAG(buf)                                                                         \
     {                                                                                         \
-        const uint8_t* Ac = As + (c) * CT * CROW;                                             \
-        const uint8_t* Bc = Bs + (c) * CT * CROW;                                             \
-        v4i af[4], bf[4];                                                                     \
+        const uint8_t* Ac = S + (buf) * 2 * CT * CROW;                                        \
+        const uint8_t* Bc = Ac + CT * CROW;                                                   \
         _Pragma("unroll") for (int a = 0; a < 4; ++a)                                         \
             af[a] = *reinterpret_cast<const v4i*>(Ac + crt_lds(wr * 64 + a * 16 + frow, fk >> 4)); \
         _Pragma("unroll") for (int b = 0; b < 4; ++b)                                         \
             bf[b] = *reinterpret_cast<const v4i*>(Bc + crt_lds(wc * 64 + b * 16 + frow, fk >> 4)); \
+    }
+#define CRT_MMA()                                                                             \
+    {                                                                                         \
         _Pragma("unroll") for (int a = 0; a < 4; ++a)                                         \
             _Pragma("unroll") for (int b = 0; b < 4; ++b)                                     \
                 acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0); \
     }
-    // Four 64-k chunks in flight in registers (16 VGPRs each): beside a
-    // saturating cell stream one global round trip costs microseconds, and with
-    // a single chunk ahead every 64-k step paid one in full (43 us per tile
-    // in-step at 1024^2 against ~2 us of MFMA work).
-    uint4 s0a0, s0a1, s0b0, s0b1, s1a0, s1a1, s1b0, s1b1;
-    uint4 s2a0, s2a1, s2b0, s2b1, s3a0, s3a1, s3b0, s3b1;
-    CRT_GLOAD(s0, 0);
-    CRT_GLOAD(s1, 1);
-    CRT_GLOAD(s2, 2);
-    CRT_GLOAD(s3, 3);
+    // chunk c lives in register set g(c mod 4) until it is stored to LDS (at
+    // step c - 1); four chunks in flight keep ~64 KB of loads outstanding per
+    // CU, what an HBM / Infinity Cache latency needs (at 2 chunks a tile took
+    // ~1 us per 64-k step, bound by bytes in flight, not by the MFMAs)
+    uint4 g0a0, g0a1, g0b0, g0b1, g1a0, g1a1, g1b0, g1b1;
+    uint4 g2a0, g2a1, g2b0, g2b1, g3a0, g3a1, g3b0, g3b1;
+    v4i af[4], bf[4];
+    CRT_GLOAD(g0, 0);
+    CRT_GLOAD(g1, 1);
+    CRT_GLOAD(g2, 2);
+    CRT_GLOAD(g3, 3);
+    CRT_LSTORE(g0, 0);
+    CRT_GLOAD(g0, 4);
+    __syncthreads();
+    tp1 = wall_clock64();
+    CRT_FRAG(0);
+    // kcn is a multiple of 4 (kpad % 256 == 0): the steps are branch-free, so
+    // the compiler's load counters see the four chunks in flight (a branch per
+    // step made it drain every load before each LDS store). The last group's
+    // stores and fragment reads of chunks >= kcn (clamped loads) are unused.
 #define CRT_STEP(g, c)                                                                        \
-    if ((c) < kcn) {                                                                          \
-        CRT_LSTORE(g, 0);                                                                     \
+    {                                                                                         \
+        CRT_LSTORE(g, ((c) + 1) & 1);                    /* chunk c + 1 into the other buffer */ \
+        CRT_GLOAD(g, (c) + 5);                           /* (c + 5) mod 4 = (c + 1) mod 4 */  \
+        CRT_MMA();                                                                            \
         __syncthreads();                                                                      \
-        if ((c) + 4 < kcn) CRT_GLOAD(g, (c) + 4);                                             \
-        CRT_MMA(0);                                                                           \
-        __syncthreads();                                                                      \
+        CRT_FRAG(((c) + 1) & 1);                                                              \
     }
     for (uint32_t c0 = 0; c0 < kcn; c0 += 4) {
-        CRT_STEP(s0, c0)
-        CRT_STEP(s1, c0 + 1)
-        CRT_STEP(s2, c0 + 2)
-        CRT_STEP(s3, c0 + 3)
+        CRT_STEP(g1, c0)
+        CRT_STEP(g2, c0 + 1)
+        CRT_STEP(g3, c0 + 2)
+        CRT_STEP(g0, c0 + 3)
     }
+    tp2 = wall_clock64();
 #undef CRT_STEP
 #undef CRT_GLOAD
 #undef CRT_LSTORE
+#undef CRT_FRAG
 #undef CRT_MMA
-    // residues -> 128 x 128 byte tile in LDS -> 128 B rows
+    // residues, stored in MFMA order: R[mod][tile][wave][a][b][lane][reg], so
+    // a lane's four accumulator rows are one 4-byte word and a wave store is
+    // 256 contiguous bytes (no LDS tile, no barrier); the combine reads the
+    // same order (crt_combine_elem)
     const int m = (int)c_crt_mod[mod];
     const float inv = c_crt_invf[mod];
-    uint8_t* T = S;
+    uint32_t* Rt = reinterpret_cast<uint32_t*>(R + ((uint64_t)mod * nblk + tile) * kCrtTileBytes) +
+                   wave * 1024 + lane;
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
+        for (int b = 0; b < 4; ++b) {
+            uint32_t w = 0;
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
                 // |acc| <= 2^27: fp32 quotient off by at most one (m >= 71)
@@ -1510,107 +1535,33 @@ __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, co
                 int r = av - __mul24(q, m);
                 r += r < 0 ? m : 0;
                 r -= r >= m ? m : 0;
-                const uint32_t tr = wr * 64 + a * 16 + (lane >> 4) * 4 + reg;
-                const uint32_t tc = wc * 64 + b * 16 + (lane & 15);
-                T[tr * CTS + tc] = (uint8_t)r;
+                w |= (uint32_t)r << (8 * reg);
             }
-    __syncthreads();
-    const uint32_t rpa = tiles_a * CT, rpb = tiles_m * CT;
-    uint8_t* Rp = R + ((uint64_t)mod * rpa + bi * CT) * (uint64_t)rpb + bj * CT;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t e = tid + q * 256, tr = e >> 3, c16 = (e & 7) * 16;
-        *reinterpret_cast<uint4*>(Rp + (uint64_t)tr * rpb + c16) =
-            *reinterpret_cast<const uint4*>(T + tr * CTS + c16);
-    }
+            Rt[(a * 4 + b) * 64] = w;
+        }
 }
 
 
-// The same tile without LDS (gemm_lds 0): each wave loads its own MFMA
-// fragments straight from the residue planes (rows of 64 B per k-chunk, 16 B
-// per lane; the two waves sharing a row or column strip re-read it through L1),
-// four chunks in flight in registers, no barriers, and the residues stored as
-// bytes from the accumulators. Nothing of the block's LDS or barriers then
-// competes with the stage blocks it runs beside.
-__device__ __forceinline__ void crt_gemm_tile_direct(const uint8_t* __restrict__ Ar,
-                                                     const uint8_t* __restrict__ Br, uint32_t astride,
-                                                     uint32_t bstride, uint32_t kpad, uint32_t tiles_a,
-                                                     uint32_t tiles_m, uint8_t* __restrict__ R, uint32_t bi,
-                                                     uint32_t bj, int mod) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t wr = wave >> 1, wc = wave & 1;
-    const uint32_t frow = lane & 15, fk = (lane >> 4) * 16;
-    const uint64_t kp16 = 16ull * kpad;
-    const uint8_t* Apw = Ar + ((uint64_t)mod * astride + bi * CT + wr * 64 + frow) * kpad + fk;
-    const uint8_t* Bpw = Br + ((uint64_t)mod * bstride + bj * CT + wc * 64 + frow) * kpad + fk;
-    const uint32_t kcn = kpad / 64;
-    v4i acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = v4i{0, 0, 0, 0};
-#define CRD_GLOAD(g, chunk)                                                                   \
-    {                                                                                         \
-        const uint64_t ko = (uint64_t)min((uint32_t)(chunk), kcn - 1) * 64;                  \
-        g##a0 = *reinterpret_cast<const v4i*>(Apw + ko);                                      \
-        g##a1 = *reinterpret_cast<const v4i*>(Apw + kp16 + ko);                               \
-        g##a2 = *reinterpret_cast<const v4i*>(Apw + 2 * kp16 + ko);                           \
-        g##a3 = *reinterpret_cast<const v4i*>(Apw + 3 * kp16 + ko);                           \
-        g##b0 = *reinterpret_cast<const v4i*>(Bpw + ko);                                      \
-        g##b1 = *reinterpret_cast<const v4i*>(Bpw + kp16 + ko);                               \
-        g##b2 = *reinterpret_cast<const v4i*>(Bpw + 2 * kp16 + ko);                           \
-        g##b3 = *reinterpret_cast<const v4i*>(Bpw + 3 * kp16 + ko);                           \
-    }
-#define CRD_MMA1(g, i, j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(g##a##i, g##b##j, acc[i][j], 0, 0, 0);
-#define CRD_MMA(g)                                                                            \
-    {                                                                                         \
-        CRD_MMA1(g, 0, 0) CRD_MMA1(g, 0, 1) CRD_MMA1(g, 0, 2) CRD_MMA1(g, 0, 3)               \
-        CRD_MMA1(g, 1, 0) CRD_MMA1(g, 1, 1) CRD_MMA1(g, 1, 2) CRD_MMA1(g, 1, 3)               \
-        CRD_MMA1(g, 2, 0) CRD_MMA1(g, 2, 1) CRD_MMA1(g, 2, 2) CRD_MMA1(g, 2, 3)               \
-        CRD_MMA1(g, 3, 0) CRD_MMA1(g, 3, 1) CRD_MMA1(g, 3, 2) CRD_MMA1(g, 3, 3)               \
-    }
-#define CRD_STEP(g, c)                                                                        \
-    if ((c) < kcn) {                                                                          \
-        CRD_MMA(g)                                                                            \
-        if ((c) + 4 < kcn) CRD_GLOAD(g, (c) + 4);                                             \
-    }
-    v4i s0a0, s0a1, s0a2, s0a3, s0b0, s0b1, s0b2, s0b3;
-    v4i s1a0, s1a1, s1a2, s1a3, s1b0, s1b1, s1b2, s1b3;
-    v4i s2a0, s2a1, s2a2, s2a3, s2b0, s2b1, s2b2, s2b3;
-    v4i s3a0, s3a1, s3a2, s3a3, s3b0, s3b1, s3b2, s3b3;
-    CRD_GLOAD(s0, 0);
-    CRD_GLOAD(s1, 1);
-    CRD_GLOAD(s2, 2);
-    CRD_GLOAD(s3, 3);
-    for (uint32_t c0 = 0; c0 < kcn; c0 += 4) {
-        CRD_STEP(s0, c0)
-        CRD_STEP(s1, c0 + 1)
-        CRD_STEP(s2, c0 + 2)
-        CRD_STEP(s3, c0 + 3)
-    }
-#undef CRD_STEP
-#undef CRD_MMA
-#undef CRD_MMA1
-#undef CRD_GLOAD
-    const int m = (int)c_crt_mod[mod];
-    const float inv = c_crt_invf[mod];
-    const uint32_t rpa = tiles_a * CT, rpb = tiles_m * CT;
-    uint8_t* Rp = R + ((uint64_t)mod * rpa + bi * CT + wr * 64) * (uint64_t)rpb + bj * CT + wc * 64 + (lane & 15);
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-                // |acc| <= 2^27: fp32 quotient off by at most one (m >= 71)
-                const int av = acc[a][b][reg];
-                const int q = (int)floorf((float)av * inv);
-                int r = av - __mul24(q, m);
-                r += r < 0 ? m : 0;
-                r -= r >= m ? m : 0;
-                Rp[(uint64_t)(a * 16 + (lane >> 4) * 4 + reg) * rpb + b * 16] = (uint8_t)r;
-            }
+// Debug timeline of the GEMM's blocks (svdw_debug_trace): per real block its
+// start and end on the 100 MHz wall clock and (XCC id << 16 | HW_ID).
+__device__ unsigned long long* g_trace = nullptr;
+hipError_t set_debug_trace(void* buf) {
+    unsigned long long* p = (unsigned long long*)buf;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &p, sizeof p);
 }
+__device__ __forceinline__ void trace_block(uint64_t t0, uint64_t t1, uint64_t t2) {
+    unsigned long long* tr = g_trace;
+    if (!tr || threadIdx.x) return;
+    uint32_t xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    tr[5 * blockIdx.x] = t0;
+    tr[5 * blockIdx.x + 1] = t1;
+    tr[5 * blockIdx.x + 2] = t2;
+    tr[5 * blockIdx.x + 3] = wall_clock64();
+    tr[5 * blockIdx.x + 4] = ((unsigned long long)xcc << 32) | hw;
+}
+
 
 // The products of a CrtBatch in one launch, placed modulus-major per XCD: the
 // work units (job, modulus < the job's device-decided count n, tile) are laid
@@ -1621,6 +1572,7 @@ __device__ __forceinline__ void crt_gemm_tile_direct(const uint8_t* __restrict__
 // (the grid is sized for n = kCrtMaxMod).
 __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
     __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes()];
+    const uint64_t t0 = wall_clock64();
     uint32_t cnt[kMaxCrtJobs], total = 0;
 #pragma unroll
     for (int j = 0; j < kMaxCrtJobs; ++j) {
@@ -1648,59 +1600,45 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
         bi = t / q.tiles_m;
         bj = t - bi * q.tiles_m;
     }
-    crt_gemm_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.tiles_a,
-                  q.sym ? q.tiles_a : q.tiles_m, q.R, bi, bj, (int)mod, S);
+    uint64_t tp1 = 0, tp2 = 0;
+    crt_gemm_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.nblk, t,
+                  q.R, bi, bj, (int)mod, S, tp1, tp2);
+    trace_block(t0, tp1, tp2);
 }
-__global__ __launch_bounds__(256) void k_gemm_crt_multi_d(const CrtBatch b) {
-    uint32_t cnt[kMaxCrtJobs], total = 0;
-#pragma unroll
-    for (int j = 0; j < kMaxCrtJobs; ++j) {
-        cnt[j] = 0;
-        if ((uint32_t)j < b.njobs)
-            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk;
-        total += cnt[j];
-    }
-    const uint32_t per = (total + 7) / 8, k = blockIdx.x >> 3;
-    if (k >= per) return;
-    uint32_t u = (blockIdx.x & 7) * per + k;
-    if (u >= total) return;
-    uint32_t j = 0;
-#pragma unroll
-    for (int q = 0; q < kMaxCrtJobs - 1; ++q)
-        if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
-    const CrtJob& q = b.job[j];
-    const uint32_t mod = u / q.nblk, t = u - mod * q.nblk;
-    uint32_t bi, bj;
+// C from its n residues, written as canonical Fr to out[i*ors + j*ocs]: one
+// element per thread in the GEMM's tile order (each block one 256-element
+// stretch of a tile), so a wave reads 64 consecutive residue bytes per modulus
+// (the n loads issued before the first use: one memory latency, not n) and
+// writes four rows of 16 consecutive cells. C mod p = sum_k r_k E_k +
+// q (-Mtot mod p), q = floor(sum_k r_k inv_k / m_k + 1/2) in f64 (|C| < Mtot / 4
+// keeps it exact), accumulated carry-free in 16-bit limbs, one 9-word
+// reduction. SYM: elements j >= i of the upper tiles (the GEMM computed upper
+// and diagonal 128-tiles), each also stored at (j, i).
+// tile t of a job -> its (row, column) tile (SYM: upper tiles row by row)
+__device__ __forceinline__ void crt_tile_rc(const CrtJob& q, uint32_t t, uint32_t* bi, uint32_t* bj) {
     if (q.sym) {
         uint32_t r = 0, rest = t, rowlen = q.tiles_a;
         while (rest >= rowlen) { rest -= rowlen; ++r; --rowlen; }
-        bi = r; bj = r + rest;
+        *bi = r; *bj = r + rest;
     } else {
-        bi = t / q.tiles_m;
-        bj = t - bi * q.tiles_m;
+        *bi = t / q.tiles_m;
+        *bj = t - *bi * q.tiles_m;
     }
-    crt_gemm_tile_direct(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad,
-                         q.tiles_a, q.sym ? q.tiles_a : q.tiles_m, q.R, bi, bj, (int)mod);
 }
-
-// C from its n residues, written as canonical Fr to out[i*ors + j*ocs]: one
-// element per thread, a block = kCombRows rows x 64 columns, so a wave reads 64
-// consecutive residue bytes per modulus (the n loads issued before the first
-// use: one memory latency, not n). C mod p = sum_k r_k E_k + q (-Mtot mod p),
-// q = floor(sum_k r_k inv_k / m_k + 1/2) in f64 (|C| < Mtot / 4 keeps it exact),
-// accumulated carry-free in 16-bit limbs, one 9-word reduction. SYM: elements
-// j >= i of the upper tiles (the GEMM computed upper and diagonal 128-tiles),
-// each also stored at (j, i).
-static constexpr uint32_t kCombRows = 4;
-__device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t tile) {
+__device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t cblk) {
     const int n = crt_nmod(*q.bits_a, *q.bits_b, q.lk);
     if (!n) return;
-    const uint32_t cts = (q.M + 63) / 64, rg = tile / cts, jt = tile - rg * cts;
-    const uint32_t i = rg * kCombRows + (threadIdx.x >> 6), j = jt * 64 + (threadIdx.x & 63);
+    // element e of tile t in the GEMM's MFMA order (wave, a, b, lane, reg)
+    const uint32_t tl = cblk / kCombBlocksPerTile;
+    const uint32_t e = (cblk - tl * kCombBlocksPerTile) * 256 + threadIdx.x;
+    const uint32_t reg = e & 3, ln = (e >> 2) & 63, ab = (e >> 8) & 15, w = e >> 12;
+    uint32_t bi, bj;
+    crt_tile_rc(q, tl, &bi, &bj);
+    const uint32_t i = bi * CT + (w >> 1) * 64 + (ab >> 2) * 16 + (ln >> 4) * 4 + reg;
+    const uint32_t j = bj * CT + (w & 1) * 64 + (ab & 3) * 16 + (ln & 15);
     if (i >= q.N || j >= q.M || (q.sym && j < i)) return;
-    const uint32_t rpb = (q.sym ? q.tiles_a : q.tiles_m) * CT;
-    const uint64_t plane = (uint64_t)q.tiles_a * CT * rpb;
-    const uint8_t* __restrict__ rp = q.R + (uint64_t)i * rpb + j;
+    const uint64_t plane = (uint64_t)q.nblk * kCrtTileBytes;
+    const uint8_t* __restrict__ rp = q.R + (uint64_t)tl * kCrtTileBytes + e;
     uint32_t r[kCrtMaxMod];
 #pragma unroll
     for (int k = 0; k < kCrtMaxMod; ++k) r[k] = k < n ? rp[k * plane] : 0u;
@@ -1760,18 +1698,15 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
         q.tiles_a = (q.N + CT - 1) / CT;
         q.tiles_m = q.sym ? q.tiles_a : (q.M + CT - 1) / CT;
         // every staged row (tiles x CT) lies inside its operand's planes
-        if (q.kpad % 64 || q.astride < q.tiles_a * CT || (!q.sym && q.bstride < q.tiles_m * CT))
+        if (q.kpad % 256 || q.astride < q.tiles_a * CT || (!q.sym && q.bstride < q.tiles_m * CT))
             return hipErrorInvalidValue;
         if (q.sym && q.N != q.M) return hipErrorInvalidValue;
         q.nblk = q.sym ? q.tiles_a * (q.tiles_a + 1) / 2 : q.tiles_a * q.tiles_m;
         units += kCrtMaxMod * q.nblk;                    // upper bound: n = kCrtMaxMod
-        q.cblk0 = cblocks;                               // (SYM: lower tiles exit at once)
-        cblocks += (q.N + kCombRows - 1) / kCombRows * ((q.M + 63) / 64);
+        q.cblk0 = cblocks;
+        cblocks += q.nblk * kCombBlocksPerTile;
     }
-    if (b.lds)
-        hipLaunchKernelGGL(k_gemm_crt_multi, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
-    else
-        hipLaunchKernelGGL(k_gemm_crt_multi_d, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
+    hipLaunchKernelGGL(k_gemm_crt_multi, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_crt_combine_multi, dim3((cblocks + 7) / 8 * 8), dim3(256), 0, st, b, cblocks);
@@ -1781,12 +1716,11 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st, int lds) {
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st) {
     if (sym && (N != M || astride != bstride)) return hipErrorInvalidValue;
     CrtBatch b;
     memset(&b, 0, sizeof b);
     b.njobs = 1;
-    b.lds = lds;
     CrtJob& q = b.job[0];
     q.Ar = Ar;
     q.Br = sym ? Ar : Br;

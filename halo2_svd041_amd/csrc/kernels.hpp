@@ -274,7 +274,9 @@ hipError_t launch_residues_f64(const ResSegs& q, const unsigned* W, int precisio
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st, int lds = 0);
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st);
+// Debug: record the CRT GEMM's block timeline into buf (3 u64 per block; null: off).
+hipError_t set_debug_trace(void* buf);
 static constexpr int kCrtMaxResidues = 40;   // = kCrtMaxMod (crt_tables.hpp)
 // Several CRT products in one GEMM launch and one combine launch (the three
 // products of check_svd_phase0; launch_gemm_crt is the one-job case). The GEMM's
@@ -297,7 +299,6 @@ struct CrtJob {
 struct CrtBatch {
     CrtJob job[kMaxCrtJobs];
     uint32_t njobs;
-    int lds;             // GEMM tiles staged through LDS (1) or fragments loaded per wave (0)
 };
 hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st);
 // w (len L) from a view (row 0 / col j of a 1 x L view) -> canonical copy

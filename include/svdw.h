@@ -95,6 +95,9 @@ int svdw_sync(svdw_ctx* ctx);
  * The Python layer (halo2_svd041_amd.zk) does both around every on-device call
  * with torch's current stream. */
 int svdw_stream_wait(svdw_ctx* ctx, void* stream);
+/* Debug: the CRT GEMM's block timeline into device buffer buf (3 u64 per block:
+ * start and end on the 100 MHz wall clock, XCC id << 32 | HW_ID); null: off. */
+int svdw_debug_trace(void* buf);
 int svdw_stream_signal(svdw_ctx* ctx, void* stream);
 const char* svdw_last_error(void);
 
