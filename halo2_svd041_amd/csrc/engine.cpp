@@ -450,7 +450,7 @@ struct svdw_ctx {
     int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
     bool gemm_batched = false;              // this witness's products went out as one batch
-    int res_first = 0;                      // "res_first": cell stream waits for the residue planes
+    int res_first = -1;                     // "res_first": cell stream waits for the residue planes
                                             // (1), not (0), -1: on row-sharded ranks
     int gemm_batch = 1;                     // "gemm_batch": svd_witness's three products in one launch
                                             // (1), one by one (0), or -1: batched on row-sharded ranks
@@ -498,8 +498,10 @@ struct svdw_ctx {
     // (k_colsum_f64), not from cells. Cleared at the end of the witness.
     struct F64Src { svdw_mat m; const double* x; };
     std::vector<F64Src> f64src;
-    DBuf colpart;                           // k_colsum_f64's per-slice partial sums
-    bool colsum = true;                     // "colsum": that path (else k_matvec_values on the cells)
+    DBuf colpart;
+    DBuf qfold;                             // k_quantize_multi's fold counters + group maxima                           // k_colsum_f64's per-slice partial sums
+    bool colsum = true;
+    bool bits_fold = true;                  // "bits_fold": bit-length words folded in the quantize launch                     // "colsum": that path (else k_matvec_values on the cells)
     bool prod_first = false;                // "prod_first": the first stages wait for the products
     // second stream: GEMMs overlap the HBM-bound stages; third: phase 1
     hipStream_t st2 = nullptr;
@@ -718,6 +720,29 @@ static void ensure_buf(svdw_ctx* c, DBuf& b, size_t bytes) {
         fail(SVDW_ENOMEM, "device allocation failed (scratch)");
     }
     b.cap = cap;
+}
+// The bit-length words out[0 .. nred) folded inside the quantize launch
+// (BitFold) when its first nred segments carry block maxima laid out back to
+// back from qs.blockmax[0]; else k_bits_reduce over `seg`, a launch of its own.
+static void bits_words(svdw_ctx* c, QuantSegs& qs, uint32_t nred, const BitSegs& seg, unsigned* out,
+                       bool* folded) {
+    *folded = false;
+    if (c->dry || !qs.nseg || qs.nseg < nred || nred > 3 || !c->bits_fold) return;
+    for (uint32_t s = 0; s < nred; ++s)
+        if (qs.blockmax[s] != qs.blockmax[0] + qs.blk0[s] || qs.blk0[s] != seg.begin[s]) return;
+    const uint32_t nblk = qs.blk0[nred];
+    if (!c->qfold.p) {
+        ensure_buf(c, c->qfold, 256);
+        hipck(hipMemset(c->qfold.p, 0, c->qfold.cap), "hipMemset");   // the counter starts at zero
+    }
+    BitFold& f = qs.fold;
+    f.bm = qs.blockmax[0];
+    f.cnt = (unsigned*)c->qfold.p;
+    f.wout = out;
+    f.nblk = nblk;
+    f.nred = nred;
+    for (uint32_t s = 0; s <= nred; ++s) f.b[s] = qs.blk0[s];
+    *folded = true;
 }
 static void grow(svdw_ctx* c, Fr*& ptr, uint64_t used, uint64_t& cap, uint64_t need) {
     if (c->dry || need <= cap) return;
@@ -1113,7 +1138,7 @@ static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, ui
                 shard_rows(c, rows, &r0, &r1);
                 qs->keep[k] = QuantKeep{cols, (uint32_t)r0, (uint32_t)r1, (uint32_t)r0, (uint32_t)r1};
             }
-            qs->blk0[k + 1] = qs->blk0[k] + (uint32_t)((n + 255) / 256);
+            qs->blk0[k + 1] = qs->blk0[k] + (uint32_t)((n + kQuantPerBlock - 1) / kQuantPerBlock);
         } else {
             ProfScope ps(c, c->st, "k_quantize", 40.0 * n, 0);
             hipck(launch_quantize(src, n, cellp(c, phase, off), (int)c->P, blockmax, c->st),
@@ -1716,7 +1741,7 @@ static void ensure_gamma_vec(svdw_ctx* c, uint32_t d, const Fr& gamma) {
     c->gp_ev = nullptr;
 }
 static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, const Fr& gamma) {
-    REQUIRE(n >= 1 && n <= kMaxScanJobs, "internal: verify_mul batch size");
+    REQUIRE(n >= 1 && n <= kMaxVerifyBatch, "internal: verify_mul batch size");
     c->ext_gamma = gamma;
     struct Plan {
         PB one, pows, eq;
@@ -1810,46 +1835,38 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         }
         bs.end();
     }
-    // operand widths per batch: host-known, or read on the device (na 0)
-    auto batch_na = [&](auto mat_of) {
-        svdw_mat ms[kMaxScanJobs];
-        for (int i = 0; i < n; ++i) ms[i] = mat_of(i);
-        return batch_na_host(c, ms, n);
-    };
-    auto run_batch = [&](const char* name, auto mat_of, auto vec_of, auto wc_of, auto tab_of,
-                         auto tl_of, int na) {
+    // One scan launch over jobs (a_q against the vector wc_q / tab_q, cells at
+    // v_q); operand widths host-known or read on the device (na 0).
+    struct Scans {
         ScanBatch sb;
-        memset(&sb, 0, sizeof sb);
+        svdw_mat ms[kMaxScanJobs];
         double bytes = 0, ops = 0;
-        for (int i = 0; i < n; ++i) {
-            const svdw_mat a = mat_of(i);
-            const svdw_vec v = vec_of(i);
-            uint64_t r0 = 0, r1 = a.rows;                 // shard: this rank's rows
-            const uint64_t rowc = 3ull * a.cols + 1, base = v.off - 3ull * a.cols;
-            if (sharded(c)) shard_rows(c, a.rows, &r0, &r1);
-            sb.job[i] = ScanJob{view_of(c, a), wc_of(i), tab_of(i), tl_of(i), cellp(c, phase, base + r0 * rowc),
-                                a.cols, (uint32_t)(r1 - r0), 0, (uint32_t)r0, job_spec(c, a)};
-            bytes += 32.0 * (r1 - r0) * (4.0 * a.cols + 1) + 64.0 * a.cols;
-            ops += (double)(r1 - r0) * a.cols;
-        }
-        sb.njobs = n;
-        sb.bitw = c->dbitw;
-        ProfScope ps(c, c->st, name, bytes, ops);
-        hipck(launch_scan_batch(sb, na, c->st), "k_matvec_scan");
+        Scans() { memset(&sb, 0, sizeof sb); }
     };
-    auto cs_of = [&](int i) { return vm[i].cs; };
-    auto b_of = [&](int i) { return vm[i].b; };
-    auto a_of = [&](int i) { return vm[i].a; };
-    const int na_cs = batch_na(cs_of), na_b = batch_na(b_of), na_a = batch_na(a_of);
-    auto gc = [&](int) { return gpc; };
-    auto gt = [&](int) { return gtab; };
-    // launch order != append order: the b and a.(b.g) scans need only the
-    // operands, the c_s scans wait for the products when those run elsewhere
-    auto gl = [&](int) { return c->gp_len; };            // the gamma table's length (>= every d)
-    run_batch("k_matvec_scan:b", b_of, [&](int i) { return pl[i].bv; }, gc, gt, gl, na_b);
+    auto add_job = [&](Scans& S, const svdw_mat& a, const svdw_vec& v, const Fr* wc, const Fr* tab,
+                       uint32_t tl) -> ScanJob& {
+        REQUIRE(S.sb.njobs < (uint32_t)kMaxScanJobs, "internal: scan batch full");
+        uint64_t r0 = 0, r1 = a.rows;                     // shard: this rank's rows
+        const uint64_t rowc = 3ull * a.cols + 1, base = v.off - 3ull * a.cols;
+        if (sharded(c)) shard_rows(c, a.rows, &r0, &r1);
+        S.ms[S.sb.njobs] = a;
+        ScanJob& j = S.sb.job[S.sb.njobs++];
+        j = ScanJob{view_of(c, a), wc, tab, tl, cellp(c, phase, base + r0 * rowc),
+                    a.cols, (uint32_t)(r1 - r0), 0, (uint32_t)r0, job_spec(c, a)};
+        S.bytes += 32.0 * (r1 - r0) * (4.0 * a.cols + 1) + 64.0 * a.cols;
+        S.ops += (double)(r1 - r0) * a.cols;
+        return j;
+    };
+    auto launch = [&](Scans& S, const char* name) {
+        S.sb.bitw = c->dbitw;
+        S.sb.f = scale_tab();
+        const int na = batch_na_host(c, S.ms, (int)S.sb.njobs);
+        ProfScope ps(c, c->st, name, S.bytes, S.ops);
+        hipck(launch_scan_batch(S.sb, na, c->st), "k_matvec_scan");
+    };
     // b.g of job i: the b scan of the first job with the same b (m.v^T and
     // v.v^T share v^T) serves every later job with it
-    int src[kMaxScanJobs];
+    int src[kMaxVerifyBatch];
     for (int i = 0; i < n; ++i) {
         src[i] = i;
         for (int k = 0; k < i; ++k)
@@ -1857,7 +1874,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
                 vm[k].b.rows == vm[i].b.rows && vm[k].b.cols == vm[i].b.cols &&
                 vm[k].b.rs == vm[i].b.rs && vm[k].b.cs == vm[i].b.cs) { src[i] = k; break; }
     }
-    const Fr* wt[kMaxScanJobs];
+    const Fr* wt[kMaxVerifyBatch];
     // b = X^T of an f64 input of svd_witness: X, else null
     auto f64_of = [&](const svdw_mat& b) -> const svdw_ctx::F64Src* {
         if (!c->colsum || b.cols > 8192) return nullptr;
@@ -1865,19 +1882,27 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
             if (is_transpose_of(b, s.m) && s.m.rs == (int64_t)s.m.cols && s.m.cs == 1) return &s;
         return nullptr;
     };
-    bool all_f64 = sharded(c);
+    bool all_f64 = true;
     for (int i = 0; i < n && all_f64; ++i) all_f64 = f64_of(vm[i].b) != nullptr;
+    // launch order != append order: the b and a.(b.g) scans need only the
+    // operands, the c_s scans wait for the products when those run elsewhere
+    Scans bs_, as_;
+    auto add_b = [&](Scans& S, int i) -> ScanJob& { return add_job(S, vm[i].b, pl[i].bv, gpc, gtab, c->gp_len); };
+    auto add_a = [&](Scans& S, int i) {
+        add_job(S, vm[i].a, pl[i].abv, (const Fr*)c->wbc[src[i]].p, wt[i], vm[i].b.rows);
+    };
     if (all_f64) {
         // every entry of b.g from the f64 rows of X (quantized in registers),
         // column-parallel and coalesced: one launch for the distinct b's, then
-        // the slices' sums folded into each vector's table (k_vec_prep_sum)
+        // the slices' sums folded into each vector's table (k_vec_prep_sum);
+        // the b and a.(b.g) scans are then independent: one launch
         ColBatch cb;
         memset(&cb, 0, sizeof cb);
         cb.tab = gtab;
         cb.tl = c->gp_len;
         cb.bitw = c->dbitw;
-        int slot[kMaxScanJobs];
-        size_t poff[kMaxScanJobs], ptot = 0;
+        int slot[kMaxVerifyBatch];
+        size_t poff[kMaxVerifyBatch], ptot = 0;
         for (int i = 0; i < n; ++i) {
             if (src[i] != i) { slot[i] = slot[src[i]]; continue; }
             REQUIRE(cb.njobs < (uint32_t)kMaxColJobs, "internal: too many distinct b for k_colsum_f64");
@@ -1909,49 +1934,73 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
                   "k_vec_prep_sum");
             wt[i] = (const Fr*)c->wbt[i].p;
         }
+        for (int i = 0; i < n; ++i) add_b(bs_, i);
+        for (int i = 0; i < n; ++i) add_a(bs_, i);
+        launch(bs_, "k_matvec_scan:ba");
     } else if (sharded(c)) {
+        for (int i = 0; i < n; ++i) add_b(bs_, i);
+        launch(bs_, "k_matvec_scan:b");
         // only this rank's rows of the b.g scans exist: every entry of b.g comes
         // from the values-only mat-vec instead (the distinct b's in one launch)
         ScanBatch vb;
         memset(&vb, 0, sizeof vb);
-        int nv = 0, slot[kMaxScanJobs];
+        svdw_mat vms[kMaxVerifyBatch];
+        int nv = 0, slot[kMaxVerifyBatch];
         for (int i = 0; i < n; ++i) {
             if (src[i] != i) { slot[i] = slot[src[i]]; continue; }
             const svdw_mat b = vm[i].b;
             ensure_buf(c, c->bvfull[nv], (size_t)b.rows * sizeof(Fr));
             vb.job[nv] = ScanJob{view_of(c, b), nullptr, gtab, c->gp_len, (Fr*)c->bvfull[nv].p, b.cols, b.rows,
                                  0, 0, job_spec(c, b)};
+            vms[nv] = b;
             slot[i] = nv++;
         }
         vb.njobs = nv;
         vb.bitw = c->dbitw;
         {
             ProfScope ps(c, c->st, "k_matvec_values", 0, 0);
-            hipck(launch_matvec_values(vb, na_b, c->st), "k_matvec_values");
+            hipck(launch_matvec_values(vb, batch_na_host(c, vms, nv), c->st), "k_matvec_values");
         }
         for (int i = 0; i < n; ++i)
             wt[i] = src[i] != i ? wt[src[i]]
                                 : vec_prep_ptr(c, (const Fr*)c->bvfull[slot[i]].p, vm[i].b.rows,
                                                c->wbc[i], c->wbt[i]);
+        for (int i = 0; i < n; ++i) add_a(as_, i);
+        launch(as_, "k_matvec_scan:a");
     } else {
-        for (int i = 0; i < n; ++i)
-            wt[i] = src[i] != i ? wt[src[i]] : vec_prep(c, pl[i].bv, c->wbc[i], c->wbt[i]);
+        // every row of b scanned: the b scan of each distinct b also writes b.g
+        // as the a scan's vector (canonical + table) from its row totals
+        for (int i = 0; i < n; ++i) {
+            ScanJob& j = add_b(bs_, i);
+            if (src[i] != i) continue;
+            const uint32_t L = vm[i].b.rows;
+            ensure_buf(c, c->wbc[i], (size_t)L * sizeof(Fr));
+            ensure_buf(c, c->wbt[i], tab_len(L) * sizeof(Fr));
+            j.pc = (Fr*)c->wbc[i].p;
+            j.ptab = (Fr*)c->wbt[i].p;
+            j.plen = L;
+        }
+        for (int i = 0; i < n; ++i) wt[i] = (const Fr*)c->wbt[src[i]].p;
+        launch(bs_, "k_matvec_scan:b");
+        for (int i = 0; i < n; ++i) add_a(as_, i);
+        launch(as_, "k_matvec_scan:a");
     }
-    run_batch("k_matvec_scan:a", a_of, [&](int i) { return pl[i].abv; },
-              [&](int i) { return (const Fr*)c->wbc[src[i]].p; }, [&](int i) { return wt[i]; },
-              [&](int i) { return vm[i].b.rows; }, na_a);
     for (hipEvent_t ev : c->wait_before_cs)
         hipck(hipStreamWaitEvent(c->st, ev, 0), "hipStreamWaitEvent");
-    run_batch("k_matvec_scan:cs", cs_of, [&](int i) { return pl[i].csv; }, gc, gt, gl, na_cs);
-    BatchScope bs(c);                                     // the is_equal rows: one launch
+    // the c_s scans; each row's is_equal(c_s.g, a.(b.g)) cells from its row
+    // total and the a scan's last cell (k_matvec_scan_dpp's eq epilogue)
+    Scans cs_;
     for (int i = 0; i < n; ++i) {
         Plan& p = pl[i];
+        ScanJob& j = add_job(cs_, vm[i].cs, p.csv, gpc, gtab, c->gp_len);
+        j.eq_out = cellp(c, phase, p.eq_off);
+        j.eq_y = cellp(c, p.abv.phase, p.abv.off);
+        j.eq_ys = (uint32_t)p.abv.stride;
         p.eq.a.view[0] = view_of(c, mat_of_vec(p.csv));
         p.eq.a.view[1] = view_of(c, mat_of_vec(p.abv));
         note_gates(c, p.eq, 1, p.eq_reg);
-        stage_launch(c, phase, p.eq, vm[i].a.rows, 1, p.eq_off, p.eq_loff, "verify_mul_is_equal");
     }
-    bs.end();
+    launch(cs_, "k_matvec_scan:cs");
 }
 static void verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svdw_mat& b,
                        const svdw_mat& cs, const Fr& gamma) {
@@ -2396,9 +2445,9 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     // m: only this rank's rows are quantized on a row-sharded rank (zkmatrix_new)
     uint64_t mr0 = 0, mr1 = N;
     if (sharded(c) && on_device && c->fused_quantize) shard_rows(c, N, &mr0, &mr1);
-    const uint32_t nbm = (uint32_t)(((mr1 - mr0) * M + 255) / 256);
-    const uint32_t nbu = (uint32_t)(((uint64_t)N * N + 255) / 256);
-    const uint32_t nbv = (uint32_t)(((uint64_t)M * M + 255) / 256);
+    const uint32_t nbm = (uint32_t)(((mr1 - mr0) * M + kQuantPerBlock - 1) / kQuantPerBlock);
+    const uint32_t nbu = (uint32_t)(((uint64_t)N * N + kQuantPerBlock - 1) / kQuantPerBlock);
+    const uint32_t nbv = (uint32_t)(((uint64_t)M * M + kQuantPerBlock - 1) / kQuantPerBlock);
     if (!c->dry) {
         // [0, 3): bit-length maxima of m, u, v; from word 64: per-block maxima
         ensure_buf(c, c->bits, (64 + nbm + nbu + nbv) * sizeof(unsigned));
@@ -2408,12 +2457,23 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     memset(&qs, 0, sizeof qs);
     QuantSegs* qp = c->fused_quantize ? &qs : nullptr;
     svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device, dbits ? dbits + 64 : nullptr, qp, true);
-    // (u, v: the rank's rows and column block only, when b.g comes from the f64 inputs)
-    const bool part = sharded(c) && on_device && c->colsum && N <= 8192 && M <= 8192;   // (f64_of's bound)
+    // (u, v: the rank's rows and column block only, when b.g comes from the f64
+    // inputs and so do the products' residue planes: no kernel reads the rest;
+    // the conditions of f64_of and of check_svd_phase0's from_f64 prelaunch)
+    const bool part = sharded(c) && on_device && c->colsum && N <= 8192 && M <= 8192 && c->overlap &&
+                      c->res_f64 && c->gemm_crt && c->gemm_rt && c->gemm_impl == SVDW_GEMM_MFMA &&
+                      c->fused_quantize;
     svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device, dbits ? dbits + 64 + nbm : nullptr, qp, false, part);
     svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device, dbits ? dbits + 64 + nbm + nbu : nullptr, qp, false,
                                part);
     svdw_mat zdm = zkmatrix_new(c, 0, d, r, 1, on_device, nullptr, qp);
+    BitSegs seg{};
+    seg.begin[0] = 0;
+    seg.begin[1] = nbm;
+    seg.begin[2] = nbm + nbu;
+    seg.begin[3] = nbm + nbu + nbv;
+    bool folded = false;
+    bits_words(c, qs, 3, seg, dbits, &folded);
     if (qs.nseg) {
         ProfScope ps(c, c->st, "k_quantize", 40.0 * ((double)N * M + (double)N * N + (double)M * M + r), 0);
         hipck(launch_quantize_multi(qs, (int)c->P, c->st), "k_quantize_multi");
@@ -2422,12 +2482,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     double es, eu;
     err_calc(c->P, std::max(N, M), cfg.max_norm, cfg.eps_svd, cfg.eps_u, &es, &eu);
     if (!c->dry) {   // operand bit lengths (GEMM digit counts): read lazily, see fetch_bits
-        BitSegs seg{};
-        seg.begin[0] = 0;
-        seg.begin[1] = nbm;
-        seg.begin[2] = nbm + nbu;
-        seg.begin[3] = nbm + nbu + nbv;
-        hipck(launch_bits_reduce(dbits + 64, seg, 3, dbits, c->st), "k_bits_reduce");
+        if (!folded) hipck(launch_bits_reduce(dbits + 64, seg, 3, dbits, c->st), "k_bits_reduce");
         flush_batch(c, c->st);
         hipck(hipEventRecord(c->ev_bits, c->st), "hipEventRecord");
         c->bits_pending = true;
@@ -2543,7 +2598,8 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     c->ext_off = 0;
     c->gp_ev = nullptr;
     unsigned* dbits = nullptr;
-    const uint32_t nba = (uint32_t)(((uint64_t)N * K + 255) / 256), nbb = (uint32_t)(((uint64_t)K * M + 255) / 256);
+    const uint32_t nba = (uint32_t)(((uint64_t)N * K + kQuantPerBlock - 1) / kQuantPerBlock),
+                   nbb = (uint32_t)(((uint64_t)K * M + kQuantPerBlock - 1) / kQuantPerBlock);
     if (!c->dry) {
         if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
         gamma_prep(c, M, gamma, c->st3);
@@ -2556,16 +2612,18 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     QuantSegs* qp = c->fused_quantize && on_device ? &qs : nullptr;
     const svdw_mat za = zkmatrix_new(c, 0, a, N, K, on_device, dbits ? dbits + 64 : nullptr, qp);
     const svdw_mat zb = zkmatrix_new(c, 0, b, K, M, on_device, dbits ? dbits + 64 + nba : nullptr, qp);
+    BitSegs seg{};
+    seg.begin[0] = 0;
+    seg.begin[1] = nba;
+    seg.begin[2] = nba + nbb;
+    bool folded = false;
+    bits_words(c, qs, 2, seg, dbits, &folded);
     if (qs.nseg) {
         ProfScope ps(c, c->st, "k_quantize", 40.0 * ((double)N * K + (double)K * M), 0);
         hipck(launch_quantize_multi(qs, (int)c->P, c->st), "k_quantize_multi");
     }
     if (!c->dry) {
-        BitSegs seg{};
-        seg.begin[0] = 0;
-        seg.begin[1] = nba;
-        seg.begin[2] = nba + nbb;
-        hipck(launch_bits_reduce(dbits + 64, seg, 2, dbits, c->st), "k_bits_reduce");
+        if (!folded) hipck(launch_bits_reduce(dbits + 64, seg, 2, dbits, c->st), "k_bits_reduce");
         c->dbitw = dbits;
         c->dwords = {{za, 0}, {zb, 1}};
     }
@@ -2782,7 +2840,7 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             if (c->st3) (void)hipStreamSynchronize(c->st3);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
             for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1], &c->w1c, &c->w1t, &c->w2c, &c->w2t,
-                            &c->bits, &c->gpc, &c->gtab, &c->crtR, &c->gbits})
+                            &c->bits, &c->gpc, &c->gtab, &c->crtR, &c->gbits, &c->colpart, &c->qfold})
                 if (b->p) (void)hipFree(b->p);
             for (int i = 0; i < kMaxScanJobs; ++i) {
                 if (c->wbc[i].p) (void)hipFree(c->wbc[i].p);
@@ -3762,6 +3820,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_crt = (int)value;
         } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
             c->stage_batch = value != 0;
+        } else if (n == "bits_fold") {
+            c->bits_fold = value != 0;
         } else if (n == "res_first") {
             REQUIRE(value >= -1 && value <= 1, "res_first: -1 (auto), 0 or 1");
             c->res_first = (int)value;

@@ -64,49 +64,118 @@ __device__ __forceinline__ uint32_t signed_bits(const Fr& x) {
 // x_q = round_half_away(|x| * 2^P) as u128 (saturating, NaN -> 0);
 // sign(x) < 0 (incl. -0.0) -> p - x_q.   [zk_fixed_point_chip quantization,
 // SURVEY.md Appendix C.1]
+// Fold of the block maxima inside the quantize launch (BitFold), fence-free:
+// each block publishes its maximum with an agent-scope atomic exchange and
+// arrives on its group's counter (group = blk & 7) only once the exchange has
+// returned (the register use below makes the arrival wait for it); the last
+// arrival of a group arrives on the global counter, the last of those sees
+// every maximum with agent-scope loads. An agent-scope release fence instead
+// writes back the whole L2 (the block's cells) per block: 670 us instead of 19.
+// Called after the block's stores are issued, so its latency overlaps them.
+__device__ __forceinline__ void bits_fold(const BitFold& f, uint32_t blk, uint32_t bmax) {
+    __shared__ uint32_t last, red[4][4];
+    if (threadIdx.x == 0) {
+        const uint32_t g = blk & 7, gsize = (f.nblk - g + 7) / 8;
+        const uint32_t old = __hip_atomic_exchange(f.bm + blk, bmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(old) : "memory");
+        bool lst = __hip_atomic_fetch_add(f.cnt + 1 + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1;
+        if (lst) {
+            __hip_atomic_store(f.cnt + 1 + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t ng = min(f.nblk, 8u);
+            lst = __hip_atomic_fetch_add(f.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+        }
+        last = lst;
+    }
+    __syncthreads();
+    if (!last) return;
+    uint32_t x[3] = {0u, 0u, 0u};
+    for (uint32_t k0 = threadIdx.x; k0 < f.nblk; k0 += 8 * blockDim.x) {
+        uint32_t v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t k = k0 + q * blockDim.x;
+            v[q] = k < f.nblk ? __hip_atomic_load(f.bm + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint32_t k = k0 + q * blockDim.x;
+#pragma unroll
+            for (int s = 0; s < 3; ++s)
+                if (k >= f.b[s] && k < f.b[s + 1]) x[s] = max(x[s], v[q]);
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x[s] = max(x[s], (uint32_t)__shfl_xor((int)x[s], off));
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][s] = x[s];
+    }
+    __syncthreads();
+    if (threadIdx.x < f.nred) {
+        const uint32_t s = threadIdx.x;
+        f.wout[s] = max(max(red[0][s], red[1][s]), max(red[2][s], red[3][s]));
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(f.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// kQuantPerBlock values per block, 16 per thread (value blk * 4096 + k * 256 +
+// tid: each store instruction coalesced), all loads issued first.
 __device__ __forceinline__ void quantize_body(const double* __restrict__ in, uint64_t n,
                                               Fr* __restrict__ out, double scale,
                                               unsigned* __restrict__ blockmax, uint32_t blk,
-                                              QuantKeep keep = QuantKeep{0, 0, 0, 0, 0}) {
-    uint64_t i = (uint64_t)blk * blockDim.x + threadIdx.x;
-    // bit length of |x_q| for the GEMM digit-count choice (wave max, one atomic)
-    uint32_t bits = 0;
-    if (i < n) {
-        double s = round(fabs(in[i]) * scale);
-        if (s >= 340282366920938463463374607431768211456.0) bits = 128;
-        else if (s >= 1.0) bits = (uint32_t)ilogb(s) + 1;
+                                              QuantKeep keep = QuantKeep{0, 0, 0, 0, 0},
+                                              const BitFold fold = BitFold{}, uint32_t gblk = 0) {
+    constexpr int PT = kQuantPerBlock / 256;
+    const uint64_t i0 = (uint64_t)blk * kQuantPerBlock + threadIdx.x;
+    uint32_t bmax = 0;
+    double xv[PT];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+        const uint64_t i = i0 + 256ull * k;
+        xv[k] = i < n ? in[i] : 0.0;
     }
     if (blockmax) {
-        // wave max -> block max (LDS) -> one plain store per block; the maxima
-        // are folded by k_bits_reduce (no contended atomics)
+        // bit length of |x_q| for the GEMM modulus count: thread max -> wave max
+        // -> block max (LDS) -> one word per block
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < PT; ++k) {
+            const double s = round(fabs(xv[k]) * scale);
+            if (s >= 340282366920938463463374607431768211456.0) bits = 128;
+            else if (s >= 1.0) bits = max(bits, (uint32_t)ilogb(s) + 1);
+        }
         __shared__ uint32_t wmax[4];
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, off));
         if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = bits;
         __syncthreads();
-        if (threadIdx.x == 0)
-            blockmax[blk] = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        bmax = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        if (!(fold.wout && gblk < fold.nblk) && threadIdx.x == 0) blockmax[blk] = bmax;
     }
-    if (i >= n) return;
-    if (keep.cols) {                                  // partial store (row-sharded rank)
-        const uint32_t r = (uint32_t)(i / keep.cols), cc = (uint32_t)(i - (uint64_t)r * keep.cols);
-        if (!((r >= keep.rlo && r < keep.rhi) || (cc >= keep.clo && cc < keep.chi))) return;
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+        const uint64_t i = i0 + 256ull * k;
+        if (i >= n) continue;
+        if (keep.cols) {                                  // partial store (row-sharded rank)
+            const uint32_t r = (uint32_t)(i / keep.cols), cc = (uint32_t)(i - (uint64_t)r * keep.cols);
+            if (!((r >= keep.rlo && r < keep.rhi) || (cc >= keep.clo && cc < keep.chi))) continue;
+        }
+        const double x = xv[k];
+        const bool neg = signbit(x) && !isnan(x);
+        const double s = round(fabs(x) * scale);
+        Fr q = fr_zero();
+        if (s >= 340282366920938463463374607431768211456.0) {
+            q.w[0] = q.w[1] = q.w[2] = q.w[3] = 0xffffffffu;
+        } else if (s > 0.0) {
+            const uint64_t bits = __double_as_longlong(s);
+            const int e = (int)((bits >> 52) & 0x7ff) - 1075;
+            const uint64_t mant = (bits & 0xfffffffffffffull) | (1ull << 52);
+            const unsigned __int128 v = e >= 0 ? ((unsigned __int128)mant << e) : (unsigned __int128)(mant >> -e);
+            q.w[0] = (uint32_t)v; q.w[1] = (uint32_t)(v >> 32);
+            q.w[2] = (uint32_t)(v >> 64); q.w[3] = (uint32_t)(v >> 96);
+        }
+        st_fr(out + i, neg ? fr_sub(fr_zero(), q) : q);
     }
-    double x = in[i];
-    bool neg = signbit(x) && !isnan(x);
-    double s = round(fabs(x) * scale);
-    Fr q = fr_zero();
-    if (s >= 340282366920938463463374607431768211456.0) {
-        q.w[0] = q.w[1] = q.w[2] = q.w[3] = 0xffffffffu;
-    } else if (s > 0.0) {
-        uint64_t bits = __double_as_longlong(s);
-        int e = (int)((bits >> 52) & 0x7ff) - 1075;
-        uint64_t mant = (bits & 0xfffffffffffffull) | (1ull << 52);
-        unsigned __int128 v = e >= 0 ? ((unsigned __int128)mant << e) : (unsigned __int128)(mant >> -e);
-        q.w[0] = (uint32_t)v; q.w[1] = (uint32_t)(v >> 32);
-        q.w[2] = (uint32_t)(v >> 64); q.w[3] = (uint32_t)(v >> 96);
-    }
-    st_fr(out + i, neg ? fr_sub(fr_zero(), q) : q);
+    if (blockmax && fold.wout && gblk < fold.nblk) bits_fold(fold, gblk, bmax);
 }
 __global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in, uint64_t n,
                                                   Fr* __restrict__ out, double scale,
@@ -130,7 +199,7 @@ __global__ __launch_bounds__(256) void k_quantize_multi(const QuantSegs q, doubl
         if (s == (uint32_t)k) {
             in = q.in[k]; out = q.out[k]; bm = q.blockmax[k]; n = q.n[k]; b0 = q.blk0[k]; keep = q.keep[k];
         }
-    quantize_body(in, n, out, scale, bm, blockIdx.x - b0, keep);
+    quantize_body(in, n, out, scale, bm, blockIdx.x - b0, keep, q.fold, blockIdx.x);
 }
 hipError_t launch_quantize_multi(const QuantSegs& q, int p, hipStream_t st) {
     if (!q.nseg || q.nseg > (uint32_t)kMaxQuantSegs || !q.blk0[q.nseg]) return hipErrorInvalidValue;
@@ -143,7 +212,7 @@ hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int p, unsigne
                            hipStream_t st) {
     if (!n) return hipSuccess;
     double scale = (double)(1ull << p);
-    hipLaunchKernelGGL(k_quantize, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, n, out,
+    hipLaunchKernelGGL(k_quantize, dim3((unsigned)((n + kQuantPerBlock - 1) / kQuantPerBlock)), dim3(256), 0, st, in, n, out,
                        scale, blockmax);
     return hipGetLastError();
 }
@@ -2381,9 +2450,11 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
     const uint32_t rb = (J.blk0 & 7) ? lb : scan_row(lb, J.rows), r = J.r_begin + rb;
     Fr* rowout = J.out + (uint64_t)rb * (3ull * L + 1);
     const Fr zero = fr_zero();
+    Fr eqy = zero;                                        // is_equal's y, loaded ahead
     if (tid == 0) {
         st_fr(rowout, zero);
         carry_s = zero;
+        if (J.eq_out) eqy = ld_fr(J.eq_y + (uint64_t)r * J.eq_ys);
     }
     for (uint32_t c0 = 0; c0 < L; c0 += 256 * T) {
         const uint32_t j0 = c0 + tid * T;
@@ -2446,6 +2517,37 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
             for (uint32_t hc = tid; hc < 2 * ncell; hc += 256) o[hc] = stage[hc + hc / (6 * T)];
             __syncthreads();
         }
+    }
+    // row-end epilogues on the row total carry_s (written before the last barrier)
+    if (J.pc && tid < 1 + kTabSlots) {
+        const Fr v = carry_s;
+        if (tid == 0) {
+            st_fr(J.pc + r, v);
+        } else {
+            const uint32_t sl = tid - 1;
+            const Fr x = mont_mul(v, B.f.f[sl]);
+            Fr* base = J.ptab + 2ull * sl * J.plen;
+            st_fr(base + r, x);
+            if (sl < kTabSlots - 1) st_fr(base + J.plen + r, fr_neg(x));
+        }
+    }
+    if (J.eq_out) {
+        if (tid == 0) {
+            const Fr x = carry_s, y = eqy;
+            const Fr d = fr_sub(x, y), one = fr_from_u64(1);
+            const bool z = fr_is_zero(d);
+            const Fr zf = z ? one : zero;
+            Fr inv = one;
+            if (!z) inv = fr_inv(d);
+            const Fr cell[12] = {d, y, one, x, zf, d, inv, one, zero, d, zf, zero};
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {
+                stage[2 * k] = make_uint4(cell[k].w[0], cell[k].w[1], cell[k].w[2], cell[k].w[3]);
+                stage[2 * k + 1] = make_uint4(cell[k].w[4], cell[k].w[5], cell[k].w[6], cell[k].w[7]);
+            }
+        }
+        __syncthreads();
+        if (tid < 24) reinterpret_cast<uint4*>(J.eq_out + 12ull * r)[tid] = stage[tid];
     }
 }
 

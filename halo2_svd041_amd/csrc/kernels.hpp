@@ -28,6 +28,12 @@ struct ScaleTab {
 // One row scan of a batched launch: rows [r_begin, r_begin + rows) of A (L
 // columns) against w (canonical wc, scaled table tab), row i's 3L+1 cells at
 // out + i*(3L+1). blk0 is set by launch_scan_batch.
+// Row-end epilogues (zero fields: none):
+//  pc / ptab: the row totals t_r (= A.w, every row of A scanned) as a vector of
+//    length plen -- canonical copy pc[r] and scaled table ptab (k_vec_prep's), so
+//    the next scan multiplies by it without a k_vec_prep launch;
+//  eq_out: verify_mul's is_equal(t_r, y_r) row (12 cells, PB::g_is_equal's
+//    [d, y, 1, x, z, d, inv, 1, 0, d, z, 0]) at eq_out + 12 r, y_r = eq_y[r eq_ys].
 struct ScanJob {
     DView A;
     const Fr* wc;
@@ -36,12 +42,20 @@ struct ScanJob {
     Fr* out;
     uint32_t L, rows, blk0, r_begin;
     NaSpec spec;
+    Fr* pc;
+    Fr* ptab;
+    uint32_t plen;
+    uint32_t eq_ys;
+    Fr* eq_out;
+    const Fr* eq_y;
 };
-static constexpr int kMaxScanJobs = 4;
+static constexpr int kMaxScanJobs = 8;
+static constexpr int kMaxVerifyBatch = 4;   // verify_mul calls per batch (b and a scans share a launch)
 struct ScanBatch {
     ScanJob job[kMaxScanJobs];
     uint32_t njobs;
     const unsigned* bitw;     // device bit-length words of the NaSpecs (na = 0 launches)
+    ScaleTab f;               // slot factors for the pc / ptab epilogue
 };
 // gamma powers from host-side Montgomery tables: g^j = t[j & 15] t[16 + (j >> 4 & 15)]
 // t[32 + (j >> 8)] (j < 256 * nhi)
@@ -55,12 +69,12 @@ struct GammaTab {
 static constexpr int kStageElems = 256;
 
 // ZkMatrix::new / ZkVector::new quantization (f64 -> Fr) of n contiguous values.
-// blockmax (nullable, ceil(n / 256) words): per-block max of bit-length(|x_q|).
+// blockmax (nullable, ceil(n / kQuantPerBlock) words): per-block max of bit-length(|x_q|).
 hipError_t launch_quantize(const double* in, uint64_t n, Fr* out, int precision_bits,
                            unsigned* blockmax, hipStream_t st);
 // Fold per-block maxima: out[s] = max(blockmax[begin[s] .. begin[s + 1])), s < nseg.
 // One launch quantizing up to 4 matrices (m, u, v, d of the SVD witness):
-// segment s covers blocks [blk0[s], blk0[s+1]) of 256 values.
+// segment s covers blocks [blk0[s], blk0[s+1]) of kQuantPerBlock values.
 // Segment k may store only part of its cells (keep[k].cols != 0: value i is
 // element (i / cols, i % cols) and is stored when its row is in [rlo, rhi) or
 // its column in [clo, chi)); its bit-length maxima still cover every value.
@@ -68,6 +82,22 @@ static constexpr int kMaxQuantSegs = 4;
 struct QuantKeep {
     uint32_t cols, rlo, rhi, clo, chi;
 };
+// In-launch fold of the per-block bit-length maxima (what k_bits_reduce does in
+// a launch of its own): blocks [0, nblk) publish bm[block] and arrive on the
+// counters cnt[1 + (block & 7)], the last of each group on cnt[0] (all zero
+// between launches, each reset by its last arrival); the last block folds
+// segment s = blocks [b[s], b[s + 1]) into wout[s].
+struct BitFold {
+    unsigned* bm;
+    unsigned* cnt;
+    unsigned* wout;
+    uint32_t nblk;
+    uint32_t nred;                       // segments folded (<= 3)
+    uint32_t b[4];
+};
+// Values per quantize block (16 per thread): few enough blocks for one wave of
+// them at 1024^2, so the fold's arrival costs each block once.
+static constexpr uint32_t kQuantPerBlock = 4096;
 struct QuantSegs {
     const double* in[kMaxQuantSegs];
     Fr* out[kMaxQuantSegs];
@@ -76,6 +106,7 @@ struct QuantSegs {
     QuantKeep keep[kMaxQuantSegs];
     uint32_t blk0[kMaxQuantSegs + 1];
     uint32_t nseg;
+    BitFold fold;                        // fold.wout null: no in-launch fold
 };
 hipError_t launch_quantize_multi(const QuantSegs& q, int precision_bits, hipStream_t st);
 // Witness checker (svdw_check_gates). A region is `nunits` repetitions of a

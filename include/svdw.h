@@ -262,6 +262,8 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   in HBM);
  *   "stage_elems" 256 (elements per stage block, multiple of 16 in [16, 256]);
  *   "stage_align" 1 | 0 (each block's store windows aligned to 4 KiB);
+ *   "bits_fold" 1 | 0 (the operand bit-length words folded inside the quantize
+ *   launch, or by k_bits_reduce, a launch of its own);
  *   "colsum" 1 | 0 (row-sharded svd_witness: every entry of the Freivalds
  *   vectors b.g from the f64 inputs, column-parallel, or 0 from the cells);
  *   "res_f64" 1 | 0 (svd_witness with inputs in HBM: the CRT residue planes of
@@ -273,8 +275,8 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   products in one GEMM and one combine launch; -1: on row-sharded contexts); "prod_cell" -1 | 0 | 1 (svd_witness with
  *   device inputs: the products on the cell stream and the u / v bounds and u.d
  *   beside them; -1 on row-sharded contexts); "res_first"
- *   0 | 1 | -1 (the cell stream waits for the residue planes; -1: on row-sharded
- *   contexts; measured slower, kept for A/B).
+ *   -1 | 0 | 1 (the cell stream waits for the residue planes; -1: on row-sharded
+ *   contexts, where it measured ~3% faster; slower at 1 GPU).
  * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:
  *   phase 1 starts with the two ctx_gate constant cells [1, 0] that
  *   examples/svd_example.rs:183's rlc.load_rlc_cache(.., 1) appends as recalled

@@ -475,8 +475,9 @@ def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device):
     assert walk_window(ctx.layout(), get, {(0, 0): a0, (0, 1): l0, (1, 0): a1}, 0, row_lim) > 0
 
 
-@pytest.mark.parametrize("rank", [0, 3, 7])
-def test_full_size_shard_rank_parity(gpu_ctx_factory, rank):
+@pytest.mark.parametrize("rank,opts", [(0, {}), (3, {}), (7, {}),
+                                       (3, {"overlap": 0, "phase1_overlap": 0})])
+def test_full_size_shard_rank_parity(gpu_ctx_factory, rank, opts):
     """BASELINE config 4 (1024^2, P=63, row blocks over 8 GPUs), rank by rank at
     full size, cell for cell: the rank's witness on the GPU (svdw_set_shard, the
     bench's device-input path) against the C oracle's row window inside that
@@ -491,6 +492,8 @@ def test_full_size_shard_rank_parity(gpu_ctx_factory, rank):
     m, u, d, v = gen_svd_input(N, N, seed=2 * N + P)
     g = gamma_for(N * N + 8)
     ctx = gpu_ctx_factory(P)
+    for k, val in opts.items():
+        ctx.set_option(k, val)
     ctx.set_shard(rank, world)
     hs.svd_witness(ctx, *_on_device(m, u, v, d), g)
     ctx.sync()

@@ -131,3 +131,39 @@ def test_fused_verify_mul_witness_full_stream(gpu_ctx_factory, n, k, m, P, dev):
     assert np.array_equal(ctx.advice(0), c0) and np.array_equal(ctx.advice(1), c1)
     chk = ctx.check_gates()
     assert chk["gate_failures"] == 0 and chk["lookup_failures"] == 0 and chk["copy_failures"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pos", ["first", "middle", "last", "b_last"])
+@pytest.mark.parametrize("fold", [1, 0])
+def test_bit_fold_outlier_block(gpu_ctx_factory, pos, fold):
+    """The operand bit-length words decide the GEMM's modulus count. One large
+    entry in one quantize block (first / middle / last block of a, last of b)
+    must reach the word through the in-launch fold (bits_fold 1) as through
+    k_bits_reduce (0): too few moduli would change c_s. 300 x 200 x 150 spans
+    several 4096-value blocks; every run repeats twice (the fold's counter is
+    reset by its last arrival)."""
+    import torch
+    import halo2_svd041_amd as hs
+    n, k, m, P = 300, 200, 150, 63
+    a, b, _ = _inputs(n, k, m, seed=11)
+    a = a * 1e-3
+    b = b * 1e-3
+    big = 3.0e7                                     # 2^63 * 3e7 ~ 2^88 bits
+    if pos == "first":
+        a[0, 5] = big
+    elif pos == "middle":
+        a[n // 2, k // 3] = -big
+    elif pos == "last":
+        a[n - 1, k - 1] = big
+    else:
+        b[k - 1, m - 1] = -big
+    g = gamma_for(n + m)
+    ctx = gpu_ctx_factory(P)
+    ctx.set_option("bits_fold", fold)
+    ta, tb = (torch.tensor(x, dtype=torch.float64, device="cuda:0") for x in (a, b))
+    c0, c1 = corc.verify_mul_witness(a, b, P, g)
+    for _ in range(2):
+        ctx.reset()
+        hs.verify_mul_witness(ctx, ta, tb, g)
+        assert np.array_equal(ctx.advice(0), c0) and np.array_equal(ctx.advice(1), c1)
