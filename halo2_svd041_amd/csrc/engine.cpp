@@ -552,16 +552,18 @@ struct svdw_ctx {
     struct Batch {
         hipStream_t st;
         std::vector<std::vector<Pending>> groups;
+        size_t last = 0;                   // group of the latest stage
     };
     std::vector<Batch> batches;
     bool stage_batch = true;
+    bool stage_front = false;               // stage_launch: the stage goes ahead of the batch's groups
     // device ingest (svdw_parse_svd_input_device) scratch
     DBuf ing_x, ing_e, ing_c, ing_p10, ing_val, ing_npos, ing_nd, ing_rpos, ing_kpos, ing_err, ing_q;
     // device equality records (eq_gen_device)
     DBuf eq_cp, eq_ks, eq_reg, eq_w, eq_k, eq_err, eq_st;
 };
 
-static void flush_batch(svdw_ctx* c, hipStream_t s);
+static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter = nullptr);
 static void sync(svdw_ctx* c) {
     if (c->dry) return;
     hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
@@ -579,6 +581,7 @@ static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
     }
     hipEvent_t e = c->deps[c->dep_next++];
     flush_batch(c, from);
+    if (getenv("SVDW_BATCH_LOG")) fprintf(stderr, "dep %p -> %p\n", (void*)from, (void*)to);
     hipck(hipEventRecord(e, from), "hipEventRecord");
     if (to) hipck(hipStreamWaitEvent(to, e, 0), "hipStreamWaitEvent");
     return e;
@@ -908,8 +911,15 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
         for (size_t k = 0; k < b.groups.size(); ++k)
             for (const auto& q : b.groups[k])
                 if (reads(q)) g = k + 1;
+        if (c->stage_front && g == 0) {                   // a launch of its own, ahead of the batch
+            b.groups.insert(b.groups.begin(), std::vector<svdw_ctx::Pending>{});
+            b.groups[0].push_back({a, std::string("k_stage:") + tag, bytes});
+            b.last = 0;
+            return;
+        }
         if (g == b.groups.size()) b.groups.emplace_back();
         b.groups[g].push_back({a, std::string("k_stage:") + tag, bytes});
+        b.last = g;
         return;
     }
     {
@@ -918,12 +928,18 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     }
 }
 // Issue a stream's pending batched stages (k_stage_multi; one program: k_stage).
-static void flush_batch(svdw_ctx* c, hipStream_t s) {
+// waiter: after the group holding the latest stage, `waiter` waits for s there
+// (it needs that stage and what came before on s, not the later groups: those
+// hold stages queued earlier that depend on other pending ones).
+static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter) {
     for (auto& b : c->batches) {
         if (b.st != s || b.groups.empty()) continue;
         std::vector<std::vector<svdw_ctx::Pending>> groups;
         groups.swap(b.groups);               // (cleared before launching: no re-entry)
-        for (const auto& grp : groups) {
+        const size_t upto = b.last;
+        for (size_t gi = 0; gi < groups.size(); ++gi) {
+            const auto& grp = groups[gi];
+            if (gi == upto + 1 && waiter) { stream_dep(c, s, waiter); waiter = nullptr; }
             if (grp.empty()) continue;
             std::vector<const StageArgs*> ps;
             double bytes = 0;
@@ -932,10 +948,16 @@ static void flush_batch(svdw_ctx* c, hipStream_t s) {
                 bytes += q.bytes;
             }
             const std::string name = grp.size() == 1 ? grp[0].name : "k_stage:multi";
+            if (getenv("SVDW_BATCH_LOG")) {
+                fprintf(stderr, "batch stream %p group %zu/%zu (last %zu):", (void*)s, gi, groups.size(), upto);
+                for (const auto& q : grp) fprintf(stderr, " %s", q.name.c_str());
+                fprintf(stderr, "\n");
+            }
             ProfScope pr(c, s, name, bytes, 0, true);
             hipck(launch_stage_multi(ps.data(), (int)ps.size(), s), "k_stage_multi");
         }
     }
+    if (waiter) stream_dep(c, s, waiter);
 }
 // RAII: stage launches on the current stream between construction and end()
 // are batched (k_stage_multi); nested scopes on the same stream join the outer
@@ -2330,8 +2352,13 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     std::swap(vt.rows, vt.cols); std::swap(vt.rs, vt.cs);
     DView udv;
     EqCell udpad;
+    // products on the cell stream: u.d (all the diff needs from st2) in a launch
+    // ahead of the bounds, so the cell stream waits for it alone
     if (r == M) {
-        udv = view_of(c, mat_times_diag_mat(c, u, d));
+        c->stage_front = pc;
+        const svdw_mat ud = mat_times_diag_mat(c, u, d);
+        c->stage_front = false;
+        udv = view_of(c, ud);
     } else {
         const svdw_vec z = put_cell(c, 0 + u.phase, fr_zero(), true);   // zero padding constant
         udpad = EqCell{(int)z.phase, z.off};
@@ -2343,7 +2370,9 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     bs.end();
     if (pc) {
         std::swap(c->st, c->st2);
-        stream_dep(c, c->st2, c->st);                   // (flushes st2's batch first)
+        // the cell stream waits for u.d (and what precedes it on st2), not for
+        // the d checks' dependent second group batched behind it
+        flush_batch(c, c->st2, c->st);
     }
     if (batched) {
         host_mark(c, "bounds(u), bounds(v), u.d queued");

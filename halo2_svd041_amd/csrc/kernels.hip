@@ -33,6 +33,14 @@ __device__ __forceinline__ void st_fr(Fr* p, const Fr& v) {
     q[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
     q[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
 }
+// Streaming store (nontemporal): cells the next kernel boundary would otherwise
+// write back from L2 (the products, the quantized operands).
+__device__ __forceinline__ void st_fr_nt(Fr* p, const Fr& v) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    v4u* q = reinterpret_cast<v4u*>(p);
+    __builtin_nontemporal_store(v4u{v.w[0], v.w[1], v.w[2], v.w[3]}, q);
+    __builtin_nontemporal_store(v4u{v.w[4], v.w[5], v.w[6], v.w[7]}, q + 1);
+}
 // X(i, j) of a view; `pad` is the value outside the view (K[v.pad_k]).
 __device__ __forceinline__ Fr view_load(const DView v, const Fr pad, uint32_t i, uint32_t j) {
     if (v.mode == VIEW_DIAG) return (i == j) ? ld_fr(v.ptr) : pad;
@@ -173,7 +181,7 @@ __device__ __forceinline__ void quantize_body(const double* __restrict__ in, uin
             q.w[0] = (uint32_t)v; q.w[1] = (uint32_t)(v >> 32);
             q.w[2] = (uint32_t)(v >> 64); q.w[3] = (uint32_t)(v >> 96);
         }
-        st_fr(out + i, neg ? fr_sub(fr_zero(), q) : q);
+        st_fr_nt(out + i, neg ? fr_sub(fr_zero(), q) : q);
     }
     if (blockmax && fold.wout && gblk < fold.nblk) bits_fold(fold, gblk, bmax);
 }
@@ -1743,8 +1751,8 @@ __device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t cblk)
     }
     x[8] = (uint32_t)t;
     const Fr v = reduce9(x);
-    st_fr(q.out + (int64_t)i * q.ors + (int64_t)j * q.ocs, v);
-    if (q.sym && j > i) st_fr(q.out + (int64_t)j * q.ors + (int64_t)i * q.ocs, v);
+    st_fr_nt(q.out + (int64_t)i * q.ors + (int64_t)j * q.ocs, v);
+    if (q.sym && j > i) st_fr_nt(q.out + (int64_t)j * q.ors + (int64_t)i * q.ocs, v);
 }
 // Combine blocks of a CrtBatch (cblocks in all, job j from cblk0[j]) dealt
 // XCD-contiguously: XCD x takes a contiguous run of the row-major tile
