@@ -297,7 +297,7 @@ def main():
                     help="skip the engine's event profiler in the timed region")
     ap.add_argument("--profile-prefix", default=None,
                     help="kernel-name prefix the timed-region profiler records "
-                         "(default k_stage for svd, all kernels for verify_mul)")
+                         "(default k_stage for svd, k_matvec_scan for verify_mul)")
     ap.add_argument("--breakdown", action="store_true", help="print per-kernel ms/step to stderr")
     ap.add_argument("--shard", choices=["replicas", "rows"], default=None,
                     help="N>1: one matrix row-block sharded over the ranks (default; strong "
@@ -391,7 +391,9 @@ def main():
     sync()
 
     profile = not args.no_profile and not args.dry
-    prefix = args.profile_prefix if args.profile_prefix is not None else ("k_stage" if svd else "")
+    # events around the dominant kernel's launches only: at config 2's size,
+    # events around all ten launches of a step doubled the step time
+    prefix = args.profile_prefix if args.profile_prefix is not None else ("k_stage" if svd else "k_matvec_scan")
     if profile:
         ctx.profile(True, prefix)
     if dist is not None:

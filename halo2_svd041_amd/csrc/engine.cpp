@@ -411,7 +411,8 @@ struct svdw_ctx {
     // each time). svd_witness queues it first thing on a side stream (gp_ev).
     Fr gp_gamma{};
     uint32_t gp_len = 0;
-    hipEvent_t gp_ev = nullptr;             // gamma_prep queued ahead (svd_witness)
+    hipEvent_t gp_ev = nullptr;
+    hipStream_t gp_st = nullptr;            // the stream gp_ev was recorded on             // gamma_prep queued ahead (svd_witness)
     // Device bit-length words of matrices written in this witness (svd_witness:
     // quantized m, u, v at dbitw[0..2]): the row scans decide their operand
     // width on the device from these (NaSpec), so the host never waits for them.
@@ -564,6 +565,10 @@ struct svdw_ctx {
 };
 
 static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter = nullptr);
+// debug logs (read once: getenv scans the environment)
+static bool env_flag(const char* name) { const char* v = getenv(name); return v && *v && *v != '0'; }
+static const bool g_batch_log = env_flag("SVDW_BATCH_LOG");
+static const bool g_stage_log = env_flag("SVDW_STAGE_LOG");
 static void sync(svdw_ctx* c) {
     if (c->dry) return;
     hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
@@ -581,7 +586,7 @@ static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
     }
     hipEvent_t e = c->deps[c->dep_next++];
     flush_batch(c, from);
-    if (getenv("SVDW_BATCH_LOG")) fprintf(stderr, "dep %p -> %p\n", (void*)from, (void*)to);
+    if (g_batch_log) fprintf(stderr, "dep %p -> %p\n", (void*)from, (void*)to);
     hipck(hipEventRecord(e, from), "hipEventRecord");
     if (to) hipck(hipStreamWaitEvent(to, e, 0), "hipStreamWaitEvent");
     return e;
@@ -859,7 +864,7 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
             ee = (uint32_t)(r1 * cw);
         }
     }
-    if (getenv("SVDW_STAGE_LOG")) {
+    if (g_stage_log) {
         uint32_t nmul = 0;
         for (uint32_t i = 0; i < a.nmo; ++i) nmul += a.mo[i].op == MO_MUL;
         fprintf(stderr, "stage %-28s elems %8u C %3u L %3u nv %2u nmo %2u muls %u nk %u\n", tag, ee - eb,
@@ -948,7 +953,7 @@ static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter) {
                 bytes += q.bytes;
             }
             const std::string name = grp.size() == 1 ? grp[0].name : "k_stage:multi";
-            if (getenv("SVDW_BATCH_LOG")) {
+            if (g_batch_log) {
                 fprintf(stderr, "batch stream %p group %zu/%zu (last %zu):", (void*)s, gi, groups.size(), upto);
                 for (const auto& q : grp) fprintf(stderr, " %s", q.name.c_str());
                 fprintf(stderr, "\n");
@@ -1756,7 +1761,7 @@ static void gamma_prep(svdw_ctx* c, uint32_t d, const Fr& gamma, hipStream_t s) 
 static void ensure_gamma_vec(svdw_ctx* c, uint32_t d, const Fr& gamma) {
     if (c->dry) return;
     if (c->gp_ev && c->gp_len >= d && fr_eq(c->gp_gamma, gamma)) {
-        hipck(hipStreamWaitEvent(c->st, c->gp_ev, 0), "hipStreamWaitEvent");
+        if (c->gp_st != c->st) hipck(hipStreamWaitEvent(c->st, c->gp_ev, 0), "hipStreamWaitEvent");
         return;
     }
     gamma_prep(c, d, gamma, c->st);
@@ -1834,6 +1839,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         stage_own(c, phase, p.eq, a.rows, 1, p.eq_off, p.eq_loff);
     }
     if (c->dry) return;
+    host_mark(c, "verify_mul layout");
     // pass 2: launches
     ensure_gamma_vec(c, dmax, gamma);
     const Fr* gpc = (const Fr*)c->gpc.p;
@@ -2007,6 +2013,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         for (int i = 0; i < n; ++i) add_a(as_, i);
         launch(as_, "k_matvec_scan:a");
     }
+    host_mark(c, "verify_mul b, a scans queued");
     for (hipEvent_t ev : c->wait_before_cs)
         hipck(hipStreamWaitEvent(c->st, ev, 0), "hipStreamWaitEvent");
     // the c_s scans; each row's is_equal(c_s.g, a.(b.g)) cells from its row
@@ -2468,6 +2475,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
         gamma_prep(c, std::max(N, M), gamma, c->st3);
         c->gp_ev = stream_dep(c, c->st3, nullptr);
+        c->gp_st = c->st3;
         host_mark(c, "gamma_prep queued");
     }
     unsigned* dbits = nullptr;
@@ -2602,6 +2610,8 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
                                       uint32_t K, uint32_t M, bool on_device, const Fr& gamma) {
     REQUIRE(N >= 1 && K >= 1 && M >= 1, "empty matrix");
     REQUIRE(!sharded(c), "verify_mul_witness: not for row-sharded contexts");
+    c->ht0 = std::chrono::steady_clock::now();
+    host_mark(c, "verify_mul_witness start");
     clear_streams(c);
     c->dep_next = 0;
     c->prelaunched = false;
@@ -2626,6 +2636,13 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     }
     c->ext_off = 0;
     c->gp_ev = nullptr;
+    if (!c->dry && c->hold_us) {       // every stream of the step waits for st's hold
+        hipck(launch_hold(c->hold_us, c->st), "k_hold");
+        if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
+        stream_dep(c, c->st, c->st3);
+        stream_dep(c, c->st, c->st2);
+    }
+    host_mark(c, "plan + gamma_prep queued");
     unsigned* dbits = nullptr;
     const uint32_t nba = (uint32_t)(((uint64_t)N * K + kQuantPerBlock - 1) / kQuantPerBlock),
                    nbb = (uint32_t)(((uint64_t)K * M + kQuantPerBlock - 1) / kQuantPerBlock);
@@ -2633,6 +2650,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
         if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
         gamma_prep(c, M, gamma, c->st3);
         c->gp_ev = stream_dep(c, c->st3, nullptr);
+        c->gp_st = c->st3;
         ensure_buf(c, c->bits, (64 + nba + nbb) * sizeof(unsigned));
         dbits = (unsigned*)c->bits.p;
     }
@@ -2656,6 +2674,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
         c->dbitw = dbits;
         c->dwords = {{za, 0}, {zb, 1}};
     }
+    host_mark(c, "quantize queued");
     // c_s = a * b (honest_prover_mat_mul's cells), the CRT GEMM sized on the device
     uint64_t off;
     append(c, 0, (uint64_t)N * M, 0, &off, nullptr, "product", N);
@@ -2665,9 +2684,66 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
         while ((1ull << lk) < K) ++lk;
         c->prods.push_back({cs, za, zb, lk});
     }
-    if (!c->dry) gemm_exec(c, c->st, za, zb, cellp(c, 0, off), ~0u, ~0u, dbits, dbits + 1, true);
+    // device inputs: residue planes of a and b^T straight from the f64 inputs
+    // (one launch), the GEMM and combine on st, and verify_mul on the third
+    // stream from the loads on: its one / gamma-power cells and the b and a
+    // scans run beside the product, only the c_s scans wait for it
+    const bool f64 = on_device && !c->dry && c->res_f64 && c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA &&
+                     c->gemm_rt && K <= 8192 && qs.nseg == 2;
+    hipEvent_t loaded = nullptr;
+    if (f64) {
+        loaded = stream_dep(c, c->st, nullptr);
+        uint32_t lk = 0;
+        while ((1ull << lk) < K) ++lk;
+        const uint32_t kpad = (K + 255) / 256 * 256, rpa = (N + 127) / 128 * 128, rpb = (M + 127) / 128 * 128;
+        ensure_buf(c, c->digA, (size_t)kCrtMaxResidues * rpa * kpad);
+        ensure_buf(c, c->digB, (size_t)kCrtMaxResidues * rpb * kpad);
+        ensure_buf(c, c->crtR, (size_t)kCrtMaxResidues * rpa * rpb);
+        ResSegs q;
+        memset(&q, 0, sizeof q);
+        auto seg = [&](const double* in, uint32_t rows, uint32_t ld, uint32_t rp, DBuf& out, uint32_t tr) {
+            ResSeg& g = q.seg[q.nseg++];
+            g.in = in; g.out = (uint32_t*)out.p;
+            g.rows = rows; g.cols = K; g.ld = ld; g.rows_pad = rp; g.kw = kpad / 4; g.tr = tr;
+            g.wa[0] = 0; g.wb[0] = 1; g.lk[0] = lk;
+            g.wa[1] = g.wb[1] = -1;
+        };
+        seg(a, N, K, rpa, c->digA, 0);
+        seg(b, M, M, rpb, c->digB, 1);                    // b^T(j, k) = b[k * M + j]
+        {
+            ProfScope ps(c, c->st, "k_residues_f64", 8.0 * ((double)N * K + (double)K * M), 0);
+            hipck(launch_residues_f64(q, dbits, (int)c->P, c->st), "k_residues_f64");
+        }
+        {
+            ProfScope ps(c, c->st, "k_gemm_crt", 32.0 * N * M, (double)N * M * K);
+            hipck(launch_gemm_crt(false, (const uint8_t*)c->digA.p, (const uint8_t*)c->digB.p, N, M, rpa, rpb,
+                                  kpad, (uint8_t*)c->crtR.p, cellp(c, 0, off), M, 1, dbits, dbits + 1, lk,
+                                  c->st),
+                  "k_gemm_crt");
+        }
+    } else if (!c->dry) {
+        gemm_exec(c, c->st, za, zb, cellp(c, 0, off), ~0u, ~0u, dbits, dbits + 1, true);
+    }
+    host_mark(c, "product queued");
     const VMul vm{za, zb, cs};
-    verify_mul_many(c, 1, &vm, 1, gamma);
+    if (f64) {
+        c->wait_before_cs = {stream_dep(c, c->st, nullptr)};
+        hipck(hipStreamWaitEvent(c->st3, loaded, 0), "hipStreamWaitEvent");
+        std::swap(c->st, c->st3);
+        try {
+            verify_mul_many(c, 1, &vm, 1, gamma);
+        } catch (...) {
+            std::swap(c->st, c->st3);
+            c->wait_before_cs.clear();
+            throw;
+        }
+        std::swap(c->st, c->st3);
+        c->wait_before_cs.clear();
+        stream_dep(c, c->st3, c->st);                     // join
+    } else {
+        verify_mul_many(c, 1, &vm, 1, gamma);
+    }
+    host_mark(c, "verify_mul_witness end");
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
 }
 

@@ -1426,12 +1426,14 @@ __global__ __launch_bounds__(256) void k_residues_f64(const ResSegs q, const uns
     if (!n) return;
     const uint64_t idx = (uint64_t)(blockIdx.x - q.blk0[s]) * blockDim.x + threadIdx.x;
     if (idx >= (uint64_t)g.rows_pad * g.kw) return;
-    const uint32_t row = (uint32_t)(idx / g.kw), kg = (uint32_t)(idx % g.kw);
+    const uint32_t row = g.tr ? (uint32_t)(idx % g.rows_pad) : (uint32_t)(idx / g.kw),
+                   kg = g.tr ? (uint32_t)(idx / g.rows_pad) : (uint32_t)(idx % g.kw);
     uint32_t w[4][4], nm[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
         const uint32_t kk = kg * 4 + t;
-        const double x = row < g.rows && kk < g.cols ? g.in[(uint64_t)row * g.ld + kk] : 0.0;
+        const uint64_t at = g.tr ? (uint64_t)kk * g.ld + row : (uint64_t)row * g.ld + kk;
+        const double x = row < g.rows && kk < g.cols ? g.in[at] : 0.0;
         quantized_words(x, scale, w[t], nm[t]);
     }
     uint32_t* o = g.out + (uint64_t)row * g.kw + kg;
@@ -1450,7 +1452,7 @@ hipError_t launch_residues_f64(const ResSegs& q0, const unsigned* W, int precisi
     uint32_t blocks = 0;
     for (uint32_t k = 0; k < q.nseg; ++k) {
         ResSeg& g = q.seg[k];
-        if (g.kw * 4 < g.cols || g.rows_pad < g.rows || g.ld < g.cols) return hipErrorInvalidValue;
+        if (g.kw * 4 < g.cols || g.rows_pad < g.rows || g.ld < (g.tr ? g.rows : g.cols)) return hipErrorInvalidValue;
         q.blk0[k] = blocks;
         blocks += (uint32_t)(((uint64_t)g.rows_pad * g.kw + 255) / 256);
     }

@@ -285,12 +285,15 @@ hipError_t launch_to_residues(const DView& x, uint32_t rows, uint32_t kdim, uint
 // and k >= cols zero; n = max over the segment's pairs p (wa[p] >= 0) of the CRT
 // modulus count of a product with operand bits W[wa[p]], W[wb[p]] and K <= 2^lk[p].
 static constexpr int kMaxResSegs = 4;
+// tr: element (row, k) is in[k * ld + row] (the planes of a transposed operand:
+// b^T of verify_mul_witness's b), threads laid along rows so the reads coalesce.
 struct ResSeg {
     const double* in;
     uint32_t* out;
     uint32_t rows, cols, ld, rows_pad, kw;
     int16_t wa[2], wb[2];
     uint32_t lk[2];
+    uint32_t tr;
 };
 struct ResSegs {
     ResSeg seg[kMaxResSegs];

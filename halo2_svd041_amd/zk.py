@@ -37,15 +37,38 @@ def int_to_words(x: int) -> np.ndarray:
     return np.array([(x >> (64 * i)) & ((1 << 64) - 1) for i in range(4)], dtype=np.uint64)
 
 
+_M64 = (1 << 64) - 1
+
+
+def _words_arg(x: int):
+    """x mod p as the 4-word little-endian argument of the C calls (a ctypes
+    array: no numpy round trip on the per-witness path)."""
+    x = int(x) % P_MOD
+    return (ct.c_uint64 * 4)(x & _M64, (x >> 64) & _M64, (x >> 128) & _M64, x >> 192)
+
+
 def words_to_int(w) -> int:
     w = [int(v) for v in w]
     return w[0] | (w[1] << 64) | (w[2] << 128) | (w[3] << 192)
 
 
+_torch = None
+
+
+def _torch_mod():
+    global _torch
+    if _torch is None:
+        import torch  # noqa: WPS433
+        _torch = torch
+    return _torch
+
+
 def _device_ptr(a) -> Optional[int]:
     """torch CUDA tensor -> device pointer (float64, contiguous) or None."""
+    if isinstance(a, np.ndarray):
+        return None
     try:
-        import torch  # noqa: WPS433
+        torch = _torch_mod()
     except ImportError:  # pragma: no cover
         return None
     if isinstance(a, torch.Tensor) and a.is_cuda:
@@ -57,8 +80,7 @@ def _device_ptr(a) -> Optional[int]:
 
 def _torch_stream(ctx: "Context") -> int:
     """torch's current stream on the context's device (hipStream_t as int)."""
-    import torch  # noqa: WPS433
-    return torch.cuda.current_stream(torch.device("cuda", ctx.device)).cuda_stream
+    return _torch_mod().cuda.current_stream(ctx.device).cuda_stream
 
 
 def _after_torch(ctx: "Context") -> None:
@@ -547,20 +569,19 @@ def svd_witness(ctx: Context, m, u, v, d, gamma: int, cfg: SvdConfigPy = SvdConf
     tensors on the context's device (then nothing is copied over PCIe)."""
     cfgc = cfg.c()
     cnt = Counts()
-    g = int_to_words(int(gamma) % P_MOD)
+    g = _words_arg(gamma)
     dps = [_device_ptr(x) for x in (m, u, v, d)]
     if all(p is not None for p in dps):
         N, M = m.shape
         _after_torch(ctx)
-        check(lib().svdw_svd_witness(ctx.handle, *dps, N, M, 1, ct.byref(cfgc), g.ctypes.data,
-                                     ct.byref(cnt)))
+        check(lib().svdw_svd_witness(ctx.handle, *dps, N, M, 1, ct.byref(cfgc), g, ct.byref(cnt)))
     else:
         arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (m, u, v, d)]
         N, M = arrs[0].shape
         if arrs[1].shape != (N, N) or arrs[2].shape != (M, M) or arrs[3].size != min(N, M):
             raise SvdwError(-1, "svd_witness: shapes must be m NxM, u NxN, v MxM, d min(N,M)")
         check(lib().svdw_svd_witness(ctx.handle, *[a.ctypes.data for a in arrs], N, M, 0,
-                                     ct.byref(cfgc), g.ctypes.data, ct.byref(cnt)))
+                                     ct.byref(cfgc), g, ct.byref(cnt)))
     ctx.last_svd = (int(N), int(M), cfg)        # for collect.plan (shard segment replay)
     return cnt.as_dict()
 
@@ -570,21 +591,21 @@ def verify_mul_witness(ctx: Context, a, b, gamma: int) -> dict:
     of a and b, c_s = a * b in phase 0, verify_mul(a, b, c_s, gamma) in phase 1.
     Inputs: numpy arrays or contiguous float64 torch tensors on the device."""
     cnt = Counts()
-    g = int_to_words(int(gamma) % P_MOD)
+    g = _words_arg(gamma)
     dps = [_device_ptr(x) for x in (a, b)]
     if all(p is not None for p in dps):
         (N, K), M = a.shape, b.shape[1]
         if b.shape[0] != K:
             raise SvdwError(-1, "verify_mul_witness: a.num_col != b.num_rows")
         _after_torch(ctx)
-        check(lib().svdw_verify_mul_witness(ctx.handle, *dps, N, K, M, 1, g.ctypes.data, ct.byref(cnt)))
+        check(lib().svdw_verify_mul_witness(ctx.handle, *dps, N, K, M, 1, g, ct.byref(cnt)))
     else:
         arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (a, b)]
         (N, K), M = arrs[0].shape, arrs[1].shape[1]
         if arrs[1].shape[0] != K:
             raise SvdwError(-1, "verify_mul_witness: a.num_col != b.num_rows")
         check(lib().svdw_verify_mul_witness(ctx.handle, arrs[0].ctypes.data, arrs[1].ctypes.data, N, K, M, 0,
-                                            g.ctypes.data, ct.byref(cnt)))
+                                            g, ct.byref(cnt)))
     return cnt.as_dict()
 
 

@@ -284,7 +284,7 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  * Timing aids (NOT bit-identical, for A/B measurements only): "stage_probe"
  *   0 | 1 (skip the stage programs) | 2 (store a constant instead of cells) |
  *   3 (constant stores, no view loads either);
- *   "hold_us" 0 | us (svd_witness: the step's streams wait behind a kernel
+ *   "hold_us" 0 | us (svd_witness, verify_mul_witness: the step's streams wait behind a kernel
  *   spinning that long, so the GPU schedule is measured without host gaps). */
 int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);
 

@@ -25,7 +25,8 @@ for cfg in "--n 1024 --p 63" "--n 512 --p 32" "--workload verify_mul"; do
 done
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/go_s8 -o run -- python3 tools/shard_sim.py --worlds 8 --rank 0 --steps 5 --opt hold_us=1500 $OPTS > /dev/null 2> $O/go_s8.err || exit $?
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/go_1k -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-profile --no-check --no-ingest --opt hold_us=3000 $OPTS > /dev/null 2> $O/go_1k.err || exit $?
-for d in go_s8 go_1k; do
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/go_vm -o run -- python3 bench.py --workload verify_mul --steps 5 --warmup 2 --no-cpu-baseline --no-profile --no-check --no-ingest --opt hold_us=1000 $OPTS > /dev/null 2> $O/go_vm.err || exit $?
+for d in go_s8 go_1k go_vm; do
   f=$(ls $O/$d/*/run_kernel_trace.csv 2>/dev/null | head -n 1)
   [ -z "$f" ] && f=$(ls $O/$d/run_kernel_trace.csv)
   python3 tools/timeline.py "$f" --all > $O/$d.timeline.txt || exit $?
