@@ -463,10 +463,12 @@ struct svdw_ctx {
     int phase1_overlap = 1;                 // "phase1_overlap": 0 off, 1 on st2 behind the
                                             // GEMMs, 2 on st3 from quantization on
     bool prelaunched = false;               // this witness's products were queued on st2
-    int prod_cell = -1;                     // "prod_cell": svd_witness's products (residues, GEMM,
+    int prod_cell = 1;                      // "prod_cell": svd_witness's products (residues, GEMM,
                                             // combine) on the cell stream and the u / v bounds and
                                             // u.d beside them on st2 (1), not (0); -1: on row-sharded
-                                            // ranks, where the product chain is the critical path
+                                            // ranks only. On by default: the product chain is the
+                                            // critical path sharded, and unsharded it measured
+                                            // 2.5 % faster at 1024^2 and 2048^2, neutral at 512^2
     bool prod_on_cell = false;              // this witness's products went on the cell stream
     uint32_t hold_us = 0;                   // "hold_us": timing aid, st spins this long first
     Fr ext_gamma{};                          // init_rand of the last verify_mul (equality source 2)

@@ -272,9 +272,9 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   u / v bounds and u.d, the d checks and constant cells, verify_mul's one cells
  *   and gamma powers, the is_equal rows; split automatically where a stage reads
  *   cells a pending one writes); "gemm_batch" 1 | 0 | -1 (svd_witness's three
- *   products in one GEMM and one combine launch; -1: on row-sharded contexts); "prod_cell" -1 | 0 | 1 (svd_witness with
+ *   products in one GEMM and one combine launch; -1: on row-sharded contexts); "prod_cell" 1 | 0 | -1 (svd_witness with
  *   device inputs: the products on the cell stream and the u / v bounds and u.d
- *   beside them; -1 on row-sharded contexts); "res_first"
+ *   beside them; -1 on row-sharded contexts only); "res_first"
  *   -1 | 0 | 1 (the cell stream waits for the residue planes; -1: on row-sharded
  *   contexts, where it measured ~3% faster; slower at 1 GPU).
  * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:

@@ -421,7 +421,7 @@ def test_row_sharded_device_inputs_parity(gpu_ctx_factory, N, M, P, world):
                                         (1, {"prod_cell": 1, "p1_at": 1}), (1, {"prod_cell": 1, "hold_us": 50}),
                                         (3, {"prod_cell": 0}), (3, {"prod_cell": 1, "stage_batch": 0}),
                                         (4, {"prod_cell": 1, "gemm_batch": 0}), (1, {"gemm_batch": 0}),
-                                        (5, {"prod_cell": 0}), (4, {"colsum": 0})])
+                                        (5, {"prod_cell": 0}), (4, {"colsum": 0}), (1, {"prod_cell": 0})])
 def test_products_on_cell_stream_parity(gpu_ctx_factory, world, opts):
     """prod_cell: the products on the cell stream, the u / v bounds and u.d on
     st2 beside them (default on row-sharded ranks), with device inputs (the
