@@ -500,12 +500,19 @@ struct svdw_ctx {
     // row-sharded rank takes b.g of b = u^T, v^T from the f64 rows directly
     // (k_colsum_f64), not from cells. Cleared at the end of the witness.
     struct F64Src { svdw_mat m; const double* x; };
+    // loaded regions whose f64 source is on the device for the current call:
+    // launches read them through VIEW_F64 (quantized in registers) instead of
+    // waiting for the quantized cells (f64_view)
+    struct F64Region { uint32_t phase; uint64_t off, n; const double* x; };
+    std::vector<F64Region> f64reg;
+    bool f64_views = true;                  // "f64_views"
     std::vector<F64Src> f64src;
     DBuf colpart;
     DBuf qfold;                             // k_quantize_multi's fold counters + group maxima                           // k_colsum_f64's per-slice partial sums
     bool colsum = true;
     bool bits_fold = true;                  // "bits_fold": bit-length words folded in the quantize launch                     // "colsum": that path (else k_matvec_values on the cells)
-    bool prod_first = false;                // "prod_first": the first stages wait for the products
+    int prod_first = 0;                     // "prod_first": the first stages wait for the products
+                                            // (1), the bounds but not u.d (2, products on the cell stream)
     // second stream: GEMMs overlap the HBM-bound stages; third: phase 1
     hipStream_t st2 = nullptr;
     bool st2_hi = false;                    // st2 is the high-priority stream
@@ -566,7 +573,7 @@ struct svdw_ctx {
     DBuf eq_cp, eq_ks, eq_reg, eq_w, eq_k, eq_err, eq_st;
 };
 
-static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter = nullptr);
+static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter = nullptr, hipEvent_t then_wait = nullptr);
 // debug logs (read once: getenv scans the environment)
 static bool env_flag(const char* name) { const char* v = getenv(name); return v && *v && *v != '0'; }
 static const bool g_batch_log = env_flag("SVDW_BATCH_LOG");
@@ -835,6 +842,27 @@ static DView view_of(svdw_ctx* c, const svdw_mat& m) {
     v.mode = VIEW_STRIDED;
     return v;
 }
+// A launch's view of loaded cells whose f64 source is registered for this call
+// (f64reg): the same elements read from the f64 input and quantized in the
+// kernel (VIEW_F64), so the launch does not wait for k_quantize_multi. The
+// checker's copies of the views (note_gates) stay cell views.
+static DView f64_view(const svdw_ctx* c, const DView& v) {
+    if (!c->f64_views || c->f64reg.empty() || v.mode != VIEW_STRIDED || !v.ptr || !v.rows || !v.cols) return v;
+    for (const auto& r : c->f64reg) {
+        const Fr* base = c->ph[r.phase].adv + r.off;
+        const int64_t o = v.ptr - base;
+        const int64_t er = (int64_t)(v.rows - 1) * v.rs, ec = (int64_t)(v.cols - 1) * v.cs;
+        const int64_t lo = o + std::min<int64_t>(er, 0) + std::min<int64_t>(ec, 0),
+                      hi = o + std::max<int64_t>(er, 0) + std::max<int64_t>(ec, 0);
+        if (lo < 0 || hi >= (int64_t)r.n) continue;
+        DView f = v;
+        f.ptr = reinterpret_cast<const Fr*>(r.x + o);
+        f.mode = VIEW_F64;
+        f._r0 = (uint8_t)c->P;
+        return f;
+    }
+    return v;
+}
 static svdw_mat mat_of_vec(const svdw_vec& v) {   // len x 1 column
     return svdw_mat{v.phase, v.len, 1, v.off, v.stride, 0};
 }
@@ -855,7 +883,7 @@ static void check_vec(const svdw_ctx* c, const svdw_vec& v) { check_mat(c, mat_o
 // Launch a stage whose cells were appended at (off, loff) earlier.
 static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, uint32_t cols,
                          uint64_t off, uint64_t loff, const char* tag) {
-    StageArgs& a = pb.a;
+    StageArgs a = pb.a;
     uint32_t eb = 0, ee = nelem;
     if (sharded(c) && nelem) {
         const uint64_t cw = cols ? cols : 1, R = nelem / cw;
@@ -875,6 +903,7 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     if (c->dry || ee <= eb) return;
     a.out_adv = cellp(c, phase, off);
     a.out_lk = a.L ? c->ph[phase].lk + loff : nullptr;
+    for (int k = 0; k < kMaxViews; ++k) a.view[k] = f64_view(c, a.view[k]);
     a.e_begin = eb;
     a.e_end = ee;
     a.cols = cols ? cols : 1;
@@ -938,7 +967,8 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
 // waiter: after the group holding the latest stage, `waiter` waits for s there
 // (it needs that stage and what came before on s, not the later groups: those
 // hold stages queued earlier that depend on other pending ones).
-static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter) {
+// then_wait: s waits for this event before the groups after that point.
+static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter, hipEvent_t then_wait) {
     for (auto& b : c->batches) {
         if (b.st != s || b.groups.empty()) continue;
         std::vector<std::vector<svdw_ctx::Pending>> groups;
@@ -946,7 +976,11 @@ static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter) {
         const size_t upto = b.last;
         for (size_t gi = 0; gi < groups.size(); ++gi) {
             const auto& grp = groups[gi];
-            if (gi == upto + 1 && waiter) { stream_dep(c, s, waiter); waiter = nullptr; }
+            if (gi == upto + 1 && waiter) {
+                stream_dep(c, s, waiter);
+                waiter = nullptr;
+                if (then_wait) hipck(hipStreamWaitEvent(s, then_wait, 0), "hipStreamWaitEvent");
+            }
             if (grp.empty()) continue;
             std::vector<const StageArgs*> ps;
             double bytes = 0;
@@ -1881,7 +1915,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         if (sharded(c)) shard_rows(c, a.rows, &r0, &r1);
         S.ms[S.sb.njobs] = a;
         ScanJob& j = S.sb.job[S.sb.njobs++];
-        j = ScanJob{view_of(c, a), wc, tab, tl, cellp(c, phase, base + r0 * rowc),
+        j = ScanJob{f64_view(c, view_of(c, a)), wc, tab, tl, cellp(c, phase, base + r0 * rowc),
                     a.cols, (uint32_t)(r1 - r0), 0, (uint32_t)r0, job_spec(c, a)};
         S.bytes += 32.0 * (r1 - r0) * (4.0 * a.cols + 1) + 64.0 * a.cols;
         S.ops += (double)(r1 - r0) * a.cols;
@@ -1980,8 +2014,8 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
             if (src[i] != i) { slot[i] = slot[src[i]]; continue; }
             const svdw_mat b = vm[i].b;
             ensure_buf(c, c->bvfull[nv], (size_t)b.rows * sizeof(Fr));
-            vb.job[nv] = ScanJob{view_of(c, b), nullptr, gtab, c->gp_len, (Fr*)c->bvfull[nv].p, b.cols, b.rows,
-                                 0, 0, job_spec(c, b)};
+            vb.job[nv] = ScanJob{f64_view(c, view_of(c, b)), nullptr, gtab, c->gp_len, (Fr*)c->bvfull[nv].p,
+                                 b.cols, b.rows, 0, 0, job_spec(c, b)};
             vms[nv] = b;
             slot[i] = nv++;
         }
@@ -2300,7 +2334,11 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
             Swap(svdw_ctx* cc, bool o) : c(cc), on(o) { if (on) std::swap(c->st, c->st2); }
             ~Swap() { if (on) std::swap(c->st, c->st2); }
         } sw(c, c->d_checks_aside && c->overlap && known_bits && !c->dry && c->bits_pending);
-        if (sw.on) hipck(hipStreamWaitEvent(c->st, c->ev_bits, 0), "hipStreamWaitEvent");  // d loaded
+        // d loaded -- unless every load these stages (and the bounds and u.d
+        // queued behind them with the products on the cell stream) read comes
+        // from the registered f64 inputs (f64_view): then st2 starts at once
+        const bool from_f64 = c->f64_views && !c->f64reg.empty() && c->prod_on_cell;
+        if (sw.on && !from_f64) hipck(hipStreamWaitEvent(c->st, c->ev_bits, 0), "hipStreamWaitEvent");
         BatchScope bs(c);                   // (desc_order_range reads desc_order_sub: two launches)
         entries_less_than(c, d, max_bits);
         entries_in_desc_order(c, d, max_bits);
@@ -2343,7 +2381,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     const bool pc = c->prod_on_cell && c->prelaunched;
     // prod_first: the bounds and u.d wait for the products (which then run with
     // the chip to themselves instead of beside the first stage launch)
-    if (c->prod_first && c->prelaunched && !c->gemm_done.empty() && !c->dry)
+    if (c->prod_first == 1 && c->prelaunched && !c->gemm_done.empty() && !c->dry)
         hipck(hipStreamWaitEvent(pc ? c->st2 : c->st, c->gemm_done.back(), 0), "hipStreamWaitEvent");
     if (pc) std::swap(c->st, c->st2);
     BatchScope bs(c);
@@ -2381,7 +2419,9 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         std::swap(c->st, c->st2);
         // the cell stream waits for u.d (and what precedes it on st2), not for
         // the d checks' dependent second group batched behind it
-        flush_batch(c, c->st2, c->st);
+        // prod_first 2: the bounds and d checks wait for the products, u.d not
+        flush_batch(c, c->st2, c->st,
+                    c->prod_first == 2 && !c->gemm_done.empty() ? c->gemm_done.back() : nullptr);
     }
     if (batched) {
         host_mark(c, "bounds(u), bounds(v), u.d queued");
@@ -2553,8 +2593,10 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         if (p1_overlap && p1mode == 2 && !c->st3)   // created on first use
             hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
         hipStream_t p1s = p1mode == 2 ? c->st3 : c->st2;
-        if (p1_overlap && p1s == c->st3) {
-            hipck(hipStreamWaitEvent(c->st3, c->ev_bits, 0), "hipStreamWaitEvent");
+        // phase 1 beside the products (st3, or st2 while the products run on the
+        // cell stream): it waits for the loads, and its c_s scans for the products
+        if (p1_overlap && (p1s == c->st3 || c->prod_on_cell)) {
+            hipck(hipStreamWaitEvent(p1s, c->ev_bits, 0), "hipStreamWaitEvent");
             c->wait_before_cs = c->gemm_done;
         }
         {
@@ -2580,11 +2622,14 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         ~F64() {
             c->svd_f64[0] = c->svd_f64[1] = c->svd_f64[2] = nullptr;
             c->f64src.clear();
+            c->f64reg.clear();
         }
     } f64clr{c};
     if (on_device && !c->dry) {
         c->svd_f64[0] = m; c->svd_f64[1] = u; c->svd_f64[2] = v;
         c->f64src = {{zu, u}, {zv, v}};
+        c->f64reg = {{zm.phase, zm.off, (uint64_t)N * M, m}, {zu.phase, zu.off, (uint64_t)N * N, u},
+                     {zv.phase, zv.off, (uint64_t)M * M, v}, {zdm.phase, zdm.off, (uint64_t)r, d}};
     }
     svdw_svd_payload pl =
         check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits, dbits, true);
@@ -2677,6 +2722,12 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
         c->dwords = {{za, 0}, {zb, 1}};
     }
     host_mark(c, "quantize queued");
+    struct RegClear {
+        svdw_ctx* c;
+        ~RegClear() { c->f64reg.clear(); }
+    } regclr{c};
+    if (on_device && !c->dry)
+        c->f64reg = {{za.phase, za.off, (uint64_t)N * K, a}, {zb.phase, zb.off, (uint64_t)K * M, b}};
     // c_s = a * b (honest_prover_mat_mul's cells), the CRT GEMM sized on the device
     uint64_t off;
     append(c, 0, (uint64_t)N * M, 0, &off, nullptr, "product", N);
@@ -3927,6 +3978,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_crt = (int)value;
         } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
             c->stage_batch = value != 0;
+        } else if (n == "f64_views") {
+            c->f64_views = value != 0;
         } else if (n == "bits_fold") {
             c->bits_fold = value != 0;
         } else if (n == "res_first") {
@@ -3949,7 +4002,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "colsum") {                 // row-sharded b.g from the f64 inputs
             c->colsum = value != 0;
         } else if (n == "prod_first") {
-            c->prod_first = value != 0;
+            REQUIRE(value >= 0 && value <= 2, "prod_first: 0, 1 or 2");
+            c->prod_first = (int)value;
         } else {
             fail(SVDW_EINVAL, "unknown option " + n);
         }

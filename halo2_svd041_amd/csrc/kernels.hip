@@ -41,9 +41,35 @@ __device__ __forceinline__ void st_fr_nt(Fr* p, const Fr& v) {
     __builtin_nontemporal_store(v4u{v.w[0], v.w[1], v.w[2], v.w[3]}, q);
     __builtin_nontemporal_store(v4u{v.w[4], v.w[5], v.w[6], v.w[7]}, q + 1);
 }
+// ZkMatrix::new's quantization of one f64 (quantize_body's arithmetic):
+// x_q = round_half_away(|x| 2^P) as u128 (saturating, NaN -> 0), sign(x) < 0
+// (incl. -0.0) -> p - x_q.
+__device__ __forceinline__ Fr quantize_fr(double x, double scale) {
+    const bool neg = signbit(x) && !isnan(x);
+    const double s = round(fabs(x) * scale);
+    Fr q = fr_zero();
+    if (s >= 340282366920938463463374607431768211456.0) {
+        q.w[0] = q.w[1] = q.w[2] = q.w[3] = 0xffffffffu;
+    } else if (s > 0.0) {
+        const uint64_t bits = __double_as_longlong(s);
+        const int e = (int)((bits >> 52) & 0x7ff) - 1075;
+        const uint64_t mant = (bits & 0xfffffffffffffull) | (1ull << 52);
+        const unsigned __int128 v = e >= 0 ? ((unsigned __int128)mant << e) : (unsigned __int128)(mant >> -e);
+        q.w[0] = (uint32_t)v; q.w[1] = (uint32_t)(v >> 32);
+        q.w[2] = (uint32_t)(v >> 64); q.w[3] = (uint32_t)(v >> 96);
+    }
+    return neg ? fr_sub(fr_zero(), q) : q;
+}
+__device__ __forceinline__ double f64_scale(const DView& v) { return ldexp(1.0, (int)v._r0); }
 // X(i, j) of a view; `pad` is the value outside the view (K[v.pad_k]).
 __device__ __forceinline__ Fr view_load(const DView v, const Fr pad, uint32_t i, uint32_t j) {
     if (v.mode == VIEW_DIAG) return (i == j) ? ld_fr(v.ptr) : pad;
+    if (v.mode == VIEW_F64) {
+        if (i < v.rows && j < v.cols)
+            return quantize_fr(reinterpret_cast<const double*>(v.ptr)[(int64_t)i * v.rs + (int64_t)j * v.cs],
+                               f64_scale(v));
+        return pad;
+    }
     if (i < v.rows && j < v.cols) return ld_fr(v.ptr + (int64_t)i * v.rs + (int64_t)j * v.cs);
     return pad;
 }
@@ -167,21 +193,7 @@ __device__ __forceinline__ void quantize_body(const double* __restrict__ in, uin
             const uint32_t r = (uint32_t)(i / keep.cols), cc = (uint32_t)(i - (uint64_t)r * keep.cols);
             if (!((r >= keep.rlo && r < keep.rhi) || (cc >= keep.clo && cc < keep.chi))) continue;
         }
-        const double x = xv[k];
-        const bool neg = signbit(x) && !isnan(x);
-        const double s = round(fabs(x) * scale);
-        Fr q = fr_zero();
-        if (s >= 340282366920938463463374607431768211456.0) {
-            q.w[0] = q.w[1] = q.w[2] = q.w[3] = 0xffffffffu;
-        } else if (s > 0.0) {
-            const uint64_t bits = __double_as_longlong(s);
-            const int e = (int)((bits >> 52) & 0x7ff) - 1075;
-            const uint64_t mant = (bits & 0xfffffffffffffull) | (1ull << 52);
-            const unsigned __int128 v = e >= 0 ? ((unsigned __int128)mant << e) : (unsigned __int128)(mant >> -e);
-            q.w[0] = (uint32_t)v; q.w[1] = (uint32_t)(v >> 32);
-            q.w[2] = (uint32_t)(v >> 64); q.w[3] = (uint32_t)(v >> 96);
-        }
-        st_fr_nt(out + i, neg ? fr_sub(fr_zero(), q) : q);
+        st_fr_nt(out + i, quantize_fr(xv[k], scale));
     }
     if (blockmax && fold.wout && gblk < fold.nblk) bits_fold(fold, gblk, bmax);
 }
@@ -630,10 +642,18 @@ __device__ __forceinline__ Prefetch stage_loads(const StageArgs& a, uint32_t blk
         if (v0.ptr && v0.mode == VIEW_STRIDED && pi < v0.rows && pj < v0.cols) {
             f.v0 = ld_fr(v0.ptr + (int64_t)pi * v0.rs + (int64_t)pj * v0.cs);
             f.in0 = true;
+        } else if (v0.ptr && v0.mode == VIEW_F64 && pi < v0.rows && pj < v0.cols) {
+            f.v0 = quantize_fr(reinterpret_cast<const double*>(v0.ptr)[(int64_t)pi * v0.rs + (int64_t)pj * v0.cs],
+                               f64_scale(v0));
+            f.in0 = true;
         }
         const DView& v1 = a.view[1];
         if (v1.ptr && v1.mode == VIEW_STRIDED && pi < v1.rows && pj < v1.cols) {
             f.v1 = ld_fr(v1.ptr + (int64_t)pi * v1.rs + (int64_t)pj * v1.cs);
+            f.in1 = true;
+        } else if (v1.ptr && v1.mode == VIEW_F64 && pi < v1.rows && pj < v1.cols) {
+            f.v1 = quantize_fr(reinterpret_cast<const double*>(v1.ptr)[(int64_t)pi * v1.rs + (int64_t)pj * v1.cs],
+                               f64_scale(v1));
             f.in1 = true;
         }
     }

@@ -27,7 +27,10 @@ namespace svdw {
 // (check_mat_id's implicit scalar_id * Id matrix, src/matrix/mod.rs:461-483).
 // mode DIAGK: X(i,j) = i==j ? K[diag_k] : K[pad_k] (the same matrix when the
 // diagonal scalar is a constant the host knows: no read of its cell).
-enum : uint32_t { VIEW_STRIDED = 0, VIEW_DIAG = 1, VIEW_DIAGK = 2 };
+// VIEW_F64: ptr is a row-major f64 input (svd_witness / verify_mul_witness
+// device inputs) laid out like the loaded cells; element (i, j) is its
+// ZkMatrix::new quantization at PRECISION_BITS = _r0, computed in registers.
+enum : uint32_t { VIEW_STRIDED = 0, VIEW_DIAG = 1, VIEW_DIAGK = 2, VIEW_F64 = 3 };
 struct DView {
     const Fr* ptr;
     int64_t rs, cs;

@@ -262,6 +262,9 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   in HBM);
  *   "stage_elems" 256 (elements per stage block, multiple of 16 in [16, 256]);
  *   "stage_align" 1 | 0 (each block's store windows aligned to 4 KiB);
+ *   "f64_views" 1 | 0 (svd_witness / verify_mul_witness with device inputs:
+ *   stages and row scans read the loaded matrices from the f64 inputs,
+ *   quantized in registers, instead of waiting for the quantized cells);
  *   "bits_fold" 1 | 0 (the operand bit-length words folded inside the quantize
  *   launch, or by k_bits_reduce, a launch of its own);
  *   "colsum" 1 | 0 (row-sharded svd_witness: every entry of the Freivalds

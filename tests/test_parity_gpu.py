@@ -347,20 +347,24 @@ def _on_device(*xs):
     return [torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev) for x in xs]
 
 
+@pytest.mark.parametrize("f64v", [1, 0])
 @pytest.mark.parametrize("res", [1, 0])
 @pytest.mark.parametrize("fused", [1, 0])
 @pytest.mark.parametrize("N,M,P", [(130, 97, 63), (64, 200, 32)])
-def test_device_inputs_parity(gpu_ctx_factory, fused, res, N, M, P):
+def test_device_inputs_parity(gpu_ctx_factory, fused, res, f64v, N, M, P):
     """The bench path: m, u, v, d already resident in HBM (torch float64 CUDA
     tensors), quantized in one fused launch (or four); the CRT residue planes of
     m, u, v built from the f64 inputs in one launch (res 1) or from the
-    quantized cells (res 0); witness vs the oracle."""
+    quantized cells (res 0); the stages and row scans reading the loaded
+    matrices through f64 views (f64v 1: quantized in registers, no wait for the
+    cells) or the cells; witness vs the oracle."""
     import halo2_svd041_amd as hs
     m, u, d, v = gen_svd_input(N, M, seed=N * M)
     g = gamma_for(N + M)
     ctx = gpu_ctx_factory(P)
     ctx.set_option("fused_quantize", fused)
     ctx.set_option("res_f64", res)
+    ctx.set_option("f64_views", f64v)
     dm, du, dv, dd = _on_device(m, u, v, d)
     hs.svd_witness(ctx, dm, du, dv, dd, g)
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
@@ -450,21 +454,34 @@ def test_products_on_cell_stream_parity(gpu_ctx_factory, world, opts):
         assert bad.size == 0, f"{key}: {bad.size} cells differ, first at {bad[:8]}"
 
 
-@pytest.mark.parametrize("N,M,P,row_lim,device", [(1024, 1024, 63, 64, False), (512, 512, 32, 128, False),
-                                                  (2048, 1024, 32, 24, False), (1024, 1024, 63, 32, True)])
-def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device):
+@pytest.mark.parametrize("N,M,P,row_lim,device,hold", [(1024, 1024, 63, 64, False, 0), (512, 512, 32, 128, False, 0),
+                                                       (2048, 1024, 32, 24, False, 0), (1024, 1024, 63, 32, True, 0),
+                                                       (1024, 1024, 63, 32, True, 3000)])
+def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device, hold):
     """BASELINE config sizes (1024^2 P=63 = the bench workload, 512^2 P=32,
     2048x1024 P=32): the GPU computes the whole witness; the C oracle computes
     the first row_lim rows of every row-parallel region and all other regions
     in full. Walking the engine's layout table (svdw_layout), every cell the
     oracle computed must equal the GPU's cell at its full-witness offset: the
     loads, d checks and gamma powers entirely, the first row_lim rows of every
-    bound / product / diff / scan / is_equal region."""
+    bound / product / diff / scan / is_equal region. hold: every stream of the
+    witness waits behind a spinning kernel until the host has queued all of it,
+    so a launch missing a cross-stream dependency runs ahead (the c_s scans
+    beside products on another stream) and reads unwritten cells."""
     import halo2_svd041_amd as hs
     from conftest import walk_window
     m, u, d, v = gen_svd_input(N, M, seed=N + M + P)
     g = gamma_for(N * M)
     ctx = gpu_ctx_factory(P)
+    if hold:
+        # a first witness of other inputs allocates every buffer (allocation
+        # synchronises), so the witness below runs fully queued behind the hold;
+        # a launch that ran ahead would read the first witness's cells
+        m2, u2, d2, v2 = gen_svd_input(N, M, seed=N + M + P + 1)
+        hs.svd_witness(ctx, *_on_device(m2, u2, v2, d2), gamma_for(N * M + 1))
+        ctx.sync()
+        ctx.reset()
+        ctx.set_option("hold_us", hold)
     if device:                                    # the bench path (inputs resident in HBM)
         hs.svd_witness(ctx, *_on_device(m, u, v, d), g)
     else:
