@@ -470,6 +470,13 @@ struct svdw_ctx {
                                             // critical path sharded, and unsharded it measured
                                             // 2.5 % faster at 1024^2 and 2048^2, neutral at 512^2
     bool prod_on_cell = false;              // this witness's products went on the cell stream
+    int prod_blocks = 1;                    // "prod_blocks": unsharded products in K row blocks on
+                                            // st3, the diff + ids launched per block as each lands
+    int prod_blk = 1;                       // this witness's block count (1: one batch)
+    bool bounds_after = true;               // "bounds_after": with row blocks, the u / v bounds
+                                            // wait for the first block's products
+    std::vector<hipEvent_t> blk_ev;         // block k's products complete (st3)
+    std::vector<uint32_t> blk_n, blk_m;     // block row bounds (K + 1) of N-row / M-row products
     uint32_t hold_us = 0;                   // "hold_us": timing aid, st spins this long first
     Fr ext_gamma{};                          // init_rand of the last verify_mul (equality source 2)
     uint64_t ext_off = 0;                    // its cell in the RLC context
@@ -999,6 +1006,51 @@ static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter, hipEvent
         }
     }
     if (waiter) stream_dep(c, s, waiter);
+}
+// The batch of stream s (the diff and ids behind row-blocked products) issued
+// block by block: before block k the stream waits for blk_ev[k], and every
+// pending stage runs only its elements in block k's rows (stages over N or M
+// rows; any other stage runs whole in the last block).
+static void flush_batch_blocks(svdw_ctx* c, hipStream_t s) {
+    const int K = c->prod_blk;
+    for (auto& b : c->batches) {
+        if (b.st != s || b.groups.empty()) continue;
+        std::vector<std::vector<svdw_ctx::Pending>> groups;
+        groups.swap(b.groups);
+        const uint32_t N = c->blk_n[K], M = c->blk_m[K];
+        for (int k = 0; k < K; ++k) {
+            hipck(hipStreamWaitEvent(s, c->blk_ev[k], 0), "hipStreamWaitEvent");
+            for (const auto& grp : groups) {
+                std::vector<StageArgs> parts;
+                parts.reserve(grp.size());
+                double bytes = 0;
+                for (const auto& q : grp) {
+                    StageArgs a = q.a;
+                    const uint32_t cols = a.cols ? a.cols : 1, R = a.e_end / cols;
+                    uint32_t r0, r1;
+                    if (R == N && a.e_end % cols == 0) {
+                        r0 = c->blk_n[k]; r1 = c->blk_n[k + 1];
+                    } else if (R == M && a.e_end % cols == 0) {
+                        r0 = c->blk_m[k]; r1 = c->blk_m[k + 1];
+                    } else {
+                        r0 = k == K - 1 ? 0 : R; r1 = k == K - 1 ? R + 1 : R;
+                    }
+                    const uint32_t e0 = std::max<uint64_t>(a.e_begin, (uint64_t)r0 * cols),
+                                   e1 = (uint32_t)std::min<uint64_t>(a.e_end, (uint64_t)r1 * cols);
+                    if (e1 <= e0) continue;
+                    a.e_begin = e0;
+                    a.e_end = e1;
+                    parts.push_back(a);
+                    bytes += q.bytes * (double)(e1 - e0) / std::max<uint32_t>(q.a.e_end - q.a.e_begin, 1);
+                }
+                if (parts.empty()) continue;
+                std::vector<const StageArgs*> ps;
+                for (const auto& a : parts) ps.push_back(&a);
+                ProfScope pr(c, s, "k_stage:multi", bytes, 0, true);
+                hipck(launch_stage_multi(ps.data(), (int)ps.size(), s), "k_stage_multi");
+            }
+        }
+    }
 }
 // RAII: stage launches on the current stream between construction and end()
 // are batched (k_stage_multi); nested scopes on the same stream join the outer
@@ -2186,6 +2238,59 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
             roff += rbytes[g];
         }
         c->gemm_batched = true;
+        if (c->prod_blk > 1) {
+            // K row blocks of all three products, in order on pst: block k's rows
+            // of m.v^T, and the upper tiles of the tile rows of u.u^T / v.v^T in
+            // block k (their mirrors land in later blocks' rows, written before
+            // those blocks' events); the diff + ids of a block start as its event
+            // fires instead of after all products
+            const int K = c->prod_blk;
+            c->blk_ev.clear();
+            c->blk_n.assign(K + 1, 0);
+            c->blk_m.assign(K + 1, 0);
+            for (int k = 1; k < K; ++k) {
+                c->blk_n[k] = std::min(N, ceil_to((uint32_t)((uint64_t)N * k / K), 128));
+                c->blk_m[k] = std::min(M, ceil_to((uint32_t)((uint64_t)M * k / K), 128));
+            }
+            c->blk_n[K] = N;
+            c->blk_m[K] = M;
+            auto start = [](uint32_t bt, uint32_t T) { return bt * T - bt * (bt - 1) / 2; };
+            hipEvent_t last = nullptr;
+            for (int k = 0; k < K; ++k) {
+                CrtBatch bk = b;
+                bk.njobs = 0;
+                for (uint32_t jj = 0; jj < b.njobs; ++jj) {
+                    CrtJob q = b.job[jj];
+                    const int g = jj;                        // unsharded: all three jobs present
+                    const std::vector<uint32_t>& bd = g == 2 ? c->blk_m : c->blk_n;
+                    const uint32_t r0 = bd[k], r1 = bd[k + 1];
+                    if (r1 <= r0) continue;
+                    if (!q.sym) {
+                        q.Ar += (uint64_t)r0 * q.kpad;
+                        q.out += (uint64_t)r0 * q.ors;
+                        q.N = r1 - r0;
+                    } else {
+                        const uint32_t T = (q.N + CT_TILE - 1) / CT_TILE, b0 = r0 / CT_TILE,
+                                       b1 = (r1 + CT_TILE - 1) / CT_TILE;
+                        q.tile0 = start(b0, T);
+                        q.tcount = start(b1, T) - q.tile0;
+                    }
+                    bk.job[bk.njobs++] = q;
+                }
+                if (bk.njobs) {
+                    ProfScope ps(c, pst, "k_gemm_crt:multi", bytes / K, ops / K);
+                    hipck(launch_gemm_crt_multi(bk, pst), "k_gemm_crt_multi");
+                }
+                last = stream_dep(c, pst, nullptr);
+                c->blk_ev.push_back(last);
+            }
+            // the cell stream waits per block (flush_batch_blocks), not here
+            for (int g = 0; g < 3; ++g) {
+                c->pre.push_back({log[g], last, c->st});
+                c->gemm_done.push_back(last);
+            }
+            return;
+        }
         if (b.njobs) {
             ProfScope ps(c, pst, "k_gemm_crt:multi", bytes, ops);
             hipck(launch_gemm_crt_multi(b, pst), "k_gemm_crt_multi");
@@ -2273,6 +2378,16 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         // products on the cell stream (prod_cell): already behind the loads there
         c->prod_on_cell = from_f64 && c->prelaunch_at == 0 && c->d_checks_aside && c->bits_pending &&
                           (c->prod_cell > 0 || (c->prod_cell < 0 && sharded(c)));
+        // row blocks: unsharded, batched, products beside the cell stream on st3
+        c->prod_blk = c->prod_on_cell && !sharded(c) && c->gemm_batch > 0 && c->prod_blocks > 1
+                          ? std::min<int>(c->prod_blocks, (int)((std::min(N, M) + 127) / 128))
+                          : 1;
+        hipStream_t pst = c->prod_on_cell ? c->st : c->st2;
+        if (c->prod_blk > 1) {
+            if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
+            pst = c->st3;
+            hipck(hipStreamWaitEvent(c->st3, c->ev_bits, 0), "hipStreamWaitEvent");
+        }
         if (c->prod_on_cell) {
         } else if (c->bits_pending) {
             hipck(hipStreamWaitEvent(c->st2, c->ev_bits, 0), "hipStreamWaitEvent");
@@ -2288,7 +2403,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         const unsigned* sa[3] = {sl[0], sl[1], sl[2]};
         const unsigned* sb[3] = {sl[2], sl[1], sl[2]};
         if (from_f64) {
-            prelaunch_products_f64(c, A, B, log, m.phase, dev_bits, c->prod_on_cell ? c->st : c->st2);
+            prelaunch_products_f64(c, A, B, log, m.phase, dev_bits, pst);
             c->prelaunched = true;
             host_mark(c, "products queued");
             return;
@@ -2419,9 +2534,13 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         std::swap(c->st, c->st2);
         // the cell stream waits for u.d (and what precedes it on st2), not for
         // the d checks' dependent second group batched behind it
-        // prod_first 2: the bounds and d checks wait for the products, u.d not
-        flush_batch(c, c->st2, c->st,
-                    c->prod_first == 2 && !c->gemm_done.empty() ? c->gemm_done.back() : nullptr);
+        // prod_first 2: the bounds and d checks wait for the products, u.d not;
+        // row-blocked products: they wait for the first block, which then has
+        // the chip to itself (beside u.d) and the diff + ids start early
+        hipEvent_t hold_bounds = nullptr;
+        if (c->prod_first == 2 && !c->gemm_done.empty()) hold_bounds = c->gemm_done.back();
+        else if (c->prod_blk > 1 && !c->blk_ev.empty() && c->bounds_after) hold_bounds = c->blk_ev.front();
+        flush_batch(c, c->st2, c->st, hold_bounds);
     }
     if (batched) {
         host_mark(c, "bounds(u), bounds(v), u.d queued");
@@ -2436,6 +2555,10 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     // products batched (one completion point): diff and the two ids in one launch
     BatchScope bs2(c);
     if (!c->gemm_batched) bs2.close();
+    // row-blocked products: the batch goes out block by block (flush_batch_blocks);
+    // launches outside it wait for all products
+    const bool blocked = c->prod_blk > 1 && !c->dry;
+    if (blocked && !bs2.mine) hipck(hipStreamWaitEvent(c->st, c->blk_ev.back(), 0), "hipStreamWaitEvent");
     svdw_mat mvt = honest_prover_mat_mul(c, m.phase, m, vt, bm, bv);
     BigU es = scale_err(err_svd, P), eu = scale_err(err_u, P);
     host_mark(c, "u.d queued");
@@ -2448,7 +2571,12 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     check_mat_id(c, uut, q2, eu, &qq);
     svdw_mat vvt = honest_prover_mat_mul(c, m.phase, v, vt, bv, bv);
     check_mat_id(c, vvt, q2, eu, &qq);
-    bs2.end();
+    if (blocked && bs2.mine) {
+        flush_batch_blocks(c, c->st);
+        bs2.close();
+    } else {
+        bs2.end();
+    }
     aside.end();
     host_mark(c, "ids queued");
     return svdw_svd_payload{ut, vt, mvt, uut, vvt};
@@ -2472,6 +2600,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     if (!c->dry) apply_gemm_prio(c, N, M);
     c->prelaunched = false;
     c->prod_on_cell = false;
+    c->prod_blk = 1;
     c->gemm_batched = false;
     c->gemm_done.clear();
     c->wait_before_cs.clear();
@@ -2510,6 +2639,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         hipck(launch_hold(c->hold_us, c->st), "k_hold");
         if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
         stream_dep(c, c->st, c->st3);
+        stream_dep(c, c->st, c->st2);  // (st2's first stages need no load with f64 views)
     }
     if (!c->dry) {
         // gamma^j depends on gamma only: queue it first, on its own stream, so it
@@ -2663,6 +2793,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     c->dep_next = 0;
     c->prelaunched = false;
     c->prod_on_cell = false;
+    c->prod_blk = 1;
     c->gemm_batched = false;
     c->gemm_done.clear();
     c->wait_before_cs.clear();
@@ -3978,6 +4109,11 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_crt = (int)value;
         } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
             c->stage_batch = value != 0;
+        } else if (n == "bounds_after") {
+            c->bounds_after = value != 0;
+        } else if (n == "prod_blocks") {
+            REQUIRE(value >= 1 && value <= 64, "prod_blocks: 1..64");
+            c->prod_blocks = (int)value;
         } else if (n == "f64_views") {
             c->f64_views = value != 0;
         } else if (n == "bits_fold") {

@@ -1495,7 +1495,7 @@ __device__ __forceinline__ void static_for_impl(F&& f) {
 template <int N, class F>
 __device__ __forceinline__ void static_for(F&& f) { static_for_impl<0, N>(f); }
 
-static constexpr int CT = 128;     // CRT GEMM block tile (4 waves of 64 x 64)
+static constexpr int CT = CT_TILE;     // CRT GEMM block tile (4 waves of 64 x 64)
 // Staged operand rows are 64 B (one k-chunk) with the four 16 B parts XOR-swizzled
 // by (row >> 2) & 3: the staging stores (4 rows x 4 parts per 16 lanes) and the
 // fragment reads (16 rows x 1 part) both land on 16 distinct 4-bank groups.
@@ -1662,6 +1662,19 @@ __device__ __forceinline__ void trace_block(uint64_t t0, uint64_t t1, uint64_t t
 }
 
 
+// tile t of a job (t < nblk; the sequence starts at tile0) -> its (row,
+// column) tile (SYM: upper tiles row by row)
+__device__ __forceinline__ void crt_tile_rc(const CrtJob& q, uint32_t t, uint32_t* bi, uint32_t* bj) {
+    t += q.tile0;
+    if (q.sym) {
+        uint32_t r = 0, rest = t, rowlen = q.tiles_a;
+        while (rest >= rowlen) { rest -= rowlen; ++r; --rowlen; }
+        *bi = r; *bj = r + rest;
+    } else {
+        *bi = t / q.tiles_m;
+        *bj = t - *bi * q.tiles_m;
+    }
+}
 // The products of a CrtBatch in one launch, placed modulus-major per XCD: the
 // work units (job, modulus < the job's device-decided count n, tile) are laid
 // out job-major, modulus-major, and XCD x (blocks x, x + 8, ... on gfx950) takes
@@ -1691,14 +1704,7 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
     const CrtJob& q = b.job[j];
     const uint32_t mod = u / q.nblk, t = u - mod * q.nblk;
     uint32_t bi, bj;
-    if (q.sym) {                                       // upper tiles, row by row
-        uint32_t r = 0, rest = t, rowlen = q.tiles_a;
-        while (rest >= rowlen) { rest -= rowlen; ++r; --rowlen; }
-        bi = r; bj = r + rest;
-    } else {
-        bi = t / q.tiles_m;
-        bj = t - bi * q.tiles_m;
-    }
+    crt_tile_rc(q, t, &bi, &bj);
     uint64_t tp1 = 0, tp2 = 0;
     crt_gemm_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.nblk, t,
                   q.R, bi, bj, (int)mod, S, tp1, tp2);
@@ -1713,17 +1719,6 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
 // keeps it exact), accumulated carry-free in 16-bit limbs, one 9-word
 // reduction. SYM: elements j >= i of the upper tiles (the GEMM computed upper
 // and diagonal 128-tiles), each also stored at (j, i).
-// tile t of a job -> its (row, column) tile (SYM: upper tiles row by row)
-__device__ __forceinline__ void crt_tile_rc(const CrtJob& q, uint32_t t, uint32_t* bi, uint32_t* bj) {
-    if (q.sym) {
-        uint32_t r = 0, rest = t, rowlen = q.tiles_a;
-        while (rest >= rowlen) { rest -= rowlen; ++r; --rowlen; }
-        *bi = r; *bj = r + rest;
-    } else {
-        *bi = t / q.tiles_m;
-        *bj = t - *bi * q.tiles_m;
-    }
-}
 __device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t cblk) {
     const int n = crt_nmod(*q.bits_a, *q.bits_b, q.lk);
     if (!n) return;
@@ -1801,6 +1796,12 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
             return hipErrorInvalidValue;
         if (q.sym && q.N != q.M) return hipErrorInvalidValue;
         q.nblk = q.sym ? q.tiles_a * (q.tiles_a + 1) / 2 : q.tiles_a * q.tiles_m;
+        if (q.tcount) {
+            if (q.tile0 + q.tcount > q.nblk) return hipErrorInvalidValue;
+            q.nblk = q.tcount;
+        } else if (q.tile0) {
+            return hipErrorInvalidValue;
+        }
         units += kCrtMaxMod * q.nblk;                    // upper bound: n = kCrtMaxMod
         q.cblk0 = cblocks;
         cblocks += q.nblk * kCombBlocksPerTile;

@@ -319,6 +319,7 @@ static constexpr int kCrtMaxResidues = 40;   // = kCrtMaxMod (crt_tables.hpp)
 // bits_a, bits_b, lk and sym (A == B: upper tiles + mirror); the launcher
 // fills the tile and block fields.
 static constexpr int kMaxCrtJobs = 3;
+static constexpr uint32_t CT_TILE = 128;   // CRT GEMM output tile edge (kernels.hip CT)
 struct CrtJob {
     const uint8_t* Ar;
     const uint8_t* Br;
@@ -329,6 +330,10 @@ struct CrtJob {
     int64_t ors, ocs;
     uint32_t astride, bstride, kpad, N, M, lk, sym;
     uint32_t tiles_a, tiles_m, nblk, cblk0;
+    // tiles [tile0, tile0 + tcount) of the job's tile sequence only (tcount 0:
+    // all): a row block of a product (SYM: the upper tiles of rows of tiles
+    // [b0, b1), whose mirrors land in later rows)
+    uint32_t tile0, tcount;
 };
 struct CrtBatch {
     CrtJob job[kMaxCrtJobs];

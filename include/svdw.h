@@ -262,6 +262,11 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   in HBM);
  *   "stage_elems" 256 (elements per stage block, multiple of 16 in [16, 256]);
  *   "stage_align" 1 | 0 (each block's store windows aligned to 4 KiB);
+ *   "prod_blocks" 1 | K (unsharded svd_witness with device inputs: the three
+ *   products in K row blocks on a side stream, the diff and ids launched per
+ *   block as each block lands; "bounds_after" 1 | 0: the u / v bounds wait
+ *   for the first block. Measured 1024^2 -1 to +4 %, 2048^2 +1 %, 4096^2 -3 %
+ *   against 1: off by default);
  *   "f64_views" 1 | 0 (svd_witness / verify_mul_witness with device inputs:
  *   stages and row scans read the loaded matrices from the f64 inputs,
  *   quantized in registers, instead of waiting for the quantized cells);

@@ -456,7 +456,8 @@ def test_products_on_cell_stream_parity(gpu_ctx_factory, world, opts):
 
 @pytest.mark.parametrize("N,M,P,row_lim,device,hold", [(1024, 1024, 63, 64, False, 0), (512, 512, 32, 128, False, 0),
                                                        (2048, 1024, 32, 24, False, 0), (1024, 1024, 63, 32, True, 0),
-                                                       (1024, 1024, 63, 32, True, 3000)])
+                                                       (1024, 1024, 63, 32, True, 3000),
+                                                       (1024, 1024, 63, 32, True, -3000)])
 def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device, hold):
     """BASELINE config sizes (1024^2 P=63 = the bench workload, 512^2 P=32,
     2048x1024 P=32): the GPU computes the whole witness; the C oracle computes
@@ -473,6 +474,9 @@ def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device, hol
     m, u, d, v = gen_svd_input(N, M, seed=N + M + P)
     g = gamma_for(N * M)
     ctx = gpu_ctx_factory(P)
+    if hold < 0:                                  # (and the products in 4 row blocks)
+        ctx.set_option("prod_blocks", 4)
+        hold = -hold
     if hold:
         # a first witness of other inputs allocates every buffer (allocation
         # synchronises), so the witness below runs fully queued behind the hold;
@@ -622,3 +626,26 @@ def test_field_mat_times_vec_parity(gpu_ctx_factory, N, M, LB, seed):
     f64 = A @ v1
     for i in range(N):
         assert abs(po.to_signed(oq[i].value) / 2.0 ** P - f64[i]) <= 1e-6 * max(1.0, abs(f64[i]))
+
+
+@pytest.mark.parametrize("N,M,P,K", [(256, 200, 63, 2), (300, 260, 32, 3), (260, 300, 63, 8)])
+def test_row_blocked_products_parity(gpu_ctx_factory, N, M, P, K):
+    """prod_blocks: the three products in K row blocks on the third stream (the
+    upper tiles of u.u^T / v.v^T by tile rows, mirrors into later blocks), the
+    diff and ids launched block by block as each block's event fires. A first
+    witness of other inputs allocates everything, then the streams are held
+    until the whole witness is queued, so a block stage that ran ahead of its
+    products would read the first witness's cells."""
+    import halo2_svd041_amd as hs
+    m, u, d, v = gen_svd_input(N, M, seed=N + 7 * M + K)
+    g = gamma_for(N + M + K)
+    ctx = gpu_ctx_factory(P)
+    ctx.set_option("prod_blocks", K)
+    m2, u2, d2, v2 = gen_svd_input(N, M, seed=N + 7 * M + K + 1)
+    hs.svd_witness(ctx, *_on_device(m2, u2, v2, d2), gamma_for(1))
+    ctx.sync()
+    ctx.reset()
+    ctx.set_option("hold_us", 2000)
+    hs.svd_witness(ctx, *_on_device(m, u, v, d), g)
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+    _assert_streams(ctx, a0, l0, a1)
