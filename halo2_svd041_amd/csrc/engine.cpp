@@ -480,6 +480,13 @@ struct svdw_ctx {
     uint32_t hold_us = 0;                   // "hold_us": timing aid, st spins this long first
     Fr ext_gamma{};                          // init_rand of the last verify_mul (equality source 2)
     uint64_t ext_off = 0;                    // its cell in the RLC context
+    // ctx_rlc of the last svd_witness with rlc_prefix: [E(one), E(zero), W(gamma)]
+    // and the phase-1 offsets of the two ctx_gate constants its first cells copy
+    struct RlcTrace {
+        uint32_t n = 0;
+        Fr cells[3];
+        uint64_t src[2];
+    } rlc;
     bool rlc_prefix = false;                 // "rlc_prefix": svd_witness's phase 1 starts with the
                                              // ctx_gate cells of load_rlc_cache(.., 1)
     int p1_at = -1;                         // "p1_at": phase 1 on st3 (mode 2) enqueued after
@@ -2629,10 +2636,17 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     // zero = ctx_gate.load_zero(): two constant cells at the head of ctx_gate (the
     // stream here); [E(one), E(zero), W(gamma)] go to ctx_rlc, whose cell 2 is init_rand.
     c->ext_off = 0;
+    c->rlc.n = 0;
     if (c->rlc_prefix) {
-        put_cell(c, 1, fr_from_u64(1), true);
-        put_cell(c, 1, fr_zero(), true);
+        const svdw_vec one = put_cell(c, 1, fr_from_u64(1), true);
+        const svdw_vec zero = put_cell(c, 1, fr_zero(), true);
         c->ext_off = 2;
+        c->rlc.n = 3;
+        c->rlc.cells[0] = fr_from_u64(1);
+        c->rlc.cells[1] = fr_zero();
+        c->rlc.cells[2] = gamma;
+        c->rlc.src[0] = (uint64_t)one.phase << 62 | one.off;
+        c->rlc.src[1] = (uint64_t)zero.phase << 62 | zero.off;
     }
     c->gp_ev = nullptr;
     if (!c->dry && c->hold_us) {       // every stream of the step waits for st's hold
@@ -4026,6 +4040,19 @@ int svdw_check_equalities(svdw_ctx* c, uint32_t phase, const void* columns0, con
         out->copy_failures = h[1];
         out->consts_checked = h[2];
         out->const_failures = h[3];
+    });
+}
+int svdw_rlc_trace(const svdw_ctx* c, uint64_t* cells, uint64_t* copies, uint32_t* n) {
+    return guarded([&] {
+        REQUIRE(c && n, "null argument");
+        *n = c->rlc.n;
+        if (!c->rlc.n) return;
+        REQUIRE(cells && copies, "null output");
+        for (uint32_t k = 0; k < c->rlc.n; ++k)
+            for (int w = 0; w < 4; ++w)
+                cells[4 * k + w] = (uint64_t)c->rlc.cells[k].w[2 * w] | (uint64_t)c->rlc.cells[k].w[2 * w + 1] << 32;
+        copies[0] = c->rlc.src[0];
+        copies[1] = c->rlc.src[1];
     });
 }
 int svdw_layout(const svdw_ctx* c, svdw_region* out, uint64_t cap, uint64_t* n) {

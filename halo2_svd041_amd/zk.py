@@ -202,6 +202,18 @@ class Context:
         return [{"phase": r.phase, "off": r.off, "n": r.n, "loff": r.loff, "nl": r.nl,
                  "rows": r.rows, "tag": r.tag.decode()} for r in buf[:n.value]]
 
+    def rlc_trace(self) -> Optional[dict]:
+        """ctx_rlc of the last svd_witness with rlc_prefix (svdw_rlc_trace;
+        parity unpinned): {"cells": (3, 4) uint64, "copies": [(phase, offset)]
+        of its two E cells}, or None without the prefix."""
+        cells = np.zeros((3, 4), dtype=np.uint64)
+        copies = np.zeros(2, dtype=np.uint64)
+        n = ct.c_uint32()
+        check(lib().svdw_rlc_trace(self._h, cells.ctypes.data, copies.ctypes.data, ct.byref(n)))
+        if not n.value:
+            return None
+        return {"cells": cells, "copies": [(int(c) >> 62, int(c) & ((1 << 62) - 1)) for c in copies]}
+
     def check_gates(self) -> dict:
         """Device constraint check of the last witness (svdw_check_gates)."""
         r = CheckResult()

@@ -346,6 +346,17 @@ typedef struct {
     char tag[40];
 } svdw_region;
 int svdw_layout(const svdw_ctx* ctx, svdw_region* out, uint64_t cap, uint64_t* n);
+/* ctx_rlc of the last svd_witness run with "rlc_prefix" 1: the RLC context of
+ * examples/svd_example.rs:181-184 (rlc.load_rlc_cache((ctx_gate, ctx_rlc),
+ * gate, 1); gamma_pow_cached()[0]), as recalled from axiom-eth's RlcChip
+ * (un-vendored: PARITY UNPINNED). An empty cache loads gamma as
+ * compute_rlc_fixed_len(ctx_rlc, [one, zero]): ctx_rlc holds
+ * [E(one), E(zero), W(gamma)], whose cell 2 is the init_rand every phase-1
+ * gamma cell copies. cells: 3 x 4 u64 (canonical LE); copies[k]: the source of
+ * ctx_rlc cell k < 2 (phase << 62 | offset in that phase's advice stream, the
+ * two ctx_gate constants at the head of phase 1). *n = 3, or 0 when the last
+ * witness had no RLC prefix (cells / copies untouched). Host memory, no GPU. */
+int svdw_rlc_trace(const svdw_ctx* ctx, uint64_t* cells, uint64_t* copies, uint32_t* n);
 
 /* Constraint check of the last witness on the device, the MockProver-style
  * verification of an (unsharded) context: every halo2-base basic gate

@@ -30,7 +30,7 @@ from __future__ import annotations
 import math
 import struct
 from dataclasses import dataclass, field
-from typing import List, Sequence, Tuple
+from typing import Optional, List, Sequence, Tuple
 
 # BN254 scalar field modulus (halo2curves bn256::Fr).
 P_MOD = 21888242871839275222246405745257275088548364400416034343698204186575808495617
@@ -543,6 +543,7 @@ class SvdWitness:
     ctx1: Context
     err_svd: float
     err_u: float
+    rlc: Optional[Context] = None     # ctx_rlc (rlc_prefix: [E(one), E(zero), W(gamma)])
 
 
 def load_rlc_cache_1(ctx_gate: Context, rlc: Context, gamma: int) -> AV:
@@ -572,7 +573,7 @@ def svd_witness(m, u, v, d, p: int, lookup_bits: int, gamma: int,
     ctx1 = Context(phase=1)
     g = load_rlc_cache_1(ctx1, rlc, gamma) if rlc_prefix else load_witness(rlc, gamma)
     check_svd_phase1(ctx1, zm, zu, zv, pl, g)
-    return SvdWitness(ctx0, ctx1, err_svd, err_u)
+    return SvdWitness(ctx0, ctx1, err_svd, err_u, rlc)
 
 
 # ---------------------------------------------------------------------------

@@ -8,7 +8,9 @@ restates it (oracle/pyoracle.py load_rlc_cache_1: recalled axiom-eth RlcChip,
 parity unpinned). For every fixture entry this computes that stream with the
 Python oracle on the fixture's stored inputs, checks that it is [1, 0] followed
 by the fixture's own phase-1 stream (whose digest the C oracle reproduces), and
-stores its SHA-256 and length as sha256_advice1_rlc / advice1_rlc.
+stores its SHA-256 and length as sha256_advice1_rlc / advice1_rlc; and the
+RLC context's own cells [E(one), E(zero), W(gamma)] (digest and the phase-1
+sources of its two copies) as rlc_trace.
 
     python tests/golden/add_rlc_digests.py
 """
@@ -54,6 +56,12 @@ for path in sorted(glob.glob(os.path.join(HERE, "svd_*.json"))):
         assert _sha(a1[2:]) == exp["sha256_advice1"], (path, exp["input"], p)
         exp["advice1_rlc"] = int(a1.shape[0])
         exp["sha256_advice1_rlc"] = _sha(a1)
+        # ctx_rlc itself: [E(one), E(zero), W(gamma)], E cells copying the two
+        # ctx_gate constants at the head of phase 1 (depends on gamma only)
+        r = _cells(w.rlc.advice)
+        assert [(a.ctx is w.ctx1, a.idx, dst) for a, dst in w.rlc.copies] == [(True, 0, 0), (True, 1, 1)]
+        case["rlc_trace"] = {"cells": int(r.shape[0]), "sha256": _sha(r),
+                             "copies": [[1, 0], [1, 1]]}
     with open(path, "w") as fh:
         json.dump(case, fh, indent=1)
         fh.write("\n")

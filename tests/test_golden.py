@@ -150,3 +150,28 @@ def test_engine_from_raw_input_files(gpu_ctx_factory, path):
         assert _sha(ctx.advice(0)) == exp["sha256_advice0"]
         assert _sha(ctx.lookups(0)) == exp["sha256_lookup0"]
         assert _sha(ctx.advice(1)) == exp["sha256_advice1"]
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
+def test_rlc_trace_golden(path):
+    """svdw_rlc_trace (the ctx_rlc stream of load_rlc_cache(.., 1), recalled
+    axiom-eth construction, parity unpinned): the engine's three RLC cells and
+    their copy sources equal the golden rlc_trace the Python oracle produced
+    (tests/golden/add_rlc_digests.py); a host-only planning context suffices,
+    the trace is host data. Without rlc_prefix there is no trace."""
+    import halo2_svd041_amd as hs
+    case = _load(path)
+    g = int(case["gamma"])
+    exp = case["expected"][0]
+    m, u, v, d = _inputs(case, exp["input"])
+    ctx = hs.Context(device=-1, precision_bits=exp["precision_bits"], lookup_bits=case["lookup_bits"])
+    hs.svd_witness(ctx, m, u, v, d, g)
+    assert ctx.rlc_trace() is None
+    ctx.set_option("rlc_prefix", 1)
+    hs.svd_witness(ctx, m, u, v, d, g)
+    tr = ctx.rlc_trace()
+    want = case["rlc_trace"]
+    assert tr["cells"].shape[0] == want["cells"]
+    assert _sha(tr["cells"]) == want["sha256"]
+    assert [list(c) for c in tr["copies"]] == want["copies"]
+    ctx.close()
