@@ -412,7 +412,14 @@ struct svdw_ctx {
     Fr gp_gamma{};
     uint32_t gp_len = 0;
     hipEvent_t gp_ev = nullptr;
-    hipStream_t gp_st = nullptr;            // the stream gp_ev was recorded on             // gamma_prep queued ahead (svd_witness)
+    hipStream_t gp_st = nullptr;            // the stream gp_ev was recorded on
+    // verify_mul_witness: the one cell and gamma powers written by k_gamma_prep
+    // (phase-1 offsets one_off / pows_off for d), so verify_mul does not launch them
+    struct PowsPre {
+        bool on = false;
+        uint64_t one_off = 0, pows_off = 0;
+        uint32_t d = 0;
+    } pows_pre;             // gamma_prep queued ahead (svd_witness)
     // Device bit-length words of matrices written in this witness (svd_witness:
     // quantized m, u, v at dbitw[0..2]): the row scans decide their operand
     // width on the device from these (NaSpec), so the host never waits for them.
@@ -1825,7 +1832,7 @@ struct VMul {
 // v = (1, g, g^2, ...): canonical (gpc) + scaled table (gtab), on stream s. The
 // powers come from three host-side Montgomery tables (g^a, g^(16 b), g^(256 c)):
 // three products per element on the device instead of a square-and-multiply chain.
-static void gamma_prep(svdw_ctx* c, uint32_t d, const Fr& gamma, hipStream_t s) {
+static void gamma_prep(svdw_ctx* c, uint32_t d, const Fr& gamma, hipStream_t s, const PowCells* pc = nullptr) {
     if (c->dry) return;
     const uint32_t len = std::max(d, 1u);
     REQUIRE((len + 255) / 256 <= (uint32_t)kGammaTab - 32, "verify_mul: vector too long");
@@ -1845,7 +1852,7 @@ static void gamma_prep(svdw_ctx* c, uint32_t d, const Fr& gamma, hipStream_t s) 
     for (uint32_t i = 1; i < g.nhi; ++i) g.t[32 + i] = mont_mul(g.t[31 + i], g256);
     {
         ProfScope ps(c, s, "k_gamma_prep", 32.0 * len * (1 + tab_len(1)), 0);
-        hipck(launch_gamma_prep(g, len, (Fr*)c->gpc.p, (Fr*)c->gtab.p, scale_tab(), s),
+        hipck(launch_gamma_prep(g, len, (Fr*)c->gpc.p, (Fr*)c->gtab.p, scale_tab(), s, pc),
               "k_gamma_prep");
     }
     c->gp_gamma = gamma;
@@ -1939,7 +1946,12 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     ensure_gamma_vec(c, dmax, gamma);
     const Fr* gpc = (const Fr*)c->gpc.p;
     const Fr* gtab = (const Fr*)c->gtab.p;
-    {
+    // verify_mul_witness: k_gamma_prep already wrote the one cell and the powers
+    const bool pre = c->pows_pre.on && n == 1 && pl[0].one_off == c->pows_pre.one_off &&
+                     pl[0].pows_off == c->pows_pre.pows_off && vm[0].cs.cols == c->pows_pre.d &&
+                     pl[0].one_loff == 0;
+    c->pows_pre.on = false;
+    if (!pre) {
         BatchScope bs(c);                                 // the one cells and gamma powers: one launch
         for (int i = 0; i < n; ++i) {
             Plan& p = pl[i];
@@ -2838,9 +2850,21 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     unsigned* dbits = nullptr;
     const uint32_t nba = (uint32_t)(((uint64_t)N * K + kQuantPerBlock - 1) / kQuantPerBlock),
                    nbb = (uint32_t)(((uint64_t)K * M + kQuantPerBlock - 1) / kQuantPerBlock);
+    c->pows_pre.on = false;
     if (!c->dry) {
         if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
-        gamma_prep(c, M, gamma, c->st3);
+        // phase 1 opens with verify_mul's one cell and its d - 1 gamma-power
+        // elements (verify_mul_many's first appends): k_gamma_prep writes them
+        PowCells pc;
+        memset(&pc, 0, sizeof pc);
+        if (M > 1 && c->ph[1].n == 0 && c->ph[1].cap >= 1 + 4ull * (M - 1)) {
+            pc.one = cellp(c, 1, 0);
+            pc.pows = cellp(c, 1, 1);
+            pc.d = M;
+            pc.gamma = gamma;
+            c->pows_pre = {true, 0, 1, M};
+        }
+        gamma_prep(c, M, gamma, c->st3, pc.one ? &pc : nullptr);
         c->gp_ev = stream_dep(c, c->st3, nullptr);
         c->gp_st = c->st3;
         ensure_buf(c, c->bits, (64 + nba + nbb) * sizeof(unsigned));

@@ -2244,18 +2244,34 @@ hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* wc, Fr* tab, const Sc
 // g^j from the host's three Montgomery tables (depth: three products, then the
 // slot's): no per-element square-and-multiply chain.
 __global__ __launch_bounds__(256) void k_gamma_prep(const GammaTab g, uint32_t L, Fr* wc, Fr* tab,
-                                                    const ScaleTab f) {
+                                                    const ScaleTab f, const PowCells pc) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= L) return;
-    const Fr vm = mont_mul(mont_mul(g.t[j & 15], g.t[16 + ((j >> 4) & 15)]), g.t[32 + (j >> 8)]);
-    tab_store(wc, tab, L, j, blockIdx.y, fr_from_mont(vm), f);
+    const Fr v = fr_from_mont(mont_mul(mont_mul(g.t[j & 15], g.t[16 + ((j >> 4) & 15)]), g.t[32 + (j >> 8)]));
+    tab_store(wc, tab, L, j, blockIdx.y, v, f);
+    if (pc.one && blockIdx.y == 0 && j < pc.d) {          // v_j = gamma^j: v_0 is the one cell
+        if (j == 0) st_fr(pc.one, v);
+        if (j >= 1) {                                      // element j - 1: [0, v_(j-1), gamma, v_j]
+            Fr* e = pc.pows + 4ull * (j - 1);
+            st_fr(e, fr_zero());
+            st_fr(e + 2, pc.gamma);
+            st_fr(e + 3, v);
+        }
+        if (j + 1 < pc.d) st_fr(pc.pows + 4ull * j + 1, v); // v_j as element j's v_(i-1)
+    }
 }
 hipError_t launch_gamma_prep(const GammaTab& g, uint32_t L, Fr* wc, Fr* tab, const ScaleTab& f,
-                             hipStream_t st) {
+                             hipStream_t st, const PowCells* pc) {
     if (!L) return hipSuccess;
     if ((L + 255) / 256 > g.nhi || g.nhi > (uint32_t)kGammaTab - 32) return hipErrorInvalidValue;
+    PowCells p;
+    memset(&p, 0, sizeof p);
+    if (pc) {
+        if (pc->d > L || !pc->d) return hipErrorInvalidValue;
+        p = *pc;
+    }
     hipLaunchKernelGGL(k_gamma_prep, dim3((L + 255) / 256, 1 + kTabSlots), dim3(256), 0, st, g, L,
-                       wc, tab, f);
+                       wc, tab, f, p);
     return hipGetLastError();
 }
 

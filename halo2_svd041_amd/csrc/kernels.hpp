@@ -345,8 +345,16 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st);
 hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* tab, const ScaleTab& f,
                            hipStream_t st);
 // w_j = gamma^j, j < L (L <= 256 * (kGammaTab - 32)): canonical copy and scaled table.
+// verify_mul's `one` cell and gamma-power cells [0, v_(i-1), gamma, v_i],
+// i = 1 .. d - 1, written by k_gamma_prep beside the table (one null: none).
+struct PowCells {
+    Fr* one;
+    Fr* pows;
+    uint32_t d;
+    Fr gamma;     // canonical
+};
 hipError_t launch_gamma_prep(const GammaTab& g, uint32_t L, Fr* w_canon, Fr* tab, const ScaleTab& f,
-                             hipStream_t st);
+                             hipStream_t st, const PowCells* pc = nullptr);
 // Freivalds inner-product rows (GateChip::inner_product, 1+3L cells per row) for
 // rows [r_begin, r_end) of A (R x L); row r's cells at out + (r - r_begin)*(3L+1):
 // one block per row, two terms per thread, DPP wave scan, small-operand products

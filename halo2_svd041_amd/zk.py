@@ -80,7 +80,11 @@ def _device_ptr(a) -> Optional[int]:
 
 def _torch_stream(ctx: "Context") -> int:
     """torch's current stream on the context's device (hipStream_t as int)."""
-    return _torch_mod().cuda.current_stream(ctx.device).cuda_stream
+    t = _torch_mod()
+    raw = getattr(t._C, "_cuda_getCurrentRawStream", None)   # no Stream object per call
+    if raw is not None:
+        return raw(ctx.device)
+    return t.cuda.current_stream(ctx.device).cuda_stream
 
 
 def _after_torch(ctx: "Context") -> None:
