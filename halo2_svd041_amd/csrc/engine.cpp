@@ -458,7 +458,7 @@ struct svdw_ctx {
     int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
     bool gemm_batched = false;              // this witness's products went out as one batch
-    int res_first = -1;                     // "res_first": cell stream waits for the residue planes
+    int res_first = 1;                      // "res_first": cell stream waits for the residue planes
                                             // (1), not (0), -1: on row-sharded ranks
     int gemm_batch = 1;                     // "gemm_batch": svd_witness's three products in one launch
                                             // (1), one by one (0), or -1: batched on row-sharded ranks
@@ -2607,6 +2607,15 @@ static void check_svd_phase1(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u, 
     verify_mul_many(c, 1, vm, 3, g);
 }
 
+// A witness call's side streams start after everything queued on st (the
+// previous call's work joins st at its end): without this, the next call's
+// gamma tables (st3) and first stages (st2, f64 views need no load) could
+// overwrite buffers the previous call's kernels still read.
+static void after_previous(svdw_ctx* c) {
+    if (c->dry) return;
+    const hipEvent_t e = stream_dep(c, c->st, c->st2);
+    if (c->st3) hipck(hipStreamWaitEvent(c->st3, e, 0), "hipStreamWaitEvent");
+}
 static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, const double* v,
                                const double* d, uint32_t N, uint32_t M, bool on_device,
                                const svdw_svd_config& cfg, const Fr& gamma) {
@@ -2616,6 +2625,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     host_mark(c, "svd_witness start");
     clear_streams(c);
     c->dep_next = 0;
+    after_previous(c);
     if (!c->dry) apply_gemm_prio(c, N, M);
     c->prelaunched = false;
     c->prod_on_cell = false;
@@ -2817,6 +2827,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     host_mark(c, "verify_mul_witness start");
     clear_streams(c);
     c->dep_next = 0;
+    after_previous(c);
     c->prelaunched = false;
     c->prod_on_cell = false;
     c->prod_blk = 1;

@@ -283,8 +283,9 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   products in one GEMM and one combine launch; -1: on row-sharded contexts); "prod_cell" 1 | 0 | -1 (svd_witness with
  *   device inputs: the products on the cell stream and the u / v bounds and u.d
  *   beside them; -1 on row-sharded contexts only); "res_first"
- *   -1 | 0 | 1 (the cell stream waits for the residue planes; -1: on row-sharded
- *   contexts, where it measured ~3% faster; slower at 1 GPU).
+ *   1 | 0 | -1 (the stages beside the products wait for the residue planes,
+ *   which then run alone; -1: on row-sharded contexts only; measured 1-3 %
+ *   faster at 512^2, 1024^2 and on 8-way shard ranks).
  * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:
  *   phase 1 starts with the two ctx_gate constant cells [1, 0] that
  *   examples/svd_example.rs:183's rlc.load_rlc_cache(.., 1) appends as recalled
