@@ -161,6 +161,7 @@ SIGNATURES = {
                                 ct.POINTER(Counts)]),
     "svdw_set_gemm_impl": (_i32, [_P, _i32]),
     "svdw_set_option": (_i32, [_P, ct.c_char_p, ct.c_int64]),
+    "svdw_graph_stats": (_i32, [_P, ct.POINTER(ct.c_uint64), ct.POINTER(ct.c_uint64)]),
     "svdw_profile_enable": (_i32, [_P, _i32]),
     "svdw_profile_filter": (_i32, [_P, ct.c_char_p]),
     "svdw_set_shard": (_i32, [_P, _u32, _u32]),

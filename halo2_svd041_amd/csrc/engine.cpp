@@ -592,6 +592,35 @@ struct svdw_ctx {
     DBuf ing_x, ing_e, ing_c, ing_p10, ing_val, ing_npos, ing_nd, ing_rpos, ing_kpos, ing_err, ing_q;
     // device equality records (eq_gen_device)
     DBuf eq_cp, eq_ks, eq_reg, eq_w, eq_k, eq_err, eq_st;
+    // ---- captured verify_mul_witness ("graph", vm_graph): the launch sequence of
+    // a device-input call is captured once into a HIP graph (the second call of
+    // a shape, when every buffer is sized) and replayed by later calls of the
+    // same key; gamma enters only through k_gamma_prep, launched eagerly on st
+    // ahead of the graph (gp_external), so the graph itself is gamma-free.
+    int graph_vm = 1;                       // "graph": 0 off, 1 verify_mul_witness
+    bool capturing = false;                 // st is capturing: no allocation, no sync
+    bool gp_external = false;               // verify_mul_witness: k_gamma_prep already queued
+    const Fr* gp_ext_one = nullptr;         // the one cell it wrote (null: none)
+    uint64_t epoch = 0;                     // bumped by every allocation / option change
+    // (layout_chk index, eqk slot) of the constants that hold gamma (the
+    // verify_mul gamma powers' init_rand), patched on replay
+    std::vector<std::pair<size_t, int>> gamma_slots;
+    struct VmGraph {
+        std::vector<uint64_t> key, seen;    // replay key; the last eager call's key
+        hipGraphExec_t exec = nullptr;
+        // host state the captured call left behind (restored on replay)
+        std::vector<svdw_region> layout;
+        std::vector<RegionChecks> layout_chk;
+        std::set<std::array<uint32_t, 8>> consts;
+        std::vector<std::pair<size_t, int>> gamma_slots;
+        std::vector<MatBits> mbits;
+        std::vector<Prod> prods;
+        std::vector<DevBits> dwords;
+        const unsigned* dbitw = nullptr;
+        uint64_t ext_off = 0;
+        svdw_counts counts{};
+        uint64_t replays = 0, captures = 0;
+    } vmg;
 };
 
 static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter = nullptr, hipEvent_t then_wait = nullptr);
@@ -601,6 +630,7 @@ static const bool g_batch_log = env_flag("SVDW_BATCH_LOG");
 static const bool g_stage_log = env_flag("SVDW_STAGE_LOG");
 static void sync(svdw_ctx* c) {
     if (c->dry) return;
+    REQUIRE(!c->capturing, "internal: synchronisation during graph capture");
     hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
     hipck(hipStreamSynchronize(c->st2), "hipStreamSynchronize");
     if (c->st3) hipck(hipStreamSynchronize(c->st3), "hipStreamSynchronize");
@@ -710,6 +740,7 @@ static void clear_streams(svdw_ctx* c) {
     c->prods.clear();
     c->dwords.clear();
     c->dbitw = nullptr;
+    c->gamma_slots.clear();
 }
 // RAII: brackets one kernel launch with HIP events on the context stream.
 struct ProfScope {
@@ -749,6 +780,8 @@ struct ProfScope {
 
 static void ensure_buf(svdw_ctx* c, DBuf& b, size_t bytes) {
     if (c->dry || b.cap >= bytes) return;
+    REQUIRE(!c->capturing, "internal: allocation during graph capture");
+    ++c->epoch;
     sync(c);
     if (b.p) hipck(hipFree(b.p), "hipFree");
     b.p = nullptr;
@@ -784,6 +817,8 @@ static void bits_words(svdw_ctx* c, QuantSegs& qs, uint32_t nred, const BitSegs&
 }
 static void grow(svdw_ctx* c, Fr*& ptr, uint64_t used, uint64_t& cap, uint64_t need) {
     if (c->dry || need <= cap) return;
+    REQUIRE(!c->capturing, "internal: allocation during graph capture");
+    ++c->epoch;
     uint64_t ncap = std::max(need, cap + cap / 2);
     Fr* np = nullptr;
     if (hipMalloc((void**)&np, ncap * sizeof(Fr)) != hipSuccess)
@@ -1834,6 +1869,7 @@ struct VMul {
 // three products per element on the device instead of a square-and-multiply chain.
 static void gamma_prep(svdw_ctx* c, uint32_t d, const Fr& gamma, hipStream_t s, const PowCells* pc = nullptr) {
     if (c->dry) return;
+    REQUIRE(!c->capturing, "internal: gamma inside a captured graph");
     const uint32_t len = std::max(d, 1u);
     REQUIRE((len + 255) / 256 <= (uint32_t)kGammaTab - 32, "verify_mul: vector too long");
     ensure_buf(c, c->gpc, (size_t)len * sizeof(Fr));
@@ -1913,6 +1949,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
             append(c, phase, (uint64_t)(d - 1) * p.pows.a.C, 0, &p.pows_off, &p.pows_loff,
                    "verify_mul_gamma_pows");
             note_gates(c, p.pows);
+            c->gamma_slots.emplace_back(c->layout_chk.size() - 1, p.pows.kext);
             // v_(i-1): the `one` cell, then the previous mul's output
             c->layout_chk.back().esrc[0] = eqsrc_chain(phase, p.one_off, phase, p.pows_off + 3, 4);
             stage_own(c, phase, p.pows, d - 1, 1, p.pows_off, p.pows_loff);
@@ -1952,6 +1989,8 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
                      pl[0].one_loff == 0;
     c->pows_pre.on = false;
     if (!pre) {
+        // (a captured graph must not hold gamma: the powers' launch carries it)
+        for (int i = 0; i < n; ++i) REQUIRE(!c->capturing || vm[i].cs.cols <= 1, "internal: gamma inside a captured graph");
         BatchScope bs(c);                                 // the one cells and gamma powers: one launch
         for (int i = 0; i < n; ++i) {
             Plan& p = pl[i];
@@ -2819,6 +2858,18 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
 // quantized in one launch, the GEMM's modulus count and the row scans' operand
 // widths decided on the device from the bit-length words, gamma^j prepared
 // first on the side stream.
+// verify_mul_witness's phase 1 opens with verify_mul's one cell and its d - 1
+// gamma-power elements (verify_mul_many's first appends at phase-1 offsets 0
+// and 1): k_gamma_prep writes them when the phase-1 stream holds them
+static bool vm_pow_cells(svdw_ctx* c, uint32_t M, const Fr& gamma, PowCells* pc) {
+    memset(pc, 0, sizeof *pc);
+    if (M <= 1 || c->ph[1].cap < 1 + 4ull * (M - 1)) return false;
+    pc->one = cellp(c, 1, 0);
+    pc->pows = cellp(c, 1, 1);
+    pc->d = M;
+    pc->gamma = gamma;
+    return true;
+}
 static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double* b, uint32_t N,
                                       uint32_t K, uint32_t M, bool on_device, const Fr& gamma) {
     REQUIRE(N >= 1 && K >= 1 && M >= 1, "empty matrix");
@@ -2867,15 +2918,15 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
         // phase 1 opens with verify_mul's one cell and its d - 1 gamma-power
         // elements (verify_mul_many's first appends): k_gamma_prep writes them
         PowCells pc;
-        memset(&pc, 0, sizeof pc);
-        if (M > 1 && c->ph[1].n == 0 && c->ph[1].cap >= 1 + 4ull * (M - 1)) {
-            pc.one = cellp(c, 1, 0);
-            pc.pows = cellp(c, 1, 1);
-            pc.d = M;
-            pc.gamma = gamma;
+        // (queued ahead: only if that launch wrote them where they are now)
+        if (c->ph[1].n == 0 && vm_pow_cells(c, M, gamma, &pc) && (!c->gp_external || c->gp_ext_one == pc.one))
             c->pows_pre = {true, 0, 1, M};
+        if (c->gp_external) {                         // queued on st ahead of the captured graph
+            c->gp_gamma = gamma;
+            c->gp_len = std::max(M, 1u);
+        } else {
+            gamma_prep(c, M, gamma, c->st3, pc.one ? &pc : nullptr);
         }
-        gamma_prep(c, M, gamma, c->st3, pc.one ? &pc : nullptr);
         c->gp_ev = stream_dep(c, c->st3, nullptr);
         c->gp_st = c->st3;
         ensure_buf(c, c->bits, (64 + nba + nbb) * sizeof(unsigned));
@@ -2978,6 +3029,119 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     }
     host_mark(c, "verify_mul_witness end");
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
+}
+
+// ---------------------------------------- captured verify_mul_witness (graph)
+// A device-input verify_mul_witness enqueues ~20 HIP calls for a GPU step of
+// ~70 us at 256^2 (BASELINE config 2), so the host bounds it. Every call of
+// one key (shape, input pointers, buffer epoch) enqueues the same launches:
+// nothing in it waits for the device, and gamma reaches the device only as
+// k_gamma_prep's tables. So k_gamma_prep goes out eagerly on st (by value),
+// the rest is captured once (on the second call of a key, when every buffer
+// is sized) and replayed with one hipGraphLaunch; the host state the call
+// leaves (layout, checks, counts) is restored from the capture, with gamma
+// patched into the constants that hold it.
+static void vmg_drop(svdw_ctx* c) {
+    if (c->vmg.exec) (void)hipGraphExecDestroy(c->vmg.exec);
+    c->vmg.exec = nullptr;
+    c->vmg.key.clear();
+}
+static void vmg_snapshot(svdw_ctx* c, const svdw_counts& k) {
+    auto& g = c->vmg;
+    g.layout = c->layout;
+    g.layout_chk = c->layout_chk;
+    g.consts = c->consts;
+    g.gamma_slots = c->gamma_slots;
+    g.mbits = c->mbits;
+    g.prods = c->prods;
+    g.dwords = c->dwords;
+    g.dbitw = c->dbitw;
+    g.ext_off = c->ext_off;
+    g.counts = k;
+}
+static svdw_counts vmg_restore(svdw_ctx* c, const Fr& gamma) {
+    const auto& g = c->vmg;
+    clear_streams(c);
+    c->layout = g.layout;
+    c->layout_chk = g.layout_chk;
+    c->consts = g.consts;
+    c->gamma_slots = g.gamma_slots;
+    for (const auto& s : c->gamma_slots) c->layout_chk.at(s.first).eqk.at((size_t)s.second) = gamma;
+    c->mbits = g.mbits;
+    c->prods = g.prods;
+    c->dwords = g.dwords;
+    c->dbitw = g.dbitw;
+    c->ext_off = g.ext_off;
+    c->ext_gamma = gamma;
+    c->ph[0].n = g.counts.advice0;
+    c->ph[1].n = g.counts.advice1;
+    c->ph[0].nl = g.counts.lookup0;
+    c->ph[1].nl = g.counts.lookup1;
+    return g.counts;
+}
+static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const double* b, uint32_t N,
+                                          uint32_t K, uint32_t M, bool on_device, const Fr& gamma) {
+    const bool usable = c->graph_vm && on_device && !c->dry && !c->prof && !c->hold_us && !sharded(c) &&
+                        N >= 1 && K >= 1 && M >= 1;
+    if (!usable) {
+        vmg_drop(c);
+        c->vmg.seen.clear();
+        return verify_mul_witness(c, a, b, N, K, M, on_device, gamma);
+    }
+    struct Flags {
+        svdw_ctx* c;
+        ~Flags() { c->gp_external = false; c->capturing = false; c->gp_ev = nullptr; c->pows_pre.on = false; }
+    } flags{c};
+    // gamma's tables (and the one / gamma-power cells when phase 1 holds them)
+    // on st, ahead of everything the call queues
+    PowCells pc;
+    const bool pw = vm_pow_cells(c, M, gamma, &pc);
+    gamma_prep(c, M, gamma, c->st, pw ? &pc : nullptr);
+    c->gp_external = true;
+    c->gp_ext_one = pw ? pc.one : nullptr;
+    const std::vector<uint64_t> key = {N, K, M, (uint64_t)(uintptr_t)a, (uint64_t)(uintptr_t)b, c->epoch};
+    if (c->vmg.exec && key == c->vmg.key) {
+        const svdw_counts k = vmg_restore(c, gamma);
+        hipck(hipGraphLaunch(c->vmg.exec, c->st), "hipGraphLaunch");
+        ++c->vmg.replays;
+        return k;
+    }
+    if (key == c->vmg.seen) {
+        vmg_drop(c);
+        hipGraph_t graph = nullptr;
+        hipck(hipStreamBeginCapture(c->st, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+        c->capturing = true;
+        svdw_counts k{};
+        try {
+            k = verify_mul_witness(c, a, b, N, K, M, on_device, gamma);
+            stream_dep(c, c->st2, c->st);                  // every forked stream joins st
+            if (c->st3) stream_dep(c, c->st3, c->st);
+        } catch (...) {
+            // nothing captured ran: end the capture and run the call eagerly
+            c->capturing = false;
+            graph = nullptr;
+            if (hipStreamEndCapture(c->st, &graph) == hipSuccess && graph) (void)hipGraphDestroy(graph);
+            (void)hipGetLastError();
+            c->vmg.seen.clear();
+            return verify_mul_witness(c, a, b, N, K, M, on_device, gamma);
+        }
+        c->capturing = false;
+        hipck(hipStreamEndCapture(c->st, &graph), "hipStreamEndCapture");
+        hipGraphExec_t exec = nullptr;
+        const hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        hipck(e, "hipGraphInstantiate");
+        c->vmg.exec = exec;
+        c->vmg.key = key;
+        vmg_snapshot(c, k);
+        hipck(hipGraphLaunch(exec, c->st), "hipGraphLaunch");
+        ++c->vmg.captures;
+        return k;
+    }
+    vmg_drop(c);
+    const svdw_counts k = verify_mul_witness(c, a, b, N, K, M, on_device, gamma);
+    c->vmg.seen = {N, K, M, (uint64_t)(uintptr_t)a, (uint64_t)(uintptr_t)b, c->epoch};
+    return k;
 }
 
 // ------------------------------------------------------ equality lists
@@ -3176,6 +3340,7 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             (void)hipStreamSynchronize(c->st);
             (void)hipStreamSynchronize(c->st2);
             if (c->st3) (void)hipStreamSynchronize(c->st3);
+            vmg_drop(c);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
             for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1], &c->w1c, &c->w1t, &c->w2c, &c->w2t,
                             &c->bits, &c->gpc, &c->gtab, &c->crtR, &c->gbits, &c->colpart, &c->qfold})
@@ -3534,7 +3699,7 @@ int svdw_verify_mul_witness(svdw_ctx* c, const double* a, const double* b, uint3
     return guarded([&] {
         REQUIRE(c && gamma, "null argument");
         REQUIRE(c->dry || (a && b), "null input matrix");
-        svdw_counts k = verify_mul_witness(c, a, b, N, K, M, on_device != 0, fr_from_words(gamma));
+        svdw_counts k = verify_mul_witness_api(c, a, b, N, K, M, on_device != 0, fr_from_words(gamma));
         if (counts) *counts = k;
     });
 }
@@ -3751,6 +3916,7 @@ int svdw_set_shard(svdw_ctx* c, uint32_t rank, uint32_t world) {
     return guarded([&] {
         REQUIRE(c, "null ctx");
         REQUIRE(world >= 1 && rank < world, "svdw_set_shard: need rank < world");
+        ++c->epoch;
         c->shard_rank = rank;
         c->shard_world = world;
         c->owned.clear();
@@ -4110,8 +4276,12 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
     return guarded([&] {
         REQUIRE(c && name, "null argument");
         sync(c);
+        ++c->epoch;                                  // a captured launch sequence may change
         const std::string n(name);
-        if (n == "gemm_impl") {
+        if (n == "graph") {                          // captured verify_mul_witness (vm_graph)
+            REQUIRE(value == 0 || value == 1, "graph: 0 or 1");
+            c->graph_vm = (int)value;
+        } else if (n == "gemm_impl") {
             REQUIRE(value == SVDW_GEMM_MFMA || value == SVDW_GEMM_VALU, "gemm_impl: 0 (mfma) or 1 (valu)");
             c->gemm_impl = (int)value;
         } else if (n == "stage_elems") {
@@ -4207,11 +4377,19 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         }
     });
 }
+int svdw_graph_stats(svdw_ctx* c, uint64_t* captures, uint64_t* replays) {
+    return guarded([&] {
+        REQUIRE(c && captures && replays, "null argument");
+        *captures = c->vmg.captures;
+        *replays = c->vmg.replays;
+    });
+}
 int svdw_set_gemm_impl(svdw_ctx* c, int impl) {
     return guarded([&] {
         REQUIRE(c, "null ctx");
         REQUIRE(impl == SVDW_GEMM_MFMA || impl == SVDW_GEMM_VALU, "unknown GEMM implementation");
         sync(c);
+        ++c->epoch;
         c->gemm_impl = impl;
     });
 }

@@ -184,6 +184,13 @@ class Context:
         if name in LAYOUT_OPTIONS:
             self.layout_opts[name] = int(value)
 
+    def graph_stats(self) -> tuple:
+        """(captures, replays) of the captured verify_mul_witness graph
+        (svdw_graph_stats; option "graph")."""
+        cap, rep = ct.c_uint64(0), ct.c_uint64(0)
+        check(lib().svdw_graph_stats(self._h, ct.byref(cap), ct.byref(rep)))
+        return cap.value, rep.value
+
     def set_shard(self, rank: int, world: int) -> None:
         """Row-block sharding of one witness over `world` contexts (svdw_set_shard)."""
         check(lib().svdw_set_shard(self._h, int(rank), int(world)))

@@ -294,8 +294,17 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   0 | 1 (skip the stage programs) | 2 (store a constant instead of cells) |
  *   3 (constant stores, no view loads either);
  *   "hold_us" 0 | us (svd_witness, verify_mul_witness: the step's streams wait behind a kernel
- *   spinning that long, so the GPU schedule is measured without host gaps). */
+ *   spinning that long, so the GPU schedule is measured without host gaps).
+ * "graph" 1 | 0: svdw_verify_mul_witness with device inputs replays a HIP graph
+ *   of its launch sequence. The second call of a key (N, K, M, the input
+ *   pointers, no allocation or option change since) is captured, later calls
+ *   of the key replay it with one hipGraphLaunch; k_gamma_prep (gamma's tables,
+ *   and the one / gamma-power cells) is queued on the context stream ahead of
+ *   the graph, so gamma is never part of it. Off while profiling or hold_us is
+ *   set. The cells are bit-identical either way. */
 int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);
+/* Captures and replays of the verify_mul_witness graph ("graph") so far. */
+int svdw_graph_stats(svdw_ctx* ctx, uint64_t* captures, uint64_t* replays);
 
 /* ----------------------------------------------------------- profiling */
 /* Per-kernel statistics from HIP events recorded around every launch on the

@@ -1,0 +1,103 @@
+"""Captured verify_mul_witness (option "graph", engine.cpp verify_mul_witness_api).
+
+The second device-input call of a key is captured into a HIP graph and later
+calls replay it, with k_gamma_prep queued ahead of the graph. Every call's cells,
+gate checks and equality records must be those of an eager call with the same
+inputs and gamma: the full advice streams are compared with the C oracle
+(oracle/svdw_oracle.c, README.md:32-46's recipe) after each call, and with a
+graph-off context.
+"""
+import numpy as np
+import pytest
+
+import corc
+from conftest import gamma_for
+
+
+def _mats(n, k, m, seed):
+    rs = np.random.RandomState(seed)
+    return rs.uniform(-1, 1, (n, k)), rs.uniform(-1, 1, (k, m))
+
+
+def _check_all(ctx, a, b, P, g):
+    c0, c1 = corc.verify_mul_witness(a, b, P, g)
+    assert np.array_equal(ctx.advice(0), c0), "phase-0 advice differs from the C oracle"
+    assert np.array_equal(ctx.advice(1), c1), "phase-1 advice differs from the C oracle"
+    chk = ctx.check_gates()
+    assert chk["gate_failures"] == 0 and chk["lookup_failures"] == 0 and chk["copy_failures"] == 0
+    eq = ctx.check_equalities(1)
+    assert eq["copy_failures"] == 0 and eq["const_failures"] == 0 and eq["copies_checked"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k,m,P", [(256, 256, 256, 32), (45, 130, 37, 63), (3, 2, 1, 32)])
+def test_graph_replays_match_oracle(gpu_ctx_factory, n, k, m, P):
+    """Five calls on the same input tensors (new values written in place) with a
+    fresh gamma each: eager, then captured, then replayed (the checks between
+    calls allocate their scratch on the first pass, which bumps the buffer
+    epoch once: capture on call 3, replays on calls 4-5)."""
+    import torch
+    import halo2_svd041_amd as hs
+    ctx = gpu_ctx_factory(P)
+    ta = torch.empty((n, k), dtype=torch.float64, device="cuda:0")
+    tb = torch.empty((k, m), dtype=torch.float64, device="cuda:0")
+    for it in range(5):
+        a, b = _mats(n, k, m, seed=100 * it + n)
+        ta.copy_(torch.from_numpy(a))
+        tb.copy_(torch.from_numpy(b))
+        g = gamma_for(it + 7 * n)
+        hs.verify_mul_witness(ctx, ta, tb, g)
+        _check_all(ctx, a, b, P, g)
+    assert ctx.graph_stats() == (1, 2)
+
+
+@pytest.mark.gpu
+def test_graph_pipelined_calls_keep_gamma_order(gpu_ctx_factory):
+    """Replays queued back to back without a host sync: each call's gamma tables
+    are written on the context stream after the previous graph has finished, so
+    the last call's cells carry the last gamma only."""
+    import torch
+    import halo2_svd041_amd as hs
+    n = k = m = 96
+    P = 32
+    a, b = _mats(n, k, m, seed=5)
+    ta, tb = (torch.tensor(x, dtype=torch.float64, device="cuda:0") for x in (a, b))
+    ctx = gpu_ctx_factory(P)
+    for it in range(8):
+        hs.verify_mul_witness(ctx, ta, tb, gamma_for(it))
+    _check_all(ctx, a, b, P, gamma_for(7))
+    cap, rep = ctx.graph_stats()
+    assert cap == 1 and rep == 6
+
+
+@pytest.mark.gpu
+def test_graph_off_and_invalidation(gpu_ctx_factory):
+    """Graph on / off give identical streams; an option change, a different shape
+    or new input pointers drop the graph (the next calls recapture)."""
+    import torch
+    import halo2_svd041_amd as hs
+    P = 32
+    a, b = _mats(64, 40, 50, seed=9)
+    ta, tb = (torch.tensor(x, dtype=torch.float64, device="cuda:0") for x in (a, b))
+    on, off = gpu_ctx_factory(P), gpu_ctx_factory(P)
+    off.set_option("graph", 0)
+    for it in range(4):
+        g = gamma_for(40 + it)
+        hs.verify_mul_witness(on, ta, tb, g)
+        hs.verify_mul_witness(off, ta, tb, g)
+        assert np.array_equal(on.advice(0), off.advice(0)) and np.array_equal(on.advice(1), off.advice(1))
+        assert on.layout() == off.layout()
+    assert on.graph_stats() == (1, 2) and off.graph_stats() == (0, 0)
+    on.set_option("stage_batch", 1)                      # any option change: recapture
+    for it in range(3):
+        hs.verify_mul_witness(on, ta, tb, gamma_for(50 + it))
+    assert on.graph_stats() == (2, 3)
+    _check_all(on, a, b, P, gamma_for(52))
+    a2, b2 = _mats(30, 40, 20, seed=3)                    # another shape, then back
+    t2a, t2b = (torch.tensor(x, dtype=torch.float64, device="cuda:0") for x in (a2, b2))
+    hs.verify_mul_witness(on, t2a, t2b, gamma_for(60))
+    _check_all(on, a2, b2, P, gamma_for(60))
+    for it in range(3):
+        hs.verify_mul_witness(on, ta, tb, gamma_for(61 + it))
+        _check_all(on, a, b, P, gamma_for(61 + it))
+    assert on.graph_stats() == (3, 4)
