@@ -167,3 +167,26 @@ def test_bit_fold_outlier_block(gpu_ctx_factory, pos, fold):
         ctx.reset()
         hs.verify_mul_witness(ctx, ta, tb, g)
         assert np.array_equal(ctx.advice(0), c0) and np.array_equal(ctx.advice(1), c1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pos", ["first", "last"])
+def test_bit_fold_many_blocks(gpu_ctx_factory, pos):
+    """A quantize launch of 2 103 blocks (4 096 values each; 4100 x 2100 a
+    against a 2100 x 2 b): the fold's last block reads the block maxima in two
+    rounds of 2 048. One outlier in the first or the last block."""
+    import torch
+    import halo2_svd041_amd as hs
+    n, k, m, P = 4100, 2100, 2, 63
+    rs = np.random.RandomState(21)
+    a = rs.uniform(-1e-3, 1e-3, (n, k))
+    b = rs.uniform(-1, 1, (k, m))
+    a[(0, 7) if pos == "first" else (n - 1, k - 1)] = 3.0e7
+    g = gamma_for(5)
+    ctx = gpu_ctx_factory(P)
+    ta, tb = (torch.tensor(x, dtype=torch.float64, device="cuda:0") for x in (a, b))
+    c0, c1 = corc.verify_mul_witness(a, b, P, g)
+    for _ in range(2):
+        ctx.reset()
+        hs.verify_mul_witness(ctx, ta, tb, g)
+        assert np.array_equal(ctx.advice(0), c0) and np.array_equal(ctx.advice(1), c1)
