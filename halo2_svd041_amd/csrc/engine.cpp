@@ -567,6 +567,14 @@ struct svdw_ctx {
     std::vector<uint64_t>* gemm_log = nullptr;   // dry run: offsets of honest_prover_mat_mul
     std::vector<hipEvent_t> deps;           // dependency events (no timing)
     size_t dep_next = 0;
+    // dependency values (stream_dep, "dep_values"): slot i's flag in depflag,
+    // its last written value dep_val[i] (0: the slot went out as an event).
+    // Off by default: with it on, a host-input svd_witness (tests/test_golden.py)
+    // hung on the GPU (cause not found)
+    bool dep_vals = false;
+    DBuf depflag;
+    std::vector<uint32_t> dep_val;
+    uint32_t dep_seq = 0;
     // Stage batches (BatchScope, "stage_batch"): stage launches on a stream with
     // an open batch are collected and issued as k_stage_multi launches when the
     // scope closes, when a stage reads cells a pending stage writes, or before
@@ -635,7 +643,16 @@ static void sync(svdw_ctx* c) {
     hipck(hipStreamSynchronize(c->st2), "hipStreamSynchronize");
     if (c->st3) hipck(hipStreamSynchronize(c->st3), "hipStreamSynchronize");
 }
-// Event recorded on `from`; `to` waits for it (cross-stream dependency).
+// Dependency recorded on `from`; `to` waits for it (cross-stream dependency).
+// The returned handle is waited on later with dep_wait. With "dep_values" on
+// (off by default) the dependency is a value the CP writes into a device flag behind `from`'s
+// work (hipStreamWriteValue32) and a wait for it (hipStreamWaitValue32),
+// not an event record + wait: tools/evgap.hip measured 9.8 us between a kernel
+// and its successor on another stream that way against 17.5 us with an event
+// (and a recorded event also delays the next kernel on `from` by 3 us). Each
+// dependency slot's value only grows (c->dep_seq), so a wait compares >=. A
+// stream being captured into a graph uses events (graph edges).
+static bool dep_values(const svdw_ctx* c) { return c->dep_vals && !c->capturing && c->depflag.p; }
 static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
     if (c->dep_next == c->deps.size()) {
         hipEvent_t e;
@@ -643,13 +660,35 @@ static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
         hipck(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice),
               "hipEventCreate");
         c->deps.push_back(e);
+        c->dep_val.push_back(0);
     }
-    hipEvent_t e = c->deps[c->dep_next++];
+    const size_t i = c->dep_next++;
+    hipEvent_t e = c->deps[i];
     flush_batch(c, from);
     if (g_batch_log) fprintf(stderr, "dep %p -> %p\n", (void*)from, (void*)to);
+    if (dep_values(c) && i < c->depflag.cap / sizeof(uint32_t)) {
+        uint32_t* flag = (uint32_t*)c->depflag.p + i;
+        const uint32_t v = ++c->dep_seq;
+        c->dep_val[i] = v;
+        hipck(hipStreamWriteValue32(from, flag, v, 0), "hipStreamWriteValue32");
+        if (to) hipck(hipStreamWaitValue32(to, flag, v, hipStreamWaitValueGte, 0xffffffffu), "hipStreamWaitValue32");
+        return e;
+    }
+    c->dep_val[i] = 0;
     hipck(hipEventRecord(e, from), "hipEventRecord");
     if (to) hipck(hipStreamWaitEvent(to, e, 0), "hipStreamWaitEvent");
     return e;
+}
+// `s` waits for a dependency stream_dep returned (or any other event)
+static void dep_wait(svdw_ctx* c, hipStream_t s, hipEvent_t e) {
+    for (size_t i = 0; i < c->dep_next && i < c->deps.size(); ++i)
+        if (c->deps[i] == e && c->dep_val[i]) {
+            hipck(hipStreamWaitValue32(s, (uint32_t*)c->depflag.p + i, c->dep_val[i], hipStreamWaitValueGte,
+                                       0xffffffffu),
+                  "hipStreamWaitValue32");
+            return;
+        }
+    hipck(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
 }
 // The second stream at high or normal dispatch priority: on a change the queued
 // work drains and st2 is re-created (one second stream at a time: an idle twin
@@ -1035,7 +1074,7 @@ static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter, hipEvent
             if (gi == upto + 1 && waiter) {
                 stream_dep(c, s, waiter);
                 waiter = nullptr;
-                if (then_wait) hipck(hipStreamWaitEvent(s, then_wait, 0), "hipStreamWaitEvent");
+                if (then_wait) dep_wait(c, s, then_wait);
             }
             if (grp.empty()) continue;
             std::vector<const StageArgs*> ps;
@@ -1068,7 +1107,7 @@ static void flush_batch_blocks(svdw_ctx* c, hipStream_t s) {
         groups.swap(b.groups);
         const uint32_t N = c->blk_n[K], M = c->blk_m[K];
         for (int k = 0; k < K; ++k) {
-            hipck(hipStreamWaitEvent(s, c->blk_ev[k], 0), "hipStreamWaitEvent");
+            dep_wait(c, s, c->blk_ev[k]);
             for (const auto& grp : groups) {
                 std::vector<StageArgs> parts;
                 parts.reserve(grp.size());
@@ -1721,7 +1760,7 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
         if (c->pre.front().off != off) fail(SVDW_EDEVICE, "internal: pre-launched GEMM offset mismatch");
         // (launched on this very stream: already ordered)
         if (c->pre.front().st != c->st)
-            hipck(hipStreamWaitEvent(c->st, c->pre.front().ev, 0), "hipStreamWaitEvent");
+            dep_wait(c, c->st, c->pre.front().ev);
         c->pre.erase(c->pre.begin());
         return cs;
     }
@@ -1899,7 +1938,7 @@ static void gamma_prep(svdw_ctx* c, uint32_t d, const Fr& gamma, hipStream_t s, 
 static void ensure_gamma_vec(svdw_ctx* c, uint32_t d, const Fr& gamma) {
     if (c->dry) return;
     if (c->gp_ev && c->gp_len >= d && fr_eq(c->gp_gamma, gamma)) {
-        if (c->gp_st != c->st) hipck(hipStreamWaitEvent(c->st, c->gp_ev, 0), "hipStreamWaitEvent");
+        if (c->gp_st != c->st) dep_wait(c, c->st, c->gp_ev);
         return;
     }
     gamma_prep(c, d, gamma, c->st);
@@ -2161,7 +2200,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     }
     host_mark(c, "verify_mul b, a scans queued");
     for (hipEvent_t ev : c->wait_before_cs)
-        hipck(hipStreamWaitEvent(c->st, ev, 0), "hipStreamWaitEvent");
+        dep_wait(c, c->st, ev);
     // the c_s scans; each row's is_equal(c_s.g, a.(b.g)) cells from its row
     // total and the a scan's last cell (k_matvec_scan_dpp's eq epilogue)
     Scans cs_;
@@ -2444,11 +2483,11 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         if (c->prod_blk > 1) {
             if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
             pst = c->st3;
-            hipck(hipStreamWaitEvent(c->st3, c->ev_bits, 0), "hipStreamWaitEvent");
+            dep_wait(c, c->st3, c->ev_bits);
         }
         if (c->prod_on_cell) {
         } else if (c->bits_pending) {
-            hipck(hipStreamWaitEvent(c->st2, c->ev_bits, 0), "hipStreamWaitEvent");
+            dep_wait(c, c->st2, c->ev_bits);
         } else {
             stream_dep(c, c->st, c->st2);
         }
@@ -2511,7 +2550,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         // queued behind them with the products on the cell stream) read comes
         // from the registered f64 inputs (f64_view): then st2 starts at once
         const bool from_f64 = c->f64_views && !c->f64reg.empty() && c->prod_on_cell;
-        if (sw.on && !from_f64) hipck(hipStreamWaitEvent(c->st, c->ev_bits, 0), "hipStreamWaitEvent");
+        if (sw.on && !from_f64) dep_wait(c, c->st, c->ev_bits);
         BatchScope bs(c);                   // (desc_order_range reads desc_order_sub: two launches)
         entries_less_than(c, d, max_bits);
         entries_in_desc_order(c, d, max_bits);
@@ -2555,7 +2594,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     // prod_first: the bounds and u.d wait for the products (which then run with
     // the chip to themselves instead of beside the first stage launch)
     if (c->prod_first == 1 && c->prelaunched && !c->gemm_done.empty() && !c->dry)
-        hipck(hipStreamWaitEvent(pc ? c->st2 : c->st, c->gemm_done.back(), 0), "hipStreamWaitEvent");
+        dep_wait(c, pc ? c->st2 : c->st, c->gemm_done.back());
     if (pc) std::swap(c->st, c->st2);
     BatchScope bs(c);
     const bool batched = bs.mine || pc;
@@ -2616,7 +2655,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     // row-blocked products: the batch goes out block by block (flush_batch_blocks);
     // launches outside it wait for all products
     const bool blocked = c->prod_blk > 1 && !c->dry;
-    if (blocked && !bs2.mine) hipck(hipStreamWaitEvent(c->st, c->blk_ev.back(), 0), "hipStreamWaitEvent");
+    if (blocked && !bs2.mine) dep_wait(c, c->st, c->blk_ev.back());
     svdw_mat mvt = honest_prover_mat_mul(c, m.phase, m, vt, bm, bv);
     BigU es = scale_err(err_svd, P), eu = scale_err(err_u, P);
     host_mark(c, "u.d queued");
@@ -2652,8 +2691,12 @@ static void check_svd_phase1(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u, 
 // overwrite buffers the previous call's kernels still read.
 static void after_previous(svdw_ctx* c) {
     if (c->dry) return;
+    if (c->dep_vals && !c->depflag.p && !c->capturing) {   // stream_dep's value flags
+        ensure_buf(c, c->depflag, 1024 * sizeof(uint32_t));
+        hipck(hipMemset(c->depflag.p, 0, c->depflag.cap), "hipMemset");
+    }
     const hipEvent_t e = stream_dep(c, c->st, c->st2);
-    if (c->st3) hipck(hipStreamWaitEvent(c->st3, e, 0), "hipStreamWaitEvent");
+    if (c->st3) dep_wait(c, c->st3, e);
 }
 static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, const double* v,
                                const double* d, uint32_t N, uint32_t M, bool on_device,
@@ -2801,7 +2844,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         // phase 1 beside the products (st3, or st2 while the products run on the
         // cell stream): it waits for the loads, and its c_s scans for the products
         if (p1_overlap && (p1s == c->st3 || c->prod_on_cell)) {
-            hipck(hipStreamWaitEvent(p1s, c->ev_bits, 0), "hipStreamWaitEvent");
+            dep_wait(c, p1s, c->ev_bits);
             c->wait_before_cs = c->gemm_done;
         }
         {
@@ -3012,7 +3055,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     const VMul vm{za, zb, cs};
     if (f64) {
         c->wait_before_cs = {stream_dep(c, c->st, nullptr)};
-        hipck(hipStreamWaitEvent(c->st3, loaded, 0), "hipStreamWaitEvent");
+        dep_wait(c, c->st3, loaded);
         std::swap(c->st, c->st3);
         try {
             verify_mul_many(c, 1, &vm, 1, gamma);
@@ -3343,7 +3386,7 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             vmg_drop(c);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
             for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1], &c->w1c, &c->w1t, &c->w2c, &c->w2t,
-                            &c->bits, &c->gpc, &c->gtab, &c->crtR, &c->gbits, &c->colpart, &c->qfold})
+                            &c->bits, &c->gpc, &c->gtab, &c->crtR, &c->gbits, &c->colpart, &c->qfold, &c->depflag})
                 if (b->p) (void)hipFree(b->p);
             for (int i = 0; i < kMaxScanJobs; ++i) {
                 if (c->wbc[i].p) (void)hipFree(c->wbc[i].p);
@@ -4278,7 +4321,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         sync(c);
         ++c->epoch;                                  // a captured launch sequence may change
         const std::string n(name);
-        if (n == "graph") {                          // captured verify_mul_witness (vm_graph)
+        if (n == "dep_values") {                     // stream_dep: CP-written flags, not events
+            c->dep_vals = value != 0;
+        } else if (n == "graph") {                   // captured verify_mul_witness (vm_graph)
             REQUIRE(value == 0 || value == 1, "graph: 0 or 1");
             c->graph_vm = (int)value;
         } else if (n == "gemm_impl") {

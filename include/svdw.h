@@ -295,6 +295,12 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   3 (constant stores, no view loads either);
  *   "hold_us" 0 | us (svd_witness, verify_mul_witness: the step's streams wait behind a kernel
  *   spinning that long, so the GPU schedule is measured without host gaps).
+ * "dep_values" 0 | 1 (EXPERIMENTAL, off): cross-stream dependencies inside a
+ *   witness as flags the command processor writes behind the producing stream
+ *   and the consuming stream waits for (hipStreamWriteValue32 /
+ *   hipStreamWaitValue32) instead of event records and waits (tools/evgap.hip:
+ *   9.8 vs 17.5 us from a kernel's end to its successor's start on another
+ *   stream). A host-input svd_witness hung with it on; do not enable.
  * "graph" 1 | 0: svdw_verify_mul_witness with device inputs replays a HIP graph
  *   of its launch sequence. The second call of a key (N, K, M, the input
  *   pointers, no allocation or option change since) is captured, later calls
