@@ -407,10 +407,12 @@ def main():
     t0 = time.perf_counter()
     for g in gammas:
         cnt = wl.step(g)
+    t_issued = time.perf_counter()          # host done enqueueing (the GPU may still run)
     sync()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    host_ms = (t_issued - t0) / args.steps * 1e3
     graph_stats = None
     if profile and graph_vm:
         graph_stats = ctx.graph_stats()
@@ -561,6 +563,9 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            # host time to enqueue a step, rank 0 (pipelined: close to ms_per_step
+            # means the host, not the GPU, bounds the step)
+            "host_enqueue_ms_per_step": round(host_ms, 4),
             "higher_is_better": True,
             "scaling": "strong" if rows_mode else "weak",
             "vs_baseline": None,
