@@ -452,21 +452,13 @@ struct svdw_ctx {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
-    uint32_t stage_flags = STAGE_ALIGN;     // STAGE_* (svdw_set_option "stage_align", "stage_inc", ...)
+    uint32_t stage_flags = STAGE_ALIGN;     // STAGE_* (4 KiB-aligned block store windows)
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
-    int prelaunch_at = 0;                   // "prelaunch_at": GEMMs queued before stage 0/1/2
-    int gemm_rt = 1;                        // "gemm_rt": digit counts decided on the device
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
     bool gemm_batched = false;              // this witness's products went out as one batch
-    int res_first = 1;                      // "res_first": cell stream waits for the residue planes
-                                            // (1), not (0), -1: on row-sharded ranks
-    int gemm_batch = 1;                     // "gemm_batch": svd_witness's three products in one launch
-                                            // (1), one by one (0), or -1: batched on row-sharded ranks
-    bool fused_quantize = true;             // "fused_quantize": m, u, v, d in one launch
     bool res_f64 = true;                    // "res_f64": CRT residue planes of m, u, v from the
                                             // f64 inputs, one launch (else from the cells)
     const double* svd_f64[3] = {nullptr, nullptr, nullptr};   // device f64 m, u, v of svd_witness
-    bool d_checks_aside = true;             // "d_checks_aside": d checks on st2 behind the products
     int phase1_overlap = 1;                 // "phase1_overlap": 0 off, 1 on st2 behind the
                                             // GEMMs, 2 on st3 from quantization on
     bool prelaunched = false;               // this witness's products were queued on st2
@@ -477,13 +469,6 @@ struct svdw_ctx {
                                             // critical path sharded, and unsharded it measured
                                             // 2.5 % faster at 1024^2 and 2048^2, neutral at 512^2
     bool prod_on_cell = false;              // this witness's products went on the cell stream
-    int prod_blocks = 1;                    // "prod_blocks": unsharded products in K row blocks on
-                                            // st3, the diff + ids launched per block as each lands
-    int prod_blk = 1;                       // this witness's block count (1: one batch)
-    bool bounds_after = true;               // "bounds_after": with row blocks, the u / v bounds
-                                            // wait for the first block's products
-    std::vector<hipEvent_t> blk_ev;         // block k's products complete (st3)
-    std::vector<uint32_t> blk_n, blk_m;     // block row bounds (K + 1) of N-row / M-row products
     uint32_t hold_us = 0;                   // "hold_us": timing aid, st spins this long first
     Fr ext_gamma{};                          // init_rand of the last verify_mul (equality source 2)
     uint64_t ext_off = 0;                    // its cell in the RLC context
@@ -529,11 +514,7 @@ struct svdw_ctx {
     bool f64_views = true;                  // "f64_views"
     std::vector<F64Src> f64src;
     DBuf colpart;
-    DBuf qfold;                             // k_quantize_multi's fold counters + group maxima                           // k_colsum_f64's per-slice partial sums
-    bool colsum = true;
-    bool bits_fold = true;                  // "bits_fold": bit-length words folded in the quantize launch                     // "colsum": that path (else k_matvec_values on the cells)
-    int prod_first = 0;                     // "prod_first": the first stages wait for the products
-                                            // (1), the bounds but not u.d (2, products on the cell stream)
+    DBuf qfold;                             // k_quantize_multi's fold counters + group maxima
     // second stream: GEMMs overlap the HBM-bound stages; third: phase 1
     hipStream_t st2 = nullptr;
     bool st2_hi = false;                    // st2 is the high-priority stream
@@ -645,13 +626,15 @@ static void sync(svdw_ctx* c) {
 }
 // Dependency recorded on `from`; `to` waits for it (cross-stream dependency).
 // The returned handle is waited on later with dep_wait. With "dep_values" on
-// (off by default) the dependency is a value the CP writes into a device flag behind `from`'s
-// work (hipStreamWriteValue32) and a wait for it (hipStreamWaitValue32),
-// not an event record + wait: tools/evgap.hip measured 9.8 us between a kernel
-// and its successor on another stream that way against 17.5 us with an event
-// (and a recorded event also delays the next kernel on `from` by 3 us). Each
-// dependency slot's value only grows (c->dep_seq), so a wait compares >=. A
-// stream being captured into a graph uses events (graph edges).
+// the dependency is a value written into a device flag behind `from`'s work
+// (hipStreamWriteValue32) and a wait for it (hipStreamWaitValue32), not an
+// event record + wait: tools/probes/evgap.hip measured 9.8 us between a kernel and
+// its successor on another stream that way against 17.5 us with an event (and
+// a recorded event also delays the next kernel on `from` by 3 us). Every
+// write of a slot carries a larger value (c->dep_seq), so a wait compares >=
+// and a wait on a handle from an earlier call is satisfied exactly when an
+// event wait on that handle would be. A stream being captured into a graph
+// uses events (graph edges).
 static bool dep_values(const svdw_ctx* c) { return c->dep_vals && !c->capturing && c->depflag.p; }
 static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
     if (c->dep_next == c->deps.size()) {
@@ -665,7 +648,7 @@ static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
     const size_t i = c->dep_next++;
     hipEvent_t e = c->deps[i];
     flush_batch(c, from);
-    if (g_batch_log) fprintf(stderr, "dep %p -> %p\n", (void*)from, (void*)to);
+    if (g_batch_log) fprintf(stderr, "dep %zu %p -> %p\n", i, (void*)from, (void*)to);
     if (dep_values(c) && i < c->depflag.cap / sizeof(uint32_t)) {
         uint32_t* flag = (uint32_t*)c->depflag.p + i;
         const uint32_t v = ++c->dep_seq;
@@ -679,15 +662,21 @@ static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
     if (to) hipck(hipStreamWaitEvent(to, e, 0), "hipStreamWaitEvent");
     return e;
 }
-// `s` waits for a dependency stream_dep returned (or any other event)
+// `s` waits for a dependency stream_dep returned (or any other event). The
+// slot is looked up over every slot, not only this call's: a handle kept from
+// an earlier call (c->gp_ev, a product's event) whose slot this call has not
+// rewritten yet went out as a value, and its event was never recorded.
 static void dep_wait(svdw_ctx* c, hipStream_t s, hipEvent_t e) {
-    for (size_t i = 0; i < c->dep_next && i < c->deps.size(); ++i)
-        if (c->deps[i] == e && c->dep_val[i]) {
-            hipck(hipStreamWaitValue32(s, (uint32_t*)c->depflag.p + i, c->dep_val[i], hipStreamWaitValueGte,
-                                       0xffffffffu),
-                  "hipStreamWaitValue32");
-            return;
-        }
+    if (!c->capturing && c->depflag.p)
+        for (size_t i = 0; i < c->deps.size(); ++i)
+            if (c->deps[i] == e) {
+                if (!c->dep_val[i]) break;                 // it went out as an event
+                if (g_batch_log) fprintf(stderr, "wait %zu on %p\n", i, (void*)s);
+                hipck(hipStreamWaitValue32(s, (uint32_t*)c->depflag.p + i, c->dep_val[i], hipStreamWaitValueGte,
+                                           0xffffffffu),
+                      "hipStreamWaitValue32");
+                return;
+            }
     hipck(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
 }
 // The second stream at high or normal dispatch priority: on a change the queued
@@ -711,9 +700,9 @@ static void pick_st2(svdw_ctx* c, bool hi) {
 // gemm_priority auto (-1): high for unsharded witnesses with 512 <= max(N, M)
 // < 1024, where the product chain on st2 is the critical path (the cell stream
 // idles ~40 us waiting for the combine at 512^2 P=32). bench.py lines, same box
-// (tools/check_gp2.sh): 512^2 P=32 0.424 -> 0.416 ms; 256^2 P=32 0.189 -> 0.194
-// ms (so off below 512); 1024^2 and 2048 x 1024 within 0.5 % (tools/probe_gp.sh);
-// 8-way shard rank 0.378 -> 0.383 ms (tools/probe_r02b.sh), off when sharded.
+// (tools/probes/check_gp2.sh): 512^2 P=32 0.424 -> 0.416 ms; 256^2 P=32 0.189 -> 0.194
+// ms (so off below 512); 1024^2 and 2048 x 1024 within 0.5 % (tools/probes/probe_gp.sh);
+// 8-way shard rank 0.378 -> 0.383 ms (tools/probes/probe_r02b.sh), off when sharded.
 static void apply_gemm_prio(svdw_ctx* c, uint32_t N, uint32_t M) {
     const bool sharded_ctx = c->shard_world > 1;
     const uint32_t mx = std::max(N, M);
@@ -837,13 +826,15 @@ static void ensure_buf(svdw_ctx* c, DBuf& b, size_t bytes) {
 static void bits_words(svdw_ctx* c, QuantSegs& qs, uint32_t nred, const BitSegs& seg, unsigned* out,
                        bool* folded) {
     *folded = false;
-    if (c->dry || !qs.nseg || qs.nseg < nred || nred > 3 || !c->bits_fold) return;
+    if (c->dry || !qs.nseg || qs.nseg < nred || nred > 3) return;
     for (uint32_t s = 0; s < nred; ++s)
         if (qs.blockmax[s] != qs.blockmax[0] + qs.blk0[s] || qs.blk0[s] != seg.begin[s]) return;
     const uint32_t nblk = qs.blk0[nred];
     if (!c->qfold.p) {
         ensure_buf(c, c->qfold, 256);
-        hipck(hipMemset(c->qfold.p, 0, c->qfold.cap), "hipMemset");   // the counter starts at zero
+        // the counters start at zero, before the quantize launch on st (a
+        // null-stream hipMemset is not ordered against it)
+        hipck(hipMemsetAsync(c->qfold.p, 0, c->qfold.cap, c->st), "hipMemsetAsync");
     }
     BitFold& f = qs.fold;
     f.bm = qs.blockmax[0];
@@ -1095,51 +1086,6 @@ static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter, hipEvent
     }
     if (waiter) stream_dep(c, s, waiter);
 }
-// The batch of stream s (the diff and ids behind row-blocked products) issued
-// block by block: before block k the stream waits for blk_ev[k], and every
-// pending stage runs only its elements in block k's rows (stages over N or M
-// rows; any other stage runs whole in the last block).
-static void flush_batch_blocks(svdw_ctx* c, hipStream_t s) {
-    const int K = c->prod_blk;
-    for (auto& b : c->batches) {
-        if (b.st != s || b.groups.empty()) continue;
-        std::vector<std::vector<svdw_ctx::Pending>> groups;
-        groups.swap(b.groups);
-        const uint32_t N = c->blk_n[K], M = c->blk_m[K];
-        for (int k = 0; k < K; ++k) {
-            dep_wait(c, s, c->blk_ev[k]);
-            for (const auto& grp : groups) {
-                std::vector<StageArgs> parts;
-                parts.reserve(grp.size());
-                double bytes = 0;
-                for (const auto& q : grp) {
-                    StageArgs a = q.a;
-                    const uint32_t cols = a.cols ? a.cols : 1, R = a.e_end / cols;
-                    uint32_t r0, r1;
-                    if (R == N && a.e_end % cols == 0) {
-                        r0 = c->blk_n[k]; r1 = c->blk_n[k + 1];
-                    } else if (R == M && a.e_end % cols == 0) {
-                        r0 = c->blk_m[k]; r1 = c->blk_m[k + 1];
-                    } else {
-                        r0 = k == K - 1 ? 0 : R; r1 = k == K - 1 ? R + 1 : R;
-                    }
-                    const uint32_t e0 = std::max<uint64_t>(a.e_begin, (uint64_t)r0 * cols),
-                                   e1 = (uint32_t)std::min<uint64_t>(a.e_end, (uint64_t)r1 * cols);
-                    if (e1 <= e0) continue;
-                    a.e_begin = e0;
-                    a.e_end = e1;
-                    parts.push_back(a);
-                    bytes += q.bytes * (double)(e1 - e0) / std::max<uint32_t>(q.a.e_end - q.a.e_begin, 1);
-                }
-                if (parts.empty()) continue;
-                std::vector<const StageArgs*> ps;
-                for (const auto& a : parts) ps.push_back(&a);
-                ProfScope pr(c, s, "k_stage:multi", bytes, 0, true);
-                hipck(launch_stage_multi(ps.data(), (int)ps.size(), s), "k_stage_multi");
-            }
-        }
-    }
-}
 // RAII: stage launches on the current stream between construction and end()
 // are batched (k_stage_multi); nested scopes on the same stream join the outer
 // one. Without end() (an exception) the pending stages are dropped.
@@ -1284,7 +1230,7 @@ static svdw_vec put_cell(svdw_ctx* c, uint32_t phase, const Fr& v, bool constant
     // Inside svd_witness (products queued ahead), a one-cell launch on the cell
     // stream would wait for a free CU behind the scans on st2 (15-35 us on the
     // critical path); it depends on nothing, so it goes on st2 itself.
-    const bool aside = c->prelaunched && c->d_checks_aside && !c->dry;
+    const bool aside = c->prelaunched && !c->dry;
     if (aside) std::swap(c->st, c->st2);
     uint64_t off = 0;
     try {
@@ -2090,7 +2036,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     const Fr* wt[kMaxVerifyBatch];
     // b = X^T of an f64 input of svd_witness: X, else null
     auto f64_of = [&](const svdw_mat& b) -> const svdw_ctx::F64Src* {
-        if (!c->colsum || b.cols > 8192) return nullptr;
+        if (b.cols > 8192) return nullptr;
         for (auto& s : c->f64src)
             if (is_transpose_of(b, s.m) && s.m.rs == (int64_t)s.m.cols && s.m.cs == 1) return &s;
         return nullptr;
@@ -2284,18 +2230,17 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
                      8.0 * ((double)rows_m * M + (double)M * M + (double)N * N), 0);
         hipck(launch_residues_f64(q, W, (int)c->P, pst), "k_residues_f64");
     }
-    // res_first: the cell stream waits for the residue planes, which then run
-    // alone instead of beside the first (HBM-saturating) stages
-    // (products on the cell stream: the stages beside them on st2 wait instead)
-    if (c->res_first > 0 || (c->res_first < 0 && sharded(c)))
-        stream_dep(c, pst, pst != c->st ? c->st : c->st2);
+    // the stages beside the products wait for the residue planes, which then
+    // run alone instead of beside the first (HBM-saturating) stages (same box:
+    // 512^2 0.427 -> 0.422 ms, 1024^2 2.098 -> 2.072 ms, 8-way rank 0.36 -> 0.35)
+    stream_dep(c, pst, pst != c->st ? c->st : c->st2);
     const uint8_t* P[3] = {(const uint8_t*)c->digA.p, (const uint8_t*)c->digC.p,
                            (const uint8_t*)c->digB.p};                 // A planes of m, u, v
     const uint32_t stride[3] = {rp_m, rp_u, rp_v}, kp[3] = {kpM, kpN, kpM}, lk[3] = {lkM, lkN, lkM};
     const int wa[3] = {0, 1, 2}, wb[3] = {2, 1, 2};
-    // one launch each for the three GEMMs and combines (same box, tools/probe_opts.sh:
+    // one launch each for the three GEMMs and combines (same box, tools/probes/probe_opts.sh:
     // 512^2 P=32 0.43 -> 0.41 ms, 1024^2 P=63 2.10 -> 2.07 ms; row-sharded ranks too)
-    if (c->gemm_batch > 0 || (c->gemm_batch < 0 && sharded(c))) {
+    {
         // the three products in one GEMM launch and one combine launch (each its
         // own residue scratch): one step of the st2 chain instead of three
         CrtBatch b;
@@ -2335,59 +2280,6 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
             roff += rbytes[g];
         }
         c->gemm_batched = true;
-        if (c->prod_blk > 1) {
-            // K row blocks of all three products, in order on pst: block k's rows
-            // of m.v^T, and the upper tiles of the tile rows of u.u^T / v.v^T in
-            // block k (their mirrors land in later blocks' rows, written before
-            // those blocks' events); the diff + ids of a block start as its event
-            // fires instead of after all products
-            const int K = c->prod_blk;
-            c->blk_ev.clear();
-            c->blk_n.assign(K + 1, 0);
-            c->blk_m.assign(K + 1, 0);
-            for (int k = 1; k < K; ++k) {
-                c->blk_n[k] = std::min(N, ceil_to((uint32_t)((uint64_t)N * k / K), 128));
-                c->blk_m[k] = std::min(M, ceil_to((uint32_t)((uint64_t)M * k / K), 128));
-            }
-            c->blk_n[K] = N;
-            c->blk_m[K] = M;
-            auto start = [](uint32_t bt, uint32_t T) { return bt * T - bt * (bt - 1) / 2; };
-            hipEvent_t last = nullptr;
-            for (int k = 0; k < K; ++k) {
-                CrtBatch bk = b;
-                bk.njobs = 0;
-                for (uint32_t jj = 0; jj < b.njobs; ++jj) {
-                    CrtJob q = b.job[jj];
-                    const int g = jj;                        // unsharded: all three jobs present
-                    const std::vector<uint32_t>& bd = g == 2 ? c->blk_m : c->blk_n;
-                    const uint32_t r0 = bd[k], r1 = bd[k + 1];
-                    if (r1 <= r0) continue;
-                    if (!q.sym) {
-                        q.Ar += (uint64_t)r0 * q.kpad;
-                        q.out += (uint64_t)r0 * q.ors;
-                        q.N = r1 - r0;
-                    } else {
-                        const uint32_t T = (q.N + CT_TILE - 1) / CT_TILE, b0 = r0 / CT_TILE,
-                                       b1 = (r1 + CT_TILE - 1) / CT_TILE;
-                        q.tile0 = start(b0, T);
-                        q.tcount = start(b1, T) - q.tile0;
-                    }
-                    bk.job[bk.njobs++] = q;
-                }
-                if (bk.njobs) {
-                    ProfScope ps(c, pst, "k_gemm_crt:multi", bytes / K, ops / K);
-                    hipck(launch_gemm_crt_multi(bk, pst), "k_gemm_crt_multi");
-                }
-                last = stream_dep(c, pst, nullptr);
-                c->blk_ev.push_back(last);
-            }
-            // the cell stream waits per block (flush_batch_blocks), not here
-            for (int g = 0; g < 3; ++g) {
-                c->pre.push_back({log[g], last, c->st});
-                c->gemm_done.push_back(last);
-            }
-            return;
-        }
         if (b.njobs) {
             ProfScope ps(c, pst, "k_gemm_crt:multi", bytes, ops);
             hipck(launch_gemm_crt_multi(b, pst), "k_gemm_crt_multi");
@@ -2397,25 +2289,6 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
             c->pre.push_back({log[g], done, pst});
             c->gemm_done.push_back(done);
         }
-        return;
-    }
-    for (int g = 0; g < 3; ++g) {
-        const uint32_t rows = (uint32_t)(rr1[g] - rr0[g]), cols = B[g].cols;
-        Fr* out = cellp(c, phase, log[g] + rr0[g] * cols);
-        if (rows) {
-            const bool sym = !sharded(c) && g > 0;          // u.u^T, v.v^T: upper tiles + mirror
-            const uint8_t* Bp = g == 0 ? (const uint8_t*)c->digB.p : P[g];
-            const uint32_t bs = g == 0 ? rp_v : stride[g];
-            // a row block of u / v is a slice of the full planes (m's are this rank's rows)
-            const uint8_t* Ap = P[g] + (g == 0 ? 0 : rr0[g] * (uint64_t)kp[g]);
-            ProfScope ps(c, pst, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * rows * cols,
-                         (double)rows * cols * A[g].cols);
-            hipck(launch_gemm_crt(sym, Ap, Bp, rows, cols, stride[g], bs, kp[g], (uint8_t*)c->crtR.p,
-                                  out, cols, 1, W + wa[g], W + wb[g], lk[g], pst),
-                  "k_gemm_crt");
-        }
-        c->pre.push_back({log[g], stream_dep(c, pst, nullptr), pst});
-        c->gemm_done.push_back(c->pre.back().ev);
     }
 }
 
@@ -2443,7 +2316,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         // integer GEMMs run under the HBM-bound check stages on st. Called after
         // the first check stage is queued, so the device is busy while the host
         // waits for the operand bit lengths.
-        const bool on_device = dev_bits && c->gemm_impl == SVDW_GEMM_MFMA && c->gemm_rt;
+        const bool on_device = dev_bits && c->gemm_impl == SVDW_GEMM_MFMA;
         if (!on_device) fetch_bits(c);
         // residue planes straight from svd_witness's f64 inputs (one launch for m,
         // u and v) when they are on the device and the CRT path applies
@@ -2473,18 +2346,8 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         // loads of m, u, v done: the quantization event when svd_witness recorded
         // one (the cell stream may already hold later stages), else st's position
         // products on the cell stream (prod_cell): already behind the loads there
-        c->prod_on_cell = from_f64 && c->prelaunch_at == 0 && c->d_checks_aside && c->bits_pending &&
-                          (c->prod_cell > 0 || (c->prod_cell < 0 && sharded(c)));
-        // row blocks: unsharded, batched, products beside the cell stream on st3
-        c->prod_blk = c->prod_on_cell && !sharded(c) && c->gemm_batch > 0 && c->prod_blocks > 1
-                          ? std::min<int>(c->prod_blocks, (int)((std::min(N, M) + 127) / 128))
-                          : 1;
+        c->prod_on_cell = from_f64 && c->bits_pending && (c->prod_cell > 0 || (c->prod_cell < 0 && sharded(c)));
         hipStream_t pst = c->prod_on_cell ? c->st : c->st2;
-        if (c->prod_blk > 1) {
-            if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
-            pst = c->st3;
-            dep_wait(c, c->st3, c->ev_bits);
-        }
         if (c->prod_on_cell) {
         } else if (c->bits_pending) {
             dep_wait(c, c->st2, c->ev_bits);
@@ -2531,11 +2394,11 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         c->prelaunched = true;
         host_mark(c, "products queued");
     };
-    if (c->prelaunch_at == 0) prelaunch();
+    prelaunch();
     // what goes aside on st2 (d checks, single constant cells) is read by no
     // later kernel: batched until the end of phase 0 (two launches)
     BatchScope aside(c, c->st2);
-    if (!(c->prelaunched && c->d_checks_aside)) aside.close();
+    if (!c->prelaunched) aside.close();
     {
         // The d checks (three latency-bound stages over r elements) depend on d
         // only: with the products queued ahead they go behind them on st2, off
@@ -2545,7 +2408,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
             bool on;
             Swap(svdw_ctx* cc, bool o) : c(cc), on(o) { if (on) std::swap(c->st, c->st2); }
             ~Swap() { if (on) std::swap(c->st, c->st2); }
-        } sw(c, c->d_checks_aside && c->overlap && known_bits && !c->dry && c->bits_pending);
+        } sw(c, c->overlap && known_bits && !c->dry && c->bits_pending);
         // d loaded -- unless every load these stages (and the bounds and u.d
         // queued behind them with the products on the cell stream) read comes
         // from the registered f64 inputs (f64_view): then st2 starts at once
@@ -2557,7 +2420,6 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         bs.end();
         host_mark(c, "d checks queued");
     }
-    if (c->prelaunch_at == 1) prelaunch();
     // svd_witness's phase 1 on the third stream, enqueued as soon as the products
     // are (their offsets from the dry replay give the payload): with only the
     // first phase-0 stages queued ahead of it, the third stream starts early
@@ -2591,10 +2453,6 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     // d checks, in the same batch), and the cell stream waits for them before
     // the diff, by when they are done.
     const bool pc = c->prod_on_cell && c->prelaunched;
-    // prod_first: the bounds and u.d wait for the products (which then run with
-    // the chip to themselves instead of beside the first stage launch)
-    if (c->prod_first == 1 && c->prelaunched && !c->gemm_done.empty() && !c->dry)
-        dep_wait(c, pc ? c->st2 : c->st, c->gemm_done.back());
     if (pc) std::swap(c->st, c->st2);
     BatchScope bs(c);
     const bool batched = bs.mine || pc;
@@ -2602,7 +2460,6 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     check_mat_entries_bounded(c, u, unit);
     host_mark(c, "bounds(u) queued");
     if (!batched) early_phase1(1);
-    if (c->prelaunch_at == 2) prelaunch();
     check_mat_entries_bounded(c, v, unit);
     host_mark(c, "bounds(v) queued");
     if (!batched) early_phase1(2);
@@ -2631,13 +2488,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         std::swap(c->st, c->st2);
         // the cell stream waits for u.d (and what precedes it on st2), not for
         // the d checks' dependent second group batched behind it
-        // prod_first 2: the bounds and d checks wait for the products, u.d not;
-        // row-blocked products: they wait for the first block, which then has
-        // the chip to itself (beside u.d) and the diff + ids start early
-        hipEvent_t hold_bounds = nullptr;
-        if (c->prod_first == 2 && !c->gemm_done.empty()) hold_bounds = c->gemm_done.back();
-        else if (c->prod_blk > 1 && !c->blk_ev.empty() && c->bounds_after) hold_bounds = c->blk_ev.front();
-        flush_batch(c, c->st2, c->st, hold_bounds);
+        flush_batch(c, c->st2, c->st);
     }
     if (batched) {
         host_mark(c, "bounds(u), bounds(v), u.d queued");
@@ -2652,10 +2503,6 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     // products batched (one completion point): diff and the two ids in one launch
     BatchScope bs2(c);
     if (!c->gemm_batched) bs2.close();
-    // row-blocked products: the batch goes out block by block (flush_batch_blocks);
-    // launches outside it wait for all products
-    const bool blocked = c->prod_blk > 1 && !c->dry;
-    if (blocked && !bs2.mine) dep_wait(c, c->st, c->blk_ev.back());
     svdw_mat mvt = honest_prover_mat_mul(c, m.phase, m, vt, bm, bv);
     BigU es = scale_err(err_svd, P), eu = scale_err(err_u, P);
     host_mark(c, "u.d queued");
@@ -2668,12 +2515,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     check_mat_id(c, uut, q2, eu, &qq);
     svdw_mat vvt = honest_prover_mat_mul(c, m.phase, v, vt, bv, bv);
     check_mat_id(c, vvt, q2, eu, &qq);
-    if (blocked && bs2.mine) {
-        flush_batch_blocks(c, c->st);
-        bs2.close();
-    } else {
-        bs2.end();
-    }
+    bs2.end();
     aside.end();
     host_mark(c, "ids queued");
     return svdw_svd_payload{ut, vt, mvt, uut, vvt};
@@ -2692,8 +2534,13 @@ static void check_svd_phase1(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u, 
 static void after_previous(svdw_ctx* c) {
     if (c->dry) return;
     if (c->dep_vals && !c->depflag.p && !c->capturing) {   // stream_dep's value flags
+        // zeroed on st and complete before the first flag write: a hipMemset
+        // (null stream) is not ordered against the non-blocking streams, and a
+        // zero landing after a write left the waits on it spinning forever
+        // (the round-3 hang of a host-input svd_witness, tests/test_golden.py)
         ensure_buf(c, c->depflag, 1024 * sizeof(uint32_t));
-        hipck(hipMemset(c->depflag.p, 0, c->depflag.cap), "hipMemset");
+        hipck(hipMemsetAsync(c->depflag.p, 0, c->depflag.cap, c->st), "hipMemsetAsync");
+        hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
     }
     const hipEvent_t e = stream_dep(c, c->st, c->st2);
     if (c->st3) dep_wait(c, c->st3, e);
@@ -2711,7 +2558,6 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     if (!c->dry) apply_gemm_prio(c, N, M);
     c->prelaunched = false;
     c->prod_on_cell = false;
-    c->prod_blk = 1;
     c->gemm_batched = false;
     c->gemm_done.clear();
     c->wait_before_cs.clear();
@@ -2755,14 +2601,12 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     c->gp_ev = nullptr;
     if (!c->dry && c->hold_us) {       // every stream of the step waits for st's hold
         hipck(launch_hold(c->hold_us, c->st), "k_hold");
-        if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
         stream_dep(c, c->st, c->st3);
         stream_dep(c, c->st, c->st2);  // (st2's first stages need no load with f64 views)
     }
     if (!c->dry) {
         // gamma^j depends on gamma only: queue it first, on its own stream, so it
         // runs beside quantization instead of on the phase-1 chain
-        if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
         gamma_prep(c, std::max(N, M), gamma, c->st3);
         c->gp_ev = stream_dep(c, c->st3, nullptr);
         c->gp_st = c->st3;
@@ -2771,7 +2615,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     unsigned* dbits = nullptr;
     // m: only this rank's rows are quantized on a row-sharded rank (zkmatrix_new)
     uint64_t mr0 = 0, mr1 = N;
-    if (sharded(c) && on_device && c->fused_quantize) shard_rows(c, N, &mr0, &mr1);
+    if (sharded(c) && on_device) shard_rows(c, N, &mr0, &mr1);
     const uint32_t nbm = (uint32_t)(((mr1 - mr0) * M + kQuantPerBlock - 1) / kQuantPerBlock);
     const uint32_t nbu = (uint32_t)(((uint64_t)N * N + kQuantPerBlock - 1) / kQuantPerBlock);
     const uint32_t nbv = (uint32_t)(((uint64_t)M * M + kQuantPerBlock - 1) / kQuantPerBlock);
@@ -2782,14 +2626,13 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     }
     QuantSegs qs;
     memset(&qs, 0, sizeof qs);
-    QuantSegs* qp = c->fused_quantize ? &qs : nullptr;
+    QuantSegs* qp = &qs;
     svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device, dbits ? dbits + 64 : nullptr, qp, true);
     // (u, v: the rank's rows and column block only, when b.g comes from the f64
     // inputs and so do the products' residue planes: no kernel reads the rest;
     // the conditions of f64_of and of check_svd_phase0's from_f64 prelaunch)
-    const bool part = sharded(c) && on_device && c->colsum && N <= 8192 && M <= 8192 && c->overlap &&
-                      c->res_f64 && c->gemm_crt && c->gemm_rt && c->gemm_impl == SVDW_GEMM_MFMA &&
-                      c->fused_quantize;
+    const bool part = sharded(c) && on_device && N <= 8192 && M <= 8192 && c->overlap && c->res_f64 &&
+                      c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA;
     svdw_mat zu = zkmatrix_new(c, 0, u, N, N, on_device, dbits ? dbits + 64 + nbm : nullptr, qp, false, part);
     svdw_mat zv = zkmatrix_new(c, 0, v, M, M, on_device, dbits ? dbits + 64 + nbm + nbu : nullptr, qp, false,
                                part);
@@ -2838,8 +2681,6 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     bool p1_queued = false;
     auto queue_phase1 = [&](const svdw_svd_payload& pl, bool overlap) {
         const bool p1_overlap = p1mode && overlap;
-        if (p1_overlap && p1mode == 2 && !c->st3)   // created on first use
-            hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
         hipStream_t p1s = p1mode == 2 ? c->st3 : c->st2;
         // phase 1 beside the products (st3, or st2 while the products run on the
         // cell stream): it waits for the loads, and its c_s scans for the products
@@ -2924,7 +2765,6 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     after_previous(c);
     c->prelaunched = false;
     c->prod_on_cell = false;
-    c->prod_blk = 1;
     c->gemm_batched = false;
     c->gemm_done.clear();
     c->wait_before_cs.clear();
@@ -2947,7 +2787,6 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     c->gp_ev = nullptr;
     if (!c->dry && c->hold_us) {       // every stream of the step waits for st's hold
         hipck(launch_hold(c->hold_us, c->st), "k_hold");
-        if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
         stream_dep(c, c->st, c->st3);
         stream_dep(c, c->st, c->st2);
     }
@@ -2957,7 +2796,6 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
                    nbb = (uint32_t)(((uint64_t)K * M + kQuantPerBlock - 1) / kQuantPerBlock);
     c->pows_pre.on = false;
     if (!c->dry) {
-        if (!c->st3) hipck(hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking), "hipStreamCreate");
         // phase 1 opens with verify_mul's one cell and its d - 1 gamma-power
         // elements (verify_mul_many's first appends): k_gamma_prep writes them
         PowCells pc;
@@ -2977,7 +2815,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     }
     QuantSegs qs;
     memset(&qs, 0, sizeof qs);
-    QuantSegs* qp = c->fused_quantize && on_device ? &qs : nullptr;
+    QuantSegs* qp = on_device ? &qs : nullptr;
     const svdw_mat za = zkmatrix_new(c, 0, a, N, K, on_device, dbits ? dbits + 64 : nullptr, qp);
     const svdw_mat zb = zkmatrix_new(c, 0, b, K, M, on_device, dbits ? dbits + 64 + nba : nullptr, qp);
     BitSegs seg{};
@@ -3016,7 +2854,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     // stream from the loads on: its one / gamma-power cells and the b and a
     // scans run beside the product, only the c_s scans wait for it
     const bool f64 = on_device && !c->dry && c->res_f64 && c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA &&
-                     c->gemm_rt && K <= 8192 && qs.nseg == 2;
+                     K <= 8192 && qs.nseg == 2;
     hipEvent_t loaded = nullptr;
     if (f64) {
         loaded = stream_dep(c, c->st, nullptr);
@@ -3358,6 +3196,7 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
         c->device = p->device;
         c->dry = p->device < 0;
         if (const char* h = getenv("SVDW_HOST_TRACE")) c->host_trace = atoi(h) != 0;
+        if (const char* d = getenv("SVDW_DEP_VALUES")) c->dep_vals = atoi(d) != 0;   // default override (tests)
         if (const char* g = getenv("SVDW_GEMM"))
             c->gemm_impl = (!strcmp(g, "valu") || !strcmp(g, "dot4")) ? SVDW_GEMM_VALU : SVDW_GEMM_MFMA;
         if (!c->dry) {
@@ -3365,6 +3204,9 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
             c->st_cell = c->st;
             if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking);
+            // the third stream exists from the start: one created lazily inside a
+            // call would not wait for what st already waits for (svdw_stream_wait)
+            if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipHostMalloc((void**)&c->hbits, 64 * sizeof(uint32_t),
                                                hipHostMallocDefault);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bits, hipEventDisableTiming | hipEventReleaseToDevice);
@@ -3827,7 +3669,10 @@ int svdw_parse_svd_input_device(svdw_ctx* c, const void* text, uint64_t len, int
             char buf[16];
             for (int i = 0; i <= 308; ++i) { snprintf(buf, sizeof buf, "1e%d", i); p10[i] = strtod(buf, nullptr); }
             ensure_buf(c, c->ing_p10, sizeof(double) * 309);
-            hipck(hipMemcpy(c->ing_p10.p, p10.data(), sizeof(double) * 309, hipMemcpyHostToDevice), "H2D");
+            // on st, complete before p10 goes out of scope (a null-stream copy
+            // is not ordered against the parse launches on st)
+            hipck(hipMemcpyAsync(c->ing_p10.p, p10.data(), sizeof(double) * 309, hipMemcpyHostToDevice, s), "H2D");
+            hipck(hipStreamSynchronize(s), "hipStreamSynchronize");
         }
         ensure_buf(c, c->ing_x, sizeof(ig::Xfer) * nc);
         ensure_buf(c, c->ing_e, sizeof(ig::Entry) * (nc + 1));
@@ -4333,14 +4178,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             REQUIRE(value >= 16 && value <= 256 && value % 16 == 0,
                     "stage_elems: a multiple of 16 in [16, 256]");
             c->stage_elems = (uint32_t)value;
-        } else if (n == "stage_align") {
-            c->stage_flags = (c->stage_flags & ~STAGE_ALIGN) | (value ? STAGE_ALIGN : 0);
-        } else if (n == "stage_probe") {             // timing probe, wrong cells (tools/ab.py)
-            REQUIRE(value >= 0 && value <= 3,
-                    "stage_probe: 0 off, 1 skip phase A, 2 constant stores, 3 constant stores, no loads");
-            c->stage_flags = (c->stage_flags & ~(STAGE_PROBE_NOA | STAGE_PROBE_CONST | STAGE_PROBE_NOLD)) |
-                             (value == 1 ? STAGE_PROBE_NOA : value == 2 ? STAGE_PROBE_CONST
-                              : value == 3 ? (STAGE_PROBE_CONST | STAGE_PROBE_NOLD) : 0);
         } else if (n == "gemm_priority") {
             // second (GEMM) stream priority: -1 auto (see apply_gemm_prio), 0 normal, 1 high
             REQUIRE(value >= -1 && value <= 1, "gemm_priority: -1, 0 or 1");
@@ -4349,10 +4186,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "prod_cell") {
             REQUIRE(value >= -1 && value <= 1, "prod_cell: -1, 0 or 1");
             c->prod_cell = (int)value;
-        } else if (n == "d_checks_aside") {
-            c->d_checks_aside = value != 0;
-        } else if (n == "fused_quantize") {
-            c->fused_quantize = value != 0;
         } else if (n == "stage_priority") {
             // cell stream priority: 0 normal, 1 high (its blocks dispatch ahead of the
             // products / phase-1 scans on the second stream)
@@ -4386,37 +4219,13 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_crt = (int)value;
         } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
             c->stage_batch = value != 0;
-        } else if (n == "bounds_after") {
-            c->bounds_after = value != 0;
-        } else if (n == "prod_blocks") {
-            REQUIRE(value >= 1 && value <= 64, "prod_blocks: 1..64");
-            c->prod_blocks = (int)value;
         } else if (n == "f64_views") {
             c->f64_views = value != 0;
-        } else if (n == "bits_fold") {
-            c->bits_fold = value != 0;
-        } else if (n == "res_first") {
-            REQUIRE(value >= -1 && value <= 1, "res_first: -1 (auto), 0 or 1");
-            c->res_first = (int)value;
-        } else if (n == "gemm_batch") {
-            REQUIRE(value >= -1 && value <= 1, "gemm_batch: -1 (auto), 0 or 1");
-            c->gemm_batch = (int)value;
-        } else if (n == "gemm_rt") {
-            REQUIRE(value == 0 || value == 1, "gemm_rt: 0 or 1");
-            c->gemm_rt = (int)value;
-        } else if (n == "prelaunch_at") {
-            REQUIRE(value >= 0 && value <= 2, "prelaunch_at: 0, 1 or 2");
-            c->prelaunch_at = (int)value;
         } else if (n == "p1_at") {
             REQUIRE(value >= -1 && value <= 3, "p1_at: -1 (auto), 0, 1, 2 or 3");
             c->p1_at = (int)value;
         } else if (n == "overlap") {
             c->overlap = value != 0;
-        } else if (n == "colsum") {                 // row-sharded b.g from the f64 inputs
-            c->colsum = value != 0;
-        } else if (n == "prod_first") {
-            REQUIRE(value >= 0 && value <= 2, "prod_first: 0, 1 or 2");
-            c->prod_first = (int)value;
         } else {
             fail(SVDW_EINVAL, "unknown option " + n);
         }

@@ -105,6 +105,10 @@ __device__ __forceinline__ uint32_t signed_bits(const Fr& x) {
 // arrival of a group arrives on the global counter, the last of those sees
 // every maximum with agent-scope loads. An agent-scope release fence instead
 // writes back the whole L2 (the block's cells) per block: 670 us instead of 19.
+// Hardware assumption (gfx950, several XCDs with their own L2): agent-scope
+// atomics are performed at the device coherence point, not in an XCD's L2, so
+// a maximum exchanged before the arrival is what the last block's agent-scope
+// load returns; the last arrival's counter update is an acquire besides.
 // Called after the block's stores are issued, so its latency overlaps them.
 __device__ __forceinline__ void bits_fold(const BitFold& f, uint32_t blk, uint32_t bmax) {
     __shared__ uint32_t last, red[4][4];
@@ -116,7 +120,8 @@ __device__ __forceinline__ void bits_fold(const BitFold& f, uint32_t blk, uint32
         if (lst) {
             __hip_atomic_store(f.cnt + 1 + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const uint32_t ng = min(f.nblk, 8u);
-            lst = __hip_atomic_fetch_add(f.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+            // acquire on the last arrival only (a cache invalidate, no write-back)
+            lst = __hip_atomic_fetch_add(f.cnt, 1u, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
         }
         last = lst;
     }
@@ -636,7 +641,7 @@ __device__ __forceinline__ Prefetch stage_loads(const StageArgs& a, uint32_t blk
     const uint32_t e0 = a.e_begin + blk * E;
     const uint32_t ne = min(E, a.e_end - e0), e = e0 + threadIdx.x;
     Prefetch f{fr_zero(), fr_zero(), false, false};
-    if (threadIdx.x < ne && !(a.flags & STAGE_PROBE_NOLD)) {
+    if (threadIdx.x < ne) {
         const uint32_t pi = e / a.cols, pj = e - pi * a.cols;
         const DView& v0 = a.view[0];
         if (v0.ptr && v0.mode == VIEW_STRIDED && pi < v0.rows && pj < v0.cols) {
@@ -669,32 +674,18 @@ __device__ __forceinline__ void stage_chunk(const StageArgs& a, const StageLds& 
     const uint32_t ne = min(E, a.e_end - e0), e = e0 + tid;
     // ---- phase A: per-element micro-ops (constants / ops / views read from LDS:
     // dynamic indexing into the by-value kernel argument would go to scratch)
-    if (tid < ne && !(a.flags & (STAGE_PROBE_NOA | STAGE_PROBE_CONST)))
+    if (tid < ne)
         element_program(a, e, L.sV + tid * stage_elem_words(nv), L.sK, L.sMo, L.sVw, f.v0, f.in0, f.v1, f.in1);
     __syncthreads();
 
     // ---- phase B: advice cells, then lookup cells
     uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
     uint4* outL = a.L ? reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L) : nullptr;
-    if (a.flags & STAGE_PROBE_CONST) {
-        const uint4 z = make_uint4(f.v0.w[0] ^ f.v1.w[0], 0, 0, 0);
-        for (uint32_t hc = tid; hc < 2 * ne * a.C; hc += blockDim.x) outA[hc] = z;
-        if (a.L)
-            for (uint32_t hc = tid; hc < 2 * ne * a.L; hc += blockDim.x) outL[hc] = z;
-    } else {
-        const uint32_t vb0 = (uint32_t)(L.sV - smem);
-        if (a.flags & STAGE_ALIGN) {
-            stream_cells_desc<true>(outA, 2 * ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv);
-            if (a.L)
-                stream_cells_desc<true>(outL, 2 * ne * a.L, L.sHD + 2 * a.C, L.sHM + 2 * a.C, a.L,
-                                        a.ldiv_magic, smem, vb0, nv);
-        } else {
-            stream_cells_desc<false>(outA, 2 * ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv);
-            if (a.L)
-                stream_cells_desc<false>(outL, 2 * ne * a.L, L.sHD + 2 * a.C, L.sHM + 2 * a.C, a.L,
-                                         a.ldiv_magic, smem, vb0, nv);
-        }
-    }
+    const uint32_t vb0 = (uint32_t)(L.sV - smem);
+    stream_cells_desc<true>(outA, 2 * ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv);
+    if (a.L)
+        stream_cells_desc<true>(outL, 2 * ne * a.L, L.sHD + 2 * a.C, L.sHM + 2 * a.C, a.L, a.ldiv_magic, smem,
+                                vb0, nv);
 }
 
 // One block of a stage: `a` supplies the scalar fields and the views (StageArgs

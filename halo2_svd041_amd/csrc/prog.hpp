@@ -65,11 +65,7 @@ struct SlotOp {
 };
 static constexpr uint8_t KSRC = 0x80;
 
-// Timing probes (wrong cells; tools/ab.py only): skip phase A / store a constant
-static constexpr uint32_t STAGE_PROBE_NOA = 64;
-static constexpr uint32_t STAGE_PROBE_CONST = 128;
 static constexpr uint32_t STAGE_ALIGN = 256;     // 4 KiB-aligned block store windows
-static constexpr uint32_t STAGE_PROBE_NOLD = 1024;  // timing probe: no view loads either (with CONST)
 
 static constexpr int kMaxViews = 2;
 static constexpr int kMaxMicro = 16;

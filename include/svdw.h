@@ -243,10 +243,9 @@ int svdw_verify_mul_witness(svdw_ctx* ctx, const double* a, const double* b, uin
 #define SVDW_GEMM_MFMA 0
 #define SVDW_GEMM_VALU 1
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
-/* Tuning knobs (bit-identical results for every value; defaults first):
+/* Options (svdw_set_option; 16 of them). Tuning knobs, bit-identical results
+ * for every value, defaults first:
  *   "gemm_impl" 0 | 1; "gemm_crt" 1 | 0 (CRT or digit-plane matrix-core GEMM);
- *   "gemm_rt" 1 | 0 (svd_witness: GEMM sizes decided on the device from the
- *   quantized operands' bit lengths, no host round trip);
  *   "overlap" 1 | 0 (the three check_svd_phase0 products run ahead on a second
  *   stream); "phase1_overlap" 1 | 2 | 0 (svd_witness: phase 1 runs on the
  *   second stream behind the products / on a third stream from quantization
@@ -254,60 +253,47 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   a row-sharded context and when max(N, M) < 1024); "p1_at" -1 | 0 | 1 | 2 | 3
  *   (with phase 1 on the third stream: queued after the first 0 / 1 / 2
  *   phase-0 stages, 3 after all of phase 0; -1: 0 on a rank of a >= 4-way shard, 3 of a
- *   2-3-way shard, else 1); "prelaunch_at" 0 | 1 | 2 (how many phase-0 stages
- *   are queued before them); "gemm_priority" -1 | 0 | 1 (second stream priority:
+ *   2-3-way shard, else 1); "gemm_priority" -1 | 0 | 1 (second stream priority:
  *   -1 auto = high for unsharded witnesses with 512 <= max(N, M) < 1024, where
- *   the product chain is the critical path; 0 normal; 1 high); "stage_priority" 0 | 1 (cell stream priority);
- *   "fused_quantize" 1 | 0 (m, u, v, d quantized in one launch when resident
- *   in HBM);
+ *   the product chain is the critical path; 0 normal; 1 high); "stage_priority"
+ *   0 | 1 (cell stream priority);
  *   "stage_elems" 256 (elements per stage block, multiple of 16 in [16, 256]);
- *   "stage_align" 1 | 0 (each block's store windows aligned to 4 KiB);
- *   "prod_blocks" 1 | K (unsharded svd_witness with device inputs: the three
- *   products in K row blocks on a side stream, the diff and ids launched per
- *   block as each block lands; "bounds_after" 1 | 0: the u / v bounds wait
- *   for the first block. Measured 1024^2 -1 to +4 %, 2048^2 +1 %, 4096^2 -3 %
- *   against 1: off by default);
  *   "f64_views" 1 | 0 (svd_witness / verify_mul_witness with device inputs:
  *   stages and row scans read the loaded matrices from the f64 inputs,
  *   quantized in registers, instead of waiting for the quantized cells);
- *   "bits_fold" 1 | 0 (the operand bit-length words folded inside the quantize
- *   launch, or by k_bits_reduce, a launch of its own);
- *   "colsum" 1 | 0 (row-sharded svd_witness: every entry of the Freivalds
- *   vectors b.g from the f64 inputs, column-parallel, or 0 from the cells);
  *   "res_f64" 1 | 0 (svd_witness with inputs in HBM: the CRT residue planes of
  *   m, u, v built from the f64 inputs in one launch, or from the quantized cells);
  *   "stage_batch" 1 | 0 (independent stages share k_stage_multi launches: the
  *   u / v bounds and u.d, the d checks and constant cells, verify_mul's one cells
  *   and gamma powers, the is_equal rows; split automatically where a stage reads
- *   cells a pending one writes); "gemm_batch" 1 | 0 | -1 (svd_witness's three
- *   products in one GEMM and one combine launch; -1: on row-sharded contexts); "prod_cell" 1 | 0 | -1 (svd_witness with
+ *   cells a pending one writes); "prod_cell" 1 | 0 | -1 (svd_witness with
  *   device inputs: the products on the cell stream and the u / v bounds and u.d
- *   beside them; -1 on row-sharded contexts only); "res_first"
- *   1 | 0 | -1 (the stages beside the products wait for the residue planes,
- *   which then run alone; -1: on row-sharded contexts only; measured 1-3 %
- *   faster at 512^2, 1024^2 and on 8-way shard ranks).
- * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:
- *   phase 1 starts with the two ctx_gate constant cells [1, 0] that
- *   examples/svd_example.rs:183's rlc.load_rlc_cache(.., 1) appends as recalled
- *   from axiom-eth's RlcChip, parity unpinned; init_rand is then RLC cell 2).
- * Timing aids (NOT bit-identical, for A/B measurements only): "stage_probe"
- *   0 | 1 (skip the stage programs) | 2 (store a constant instead of cells) |
- *   3 (constant stores, no view loads either);
- *   "hold_us" 0 | us (svd_witness, verify_mul_witness: the step's streams wait behind a kernel
- *   spinning that long, so the GPU schedule is measured without host gaps).
- * "dep_values" 0 | 1 (EXPERIMENTAL, off): cross-stream dependencies inside a
- *   witness as flags the command processor writes behind the producing stream
- *   and the consuming stream waits for (hipStreamWriteValue32 /
- *   hipStreamWaitValue32) instead of event records and waits (tools/evgap.hip:
- *   9.8 vs 17.5 us from a kernel's end to its successor's start on another
- *   stream). A host-input svd_witness hung with it on; do not enable.
- * "graph" 1 | 0: svdw_verify_mul_witness with device inputs replays a HIP graph
+ *   beside them; -1 on row-sharded contexts only);
+ *   "dep_values" 0 | 1: cross-stream dependencies inside a witness as flags
+ *   written behind the producing stream and waited for by the consuming one
+ *   (hipStreamWriteValue32 / hipStreamWaitValue32) instead of event records
+ *   and waits (tools/probes/evgap.hip: 9.8 vs 17.5 us from a kernel's end to its
+ *   successor's start on another stream);
+ *   "graph" 1 | 0: svdw_verify_mul_witness with device inputs replays a HIP graph
  *   of its launch sequence. The second call of a key (N, K, M, the input
  *   pointers, no allocation or option change since) is captured, later calls
  *   of the key replay it with one hipGraphLaunch; k_gamma_prep (gamma's tables,
  *   and the one / gamma-power cells) is queued on the context stream ahead of
  *   the graph, so gamma is never part of it. Off while profiling or hold_us is
- *   set. The cells are bit-identical either way. */
+ *   set.
+ * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:
+ *   phase 1 starts with the two ctx_gate constant cells [1, 0] that
+ *   examples/svd_example.rs:183's rlc.load_rlc_cache(.., 1) appends as recalled
+ *   from axiom-eth's RlcChip, parity unpinned; init_rand is then RLC cell 2).
+ * Test hook: "hold_us" 0 | us (svd_witness, verify_mul_witness: the step's
+ *   streams wait behind a kernel spinning that long, so the GPU schedule is
+ *   measured without host gaps and a missing cross-stream dependency shows).
+ * Fixed since round 4 (measured, no longer options): products batched into one
+ *   GEMM and one combine launch, residue planes before the stages beside them,
+ *   the d checks and constant cells on the second stream, m, u, v, d quantized
+ *   in one launch with the bit-length words folded inside it, b.g of a
+ *   row-sharded rank from the f64 inputs, 4 KiB-aligned stage store windows,
+ *   GEMM sizes decided on the device. */
 int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);
 /* Captures and replays of the verify_mul_witness graph ("graph") so far. */
 int svdw_graph_stats(svdw_ctx* ctx, uint64_t* captures, uint64_t* replays);

@@ -166,14 +166,12 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                     | (int(got[i, j, 3]) << 192) == want
 
 
-@pytest.mark.parametrize("opts", [{"gemm_rt": 0}, {"prelaunch_at": 2}, {"gemm_crt": 0},
-                                  {"stage_elems": 64}, {"stage_elems": 192},
+@pytest.mark.parametrize("opts", [{"gemm_crt": 0}, {"stage_elems": 64}, {"stage_elems": 192},
                                   {"phase1_overlap": 0}, {"phase1_overlap": 2},
-                                  {"stage_align": 0}, {"stage_align": 0, "stage_elems": 64},
                                   {"overlap": 0}, {"stage_priority": 1},
                                   {"gemm_priority": 1}, {"gemm_priority": 0},
-                                  {"fused_quantize": 0}, {"d_checks_aside": 0},
-                                  {"stage_batch": 0}, {"gemm_batch": 0}, {"res_first": 1}, {"colsum": 0}])
+                                  {"stage_batch": 0}, {"dep_values": 1}, {"dep_values": 1, "phase1_overlap": 2},
+                                  {"gemm_impl": 1}, {"res_f64": 0}, {"f64_views": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
@@ -349,20 +347,21 @@ def _on_device(*xs):
 
 @pytest.mark.parametrize("f64v", [1, 0])
 @pytest.mark.parametrize("res", [1, 0])
-@pytest.mark.parametrize("fused", [1, 0])
+@pytest.mark.parametrize("dv", [0, 1])
 @pytest.mark.parametrize("N,M,P", [(130, 97, 63), (64, 200, 32)])
-def test_device_inputs_parity(gpu_ctx_factory, fused, res, f64v, N, M, P):
+def test_device_inputs_parity(gpu_ctx_factory, dv, res, f64v, N, M, P):
     """The bench path: m, u, v, d already resident in HBM (torch float64 CUDA
-    tensors), quantized in one fused launch (or four); the CRT residue planes of
+    tensors), quantized in one fused launch; the CRT residue planes of
     m, u, v built from the f64 inputs in one launch (res 1) or from the
     quantized cells (res 0); the stages and row scans reading the loaded
     matrices through f64 views (f64v 1: quantized in registers, no wait for the
-    cells) or the cells; witness vs the oracle."""
+    cells) or the cells; dependencies between the streams as events or values
+    (dv, dep_values); witness vs the oracle."""
     import halo2_svd041_amd as hs
     m, u, d, v = gen_svd_input(N, M, seed=N * M)
     g = gamma_for(N + M)
     ctx = gpu_ctx_factory(P)
-    ctx.set_option("fused_quantize", fused)
+    ctx.set_option("dep_values", dv)
     ctx.set_option("res_f64", res)
     ctx.set_option("f64_views", f64v)
     dm, du, dv, dd = _on_device(m, u, v, d)
@@ -424,8 +423,8 @@ def test_row_sharded_device_inputs_parity(gpu_ctx_factory, N, M, P, world):
 @pytest.mark.parametrize("world,opts", [(1, {"prod_cell": 1}), (1, {"prod_cell": 1, "stage_batch": 0}),
                                         (1, {"prod_cell": 1, "p1_at": 1}), (1, {"prod_cell": 1, "hold_us": 50}),
                                         (3, {"prod_cell": 0}), (3, {"prod_cell": 1, "stage_batch": 0}),
-                                        (4, {"prod_cell": 1, "gemm_batch": 0}), (1, {"gemm_batch": 0}),
-                                        (5, {"prod_cell": 0}), (4, {"colsum": 0}), (1, {"prod_cell": 0})])
+                                        (4, {"prod_cell": 1, "dep_values": 1}), (1, {"dep_values": 1}),
+                                        (5, {"prod_cell": 0}), (4, {"p1_at": 3}), (1, {"prod_cell": 0})])
 def test_products_on_cell_stream_parity(gpu_ctx_factory, world, opts):
     """prod_cell: the products on the cell stream, the u / v bounds and u.d on
     st2 beside them (default on row-sharded ranks), with device inputs (the
@@ -474,8 +473,8 @@ def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device, hol
     m, u, d, v = gen_svd_input(N, M, seed=N + M + P)
     g = gamma_for(N * M)
     ctx = gpu_ctx_factory(P)
-    if hold < 0:                                  # (and the products in 4 row blocks)
-        ctx.set_option("prod_blocks", 4)
+    if hold < 0:                                  # (and value dependencies between the streams)
+        ctx.set_option("dep_values", 1)
         hold = -hold
     if hold:
         # a first witness of other inputs allocates every buffer (allocation
@@ -626,26 +625,3 @@ def test_field_mat_times_vec_parity(gpu_ctx_factory, N, M, LB, seed):
     f64 = A @ v1
     for i in range(N):
         assert abs(po.to_signed(oq[i].value) / 2.0 ** P - f64[i]) <= 1e-6 * max(1.0, abs(f64[i]))
-
-
-@pytest.mark.parametrize("N,M,P,K", [(256, 200, 63, 2), (300, 260, 32, 3), (260, 300, 63, 8)])
-def test_row_blocked_products_parity(gpu_ctx_factory, N, M, P, K):
-    """prod_blocks: the three products in K row blocks on the third stream (the
-    upper tiles of u.u^T / v.v^T by tile rows, mirrors into later blocks), the
-    diff and ids launched block by block as each block's event fires. A first
-    witness of other inputs allocates everything, then the streams are held
-    until the whole witness is queued, so a block stage that ran ahead of its
-    products would read the first witness's cells."""
-    import halo2_svd041_amd as hs
-    m, u, d, v = gen_svd_input(N, M, seed=N + 7 * M + K)
-    g = gamma_for(N + M + K)
-    ctx = gpu_ctx_factory(P)
-    ctx.set_option("prod_blocks", K)
-    m2, u2, d2, v2 = gen_svd_input(N, M, seed=N + 7 * M + K + 1)
-    hs.svd_witness(ctx, *_on_device(m2, u2, v2, d2), gamma_for(1))
-    ctx.sync()
-    ctx.reset()
-    ctx.set_option("hold_us", 2000)
-    hs.svd_witness(ctx, *_on_device(m, u, v, d), g)
-    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
-    _assert_streams(ctx, a0, l0, a1)

@@ -135,12 +135,11 @@ def test_fused_verify_mul_witness_full_stream(gpu_ctx_factory, n, k, m, P, dev):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("pos", ["first", "middle", "last", "b_last"])
-@pytest.mark.parametrize("fold", [1, 0])
-def test_bit_fold_outlier_block(gpu_ctx_factory, pos, fold):
+def test_bit_fold_outlier_block(gpu_ctx_factory, pos):
     """The operand bit-length words decide the GEMM's modulus count. One large
     entry in one quantize block (first / middle / last block of a, last of b)
-    must reach the word through the in-launch fold (bits_fold 1) as through
-    k_bits_reduce (0): too few moduli would change c_s. 300 x 200 x 150 spans
+    must reach the word through the in-launch fold: too few moduli would
+    change c_s. 300 x 200 x 150 spans
     several 4096-value blocks; every run repeats twice (the fold's counter is
     reset by its last arrival)."""
     import torch
@@ -160,7 +159,6 @@ def test_bit_fold_outlier_block(gpu_ctx_factory, pos, fold):
         b[k - 1, m - 1] = -big
     g = gamma_for(n + m)
     ctx = gpu_ctx_factory(P)
-    ctx.set_option("bits_fold", fold)
     ta, tb = (torch.tensor(x, dtype=torch.float64, device="cuda:0") for x in (a, b))
     c0, c1 = corc.verify_mul_witness(a, b, P, g)
     for _ in range(2):

@@ -1,12 +1,12 @@
 #!/bin/bash
-# Same-box A/B of libsvdw_base.so (tools/build_base.sh) against the working
+# Same-box A/B of libsvdw_base.so (tools/probes/build_base.sh) against the working
 # tree's build at 1024^2 P=63, 512^2 P=32 and an 8-way shard rank.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 R=${ROUNDS:-3}
-bash tools/ab_lib.sh $R --no-check --no-profile || exit $?
-bash tools/ab_lib.sh $R --no-check --no-profile --n 512 --p 32 || exit $?
+bash tools/probes/ab_lib.sh $R --no-check --no-profile || exit $?
+bash tools/probes/ab_lib.sh $R --no-check --no-profile --n 512 --p 32 || exit $?
 for i in $(seq 1 $R); do
   for v in base new; do
     if [ $v = base ]; then lib=$PWD/halo2_svd041_amd/libsvdw_base.so; else lib=$PWD/halo2_svd041_amd/libsvdw.so; fi

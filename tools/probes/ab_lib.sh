@@ -1,9 +1,9 @@
 #!/bin/bash
-# Same-box A/B of two library builds: base (libsvdw_base.so, tools/build_base.sh)
+# Same-box A/B of two library builds: base (libsvdw_base.so, tools/probes/build_base.sh)
 # and the working tree's libsvdw.so, alternating short bench runs.
-# Usage (on the GPU box): bash tools/ab_lib.sh [rounds] [bench args...]
+# Usage (on the GPU box): bash tools/probes/ab_lib.sh [rounds] [bench args...]
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=${1:-3}; shift || true
 mkdir -p gpurun_out
 for i in $(seq 1 "$R"); do

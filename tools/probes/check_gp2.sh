@@ -2,7 +2,7 @@
 # GPU tests + smoke, then bench.py lines of the small shapes with the automatic
 # product-stream priority (gemm_priority -1) against priority forced off (0).
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
   timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }

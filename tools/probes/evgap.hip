@@ -4,7 +4,7 @@
 // cross-stream event wait, an event attached to the launch itself via
 // hipExtLaunchKernelGGL, stream wait/write-value). Everything is enqueued
 // behind a spinning kernel first, so the gaps are GPU-side only.
-//   hipcc --offload-arch=gfx950 -O2 tools/evgap.hip -o /tmp/evgap && /tmp/evgap
+//   hipcc --offload-arch=gfx950 -O2 tools/probes/evgap.hip -o /tmp/evgap && /tmp/evgap
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <algorithm>

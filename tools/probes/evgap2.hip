@@ -8,7 +8,7 @@
 //   - big kernel argument: the successor takes a 3.5 KiB by-value argument
 //     (k_stage_multi's StageMulti is of that size);
 //   - timestamps: min start from s_memrealtime (100 MHz) per block.
-//   hipcc --offload-arch=gfx950 -O2 tools/evgap2.hip -o /tmp/evgap2 && /tmp/evgap2
+//   hipcc --offload-arch=gfx950 -O2 tools/probes/evgap2.hip -o /tmp/evgap2 && /tmp/evgap2
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>

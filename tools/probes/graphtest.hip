@@ -1,6 +1,6 @@
 // Probe: does a hipGraph captured across two streams replay correctly, and do
 // hipEventRecord calls captured on the origin stream time its kernels on replay?
-//   hipcc --offload-arch=gfx950 -O2 tools/graphtest.hip -o tools/graphtest && ./tools/graphtest
+//   hipcc --offload-arch=gfx950 -O2 tools/probes/graphtest.hip -o tools/probes/graphtest && ./tools/probes/graphtest
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <chrono>

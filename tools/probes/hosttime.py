@@ -3,7 +3,7 @@
 pipelined step time, at 512^2 P=32 and 1024^2 P=63. When the host call is as
 long as the step, the step is host-bound (launch overhead), not GPU-bound.
 
-    python tools/hosttime.py
+    python tools/probes/hosttime.py
 """
 import sys, time, os
 WORLD = int(os.environ.get("HT_WORLD", "1"))   # >1: time rank 0 of a row-sharded witness

@@ -2,7 +2,7 @@
 """Per-kernel durations of one svd_witness configuration with the streams
 serialised (overlap 0, phase1_overlap 0): each kernel alone on the GPU.
 
-    python tools/kprobe.py [--n 1024] [--p 63] [--world 8 --rank 0] [--opt k=v ...]
+    python tools/probes/kprobe.py [--n 1024] [--p 63] [--world 8 --rank 0] [--opt k=v ...]
 """
 import argparse
 import json
@@ -11,7 +11,7 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from bench import gamma_for, gen_input  # noqa: E402
 
 

@@ -3,7 +3,7 @@
 plan (svdw_physical_layout, host) and svdw_assign_columns per phase (device
 D2D column copies + selector bytes + lookup columns), with the bytes moved.
 
-    python tools/phys_time.py [--n 1024] [--p 63] [--k 24] [--reps 3]
+    python tools/probes/phys_time.py [--n 1024] [--p 63] [--k 24] [--reps 3]
 """
 import argparse
 import json
@@ -11,7 +11,7 @@ import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from bench import gamma_for, gen_input  # noqa: E402
 

@@ -1,9 +1,9 @@
 #!/bin/bash
 # Same-box option sweep: bench.py at one size with each option set (space-
 # separated name=value lists, ';' between sets), alternating, ROUNDS rounds.
-# Usage: N=512 P=32 SETS="gemm_batch=1;prod_cell=1" bash tools/probe_opts.sh
+# Usage: N=512 P=32 SETS="gemm_batch=1;prod_cell=1" bash tools/probes/probe_opts.sh
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
 N=${N:-512}; P=${P:-32}; R=${ROUNDS:-2}
 IFS=';' read -ra sets <<< "-;${SETS}"

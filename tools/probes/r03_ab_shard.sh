@@ -1,9 +1,9 @@
 #!/bin/bash
 # A/B of engine options on the 8-way row shard (ranks 0 and 5 timed alone,
-# alternating variants, two rounds): bash tools/r03_ab_shard.sh tag "opt=v opt=v" "opt=v" ...
+# alternating variants, two rounds): bash tools/probes/r03_ab_shard.sh tag "opt=v opt=v" "opt=v" ...
 # (an empty string is the default configuration)
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 T=$1
 shift
 O=gpurun_out/$T

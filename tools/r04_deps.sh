@@ -1,12 +1,15 @@
 #!/bin/bash
-# Value-based stream dependencies (dep_values): GPU tests, then same-process
-# A/B on the 8-way rank, 512^2, 1024^2 and config 2.
+# dep_values after the flag-initialisation fix: the whole GPU suite with value
+# dependencies as the default (SVDW_DEP_VALUES=1), then same-process A/B on the
+# 8-way rank, 512^2, 1024^2 and config 2.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-O=gpurun_out/deps
+O=gpurun_out/deps4
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest0.log 2>&1 || { tail -30 $O/pytest0.log; exit 1; }
+tail -1 $O/pytest0.log
+SVDW_DEP_VALUES=1 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 : > $O/ab.txt
 for round in 1 2; do
@@ -19,7 +22,9 @@ for round in 1 2; do
 done
 timeout -k 10 300 python tools/ab.py --n 512 --p 32 --rounds 5 --steps 5 --variant on:dep_values=1 --variant off:dep_values=0 > $O/ab512.txt 2>>$O/ab.err || exit 3
 timeout -k 10 300 python tools/ab.py --n 1024 --p 63 --rounds 5 --steps 3 --variant on:dep_values=1 --variant off:dep_values=0 > $O/ab1024.txt 2>>$O/ab.err || exit 3
+timeout -k 10 300 python tools/ab.py --n 1024 --p 63 --rounds 5 --steps 3 --variant hi:stage_priority=1 --variant lo:stage_priority=0 > $O/ab1024_sp.txt 2>>$O/ab.err || exit 3
 for i in 1 2; do
-  timeout -k 10 300 python bench.py --workload verify_mul --no-cpu-baseline > $O/vm_on_$i.json 2>> $O/ab.err || exit 4
+  timeout -k 10 300 python bench.py --workload verify_mul --no-cpu-baseline --opt dep_values=1 > $O/vm_on_$i.json 2>> $O/ab.err || exit 4
   timeout -k 10 300 python bench.py --workload verify_mul --no-cpu-baseline --opt dep_values=0 > $O/vm_off_$i.json 2>> $O/ab.err || exit 4
 done
+echo done
