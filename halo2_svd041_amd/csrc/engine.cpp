@@ -512,6 +512,7 @@ struct svdw_ctx {
     struct F64Region { uint32_t phase; uint64_t off, n; const double* x; };
     std::vector<F64Region> f64reg;
     bool f64_views = true;                  // "f64_views"
+    bool q_aside = true;                    // "q_aside" (A/B): quantize beside the product chain
     std::vector<F64Src> f64src;
     DBuf colpart;
     DBuf qfold;                             // k_quantize_multi's fold counters + group maxima
@@ -548,14 +549,6 @@ struct svdw_ctx {
     std::vector<uint64_t>* gemm_log = nullptr;   // dry run: offsets of honest_prover_mat_mul
     std::vector<hipEvent_t> deps;           // dependency events (no timing)
     size_t dep_next = 0;
-    // dependency values (stream_dep, "dep_values"): slot i's flag in depflag,
-    // its last written value dep_val[i] (0: the slot went out as an event).
-    // Off by default: with it on, a host-input svd_witness (tests/test_golden.py)
-    // hung on the GPU (cause not found)
-    bool dep_vals = false;
-    DBuf depflag;
-    std::vector<uint32_t> dep_val;
-    uint32_t dep_seq = 0;
     // Stage batches (BatchScope, "stage_batch"): stage launches on a stream with
     // an open batch are collected and issued as k_stage_multi launches when the
     // scope closes, when a stage reads cells a pending stage writes, or before
@@ -625,17 +618,11 @@ static void sync(svdw_ctx* c) {
     if (c->st3) hipck(hipStreamSynchronize(c->st3), "hipStreamSynchronize");
 }
 // Dependency recorded on `from`; `to` waits for it (cross-stream dependency).
-// The returned handle is waited on later with dep_wait. With "dep_values" on
-// the dependency is a value written into a device flag behind `from`'s work
-// (hipStreamWriteValue32) and a wait for it (hipStreamWaitValue32), not an
-// event record + wait: tools/probes/evgap.hip measured 9.8 us between a kernel and
-// its successor on another stream that way against 17.5 us with an event (and
-// a recorded event also delays the next kernel on `from` by 3 us). Every
-// write of a slot carries a larger value (c->dep_seq), so a wait compares >=
-// and a wait on a handle from an earlier call is satisfied exactly when an
-// event wait on that handle would be. A stream being captured into a graph
-// uses events (graph edges).
-static bool dep_values(const svdw_ctx* c) { return c->dep_vals && !c->capturing && c->depflag.p; }
+// The returned handle is waited on later with dep_wait. (Round 4 measured the
+// alternative of stream values, hipStreamWriteValue32 / hipStreamWaitValue32,
+// once its flag initialisation was ordered: the suite passed, but 512^2 went
+// 0.417 -> 0.444 ms and 1024^2 2.078 -> 2.100 ms, 8-way ranks unchanged --
+// HIP runs those waits and writes as kernels of their own -- so it was removed.)
 static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
     if (c->dep_next == c->deps.size()) {
         hipEvent_t e;
@@ -643,40 +630,16 @@ static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
         hipck(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice),
               "hipEventCreate");
         c->deps.push_back(e);
-        c->dep_val.push_back(0);
     }
-    const size_t i = c->dep_next++;
-    hipEvent_t e = c->deps[i];
+    hipEvent_t e = c->deps[c->dep_next++];
     flush_batch(c, from);
-    if (g_batch_log) fprintf(stderr, "dep %zu %p -> %p\n", i, (void*)from, (void*)to);
-    if (dep_values(c) && i < c->depflag.cap / sizeof(uint32_t)) {
-        uint32_t* flag = (uint32_t*)c->depflag.p + i;
-        const uint32_t v = ++c->dep_seq;
-        c->dep_val[i] = v;
-        hipck(hipStreamWriteValue32(from, flag, v, 0), "hipStreamWriteValue32");
-        if (to) hipck(hipStreamWaitValue32(to, flag, v, hipStreamWaitValueGte, 0xffffffffu), "hipStreamWaitValue32");
-        return e;
-    }
-    c->dep_val[i] = 0;
+    if (g_batch_log) fprintf(stderr, "dep %p -> %p\n", (void*)from, (void*)to);
     hipck(hipEventRecord(e, from), "hipEventRecord");
     if (to) hipck(hipStreamWaitEvent(to, e, 0), "hipStreamWaitEvent");
     return e;
 }
-// `s` waits for a dependency stream_dep returned (or any other event). The
-// slot is looked up over every slot, not only this call's: a handle kept from
-// an earlier call (c->gp_ev, a product's event) whose slot this call has not
-// rewritten yet went out as a value, and its event was never recorded.
-static void dep_wait(svdw_ctx* c, hipStream_t s, hipEvent_t e) {
-    if (!c->capturing && c->depflag.p)
-        for (size_t i = 0; i < c->deps.size(); ++i)
-            if (c->deps[i] == e) {
-                if (!c->dep_val[i]) break;                 // it went out as an event
-                if (g_batch_log) fprintf(stderr, "wait %zu on %p\n", i, (void*)s);
-                hipck(hipStreamWaitValue32(s, (uint32_t*)c->depflag.p + i, c->dep_val[i], hipStreamWaitValueGte,
-                                           0xffffffffu),
-                      "hipStreamWaitValue32");
-                return;
-            }
+// `s` waits for a dependency stream_dep returned (or any other event)
+static void dep_wait(svdw_ctx*, hipStream_t s, hipEvent_t e) {
     hipck(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
 }
 // The second stream at high or normal dispatch priority: on a change the queued
@@ -844,6 +807,30 @@ static void bits_words(svdw_ctx* c, QuantSegs& qs, uint32_t nred, const BitSegs&
     f.nred = nred;
     for (uint32_t s = 0; s <= nred; ++s) f.b[s] = qs.blk0[s];
     *folded = true;
+}
+// Quantization off the product chain: when every in-witness reader of the
+// loaded cells goes through an f64 view (f64_views) and the products' residue
+// planes come from the f64 inputs, the GEMM needs only the operand bit-length
+// words. k_bits_f64 writes those on st (read-only, 8 B per value, the fold of
+// qs), and k_quantize_multi writes the cells on `aside` beside the residues
+// and GEMM. The caller joins `aside` into st before the witness ends.
+static void quantize_aside(svdw_ctx* c, const QuantSegs& qs, uint32_t nbit_segs, hipStream_t aside) {
+    QuantSegs qb = qs;
+    qb.nseg = nbit_segs;
+    double nb = 0, nq = 0;
+    for (uint32_t k = 0; k < qs.nseg; ++k) {
+        nq += (double)qs.n[k];
+        if (k < nbit_segs) nb += (double)qs.n[k];
+    }
+    {
+        ProfScope ps(c, c->st, "k_bits_f64", 8.0 * nb, 0);
+        hipck(launch_bits_f64(qb, (int)c->P, c->st), "k_bits_f64");
+    }
+    QuantSegs qq = qs;
+    for (uint32_t k = 0; k < (uint32_t)kMaxQuantSegs; ++k) qq.blockmax[k] = nullptr;
+    memset(&qq.fold, 0, sizeof qq.fold);
+    ProfScope ps(c, aside, "k_quantize", 40.0 * nq, 0);
+    hipck(launch_quantize_multi(qq, (int)c->P, aside), "k_quantize_multi");
 }
 static void grow(svdw_ctx* c, Fr*& ptr, uint64_t used, uint64_t& cap, uint64_t need) {
     if (c->dry || need <= cap) return;
@@ -2533,15 +2520,6 @@ static void check_svd_phase1(svdw_ctx* c, const svdw_mat& m, const svdw_mat& u, 
 // overwrite buffers the previous call's kernels still read.
 static void after_previous(svdw_ctx* c) {
     if (c->dry) return;
-    if (c->dep_vals && !c->depflag.p && !c->capturing) {   // stream_dep's value flags
-        // zeroed on st and complete before the first flag write: a hipMemset
-        // (null stream) is not ordered against the non-blocking streams, and a
-        // zero landing after a write left the waits on it spinning forever
-        // (the round-3 hang of a host-input svd_witness, tests/test_golden.py)
-        ensure_buf(c, c->depflag, 1024 * sizeof(uint32_t));
-        hipck(hipMemsetAsync(c->depflag.p, 0, c->depflag.cap, c->st), "hipMemsetAsync");
-        hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
-    }
     const hipEvent_t e = stream_dep(c, c->st, c->st2);
     if (c->st3) dep_wait(c, c->st3, e);
 }
@@ -2644,7 +2622,13 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     seg.begin[3] = nbm + nbu + nbv;
     bool folded = false;
     bits_words(c, qs, 3, seg, dbits, &folded);
-    if (qs.nseg) {
+    // the cells beside the product chain on st2 (its stages wait for the
+    // residue planes anyway) when no launch of the witness reads them
+    const bool q_aside = c->q_aside && folded && qs.nseg == 4 && on_device && !c->dry && c->f64_views && c->overlap &&
+                         c->res_f64 && c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA && N <= 8192 && M <= 8192;
+    if (q_aside) {
+        quantize_aside(c, qs, 3, c->st2);
+    } else if (qs.nseg) {
         ProfScope ps(c, c->st, "k_quantize", 40.0 * ((double)N * M + (double)N * N + (double)M * M + r), 0);
         hipck(launch_quantize_multi(qs, (int)c->P, c->st), "k_quantize_multi");
     }
@@ -2729,9 +2713,9 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     if (!p1_queued) queue_phase1(pl, p1_overlap);
     host_mark(c, "phase 1 queued");
     if (p1_overlap) stream_dep(c, p1s, c->st);
-    // st2 also carries the d checks and single cells queued aside (and, with
-    // phase 1 on st3, nothing else joins it): join it too
-    if (c->prelaunched && !c->dry && !(p1_overlap && p1s == c->st2)) stream_dep(c, c->st2, c->st);
+    // st2 also carries the quantized cells and the d checks and single cells
+    // queued aside (and, with phase 1 on st3, nothing else joins it): join it too
+    if ((c->prelaunched || q_aside) && !c->dry && !(p1_overlap && p1s == c->st2)) stream_dep(c, c->st2, c->st);
     host_mark(c, "svd_witness end");
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
 }
@@ -2824,7 +2808,13 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     seg.begin[2] = nba + nbb;
     bool folded = false;
     bits_words(c, qs, 2, seg, dbits, &folded);
-    if (qs.nseg) {
+    // the cells on st2 beside the chain when only f64 views and the f64
+    // residue planes read the loads (quantize_aside); st2 joins st at the end
+    const bool q_aside = c->q_aside && folded && qs.nseg == 2 && on_device && !c->dry && c->f64_views && c->res_f64 &&
+                         c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA && K <= 8192;
+    if (q_aside) {
+        quantize_aside(c, qs, 2, c->st2);
+    } else if (qs.nseg) {
         ProfScope ps(c, c->st, "k_quantize", 40.0 * ((double)N * K + (double)K * M), 0);
         hipck(launch_quantize_multi(qs, (int)c->P, c->st), "k_quantize_multi");
     }
@@ -2908,6 +2898,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     } else {
         verify_mul_many(c, 1, &vm, 1, gamma);
     }
+    if (q_aside && !c->capturing) stream_dep(c, c->st2, c->st);   // (a capture joins st2 itself)
     host_mark(c, "verify_mul_witness end");
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
 }
@@ -3196,7 +3187,6 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
         c->device = p->device;
         c->dry = p->device < 0;
         if (const char* h = getenv("SVDW_HOST_TRACE")) c->host_trace = atoi(h) != 0;
-        if (const char* d = getenv("SVDW_DEP_VALUES")) c->dep_vals = atoi(d) != 0;   // default override (tests)
         if (const char* g = getenv("SVDW_GEMM"))
             c->gemm_impl = (!strcmp(g, "valu") || !strcmp(g, "dot4")) ? SVDW_GEMM_VALU : SVDW_GEMM_MFMA;
         if (!c->dry) {
@@ -3228,7 +3218,7 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             vmg_drop(c);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
             for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1], &c->w1c, &c->w1t, &c->w2c, &c->w2t,
-                            &c->bits, &c->gpc, &c->gtab, &c->crtR, &c->gbits, &c->colpart, &c->qfold, &c->depflag})
+                            &c->bits, &c->gpc, &c->gtab, &c->crtR, &c->gbits, &c->colpart, &c->qfold})
                 if (b->p) (void)hipFree(b->p);
             for (int i = 0; i < kMaxScanJobs; ++i) {
                 if (c->wbc[i].p) (void)hipFree(c->wbc[i].p);
@@ -4166,9 +4156,7 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         sync(c);
         ++c->epoch;                                  // a captured launch sequence may change
         const std::string n(name);
-        if (n == "dep_values") {                     // stream_dep: CP-written flags, not events
-            c->dep_vals = value != 0;
-        } else if (n == "graph") {                   // captured verify_mul_witness (vm_graph)
+        if (n == "graph") {                   // captured verify_mul_witness (vm_graph)
             REQUIRE(value == 0 || value == 1, "graph: 0 or 1");
             c->graph_vm = (int)value;
         } else if (n == "gemm_impl") {
@@ -4186,24 +4174,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "prod_cell") {
             REQUIRE(value >= -1 && value <= 1, "prod_cell: -1, 0 or 1");
             c->prod_cell = (int)value;
-        } else if (n == "stage_priority") {
-            // cell stream priority: 0 normal, 1 high (its blocks dispatch ahead of the
-            // products / phase-1 scans on the second stream)
-            REQUIRE(value == 0 || value == 1, "stage_priority: 0 or 1");
-            if (!c->dry) {
-                int lo = 0, hi = 0;
-                hipck(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
-                (void)lo;                                  // 0: the default priority
-                hipStream_t s;
-                if (value)
-                    hipck(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi),
-                          "hipStreamCreateWithPriority");
-                else
-                    hipck(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
-                hipck(hipStreamDestroy(c->st), "hipStreamDestroy");
-                c->st = s;
-                c->st_cell = s;
-            }
         } else if (n == "phase1_overlap") {
             REQUIRE(value >= 0 && value <= 2, "phase1_overlap: 0, 1 or 2");
             c->phase1_overlap = (int)value;
@@ -4219,6 +4189,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_crt = (int)value;
         } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
             c->stage_batch = value != 0;
+        } else if (n == "q_aside") {
+            c->q_aside = value != 0;
         } else if (n == "f64_views") {
             c->f64_views = value != 0;
         } else if (n == "p1_at") {

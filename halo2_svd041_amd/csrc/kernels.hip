@@ -156,6 +156,24 @@ __device__ __forceinline__ void bits_fold(const BitFold& f, uint32_t blk, uint32
     }
     if (threadIdx.x == 0) __hip_atomic_store(f.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// bit length of |x_q| over a block's values (for the GEMM modulus count):
+// thread max -> wave max -> block max (LDS)
+template <int PT>
+__device__ __forceinline__ uint32_t block_bits(const double (&xv)[PT], double scale) {
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+        const double s = round(fabs(xv[k]) * scale);
+        if (s >= 340282366920938463463374607431768211456.0) bits = 128;
+        else if (s >= 1.0) bits = max(bits, (uint32_t)ilogb(s) + 1);
+    }
+    __shared__ uint32_t wmax[4];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, off));
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = bits;
+    __syncthreads();
+    return max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+}
 // kQuantPerBlock values per block, 16 per thread (value blk * 4096 + k * 256 +
 // tid: each store instruction coalesced), all loads issued first.
 __device__ __forceinline__ void quantize_body(const double* __restrict__ in, uint64_t n,
@@ -173,21 +191,7 @@ __device__ __forceinline__ void quantize_body(const double* __restrict__ in, uin
         xv[k] = i < n ? in[i] : 0.0;
     }
     if (blockmax) {
-        // bit length of |x_q| for the GEMM modulus count: thread max -> wave max
-        // -> block max (LDS) -> one word per block
-        uint32_t bits = 0;
-#pragma unroll
-        for (int k = 0; k < PT; ++k) {
-            const double s = round(fabs(xv[k]) * scale);
-            if (s >= 340282366920938463463374607431768211456.0) bits = 128;
-            else if (s >= 1.0) bits = max(bits, (uint32_t)ilogb(s) + 1);
-        }
-        __shared__ uint32_t wmax[4];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, off));
-        if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = bits;
-        __syncthreads();
-        bmax = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        bmax = block_bits<PT>(xv, scale);
         if (!(fold.wout && gblk < fold.nblk) && threadIdx.x == 0) blockmax[blk] = bmax;
     }
 #pragma unroll
@@ -198,7 +202,7 @@ __device__ __forceinline__ void quantize_body(const double* __restrict__ in, uin
             const uint32_t r = (uint32_t)(i / keep.cols), cc = (uint32_t)(i - (uint64_t)r * keep.cols);
             if (!((r >= keep.rlo && r < keep.rhi) || (cc >= keep.clo && cc < keep.chi))) continue;
         }
-        st_fr_nt(out + i, quantize_fr(xv[k], scale));
+        st_fr(out + i, quantize_fr(xv[k], scale));    // (L2 joins the two halves of a line)
     }
     if (blockmax && fold.wout && gblk < fold.nblk) bits_fold(fold, gblk, bmax);
 }
@@ -225,6 +229,39 @@ __global__ __launch_bounds__(256) void k_quantize_multi(const QuantSegs q, doubl
             in = q.in[k]; out = q.out[k]; bm = q.blockmax[k]; n = q.n[k]; b0 = q.blk0[k]; keep = q.keep[k];
         }
     quantize_body(in, n, out, scale, bm, blockIdx.x - b0, keep, q.fold, blockIdx.x);
+}
+// The operand bit-length words alone, read-only from the f64 inputs (the
+// segments and block layout of k_quantize_multi, its fold): the residue planes
+// and the GEMM need only these, so the quantized cells can be written beside
+// the product chain instead of ahead of it (8 B read per value).
+__global__ __launch_bounds__(256) void k_bits_f64(const QuantSegs q, double scale) {
+    constexpr int PT = kQuantPerBlock / 256;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxQuantSegs; ++k) s += (uint32_t)k < q.nseg && blockIdx.x >= q.blk0[k];
+    const double* in = q.in[0];
+    unsigned* bm = q.blockmax[0];
+    uint64_t n = q.n[0];
+    uint32_t b0 = q.blk0[0];
+#pragma unroll
+    for (int k = 1; k < kMaxQuantSegs; ++k)
+        if (s == (uint32_t)k) { in = q.in[k]; bm = q.blockmax[k]; n = q.n[k]; b0 = q.blk0[k]; }
+    const uint32_t blk = blockIdx.x - b0;
+    const uint64_t i0 = (uint64_t)blk * kQuantPerBlock + threadIdx.x;
+    double xv[PT];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+        const uint64_t i = i0 + 256ull * k;
+        xv[k] = i < n ? __builtin_nontemporal_load(in + i) : 0.0;
+    }
+    const uint32_t bmax = block_bits<PT>(xv, scale);
+    if (q.fold.wout && blockIdx.x < q.fold.nblk) bits_fold(q.fold, blockIdx.x, bmax);
+    else if (bm && threadIdx.x == 0) bm[blk] = bmax;
+}
+hipError_t launch_bits_f64(const QuantSegs& q, int p, hipStream_t st) {
+    if (!q.nseg || q.nseg > (uint32_t)kMaxQuantSegs || !q.blk0[q.nseg]) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_bits_f64, dim3(q.blk0[q.nseg]), dim3(256), 0, st, q, (double)(1ull << p));
+    return hipGetLastError();
 }
 hipError_t launch_quantize_multi(const QuantSegs& q, int p, hipStream_t st) {
     if (!q.nseg || q.nseg > (uint32_t)kMaxQuantSegs || !q.blk0[q.nseg]) return hipErrorInvalidValue;

@@ -109,6 +109,9 @@ struct QuantSegs {
     BitFold fold;                        // fold.wout null: no in-launch fold
 };
 hipError_t launch_quantize_multi(const QuantSegs& q, int precision_bits, hipStream_t st);
+// k_bits_f64: only the bit-length words of q's segments (blockmax / fold as
+// k_quantize_multi would write them), read-only from the f64 inputs
+hipError_t launch_bits_f64(const QuantSegs& q, int precision_bits, hipStream_t st);
 // Witness checker (svdw_check_gates). A region is `nunits` repetitions of a
 // `unit`-cell block (element u = row u / cols, column u % cols); check words:
 //   CHK_GATE g      a + b*c = d on cells g..g+3

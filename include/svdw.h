@@ -243,7 +243,7 @@ int svdw_verify_mul_witness(svdw_ctx* ctx, const double* a, const double* b, uin
 #define SVDW_GEMM_MFMA 0
 #define SVDW_GEMM_VALU 1
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
-/* Options (svdw_set_option; 16 of them). Tuning knobs, bit-identical results
+/* Options (svdw_set_option; 15 of them). Tuning knobs, bit-identical results
  * for every value, defaults first:
  *   "gemm_impl" 0 | 1; "gemm_crt" 1 | 0 (CRT or digit-plane matrix-core GEMM);
  *   "overlap" 1 | 0 (the three check_svd_phase0 products run ahead on a second
@@ -255,8 +255,7 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   phase-0 stages, 3 after all of phase 0; -1: 0 on a rank of a >= 4-way shard, 3 of a
  *   2-3-way shard, else 1); "gemm_priority" -1 | 0 | 1 (second stream priority:
  *   -1 auto = high for unsharded witnesses with 512 <= max(N, M) < 1024, where
- *   the product chain is the critical path; 0 normal; 1 high); "stage_priority"
- *   0 | 1 (cell stream priority);
+ *   the product chain is the critical path; 0 normal; 1 high);
  *   "stage_elems" 256 (elements per stage block, multiple of 16 in [16, 256]);
  *   "f64_views" 1 | 0 (svd_witness / verify_mul_witness with device inputs:
  *   stages and row scans read the loaded matrices from the f64 inputs,
@@ -269,11 +268,10 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   cells a pending one writes); "prod_cell" 1 | 0 | -1 (svd_witness with
  *   device inputs: the products on the cell stream and the u / v bounds and u.d
  *   beside them; -1 on row-sharded contexts only);
- *   "dep_values" 0 | 1: cross-stream dependencies inside a witness as flags
- *   written behind the producing stream and waited for by the consuming one
- *   (hipStreamWriteValue32 / hipStreamWaitValue32) instead of event records
- *   and waits (tools/probes/evgap.hip: 9.8 vs 17.5 us from a kernel's end to its
- *   successor's start on another stream);
+ *   "q_aside" 1 | 0 (svd_witness / verify_mul_witness with device inputs, f64
+ *   views and the f64 residue path: the operand bit-length words from a read-only
+ *   pass on the cell stream and the quantized cells written beside the product
+ *   chain on the second stream, or the quantization ahead of it);
  *   "graph" 1 | 0: svdw_verify_mul_witness with device inputs replays a HIP graph
  *   of its launch sequence. The second call of a key (N, K, M, the input
  *   pointers, no allocation or option change since) is captured, later calls

@@ -168,9 +168,8 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
 
 @pytest.mark.parametrize("opts", [{"gemm_crt": 0}, {"stage_elems": 64}, {"stage_elems": 192},
                                   {"phase1_overlap": 0}, {"phase1_overlap": 2},
-                                  {"overlap": 0}, {"stage_priority": 1},
-                                  {"gemm_priority": 1}, {"gemm_priority": 0},
-                                  {"stage_batch": 0}, {"dep_values": 1}, {"dep_values": 1, "phase1_overlap": 2},
+                                  {"overlap": 0}, {"gemm_priority": 1}, {"gemm_priority": 0},
+                                  {"stage_batch": 0}, {"q_aside": 0}, {"q_aside": 0, "phase1_overlap": 2},
                                   {"gemm_impl": 1}, {"res_f64": 0}, {"f64_views": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
@@ -347,21 +346,21 @@ def _on_device(*xs):
 
 @pytest.mark.parametrize("f64v", [1, 0])
 @pytest.mark.parametrize("res", [1, 0])
-@pytest.mark.parametrize("dv", [0, 1])
+@pytest.mark.parametrize("qa", [1, 0])
 @pytest.mark.parametrize("N,M,P", [(130, 97, 63), (64, 200, 32)])
-def test_device_inputs_parity(gpu_ctx_factory, dv, res, f64v, N, M, P):
+def test_device_inputs_parity(gpu_ctx_factory, qa, res, f64v, N, M, P):
     """The bench path: m, u, v, d already resident in HBM (torch float64 CUDA
     tensors), quantized in one fused launch; the CRT residue planes of
     m, u, v built from the f64 inputs in one launch (res 1) or from the
     quantized cells (res 0); the stages and row scans reading the loaded
     matrices through f64 views (f64v 1: quantized in registers, no wait for the
-    cells) or the cells; dependencies between the streams as events or values
-    (dv, dep_values); witness vs the oracle."""
+    cells) or the cells; the quantized cells written beside the product chain
+    (qa, q_aside) or ahead of it; witness vs the oracle."""
     import halo2_svd041_amd as hs
     m, u, d, v = gen_svd_input(N, M, seed=N * M)
     g = gamma_for(N + M)
     ctx = gpu_ctx_factory(P)
-    ctx.set_option("dep_values", dv)
+    ctx.set_option("q_aside", qa)
     ctx.set_option("res_f64", res)
     ctx.set_option("f64_views", f64v)
     dm, du, dv, dd = _on_device(m, u, v, d)
@@ -423,7 +422,7 @@ def test_row_sharded_device_inputs_parity(gpu_ctx_factory, N, M, P, world):
 @pytest.mark.parametrize("world,opts", [(1, {"prod_cell": 1}), (1, {"prod_cell": 1, "stage_batch": 0}),
                                         (1, {"prod_cell": 1, "p1_at": 1}), (1, {"prod_cell": 1, "hold_us": 50}),
                                         (3, {"prod_cell": 0}), (3, {"prod_cell": 1, "stage_batch": 0}),
-                                        (4, {"prod_cell": 1, "dep_values": 1}), (1, {"dep_values": 1}),
+                                        (4, {"prod_cell": 1, "q_aside": 0}), (1, {"q_aside": 0}),
                                         (5, {"prod_cell": 0}), (4, {"p1_at": 3}), (1, {"prod_cell": 0})])
 def test_products_on_cell_stream_parity(gpu_ctx_factory, world, opts):
     """prod_cell: the products on the cell stream, the u / v bounds and u.d on
@@ -473,8 +472,8 @@ def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device, hol
     m, u, d, v = gen_svd_input(N, M, seed=N + M + P)
     g = gamma_for(N * M)
     ctx = gpu_ctx_factory(P)
-    if hold < 0:                                  # (and value dependencies between the streams)
-        ctx.set_option("dep_values", 1)
+    if hold < 0:                                  # (and quantization on the cell stream)
+        ctx.set_option("q_aside", 0)
         hold = -hold
     if hold:
         # a first witness of other inputs allocates every buffer (allocation

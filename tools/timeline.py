@@ -33,16 +33,24 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]),
                          r.get("Stream_Id", r.get("Queue_Id")), int(r["Grid_Size_X"])))
     rows.sort()
-    # step boundaries: a k_quantize preceded by a gap or a non-quantize kernel
-    starts = [i for i, r in enumerate(rows) if r[2].startswith("k_quantize")
-              and (i == 0 or not rows[i - 1][2].startswith("k_quantize"))]
-    if len(starts) < 2:
-        raise SystemExit("could not find step boundaries")
-    s0, s1 = starts[-2], starts[-1]
-    step = rows[s0:s1]
+    # step boundaries: with hold_us, each k_hold ends where a step's queued
+    # work starts; else the first k_bits_f64 / k_quantize of a run of them
+    holds = [i for i, r in enumerate(rows) if r[2].startswith("k_hold")]
+    if len(holds) >= 2:
+        h0, h1 = holds[-2], holds[-1]
+        step = [r for r in rows if rows[h0][1] <= r[0] < rows[h1][1] and not r[2].startswith("k_hold")]
+        step_end = max(r[1] for r in step)           # (the next step waits behind its hold)
+    else:
+        mark = lambda n: n.startswith("k_quantize") or n.startswith("k_bits_f64")   # noqa: E731
+        starts = [i for i, r in enumerate(rows) if mark(r[2]) and (i == 0 or not mark(rows[i - 1][2]))]
+        if len(starts) < 2:
+            raise SystemExit("could not find step boundaries")
+        s0, s1 = starts[-2], starts[-1]
+        step = rows[s0:s1]
+        step_end = rows[s1][0]
     t0 = step[0][0]
     tend = max(r[1] for r in step)
-    span = (rows[s1][0] - t0) / 1e3
+    span = (step_end - t0) / 1e3
     # union busy time
     busy, cur_s, cur_e = 0, None, None
     for s, e, *_ in step:
