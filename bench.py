@@ -144,12 +144,30 @@ def reduce_over_ranks(elapsed, cells_step, dist, device):
     return float(t.item()), float(c.item())
 
 
-def pmc_traffic(kernel, workload, N, M, P, LB):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC
-    summary of this exact workload (profiles/*_pmc_summary.json, written by
-    tools/pmc_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE passes)."""
+def sources_sha16():
+    """Hash of the engine and kernel sources (halo2_svd041_amd/csrc): a PMC
+    summary is only evidence for the build it was collected on."""
+    import glob
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(ROOT, "halo2_svd041_amd", "csrc", "*"))):
+        if f.endswith((".hip", ".cpp", ".hpp")):
+            h.update(os.path.basename(f).encode())
+            with open(f, "rb") as fh:
+                h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(kernel, workload, N, M, P, LB, world=1, rank=0):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary
+    of this exact workload AND these kernel sources (profiles/*_pmc_summary.json,
+    written by tools/pmc_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE
+    passes; a summary of other sources is refused). Returns (bytes, file, note)."""
     import glob
     want = {"N": N, "M": M, "P": P, "LB": LB}
+    if world > 1:
+        want.update({"world": world, "rank": rank})
+    sha = sources_sha16()
+    stale = []
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json")), reverse=True):
         try:
             with open(f) as fh:
@@ -158,8 +176,34 @@ def pmc_traffic(kernel, workload, N, M, P, LB):
             continue
         if (s.get("config") == want and s.get("workload", "svd") == workload
                 and kernel in s.get("kernels", {})):
-            return s["kernels"][kernel]["traffic_per_launch"], os.path.relpath(f, ROOT)
-    return None, None
+            if s.get("sources_sha16") != sha:
+                stale.append(os.path.relpath(f, ROOT))
+                continue
+            return s["kernels"][kernel]["traffic_per_launch"], os.path.relpath(f, ROOT), None
+    note = ("no PMC summary of these kernel sources (sha16 %s)" % sha
+            + ("; refused summaries of other sources: %s" % ", ".join(stale) if stale else ""))
+    return None, None, note
+
+
+def gpu_only_chain(workload, N, M, P, LB):
+    """The GPU-only schedule of this workload (tools/timeline.py --json over a
+    rocprofv3 kernel trace of the same kernel sources, run with hold_us so the
+    host has queued the whole step first): span, busy time and the critical
+    chain's launches, kernel time and launch-boundary time."""
+    import glob
+    sha = sources_sha16()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_chain_*.json")), reverse=True):
+        try:
+            with open(f) as fh:
+                s = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if (s.get("workload") == workload and s.get("config") == {"N": N, "M": M, "P": P, "LB": LB}
+                and s.get("sources_sha16") == sha):
+            s = dict(s)
+            s["file"] = os.path.relpath(f, ROOT)
+            return s
+    return None
 
 
 # ----------------------------------------------------------------- CPU baseline
@@ -606,11 +650,14 @@ def main():
             step["note"] = "each rank's whole witness per step against one GPU's peak"
         if stats:
             kname, roof, breakdown = roofline_from_profile(stats, args.steps)
-            traffic, src = (None, None) if rows_mode else pmc_traffic(
-                kname, args.workload, N, M, P, args.lb)
+            traffic, src, tnote = pmc_traffic(kname, args.workload, N, M, P, args.lb,
+                                              world if rows_mode else 1, rank)
             if traffic is not None:
                 roof["traffic"] = traffic
                 roof["traffic_source"] = src
+            else:
+                roof["traffic_note"] = tnote
+            roof["sources_sha16"] = sources_sha16()
             cell = cell_stream_rate(stats, args.steps)
             if cell is not None and roof["kernel"] == "k_stage":
                 roof["cell_stream"] = cell
@@ -625,6 +672,21 @@ def main():
             roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": None, "traffic": None, "kernel": None}
         roof["step"] = step
+        if not svd:
+            # a 256^2 witness moves 26 MB: the step is bound by its dependent
+            # launches and their boundaries, not by HBM (its whole-step fraction
+            # says so); the GPU-only chain of the same sources, when committed
+            roof["bound"] = "latency"
+            ch = gpu_only_chain(args.workload, N, M, P, args.lb)
+            roof["latency"] = ({"gpu_only_step_us": ch["span_us"], "gpu_busy_us": ch["busy_us"],
+                                "critical_launches": ch["chain"]["launches"],
+                                "critical_kernel_us": ch["chain"]["kernel_us"],
+                                "critical_boundary_us": ch["chain"]["boundary_us"],
+                                "critical_kernels": ch["chain"]["kernels"], "source": ch["file"],
+                                "note": "GPU-only schedule (hold_us) of the same kernel sources; the "
+                                        "per-kernel HBM fraction above is the dominant kernel's"}
+                               if ch else {"note": "no committed GPU-only chain of these kernel sources "
+                                                   "(profiles/*_chain_*.json)"})
         if graph_stats is not None:
             roof["timing_note"] = ("timed steps replay the captured launch graph (captures, replays "
                                    "= %d, %d); the kernel's launches timed in a second, eager pass of "

@@ -14,7 +14,10 @@ import argparse
 import csv
 import json
 import os
+import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def short(name):
@@ -43,7 +46,16 @@ def main():
     ap.add_argument("pmc_dir")
     ap.add_argument("--config", default="")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--workload", default="svd")
     a = ap.parse_args()
+    # the kernel sources the passes ran (written on the GPU box next to the
+    # passes, tools/pmc.sh); bench.py only uses a summary of its own sources
+    shaf = os.path.join(a.pmc_dir, "sources_sha16")
+    if os.path.exists(shaf):
+        sha = open(shaf).read().strip()
+    else:
+        from bench import sources_sha16
+        sha = sources_sha16()
     fetch = load(os.path.join(a.pmc_dir, "pass1"), "FETCH_SIZE")
     write = load(os.path.join(a.pmc_dir, "pass2"), "WRITE_SIZE")
     cfg = dict(kv.split("=") for kv in a.config.split(",") if kv)
@@ -51,6 +63,8 @@ def main():
                      "bench.py --steps 2 --warmup 1 --no-profile",
            "correction": "bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (FETCH_SIZE halved on gfx950)",
            "config": {k: int(v) for k, v in cfg.items()},
+           "workload": a.workload,
+           "sources_sha16": sha,
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         nf, fk = fetch.get(k, [0, 0.0])

@@ -10,6 +10,8 @@ launch gaps and serial tails are visible.
 """
 import argparse
 import csv
+import json
+import os
 from collections import defaultdict
 
 
@@ -26,6 +28,10 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--all", action="store_true", help="print every dispatch of the last step")
+    ap.add_argument("--json", default=None, help="also write the step summary and its critical chain here")
+    ap.add_argument("--workload", default=None, help="workload tag recorded in --json (e.g. verify_mul)")
+    ap.add_argument("--sha", default=None, help="kernel-source hash recorded in --json (bench.sources_sha16)")
+    ap.add_argument("--config", default="", help="N=..,M=..,P=..,LB=.. recorded in --json")
     a = ap.parse_args()
     rows = []
     with open(a.trace) as f:
@@ -69,6 +75,31 @@ def main():
         agg[n][1] += (e - s) / 1e3
     for n, (cnt, tot) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         print(f"  {tot:9.1f} us  x{cnt:3d}  {n}")
+    # critical chain: back from the last kernel to end, each time to the kernel
+    # (any stream) that ended last before the current one started -- what it
+    # waited for in a GPU-only (hold_us) schedule; boundary = the gaps between
+    chain = [max(step, key=lambda r: r[1])]
+    while True:
+        cur = chain[-1]
+        prev = [r for r in step if r[1] <= cur[0] and r is not cur]
+        if not prev:
+            break
+        chain.append(max(prev, key=lambda r: r[1]))
+    chain.reverse()
+    kern = sum(r[1] - r[0] for r in chain) / 1e3
+    gaps = sum(max(0, chain[i + 1][0] - chain[i][1]) for i in range(len(chain) - 1)) / 1e3
+    lead = (chain[0][0] - t0) / 1e3
+    print(f"critical chain: {len(chain)} launches, {kern:.1f} us in kernels, {gaps:.1f} us at launch "
+          f"boundaries, starts {lead:.1f} us into the step: " + " -> ".join(r[2] for r in chain))
+    if a.json:
+        out = {"span_us": round(span, 1), "busy_us": round(busy / 1e3, 1), "dispatches": len(step),
+               "chain": {"launches": len(chain), "kernel_us": round(kern, 1), "boundary_us": round(gaps, 1),
+                         "lead_us": round(lead, 1), "kernels": [r[2] for r in chain]},
+               "kernels_us": {n: round(t, 1) for n, (c, t) in agg.items()},
+               "source": os.path.relpath(a.trace), "workload": a.workload, "sources_sha16": a.sha,
+               "config": {k: int(v) for k, v in (kv.split("=") for kv in a.config.split(",") if kv)}}
+        with open(a.json, "w") as fh:
+            json.dump(out, fh, indent=1)
     if a.all:
         prev_end = t0
         for s, e, n, st, g in step:
