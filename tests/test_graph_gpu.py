@@ -101,3 +101,34 @@ def test_graph_off_and_invalidation(gpu_ctx_factory):
         hs.verify_mul_witness(on, ta, tb, gamma_for(61 + it))
         _check_all(on, a, b, P, gamma_for(61 + it))
     assert on.graph_stats() == (3, 4)
+
+
+@pytest.mark.gpu
+def test_graph_replay_after_svd_witness(gpu_ctx_factory):
+    """A replay after another call on the same context: the captured graph's
+    host state (layout, checks, constants, counts, product bounds) must be
+    restored over whatever svd_witness left, with nothing reallocated in
+    between (the svd witness runs first at the same sizes, so the second one
+    grows nothing and the epoch, hence the graph, survives)."""
+    import torch
+    import halo2_svd041_amd as hs
+    from conftest import gen_svd_input
+    P = 32
+    a, b = _mats(64, 40, 50, seed=21)
+    ta, tb = (torch.tensor(x, dtype=torch.float64, device="cuda:0") for x in (a, b))
+    m, u, d, v = gen_svd_input(48, 40, seed=22)
+    dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device="cuda:0")
+                      for x in (m, u, v, d))
+    ctx = gpu_ctx_factory(P)
+    hs.svd_witness(ctx, dm, du, dv, dd, gamma_for(70))
+    for it in range(3):                                   # eager, capture, replay
+        hs.verify_mul_witness(ctx, ta, tb, gamma_for(71 + it))
+    c0, c1 = corc.verify_mul_witness(a, b, P, gamma_for(73))   # (no checker here: its scratch
+    assert np.array_equal(ctx.advice(0), c0) and np.array_equal(ctx.advice(1), c1)   # would bump the epoch)
+    assert ctx.graph_stats() == (1, 1)
+    hs.svd_witness(ctx, dm, du, dv, dd, gamma_for(74))
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, gamma_for(74))
+    assert np.array_equal(ctx.advice(0), a0) and np.array_equal(ctx.advice(1), a1)
+    hs.verify_mul_witness(ctx, ta, tb, gamma_for(75))
+    assert ctx.graph_stats() == (1, 2), "the svd witness reallocated: no replay was tested"
+    _check_all(ctx, a, b, P, gamma_for(75))

@@ -12,7 +12,7 @@ tail -1 $O/pytest.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 2
 timeout -k 10 300 python tools/ab.py --n 1024 --p 63 --rounds 5 --steps 3 --variant on:q_aside=1 --variant off:q_aside=0 > $O/ab1024.txt 2>>$O/ab.err || exit 3
 timeout -k 10 400 python tools/ab.py --n 1024 --p 63 --rounds 5 --steps 3 --variant base: --variant s2:bounds_wait=1,phase1_overlap=2 --variant p2:phase1_overlap=2 --variant bw:bounds_wait=1 > $O/ab1024_s2.txt 2>>$O/ab.err || exit 3
-timeout -k 10 300 python tools/ab.py --n 512 --p 32 --rounds 5 --steps 5 --variant base: --variant bw:bounds_wait=1 > $O/ab512_s2.txt 2>>$O/ab.err || exit 3
+timeout -k 10 300 python tools/ab.py --n 512 --p 32 --rounds 5 --steps 5 --variant base: --variant bw:bounds_wait=1 --variant e128:stage_elems=128 --variant e64:stage_elems=64 > $O/ab512_s2.txt 2>>$O/ab.err || exit 3
 timeout -k 10 300 python tools/ab.py --n 512 --p 32 --rounds 5 --steps 5 --variant on:q_aside=1 --variant off:q_aside=0 > $O/ab512.txt 2>>$O/ab.err || exit 3
 : > $O/ab_s8.txt
 for round in 1 2; do
