@@ -33,14 +33,6 @@ __device__ __forceinline__ void st_fr(Fr* p, const Fr& v) {
     q[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
     q[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
 }
-// Streaming store (nontemporal): cells the next kernel boundary would otherwise
-// write back from L2 (the products, the quantized operands).
-__device__ __forceinline__ void st_fr_nt(Fr* p, const Fr& v) {
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    v4u* q = reinterpret_cast<v4u*>(p);
-    __builtin_nontemporal_store(v4u{v.w[0], v.w[1], v.w[2], v.w[3]}, q);
-    __builtin_nontemporal_store(v4u{v.w[4], v.w[5], v.w[6], v.w[7]}, q + 1);
-}
 // ZkMatrix::new's quantization of one f64 (quantize_body's arithmetic):
 // x_q = round_half_away(|x| 2^P) as u128 (saturating, NaN -> 0), sign(x) < 0
 // (incl. -0.0) -> p - x_q.
@@ -1796,8 +1788,11 @@ __device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t cblk)
     }
     x[8] = (uint32_t)t;
     const Fr v = reduce9(x);
-    st_fr_nt(q.out + (int64_t)i * q.ors + (int64_t)j * q.ocs, v);
-    if (q.sym && j > i) st_fr_nt(q.out + (int64_t)j * q.ors + (int64_t)i * q.ocs, v);
+    // plain stores: the two 16 B halves of a cell (and, for the mirror, the
+    // other lanes' cells of a line) meet in L2 and go out as whole lines (the
+    // nontemporal form wrote x1.24 the cell bytes, r03_pmc_summary.json)
+    st_fr(q.out + (int64_t)i * q.ors + (int64_t)j * q.ocs, v);
+    if (q.sym && j > i) st_fr(q.out + (int64_t)j * q.ors + (int64_t)i * q.ocs, v);
 }
 // Combine blocks of a CrtBatch (cblocks in all, job j from cblk0[j]) dealt
 // XCD-contiguously: XCD x takes a contiguous run of the row-major tile

@@ -16,7 +16,7 @@ timeout -k 10 300 python tools/ab.py --n 512 --p 32 --rounds 5 --steps 5 --varia
 timeout -k 10 300 python tools/ab.py --n 512 --p 32 --rounds 5 --steps 5 --variant on:q_aside=1 --variant off:q_aside=0 > $O/ab512.txt 2>>$O/ab.err || exit 3
 : > $O/ab_s8.txt
 for round in 1 2; do
-  for v in "q_aside=1" "q_aside=0"; do
+  for v in "q_aside=1" "q_aside=0" "bounds_wait=1"; do
     for r in 0 5; do
       ms=$(timeout -k 10 120 python3 tools/shard_sim.py --worlds 8 --rank $r --steps 20 --opt $v 2>>$O/ab.err | python3 -c "import json,sys; d=json.load(sys.stdin); print(d['worlds']['8']['step_ms'])") || exit 4
       echo "round $round s8 rank $r [$v] $ms" >> $O/ab_s8.txt
