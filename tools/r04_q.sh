@@ -37,4 +37,8 @@ for grp in "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d $O/pmc/pass$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-check --no-ingest > $O/pmc_pass$i.log 2>&1 || exit 10
 done
+timeout -k 10 200 python tools/probes/gemm_trace.py > $O/gemm_trace.jsonl 2>> $O/ab.err || exit 11
+timeout -k 10 200 python tools/probes/gemm_trace.py --opt bounds_wait=1 >> $O/gemm_trace.jsonl 2>> $O/ab.err || exit 11
+timeout -k 10 200 python tools/probes/gemm_trace.py --world 8 --rank 0 >> $O/gemm_trace.jsonl 2>> $O/ab.err || exit 11
+timeout -k 10 200 python tools/probes/gemm_trace.py --n 512 --p 32 >> $O/gemm_trace.jsonl 2>> $O/ab.err || exit 11
 echo done
