@@ -1757,22 +1757,19 @@ __device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t cblk)
 #pragma unroll
     for (int k = 0; k < kCrtMaxMod; ++k) r[k] = k < n ? rp[k * plane] : 0u;
     const int off = n * (n - 1) / 2;
-    // 16 accumulators, one per 16-bit limb of E_k: r (8 bit) x limb (16 bit)
-    // < 2^24; n <= 40 terms plus q x nmp stay below 2^31 -> no carries
-    uint32_t acc[16];
+    // one 64-bit accumulator per 32-bit word of E_k (v_mad_u64_u32): r (8 bit)
+    // x word (32 bit) summed over n <= 40 moduli stays below 2^46 -> no carries
+    // until the end (half the VALU of 16-bit limbs with 24-bit products)
+    uint64_t acc[8];
 #pragma unroll
-    for (int w = 0; w < 16; ++w) acc[w] = 0;
+    for (int w = 0; w < 8; ++w) acc[w] = 0;
     double sq = 0.0;
 #pragma unroll
     for (int k = 0; k < kCrtMaxMod; ++k) {
         if (k < n) {                                       // (uniform)
             sq = fma((double)r[k], c_crt_frac[off + k], sq);
 #pragma unroll
-            for (int w = 0; w < 8; ++w) {
-                const uint32_t e = c_crt_ep[off + k][w];
-                acc[2 * w] = __umul24(r[k], e & 0xffffu) + acc[2 * w];
-                acc[2 * w + 1] = __umul24(r[k], e >> 16) + acc[2 * w + 1];
-            }
+            for (int w = 0; w < 8; ++w) acc[w] += (uint64_t)r[k] * c_crt_ep[off + k][w];
         }
     }
     const uint32_t qq = (uint32_t)floor(sq + 0.5);         // < 2^14
@@ -1780,9 +1777,7 @@ __device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t cblk)
     uint64_t t = 0;
 #pragma unroll
     for (int w = 0; w < 8; ++w) {
-        const uint32_t e = c_crt_nmp[n][w];
-        t += (uint64_t)(__umul24(qq, e & 0xffffu) + acc[2 * w]) +
-             ((uint64_t)(__umul24(qq, e >> 16) + acc[2 * w + 1]) << 16);
+        t += acc[w] + (uint64_t)qq * c_crt_nmp[n][w];       // < 2^47 + carry
         x[w] = (uint32_t)t;
         t >>= 32;
     }
