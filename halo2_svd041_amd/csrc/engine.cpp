@@ -514,6 +514,7 @@ struct svdw_ctx {
     bool f64_views = true;                  // "f64_views"
     bool q_aside = true;                    // "q_aside" (A/B): quantize beside the product chain
     bool bounds_wait = false;               // "bounds_wait" (A/B): the u / v bounds wait for the products
+    bool gemm_big = true;                   // "gemm_tile" 256 | 128: CRT GEMM output tile edge
     std::vector<F64Src> f64src;
     DBuf colpart;
     DBuf qfold;                             // k_quantize_multi's fold counters + group maxima
@@ -1548,7 +1549,7 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
         while ((1ull << lk) < K) ++lk;
         const uint32_t kpad = (K + 255) / 256 * 256;      // whole groups of four 64-k chunks
         const uint32_t rpa = (N + 127) / 128 * 128, rpb = (M + 127) / 128 * 128;
-        ensure_buf(c, c->crtR, (size_t)kCrtMaxResidues * rpa * (sym ? rpa : rpb));
+        ensure_buf(c, c->crtR, crt_scratch_bytes(N, M));
         const uint8_t* Ar;
         if (a_from_b && sym) {
             Ar = (const uint8_t*)BB.p;                    // planes of this operand already built
@@ -1573,7 +1574,7 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
             ProfScope ps(c, s, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * N * M,
                          (double)N * M * K);
             hipck(launch_gemm_crt(sym, Ar, Br, N, M, rpa, sym ? rpa : rpb,
-                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s),
+                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s, c->gemm_big),
                   "k_gemm_crt");
         }
         if (!quantized)
@@ -2207,8 +2208,6 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
     ensure_buf(c, c->digA, (size_t)kCrtMaxResidues * rp_m * kpM);
     ensure_buf(c, c->digB, (size_t)kCrtMaxResidues * rp_v * kpM);
     ensure_buf(c, c->digC, (size_t)kCrtMaxResidues * rp_u * kpN);
-    ensure_buf(c, c->crtR, (size_t)kCrtMaxResidues * ceil_to(std::max(N, M), 128) *
-                               ceil_to(std::max(N, M), 128));
     ResSegs q;
     memset(&q, 0, sizeof q);
     auto seg = [&](const double* in, uint32_t rows, uint32_t cols, uint32_t rp, uint32_t kp,
@@ -2245,8 +2244,7 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
         memset(&b, 0, sizeof b);
         size_t rbytes[3], rtot = 0;
         for (int g = 0; g < 3; ++g) {
-            rbytes[g] = (size_t)kCrtMaxResidues * ceil_to(std::max<uint32_t>((uint32_t)(rr1[g] - rr0[g]), 1), 128) *
-                        ceil_to(B[g].cols, 128);
+            rbytes[g] = crt_scratch_bytes(std::max<uint32_t>((uint32_t)(rr1[g] - rr0[g]), 1), B[g].cols);
             rtot += rbytes[g];
         }
         ensure_buf(c, c->crtR, rtot);
@@ -2280,7 +2278,7 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
         c->gemm_batched = true;
         if (b.njobs) {
             ProfScope ps(c, pst, "k_gemm_crt:multi", bytes, ops);
-            hipck(launch_gemm_crt_multi(b, pst), "k_gemm_crt_multi");
+            hipck(launch_gemm_crt_multi(b, pst, c->gemm_big), "k_gemm_crt_multi");
         }
         const hipEvent_t done = stream_dep(c, pst, nullptr);   // one completion point
         for (int g = 0; g < 3; ++g) {
@@ -2868,7 +2866,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
         const uint32_t kpad = (K + 255) / 256 * 256, rpa = (N + 127) / 128 * 128, rpb = (M + 127) / 128 * 128;
         ensure_buf(c, c->digA, (size_t)kCrtMaxResidues * rpa * kpad);
         ensure_buf(c, c->digB, (size_t)kCrtMaxResidues * rpb * kpad);
-        ensure_buf(c, c->crtR, (size_t)kCrtMaxResidues * rpa * rpb);
+        ensure_buf(c, c->crtR, crt_scratch_bytes(N, M));
         ResSegs q;
         memset(&q, 0, sizeof q);
         auto seg = [&](const double* in, uint32_t rows, uint32_t ld, uint32_t rp, DBuf& out, uint32_t tr) {
@@ -2888,7 +2886,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
             ProfScope ps(c, c->st, "k_gemm_crt", 32.0 * N * M, (double)N * M * K);
             hipck(launch_gemm_crt(false, (const uint8_t*)c->digA.p, (const uint8_t*)c->digB.p, N, M, rpa, rpb,
                                   kpad, (uint8_t*)c->crtR.p, cellp(c, 0, off), M, 1, dbits, dbits + 1, lk,
-                                  c->st),
+                                  c->st, c->gemm_big),
                   "k_gemm_crt");
         }
     } else if (!c->dry) {
@@ -4224,6 +4222,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_crt = (int)value;
         } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
             c->stage_batch = value != 0;
+        } else if (n == "gemm_tile") {
+            REQUIRE(value == 128 || value == 256, "gemm_tile: 128 or 256");
+            c->gemm_big = value == 256;
         } else if (n == "bounds_wait") {
             c->bounds_wait = value != 0;
         } else if (n == "q_aside") {

@@ -1521,7 +1521,6 @@ static constexpr int CT = CT_TILE;     // CRT GEMM block tile (4 waves of 64 x 6
 // fragment reads (16 rows x 1 part) both land on 16 distinct 4-bank groups.
 static constexpr int CROW = 64;
 static constexpr uint32_t kCrtTileBytes = CT * CT;             // residues of one (tile, modulus)
-static constexpr uint32_t kCombBlocksPerTile = kCrtTileBytes / 256;
 __device__ __forceinline__ uint32_t crt_lds(uint32_t row, uint32_t part) {
     return row * CROW + 16u * (part ^ ((row >> 2) & 3u));
 }
@@ -1730,6 +1729,136 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
                   q.R, bi, bj, (int)mod, S, tp1, tp2);
     trace_block(t0, tp1, tp2);
 }
+// ---- 256 x 256 tiles (k_gemm_crt_big). 512 threads = 8 waves (2 x 4), each
+// 128 x 64 of the tile = 8 x 4 MFMA blocks (128 accumulator registers): four
+// times the MACs per staged byte of the 128 x 128 tile. Operands go global ->
+// LDS by global_load_lds (16 B per lane, no VGPR staging) into two stages of
+// 32 KiB (A and B: 256 rows x 64 B, the XOR-swizzled rows of crt_lds, the
+// swizzle applied on the source address since the DMA writes lane-linear);
+// the next stage's DMA stays in flight across the barrier (raw s_barrier and a
+// counted vmcnt: __syncthreads would drain it).
+static constexpr int CB = 256;
+static constexpr uint32_t kCrtBigTileBytes = CB * CB;
+static constexpr int kBigStage = 2 * CB * CROW;
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+// chunk `chunk` (64 k) of the tile's A and B rows into stage St: wave w moves A
+// rows [32w, 32w + 32) and B rows likewise, 16 rows (1 KiB) per instruction;
+// rows past the operands' last rows (amax / bmax: the last valid local row)
+// read that row again (their sums are never stored)
+__device__ __forceinline__ void big_issue(const uint8_t* __restrict__ Ap, const uint8_t* __restrict__ Bp,
+                                          uint32_t kpad, uint32_t amax, uint32_t bmax, uint32_t chunk,
+                                          uint8_t* St) {
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t r0 = 32 * w + 16 * h, row = r0 + (lane >> 2);
+        const uint32_t part = (lane & 3) ^ ((row >> 2) & 3);      // LDS part (lane & 3) holds this part
+        const uint64_t ko = (uint64_t)chunk * 64 + 16 * part;
+        __builtin_amdgcn_global_load_lds((glb_void_t*)(Ap + (uint64_t)min(row, amax) * kpad + ko),
+                                         (lds_void_t*)(St + r0 * CROW), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((glb_void_t*)(Bp + (uint64_t)min(row, bmax) * kpad + ko),
+                                         (lds_void_t*)(St + CB * CROW + r0 * CROW), 16, 0, 0);
+    }
+}
+__device__ __forceinline__ void crt_gemm_big_tile(const uint8_t* __restrict__ Ar, const uint8_t* __restrict__ Br,
+                                                  uint32_t astride, uint32_t bstride, uint32_t kpad,
+                                                  uint32_t nblk, uint32_t tile, uint8_t* __restrict__ R,
+                                                  uint32_t bi, uint32_t bj, int mod, uint8_t* S,
+                                                  uint32_t N, uint32_t M, uint64_t& tp1, uint64_t& tp2) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t wr = wave >> 2, wc = wave & 3;
+    const uint8_t* Ap = Ar + ((uint64_t)mod * astride + bi * CB) * kpad;
+    const uint8_t* Bp = Br + ((uint64_t)mod * bstride + bj * CB) * kpad;
+    const uint32_t amax = N - 1 - bi * CB, bmax = M - 1 - bj * CB;   // (the tile holds rows bi * CB < N)
+    const uint32_t kcn = kpad / 64;
+    v4i acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = v4i{0, 0, 0, 0};
+    const uint32_t frow = lane & 15, fpart = lane >> 4;
+    big_issue(Ap, Bp, kpad, amax, bmax, 0, S);
+    big_issue(Ap, Bp, kpad, amax, bmax, 1, S + kBigStage);            // (kpad >= 256: kcn >= 4)
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                 // chunk 0 landed (this thread's part)
+    __builtin_amdgcn_s_barrier();                                    // ... and every thread's
+    tp1 = wall_clock64();
+    for (uint32_t c = 0; c < kcn; ++c) {
+        const uint8_t* St = S + (c & 1) * kBigStage;
+        v4i af[8], bf[4];
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+            af[a] = *reinterpret_cast<const v4i*>(St + crt_lds(wr * 128 + a * 16 + frow, fpart));
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            bf[b] = *reinterpret_cast<const v4i*>(St + CB * CROW + crt_lds(wc * 64 + b * 16 + frow, fpart));
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");              // this wave's reads of stage c & 1 done
+        __builtin_amdgcn_s_barrier();                                    // every wave's
+        if (c + 2 < kcn) {
+            big_issue(Ap, Bp, kpad, amax, bmax, c + 2, S + (c & 1) * kBigStage);
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");             // chunk c + 1 landed
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+    }
+    tp2 = wall_clock64();
+    // residues in MFMA order: word (wave, a, b, lane) holds rows (lane >> 4) * 4 +
+    // reg of block (a, b); a wave store is 256 contiguous bytes (crt_elem_big)
+    const int m = (int)c_crt_mod[mod];
+    const float inv = c_crt_invf[mod];
+    uint32_t* Rt = reinterpret_cast<uint32_t*>(R + ((uint64_t)mod * nblk + tile) * kCrtBigTileBytes) +
+                   wave * 2048 + lane;
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                const int av = acc[a][b][reg];                     // |av| <= 2^27
+                const int q = (int)floorf((float)av * inv);
+                int r = av - __mul24(q, m);
+                r += r < 0 ? m : 0;
+                r -= r >= m ? m : 0;
+                w |= (uint32_t)r << (8 * reg);
+            }
+            Rt[(a * 4 + b) * 64] = w;
+        }
+}
+__global__ __launch_bounds__(512) void k_gemm_crt_big(const CrtBatch b) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[2 * kBigStage];
+    const uint64_t t0 = wall_clock64();
+    uint32_t cnt[kMaxCrtJobs], total = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxCrtJobs; ++j) {
+        cnt[j] = 0;
+        if ((uint32_t)j < b.njobs)
+            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk;
+        total += cnt[j];
+    }
+    const uint32_t per = (total + 7) / 8, k = blockIdx.x >> 3;
+    if (k >= per) return;
+    uint32_t u = (blockIdx.x & 7) * per + k;
+    if (u >= total) return;
+    uint32_t j = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxCrtJobs - 1; ++q)
+        if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
+    const CrtJob& q = b.job[j];
+    const uint32_t mod = u / q.nblk, t = u - mod * q.nblk;
+    uint32_t bi, bj;
+    crt_tile_rc(q, t, &bi, &bj);
+    uint64_t tp1 = 0, tp2 = 0;
+    crt_gemm_big_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.nblk, t,
+                      q.R, bi, bj, (int)mod, S, q.N, q.sym ? q.N : q.M, tp1, tp2);
+    trace_block(t0, tp1, tp2);
+}
 // C from its n residues, written as canonical Fr to out[i*ors + j*ocs]: one
 // element per thread in the GEMM's tile order (each block one 256-element
 // stretch of a tile), so a wave reads 64 consecutive residue bytes per modulus
@@ -1739,20 +1868,29 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
 // keeps it exact), accumulated carry-free in 16-bit limbs, one 9-word
 // reduction. SYM: elements j >= i of the upper tiles (the GEMM computed upper
 // and diagonal 128-tiles), each also stored at (j, i).
+template <bool BIG>
 __device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t cblk) {
     const int n = crt_nmod(*q.bits_a, *q.bits_b, q.lk);
     if (!n) return;
     // element e of tile t in the GEMM's MFMA order (wave, a, b, lane, reg)
-    const uint32_t tl = cblk / kCombBlocksPerTile;
-    const uint32_t e = (cblk - tl * kCombBlocksPerTile) * 256 + threadIdx.x;
-    const uint32_t reg = e & 3, ln = (e >> 2) & 63, ab = (e >> 8) & 15, w = e >> 12;
-    uint32_t bi, bj;
+    constexpr uint32_t TB = BIG ? kCrtBigTileBytes : kCrtTileBytes, BPT = TB / 256;
+    const uint32_t tl = cblk / BPT;
+    const uint32_t e = (cblk - tl * BPT) * 256 + threadIdx.x;
+    const uint32_t reg = e & 3, ln = (e >> 2) & 63;
+    uint32_t bi, bj, i, j;
     crt_tile_rc(q, tl, &bi, &bj);
-    const uint32_t i = bi * CT + (w >> 1) * 64 + (ab >> 2) * 16 + (ln >> 4) * 4 + reg;
-    const uint32_t j = bj * CT + (w & 1) * 64 + (ab & 3) * 16 + (ln & 15);
+    if (BIG) {                                   // 8 waves (2 x 4) of 8 x 4 blocks
+        const uint32_t ab = (e >> 8) & 31, w = e >> 13;
+        i = bi * CB + (w >> 2) * 128 + (ab >> 2) * 16 + (ln >> 4) * 4 + reg;
+        j = bj * CB + (w & 3) * 64 + (ab & 3) * 16 + (ln & 15);
+    } else {                                     // 4 waves (2 x 2) of 4 x 4 blocks
+        const uint32_t ab = (e >> 8) & 15, w = e >> 12;
+        i = bi * CT + (w >> 1) * 64 + (ab >> 2) * 16 + (ln >> 4) * 4 + reg;
+        j = bj * CT + (w & 1) * 64 + (ab & 3) * 16 + (ln & 15);
+    }
     if (i >= q.N || j >= q.M || (q.sym && j < i)) return;
-    const uint64_t plane = (uint64_t)q.nblk * kCrtTileBytes;
-    const uint8_t* __restrict__ rp = q.R + (uint64_t)tl * kCrtTileBytes + e;
+    const uint64_t plane = (uint64_t)q.nblk * TB;
+    const uint8_t* __restrict__ rp = q.R + (uint64_t)tl * TB + e;
     uint32_t r[kCrtMaxMod];
 #pragma unroll
     for (int k = 0; k < kCrtMaxMod; ++k) r[k] = k < n ? rp[k * plane] : 0u;
@@ -1793,24 +1931,32 @@ __device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t cblk)
 // XCD-contiguously: XCD x takes a contiguous run of the row-major tile
 // sequence, so the halves of a 128-byte residue line that neighbouring tiles
 // read come through the same L2.
+template <bool BIG>
 __global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b, uint32_t cblocks) {
     const uint32_t per = (cblocks + 7) / 8, t = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
     if (t >= cblocks) return;
     uint32_t j = 0;
     for (uint32_t k = 1; k < b.njobs; ++k) j += t >= b.job[k].cblk0;
-    crt_combine_elem(b.job[j], t - b.job[j].cblk0);
+    crt_combine_elem<BIG>(b.job[j], t - b.job[j].cblk0);
 }
 
-hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
+size_t crt_scratch_bytes(uint32_t N, uint32_t M) {
+    // the residue scratch R of either tile shape: kCrtMaxMod planes of whole tiles
+    const uint64_t a = ((uint64_t)N + CB - 1) / CB * CB, m = ((uint64_t)M + CB - 1) / CB * CB;
+    return (size_t)(kCrtMaxMod * a * m);
+}
+hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st, bool big) {
     CrtBatch b = b0;
     if (b.njobs < 1 || b.njobs > (uint32_t)kMaxCrtJobs) return hipErrorInvalidValue;
     uint32_t units = 0, cblocks = 0;
+    const uint32_t T = big ? CB : CT;
     for (uint32_t j = 0; j < b.njobs; ++j) {
         CrtJob& q = b.job[j];
-        q.tiles_a = (q.N + CT - 1) / CT;
-        q.tiles_m = q.sym ? q.tiles_a : (q.M + CT - 1) / CT;
-        // every staged row (tiles x CT) lies inside its operand's planes
-        if (q.kpad % 256 || q.astride < q.tiles_a * CT || (!q.sym && q.bstride < q.tiles_m * CT))
+        q.tiles_a = (q.N + T - 1) / T;
+        q.tiles_m = q.sym ? q.tiles_a : (q.M + T - 1) / T;
+        // every staged row (tiles x CT) lies inside its operand's planes (the big
+        // tiles clamp their row reads to the planes instead)
+        if (q.kpad % 256 || (!big && (q.astride < q.tiles_a * CT || (!q.sym && q.bstride < q.tiles_m * CT))))
             return hipErrorInvalidValue;
         if (q.sym && q.N != q.M) return hipErrorInvalidValue;
         q.nblk = q.sym ? q.tiles_a * (q.tiles_a + 1) / 2 : q.tiles_a * q.tiles_m;
@@ -1822,19 +1968,25 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
         }
         units += kCrtMaxMod * q.nblk;                    // upper bound: n = kCrtMaxMod
         q.cblk0 = cblocks;
-        cblocks += q.nblk * kCombBlocksPerTile;
+        cblocks += q.nblk * ((big ? kCrtBigTileBytes : kCrtTileBytes) / 256);
     }
-    hipLaunchKernelGGL(k_gemm_crt_multi, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
+    if (big)
+        hipLaunchKernelGGL(k_gemm_crt_big, dim3((units + 7) / 8 * 8), dim3(512), 0, st, b);
+    else
+        hipLaunchKernelGGL(k_gemm_crt_multi, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_crt_combine_multi, dim3((cblocks + 7) / 8 * 8), dim3(256), 0, st, b, cblocks);
+    if (big)
+        hipLaunchKernelGGL(k_crt_combine_multi<true>, dim3((cblocks + 7) / 8 * 8), dim3(256), 0, st, b, cblocks);
+    else
+        hipLaunchKernelGGL(k_crt_combine_multi<false>, dim3((cblocks + 7) / 8 * 8), dim3(256), 0, st, b, cblocks);
     return hipGetLastError();
 }
 
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st) {
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st, bool big) {
     if (sym && (N != M || astride != bstride)) return hipErrorInvalidValue;
     CrtBatch b;
     memset(&b, 0, sizeof b);
@@ -1855,7 +2007,7 @@ hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint3
     q.M = M;
     q.lk = lk;
     q.sym = sym;
-    return launch_gemm_crt_multi(b, st);
+    return launch_gemm_crt_multi(b, st, big);
 }
 
 // -------------------------------------------------------- Montgomery GEMM

@@ -306,12 +306,12 @@ struct ResSegs {
 hipError_t launch_residues_f64(const ResSegs& q, const unsigned* W, int precision_bits,
                                hipStream_t st);
 // c_s = A * Bt from residue planes Ar (plane stride astride rows, from the A rows'
-// first row) and Br (bstride): N x M, tiles of 128 rows / columns read from each;
-// R is the residue scratch [kCrtMaxResidues][ceil128(N)][ceil128(M)] bytes.
+// first row) and Br (bstride): N x M; R is the residue scratch
+// (crt_scratch_bytes(N, M) bytes).
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st);
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st, bool big);
 // Debug: record the CRT GEMM's block timeline into buf (3 u64 per block; null: off).
 hipError_t set_debug_trace(void* buf);
 static constexpr int kCrtMaxResidues = 40;   // = kCrtMaxMod (crt_tables.hpp)
@@ -342,7 +342,11 @@ struct CrtBatch {
     CrtJob job[kMaxCrtJobs];
     uint32_t njobs;
 };
-hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st);
+// big: 256 x 256 output tiles (k_gemm_crt_big: 8 waves, operands by
+// global_load_lds), else 128 x 128 (k_gemm_crt_multi); R sized crt_scratch_bytes
+hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st, bool big);
+// residue scratch R one CRT product of N x M needs (either tile shape)
+size_t crt_scratch_bytes(uint32_t N, uint32_t M);
 // w (len L) from a view (row 0 / col j of a 1 x L view) -> canonical copy
 // (w_canon nullable) and its scaled table (ScaleTab f: see kTabSlots).
 hipError_t launch_vec_prep(const DView& w, uint32_t L, Fr* w_canon, Fr* tab, const ScaleTab& f,
