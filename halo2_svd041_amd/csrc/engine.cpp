@@ -579,18 +579,12 @@ struct svdw_ctx {
     // ---- captured verify_mul_witness ("graph", vm_graph): the launch sequence of
     // a device-input call is captured once into a HIP graph (the second call of
     // a shape, when every buffer is sized) and replayed by later calls of the
-    // same key; gamma enters only through k_gamma_prep, launched eagerly on st3
-    // beside the graph (gp_external, gx_ev), so the graph itself is gamma-free.
+    // same key; gamma enters only through k_gamma_prep, launched eagerly on st
+    // ahead of the graph (gp_external), so the graph itself is gamma-free.
     int graph_vm = 1;                       // "graph": 0 off, 1 verify_mul_witness
     bool capturing = false;                 // st is capturing: no allocation, no sync
     bool gp_external = false;               // verify_mul_witness: k_gamma_prep already queued
     const Fr* gp_ext_one = nullptr;         // the one cell it wrote (null: none)
-    // that launch went out eagerly on st3 beside the graph (verify_mul_witness_api):
-    // gx_ev is recorded behind it, gx_prev on st before it (the previous call's
-    // graph still reads the tables); the graph waits for gx_ev as an external
-    // event node, so its product chain does not wait for gamma
-    hipEvent_t gx_ev = nullptr, gx_prev = nullptr;
-    bool gp_ev_ext = false;                 // gp_ev is gx_ev (external to a capture)
     uint64_t epoch = 0;                     // bumped by every allocation / option change
     // (layout_chk index, eqk slot) of the constants that hold gamma (the
     // verify_mul gamma powers' init_rand), patched on replay
@@ -1879,11 +1873,7 @@ static void gamma_prep(svdw_ctx* c, uint32_t d, const Fr& gamma, hipStream_t s, 
 static void ensure_gamma_vec(svdw_ctx* c, uint32_t d, const Fr& gamma) {
     if (c->dry) return;
     if (c->gp_ev && c->gp_len >= d && fr_eq(c->gp_gamma, gamma)) {
-        if (c->gp_ev_ext)
-            hipck(hipStreamWaitEvent(c->st, c->gp_ev, c->capturing ? hipEventWaitExternal : 0u),
-                  "hipStreamWaitEvent");
-        else if (c->gp_st != c->st)
-            dep_wait(c, c->st, c->gp_ev);
+        if (c->gp_st != c->st) dep_wait(c, c->st, c->gp_ev);
         return;
     }
     gamma_prep(c, d, gamma, c->st);
@@ -2796,17 +2786,14 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
         // (queued ahead: only if that launch wrote them where they are now)
         if (c->ph[1].n == 0 && vm_pow_cells(c, M, gamma, &pc) && (!c->gp_external || c->gp_ext_one == pc.one))
             c->pows_pre = {true, 0, 1, M};
-        if (c->gp_external) {                         // queued on st3 ahead of this call (gx_ev)
+        if (c->gp_external) {                         // queued on st ahead of the captured graph
             c->gp_gamma = gamma;
             c->gp_len = std::max(M, 1u);
-            c->gp_ev = c->gx_ev;
-            c->gp_st = nullptr;
-            c->gp_ev_ext = true;
         } else {
             gamma_prep(c, M, gamma, c->st3, pc.one ? &pc : nullptr);
-            c->gp_ev = stream_dep(c, c->st3, nullptr);
-            c->gp_st = c->st3;
         }
+        c->gp_ev = stream_dep(c, c->st3, nullptr);
+        c->gp_st = c->st3;
         ensure_buf(c, c->bits, (64 + nba + nbb) * sizeof(unsigned));
         dbits = (unsigned*)c->bits.p;
     }
@@ -2921,9 +2908,8 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
 // ~70 us at 256^2 (BASELINE config 2), so the host bounds it. Every call of
 // one key (shape, input pointers, buffer epoch) enqueues the same launches:
 // nothing in it waits for the device, and gamma reaches the device only as
-// k_gamma_prep's tables. So k_gamma_prep goes out eagerly on st3 (by value;
-// the graph's row scans wait for it through an external event node, its
-// product chain does not), the rest is captured once (on the second call of a key, when every buffer
+// k_gamma_prep's tables. So k_gamma_prep goes out eagerly on st (by value),
+// the rest is captured once (on the second call of a key, when every buffer
 // is sized) and replayed with one hipGraphLaunch; the host state the call
 // leaves (layout, checks, counts) is restored from the capture, with gamma
 // patched into the constants that hold it.
@@ -2978,28 +2964,18 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
         svdw_ctx* c;
         ~Flags() {
             c->gp_external = false;
-            c->gp_ev_ext = false;
             c->capturing = false;
             c->gp_ev = nullptr;
             c->pows_pre.on = false;
         }
     } flags{c};
     // gamma's tables (and the one / gamma-power cells when phase 1 holds them)
-    // on st3, beside the call's product chain: st3 first waits for everything
-    // queued on st (the previous call's graph still reads the tables), and the
-    // call's row scans wait for gx_ev (in the graph: an external event node,
-    // waiting for the record made before that launch)
-    if (!c->gx_ev) {
-        hipck(hipEventCreateWithFlags(&c->gx_ev, hipEventDisableTiming), "hipEventCreate");
-        hipck(hipEventCreateWithFlags(&c->gx_prev, hipEventDisableTiming), "hipEventCreate");
-    }
+    // on st, ahead of everything the call queues. (Round 4 tried them on st3
+    // beside the graph, the graph's scans waiting through an external event
+    // node (hipEventWaitExternal): the runtime aborted in the capture/replay.)
     PowCells pc;
     const bool pw = vm_pow_cells(c, M, gamma, &pc);
-    flush_batch(c, c->st);
-    hipck(hipEventRecord(c->gx_prev, c->st), "hipEventRecord");
-    hipck(hipStreamWaitEvent(c->st3, c->gx_prev, 0), "hipStreamWaitEvent");
-    gamma_prep(c, M, gamma, c->st3, pw ? &pc : nullptr);
-    hipck(hipEventRecord(c->gx_ev, c->st3), "hipEventRecord");
+    gamma_prep(c, M, gamma, c->st, pw ? &pc : nullptr);
     c->gp_external = true;
     c->gp_ext_one = pw ? pc.one : nullptr;
     const std::vector<uint64_t> key = {N, K, M, (uint64_t)(uintptr_t)a, (uint64_t)(uintptr_t)b, c->epoch};
@@ -3258,8 +3234,6 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             }
             if (c->hbits) (void)hipHostFree(c->hbits);
             if (c->ev_bits) (void)hipEventDestroy(c->ev_bits);
-            if (c->gx_ev) (void)hipEventDestroy(c->gx_ev);
-            if (c->gx_prev) (void)hipEventDestroy(c->gx_prev);
             for (auto e : c->xev)
                 if (e) (void)hipEventDestroy(e);
             for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
