@@ -512,9 +512,9 @@ struct svdw_ctx {
     struct F64Region { uint32_t phase; uint64_t off, n; const double* x; };
     std::vector<F64Region> f64reg;
     bool f64_views = true;                  // "f64_views"
-    bool q_aside = true;                    // "q_aside" (A/B): quantize beside the product chain
+    bool q_aside = true;                    // "q_aside": quantize beside the product chain (quantize_aside)
+    BitMax bx_pend{};                       // its maxima, reduced by the next residue launch
     bool bounds_wait = false;               // "bounds_wait" (A/B): the u / v bounds wait for the products
-    bool gemm_big = true;                   // "gemm_tile" 256 | 128: CRT GEMM output tile edge
     std::vector<F64Src> f64src;
     DBuf colpart;
     DBuf qfold;                             // k_quantize_multi's fold counters + group maxima
@@ -812,13 +812,12 @@ static void bits_words(svdw_ctx* c, QuantSegs& qs, uint32_t nred, const BitSegs&
 }
 // Quantization off the product chain: when every in-witness reader of the
 // loaded cells goes through an f64 view (f64_views) and the products' residue
-// planes come from the f64 inputs, the GEMM needs only the operand bit-length
-// words. k_bits_f64 writes those on st (read-only, 8 B per value, the fold of
-// qs), and k_quantize_multi writes the cells on `aside` beside the residues
-// and GEMM. The caller joins `aside` into st before the witness ends.
+// planes come from the f64 inputs on the cell stream, the GEMM needs only the
+// operand bit-length words. k_bits_f64 writes per-block maxima of m, u, v on st
+// (read-only, 8 B per value, no fold), the residue launch reduces them
+// (c->bx_pend; ev_bits is recorded behind it), and k_quantize_multi writes the
+// cells on `aside` beside the chain. The caller joins `aside` into st.
 static void quantize_aside(svdw_ctx* c, const QuantSegs& qs, uint32_t nbit_segs, hipStream_t aside) {
-    QuantSegs qb = qs;
-    qb.nseg = nbit_segs;
     double nb = 0, nq = 0;
     for (uint32_t k = 0; k < qs.nseg; ++k) {
         nq += (double)qs.n[k];
@@ -826,7 +825,7 @@ static void quantize_aside(svdw_ctx* c, const QuantSegs& qs, uint32_t nbit_segs,
     }
     {
         ProfScope ps(c, c->st, "k_bits_f64", 8.0 * nb, 0);
-        hipck(launch_bits_f64(qb, (int)c->P, c->st), "k_bits_f64");
+        hipck(launch_bits_f64(qs, nbit_segs, (int)c->P, qs.blockmax[0], &c->bx_pend, c->st), "k_bits_f64");
     }
     QuantSegs qq = qs;
     for (uint32_t k = 0; k < (uint32_t)kMaxQuantSegs; ++k) qq.blockmax[k] = nullptr;
@@ -1568,7 +1567,7 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
             ProfScope ps(c, s, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * N * M,
                          (double)N * M * K);
             hipck(launch_gemm_crt(sym, Ar, Br, N, M, rpa, sym ? rpa : rpb,
-                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s, c->gemm_big),
+                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s),
                   "k_gemm_crt");
         }
         if (!quantized)
@@ -2182,7 +2181,7 @@ static BigU scale_err(double err, uint32_t p) {
 // products' stream offsets (dry replay); W: the device bit-length words of m, u, v.
 static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const svdw_mat (&B)[3],
                                    const std::vector<uint64_t>& log, uint32_t phase,
-                                   const unsigned* W, hipStream_t pst) {
+                                   unsigned* W, hipStream_t pst) {
     const uint32_t N = A[0].rows, M = A[0].cols;
     auto clog2 = [](uint32_t k) { uint32_t l = 0; while ((1ull << l) < k) ++l; return l; };
     auto ceil_to = [](uint32_t x, uint32_t a) { return (x + a - 1) / a * a; };
@@ -2212,10 +2211,17 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
     if (rows_m) seg(c->svd_f64[0] + rr0[0] * M, rows_m, M, rp_m, kpM, c->digA, {{0, 2, (int)lkM}});
     seg(c->svd_f64[2], M, M, rp_v, kpM, c->digB, {{0, 2, (int)lkM}, {2, 2, (int)lkM}});
     seg(c->svd_f64[1], N, N, rp_u, kpN, c->digC, {{1, 1, (int)lkN}});
+    q.bx = c->bx_pend;                    // (quantize_aside: the words come from its maxima)
+    REQUIRE(!q.bx.bm || pst == c->st, "internal: bit maxima reduced off the cell stream");
     {
         ProfScope ps(c, pst, "k_residues_f64",
                      8.0 * ((double)rows_m * M + (double)M * M + (double)N * N), 0);
         hipck(launch_residues_f64(q, W, (int)c->P, pst), "k_residues_f64");
+    }
+    if (q.bx.bm) {                        // the words are final here
+        flush_batch(c, pst);
+        hipck(hipEventRecord(c->ev_bits, pst), "hipEventRecord");
+        memset(&c->bx_pend, 0, sizeof c->bx_pend);
     }
     // the stages beside the products wait for the residue planes, which then
     // run alone instead of beside the first (HBM-saturating) stages (same box:
@@ -2268,7 +2274,7 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
         c->gemm_batched = true;
         if (b.njobs) {
             ProfScope ps(c, pst, "k_gemm_crt:multi", bytes, ops);
-            hipck(launch_gemm_crt_multi(b, pst, c->gemm_big), "k_gemm_crt_multi");
+            hipck(launch_gemm_crt_multi(b, pst), "k_gemm_crt_multi");
         }
         const hipEvent_t done = stream_dep(c, pst, nullptr);   // one completion point
         for (int g = 0; g < 3; ++g) {
@@ -2349,7 +2355,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         const unsigned* sa[3] = {sl[0], sl[1], sl[2]};
         const unsigned* sb[3] = {sl[2], sl[1], sl[2]};
         if (from_f64) {
-            prelaunch_products_f64(c, A, B, log, m.phase, dev_bits, pst);
+            prelaunch_products_f64(c, A, B, log, m.phase, const_cast<unsigned*>(dev_bits), pst);   // (c->bits)
             c->prelaunched = true;
             host_mark(c, "products queued");
             return;
@@ -2624,8 +2630,12 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     bits_words(c, qs, 3, seg, dbits, &folded);
     // the cells beside the product chain on st2 (its stages wait for the
     // residue planes anyway) when no launch of the witness reads them
+    // (the products on the cell stream: their residue launch, on st behind
+    // k_bits_f64, reduces its maxima into the words)
     const bool q_aside = c->q_aside && folded && qs.nseg == 4 && on_device && !c->dry && c->f64_views && c->overlap &&
-                         c->res_f64 && c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA && N <= 8192 && M <= 8192;
+                         c->res_f64 && c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA && N <= 8192 && M <= 8192 &&
+                         (c->prod_cell > 0 || (c->prod_cell < 0 && sharded(c)));
+    memset(&c->bx_pend, 0, sizeof c->bx_pend);
     if (q_aside) {
         quantize_aside(c, qs, 3, c->st2);
     } else if (qs.nseg) {
@@ -2638,7 +2648,9 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     if (!c->dry) {   // operand bit lengths (GEMM digit counts): read lazily, see fetch_bits
         if (!folded) hipck(launch_bits_reduce(dbits + 64, seg, 3, dbits, c->st), "k_bits_reduce");
         flush_batch(c, c->st);
-        hipck(hipEventRecord(c->ev_bits, c->st), "hipEventRecord");
+        // (q_aside: the words exist once the residue launch has reduced them;
+        // prelaunch_products_f64 records ev_bits behind it)
+        if (!q_aside) hipck(hipEventRecord(c->ev_bits, c->st), "hipEventRecord");
         c->bits_pending = true;
         c->qmat[0] = zm; c->qmat[1] = zu; c->qmat[2] = zv;
         // the same words for the device-side choices (row-scan operand widths)
@@ -2707,6 +2719,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     svdw_svd_payload pl =
         check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits, dbits, true);
     c->early_p1 = nullptr;
+    REQUIRE(!c->bx_pend.bm, "internal: k_bits_f64's maxima were never reduced (no f64 product launch)");
     const bool p1_overlap = p1mode && c->prelaunched && !c->dry;
     hipStream_t p1s = p1mode == 2 ? c->st3 : c->st2;
     host_mark(c, "phase 0 queued");
@@ -2808,13 +2821,9 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     seg.begin[2] = nba + nbb;
     bool folded = false;
     bits_words(c, qs, 2, seg, dbits, &folded);
-    // the cells on st2 beside the chain when only f64 views and the f64
-    // residue planes read the loads (quantize_aside); st2 joins st at the end
-    const bool q_aside = c->q_aside && folded && qs.nseg == 2 && on_device && !c->dry && c->f64_views && c->res_f64 &&
-                         c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA && K <= 8192;
-    if (q_aside) {
-        quantize_aside(c, qs, 2, c->st2);
-    } else if (qs.nseg) {
+    // (quantization stays on the chain here: beside it on st2, config 2 measured
+    // 0.091-0.096 -> 0.106 ms, host-bound, round 4)
+    if (qs.nseg) {
         ProfScope ps(c, c->st, "k_quantize", 40.0 * ((double)N * K + (double)K * M), 0);
         hipck(launch_quantize_multi(qs, (int)c->P, c->st), "k_quantize_multi");
     }
@@ -2873,7 +2882,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
             ProfScope ps(c, c->st, "k_gemm_crt", 32.0 * N * M, (double)N * M * K);
             hipck(launch_gemm_crt(false, (const uint8_t*)c->digA.p, (const uint8_t*)c->digB.p, N, M, rpa, rpb,
                                   kpad, (uint8_t*)c->crtR.p, cellp(c, 0, off), M, 1, dbits, dbits + 1, lk,
-                                  c->st, c->gemm_big),
+                                  c->st),
                   "k_gemm_crt");
         }
     } else if (!c->dry) {
@@ -2898,7 +2907,6 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     } else {
         verify_mul_many(c, 1, &vm, 1, gamma);
     }
-    if (q_aside && !c->capturing) stream_dep(c, c->st2, c->st);   // (a capture joins st2 itself)
     host_mark(c, "verify_mul_witness end");
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
 }
@@ -4196,9 +4204,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_crt = (int)value;
         } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
             c->stage_batch = value != 0;
-        } else if (n == "gemm_tile") {
-            REQUIRE(value == 128 || value == 256, "gemm_tile: 128 or 256");
-            c->gemm_big = value == 256;
         } else if (n == "bounds_wait") {
             c->bounds_wait = value != 0;
         } else if (n == "q_aside") {

@@ -222,37 +222,64 @@ __global__ __launch_bounds__(256) void k_quantize_multi(const QuantSegs q, doubl
         }
     quantize_body(in, n, out, scale, bm, blockIdx.x - b0, keep, q.fold, blockIdx.x);
 }
-// The operand bit-length words alone, read-only from the f64 inputs (the
-// segments and block layout of k_quantize_multi, its fold): the residue planes
-// and the GEMM need only these, so the quantized cells can be written beside
-// the product chain instead of ahead of it (8 B read per value).
-__global__ __launch_bounds__(256) void k_bits_f64(const QuantSegs q, double scale) {
+// The operand bit-length maxima alone, read-only from the f64 inputs: block b of
+// matrix s covers vpb values of it (kQuantPerBlock per round), writes one
+// maximum, no cross-block fold (same-address atomics of ~800 blocks serialised
+// to ~20 us at 1024^2, measured); k_residues_f64 reduces the ranges it needs.
+struct BitArgs {
+    const double* in[3];
+    uint64_t n[3];
+    uint32_t begin[4];
+    uint32_t vpb;
+    unsigned* bm;
+};
+__global__ __launch_bounds__(256) void k_bits_f64(const BitArgs a, double scale) {
     constexpr int PT = kQuantPerBlock / 256;
     uint32_t s = 0;
 #pragma unroll
-    for (int k = 1; k < kMaxQuantSegs; ++k) s += (uint32_t)k < q.nseg && blockIdx.x >= q.blk0[k];
-    const double* in = q.in[0];
-    unsigned* bm = q.blockmax[0];
-    uint64_t n = q.n[0];
-    uint32_t b0 = q.blk0[0];
+    for (int k = 1; k < 3; ++k) s += blockIdx.x >= a.begin[k];
+    const double* in = s == 0 ? a.in[0] : s == 1 ? a.in[1] : a.in[2];
+    const uint64_t n = s == 0 ? a.n[0] : s == 1 ? a.n[1] : a.n[2];
+    const uint64_t v0 = (uint64_t)(blockIdx.x - a.begin[s]) * a.vpb;
+    uint32_t bmax = 0;
+    for (uint32_t r = 0; r < a.vpb; r += kQuantPerBlock) {
+        double xv[PT];
 #pragma unroll
-    for (int k = 1; k < kMaxQuantSegs; ++k)
-        if (s == (uint32_t)k) { in = q.in[k]; bm = q.blockmax[k]; n = q.n[k]; b0 = q.blk0[k]; }
-    const uint32_t blk = blockIdx.x - b0;
-    const uint64_t i0 = (uint64_t)blk * kQuantPerBlock + threadIdx.x;
-    double xv[PT];
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-        const uint64_t i = i0 + 256ull * k;
-        xv[k] = i < n ? __builtin_nontemporal_load(in + i) : 0.0;
+        for (int k = 0; k < PT; ++k) {
+            const uint64_t i = v0 + r + threadIdx.x + 256ull * k;
+            xv[k] = i < n ? __builtin_nontemporal_load(in + i) : 0.0;
+        }
+        bmax = max(bmax, block_bits<PT>(xv, scale));
+        __syncthreads();                                // (block_bits' LDS reused next round)
     }
-    const uint32_t bmax = block_bits<PT>(xv, scale);
-    if (q.fold.wout && blockIdx.x < q.fold.nblk) bits_fold(q.fold, blockIdx.x, bmax);
-    else if (bm && threadIdx.x == 0) bm[blk] = bmax;
+    if (threadIdx.x == 0) a.bm[blockIdx.x] = bmax;
 }
-hipError_t launch_bits_f64(const QuantSegs& q, int p, hipStream_t st) {
-    if (!q.nseg || q.nseg > (uint32_t)kMaxQuantSegs || !q.blk0[q.nseg]) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_bits_f64, dim3(q.blk0[q.nseg]), dim3(256), 0, st, q, (double)(1ull << p));
+hipError_t launch_bits_f64(const QuantSegs& q, uint32_t nseg, int p, unsigned* maxima, BitMax* bx,
+                           hipStream_t st) {
+    if (nseg < 1 || nseg > 3 || nseg > q.nseg) return hipErrorInvalidValue;
+    BitArgs a;
+    memset(&a, 0, sizeof a);
+    uint64_t tot = 0;
+    for (uint32_t k = 0; k < nseg; ++k) tot += q.n[k];
+    // ~512 blocks whatever the size (so the consumers' reductions stay short)
+    const uint64_t want = (tot + 511) / 512;
+    const uint64_t vpb = (want + kQuantPerBlock - 1) / kQuantPerBlock * kQuantPerBlock;
+    a.vpb = (uint32_t)(vpb > kQuantPerBlock ? vpb : kQuantPerBlock);
+    uint32_t blocks = 0;
+    for (uint32_t k = 0; k < 3; ++k) {
+        a.begin[k] = blocks;
+        if (k < nseg) {
+            a.in[k] = q.in[k];
+            a.n[k] = q.n[k];
+            blocks += (uint32_t)((q.n[k] + a.vpb - 1) / a.vpb);
+        }
+    }
+    a.begin[3] = blocks;
+    a.bm = maxima;
+    bx->bm = maxima;
+    for (int k = 0; k < 4; ++k) bx->begin[k] = a.begin[k];
+    if (!blocks) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_bits_f64, dim3(blocks), dim3(256), 0, st, a, (double)(1ull << p));
     return hipGetLastError();
 }
 hipError_t launch_quantize_multi(const QuantSegs& q, int p, hipStream_t st) {
@@ -1321,9 +1348,13 @@ hipError_t launch_gemm_mfma(int DA, int DB, bool sym, const uint8_t* Ad, const u
 __device__ __forceinline__ int crt_nmod(uint32_t ba, uint32_t bb, uint32_t lk) {
     if (ba > 128 || bb > 128) return 0;
     const uint32_t need = ba + bb + lk + 2;
-    for (int n = 1; n <= kCrtMaxMod; ++n)
-        if (c_crt_cum_bits[n] >= need) return n;
-    return 0;
+    // lane k tests table entry k + 1 (one load per lane; a scalar loop of
+    // dependent loads cost ~2 us per call, measured in the GEMM's block
+    // prologue). Called with the whole wave active.
+    const uint32_t lane = threadIdx.x & 63;
+    const bool ok = lane < (uint32_t)kCrtMaxMod && c_crt_cum_bits[lane + 1] >= need;
+    const unsigned long long m = __ballot(ok);
+    return m ? __ffsll(m) : 0;
 }
 
 // Balanced residues bal = ((x + h) mod m) - h, h = floor(m / 2), in [-128, 127],
@@ -1446,18 +1477,39 @@ __device__ __forceinline__ void quantized_words(double x, double scale, uint32_t
 // Residue planes straight from the f64 inputs of svd_witness (what k_to_residues
 // computes from the quantized cells, without reading the 32 B cells back): up to
 // kMaxResSegs matrices in one launch, segment s covering blocks [blk0[s], blk0[s+1]).
-__global__ __launch_bounds__(256) void k_residues_f64(const ResSegs q, const unsigned* __restrict__ W,
+// Bit-length words 0..2 from k_bits_f64's per-block maxima (BitMax): one
+// block-wide max per range, every lane of the block holding the results.
+__device__ __forceinline__ void bit_words_from_maxima(const BitMax& bx, uint32_t (&w)[3]) {
+    __shared__ uint32_t red[3][4];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+        uint32_t x = 0;
+        for (uint32_t i = bx.begin[s] + threadIdx.x; i < bx.begin[s + 1]; i += blockDim.x) x = max(x, bx.bm[i]);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off));
+        if ((threadIdx.x & 63) == 0) red[s][threadIdx.x >> 6] = x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 3; ++s) w[s] = max(max(red[s][0], red[s][1]), max(red[s][2], red[s][3]));
+}
+__global__ __launch_bounds__(256) void k_residues_f64(const ResSegs q, unsigned* __restrict__ W,
                                                       double scale) {
     uint32_t s = 0;
 #pragma unroll
     for (int k = 1; k < kMaxResSegs; ++k) s += (uint32_t)k < q.nseg && blockIdx.x >= q.blk0[k];
     const ResSeg g = q.seg[s];
+    uint32_t wv[3] = {0u, 0u, 0u};
+    if (q.bx.bm) {                       // words from the maxima; block 0 publishes them
+        bit_words_from_maxima(q.bx, wv);
+        if (blockIdx.x == 0 && threadIdx.x < 3) W[threadIdx.x] = wv[threadIdx.x];
+    }
     int n = 0;
     uint32_t bmax = 0;
 #pragma unroll
     for (int p = 0; p < 2; ++p)
         if (g.wa[p] >= 0) {
-            const uint32_t ba = W[g.wa[p]], bb = W[g.wb[p]];
+            const uint32_t ba = q.bx.bm ? wv[g.wa[p]] : W[g.wa[p]], bb = q.bx.bm ? wv[g.wb[p]] : W[g.wb[p]];
             const int np = crt_nmod(ba, bb, g.lk[p]);
             if (!np) return;                                   // too wide: no CRT product
             n = max(n, np);
@@ -1485,7 +1537,7 @@ __global__ __launch_bounds__(256) void k_residues_f64(const ResSegs q, const uns
     else
         residues_emit<4>(w, nm, o, plane, n);
 }
-hipError_t launch_residues_f64(const ResSegs& q0, const unsigned* W, int precision_bits,
+hipError_t launch_residues_f64(const ResSegs& q0, unsigned* W, int precision_bits,
                                hipStream_t st) {
     ResSegs q = q0;
     if (!q.nseg || q.nseg > (uint32_t)kMaxResSegs) return hipErrorInvalidValue;
@@ -1729,136 +1781,6 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
                   q.R, bi, bj, (int)mod, S, tp1, tp2);
     trace_block(t0, tp1, tp2);
 }
-// ---- 256 x 256 tiles (k_gemm_crt_big). 512 threads = 8 waves (2 x 4), each
-// 128 x 64 of the tile = 8 x 4 MFMA blocks (128 accumulator registers): four
-// times the MACs per staged byte of the 128 x 128 tile. Operands go global ->
-// LDS by global_load_lds (16 B per lane, no VGPR staging) into two stages of
-// 32 KiB (A and B: 256 rows x 64 B, the XOR-swizzled rows of crt_lds, the
-// swizzle applied on the source address since the DMA writes lane-linear);
-// the next stage's DMA stays in flight across the barrier (raw s_barrier and a
-// counted vmcnt: __syncthreads would drain it).
-static constexpr int CB = 256;
-static constexpr uint32_t kCrtBigTileBytes = CB * CB;
-static constexpr int kBigStage = 2 * CB * CROW;
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void glb_void_t;
-// chunk `chunk` (64 k) of the tile's A and B rows into stage St: wave w moves A
-// rows [32w, 32w + 32) and B rows likewise, 16 rows (1 KiB) per instruction;
-// rows past the operands' last rows (amax / bmax: the last valid local row)
-// read that row again (their sums are never stored)
-__device__ __forceinline__ void big_issue(const uint8_t* __restrict__ Ap, const uint8_t* __restrict__ Bp,
-                                          uint32_t kpad, uint32_t amax, uint32_t bmax, uint32_t chunk,
-                                          uint8_t* St) {
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const uint32_t r0 = 32 * w + 16 * h, row = r0 + (lane >> 2);
-        const uint32_t part = (lane & 3) ^ ((row >> 2) & 3);      // LDS part (lane & 3) holds this part
-        const uint64_t ko = (uint64_t)chunk * 64 + 16 * part;
-        __builtin_amdgcn_global_load_lds((glb_void_t*)(Ap + (uint64_t)min(row, amax) * kpad + ko),
-                                         (lds_void_t*)(St + r0 * CROW), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((glb_void_t*)(Bp + (uint64_t)min(row, bmax) * kpad + ko),
-                                         (lds_void_t*)(St + CB * CROW + r0 * CROW), 16, 0, 0);
-    }
-}
-__device__ __forceinline__ void crt_gemm_big_tile(const uint8_t* __restrict__ Ar, const uint8_t* __restrict__ Br,
-                                                  uint32_t astride, uint32_t bstride, uint32_t kpad,
-                                                  uint32_t nblk, uint32_t tile, uint8_t* __restrict__ R,
-                                                  uint32_t bi, uint32_t bj, int mod, uint8_t* S,
-                                                  uint32_t N, uint32_t M, uint64_t& tp1, uint64_t& tp2) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t wr = wave >> 2, wc = wave & 3;
-    const uint8_t* Ap = Ar + ((uint64_t)mod * astride + bi * CB) * kpad;
-    const uint8_t* Bp = Br + ((uint64_t)mod * bstride + bj * CB) * kpad;
-    const uint32_t amax = N - 1 - bi * CB, bmax = M - 1 - bj * CB;   // (the tile holds rows bi * CB < N)
-    const uint32_t kcn = kpad / 64;
-    v4i acc[8][4];
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = v4i{0, 0, 0, 0};
-    const uint32_t frow = lane & 15, fpart = lane >> 4;
-    big_issue(Ap, Bp, kpad, amax, bmax, 0, S);
-    big_issue(Ap, Bp, kpad, amax, bmax, 1, S + kBigStage);            // (kpad >= 256: kcn >= 4)
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");                 // chunk 0 landed (this thread's part)
-    __builtin_amdgcn_s_barrier();                                    // ... and every thread's
-    tp1 = wall_clock64();
-    for (uint32_t c = 0; c < kcn; ++c) {
-        const uint8_t* St = S + (c & 1) * kBigStage;
-        v4i af[8], bf[4];
-#pragma unroll
-        for (int a = 0; a < 8; ++a)
-            af[a] = *reinterpret_cast<const v4i*>(St + crt_lds(wr * 128 + a * 16 + frow, fpart));
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-            bf[b] = *reinterpret_cast<const v4i*>(St + CB * CROW + crt_lds(wc * 64 + b * 16 + frow, fpart));
-#pragma unroll
-        for (int a = 0; a < 8; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");              // this wave's reads of stage c & 1 done
-        __builtin_amdgcn_s_barrier();                                    // every wave's
-        if (c + 2 < kcn) {
-            big_issue(Ap, Bp, kpad, amax, bmax, c + 2, S + (c & 1) * kBigStage);
-            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");             // chunk c + 1 landed
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __builtin_amdgcn_s_barrier();
-    }
-    tp2 = wall_clock64();
-    // residues in MFMA order: word (wave, a, b, lane) holds rows (lane >> 4) * 4 +
-    // reg of block (a, b); a wave store is 256 contiguous bytes (crt_elem_big)
-    const int m = (int)c_crt_mod[mod];
-    const float inv = c_crt_invf[mod];
-    uint32_t* Rt = reinterpret_cast<uint32_t*>(R + ((uint64_t)mod * nblk + tile) * kCrtBigTileBytes) +
-                   wave * 2048 + lane;
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            uint32_t w = 0;
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-                const int av = acc[a][b][reg];                     // |av| <= 2^27
-                const int q = (int)floorf((float)av * inv);
-                int r = av - __mul24(q, m);
-                r += r < 0 ? m : 0;
-                r -= r >= m ? m : 0;
-                w |= (uint32_t)r << (8 * reg);
-            }
-            Rt[(a * 4 + b) * 64] = w;
-        }
-}
-__global__ __launch_bounds__(512) void k_gemm_crt_big(const CrtBatch b) {
-    __shared__ __attribute__((aligned(16))) uint8_t S[2 * kBigStage];
-    const uint64_t t0 = wall_clock64();
-    uint32_t cnt[kMaxCrtJobs], total = 0;
-#pragma unroll
-    for (int j = 0; j < kMaxCrtJobs; ++j) {
-        cnt[j] = 0;
-        if ((uint32_t)j < b.njobs)
-            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk;
-        total += cnt[j];
-    }
-    const uint32_t per = (total + 7) / 8, k = blockIdx.x >> 3;
-    if (k >= per) return;
-    uint32_t u = (blockIdx.x & 7) * per + k;
-    if (u >= total) return;
-    uint32_t j = 0;
-#pragma unroll
-    for (int q = 0; q < kMaxCrtJobs - 1; ++q)
-        if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
-    const CrtJob& q = b.job[j];
-    const uint32_t mod = u / q.nblk, t = u - mod * q.nblk;
-    uint32_t bi, bj;
-    crt_tile_rc(q, t, &bi, &bj);
-    uint64_t tp1 = 0, tp2 = 0;
-    crt_gemm_big_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.nblk, t,
-                      q.R, bi, bj, (int)mod, S, q.N, q.sym ? q.N : q.M, tp1, tp2);
-    trace_block(t0, tp1, tp2);
-}
 // C from its n residues, written as canonical Fr to out[i*ors + j*ocs]: one
 // element per thread in the GEMM's tile order (each block one 256-element
 // stretch of a tile), so a wave reads 64 consecutive residue bytes per modulus
@@ -1868,29 +1790,21 @@ __global__ __launch_bounds__(512) void k_gemm_crt_big(const CrtBatch b) {
 // keeps it exact), accumulated carry-free in 16-bit limbs, one 9-word
 // reduction. SYM: elements j >= i of the upper tiles (the GEMM computed upper
 // and diagonal 128-tiles), each also stored at (j, i).
-template <bool BIG>
 __device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t cblk) {
     const int n = crt_nmod(*q.bits_a, *q.bits_b, q.lk);
     if (!n) return;
     // element e of tile t in the GEMM's MFMA order (wave, a, b, lane, reg)
-    constexpr uint32_t TB = BIG ? kCrtBigTileBytes : kCrtTileBytes, BPT = TB / 256;
+    constexpr uint32_t BPT = kCrtTileBytes / 256;
     const uint32_t tl = cblk / BPT;
     const uint32_t e = (cblk - tl * BPT) * 256 + threadIdx.x;
-    const uint32_t reg = e & 3, ln = (e >> 2) & 63;
-    uint32_t bi, bj, i, j;
+    const uint32_t reg = e & 3, ln = (e >> 2) & 63, ab = (e >> 8) & 15, w = e >> 12;
+    uint32_t bi, bj;
     crt_tile_rc(q, tl, &bi, &bj);
-    if (BIG) {                                   // 8 waves (2 x 4) of 8 x 4 blocks
-        const uint32_t ab = (e >> 8) & 31, w = e >> 13;
-        i = bi * CB + (w >> 2) * 128 + (ab >> 2) * 16 + (ln >> 4) * 4 + reg;
-        j = bj * CB + (w & 3) * 64 + (ab & 3) * 16 + (ln & 15);
-    } else {                                     // 4 waves (2 x 2) of 4 x 4 blocks
-        const uint32_t ab = (e >> 8) & 15, w = e >> 12;
-        i = bi * CT + (w >> 1) * 64 + (ab >> 2) * 16 + (ln >> 4) * 4 + reg;
-        j = bj * CT + (w & 1) * 64 + (ab & 3) * 16 + (ln & 15);
-    }
+    const uint32_t i = bi * CT + (w >> 1) * 64 + (ab >> 2) * 16 + (ln >> 4) * 4 + reg;
+    const uint32_t j = bj * CT + (w & 1) * 64 + (ab & 3) * 16 + (ln & 15);
     if (i >= q.N || j >= q.M || (q.sym && j < i)) return;
-    const uint64_t plane = (uint64_t)q.nblk * TB;
-    const uint8_t* __restrict__ rp = q.R + (uint64_t)tl * TB + e;
+    const uint64_t plane = (uint64_t)q.nblk * kCrtTileBytes;
+    const uint8_t* __restrict__ rp = q.R + (uint64_t)tl * kCrtTileBytes + e;
     uint32_t r[kCrtMaxMod];
 #pragma unroll
     for (int k = 0; k < kCrtMaxMod; ++k) r[k] = k < n ? rp[k * plane] : 0u;
@@ -1931,32 +1845,29 @@ __device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t cblk)
 // XCD-contiguously: XCD x takes a contiguous run of the row-major tile
 // sequence, so the halves of a 128-byte residue line that neighbouring tiles
 // read come through the same L2.
-template <bool BIG>
 __global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b, uint32_t cblocks) {
     const uint32_t per = (cblocks + 7) / 8, t = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
     if (t >= cblocks) return;
     uint32_t j = 0;
     for (uint32_t k = 1; k < b.njobs; ++k) j += t >= b.job[k].cblk0;
-    crt_combine_elem<BIG>(b.job[j], t - b.job[j].cblk0);
+    crt_combine_elem(b.job[j], t - b.job[j].cblk0);
 }
 
 size_t crt_scratch_bytes(uint32_t N, uint32_t M) {
-    // the residue scratch R of either tile shape: kCrtMaxMod planes of whole tiles
-    const uint64_t a = ((uint64_t)N + CB - 1) / CB * CB, m = ((uint64_t)M + CB - 1) / CB * CB;
+    // kCrtMaxMod planes of whole 128 x 128 tiles
+    const uint64_t a = ((uint64_t)N + CT - 1) / CT * CT, m = ((uint64_t)M + CT - 1) / CT * CT;
     return (size_t)(kCrtMaxMod * a * m);
 }
-hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st, bool big) {
+hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
     CrtBatch b = b0;
     if (b.njobs < 1 || b.njobs > (uint32_t)kMaxCrtJobs) return hipErrorInvalidValue;
     uint32_t units = 0, cblocks = 0;
-    const uint32_t T = big ? CB : CT;
     for (uint32_t j = 0; j < b.njobs; ++j) {
         CrtJob& q = b.job[j];
-        q.tiles_a = (q.N + T - 1) / T;
-        q.tiles_m = q.sym ? q.tiles_a : (q.M + T - 1) / T;
-        // every staged row (tiles x CT) lies inside its operand's planes (the big
-        // tiles clamp their row reads to the planes instead)
-        if (q.kpad % 256 || (!big && (q.astride < q.tiles_a * CT || (!q.sym && q.bstride < q.tiles_m * CT))))
+        q.tiles_a = (q.N + CT - 1) / CT;
+        q.tiles_m = q.sym ? q.tiles_a : (q.M + CT - 1) / CT;
+        // every staged row (tiles x CT) lies inside its operand's planes
+        if (q.kpad % 256 || q.astride < q.tiles_a * CT || (!q.sym && q.bstride < q.tiles_m * CT))
             return hipErrorInvalidValue;
         if (q.sym && q.N != q.M) return hipErrorInvalidValue;
         q.nblk = q.sym ? q.tiles_a * (q.tiles_a + 1) / 2 : q.tiles_a * q.tiles_m;
@@ -1968,25 +1879,19 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st, bool big) {
         }
         units += kCrtMaxMod * q.nblk;                    // upper bound: n = kCrtMaxMod
         q.cblk0 = cblocks;
-        cblocks += q.nblk * ((big ? kCrtBigTileBytes : kCrtTileBytes) / 256);
+        cblocks += q.nblk * (kCrtTileBytes / 256);
     }
-    if (big)
-        hipLaunchKernelGGL(k_gemm_crt_big, dim3((units + 7) / 8 * 8), dim3(512), 0, st, b);
-    else
-        hipLaunchKernelGGL(k_gemm_crt_multi, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
+    hipLaunchKernelGGL(k_gemm_crt_multi, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (big)
-        hipLaunchKernelGGL(k_crt_combine_multi<true>, dim3((cblocks + 7) / 8 * 8), dim3(256), 0, st, b, cblocks);
-    else
-        hipLaunchKernelGGL(k_crt_combine_multi<false>, dim3((cblocks + 7) / 8 * 8), dim3(256), 0, st, b, cblocks);
+    hipLaunchKernelGGL(k_crt_combine_multi, dim3((cblocks + 7) / 8 * 8), dim3(256), 0, st, b, cblocks);
     return hipGetLastError();
 }
 
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st, bool big) {
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st) {
     if (sym && (N != M || astride != bstride)) return hipErrorInvalidValue;
     CrtBatch b;
     memset(&b, 0, sizeof b);
@@ -2007,7 +1912,7 @@ hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint3
     q.M = M;
     q.lk = lk;
     q.sym = sym;
-    return launch_gemm_crt_multi(b, st, big);
+    return launch_gemm_crt_multi(b, st);
 }
 
 // -------------------------------------------------------- Montgomery GEMM

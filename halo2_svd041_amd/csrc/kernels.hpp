@@ -109,9 +109,17 @@ struct QuantSegs {
     BitFold fold;                        // fold.wout null: no in-launch fold
 };
 hipError_t launch_quantize_multi(const QuantSegs& q, int precision_bits, hipStream_t st);
-// k_bits_f64: only the bit-length words of q's segments (blockmax / fold as
-// k_quantize_multi would write them), read-only from the f64 inputs
-hipError_t launch_bits_f64(const QuantSegs& q, int precision_bits, hipStream_t st);
+// Per-block bit-length maxima of up to three f64 matrices (k_bits_f64, read-only,
+// no in-launch fold): matrix s's values go in blocks [begin[s], begin[s+1]) of
+// vpb values each; the consumer (k_residues_f64) reduces a matrix's range.
+struct BitMax {
+    const unsigned* bm;       // null: the bit-length words are final already
+    uint32_t begin[4];
+};
+// k_bits_f64 over the first nseg segments of q (their inputs and lengths):
+// fills *bx (bm = maxima, ~512 blocks in all)
+hipError_t launch_bits_f64(const QuantSegs& q, uint32_t nseg, int precision_bits, unsigned* maxima,
+                           BitMax* bx, hipStream_t st);
 // Witness checker (svdw_check_gates). A region is `nunits` repetitions of a
 // `unit`-cell block (element u = row u / cols, column u % cols); check words:
 //   CHK_GATE g      a + b*c = d on cells g..g+3
@@ -302,8 +310,11 @@ struct ResSegs {
     ResSeg seg[kMaxResSegs];
     uint32_t blk0[kMaxResSegs + 1];   // set by the launcher
     uint32_t nseg;
+    // bx.bm set: every block reduces the words it needs from k_bits_f64's
+    // maxima, and block 0 writes all three to W (for the GEMM, combine, scans)
+    BitMax bx;
 };
-hipError_t launch_residues_f64(const ResSegs& q, const unsigned* W, int precision_bits,
+hipError_t launch_residues_f64(const ResSegs& q, unsigned* W, int precision_bits,
                                hipStream_t st);
 // c_s = A * Bt from residue planes Ar (plane stride astride rows, from the A rows'
 // first row) and Br (bstride): N x M; R is the residue scratch
@@ -311,7 +322,7 @@ hipError_t launch_residues_f64(const ResSegs& q, const unsigned* W, int precisio
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st, bool big);
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st);
 // Debug: record the CRT GEMM's block timeline into buf (3 u64 per block; null: off).
 hipError_t set_debug_trace(void* buf);
 static constexpr int kCrtMaxResidues = 40;   // = kCrtMaxMod (crt_tables.hpp)
@@ -342,10 +353,9 @@ struct CrtBatch {
     CrtJob job[kMaxCrtJobs];
     uint32_t njobs;
 };
-// big: 256 x 256 output tiles (k_gemm_crt_big: 8 waves, operands by
-// global_load_lds), else 128 x 128 (k_gemm_crt_multi); R sized crt_scratch_bytes
-hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st, bool big);
-// residue scratch R one CRT product of N x M needs (either tile shape)
+// R sized crt_scratch_bytes per job
+hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st);
+// residue scratch R one CRT product of N x M needs
 size_t crt_scratch_bytes(uint32_t N, uint32_t M);
 // w (len L) from a view (row 0 / col j of a 1 x L view) -> canonical copy
 // (w_canon nullable) and its scaled table (ScaleTab f: see kTabSlots).
