@@ -514,7 +514,6 @@ struct svdw_ctx {
     bool f64_views = true;                  // "f64_views"
     bool q_aside = true;                    // "q_aside": quantize beside the product chain (quantize_aside)
     BitMax bx_pend{};                       // its maxima, reduced by the next residue launch
-    bool bounds_wait = false;               // "bounds_wait" (A/B): the u / v bounds wait for the products
     std::vector<F64Src> f64src;
     DBuf colpart;
     DBuf qfold;                             // k_quantize_multi's fold counters + group maxima
@@ -2480,8 +2479,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         std::swap(c->st, c->st2);
         // the cell stream waits for u.d (and what precedes it on st2), not for
         // the d checks' dependent second group batched behind it
-        flush_batch(c, c->st2, c->st,
-                    c->bounds_wait && !c->gemm_done.empty() ? c->gemm_done.back() : nullptr);
+        flush_batch(c, c->st2, c->st);
     }
     if (batched) {
         host_mark(c, "bounds(u), bounds(v), u.d queued");
@@ -4204,8 +4202,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_crt = (int)value;
         } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
             c->stage_batch = value != 0;
-        } else if (n == "bounds_wait") {
-            c->bounds_wait = value != 0;
         } else if (n == "q_aside") {
             c->q_aside = value != 0;
         } else if (n == "f64_views") {
