@@ -404,6 +404,22 @@ struct svdw_ctx {
     hipStream_t st = nullptr;
     uint32_t P = 32, LB = 19;
     Stream ph[2];
+    // Pipelined svd_witness ("pipeline", svd_witness_pipe): consecutive
+    // witnesses alternate between two sets of cell streams (ph and alt), so call
+    // j's product chain (st) runs beside call j - 1's HBM-bound stages (st2) and
+    // row scans (st3) instead of after them. Call j's st first waits for call
+    // j - 2's tail (tail_ev[parity]: its last work on st2 / st3), the last user
+    // of this cell set and of this half of the bit-length words. Anything else
+    // that touches the streams after a pipelined call settles first (settle).
+    Stream alt[2];
+    int pipeline = 1;                       // "pipeline": 1 on, 0 off
+    bool in_pipe = false;                   // inside a pipelined svd_witness
+    int pipe_par = 0;                       // this call's parity (cell set, bit words)
+    hipEvent_t tail_ev[2][2] = {};          // [parity][st2, st3]
+    bool tail_valid[2] = {false, false};
+    bool tail_pending = false;              // the last pipelined call's tail not yet joined into st
+    int tail_last = 0;
+    size_t mem_total = 0;                   // device memory (hipMemGetInfo at create)
     DBuf f64in, digA, digB, digC, w1c, w1t, w2c, w2t, bits, gpc, gtab, crtR, gbits, chk, chkg;
     DBuf wbc[kMaxScanJobs], wbt[kMaxScanJobs];   // b.v per batched verify_mul (canonical, table)
     // gamma^j (canonical gpc, scaled table gtab, kernels.hpp kTabSlots) of the
@@ -512,8 +528,6 @@ struct svdw_ctx {
     struct F64Region { uint32_t phase; uint64_t off, n; const double* x; };
     std::vector<F64Region> f64reg;
     bool f64_views = true;                  // "f64_views"
-    bool q_aside = true;                    // "q_aside": quantize beside the product chain (quantize_aside)
-    BitMax bx_pend{};                       // its maxima, reduced by the next residue launch
     std::vector<F64Src> f64src;
     DBuf colpart;
     DBuf qfold;                             // k_quantize_multi's fold counters + group maxima
@@ -617,6 +631,15 @@ static void sync(svdw_ctx* c) {
     hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
     hipck(hipStreamSynchronize(c->st2), "hipStreamSynchronize");
     if (c->st3) hipck(hipStreamSynchronize(c->st3), "hipStreamSynchronize");
+    c->tail_pending = false;
+}
+// After a pipelined svd_witness its tail (st2, st3) is not joined into st:
+// anything else queued on the context waits for it first.
+static void settle(svdw_ctx* c) {
+    if (c->dry || !c->tail_pending || c->in_pipe) return;
+    for (int k = 0; k < 2; ++k)
+        hipck(hipStreamWaitEvent(c->st, c->tail_ev[c->tail_last][k], 0), "hipStreamWaitEvent");
+    c->tail_pending = false;
 }
 // Dependency recorded on `from`; `to` waits for it (cross-stream dependency).
 // The returned handle is waited on later with dep_wait. (Round 4 measured the
@@ -809,29 +832,6 @@ static void bits_words(svdw_ctx* c, QuantSegs& qs, uint32_t nred, const BitSegs&
     for (uint32_t s = 0; s <= nred; ++s) f.b[s] = qs.blk0[s];
     *folded = true;
 }
-// Quantization off the product chain: when every in-witness reader of the
-// loaded cells goes through an f64 view (f64_views) and the products' residue
-// planes come from the f64 inputs on the cell stream, the GEMM needs only the
-// operand bit-length words. k_bits_f64 writes per-block maxima of m, u, v on st
-// (read-only, 8 B per value, no fold), the residue launch reduces them
-// (c->bx_pend; ev_bits is recorded behind it), and k_quantize_multi writes the
-// cells on `aside` beside the chain. The caller joins `aside` into st.
-static void quantize_aside(svdw_ctx* c, const QuantSegs& qs, uint32_t nbit_segs, hipStream_t aside) {
-    double nb = 0, nq = 0;
-    for (uint32_t k = 0; k < qs.nseg; ++k) {
-        nq += (double)qs.n[k];
-        if (k < nbit_segs) nb += (double)qs.n[k];
-    }
-    {
-        ProfScope ps(c, c->st, "k_bits_f64", 8.0 * nb, 0);
-        hipck(launch_bits_f64(qs, nbit_segs, (int)c->P, qs.blockmax[0], &c->bx_pend, c->st), "k_bits_f64");
-    }
-    QuantSegs qq = qs;
-    for (uint32_t k = 0; k < (uint32_t)kMaxQuantSegs; ++k) qq.blockmax[k] = nullptr;
-    memset(&qq.fold, 0, sizeof qq.fold);
-    ProfScope ps(c, aside, "k_quantize", 40.0 * nq, 0);
-    hipck(launch_quantize_multi(qq, (int)c->P, aside), "k_quantize_multi");
-}
 static void grow(svdw_ctx* c, Fr*& ptr, uint64_t used, uint64_t& cap, uint64_t need) {
     if (c->dry || need <= cap) return;
     REQUIRE(!c->capturing, "internal: allocation during graph capture");
@@ -856,6 +856,7 @@ static void grow(svdw_ctx* c, Fr*& ptr, uint64_t used, uint64_t& cap, uint64_t n
 static void append(svdw_ctx* c, uint32_t phase, uint64_t n, uint64_t nl, uint64_t* off,
                    uint64_t* loff, const char* tag, uint64_t rows = 1) {
     REQUIRE(phase < 2, "phase must be 0 or 1");
+    settle(c);
     Stream& s = c->ph[phase];
     c->phys.valid = false;
     grow(c, s.adv, s.n, s.cap, s.n + n);
@@ -1486,6 +1487,7 @@ static bool is_transpose_of(const svdw_mat& b, const svdw_mat& a) {
 static std::vector<uint32_t> maxbits_many(svdw_ctx* c, const std::vector<svdw_mat>& ms) {
     std::vector<uint32_t> out(ms.size(), 0);
     if (c->dry || ms.empty()) return out;
+    settle(c);                                  // a pipelined witness's row scans read c->bits
     const size_t words = ms.size() * kMaxBitBlocks;
     ensure_buf(c, c->bits, words * sizeof(unsigned));
     std::vector<uint32_t> nb(ms.size());
@@ -2210,17 +2212,10 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
     if (rows_m) seg(c->svd_f64[0] + rr0[0] * M, rows_m, M, rp_m, kpM, c->digA, {{0, 2, (int)lkM}});
     seg(c->svd_f64[2], M, M, rp_v, kpM, c->digB, {{0, 2, (int)lkM}, {2, 2, (int)lkM}});
     seg(c->svd_f64[1], N, N, rp_u, kpN, c->digC, {{1, 1, (int)lkN}});
-    q.bx = c->bx_pend;                    // (quantize_aside: the words come from its maxima)
-    REQUIRE(!q.bx.bm || pst == c->st, "internal: bit maxima reduced off the cell stream");
     {
         ProfScope ps(c, pst, "k_residues_f64",
                      8.0 * ((double)rows_m * M + (double)M * M + (double)N * N), 0);
         hipck(launch_residues_f64(q, W, (int)c->P, pst), "k_residues_f64");
-    }
-    if (q.bx.bm) {                        // the words are final here
-        flush_batch(c, pst);
-        hipck(hipEventRecord(c->ev_bits, pst), "hipEventRecord");
-        memset(&c->bx_pend, 0, sizeof c->bx_pend);
     }
     // the stages beside the products wait for the residue planes, which then
     // run alone instead of beside the first (HBM-saturating) stages (same box:
@@ -2491,7 +2486,12 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         fetch_bits(c);
         bm = known_bits[0]; bu = known_bits[1]; bv = known_bits[2];
     }
-    // products batched (one completion point): diff and the two ids in one launch
+    // products batched (one completion point): diff and the two ids in one launch;
+    // pipelined (c->in_pipe), on st2 behind the bounds, so that st is free for
+    // the next call's product chain (honest_prover_mat_mul's wait for the
+    // products lands on st2)
+    const bool dst2 = c->in_pipe && pc;
+    if (dst2) std::swap(c->st, c->st2);
     BatchScope bs2(c);
     if (!c->gemm_batched) bs2.close();
     svdw_mat mvt = honest_prover_mat_mul(c, m.phase, m, vt, bm, bv);
@@ -2507,6 +2507,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     svdw_mat vvt = honest_prover_mat_mul(c, m.phase, v, vt, bv, bv);
     check_mat_id(c, vvt, q2, eu, &qq);
     bs2.end();
+    if (dst2) std::swap(c->st, c->st2);
     aside.end();
     host_mark(c, "ids queued");
     return svdw_svd_payload{ut, vt, mvt, uut, vvt};
@@ -2536,7 +2537,6 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     host_mark(c, "svd_witness start");
     clear_streams(c);
     c->dep_next = 0;
-    after_previous(c);
     if (!c->dry) apply_gemm_prio(c, N, M);
     c->prelaunched = false;
     c->prod_on_cell = false;
@@ -2544,6 +2544,21 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     c->gemm_done.clear();
     c->wait_before_cs.clear();
     c->pre.clear();
+    c->in_pipe = false;
+    struct PipeGuard {                     // an exception inside a pipelined call: its
+        svdw_ctx* c;                       // tail is whatever reached st2 / st3 -- join it
+        ~PipeGuard() {
+            if (!c->in_pipe) return;
+            const int par = c->pipe_par;
+            (void)hipEventRecord(c->tail_ev[par][0], c->st2);
+            (void)hipEventRecord(c->tail_ev[par][1], c->st3);
+            c->tail_valid[par] = true;
+            c->tail_pending = true;
+            c->tail_last = par;
+            c->pipe_par ^= 1;
+            c->in_pipe = false;
+        }
+    } pguard{c};
     if (!c->dry) {
         // exact sizes from the dry planner: no growth copies inside the step
         const std::vector<uint64_t> key = {N, M, cfg.max_bits_d, f64_key(cfg.max_norm),
@@ -2555,6 +2570,27 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
             svd_witness(&plan, nullptr, nullptr, nullptr, nullptr, N, M, false, cfg, gamma);
             c->plan_key = key;
             c->plan_val = {plan.ph[0].n, plan.ph[0].nl, plan.ph[1].n, plan.ph[1].nl};
+        }
+        // Pipelined (svd_witness_pipe): device inputs on the f64 product path
+        // with the products on the cell stream, and two cell sets that fit in
+        // at most 60 % of the device memory (1024^2 P=63: 2 x 9.3 GB; 4096^2
+        // P=63, 2 x 148 GB, runs unpipelined)
+        const double wbytes = 32.0 * (double)(c->plan_val[0] + c->plan_val[1] + c->plan_val[2] + c->plan_val[3]);
+        c->in_pipe = c->pipeline && on_device && c->overlap && c->res_f64 && c->gemm_crt &&
+                     c->gemm_impl == SVDW_GEMM_MFMA && N <= 8192 && M <= 8192 &&
+                     (c->prod_cell > 0 || (c->prod_cell < 0 && sharded(c))) &&
+                     2.0 * wbytes <= 0.6 * (double)c->mem_total;
+        if (c->in_pipe) {
+            // the other cell set (last written by call j - 2): st waits for that
+            // call's tail, the last reader of these cells and bit words
+            for (int p = 0; p < 2; ++p) std::swap(c->ph[p], c->alt[p]);
+            clear_streams(c);
+            if (c->tail_valid[c->pipe_par])
+                for (int k = 0; k < 2; ++k)
+                    hipck(hipStreamWaitEvent(c->st, c->tail_ev[c->pipe_par][k], 0), "hipStreamWaitEvent");
+        } else {
+            settle(c);
+            after_previous(c);
         }
         for (int p = 0; p < 2; ++p) {
             grow(c, c->ph[p].adv, 0, c->ph[p].cap, c->plan_val[2 * p]);
@@ -2603,8 +2639,10 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     const uint32_t nbv = (uint32_t)(((uint64_t)M * M + kQuantPerBlock - 1) / kQuantPerBlock);
     if (!c->dry) {
         // [0, 3): bit-length maxima of m, u, v; from word 64: per-block maxima
-        ensure_buf(c, c->bits, (64 + nbm + nbu + nbv) * sizeof(unsigned));
-        dbits = (unsigned*)c->bits.p;
+        // (pipelined: a half per parity, call j - 1's row scans still read theirs)
+        const size_t words = (64 + nbm + nbu + nbv + 63) / 64 * 64;
+        ensure_buf(c, c->bits, 2 * words * sizeof(unsigned));
+        dbits = (unsigned*)c->bits.p + (c->in_pipe ? c->pipe_par * words : 0);
     }
     QuantSegs qs;
     memset(&qs, 0, sizeof qs);
@@ -2626,17 +2664,11 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     seg.begin[3] = nbm + nbu + nbv;
     bool folded = false;
     bits_words(c, qs, 3, seg, dbits, &folded);
-    // the cells beside the product chain on st2 (its stages wait for the
-    // residue planes anyway) when no launch of the witness reads them
-    // (the products on the cell stream: their residue launch, on st behind
-    // k_bits_f64, reduces its maxima into the words)
-    const bool q_aside = c->q_aside && folded && qs.nseg == 4 && on_device && !c->dry && c->f64_views && c->overlap &&
-                         c->res_f64 && c->gemm_crt && c->gemm_impl == SVDW_GEMM_MFMA && N <= 8192 && M <= 8192 &&
-                         (c->prod_cell > 0 || (c->prod_cell < 0 && sharded(c)));
-    memset(&c->bx_pend, 0, sizeof c->bx_pend);
-    if (q_aside) {
-        quantize_aside(c, qs, 3, c->st2);
-    } else if (qs.nseg) {
+    // (Round 4 measured the quantization beside the product chain instead: the
+    // bit-length words from a read-only k_bits_f64 on st, the cells on st2; it
+    // was 0.7-4 % slower at 1024^2, 512^2 and on 8-way ranks -- the words'
+    // cross-block reduction costs what the cells' stores did -- and was removed.)
+    if (qs.nseg) {
         ProfScope ps(c, c->st, "k_quantize", 40.0 * ((double)N * M + (double)N * N + (double)M * M + r), 0);
         hipck(launch_quantize_multi(qs, (int)c->P, c->st), "k_quantize_multi");
     }
@@ -2646,9 +2678,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     if (!c->dry) {   // operand bit lengths (GEMM digit counts): read lazily, see fetch_bits
         if (!folded) hipck(launch_bits_reduce(dbits + 64, seg, 3, dbits, c->st), "k_bits_reduce");
         flush_batch(c, c->st);
-        // (q_aside: the words exist once the residue launch has reduced them;
-        // prelaunch_products_f64 records ev_bits behind it)
-        if (!q_aside) hipck(hipEventRecord(c->ev_bits, c->st), "hipEventRecord");
+        hipck(hipEventRecord(c->ev_bits, c->st), "hipEventRecord");
         c->bits_pending = true;
         c->qmat[0] = zm; c->qmat[1] = zu; c->qmat[2] = zv;
         // the same words for the device-side choices (row-scan operand widths)
@@ -2671,7 +2701,8 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     // 0.454 ms, 768^2 P=63 1.328 -> 1.272 ms); from 1024 on it is neutral to
     // 1 % slower.
     const bool p1_small = std::max(N, M) < 1024;
-    const int p1mode = c->phase1_overlap == 1 && (sharded(c) || p1_small) ? 2 : c->phase1_overlap;
+    // (pipelined: st2 carries the diff and ids after the bounds, phase 1 goes to st3)
+    const int p1mode = c->phase1_overlap == 1 && (sharded(c) || p1_small || c->in_pipe) ? 2 : c->phase1_overlap;
     bool p1_queued = false;
     auto queue_phase1 = [&](const svdw_svd_payload& pl, bool overlap) {
         const bool p1_overlap = p1mode && overlap;
@@ -2717,16 +2748,31 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     svdw_svd_payload pl =
         check_svd_phase0(c, zm, zu, zv, zd, es, eu, cfg.max_bits_d, c->qbits, dbits, true);
     c->early_p1 = nullptr;
-    REQUIRE(!c->bx_pend.bm, "internal: k_bits_f64's maxima were never reduced (no f64 product launch)");
     const bool p1_overlap = p1mode && c->prelaunched && !c->dry;
     hipStream_t p1s = p1mode == 2 ? c->st3 : c->st2;
     host_mark(c, "phase 0 queued");
     if (!p1_queued) queue_phase1(pl, p1_overlap);
     host_mark(c, "phase 1 queued");
+    if (c->in_pipe) {
+        // no join into st: the next call's product chain starts on st while this
+        // call's stages (st2) and row scans (st3) finish; they end at tail_ev
+        const int par = c->pipe_par;
+        flush_batch(c, c->st2);
+        flush_batch(c, c->st3);
+        hipck(hipEventRecord(c->tail_ev[par][0], c->st2), "hipEventRecord");
+        hipck(hipEventRecord(c->tail_ev[par][1], c->st3), "hipEventRecord");
+        c->tail_valid[par] = true;
+        c->tail_pending = true;
+        c->tail_last = par;
+        c->pipe_par ^= 1;
+        c->in_pipe = false;
+        host_mark(c, "svd_witness end (pipelined)");
+        return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
+    }
     if (p1_overlap) stream_dep(c, p1s, c->st);
-    // st2 also carries the quantized cells and the d checks and single cells
-    // queued aside (and, with phase 1 on st3, nothing else joins it): join it too
-    if ((c->prelaunched || q_aside) && !c->dry && !(p1_overlap && p1s == c->st2)) stream_dep(c, c->st2, c->st);
+    // st2 also carries the d checks and single cells queued aside (and, with
+    // phase 1 on st3, nothing else joins it): join it too
+    if (c->prelaunched && !c->dry && !(p1_overlap && p1s == c->st2)) stream_dep(c, c->st2, c->st);
     host_mark(c, "svd_witness end");
     return svdw_counts{c->ph[0].n, c->ph[1].n, c->ph[0].nl, c->ph[1].nl};
 }
@@ -2757,6 +2803,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     host_mark(c, "verify_mul_witness start");
     clear_streams(c);
     c->dep_next = 0;
+    settle(c);
     after_previous(c);
     c->prelaunched = false;
     c->prod_on_cell = false;
@@ -2979,6 +3026,7 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
     // on st, ahead of everything the call queues. (Round 4 tried them on st3
     // beside the graph, the graph's scans waiting through an external event
     // node (hipEventWaitExternal): the runtime aborted in the capture/replay.)
+    settle(c);
     PowCells pc;
     const bool pw = vm_pow_cells(c, M, gamma, &pc);
     gamma_prep(c, M, gamma, c->st, pw ? &pc : nullptr);
@@ -3213,6 +3261,10 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
             if (e == hipSuccess) e = hipHostMalloc((void**)&c->hbits, 64 * sizeof(uint32_t),
                                                hipHostMallocDefault);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bits, hipEventDisableTiming | hipEventReleaseToDevice);
+            for (int k = 0; k < 4 && e == hipSuccess; ++k)
+                e = hipEventCreateWithFlags(&c->tail_ev[k / 2][k % 2], hipEventDisableTiming | hipEventReleaseToDevice);
+            size_t mfree = 0;
+            if (e == hipSuccess) e = hipMemGetInfo(&mfree, &c->mem_total);
             if (e != hipSuccess) {
                 delete c;
                 fail(SVDW_EDEVICE, std::string("HIP device init failed: ") + hipGetErrorString(e));
@@ -3230,6 +3282,10 @@ int svdw_ctx_destroy(svdw_ctx* c) {
             if (c->st3) (void)hipStreamSynchronize(c->st3);
             vmg_drop(c);
             for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
+            for (auto& s : c->alt) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
+            for (auto& t : c->tail_ev)
+                for (auto e : t)
+                    if (e) (void)hipEventDestroy(e);
             for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1], &c->w1c, &c->w1t, &c->w2c, &c->w2t,
                             &c->bits, &c->gpc, &c->gtab, &c->crtR, &c->gbits, &c->colpart, &c->qfold})
                 if (b->p) (void)hipFree(b->p);
@@ -3325,6 +3381,7 @@ static int copy_cells(svdw_ctx* c, uint32_t phase, uint64_t off, uint64_t n, uin
         const Stream& s = c->ph[phase];
         REQUIRE(off + n <= (lk ? s.nl : s.n), "copy range outside the stream");
         if (!n) return;
+        settle(c);
         hipck(hipMemcpyAsync(out, (lk ? s.lk : s.adv) + off, n * sizeof(Fr), hipMemcpyDeviceToHost,
                              c->st), "D2H");
         sync(c);
@@ -4043,6 +4100,7 @@ int svdw_check_physical(svdw_ctx* c, uint32_t phase, const void* advice, const u
         REQUIRE(!c->dry, "svdw_check_physical needs a device context");
         REQUIRE(c->phys.valid, "svdw_check_physical: call svdw_physical_layout first");
         memset(out, 0, sizeof *out);
+        settle(c);
         ensure_buf(c, c->chk, 6 * sizeof(unsigned long long));
         unsigned long long* cnt = (unsigned long long*)c->chk.p;
         hipck(hipMemsetAsync(cnt, 0, 6 * sizeof(unsigned long long), c->st), "hipMemsetAsync");
@@ -4169,7 +4227,10 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         sync(c);
         ++c->epoch;                                  // a captured launch sequence may change
         const std::string n(name);
-        if (n == "graph") {                   // captured verify_mul_witness (vm_graph)
+        if (n == "pipeline") {                       // pipelined svd_witness (svd_witness)
+            REQUIRE(value == 0 || value == 1, "pipeline: 0 or 1");
+            c->pipeline = (int)value;
+        } else if (n == "graph") {                   // captured verify_mul_witness (vm_graph)
             REQUIRE(value == 0 || value == 1, "graph: 0 or 1");
             c->graph_vm = (int)value;
         } else if (n == "gemm_impl") {
@@ -4202,8 +4263,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gemm_crt = (int)value;
         } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
             c->stage_batch = value != 0;
-        } else if (n == "q_aside") {
-            c->q_aside = value != 0;
         } else if (n == "f64_views") {
             c->f64_views = value != 0;
         } else if (n == "p1_at") {

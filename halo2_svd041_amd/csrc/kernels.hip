@@ -222,66 +222,6 @@ __global__ __launch_bounds__(256) void k_quantize_multi(const QuantSegs q, doubl
         }
     quantize_body(in, n, out, scale, bm, blockIdx.x - b0, keep, q.fold, blockIdx.x);
 }
-// The operand bit-length maxima alone, read-only from the f64 inputs: block b of
-// matrix s covers vpb values of it (kQuantPerBlock per round), writes one
-// maximum, no cross-block fold (same-address atomics of ~800 blocks serialised
-// to ~20 us at 1024^2, measured); k_residues_f64 reduces the ranges it needs.
-struct BitArgs {
-    const double* in[3];
-    uint64_t n[3];
-    uint32_t begin[4];
-    uint32_t vpb;
-    unsigned* bm;
-};
-__global__ __launch_bounds__(256) void k_bits_f64(const BitArgs a, double scale) {
-    constexpr int PT = kQuantPerBlock / 256;
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 1; k < 3; ++k) s += blockIdx.x >= a.begin[k];
-    const double* in = s == 0 ? a.in[0] : s == 1 ? a.in[1] : a.in[2];
-    const uint64_t n = s == 0 ? a.n[0] : s == 1 ? a.n[1] : a.n[2];
-    const uint64_t v0 = (uint64_t)(blockIdx.x - a.begin[s]) * a.vpb;
-    uint32_t bmax = 0;
-    for (uint32_t r = 0; r < a.vpb; r += kQuantPerBlock) {
-        double xv[PT];
-#pragma unroll
-        for (int k = 0; k < PT; ++k) {
-            const uint64_t i = v0 + r + threadIdx.x + 256ull * k;
-            xv[k] = i < n ? __builtin_nontemporal_load(in + i) : 0.0;
-        }
-        bmax = max(bmax, block_bits<PT>(xv, scale));
-        __syncthreads();                                // (block_bits' LDS reused next round)
-    }
-    if (threadIdx.x == 0) a.bm[blockIdx.x] = bmax;
-}
-hipError_t launch_bits_f64(const QuantSegs& q, uint32_t nseg, int p, unsigned* maxima, BitMax* bx,
-                           hipStream_t st) {
-    if (nseg < 1 || nseg > 3 || nseg > q.nseg) return hipErrorInvalidValue;
-    BitArgs a;
-    memset(&a, 0, sizeof a);
-    uint64_t tot = 0;
-    for (uint32_t k = 0; k < nseg; ++k) tot += q.n[k];
-    // ~512 blocks whatever the size (so the consumers' reductions stay short)
-    const uint64_t want = (tot + 511) / 512;
-    const uint64_t vpb = (want + kQuantPerBlock - 1) / kQuantPerBlock * kQuantPerBlock;
-    a.vpb = (uint32_t)(vpb > kQuantPerBlock ? vpb : kQuantPerBlock);
-    uint32_t blocks = 0;
-    for (uint32_t k = 0; k < 3; ++k) {
-        a.begin[k] = blocks;
-        if (k < nseg) {
-            a.in[k] = q.in[k];
-            a.n[k] = q.n[k];
-            blocks += (uint32_t)((q.n[k] + a.vpb - 1) / a.vpb);
-        }
-    }
-    a.begin[3] = blocks;
-    a.bm = maxima;
-    bx->bm = maxima;
-    for (int k = 0; k < 4; ++k) bx->begin[k] = a.begin[k];
-    if (!blocks) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_bits_f64, dim3(blocks), dim3(256), 0, st, a, (double)(1ull << p));
-    return hipGetLastError();
-}
 hipError_t launch_quantize_multi(const QuantSegs& q, int p, hipStream_t st) {
     if (!q.nseg || q.nseg > (uint32_t)kMaxQuantSegs || !q.blk0[q.nseg]) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_quantize_multi, dim3(q.blk0[q.nseg]), dim3(256), 0, st, q,
@@ -1477,39 +1417,18 @@ __device__ __forceinline__ void quantized_words(double x, double scale, uint32_t
 // Residue planes straight from the f64 inputs of svd_witness (what k_to_residues
 // computes from the quantized cells, without reading the 32 B cells back): up to
 // kMaxResSegs matrices in one launch, segment s covering blocks [blk0[s], blk0[s+1]).
-// Bit-length words 0..2 from k_bits_f64's per-block maxima (BitMax): one
-// block-wide max per range, every lane of the block holding the results.
-__device__ __forceinline__ void bit_words_from_maxima(const BitMax& bx, uint32_t (&w)[3]) {
-    __shared__ uint32_t red[3][4];
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-        uint32_t x = 0;
-        for (uint32_t i = bx.begin[s] + threadIdx.x; i < bx.begin[s + 1]; i += blockDim.x) x = max(x, bx.bm[i]);
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off));
-        if ((threadIdx.x & 63) == 0) red[s][threadIdx.x >> 6] = x;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int s = 0; s < 3; ++s) w[s] = max(max(red[s][0], red[s][1]), max(red[s][2], red[s][3]));
-}
-__global__ __launch_bounds__(256) void k_residues_f64(const ResSegs q, unsigned* __restrict__ W,
+__global__ __launch_bounds__(256) void k_residues_f64(const ResSegs q, const unsigned* __restrict__ W,
                                                       double scale) {
     uint32_t s = 0;
 #pragma unroll
     for (int k = 1; k < kMaxResSegs; ++k) s += (uint32_t)k < q.nseg && blockIdx.x >= q.blk0[k];
     const ResSeg g = q.seg[s];
-    uint32_t wv[3] = {0u, 0u, 0u};
-    if (q.bx.bm) {                       // words from the maxima; block 0 publishes them
-        bit_words_from_maxima(q.bx, wv);
-        if (blockIdx.x == 0 && threadIdx.x < 3) W[threadIdx.x] = wv[threadIdx.x];
-    }
     int n = 0;
     uint32_t bmax = 0;
 #pragma unroll
     for (int p = 0; p < 2; ++p)
         if (g.wa[p] >= 0) {
-            const uint32_t ba = q.bx.bm ? wv[g.wa[p]] : W[g.wa[p]], bb = q.bx.bm ? wv[g.wb[p]] : W[g.wb[p]];
+            const uint32_t ba = W[g.wa[p]], bb = W[g.wb[p]];
             const int np = crt_nmod(ba, bb, g.lk[p]);
             if (!np) return;                                   // too wide: no CRT product
             n = max(n, np);
@@ -1537,7 +1456,7 @@ __global__ __launch_bounds__(256) void k_residues_f64(const ResSegs q, unsigned*
     else
         residues_emit<4>(w, nm, o, plane, n);
 }
-hipError_t launch_residues_f64(const ResSegs& q0, unsigned* W, int precision_bits,
+hipError_t launch_residues_f64(const ResSegs& q0, const unsigned* W, int precision_bits,
                                hipStream_t st) {
     ResSegs q = q0;
     if (!q.nseg || q.nseg > (uint32_t)kMaxResSegs) return hipErrorInvalidValue;

@@ -109,17 +109,6 @@ struct QuantSegs {
     BitFold fold;                        // fold.wout null: no in-launch fold
 };
 hipError_t launch_quantize_multi(const QuantSegs& q, int precision_bits, hipStream_t st);
-// Per-block bit-length maxima of up to three f64 matrices (k_bits_f64, read-only,
-// no in-launch fold): matrix s's values go in blocks [begin[s], begin[s+1]) of
-// vpb values each; the consumer (k_residues_f64) reduces a matrix's range.
-struct BitMax {
-    const unsigned* bm;       // null: the bit-length words are final already
-    uint32_t begin[4];
-};
-// k_bits_f64 over the first nseg segments of q (their inputs and lengths):
-// fills *bx (bm = maxima, ~512 blocks in all)
-hipError_t launch_bits_f64(const QuantSegs& q, uint32_t nseg, int precision_bits, unsigned* maxima,
-                           BitMax* bx, hipStream_t st);
 // Witness checker (svdw_check_gates). A region is `nunits` repetitions of a
 // `unit`-cell block (element u = row u / cols, column u % cols); check words:
 //   CHK_GATE g      a + b*c = d on cells g..g+3
@@ -310,11 +299,8 @@ struct ResSegs {
     ResSeg seg[kMaxResSegs];
     uint32_t blk0[kMaxResSegs + 1];   // set by the launcher
     uint32_t nseg;
-    // bx.bm set: every block reduces the words it needs from k_bits_f64's
-    // maxima, and block 0 writes all three to W (for the GEMM, combine, scans)
-    BitMax bx;
 };
-hipError_t launch_residues_f64(const ResSegs& q, unsigned* W, int precision_bits,
+hipError_t launch_residues_f64(const ResSegs& q, const unsigned* W, int precision_bits,
                                hipStream_t st);
 // c_s = A * Bt from residue planes Ar (plane stride astride rows, from the A rows'
 // first row) and Br (bstride): N x M; R is the residue scratch

@@ -268,10 +268,13 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   cells a pending one writes); "prod_cell" 1 | 0 | -1 (svd_witness with
  *   device inputs: the products on the cell stream and the u / v bounds and u.d
  *   beside them; -1 on row-sharded contexts only);
- *   "q_aside" 1 | 0 (svd_witness / verify_mul_witness with device inputs, f64
- *   views and the f64 residue path: the operand bit-length words from a read-only
- *   pass on the cell stream and the quantized cells written beside the product
- *   chain on the second stream, or the quantization ahead of it);
+ *   "pipeline" 1 | 0 (svd_witness with device inputs on the f64 CRT product
+ *   path with the products on the cell stream, two cell sets within 60 % of
+ *   the device memory: consecutive calls overlap -- a call returns with its
+ *   d / u.d / bound / diff stages and its phase-1 row scans still running on
+ *   the second and third streams, and the next call's quantization and
+ *   products start on the cell stream beside them, into the other cell set;
+ *   any other call on the context, a copy and svdw_sync wait for that tail);
  *   "graph" 1 | 0: svdw_verify_mul_witness with device inputs replays a HIP graph
  *   of its launch sequence. The second call of a key (N, K, M, the input
  *   pointers, no allocation or option change since) is captured, later calls

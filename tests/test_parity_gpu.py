@@ -198,7 +198,7 @@ def test_crt_gemm_tiles_parity(gpu_ctx_factory, N, M, P, world, device):
 @pytest.mark.parametrize("opts", [{"gemm_crt": 0}, {"stage_elems": 64}, {"stage_elems": 192},
                                   {"phase1_overlap": 0}, {"phase1_overlap": 2},
                                   {"overlap": 0}, {"gemm_priority": 1}, {"gemm_priority": 0},
-                                  {"stage_batch": 0}, {"q_aside": 0}, {"q_aside": 0, "phase1_overlap": 2},
+                                  {"stage_batch": 0}, {"pipeline": 0}, {"pipeline": 0, "phase1_overlap": 2},
                                   {"gemm_impl": 1}, {"res_f64": 0}, {"f64_views": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
@@ -375,21 +375,20 @@ def _on_device(*xs):
 
 @pytest.mark.parametrize("f64v", [1, 0])
 @pytest.mark.parametrize("res", [1, 0])
-@pytest.mark.parametrize("qa", [1, 0])
+@pytest.mark.parametrize("pipe", [1, 0])
 @pytest.mark.parametrize("N,M,P", [(130, 97, 63), (64, 200, 32)])
-def test_device_inputs_parity(gpu_ctx_factory, qa, res, f64v, N, M, P):
+def test_device_inputs_parity(gpu_ctx_factory, pipe, res, f64v, N, M, P):
     """The bench path: m, u, v, d already resident in HBM (torch float64 CUDA
     tensors), quantized in one fused launch; the CRT residue planes of
     m, u, v built from the f64 inputs in one launch (res 1) or from the
     quantized cells (res 0); the stages and row scans reading the loaded
     matrices through f64 views (f64v 1: quantized in registers, no wait for the
-    cells) or the cells; the quantized cells written beside the product chain
-    (qa, q_aside) or ahead of it; witness vs the oracle."""
+    cells) or the cells; pipelined (pipe) or not; witness vs the oracle."""
     import halo2_svd041_amd as hs
     m, u, d, v = gen_svd_input(N, M, seed=N * M)
     g = gamma_for(N + M)
     ctx = gpu_ctx_factory(P)
-    ctx.set_option("q_aside", qa)
+    ctx.set_option("pipeline", pipe)
     ctx.set_option("res_f64", res)
     ctx.set_option("f64_views", f64v)
     dm, du, dv, dd = _on_device(m, u, v, d)
@@ -451,7 +450,7 @@ def test_row_sharded_device_inputs_parity(gpu_ctx_factory, N, M, P, world):
 @pytest.mark.parametrize("world,opts", [(1, {"prod_cell": 1}), (1, {"prod_cell": 1, "stage_batch": 0}),
                                         (1, {"prod_cell": 1, "p1_at": 1}), (1, {"prod_cell": 1, "hold_us": 50}),
                                         (3, {"prod_cell": 0}), (3, {"prod_cell": 1, "stage_batch": 0}),
-                                        (4, {"prod_cell": 1, "q_aside": 0}), (1, {"q_aside": 0}),
+                                        (4, {"prod_cell": 1, "pipeline": 0}), (1, {"pipeline": 0}),
                                         (5, {"prod_cell": 0}), (4, {"p1_at": 3}), (1, {"prod_cell": 0})])
 def test_products_on_cell_stream_parity(gpu_ctx_factory, world, opts):
     """prod_cell: the products on the cell stream, the u / v bounds and u.d on
@@ -481,6 +480,61 @@ def test_products_on_cell_stream_parity(gpu_ctx_factory, world, opts):
         assert bad.size == 0, f"{key}: {bad.size} cells differ, first at {bad[:8]}"
 
 
+@pytest.mark.parametrize("N,M,P,world,hold", [(70, 53, 63, 1, 0), (53, 70, 32, 1, 200), (130, 97, 63, 4, 0),
+                                             (40, 33, 63, 1, 0)])
+def test_pipelined_witnesses_parity(gpu_ctx_factory, N, M, P, world, hold):
+    """pipeline: consecutive svd_witness calls on one context overlap (a call
+    returns with its stages and row scans still running; the next call's
+    quantization and products start beside them, into the other cell set).
+    Four calls of different inputs (and, between the second and third, a
+    change of shape) queued back to back without a host wait; the last
+    witness vs the oracle, then a non-pipelined call (check_svd_phase0 through
+    the modular API would append cells: a verify_mul_witness) and a further
+    pipelined witness, each vs the oracle. hold: every call's streams wait
+    behind a spinning kernel, so a missing cross-call dependency shows."""
+    import halo2_svd041_amd as hs
+    ctx = gpu_ctx_factory(P)
+    if world > 1:
+        ctx.set_shard(world - 1, world)
+    if hold:
+        ctx.set_option("hold_us", hold)
+    ins = []
+    for k in range(4):
+        n, m_ = (N, M) if k != 2 else (M, N)
+        m, u, d, v = gen_svd_input(n, m_, seed=400 + 13 * k + N)
+        ins.append((m, u, d, v, gamma_for(500 + k)))
+    devs = [_on_device(m, u, v, d) for m, u, d, v, _ in ins]
+    for (m, u, d, v, g), dv in zip(ins, devs):
+        counts = hs.svd_witness(ctx, *dv, g)
+
+    def check(m, u, d, v, g, counts):
+        a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+        if world == 1:
+            _assert_streams(ctx, a0, l0, a1)
+            return
+        streams = {(0, 0): ctx.advice(0), (1, 0): ctx.advice(1), (0, 1): ctx.lookups(0)}
+        for phase, lookup, off, n in ctx.shard_segments():
+            if (phase, lookup) not in streams:
+                continue
+            want = {(0, 0): a0, (1, 0): a1, (0, 1): l0}[(phase, lookup)]
+            got = streams[(phase, lookup)]
+            bad = np.nonzero(np.any(got[off:off + n] != want[off:off + n], axis=1))[0]
+            assert bad.size == 0, f"{(phase, lookup)}: {bad.size} owned cells differ from {off}"
+
+    check(*ins[3], counts)
+    if world == 1:
+        a = np.random.RandomState(3).standard_normal((9, 7))
+        b = np.random.RandomState(4).standard_normal((7, 5))
+        gv = gamma_for(77)
+        hs.verify_mul_witness(ctx, *_on_device(a, b), gv)
+        w0, w1 = corc.verify_mul_witness(a, b, P, gv)
+        np.testing.assert_array_equal(ctx.advice(0, 0, w0.shape[0]), w0)
+        np.testing.assert_array_equal(ctx.advice(1, 0, w1.shape[0]), w1)
+    ctx.reset()
+    counts = hs.svd_witness(ctx, *devs[1], ins[1][4])
+    check(*ins[1], counts)
+
+
 @pytest.mark.parametrize("N,M,P,row_lim,device,hold", [(1024, 1024, 63, 64, False, 0), (512, 512, 32, 128, False, 0),
                                                        (2048, 1024, 32, 24, False, 0), (1024, 1024, 63, 32, True, 0),
                                                        (1024, 1024, 63, 32, True, 3000),
@@ -501,15 +555,17 @@ def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device, hol
     m, u, d, v = gen_svd_input(N, M, seed=N + M + P)
     g = gamma_for(N * M)
     ctx = gpu_ctx_factory(P)
-    if hold < 0:                                  # (and quantization on the cell stream)
-        ctx.set_option("q_aside", 0)
+    if hold < 0:                                  # (and not pipelined)
+        ctx.set_option("pipeline", 0)
         hold = -hold
     if hold:
         # a first witness of other inputs allocates every buffer (allocation
         # synchronises), so the witness below runs fully queued behind the hold;
         # a launch that ran ahead would read the first witness's cells
+        # (twice: a pipelined context alternates between two cell sets)
         m2, u2, d2, v2 = gen_svd_input(N, M, seed=N + M + P + 1)
-        hs.svd_witness(ctx, *_on_device(m2, u2, v2, d2), gamma_for(N * M + 1))
+        for k in range(2):
+            hs.svd_witness(ctx, *_on_device(m2, u2, v2, d2), gamma_for(N * M + 1 + k))
         ctx.sync()
         ctx.reset()
         ctx.set_option("hold_us", hold)
