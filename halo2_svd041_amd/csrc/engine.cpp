@@ -2581,13 +2581,15 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
                      (c->prod_cell > 0 || (c->prod_cell < 0 && sharded(c))) &&
                      2.0 * wbytes <= 0.6 * (double)c->mem_total;
         if (c->in_pipe) {
-            // the other cell set (last written by call j - 2): st waits for that
-            // call's tail, the last reader of these cells and bit words
+            // the other cell set (last written by call j - 2): every stream waits
+            // for that call's tail, the last reader of these cells and bit words
+            // (st2's first stages write cells that call's st3 scans read)
             for (int p = 0; p < 2; ++p) std::swap(c->ph[p], c->alt[p]);
             clear_streams(c);
             if (c->tail_valid[c->pipe_par])
-                for (int k = 0; k < 2; ++k)
-                    hipck(hipStreamWaitEvent(c->st, c->tail_ev[c->pipe_par][k], 0), "hipStreamWaitEvent");
+                for (hipStream_t t : {c->st, c->st2, c->st3})
+                    for (int k = 0; k < 2; ++k)
+                        hipck(hipStreamWaitEvent(t, c->tail_ev[c->pipe_par][k], 0), "hipStreamWaitEvent");
         } else {
             settle(c);
             after_previous(c);
