@@ -3034,7 +3034,10 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
     gamma_prep(c, M, gamma, c->st, pw ? &pc : nullptr);
     c->gp_external = true;
     c->gp_ext_one = pw ? pc.one : nullptr;
-    const std::vector<uint64_t> key = {N, K, M, (uint64_t)(uintptr_t)a, (uint64_t)(uintptr_t)b, c->epoch};
+    // (the cell set too: a pipelined svd_witness alternates between two)
+    const std::vector<uint64_t> key = {N, K, M, (uint64_t)(uintptr_t)a, (uint64_t)(uintptr_t)b, c->epoch,
+                                       (uint64_t)(uintptr_t)c->ph[0].adv, (uint64_t)(uintptr_t)c->ph[1].adv,
+                                       (uint64_t)(uintptr_t)c->ph[0].lk, (uint64_t)(uintptr_t)c->ph[1].lk};
     if (c->vmg.exec && key == c->vmg.key) {
         const svdw_counts k = vmg_restore(c, gamma);
         hipck(hipGraphLaunch(c->vmg.exec, c->st), "hipGraphLaunch");

@@ -109,7 +109,9 @@ def test_graph_replay_after_svd_witness(gpu_ctx_factory):
     host state (layout, checks, constants, counts, product bounds) must be
     restored over whatever svd_witness left, with nothing reallocated in
     between (the svd witness runs first at the same sizes, so the second one
-    grows nothing and the epoch, hence the graph, survives)."""
+    grows nothing and the epoch, hence the graph, survives). A pipelined
+    svd_witness alternates between two cell sets: two calls allocate both, and
+    the graph replays only on the set it was captured on (part of its key)."""
     import torch
     import halo2_svd041_amd as hs
     from conftest import gen_svd_input
@@ -120,13 +122,15 @@ def test_graph_replay_after_svd_witness(gpu_ctx_factory):
     dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device="cuda:0")
                       for x in (m, u, v, d))
     ctx = gpu_ctx_factory(P)
-    hs.svd_witness(ctx, dm, du, dv, dd, gamma_for(70))
+    for k in range(2):
+        hs.svd_witness(ctx, dm, du, dv, dd, gamma_for(69 + k))
     for it in range(3):                                   # eager, capture, replay
         hs.verify_mul_witness(ctx, ta, tb, gamma_for(71 + it))
     c0, c1 = corc.verify_mul_witness(a, b, P, gamma_for(73))   # (no checker here: its scratch
     assert np.array_equal(ctx.advice(0), c0) and np.array_equal(ctx.advice(1), c1)   # would bump the epoch)
     assert ctx.graph_stats() == (1, 1)
-    hs.svd_witness(ctx, dm, du, dv, dd, gamma_for(74))
+    for k in range(2):                                    # (back on the graph's cell set)
+        hs.svd_witness(ctx, dm, du, dv, dd, gamma_for(74))
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, gamma_for(74))
     assert np.array_equal(ctx.advice(0), a0) and np.array_equal(ctx.advice(1), a1)
     hs.verify_mul_witness(ctx, ta, tb, gamma_for(75))
