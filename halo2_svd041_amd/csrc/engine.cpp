@@ -3035,9 +3035,12 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
     c->gp_external = true;
     c->gp_ext_one = pw ? pc.one : nullptr;
     // (the cell set too: a pipelined svd_witness alternates between two)
-    const std::vector<uint64_t> key = {N, K, M, (uint64_t)(uintptr_t)a, (uint64_t)(uintptr_t)b, c->epoch,
-                                       (uint64_t)(uintptr_t)c->ph[0].adv, (uint64_t)(uintptr_t)c->ph[1].adv,
-                                       (uint64_t)(uintptr_t)c->ph[0].lk, (uint64_t)(uintptr_t)c->ph[1].lk};
+    auto key_now = [&] {
+        return std::vector<uint64_t>{N, K, M, (uint64_t)(uintptr_t)a, (uint64_t)(uintptr_t)b, c->epoch,
+                                     (uint64_t)(uintptr_t)c->ph[0].adv, (uint64_t)(uintptr_t)c->ph[1].adv,
+                                     (uint64_t)(uintptr_t)c->ph[0].lk, (uint64_t)(uintptr_t)c->ph[1].lk};
+    };
+    const std::vector<uint64_t> key = key_now();
     if (c->vmg.exec && key == c->vmg.key) {
         const svdw_counts k = vmg_restore(c, gamma);
         hipck(hipGraphLaunch(c->vmg.exec, c->st), "hipGraphLaunch");
@@ -3078,7 +3081,7 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
     }
     vmg_drop(c);
     const svdw_counts k = verify_mul_witness(c, a, b, N, K, M, on_device, gamma);
-    c->vmg.seen = {N, K, M, (uint64_t)(uintptr_t)a, (uint64_t)(uintptr_t)b, c->epoch};
+    c->vmg.seen = key_now();
     return k;
 }
 
