@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-4 probe: config-2 host time and two-context alternation; steady-state
+# (no hold) kernel traces of pipelined witnesses at 1024^2, 512^2, 8-way rank.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/p2
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 200 python tools/probes/vmhost.py > $O/vmhost.json 2> $O/vmhost.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/ss_1024 -o run -- python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-profile --no-check --no-ingest > /dev/null 2> $O/ss_1024.err || exit 2
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/ss_s8 -o run -- python3 tools/shard_sim.py --worlds 8 --rank 0 --steps 8 > /dev/null 2> $O/ss_s8.err || exit 3
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/ss_512 -o run -- python3 bench.py --n 512 --p 32 --steps 8 --warmup 2 --no-cpu-baseline --no-profile --no-check --no-ingest > /dev/null 2> $O/ss_512.err || exit 4
+echo done
