@@ -1275,7 +1275,8 @@ static svdw_mat zkmatrix_new(svdw_ctx* c, uint32_t phase, const double* data, ui
                 shard_rows(c, rows, &r0, &r1);
                 qs->keep[k] = QuantKeep{cols, (uint32_t)r0, (uint32_t)r1, (uint32_t)r0, (uint32_t)r1};
             }
-            qs->blk0[k + 1] = qs->blk0[k] + (uint32_t)((n + kQuantPerBlock - 1) / kQuantPerBlock);
+            const uint32_t pb = qs->per_block ? qs->per_block : kQuantPerBlock;
+            qs->blk0[k + 1] = qs->blk0[k] + (uint32_t)((n + pb - 1) / pb);
         } else {
             ProfScope ps(c, c->st, "k_quantize", 40.0 * n, 0);
             hipck(launch_quantize(src, n, cellp(c, phase, off), (int)c->P, blockmax, c->st),
@@ -2636,9 +2637,10 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     // m: only this rank's rows are quantized on a row-sharded rank (zkmatrix_new)
     uint64_t mr0 = 0, mr1 = N;
     if (sharded(c) && on_device) shard_rows(c, N, &mr0, &mr1);
-    const uint32_t nbm = (uint32_t)(((mr1 - mr0) * M + kQuantPerBlock - 1) / kQuantPerBlock);
-    const uint32_t nbu = (uint32_t)(((uint64_t)N * N + kQuantPerBlock - 1) / kQuantPerBlock);
-    const uint32_t nbv = (uint32_t)(((uint64_t)M * M + kQuantPerBlock - 1) / kQuantPerBlock);
+    const uint32_t qpb = quant_per_block((mr1 - mr0) * M + (uint64_t)N * N + (uint64_t)M * M + r);
+    const uint32_t nbm = (uint32_t)(((mr1 - mr0) * M + qpb - 1) / qpb);
+    const uint32_t nbu = (uint32_t)(((uint64_t)N * N + qpb - 1) / qpb);
+    const uint32_t nbv = (uint32_t)(((uint64_t)M * M + qpb - 1) / qpb);
     if (!c->dry) {
         // [0, 3): bit-length maxima of m, u, v; from word 64: per-block maxima
         // (pipelined: a half per parity, call j - 1's row scans still read theirs)
@@ -2648,6 +2650,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     }
     QuantSegs qs;
     memset(&qs, 0, sizeof qs);
+    qs.per_block = qpb;
     QuantSegs* qp = &qs;
     svdw_mat zm = zkmatrix_new(c, 0, m, N, M, on_device, dbits ? dbits + 64 : nullptr, qp, true);
     // (u, v: the rank's rows and column block only, when b.g comes from the f64
@@ -2836,8 +2839,9 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     }
     host_mark(c, "plan + gamma_prep queued");
     unsigned* dbits = nullptr;
-    const uint32_t nba = (uint32_t)(((uint64_t)N * K + kQuantPerBlock - 1) / kQuantPerBlock),
-                   nbb = (uint32_t)(((uint64_t)K * M + kQuantPerBlock - 1) / kQuantPerBlock);
+    const uint32_t qpb = quant_per_block((uint64_t)N * K + (uint64_t)K * M);
+    const uint32_t nba = (uint32_t)(((uint64_t)N * K + qpb - 1) / qpb),
+                   nbb = (uint32_t)(((uint64_t)K * M + qpb - 1) / qpb);
     c->pows_pre.on = false;
     if (!c->dry) {
         // phase 1 opens with verify_mul's one cell and its d - 1 gamma-power
@@ -2859,6 +2863,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     }
     QuantSegs qs;
     memset(&qs, 0, sizeof qs);
+    qs.per_block = qpb;
     QuantSegs* qp = on_device ? &qs : nullptr;
     const svdw_mat za = zkmatrix_new(c, 0, a, N, K, on_device, dbits ? dbits + 64 : nullptr, qp);
     const svdw_mat zb = zkmatrix_new(c, 0, b, K, M, on_device, dbits ? dbits + 64 + nba : nullptr, qp);

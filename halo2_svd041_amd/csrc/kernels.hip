@@ -166,15 +166,15 @@ __device__ __forceinline__ uint32_t block_bits(const double (&xv)[PT], double sc
     __syncthreads();
     return max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
 }
-// kQuantPerBlock values per block, 16 per thread (value blk * 4096 + k * 256 +
+// PT * 256 values per block, PT per thread (value blk * PT * 256 + k * 256 +
 // tid: each store instruction coalesced), all loads issued first.
+template <int PT>
 __device__ __forceinline__ void quantize_body(const double* __restrict__ in, uint64_t n,
                                               Fr* __restrict__ out, double scale,
                                               unsigned* __restrict__ blockmax, uint32_t blk,
                                               QuantKeep keep = QuantKeep{0, 0, 0, 0, 0},
                                               const BitFold fold = BitFold{}, uint32_t gblk = 0) {
-    constexpr int PT = kQuantPerBlock / 256;
-    const uint64_t i0 = (uint64_t)blk * kQuantPerBlock + threadIdx.x;
+    const uint64_t i0 = (uint64_t)blk * (PT * 256) + threadIdx.x;
     uint32_t bmax = 0;
     double xv[PT];
 #pragma unroll
@@ -201,10 +201,11 @@ __device__ __forceinline__ void quantize_body(const double* __restrict__ in, uin
 __global__ __launch_bounds__(256) void k_quantize(const double* __restrict__ in, uint64_t n,
                                                   Fr* __restrict__ out, double scale,
                                                   unsigned* __restrict__ blockmax) {
-    quantize_body(in, n, out, scale, blockmax, blockIdx.x);
+    quantize_body<kQuantPerBlock / 256>(in, n, out, scale, blockmax, blockIdx.x);
 }
 // m, u, v, d in one launch (their ZkMatrix::new calls are back to back,
 // examples/svd_example.rs:138-144): one ramp-up / tail instead of four.
+template <int PT>
 __global__ __launch_bounds__(256) void k_quantize_multi(const QuantSegs q, double scale) {
     uint32_t s = 0;
 #pragma unroll
@@ -220,12 +221,19 @@ __global__ __launch_bounds__(256) void k_quantize_multi(const QuantSegs q, doubl
         if (s == (uint32_t)k) {
             in = q.in[k]; out = q.out[k]; bm = q.blockmax[k]; n = q.n[k]; b0 = q.blk0[k]; keep = q.keep[k];
         }
-    quantize_body(in, n, out, scale, bm, blockIdx.x - b0, keep, q.fold, blockIdx.x);
+    quantize_body<PT>(in, n, out, scale, bm, blockIdx.x - b0, keep, q.fold, blockIdx.x);
 }
 hipError_t launch_quantize_multi(const QuantSegs& q, int p, hipStream_t st) {
     if (!q.nseg || q.nseg > (uint32_t)kMaxQuantSegs || !q.blk0[q.nseg]) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_quantize_multi, dim3(q.blk0[q.nseg]), dim3(256), 0, st, q,
-                       (double)(1ull << p));
+    const uint32_t pb = q.per_block ? q.per_block : kQuantPerBlock;
+    if (pb == kQuantPerBlockSmall)
+        hipLaunchKernelGGL(k_quantize_multi<kQuantPerBlockSmall / 256>, dim3(q.blk0[q.nseg]), dim3(256), 0, st, q,
+                           (double)(1ull << p));
+    else if (pb == kQuantPerBlock)
+        hipLaunchKernelGGL(k_quantize_multi<kQuantPerBlock / 256>, dim3(q.blk0[q.nseg]), dim3(256), 0, st, q,
+                           (double)(1ull << p));
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

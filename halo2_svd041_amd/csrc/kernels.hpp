@@ -96,8 +96,14 @@ struct BitFold {
     uint32_t b[4];
 };
 // Values per quantize block (16 per thread): few enough blocks for one wave of
-// them at 1024^2, so the fold's arrival costs each block once.
+// them at 1024^2, so the fold's arrival costs each block once. Launches of
+// fewer than 2^21 values use 1024 per block (4 per thread): 256^2 x 2 is
+// otherwise 32 blocks on 256 CUs.
 static constexpr uint32_t kQuantPerBlock = 4096;
+static constexpr uint32_t kQuantPerBlockSmall = 1024;
+static inline uint32_t quant_per_block(uint64_t total_values) {
+    return total_values < (1ull << 21) ? kQuantPerBlockSmall : kQuantPerBlock;
+}
 struct QuantSegs {
     const double* in[kMaxQuantSegs];
     Fr* out[kMaxQuantSegs];
@@ -106,6 +112,7 @@ struct QuantSegs {
     QuantKeep keep[kMaxQuantSegs];
     uint32_t blk0[kMaxQuantSegs + 1];
     uint32_t nseg;
+    uint32_t per_block;                  // values per block: kQuantPerBlock(Small); 0 = kQuantPerBlock
     BitFold fold;                        // fold.wout null: no in-launch fold
 };
 hipError_t launch_quantize_multi(const QuantSegs& q, int precision_bits, hipStream_t st);
