@@ -420,6 +420,15 @@ struct svdw_ctx {
     bool tail_pending = false;              // the last pipelined call's tail not yet joined into st
     int tail_last = 0;
     size_t mem_total = 0;                   // device memory (hipMemGetInfo at create)
+    // "lanes" 2: svdw_verify_mul_witness on its captured-graph path alternates
+    // between two complete context states, this one and `lane` (own streams,
+    // cells, scratch, graph). The states are exchanged (std::swap) at the start
+    // of a call, so call j + 1 runs on the other state's streams beside call j
+    // and the handle always holds the latest call's cells. sync, stream_wait,
+    // stream_signal, graph_stats and destroy cover both; lane / lanes stay with
+    // the handle.
+    int lanes = 1;
+    svdw_ctx* lane = nullptr;
     DBuf f64in, digA, digB, digC, w1c, w1t, w2c, w2t, bits, gpc, gtab, crtR, gbits, chk, chkg;
     DBuf wbc[kMaxScanJobs], wbt[kMaxScanJobs];   // b.v per batched verify_mul (canonical, table)
     // gamma^j (canonical gpc, scaled table gtab, kernels.hpp kTabSlots) of the
@@ -632,6 +641,7 @@ static void sync(svdw_ctx* c) {
     hipck(hipStreamSynchronize(c->st2), "hipStreamSynchronize");
     if (c->st3) hipck(hipStreamSynchronize(c->st3), "hipStreamSynchronize");
     c->tail_pending = false;
+    if (c->lane) sync(c->lane);
 }
 // After a pipelined svd_witness its tail (st2, st3) is not joined into st:
 // anything else queued on the context waits for it first.
@@ -3011,6 +3021,107 @@ static svdw_counts vmg_restore(svdw_ctx* c, const Fr& gamma) {
     c->ph[1].nl = g.counts.lookup1;
     return g.counts;
 }
+static void ctx_release(svdw_ctx* c) {
+    if (!c) return;
+    if (c->lane) ctx_release(c->lane);
+    if (!c->dry && c->st && c->st2) {
+        (void)hipStreamSynchronize(c->st);
+        (void)hipStreamSynchronize(c->st2);
+        if (c->st3) (void)hipStreamSynchronize(c->st3);
+        vmg_drop(c);
+        for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
+        for (auto& s : c->alt) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
+        for (auto& t : c->tail_ev)
+            for (auto e : t)
+                if (e) (void)hipEventDestroy(e);
+        for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1], &c->w1c, &c->w1t, &c->w2c, &c->w2t,
+                        &c->bits, &c->gpc, &c->gtab, &c->crtR, &c->gbits, &c->colpart, &c->qfold,
+                        &c->ing_x, &c->ing_e, &c->ing_c, &c->ing_p10, &c->ing_val, &c->ing_npos, &c->ing_nd,
+                        &c->ing_rpos, &c->ing_kpos, &c->ing_err, &c->ing_q, &c->eq_cp, &c->eq_ks, &c->eq_reg,
+                        &c->eq_w, &c->eq_k, &c->eq_err, &c->eq_st})
+            if (b->p) (void)hipFree(b->p);
+        for (int i = 0; i < kMaxScanJobs; ++i) {
+            if (c->wbc[i].p) (void)hipFree(c->wbc[i].p);
+            if (c->wbt[i].p) (void)hipFree(c->wbt[i].p);
+            if (c->bvfull[i].p) (void)hipFree(c->bvfull[i].p);
+        }
+        if (c->hbits) (void)hipHostFree(c->hbits);
+        if (c->ev_bits) (void)hipEventDestroy(c->ev_bits);
+        for (auto e : c->xev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
+        for (auto e : c->pool) (void)hipEventDestroy(e);
+        for (auto e : c->deps) (void)hipEventDestroy(e);
+        (void)hipStreamSynchronize(c->st2);
+        if (c->st3) {
+            (void)hipStreamSynchronize(c->st3);
+            (void)hipStreamDestroy(c->st3);
+        }
+        (void)hipStreamDestroy(c->st2);
+        (void)hipStreamDestroy(c->st);
+    }
+    delete c;
+}
+// Device state of a new context: its three streams, the pinned bit words, events.
+static void ctx_init_device(svdw_ctx* c) {
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
+    c->st_cell = c->st;
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking);
+    // the third stream exists from the start: one created lazily inside a
+    // call would not wait for what st already waits for (svdw_stream_wait)
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->hbits, 64 * sizeof(uint32_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bits, hipEventDisableTiming | hipEventReleaseToDevice);
+    for (int k = 0; k < 4 && e == hipSuccess; ++k)
+        e = hipEventCreateWithFlags(&c->tail_ev[k / 2][k % 2], hipEventDisableTiming | hipEventReleaseToDevice);
+    size_t mfree = 0;
+    if (e == hipSuccess) e = hipMemGetInfo(&mfree, &c->mem_total);
+    if (e != hipSuccess) fail(SVDW_EDEVICE, std::string("HIP device init failed: ") + hipGetErrorString(e));
+}
+// The settings (options, shard, profiler) of `s` onto the lane `d`; a change
+// bumps the lane's epoch (its captured graph no longer applies).
+static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
+    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->gemm_crt, s->res_f64,
+                         s->phase1_overlap, s->prod_cell, s->hold_us, s->rlc_prefix, s->p1_at,
+                         s->f64_views, s->overlap, s->stage_batch, s->graph_vm, s->pipeline,
+                         s->shard_rank, s->shard_world, s->prof, s->gemm_prio, s->host_trace};
+    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->gemm_crt, d->res_f64,
+                         d->phase1_overlap, d->prod_cell, d->hold_us, d->rlc_prefix, d->p1_at,
+                         d->f64_views, d->overlap, d->stage_batch, d->graph_vm, d->pipeline,
+                         d->shard_rank, d->shard_world, d->prof, d->gemm_prio, d->host_trace};
+    if (!memcmp(a, b, sizeof a) && d->prof_filter == s->prof_filter) return;
+    d->gemm_impl = s->gemm_impl; d->stage_flags = s->stage_flags; d->stage_elems = s->stage_elems;
+    d->gemm_crt = s->gemm_crt; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
+    d->prod_cell = s->prod_cell; d->hold_us = s->hold_us; d->rlc_prefix = s->rlc_prefix;
+    d->p1_at = s->p1_at; d->f64_views = s->f64_views; d->overlap = s->overlap;
+    d->stage_batch = s->stage_batch; d->graph_vm = s->graph_vm; d->pipeline = s->pipeline;
+    d->shard_rank = s->shard_rank; d->shard_world = s->shard_world; d->prof = s->prof;
+    d->gemm_prio = s->gemm_prio; d->host_trace = s->host_trace; d->prof_filter = s->prof_filter;
+    ++d->epoch;
+}
+// "lanes": exchange this state with the lane's (created on first use).
+static void lane_switch(svdw_ctx* c) {
+    if (!c->lane) {
+        svdw_ctx* L = new svdw_ctx();
+        L->P = c->P;
+        L->LB = c->LB;
+        L->device = c->device;
+        L->dry = false;
+        try {
+            ctx_init_device(L);
+        } catch (...) {
+            ctx_release(L);
+            throw;
+        }
+        c->lane = L;
+    }
+    svdw_ctx* L = c->lane;
+    copy_settings(L, c);
+    std::swap(*c, *L);
+    std::swap(c->lane, L->lane);                  // (the handle keeps the lane and the option)
+    std::swap(c->lanes, L->lanes);
+}
 static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const double* b, uint32_t N,
                                           uint32_t K, uint32_t M, bool on_device, const Fr& gamma) {
     const bool usable = c->graph_vm && on_device && !c->dry && !c->prof && !c->hold_us && !sharded(c) &&
@@ -3020,6 +3131,7 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
         c->vmg.seen.clear();
         return verify_mul_witness(c, a, b, N, K, M, on_device, gamma);
     }
+    if (c->lanes > 1) lane_switch(c);
     struct Flags {
         svdw_ctx* c;
         ~Flags() {
@@ -3264,66 +3376,18 @@ int svdw_ctx_create(const svdw_params* p, svdw_ctx** out) {
         if (const char* g = getenv("SVDW_GEMM"))
             c->gemm_impl = (!strcmp(g, "valu") || !strcmp(g, "dot4")) ? SVDW_GEMM_VALU : SVDW_GEMM_MFMA;
         if (!c->dry) {
-            hipError_t e = hipSetDevice(p->device);
-            if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
-            c->st_cell = c->st;
-            if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking);
-            // the third stream exists from the start: one created lazily inside a
-            // call would not wait for what st already waits for (svdw_stream_wait)
-            if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st3, hipStreamNonBlocking);
-            if (e == hipSuccess) e = hipHostMalloc((void**)&c->hbits, 64 * sizeof(uint32_t),
-                                               hipHostMallocDefault);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bits, hipEventDisableTiming | hipEventReleaseToDevice);
-            for (int k = 0; k < 4 && e == hipSuccess; ++k)
-                e = hipEventCreateWithFlags(&c->tail_ev[k / 2][k % 2], hipEventDisableTiming | hipEventReleaseToDevice);
-            size_t mfree = 0;
-            if (e == hipSuccess) e = hipMemGetInfo(&mfree, &c->mem_total);
-            if (e != hipSuccess) {
-                delete c;
-                fail(SVDW_EDEVICE, std::string("HIP device init failed: ") + hipGetErrorString(e));
+            try {
+                ctx_init_device(c);
+            } catch (...) {
+                ctx_release(c);
+                throw;
             }
         }
         *out = c;
     });
 }
 int svdw_ctx_destroy(svdw_ctx* c) {
-    return guarded([&] {
-        if (!c) return;
-        if (!c->dry) {
-            (void)hipStreamSynchronize(c->st);
-            (void)hipStreamSynchronize(c->st2);
-            if (c->st3) (void)hipStreamSynchronize(c->st3);
-            vmg_drop(c);
-            for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
-            for (auto& s : c->alt) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
-            for (auto& t : c->tail_ev)
-                for (auto e : t)
-                    if (e) (void)hipEventDestroy(e);
-            for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1], &c->w1c, &c->w1t, &c->w2c, &c->w2t,
-                            &c->bits, &c->gpc, &c->gtab, &c->crtR, &c->gbits, &c->colpart, &c->qfold})
-                if (b->p) (void)hipFree(b->p);
-            for (int i = 0; i < kMaxScanJobs; ++i) {
-                if (c->wbc[i].p) (void)hipFree(c->wbc[i].p);
-                if (c->wbt[i].p) (void)hipFree(c->wbt[i].p);
-                if (c->bvfull[i].p) (void)hipFree(c->bvfull[i].p);
-            }
-            if (c->hbits) (void)hipHostFree(c->hbits);
-            if (c->ev_bits) (void)hipEventDestroy(c->ev_bits);
-            for (auto e : c->xev)
-                if (e) (void)hipEventDestroy(e);
-            for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
-            for (auto e : c->pool) (void)hipEventDestroy(e);
-            for (auto e : c->deps) (void)hipEventDestroy(e);
-            (void)hipStreamSynchronize(c->st2);
-            if (c->st3) {
-                (void)hipStreamSynchronize(c->st3);
-                (void)hipStreamDestroy(c->st3);
-            }
-            (void)hipStreamDestroy(c->st2);
-            (void)hipStreamDestroy(c->st);
-        }
-        delete c;
-    });
+    return guarded([&] { ctx_release(c); });
 }
 int svdw_ctx_reset(svdw_ctx* c) {
     return guarded([&] {
@@ -3350,6 +3414,7 @@ static hipEvent_t xevent(svdw_ctx* c, int i) {
         hipck(hipEventCreateWithFlags(&c->xev[i], hipEventDisableTiming), "hipEventCreate");
     return c->xev[i];
 }
+// (with lanes: both states' streams, since the next call may run on either)
 int svdw_stream_wait(svdw_ctx* c, void* stream) {
     return guarded([&] {
         REQUIRE(c, "null ctx");
@@ -3357,8 +3422,10 @@ int svdw_stream_wait(svdw_ctx* c, void* stream) {
         const hipStream_t s = (hipStream_t)stream;
         const hipEvent_t e = xevent(c, 0);
         hipck(hipEventRecord(e, s), "hipEventRecord");
-        for (hipStream_t t : {c->st, c->st2, c->st3})
-            if (t) hipck(hipStreamWaitEvent(t, e, 0), "hipStreamWaitEvent");
+        for (svdw_ctx* x : {c, c->lane})
+            if (x)
+                for (hipStream_t t : {x->st, x->st2, x->st3})
+                    if (t) hipck(hipStreamWaitEvent(t, e, 0), "hipStreamWaitEvent");
     });
 }
 int svdw_stream_signal(svdw_ctx* c, void* stream) {
@@ -3366,13 +3433,16 @@ int svdw_stream_signal(svdw_ctx* c, void* stream) {
         REQUIRE(c, "null ctx");
         if (c->dry) return;
         const hipStream_t s = (hipStream_t)stream;
-        int i = 1;
-        for (hipStream_t t : {c->st, c->st2, c->st3}) {
-            if (!t) continue;
-            flush_batch(c, t);
-            const hipEvent_t e = xevent(c, i++);
-            hipck(hipEventRecord(e, t), "hipEventRecord");
-            hipck(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
+        for (svdw_ctx* x : {c, c->lane}) {
+            if (!x) continue;
+            int i = 1;
+            for (hipStream_t t : {x->st, x->st2, x->st3}) {
+                if (!t) continue;
+                flush_batch(x, t);
+                const hipEvent_t e = xevent(x, i++);
+                hipck(hipEventRecord(e, t), "hipEventRecord");
+                hipck(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
+            }
         }
     });
 }
@@ -4240,7 +4310,10 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         sync(c);
         ++c->epoch;                                  // a captured launch sequence may change
         const std::string n(name);
-        if (n == "pipeline") {                       // pipelined svd_witness (svd_witness)
+        if (n == "lanes") {                          // verify_mul_witness on two alternating states
+            REQUIRE(value == 1 || value == 2, "lanes: 1 or 2");
+            c->lanes = (int)value;
+        } else if (n == "pipeline") {                // pipelined svd_witness (svd_witness)
             REQUIRE(value == 0 || value == 1, "pipeline: 0 or 1");
             c->pipeline = (int)value;
         } else if (n == "graph") {                   // captured verify_mul_witness (vm_graph)
@@ -4291,8 +4364,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
 int svdw_graph_stats(svdw_ctx* c, uint64_t* captures, uint64_t* replays) {
     return guarded([&] {
         REQUIRE(c && captures && replays, "null argument");
-        *captures = c->vmg.captures;
-        *replays = c->vmg.replays;
+        *captures = c->vmg.captures + (c->lane ? c->lane->vmg.captures : 0);
+        *replays = c->vmg.replays + (c->lane ? c->lane->vmg.replays : 0);
     });
 }
 int svdw_set_gemm_impl(svdw_ctx* c, int impl) {

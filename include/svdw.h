@@ -243,7 +243,7 @@ int svdw_verify_mul_witness(svdw_ctx* ctx, const double* a, const double* b, uin
 #define SVDW_GEMM_MFMA 0
 #define SVDW_GEMM_VALU 1
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
-/* Options (svdw_set_option; 15 of them). Tuning knobs, bit-identical results
+/* Options (svdw_set_option; 16 of them). Tuning knobs, bit-identical results
  * for every value, defaults first:
  *   "gemm_impl" 0 | 1; "gemm_crt" 1 | 0 (CRT or digit-plane matrix-core GEMM);
  *   "overlap" 1 | 0 (the three check_svd_phase0 products run ahead on a second
@@ -275,6 +275,11 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   the second and third streams, and the next call's quantization and
  *   products start on the cell stream beside them, into the other cell set;
  *   any other call on the context, a copy and svdw_sync wait for that tail);
+ *   "lanes" 1 | 2 (svdw_verify_mul_witness on the graph path: 2 alternates
+ *   between two complete context states, exchanged behind the handle at each
+ *   call, so consecutive calls run beside each other on separate streams; the
+ *   handle always shows the latest call's cells; svdw_sync, stream_wait /
+ *   _signal, graph_stats and destroy cover both states);
  *   "graph" 1 | 0: svdw_verify_mul_witness with device inputs replays a HIP graph
  *   of its launch sequence. The second call of a key (N, K, M, the input
  *   pointers, no allocation or option change since) is captured, later calls

@@ -136,3 +136,55 @@ def test_graph_replay_after_svd_witness(gpu_ctx_factory):
     hs.verify_mul_witness(ctx, ta, tb, gamma_for(75))
     assert ctx.graph_stats() == (1, 2), "the svd witness reallocated: no replay was tested"
     _check_all(ctx, a, b, P, gamma_for(75))
+
+
+@pytest.mark.gpu
+def test_lanes_alternate_match_oracle(gpu_ctx_factory):
+    """lanes 2: consecutive verify_mul_witness calls alternate between two
+    complete context states (streams, cells, scratch, graph), exchanged behind
+    the handle at each call, so the handle shows the latest call's cells. Ten
+    calls with new values and gamma, each checked (cells, gates, equalities):
+    each state captures on its third call and replays after."""
+    import torch
+    import halo2_svd041_amd as hs
+    P, n, k, m = 32, 64, 48, 40
+    ctx = gpu_ctx_factory(P)
+    ctx.set_option("lanes", 2)
+    ta = torch.empty((n, k), dtype=torch.float64, device="cuda:0")
+    tb = torch.empty((k, m), dtype=torch.float64, device="cuda:0")
+    for it in range(10):
+        a, b = _mats(n, k, m, seed=300 + it)
+        ta.copy_(torch.from_numpy(a))
+        tb.copy_(torch.from_numpy(b))
+        g = gamma_for(900 + it)
+        hs.verify_mul_witness(ctx, ta, tb, g)
+        _check_all(ctx, a, b, P, g)
+    assert ctx.graph_stats() == (2, 4)
+
+
+@pytest.mark.gpu
+def test_lanes_back_to_back_then_svd(gpu_ctx_factory):
+    """lanes 2 without a host wait between calls (call j + 1 runs beside call
+    j on the other state's streams): the last call's witness matches the
+    oracle; then an svd_witness and another verify_mul on the same handle."""
+    import torch
+    import halo2_svd041_amd as hs
+    from conftest import gen_svd_input
+    P = 32
+    ctx = gpu_ctx_factory(P)
+    ctx.set_option("lanes", 2)
+    a, b = _mats(96, 80, 72, seed=41)
+    ta, tb = (torch.tensor(x, dtype=torch.float64, device="cuda:0") for x in (a, b))
+    for it in range(9):
+        hs.verify_mul_witness(ctx, ta, tb, gamma_for(950 + it))
+    c0, c1 = corc.verify_mul_witness(a, b, P, gamma_for(958))
+    assert np.array_equal(ctx.advice(0), c0) and np.array_equal(ctx.advice(1), c1)
+    assert ctx.graph_stats()[1] >= 2
+    mm, u, d, v = gen_svd_input(40, 36, seed=43)
+    dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device="cuda:0")
+                      for x in (mm, u, v, d))
+    hs.svd_witness(ctx, dm, du, dv, dd, gamma_for(960))
+    a0, l0, a1 = corc.svd_witness(mm, u, v, d, P, 19, gamma_for(960))
+    assert np.array_equal(ctx.advice(0), a0) and np.array_equal(ctx.advice(1), a1)
+    hs.verify_mul_witness(ctx, ta, tb, gamma_for(961))
+    _check_all(ctx, a, b, P, gamma_for(961))

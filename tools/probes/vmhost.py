@@ -44,7 +44,14 @@ for c in ctxs:
         hs.verify_mul_witness(c, ta, tb, gs[k])
     c.sync()
 c0 = ctxs[0]
+cl = hs.Context(device=0, precision_bits=P, lookup_bits=19)
+cl.set_option("lanes", 2)
+for k in range(10):
+    hs.verify_mul_witness(cl, ta, tb, gs[k])
+cl.sync()
 for rnd in range(3):
+    h, s = timed(lambda k: hs.verify_mul_witness(cl, ta, tb, gs[k]))
+    out.setdefault("lanes2", []).append({"host_ms": round(h, 4), "step_ms": round(s, 4)})
     h, s = timed(lambda k: hs.verify_mul_witness(c0, ta, tb, gs[k]))
     out.setdefault("one_ctx", []).append({"host_ms": round(h, 4), "step_ms": round(s, 4)})
     h, s = timed(lambda k: hs.verify_mul_witness(ctxs[k & 1], ta, tb, gs[k]))
@@ -63,5 +70,5 @@ h, s = timed(lambda k: zk._words_arg(gs[k]))
 out["gamma_words_only"] = {"host_ms": round(h, 4)}
 h, s = timed(lambda k: zk._torch_stream(c0))
 out["torch_stream_lookup"] = {"host_ms": round(h, 4)}
-out["graph_stats"] = [list(c.graph_stats()) for c in ctxs]
+out["graph_stats"] = [list(c.graph_stats()) for c in ctxs + [cl]]
 print(json.dumps(out))

@@ -9,7 +9,9 @@ export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_parity_gpu.py tests/test_verify_mul_config.py tests/test_graph_gpu.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 9; }
 tail -1 $O/pytest.log
 for i in 1 2; do
-  timeout -k 10 300 python bench.py --workload verify_mul --no-cpu-baseline > $O/vm_$i.json 2>> $O/vm.err || exit 8
+  for l in 1 2; do
+    timeout -k 10 300 python bench.py --workload verify_mul --no-cpu-baseline --opt lanes=$l > $O/vm_l${l}_$i.json 2>> $O/vm.err || exit 8
+  done
 done
 timeout -k 10 200 python tools/probes/vmhost.py > $O/vmhost.json 2> $O/vmhost.err || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/ss_1024 -o run -- python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-profile --no-check --no-ingest > /dev/null 2> $O/ss_1024.err || exit 2
