@@ -2647,7 +2647,9 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     // m: only this rank's rows are quantized on a row-sharded rank (zkmatrix_new)
     uint64_t mr0 = 0, mr1 = N;
     if (sharded(c) && on_device) shard_rows(c, N, &mr0, &mr1);
-    const uint32_t qpb = quant_per_block((mr1 - mr0) * M + (uint64_t)N * N + (uint64_t)M * M + r);
+    // (host inputs go through launch_quantize, kQuantPerBlock values per block)
+    const uint32_t qpb = on_device ? quant_per_block((mr1 - mr0) * M + (uint64_t)N * N + (uint64_t)M * M + r)
+                                   : kQuantPerBlock;
     const uint32_t nbm = (uint32_t)(((mr1 - mr0) * M + qpb - 1) / qpb);
     const uint32_t nbu = (uint32_t)(((uint64_t)N * N + qpb - 1) / qpb);
     const uint32_t nbv = (uint32_t)(((uint64_t)M * M + qpb - 1) / qpb);
@@ -2849,7 +2851,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     }
     host_mark(c, "plan + gamma_prep queued");
     unsigned* dbits = nullptr;
-    const uint32_t qpb = quant_per_block((uint64_t)N * K + (uint64_t)K * M);
+    const uint32_t qpb = on_device ? quant_per_block((uint64_t)N * K + (uint64_t)K * M) : kQuantPerBlock;
     const uint32_t nba = (uint32_t)(((uint64_t)N * K + qpb - 1) / qpb),
                    nbb = (uint32_t)(((uint64_t)K * M + qpb - 1) / qpb);
     c->pows_pre.on = false;
