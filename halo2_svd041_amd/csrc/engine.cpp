@@ -981,8 +981,9 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     if (g_stage_log) {
         uint32_t nmul = 0;
         for (uint32_t i = 0; i < a.nmo; ++i) nmul += a.mo[i].op == MO_MUL;
-        fprintf(stderr, "stage %-28s elems %8u C %3u L %3u nv %2u nmo %2u muls %u nk %u\n", tag, ee - eb,
-                a.C, a.L, a.nv, a.nmo, nmul, a.nk);
+        const int sid = c->st == c->st_cell ? 1 : c->st == c->st2 ? 2 : c->st == c->st3 ? 3 : 0;
+        fprintf(stderr, "stage %-28s elems %8u C %3u L %3u nv %2u nmo %2u muls %u nk %u  s%d\n", tag, ee - eb,
+                a.C, a.L, a.nv, a.nmo, nmul, a.nk, sid);
     }
     if (c->dry || ee <= eb) return;
     a.out_adv = cellp(c, phase, off);
@@ -3103,6 +3104,7 @@ static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
     ++d->epoch;
 }
 // "lanes": exchange this state with the lane's (created on first use).
+static_assert(std::is_nothrow_move_constructible<svdw_ctx>::value && std::is_nothrow_move_assignable<svdw_ctx>::value, "svdw_ctx moves");
 static void lane_switch(svdw_ctx* c) {
     if (!c->lane) {
         svdw_ctx* L = new svdw_ctx();
