@@ -1228,8 +1228,10 @@ static svdw_vec put_cell(svdw_ctx* c, uint32_t phase, const Fr& v, bool constant
     pb.cell(pb.K(v));
     // Inside svd_witness (products queued ahead), a one-cell launch on the cell
     // stream would wait for a free CU behind the scans on st2 (15-35 us on the
-    // critical path); it depends on nothing, so it goes on st2 itself.
-    const bool aside = c->prelaunched && !c->dry;
+    // critical path); it depends on nothing, so it goes on st2 itself (never
+    // back onto the cell stream: with st and st2 exchanged, as for a pipelined
+    // witness's diff and ids, it stays where it is).
+    const bool aside = c->prelaunched && !c->dry && c->st2 != c->st_cell;
     if (aside) std::swap(c->st, c->st2);
     uint64_t off = 0;
     try {
