@@ -3420,7 +3420,8 @@ static hipEvent_t xevent(svdw_ctx* c, int i) {
         hipck(hipEventCreateWithFlags(&c->xev[i], hipEventDisableTiming), "hipEventCreate");
     return c->xev[i];
 }
-// (with lanes: both states' streams, since the next call may run on either)
+// (with lanes, the lane's state runs only the captured verify_mul graph, whose
+// side streams fork from st: its st waits too)
 int svdw_stream_wait(svdw_ctx* c, void* stream) {
     return guarded([&] {
         REQUIRE(c, "null ctx");
@@ -3428,10 +3429,9 @@ int svdw_stream_wait(svdw_ctx* c, void* stream) {
         const hipStream_t s = (hipStream_t)stream;
         const hipEvent_t e = xevent(c, 0);
         hipck(hipEventRecord(e, s), "hipEventRecord");
-        for (svdw_ctx* x : {c, c->lane})
-            if (x)
-                for (hipStream_t t : {x->st, x->st2, x->st3})
-                    if (t) hipck(hipStreamWaitEvent(t, e, 0), "hipStreamWaitEvent");
+        for (hipStream_t t : {c->st, c->st2, c->st3})
+            if (t) hipck(hipStreamWaitEvent(t, e, 0), "hipStreamWaitEvent");
+        if (c->lane) hipck(hipStreamWaitEvent(c->lane->st, e, 0), "hipStreamWaitEvent");
     });
 }
 int svdw_stream_signal(svdw_ctx* c, void* stream) {
