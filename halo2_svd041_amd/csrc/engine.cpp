@@ -2402,18 +2402,24 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     {
         // The d checks (three latency-bound stages over r elements) depend on d
         // only: with the products queued ahead they go behind them on st2, off
-        // the cell stream, which starts on the u / v bounds at once.
+        // the cell stream, which starts on the u / v bounds at once. Pipelined
+        // (st2 then carries every stage of the call back to back), on st3
+        // ahead of phase 1: their dependent second launch would otherwise sit
+        // between the bounds and the diff.
         struct Swap {
             svdw_ctx* c;
-            bool on;
-            Swap(svdw_ctx* cc, bool o) : c(cc), on(o) { if (on) std::swap(c->st, c->st2); }
-            ~Swap() { if (on) std::swap(c->st, c->st2); }
-        } sw(c, c->overlap && known_bits && !c->dry && c->bits_pending);
+            hipStream_t* other;
+            Swap(svdw_ctx* cc, bool o, bool third) : c(cc), other(o ? (third ? &cc->st3 : &cc->st2) : nullptr) {
+                if (other) std::swap(c->st, *other);
+            }
+            ~Swap() { if (other) std::swap(c->st, *other); }
+            bool on() const { return other != nullptr; }
+        } sw(c, c->overlap && known_bits && !c->dry && c->bits_pending, c->in_pipe && c->st3);
         // d loaded -- unless every load these stages (and the bounds and u.d
         // queued behind them with the products on the cell stream) read comes
         // from the registered f64 inputs (f64_view): then st2 starts at once
         const bool from_f64 = c->f64_views && !c->f64reg.empty() && c->prod_on_cell;
-        if (sw.on && !from_f64) dep_wait(c, c->st, c->ev_bits);
+        if (sw.on() && !from_f64) dep_wait(c, c->st, c->ev_bits);
         BatchScope bs(c);                   // (desc_order_range reads desc_order_sub: two launches)
         entries_less_than(c, d, max_bits);
         entries_in_desc_order(c, d, max_bits);
@@ -2487,8 +2493,9 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     if (pc) {
         std::swap(c->st, c->st2);
         // the cell stream waits for u.d (and what precedes it on st2), not for
-        // the d checks' dependent second group batched behind it
-        flush_batch(c, c->st2, c->st);
+        // the d checks' dependent second group batched behind it; pipelined,
+        // the diff is on st2 itself and st carries the next call: no wait
+        flush_batch(c, c->st2, c->in_pipe ? nullptr : c->st);
     }
     if (batched) {
         host_mark(c, "bounds(u), bounds(v), u.d queued");
