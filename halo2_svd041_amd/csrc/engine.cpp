@@ -3145,6 +3145,7 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
         return verify_mul_witness(c, a, b, N, K, M, on_device, gamma);
     }
     if (c->lanes > 1) lane_switch(c);
+    c->ht0 = std::chrono::steady_clock::now();
     struct Flags {
         svdw_ctx* c;
         ~Flags() {
@@ -3162,6 +3163,7 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
     PowCells pc;
     const bool pw = vm_pow_cells(c, M, gamma, &pc);
     gamma_prep(c, M, gamma, c->st, pw ? &pc : nullptr);
+    host_mark(c, "vm: gamma_prep queued");
     c->gp_external = true;
     c->gp_ext_one = pw ? pc.one : nullptr;
     // (the cell set too: a pipelined svd_witness alternates between two)
@@ -3173,7 +3175,9 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
     const std::vector<uint64_t> key = key_now();
     if (c->vmg.exec && key == c->vmg.key) {
         const svdw_counts k = vmg_restore(c, gamma);
+        host_mark(c, "vm: host state restored");
         hipck(hipGraphLaunch(c->vmg.exec, c->st), "hipGraphLaunch");
+        host_mark(c, "vm: graph launched");
         ++c->vmg.replays;
         return k;
     }

@@ -72,3 +72,5 @@ h, s = timed(lambda k: zk._torch_stream(c0))
 out["torch_stream_lookup"] = {"host_ms": round(h, 4)}
 out["graph_stats"] = [list(c.graph_stats()) for c in ctxs + [cl]]
 print(json.dumps(out))
+if os.environ.get("SVDW_HOST_TRACE"):
+    sys.stderr.flush()

@@ -22,3 +22,5 @@ timeout -k 10 300 python tools/ab.py --n 1024 --p 63 --rounds 5 --steps 5 --vari
 timeout -k 10 300 python tools/ab.py --n 512 --p 32 --rounds 5 --steps 8 --variant on:pipeline=1 --variant off:pipeline=0 > $O/ab512.txt 2>>$O/ab.err || exit 3
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/ss_s8 -o run -- python3 tools/shard_sim.py --worlds 8 --rank 0 --steps 8 > /dev/null 2> $O/ss_s8.err || exit 5
 echo done
+SVDW_HOST_TRACE=1 timeout -k 10 200 python tools/probes/vmhost.py > $O/vmhost.json 2> $O/vmhost_trace.txt || exit 6
+echo done2
