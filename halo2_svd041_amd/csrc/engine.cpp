@@ -3137,14 +3137,15 @@ static void lane_switch(svdw_ctx* c) {
 }
 static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const double* b, uint32_t N,
                                           uint32_t K, uint32_t M, bool on_device, const Fr& gamma) {
-    const bool usable = c->graph_vm && on_device && !c->dry && !c->prof && !c->hold_us && !sharded(c) &&
-                        N >= 1 && K >= 1 && M >= 1;
+    const bool plain = on_device && !c->dry && !c->prof && !c->hold_us && !sharded(c) && N >= 1 && K >= 1 &&
+                       M >= 1;
+    if (plain && c->lanes > 1) lane_switch(c);
+    const bool usable = c->graph_vm && plain;
     if (!usable) {
         vmg_drop(c);
         c->vmg.seen.clear();
         return verify_mul_witness(c, a, b, N, K, M, on_device, gamma);
     }
-    if (c->lanes > 1) lane_switch(c);
     c->ht0 = std::chrono::steady_clock::now();
     struct Flags {
         svdw_ctx* c;

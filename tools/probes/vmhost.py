@@ -44,6 +44,19 @@ for c in ctxs:
         hs.verify_mul_witness(c, ta, tb, gs[k])
     c.sync()
 c0 = ctxs[0]
+ce = hs.Context(device=0, precision_bits=P, lookup_bits=19)       # eager (no graph)
+ce.set_option("graph", 0)
+cel = hs.Context(device=0, precision_bits=P, lookup_bits=19)      # eager, two lanes
+cel.set_option("graph", 0)
+cel.set_option("lanes", 2)
+for c in (ce, cel):
+    for k in range(6):
+        hs.verify_mul_witness(c, ta, tb, gs[k])
+    c.sync()
+for rnd in range(3):
+    for name, c in (("eager_one_ctx", ce), ("eager_lanes2", cel)):
+        h, s = timed(lambda k: hs.verify_mul_witness(c, ta, tb, gs[k]))
+        out.setdefault(name, []).append({"host_ms": round(h, 4), "step_ms": round(s, 4)})
 cl = hs.Context(device=0, precision_bits=P, lookup_bits=19)
 cl.set_option("lanes", 2)
 for k in range(10):
