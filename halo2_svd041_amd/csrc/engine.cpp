@@ -427,8 +427,13 @@ struct svdw_ctx {
     // and the handle always holds the latest call's cells. sync, stream_wait,
     // stream_signal, graph_stats and destroy cover both; lane / lanes stay with
     // the handle.
-    int lanes = 1;
+    int lanes = 2;                          // (config 2, same box: 0.081 -> 0.058 ms per call)
     svdw_ctx* lane = nullptr;
+    // svdw_stream_wait's event (the caller's stream), not yet waited on by
+    // st2 / st3: st waits at once; the side streams inherit it through
+    // after_previous or the captured graph's fork from st, and the pipelined
+    // svd_witness (whose side streams do not wait for st) waits explicitly
+    hipEvent_t xwait_side = nullptr;
     DBuf f64in, digA, digB, digC, w1c, w1t, w2c, w2t, bits, gpc, gtab, crtR, gbits, chk, chkg;
     DBuf wbc[kMaxScanJobs], wbt[kMaxScanJobs];   // b.v per batched verify_mul (canonical, table)
     // gamma^j (canonical gpc, scaled table gtab, kernels.hpp kTabSlots) of the
@@ -2548,6 +2553,7 @@ static void after_previous(svdw_ctx* c) {
     if (c->dry) return;
     const hipEvent_t e = stream_dep(c, c->st, c->st2);
     if (c->st3) dep_wait(c, c->st3, e);
+    c->xwait_side = nullptr;                      // (st waited for the caller's stream)
 }
 static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, const double* v,
                                const double* d, uint32_t N, uint32_t M, bool on_device,
@@ -2611,6 +2617,11 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
                 for (hipStream_t t : {c->st, c->st2, c->st3})
                     for (int k = 0; k < 2; ++k)
                         hipck(hipStreamWaitEvent(t, c->tail_ev[c->pipe_par][k], 0), "hipStreamWaitEvent");
+            if (c->xwait_side) {                  // the caller's stream (svdw_stream_wait)
+                for (hipStream_t t : {c->st2, c->st3})
+                    hipck(hipStreamWaitEvent(t, c->xwait_side, 0), "hipStreamWaitEvent");
+                c->xwait_side = nullptr;
+            }
         } else {
             settle(c);
             after_previous(c);
@@ -3178,6 +3189,7 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
         const svdw_counts k = vmg_restore(c, gamma);
         host_mark(c, "vm: host state restored");
         hipck(hipGraphLaunch(c->vmg.exec, c->st), "hipGraphLaunch");
+        c->xwait_side = nullptr;                      // (its side streams fork from st)
         host_mark(c, "vm: graph launched");
         ++c->vmg.replays;
         return k;
@@ -3432,8 +3444,9 @@ static hipEvent_t xevent(svdw_ctx* c, int i) {
         hipck(hipEventCreateWithFlags(&c->xev[i], hipEventDisableTiming), "hipEventCreate");
     return c->xev[i];
 }
-// (with lanes, the lane's state runs only the captured verify_mul graph, whose
-// side streams fork from st: its st waits too)
+// st waits at once; st2 / st3 inherit the wait from st where a call orders them
+// after it, else wait themselves (xwait_side). With lanes, the lane's state too
+// (the next verify_mul_witness runs there).
 int svdw_stream_wait(svdw_ctx* c, void* stream) {
     return guarded([&] {
         REQUIRE(c, "null ctx");
@@ -3441,9 +3454,11 @@ int svdw_stream_wait(svdw_ctx* c, void* stream) {
         const hipStream_t s = (hipStream_t)stream;
         const hipEvent_t e = xevent(c, 0);
         hipck(hipEventRecord(e, s), "hipEventRecord");
-        for (hipStream_t t : {c->st, c->st2, c->st3})
-            if (t) hipck(hipStreamWaitEvent(t, e, 0), "hipStreamWaitEvent");
-        if (c->lane) hipck(hipStreamWaitEvent(c->lane->st, e, 0), "hipStreamWaitEvent");
+        for (svdw_ctx* x : {c, c->lane}) {
+            if (!x) continue;
+            hipck(hipStreamWaitEvent(x->st, e, 0), "hipStreamWaitEvent");
+            x->xwait_side = e;
+        }
     });
 }
 int svdw_stream_signal(svdw_ctx* c, void* stream) {

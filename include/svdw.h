@@ -275,7 +275,7 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   the second and third streams, and the next call's quantization and
  *   products start on the cell stream beside them, into the other cell set;
  *   any other call on the context, a copy and svdw_sync wait for that tail);
- *   "lanes" 1 | 2 (svdw_verify_mul_witness on the graph path: 2 alternates
+ *   "lanes" 2 | 1 (svdw_verify_mul_witness with device inputs: 2 alternates
  *   between two complete context states, exchanged behind the handle at each
  *   call, so consecutive calls run beside each other on separate streams; the
  *   handle always shows the latest call's cells; svdw_sync, stream_wait /

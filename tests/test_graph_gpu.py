@@ -39,6 +39,7 @@ def test_graph_replays_match_oracle(gpu_ctx_factory, n, k, m, P):
     import torch
     import halo2_svd041_amd as hs
     ctx = gpu_ctx_factory(P)
+    ctx.set_option("lanes", 1)                        # (counts of one state's graph)
     ta = torch.empty((n, k), dtype=torch.float64, device="cuda:0")
     tb = torch.empty((k, m), dtype=torch.float64, device="cuda:0")
     for it in range(5):
@@ -63,6 +64,7 @@ def test_graph_pipelined_calls_keep_gamma_order(gpu_ctx_factory):
     a, b = _mats(n, k, m, seed=5)
     ta, tb = (torch.tensor(x, dtype=torch.float64, device="cuda:0") for x in (a, b))
     ctx = gpu_ctx_factory(P)
+    ctx.set_option("lanes", 1)                        # (counts of one state's graph)
     for it in range(8):
         hs.verify_mul_witness(ctx, ta, tb, gamma_for(it))
     _check_all(ctx, a, b, P, gamma_for(7))
@@ -80,6 +82,8 @@ def test_graph_off_and_invalidation(gpu_ctx_factory):
     a, b = _mats(64, 40, 50, seed=9)
     ta, tb = (torch.tensor(x, dtype=torch.float64, device="cuda:0") for x in (a, b))
     on, off = gpu_ctx_factory(P), gpu_ctx_factory(P)
+    for x in (on, off):
+        x.set_option("lanes", 1)
     off.set_option("graph", 0)
     for it in range(4):
         g = gamma_for(40 + it)
@@ -122,6 +126,7 @@ def test_graph_replay_after_svd_witness(gpu_ctx_factory):
     dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device="cuda:0")
                       for x in (m, u, v, d))
     ctx = gpu_ctx_factory(P)
+    ctx.set_option("lanes", 1)                        # (counts of one state's graph)
     for k in range(2):
         hs.svd_witness(ctx, dm, du, dv, dd, gamma_for(69 + k))
     for it in range(3):                                   # eager, capture, replay

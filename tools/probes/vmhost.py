@@ -40,12 +40,15 @@ def timed(fn, iters=200):
 
 ctxs = [hs.Context(device=0, precision_bits=P, lookup_bits=19) for _ in range(2)]
 for c in ctxs:
+    c.set_option("lanes", 1)
+for c in ctxs:
     for k in range(6):
         hs.verify_mul_witness(c, ta, tb, gs[k])
     c.sync()
 c0 = ctxs[0]
 ce = hs.Context(device=0, precision_bits=P, lookup_bits=19)       # eager (no graph)
 ce.set_option("graph", 0)
+ce.set_option("lanes", 1)
 cel = hs.Context(device=0, precision_bits=P, lookup_bits=19)      # eager, two lanes
 cel.set_option("graph", 0)
 cel.set_option("lanes", 2)
