@@ -327,7 +327,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps (default 3; verify_mul 8: each of its two lanes "
+                         "captures its launch graph on its second or third call)")
     ap.add_argument("--workload", choices=["svd", "verify_mul"], default="svd")
     ap.add_argument("--n", type=int, default=None, help="rows (default 1024 svd, 256 verify_mul)")
     ap.add_argument("--m", type=int, default=None)
@@ -370,6 +372,8 @@ def main():
         return launch_ranks(args.gpus)
 
     svd = args.workload == "svd"
+    if args.warmup is None:
+        args.warmup = 3 if svd else 8
     N = args.n or (1024 if svd else 256)
     M = args.m or N
     P = args.p or (63 if svd else 32)
