@@ -547,8 +547,6 @@ struct svdw_ctx {
     DBuf qfold;                             // k_quantize_multi's fold counters + group maxima
     // second stream: GEMMs overlap the HBM-bound stages; third: phase 1
     hipStream_t st2 = nullptr;
-    bool st2_hi = false;                    // st2 is the high-priority stream
-    int gemm_prio = -1;                     // "gemm_priority": -1 auto, 0 normal, 1 high
     hipStream_t st3 = nullptr;
     hipStream_t st_cell = nullptr;          // the cell stream proper (st is swapped at times)
     hipEvent_t xev[4] = {};                 // svdw_stream_wait / _signal (caller's stream)
@@ -684,32 +682,10 @@ static void dep_wait(svdw_ctx*, hipStream_t s, hipEvent_t e) {
 // The second stream at high or normal dispatch priority: on a change the queued
 // work drains and st2 is re-created (one second stream at a time: an idle twin
 // kept beside it measured 2.7x slower at 512^2 under bench.py's event profiler).
-static void pick_st2(svdw_ctx* c, bool hi) {
-    if (c->dry || hi == c->st2_hi) return;
-    sync(c);
-    hipStream_t s;
-    if (hi) {
-        int lo = 0, top = 0;
-        hipck(hipDeviceGetStreamPriorityRange(&lo, &top), "hipDeviceGetStreamPriorityRange");
-        hipck(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, top), "hipStreamCreateWithPriority");
-    } else {
-        hipck(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
-    }
-    hipck(hipStreamDestroy(c->st2), "hipStreamDestroy");
-    c->st2 = s;
-    c->st2_hi = hi;
-}
-// gemm_priority auto (-1): high for unsharded witnesses with 512 <= max(N, M)
-// < 1024, where the product chain on st2 is the critical path (the cell stream
-// idles ~40 us waiting for the combine at 512^2 P=32). bench.py lines, same box
-// (tools/probes/check_gp2.sh): 512^2 P=32 0.424 -> 0.416 ms; 256^2 P=32 0.189 -> 0.194
-// ms (so off below 512); 1024^2 and 2048 x 1024 within 0.5 % (tools/probes/probe_gp.sh);
-// 8-way shard rank 0.378 -> 0.383 ms (tools/probes/probe_r02b.sh), off when sharded.
-static void apply_gemm_prio(svdw_ctx* c, uint32_t N, uint32_t M) {
-    const bool sharded_ctx = c->shard_world > 1;
-    const uint32_t mx = std::max(N, M);
-    pick_st2(c, c->gemm_prio > 0 || (c->gemm_prio < 0 && !sharded_ctx && mx >= 512 && mx < 1024));
-}
+// (Round 4 removed "gemm_priority", a high-priority second stream at 512 <=
+// max(N, M) < 1024: +2 % in round 2's tools/ab.py runs, but bench.py at 512^2
+// P=32 measured 0.68 ms with it and 0.41 ms without -- the stream created
+// mid-run shares a hardware queue with the cell stream, GPU_MAX_HW_QUEUES = 4.)
 static bool same_cells(const svdw_mat& a, const svdw_mat& b) {
     if (a.phase != b.phase || a.off != b.off) return false;
     return (a.rows == b.rows && a.cols == b.cols && a.rs == b.rs && a.cs == b.cs) ||
@@ -2564,7 +2540,6 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     host_mark(c, "svd_witness start");
     clear_streams(c);
     c->dep_next = 0;
-    if (!c->dry) apply_gemm_prio(c, N, M);
     c->prelaunched = false;
     c->prod_on_cell = false;
     c->gemm_batched = false;
@@ -3108,11 +3083,11 @@ static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
     const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->gemm_crt, s->res_f64,
                          s->phase1_overlap, s->prod_cell, s->hold_us, s->rlc_prefix, s->p1_at,
                          s->f64_views, s->overlap, s->stage_batch, s->graph_vm, s->pipeline,
-                         s->shard_rank, s->shard_world, s->prof, s->gemm_prio, s->host_trace};
+                         s->shard_rank, s->shard_world, s->prof, s->host_trace};
     const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->gemm_crt, d->res_f64,
                          d->phase1_overlap, d->prod_cell, d->hold_us, d->rlc_prefix, d->p1_at,
                          d->f64_views, d->overlap, d->stage_batch, d->graph_vm, d->pipeline,
-                         d->shard_rank, d->shard_world, d->prof, d->gemm_prio, d->host_trace};
+                         d->shard_rank, d->shard_world, d->prof, d->host_trace};
     if (!memcmp(a, b, sizeof a) && d->prof_filter == s->prof_filter) return;
     d->gemm_impl = s->gemm_impl; d->stage_flags = s->stage_flags; d->stage_elems = s->stage_elems;
     d->gemm_crt = s->gemm_crt; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
@@ -3120,7 +3095,7 @@ static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
     d->p1_at = s->p1_at; d->f64_views = s->f64_views; d->overlap = s->overlap;
     d->stage_batch = s->stage_batch; d->graph_vm = s->graph_vm; d->pipeline = s->pipeline;
     d->shard_rank = s->shard_rank; d->shard_world = s->shard_world; d->prof = s->prof;
-    d->gemm_prio = s->gemm_prio; d->host_trace = s->host_trace; d->prof_filter = s->prof_filter;
+    d->host_trace = s->host_trace; d->prof_filter = s->prof_filter;
     ++d->epoch;
 }
 // "lanes": exchange this state with the lane's (created on first use).
@@ -4359,11 +4334,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             REQUIRE(value >= 16 && value <= 256 && value % 16 == 0,
                     "stage_elems: a multiple of 16 in [16, 256]");
             c->stage_elems = (uint32_t)value;
-        } else if (n == "gemm_priority") {
-            // second (GEMM) stream priority: -1 auto (see apply_gemm_prio), 0 normal, 1 high
-            REQUIRE(value >= -1 && value <= 1, "gemm_priority: -1, 0 or 1");
-            c->gemm_prio = (int)value;
-            if (value >= 0) pick_st2(c, value == 1);
         } else if (n == "prod_cell") {
             REQUIRE(value >= -1 && value <= 1, "prod_cell: -1, 0 or 1");
             c->prod_cell = (int)value;

@@ -243,7 +243,7 @@ int svdw_verify_mul_witness(svdw_ctx* ctx, const double* a, const double* b, uin
 #define SVDW_GEMM_MFMA 0
 #define SVDW_GEMM_VALU 1
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
-/* Options (svdw_set_option; 16 of them). Tuning knobs, bit-identical results
+/* Options (svdw_set_option; 15 of them). Tuning knobs, bit-identical results
  * for every value, defaults first:
  *   "gemm_impl" 0 | 1; "gemm_crt" 1 | 0 (CRT or digit-plane matrix-core GEMM);
  *   "overlap" 1 | 0 (the three check_svd_phase0 products run ahead on a second
@@ -253,9 +253,7 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   a row-sharded context and when max(N, M) < 1024); "p1_at" -1 | 0 | 1 | 2 | 3
  *   (with phase 1 on the third stream: queued after the first 0 / 1 / 2
  *   phase-0 stages, 3 after all of phase 0; -1: 0 on a rank of a >= 4-way shard, 3 of a
- *   2-3-way shard, else 1); "gemm_priority" -1 | 0 | 1 (second stream priority:
- *   -1 auto = high for unsharded witnesses with 512 <= max(N, M) < 1024, where
- *   the product chain is the critical path; 0 normal; 1 high);
+ *   2-3-way shard, else 1);
  *   "stage_elems" 256 (elements per stage block, multiple of 16 in [16, 256]);
  *   "f64_views" 1 | 0 (svd_witness / verify_mul_witness with device inputs:
  *   stages and row scans read the loaded matrices from the f64 inputs,

@@ -197,7 +197,7 @@ def test_crt_gemm_tiles_parity(gpu_ctx_factory, N, M, P, world, device):
 
 @pytest.mark.parametrize("opts", [{"gemm_crt": 0}, {"stage_elems": 64}, {"stage_elems": 192},
                                   {"phase1_overlap": 0}, {"phase1_overlap": 2},
-                                  {"overlap": 0}, {"gemm_priority": 1}, {"gemm_priority": 0},
+                                  {"overlap": 0},
                                   {"stage_batch": 0}, {"pipeline": 0}, {"pipeline": 0, "phase1_overlap": 2},
                                   {"gemm_impl": 1}, {"res_f64": 0}, {"f64_views": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
@@ -212,22 +212,6 @@ def test_tuning_options_parity(gpu_ctx_factory, opts):
     hs.svd_witness(ctx, m, u, v, d, g)
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
     _assert_streams(ctx, a0, l0, a1)
-
-
-def test_gemm_priority_switch_parity(gpu_ctx_factory):
-    """The auto product-stream priority (high below 1024, normal from 1024 on)
-    switches st2 between two streams across witnesses of one context; every
-    witness stays bit-identical to the oracle, whichever stream it ran on."""
-    import halo2_svd041_amd as hs
-    P = 63
-    ctx = gpu_ctx_factory(P)
-    for (N, M, seed, prio) in [(45, 37, 4, -1), (33, 52, 5, 0), (40, 40, 6, -1), (38, 29, 7, 1)]:
-        ctx.set_option("gemm_priority", prio)
-        m, u, d, v = gen_svd_input(N, M, seed=seed)
-        g = gamma_for(seed)
-        hs.svd_witness(ctx, m, u, v, d, g)
-        a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
-        _assert_streams(ctx, a0, l0, a1)
 
 
 def test_modular_verify_mul_parity(gpu_ctx_factory):
