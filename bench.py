@@ -174,12 +174,15 @@ def pmc_traffic(kernel, workload, N, M, P, LB, world=1, rank=0):
                 s = json.load(fh)
         except (OSError, ValueError):
             continue
-        if (s.get("config") == want and s.get("workload", "svd") == workload
-                and kernel in s.get("kernels", {})):
+        ks = s.get("kernels", {})
+        # the profiler's family name (k_matvec_scan) or rocprof's kernel name (k_matvec_scan_dpp)
+        pre = [k for k in ks if k.startswith(kernel + "_")]
+        key = kernel if kernel in ks else (pre[0] if len(pre) == 1 else None)
+        if s.get("config") == want and s.get("workload", "svd") == workload and key:
             if s.get("sources_sha16") != sha:
                 stale.append(os.path.relpath(f, ROOT))
                 continue
-            return s["kernels"][kernel]["traffic_per_launch"], os.path.relpath(f, ROOT), None
+            return ks[key]["traffic_per_launch"], os.path.relpath(f, ROOT), None
     note = ("no PMC summary of these kernel sources (sha16 %s)" % sha
             + ("; refused summaries of other sources: %s" % ", ".join(stale) if stale else ""))
     return None, None, note
