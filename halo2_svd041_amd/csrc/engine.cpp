@@ -2715,10 +2715,7 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     // 1 % slower.
     const bool p1_small = std::max(N, M) < 1024;
     // (pipelined: st2 carries the diff and ids after the bounds, phase 1 goes to st3)
-    // (3: mode 1 in every case -- pipelined, phase 1 then follows the diff and
-    // ids on st2, every cell-writing launch of the call on one stream)
-    const int p1mode = c->phase1_overlap == 3 ? 1
-                       : c->phase1_overlap == 1 && (sharded(c) || p1_small || c->in_pipe) ? 2 : c->phase1_overlap;
+    const int p1mode = c->phase1_overlap == 1 && (sharded(c) || p1_small || c->in_pipe) ? 2 : c->phase1_overlap;
     bool p1_queued = false;
     auto queue_phase1 = [&](const svdw_svd_payload& pl, bool overlap) {
         const bool p1_overlap = p1mode && overlap;
@@ -4341,7 +4338,7 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             REQUIRE(value >= -1 && value <= 1, "prod_cell: -1, 0 or 1");
             c->prod_cell = (int)value;
         } else if (n == "phase1_overlap") {
-            REQUIRE(value >= 0 && value <= 3, "phase1_overlap: 0, 1, 2 or 3");
+            REQUIRE(value >= 0 && value <= 2, "phase1_overlap: 0, 1 or 2");
             c->phase1_overlap = (int)value;
         } else if (n == "hold_us") {         // timing aid: GPU-only schedule of a witness
             REQUIRE(value >= 0 && value <= 100000, "hold_us: 0..100000");

@@ -198,7 +198,7 @@ def test_crt_gemm_tiles_parity(gpu_ctx_factory, N, M, P, world, device):
 @pytest.mark.parametrize("opts", [{"gemm_crt": 0}, {"stage_elems": 64}, {"stage_elems": 192},
                                   {"phase1_overlap": 0}, {"phase1_overlap": 2},
                                   {"overlap": 0},
-                                  {"stage_batch": 0}, {"pipeline": 0}, {"pipeline": 0, "phase1_overlap": 2}, {"phase1_overlap": 3},
+                                  {"stage_batch": 0}, {"pipeline": 0}, {"pipeline": 0, "phase1_overlap": 2},
                                   {"gemm_impl": 1}, {"res_f64": 0}, {"f64_views": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
