@@ -3063,13 +3063,7 @@ static void ctx_release(svdw_ctx* c) {
 // Device state of a new context: its three streams, the pinned bit words, events.
 static void ctx_init_device(svdw_ctx* c) {
     hipError_t e = hipSetDevice(c->device);
-    if (const char* pr = getenv("SVDW_CELL_PRIORITY"); pr && atoi(pr) > 0) {
-        int lo = 0, top = 0;
-        if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&lo, &top);
-        if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, top);
-    } else if (e == hipSuccess) {
-        e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
-    }
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
     c->st_cell = c->st;
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->st2, hipStreamNonBlocking);
     // the third stream exists from the start: one created lazily inside a
