@@ -557,6 +557,8 @@ struct svdw_ctx {
         hipStream_t st;                     // the stream it was launched on
     };
     std::vector<PreGemm> pre;               // GEMMs launched ahead on st2, in append order
+    hipStream_t pre_wait_st = nullptr;      // the last (stream, event) waited on for them
+    hipEvent_t pre_wait_ev = nullptr;
     std::vector<svdw_region> layout;        // every appended region of the current witness
     // per region: gate offsets within one element's cells and cells per element
     // (program regions; empty otherwise; svdw_check_gates)
@@ -679,9 +681,6 @@ static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
 static void dep_wait(svdw_ctx*, hipStream_t s, hipEvent_t e) {
     hipck(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
 }
-// The second stream at high or normal dispatch priority: on a change the queued
-// work drains and st2 is re-created (one second stream at a time: an idle twin
-// kept beside it measured 2.7x slower at 512^2 under bench.py's event profiler).
 // (Round 4 removed "gemm_priority", a high-priority second stream at 512 <=
 // max(N, M) < 1024: +2 % in round 2's tools/ab.py runs, but bench.py at 512^2
 // P=32 measured 0.68 ms with it and 0.41 ms without -- the stream created
@@ -1688,9 +1687,13 @@ static svdw_mat honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_ma
     if (c->dry) return cs;
     if (!c->pre.empty()) {
         if (c->pre.front().off != off) fail(SVDW_EDEVICE, "internal: pre-launched GEMM offset mismatch");
-        // (launched on this very stream: already ordered)
-        if (c->pre.front().st != c->st)
+        // (launched on this very stream: already ordered; the three batched
+        // products share one event: one wait per stream)
+        if (c->pre.front().st != c->st && !(c->pre_wait_st == c->st && c->pre_wait_ev == c->pre.front().ev)) {
             dep_wait(c, c->st, c->pre.front().ev);
+            c->pre_wait_st = c->st;
+            c->pre_wait_ev = c->pre.front().ev;
+        }
         c->pre.erase(c->pre.begin());
         return cs;
     }
@@ -2546,6 +2549,8 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     c->gemm_done.clear();
     c->wait_before_cs.clear();
     c->pre.clear();
+    c->pre_wait_st = nullptr;
+    c->pre_wait_ev = nullptr;
     c->in_pipe = false;
     struct PipeGuard {                     // an exception inside a pipelined call: its
         svdw_ctx* c;                       // tail is whatever reached st2 / st3 -- join it
@@ -2588,10 +2593,13 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
             // (st2's first stages write cells that call's st3 scans read)
             for (int p = 0; p < 2; ++p) std::swap(c->ph[p], c->alt[p]);
             clear_streams(c);
+            // (tail_ev[.][0] was recorded on st2, [.][1] on st3: a stream does not
+            // wait for its own earlier work)
             if (c->tail_valid[c->pipe_par])
                 for (hipStream_t t : {c->st, c->st2, c->st3})
                     for (int k = 0; k < 2; ++k)
-                        hipck(hipStreamWaitEvent(t, c->tail_ev[c->pipe_par][k], 0), "hipStreamWaitEvent");
+                        if (t != (k ? c->st3 : c->st2))
+                            hipck(hipStreamWaitEvent(t, c->tail_ev[c->pipe_par][k], 0), "hipStreamWaitEvent");
             if (c->xwait_side) {                  // the caller's stream (svdw_stream_wait)
                 for (hipStream_t t : {c->st2, c->st3})
                     hipck(hipStreamWaitEvent(t, c->xwait_side, 0), "hipStreamWaitEvent");
@@ -2824,6 +2832,8 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
     c->gemm_done.clear();
     c->wait_before_cs.clear();
     c->pre.clear();
+    c->pre_wait_st = nullptr;
+    c->pre_wait_ev = nullptr;
     if (!c->dry) {
         const std::vector<uint64_t> key = {0x766d77ull, N, K, M};      // sizes from the dry plan
         if (key != c->plan_key) {
@@ -3400,6 +3410,8 @@ int svdw_ctx_reset(svdw_ctx* c) {
         sync(c);
         clear_streams(c);
         c->pre.clear();
+        c->pre_wait_st = nullptr;
+        c->pre_wait_ev = nullptr;
     });
 }
 int svdw_reserve(svdw_ctx* c, uint32_t phase, uint64_t na, uint64_t nl) {
