@@ -2459,9 +2459,10 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     DView udv;
     EqCell udpad;
     // products on the cell stream: u.d (all the diff needs from st2) in a launch
-    // ahead of the bounds, so the cell stream waits for it alone
+    // ahead of the bounds, so the cell stream waits for it alone (pipelined, the
+    // diff follows on st2 itself: u.d shares the bounds' launch)
     if (r == M) {
-        c->stage_front = pc;
+        c->stage_front = pc && !c->in_pipe;
         const svdw_mat ud = mat_times_diag_mat(c, u, d);
         c->stage_front = false;
         udv = view_of(c, ud);
