@@ -168,6 +168,7 @@ SIGNATURES = {
     "svdw_parse_svd_input": (_i32, [ct.c_char_p, _u64, _i32, ct.POINTER(InputDims), _P, _P, _P, _P]),
     "svdw_rlc_trace": (_i32, [_P, _P, _P, ct.POINTER(ct.c_uint32)]),
     "svdw_verify_mul_witness": (_i32, [_P, _P, _P, _u32, _u32, _u32, _i32, _P, ct.POINTER(Counts)]),
+    "svdw_verify_mul_witness_on": (_i32, [_P, _P, _P, _P, _u32, _u32, _u32, _P, ct.POINTER(Counts)]),
     "svdw_parse_svd_input_device": (_i32, [_P, _P, _u64, _i32, ct.POINTER(InputDims), _P, _P, _P, _P]),
     "svdw_shard_segments": (_i32, [_P, ct.POINTER(Segment), _u64, _u64p]),
     "svdw_layout": (_i32, [_P, ct.POINTER(Region), _u64, _u64p]),

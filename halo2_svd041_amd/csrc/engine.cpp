@@ -3132,11 +3132,21 @@ static void lane_switch(svdw_ctx* c) {
     std::swap(c->lane, L->lane);                  // (the handle keeps the lane and the option)
     std::swap(c->lanes, L->lanes);
 }
+static hipEvent_t xevent(svdw_ctx* c, int i);
+// caller: the caller's stream (svdw_verify_mul_witness_on), waited for by the
+// state that runs the call (after the lane switch)
 static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const double* b, uint32_t N,
-                                          uint32_t K, uint32_t M, bool on_device, const Fr& gamma) {
+                                          uint32_t K, uint32_t M, bool on_device, const Fr& gamma,
+                                          hipStream_t caller = nullptr, bool has_caller = false) {
     const bool plain = on_device && !c->dry && !c->prof && !c->hold_us && !sharded(c) && N >= 1 && K >= 1 &&
                        M >= 1;
     if (plain && c->lanes > 1) lane_switch(c);
+    if (has_caller && !c->dry) {
+        const hipEvent_t e = xevent(c, 0);
+        hipck(hipEventRecord(e, caller), "hipEventRecord");
+        hipck(hipStreamWaitEvent(c->st, e, 0), "hipStreamWaitEvent");
+        c->xwait_side = e;                        // (st2 / st3: through st, see after_previous)
+    }
     const bool usable = c->graph_vm && plain;
     if (!usable) {
         vmg_drop(c);
@@ -3749,6 +3759,16 @@ int svdw_verify_mul_witness(svdw_ctx* c, const double* a, const double* b, uint3
         REQUIRE(c && gamma, "null argument");
         REQUIRE(c->dry || (a && b), "null input matrix");
         svdw_counts k = verify_mul_witness_api(c, a, b, N, K, M, on_device != 0, fr_from_words(gamma));
+        if (counts) *counts = k;
+    });
+}
+int svdw_verify_mul_witness_on(svdw_ctx* c, void* stream, const double* a, const double* b, uint32_t N,
+                               uint32_t K, uint32_t M, const uint64_t gamma[4], svdw_counts* counts) {
+    return guarded([&] {
+        REQUIRE(c && gamma, "null argument");
+        REQUIRE(c->dry || (a && b), "null input matrix");
+        svdw_counts k = verify_mul_witness_api(c, a, b, N, K, M, true, fr_from_words(gamma), (hipStream_t)stream,
+                                               true);
         if (counts) *counts = k;
     });
 }

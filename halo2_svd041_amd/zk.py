@@ -620,8 +620,8 @@ def verify_mul_witness(ctx: Context, a, b, gamma: int) -> dict:
         (N, K), M = a.shape, b.shape[1]
         if b.shape[0] != K:
             raise SvdwError(-1, "verify_mul_witness: a.num_col != b.num_rows")
-        _after_torch(ctx)
-        check(lib().svdw_verify_mul_witness(ctx.handle, *dps, N, K, M, 1, g, ct.byref(cnt)))
+        # (the hand-off to torch's stream inside the call, on the state that runs it)
+        check(lib().svdw_verify_mul_witness_on(ctx.handle, _torch_stream(ctx), *dps, N, K, M, g, ct.byref(cnt)))
     else:
         arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (a, b)]
         (N, K), M = arrs[0].shape, arrs[1].shape[1]

@@ -229,6 +229,12 @@ int svdw_svd_witness(svdw_ctx* ctx, const double* m, const double* u, const doub
  * on_device). */
 int svdw_verify_mul_witness(svdw_ctx* ctx, const double* a, const double* b, uint32_t N, uint32_t K,
                             uint32_t M, int on_device, const uint64_t gamma[4], svdw_counts* counts);
+/* svdw_verify_mul_witness with device inputs, ordered after the work queued
+ * so far on the caller's stream `stream` (svdw_stream_wait inside the call, on
+ * the context state that runs it -- with "lanes" 2 the other one): one call
+ * and one hand-off wait instead of two calls and a wait per state. */
+int svdw_verify_mul_witness_on(svdw_ctx* ctx, void* stream, const double* a, const double* b, uint32_t N,
+                               uint32_t K, uint32_t M, const uint64_t gamma[4], svdw_counts* counts);
 /* Exact integer GEMM of honest_prover_mat_mul (the integer sum of quantized
  * products, reduced mod p once). Matrix-core paths (SVDW_GEMM_MFMA, default):
  *   - multi-modular / CRT (option "gemm_crt" 1, default): balanced residues

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Config 2: does recording the caller-stream hand-off event on torch's default
-(null) stream serialize consecutive calls? lanes 1 / 2, with torch's current
-stream the default stream or a side stream, 300 calls each, interleaved.
+"""Config 2: the caller-stream hand-off. lanes 1 / 2; torch's current stream the
+default stream or a side stream; the hand-off as its own call
+(svdw_stream_wait, "old") or inside svdw_verify_mul_witness_on ("on").
+300 calls each, interleaved.
 
     python tools/probes/vmstream.py
 """
@@ -34,10 +35,33 @@ for lanes in (1, 2):
     c.sync()
     ctxs[lanes] = c
 torch.cuda.synchronize()
+import ctypes as ct
+from halo2_svd041_amd import zk
+from halo2_svd041_amd._lib import lib
+
+
+def old_call(c, g):
+    cnt = zk.Counts()
+    zk._after_torch(c)
+    zk.check(lib().svdw_verify_mul_witness(c.handle, ta.data_ptr(), tb.data_ptr(), N, N, N, 1,
+                                           zk._words_arg(g), ct.byref(cnt)))
+
+
 for rnd in range(3):
     for lanes in (1, 2):
+        c = ctxs[lanes]
+        torch.cuda.synchronize()
+        c.sync()
+        t0 = time.perf_counter()
+        for k in range(300):
+            old_call(c, gs[k])
+        t1 = time.perf_counter()
+        c.sync()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        out.setdefault(f"lanes{lanes}_default_old", []).append(
+            {"host_ms": round((t1 - t0) / 300 * 1e3, 4), "step_ms": round((t2 - t0) / 300 * 1e3, 4)})
         for sname in ("default", "side"):
-            c = ctxs[lanes]
             torch.cuda.synchronize()
             c.sync()
             if sname == "side":
