@@ -2230,7 +2230,6 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
         // own residue scratch): one step of the st2 chain instead of three
         CrtBatch b;
         memset(&b, 0, sizeof b);
-        if (const char* gg = getenv("SVDW_GEMM_GRID")) b.max_blocks = (uint32_t)atoi(gg);
         size_t rbytes[3], rtot = 0;
         for (int g = 0; g < 3; ++g) {
             rbytes[g] = crt_scratch_bytes(std::max<uint32_t>((uint32_t)(rr1[g] - rr0[g]), 1), B[g].cols);

@@ -1691,26 +1691,22 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
             cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk;
         total += cnt[j];
     }
-    // units of XCD x = blockIdx & 7: [x * per, (x + 1) * per); a capped grid
-    // (max_blocks) walks them in strides of gridDim / 8
-    const uint32_t per = (total + 7) / 8, kstep = gridDim.x >> 3;
-    for (uint32_t k = blockIdx.x >> 3; k < per; k += kstep) {
-        uint32_t u = (blockIdx.x & 7) * per + k;
-        if (u >= total) break;
-        uint32_t j = 0;
+    const uint32_t per = (total + 7) / 8, k = blockIdx.x >> 3;
+    if (k >= per) return;
+    uint32_t u = (blockIdx.x & 7) * per + k;
+    if (u >= total) return;
+    uint32_t j = 0;
 #pragma unroll
-        for (int q = 0; q < kMaxCrtJobs - 1; ++q)
-            if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
-        const CrtJob& q = b.job[j];
-        const uint32_t mod = u / q.nblk, t = u - mod * q.nblk;
-        uint32_t bi, bj;
-        crt_tile_rc(q, t, &bi, &bj);
-        uint64_t tp1 = 0, tp2 = 0;
-        crt_gemm_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.nblk, t,
-                      q.R, bi, bj, (int)mod, S, tp1, tp2);
-        trace_block(t0, tp1, tp2);
-        __syncthreads();                                  // (S is the next tile's)
-    }
+    for (int q = 0; q < kMaxCrtJobs - 1; ++q)
+        if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
+    const CrtJob& q = b.job[j];
+    const uint32_t mod = u / q.nblk, t = u - mod * q.nblk;
+    uint32_t bi, bj;
+    crt_tile_rc(q, t, &bi, &bj);
+    uint64_t tp1 = 0, tp2 = 0;
+    crt_gemm_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.nblk, t,
+                  q.R, bi, bj, (int)mod, S, tp1, tp2);
+    trace_block(t0, tp1, tp2);
 }
 // C from its n residues, written as canonical Fr to out[i*ors + j*ocs]: one
 // element per thread in the GEMM's tile order (each block one 256-element
@@ -1812,9 +1808,7 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
         q.cblk0 = cblocks;
         cblocks += q.nblk * (kCrtTileBytes / 256);
     }
-    uint32_t grid = (units + 7) / 8 * 8;
-    if (b.max_blocks && grid > b.max_blocks) grid = std::max(8u, b.max_blocks / 8 * 8);
-    hipLaunchKernelGGL(k_gemm_crt_multi, dim3(grid), dim3(256), 0, st, b);
+    hipLaunchKernelGGL(k_gemm_crt_multi, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_crt_combine_multi, dim3((cblocks + 7) / 8 * 8), dim3(256), 0, st, b, cblocks);

@@ -345,7 +345,6 @@ struct CrtJob {
 struct CrtBatch {
     CrtJob job[kMaxCrtJobs];
     uint32_t njobs;
-    uint32_t max_blocks;                 // GEMM grid cap (multiple of 8; blocks loop over units); 0: none
 };
 // R sized crt_scratch_bytes per job
 hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st);
