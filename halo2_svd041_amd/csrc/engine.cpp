@@ -2387,9 +2387,8 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         // The d checks (three latency-bound stages over r elements) depend on d
         // only: with the products queued ahead they go behind them on st2, off
         // the cell stream, which starts on the u / v bounds at once. Pipelined
-        // (st2 then carries every stage of the call back to back), on st3
-        // ahead of phase 1: their dependent second launch would otherwise sit
-        // between the bounds and the diff.
+        // (st2 then carries every stage of the call back to back, st3 phase 1),
+        // on the cell stream behind the products, its least loaded stream.
         struct Swap {
             svdw_ctx* c;
             hipStream_t* other;
@@ -2398,7 +2397,7 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
             }
             ~Swap() { if (other) std::swap(c->st, *other); }
             bool on() const { return other != nullptr; }
-        } sw(c, c->overlap && known_bits && !c->dry && c->bits_pending, c->in_pipe && c->st3);
+        } sw(c, c->overlap && known_bits && !c->dry && c->bits_pending && !c->in_pipe, false);
         // d loaded -- unless every load these stages (and the bounds and u.d
         // queued behind them with the products on the cell stream) read comes
         // from the registered f64 inputs (f64_view): then st2 starts at once
