@@ -2030,27 +2030,18 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
     };
     bool all_f64 = true;
     for (int i = 0; i < n && all_f64; ++i) all_f64 = f64_of(vm[i].b) != nullptr;
-    // pipelined svd_witness: the column sums and vector prep go on the cell
-    // stream (behind the products and d checks, its least loaded stream) and
-    // the scans here wait for them; their outputs alternate by call parity (the
-    // previous call's scans may still read the other half)
-    const bool col_cell = c->in_pipe && all_f64 && c->st != c->st_cell;
-    const int wo = col_cell ? kMaxVerifyBatch * c->pipe_par : 0;
-    static_assert(2 * kMaxVerifyBatch <= kMaxScanJobs, "b.g buffers per parity");
     // launch order != append order: the b and a.(b.g) scans need only the
     // operands, the c_s scans wait for the products when those run elsewhere
     Scans bs_, as_;
     auto add_b = [&](Scans& S, int i) -> ScanJob& { return add_job(S, vm[i].b, pl[i].bv, gpc, gtab, c->gp_len); };
     auto add_a = [&](Scans& S, int i) {
-        add_job(S, vm[i].a, pl[i].abv, (const Fr*)c->wbc[wo + src[i]].p, wt[i], vm[i].b.rows);
+        add_job(S, vm[i].a, pl[i].abv, (const Fr*)c->wbc[src[i]].p, wt[i], vm[i].b.rows);
     };
     if (all_f64) {
         // every entry of b.g from the f64 rows of X (quantized in registers),
         // column-parallel and coalesced: one launch for the distinct b's, then
         // the slices' sums folded into each vector's table (k_vec_prep_sum);
         // the b and a.(b.g) scans are then independent: one launch
-        hipStream_t cs = col_cell ? c->st_cell : c->st;
-        if (col_cell && c->gp_ev && c->gp_st != cs) dep_wait(c, cs, c->gp_ev);   // (gamma's tables)
         ColBatch cb;
         memset(&cb, 0, sizeof cb);
         cb.tab = gtab;
@@ -2072,25 +2063,23 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
             ptot += (size_t)colsum_slices(j.R) * j.C;
             slot[i] = (int)cb.njobs++;
         }
-        ensure_buf(c, c->colpart, (col_cell ? 2 : 1) * ptot * sizeof(Fr));
-        const size_t po = col_cell ? (size_t)c->pipe_par * ptot : 0;
-        for (uint32_t q = 0; q < cb.njobs; ++q) cb.job[q].part = (Fr*)c->colpart.p + po + poff[q];
+        ensure_buf(c, c->colpart, ptot * sizeof(Fr));
+        for (uint32_t q = 0; q < cb.njobs; ++q) cb.job[q].part = (Fr*)c->colpart.p + poff[q];
         {
-            ProfScope ps(c, cs, "k_colsum_f64", 0, 0);
-            hipck(launch_colsum_f64(cb, (int)c->P, cs), "k_colsum_f64");
+            ProfScope ps(c, c->st, "k_colsum_f64", 0, 0);
+            hipck(launch_colsum_f64(cb, (int)c->P, c->st), "k_colsum_f64");
         }
         for (int i = 0; i < n; ++i) {
             if (src[i] != i) { wt[i] = wt[src[i]]; continue; }
             const uint32_t L = vm[i].b.rows;
-            ensure_buf(c, c->wbc[wo + i], (size_t)L * sizeof(Fr));
-            ensure_buf(c, c->wbt[wo + i], tab_len(L) * sizeof(Fr));
-            ProfScope ps(c, cs, "k_vec_prep", 32.0 * L * (2 + tab_len(1)), 0);
+            ensure_buf(c, c->wbc[i], (size_t)L * sizeof(Fr));
+            ensure_buf(c, c->wbt[i], tab_len(L) * sizeof(Fr));
+            ProfScope ps(c, c->st, "k_vec_prep", 32.0 * L * (2 + tab_len(1)), 0);
             hipck(launch_vec_prep_sum(cb.job[slot[i]].part, colsum_slices(cb.job[slot[i]].R), L,
-                                      (Fr*)c->wbc[wo + i].p, (Fr*)c->wbt[wo + i].p, scale_tab(), cs),
+                                      (Fr*)c->wbc[i].p, (Fr*)c->wbt[i].p, scale_tab(), c->st),
                   "k_vec_prep_sum");
-            wt[i] = (const Fr*)c->wbt[wo + i].p;
+            wt[i] = (const Fr*)c->wbt[i].p;
         }
-        if (col_cell) stream_dep(c, cs, c->st);
         for (int i = 0; i < n; ++i) add_b(bs_, i);
         for (int i = 0; i < n; ++i) add_a(bs_, i);
         launch(bs_, "k_matvec_scan:ba");
