@@ -2069,16 +2069,24 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
             ProfScope ps(c, c->st, "k_colsum_f64", 0, 0);
             hipck(launch_colsum_f64(cb, (int)c->P, c->st), "k_colsum_f64");
         }
+        // the distinct b's vectors in one launch
+        VecPrepBatch vp;
+        memset(&vp, 0, sizeof vp);
+        double vbytes = 0;
         for (int i = 0; i < n; ++i) {
             if (src[i] != i) { wt[i] = wt[src[i]]; continue; }
             const uint32_t L = vm[i].b.rows;
             ensure_buf(c, c->wbc[i], (size_t)L * sizeof(Fr));
             ensure_buf(c, c->wbt[i], tab_len(L) * sizeof(Fr));
-            ProfScope ps(c, c->st, "k_vec_prep", 32.0 * L * (2 + tab_len(1)), 0);
-            hipck(launch_vec_prep_sum(cb.job[slot[i]].part, colsum_slices(cb.job[slot[i]].R), L,
-                                      (Fr*)c->wbc[i].p, (Fr*)c->wbt[i].p, scale_tab(), c->st),
-                  "k_vec_prep_sum");
+            REQUIRE(vp.njobs < (uint32_t)kMaxColJobs, "internal: too many distinct b for k_vec_prep_sum");
+            vp.job[vp.njobs++] = VecPrepJob{cb.job[slot[i]].part, colsum_slices(cb.job[slot[i]].R), L,
+                                            (Fr*)c->wbc[i].p, (Fr*)c->wbt[i].p, 0};
+            vbytes += 32.0 * L * (2 + tab_len(1));
             wt[i] = (const Fr*)c->wbt[i].p;
+        }
+        {
+            ProfScope ps(c, c->st, "k_vec_prep", vbytes, 0);
+            hipck(launch_vec_prep_sum_multi(vp, scale_tab(), c->st), "k_vec_prep_sum_multi");
         }
         for (int i = 0; i < n; ++i) add_b(bs_, i);
         for (int i = 0; i < n; ++i) add_a(bs_, i);

@@ -2777,6 +2777,48 @@ __global__ __launch_bounds__(256) void k_vec_prep_sum(const Fr* __restrict__ par
     }
     tab_store(wc, tab, L, j, blockIdx.y, v, f);
 }
+// k_vec_prep_sum over the jobs of a batch (block x: job by blk0 ranges)
+__global__ __launch_bounds__(256) void k_vec_prep_sum_multi(const VecPrepBatch b, const ScaleTab f) {
+    uint32_t q = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxColJobs; ++k) q += (uint32_t)k < b.njobs && blockIdx.x >= b.job[k].blk0;
+    const Fr* part = b.job[0].part;
+    uint32_t S = b.job[0].S, L = b.job[0].L, b0 = b.job[0].blk0;
+    Fr* wc = b.job[0].wc;
+    Fr* tab = b.job[0].tab;
+#pragma unroll
+    for (int k = 1; k < kMaxColJobs; ++k)                 // selects, not a dynamic index into the argument
+        if (q == (uint32_t)k) {
+            part = b.job[k].part; S = b.job[k].S; L = b.job[k].L; b0 = b.job[k].blk0; wc = b.job[k].wc;
+            tab = b.job[k].tab;
+        }
+    const uint32_t j = (blockIdx.x - b0) * blockDim.x + threadIdx.x;
+    if (j >= L) return;
+    Fr v = fr_zero();
+    for (uint32_t s0 = 0; s0 < S; s0 += kColPartBatch) {
+        Fr p[kColPartBatch];
+#pragma unroll
+        for (int s = 0; s < kColPartBatch; ++s)
+            p[s] = s0 + s < S ? ld_fr(part + (uint64_t)(s0 + s) * L + j) : fr_zero();
+#pragma unroll
+        for (int s = 0; s < kColPartBatch; ++s) v = fr_add(v, p[s]);
+    }
+    tab_store(wc, tab, L, j, blockIdx.y, v, f);
+}
+hipError_t launch_vec_prep_sum_multi(const VecPrepBatch& b0, const ScaleTab& f, hipStream_t st) {
+    if (!b0.njobs || b0.njobs > (uint32_t)kMaxColJobs) return hipErrorInvalidValue;
+    VecPrepBatch b = b0;
+    uint32_t blocks = 0;
+    for (uint32_t q = 0; q < b.njobs; ++q) {
+        if (!b.job[q].S) return hipErrorInvalidValue;
+        b.job[q].blk0 = blocks;
+        blocks += (b.job[q].L + 255) / 256;
+    }
+    for (uint32_t q = b.njobs; q < (uint32_t)kMaxColJobs; ++q) b.job[q].blk0 = ~0u;
+    if (!blocks) return hipSuccess;
+    hipLaunchKernelGGL(k_vec_prep_sum_multi, dim3(blocks, 1 + kTabSlots), dim3(256), 0, st, b, f);
+    return hipGetLastError();
+}
 hipError_t launch_vec_prep_sum(const Fr* part, uint32_t S, uint32_t L, Fr* wc, Fr* tab, const ScaleTab& f,
                                hipStream_t st) {
     if (!L) return hipSuccess;

@@ -400,6 +400,19 @@ uint32_t colsum_slices(uint32_t R);
 hipError_t launch_colsum_f64(const ColBatch& b, int precision_bits, hipStream_t st);
 hipError_t launch_vec_prep_sum(const Fr* part, uint32_t S, uint32_t L, Fr* w_canon, Fr* tab,
                                const ScaleTab& f, hipStream_t st);
+// The same for up to kMaxColJobs vectors in one launch.
+struct VecPrepJob {
+    const Fr* part;
+    uint32_t S, L;
+    Fr* wc;
+    Fr* tab;
+    uint32_t blk0;                       // set by the launcher
+};
+struct VecPrepBatch {
+    VecPrepJob job[kMaxColJobs];
+    uint32_t njobs;
+};
+hipError_t launch_vec_prep_sum_multi(const VecPrepBatch& b, const ScaleTab& f, hipStream_t st);
 // Up to kMaxScanJobs DPP row scans in one launch (two terms per thread; na
 // shared by every job; na = 0: the max over the jobs' NaSpecs, read on the
 // device from b.bitw, so the host needs no operand bounds).
