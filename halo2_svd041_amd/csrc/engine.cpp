@@ -1960,7 +1960,11 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
                      pl[0].pows_off == c->pows_pre.pows_off && vm[0].cs.cols == c->pows_pre.d &&
                      pl[0].one_loff == 0;
     c->pows_pre.on = false;
-    if (!pre) {
+    // the one cells and gamma powers: read by no kernel of the call (gpc, not
+    // these cells, feeds the scans), so a pipelined svd_witness launches them
+    // after the scans, off the head of phase 1's stream
+    auto pows_launch = [&] {
+        if (pre) return;
         // (a captured graph must not hold gamma: the powers' launch carries it)
         for (int i = 0; i < n; ++i) REQUIRE(!c->capturing || vm[i].cs.cols <= 1, "internal: gamma inside a captured graph");
         BatchScope bs(c);                                 // the one cells and gamma powers: one launch
@@ -1980,7 +1984,9 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
             }
         }
         bs.end();
-    }
+    };
+    const bool pows_late = c->in_pipe;
+    if (!pows_late) pows_launch();
     // One scan launch over jobs (a_q against the vector wc_q / tab_q, cells at
     // v_q); operand widths host-known or read on the device (na 0).
     struct Scans {
@@ -2156,6 +2162,7 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         note_gates(c, p.eq, 1, p.eq_reg);
     }
     launch(cs_, "k_matvec_scan:cs");
+    if (pows_late) pows_launch();
 }
 static void verify_mul(svdw_ctx* c, uint32_t phase, const svdw_mat& a, const svdw_mat& b,
                        const svdw_mat& cs, const Fr& gamma) {
