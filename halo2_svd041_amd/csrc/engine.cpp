@@ -435,6 +435,7 @@ struct svdw_ctx {
     // svd_witness (whose side streams do not wait for st) waits explicitly
     hipEvent_t xwait_side = nullptr;
     DBuf f64in, digA, digB, digC, w1c, w1t, w2c, w2t, bits, gpc, gtab, crtR, gbits, chk, chkg;
+    DBuf gpc_alt, gtab_alt;                 // pipelined svd_witness: gamma tables of the other parity
     DBuf wbc[kMaxScanJobs], wbt[kMaxScanJobs];   // b.v per batched verify_mul (canonical, table)
     // gamma^j (canonical gpc, scaled table gtab, kernels.hpp kTabSlots) of the
     // current verify_mul calls: recomputed for every witness (a fresh challenge
@@ -2607,6 +2608,8 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
             // for that call's tail, the last reader of these cells and bit words
             // (st2's first stages write cells that call's st3 scans read)
             for (int p = 0; p < 2; ++p) std::swap(c->ph[p], c->alt[p]);
+            std::swap(c->gpc, c->gpc_alt);        // (call j - 1's scans still read the others)
+            std::swap(c->gtab, c->gtab_alt);
             clear_streams(c);
             // (tail_ev[.][0] was recorded on st2, [.][1] on st3: a stream does not
             // wait for its own earlier work)
@@ -2656,10 +2659,12 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
     }
     if (!c->dry) {
         // gamma^j depends on gamma only: queue it first, on its own stream, so it
-        // runs beside quantization instead of on the phase-1 chain
-        gamma_prep(c, std::max(N, M), gamma, c->st3);
-        c->gp_ev = stream_dep(c, c->st3, nullptr);
-        c->gp_st = c->st3;
+        // runs beside quantization instead of on the phase-1 chain (pipelined: on
+        // the cell stream, the least loaded one, into this parity's tables)
+        hipStream_t gs = c->in_pipe ? c->st_cell : c->st3;
+        gamma_prep(c, std::max(N, M), gamma, gs);
+        c->gp_ev = stream_dep(c, gs, nullptr);
+        c->gp_st = gs;
         host_mark(c, "gamma_prep queued");
     }
     unsigned* dbits = nullptr;
@@ -3058,7 +3063,7 @@ static void ctx_release(svdw_ctx* c) {
             for (auto e : t)
                 if (e) (void)hipEventDestroy(e);
         for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1], &c->w1c, &c->w1t, &c->w2c, &c->w2t,
-                        &c->bits, &c->gpc, &c->gtab, &c->crtR, &c->gbits, &c->colpart, &c->qfold,
+                        &c->bits, &c->gpc, &c->gtab, &c->gpc_alt, &c->gtab_alt, &c->crtR, &c->gbits, &c->colpart, &c->qfold,
                         &c->ing_x, &c->ing_e, &c->ing_c, &c->ing_p10, &c->ing_val, &c->ing_npos, &c->ing_nd,
                         &c->ing_rpos, &c->ing_kpos, &c->ing_err, &c->ing_q, &c->eq_cp, &c->eq_ks, &c->eq_reg,
                         &c->eq_w, &c->eq_k, &c->eq_err, &c->eq_st})
@@ -3188,11 +3193,12 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
     host_mark(c, "vm: gamma_prep queued");
     c->gp_external = true;
     c->gp_ext_one = pw ? pc.one : nullptr;
-    // (the cell set too: a pipelined svd_witness alternates between two)
+    // (the cell set and gamma tables too: a pipelined svd_witness alternates between two)
     auto key_now = [&] {
         return std::vector<uint64_t>{N, K, M, (uint64_t)(uintptr_t)a, (uint64_t)(uintptr_t)b, c->epoch,
                                      (uint64_t)(uintptr_t)c->ph[0].adv, (uint64_t)(uintptr_t)c->ph[1].adv,
-                                     (uint64_t)(uintptr_t)c->ph[0].lk, (uint64_t)(uintptr_t)c->ph[1].lk};
+                                     (uint64_t)(uintptr_t)c->ph[0].lk, (uint64_t)(uintptr_t)c->ph[1].lk,
+                                     (uint64_t)(uintptr_t)c->gpc.p, (uint64_t)(uintptr_t)c->gtab.p};
     };
     const std::vector<uint64_t> key = key_now();
     if (c->vmg.exec && key == c->vmg.key) {
