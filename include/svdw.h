@@ -275,10 +275,11 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   "pipeline" 1 | 0 (svd_witness with device inputs on the f64 CRT product
  *   path with the products on the cell stream, two cell sets within 60 % of
  *   the device memory: consecutive calls overlap -- a call returns with its
- *   d / u.d / bound / diff stages and its phase-1 row scans still running on
- *   the second and third streams, and the next call's quantization and
- *   products start on the cell stream beside them, into the other cell set;
- *   any other call on the context, a copy and svdw_sync wait for that tail);
+ *   u.d / bound / diff stages and its phase-1 row scans still running on the
+ *   second and third streams, and the next call's gamma tables, quantization
+ *   and products start on the cell stream beside them, into the other cell
+ *   set and tables; any other call on the context, a copy and svdw_sync wait
+ *   for that tail);
  *   "lanes" 2 | 1 (svdw_verify_mul_witness with device inputs: 2 alternates
  *   between two complete context states, exchanged behind the handle at each
  *   call, so consecutive calls run beside each other on separate streams; the
