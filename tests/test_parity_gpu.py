@@ -521,6 +521,7 @@ def test_pipelined_witnesses_parity(gpu_ctx_factory, N, M, P, world, hold):
 
 @pytest.mark.parametrize("N,M,P,row_lim,device,hold", [(1024, 1024, 63, 64, False, 0), (512, 512, 32, 128, False, 0),
                                                        (2048, 1024, 32, 24, False, 0), (1024, 1024, 63, 32, True, 0),
+                                                       (2048, 1024, 32, 16, True, 0),
                                                        (1024, 1024, 63, 32, True, 3000),
                                                        (1024, 1024, 63, 32, True, -3000)])
 def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device, hold):
