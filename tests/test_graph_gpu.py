@@ -193,3 +193,31 @@ def test_lanes_back_to_back_then_svd(gpu_ctx_factory):
     assert np.array_equal(ctx.advice(0), a0) and np.array_equal(ctx.advice(1), a1)
     hs.verify_mul_witness(ctx, ta, tb, gamma_for(961))
     _check_all(ctx, a, b, P, gamma_for(961))
+
+
+@pytest.mark.gpu
+def test_pipelined_svd_and_lanes_interleaved(gpu_ctx_factory):
+    """svd_witness (pipelined, alternating cell sets and gamma tables) and
+    verify_mul_witness (two lanes, captured graphs) interleaved on one handle
+    without a host wait, six rounds: each call's cells are the oracle's when
+    read right after it, and the last of each kind again at the end."""
+    import torch
+    import halo2_svd041_amd as hs
+    from conftest import gen_svd_input
+    P = 32
+    ctx = gpu_ctx_factory(P)
+    a, b = _mats(72, 56, 48, seed=61)
+    ta, tb = (torch.tensor(x, dtype=torch.float64, device="cuda:0") for x in (a, b))
+    mm, u, d, v = gen_svd_input(44, 38, seed=62)
+    dm, du, dv, dd = (torch.tensor(np.ascontiguousarray(x), dtype=torch.float64, device="cuda:0")
+                      for x in (mm, u, v, d))
+    for r in range(6):
+        hs.svd_witness(ctx, dm, du, dv, dd, gamma_for(970 + r))
+        hs.verify_mul_witness(ctx, ta, tb, gamma_for(980 + r))
+        if r in (1, 4):
+            c0, c1 = corc.verify_mul_witness(a, b, P, gamma_for(980 + r))
+            assert np.array_equal(ctx.advice(0), c0) and np.array_equal(ctx.advice(1), c1), r
+    hs.svd_witness(ctx, dm, du, dv, dd, gamma_for(990))
+    a0, l0, a1 = corc.svd_witness(mm, u, v, d, P, 19, gamma_for(990))
+    assert np.array_equal(ctx.advice(0), a0) and np.array_equal(ctx.advice(1), a1)
+    assert np.array_equal(ctx.lookups(0), l0)
