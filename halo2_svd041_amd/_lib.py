@@ -117,6 +117,7 @@ SIGNATURES = {
     "svdw_ctx_reset": (_i32, [_P]),
     "svdw_reserve": (_i32, [_P, _u32, _u64, _u64]),
     "svdw_sync": (_i32, [_P]),
+    "svdw_query": (_i32, [_P]),
     "svdw_stream_wait": (_i32, [_P, _P]),
     "svdw_stream_signal": (_i32, [_P, _P]),
     "svdw_debug_trace": (_i32, [_P]),

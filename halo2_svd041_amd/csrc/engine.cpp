@@ -485,6 +485,13 @@ struct svdw_ctx {
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
     uint32_t stage_flags = STAGE_ALIGN;     // STAGE_* (4 KiB-aligned block store windows)
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
+    // "stage_occ": blocks per CU of the persistent stage streamer (k_stage_pers);
+    // 0: the one-block-per-chunk kernels (k_stage / k_stage_multi). Its tile
+    // counters: one 256-byte slot per stream (cell stream, st2, st3), zero
+    // between launches (each launch's last block resets its slot).
+    uint32_t stage_occ = 2;
+    DBuf stage_ctr;
+    hipStream_t stream_id[3] = {};          // st, st2, st3 as created (st / st2 / st3 are swapped at times)
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
     bool gemm_batched = false;              // this witness's products went out as one batch
     bool res_f64 = true;                    // "res_f64": CRT residue planes of m, u, v from the
@@ -656,6 +663,21 @@ static void settle(svdw_ctx* c) {
     for (int k = 0; k < 2; ++k)
         hipck(hipStreamWaitEvent(c->st, c->tail_ev[c->tail_last][k], 0), "hipStreamWaitEvent");
     c->tail_pending = false;
+}
+// Device bytes held by a set of cell streams (both phases, advice + lookups).
+static double set_bytes(const Stream (&s)[2]) {
+    return 32.0 * (double)(s[0].cap + s[0].lcap + s[1].cap + s[1].lcap);
+}
+// Free the pipeline's other cell set (after the work that may read it).
+static void release_alt(svdw_ctx* c) {
+    if (c->dry || set_bytes(c->alt) == 0) return;
+    sync(c);
+    for (auto& s : c->alt) {
+        if (s.adv) hipck(hipFree(s.adv), "hipFree");
+        if (s.lk) hipck(hipFree(s.lk), "hipFree");
+        s = Stream{};
+    }
+    ++c->epoch;
 }
 // Dependency recorded on `from`; `to` waits for it (cross-stream dependency).
 // The returned handle is waited on later with dep_wait. (Round 4 measured the
@@ -944,6 +966,13 @@ static void check_mat(const svdw_ctx* c, const svdw_mat& m) {
 static void check_vec(const svdw_ctx* c, const svdw_vec& v) { check_mat(c, mat_of_vec(v)); }
 
 // ------------------------------------------------------- stage launches
+// The persistent stage kernel's tile counters for a launch on stream s (null:
+// not one of the context's streams -> the one-block-per-chunk kernels).
+static uint32_t* stage_ctr_for(svdw_ctx* c, hipStream_t s) {
+    if (!c->stage_occ || !c->stage_ctr.p) return nullptr;
+    const int k = s == c->stream_id[0] ? 0 : s == c->stream_id[1] ? 1 : s == c->stream_id[2] ? 2 : -1;
+    return k < 0 ? nullptr : reinterpret_cast<uint32_t*>(static_cast<char*>(c->stage_ctr.p) + 256 * k);
+}
 // Appends the stage's cells for `nelem` elements; returns the advice offset.
 // Launch a stage whose cells were appended at (off, loff) earlier.
 static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, uint32_t cols,
@@ -1026,7 +1055,8 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     }
     {
         ProfScope ps(c, c->st, std::string("k_stage:") + tag, bytes, 0);
-        hipck(launch_stage(a, c->st), "k_stage");
+        const StageArgs* one = &a;
+        hipck(launch_stage_pers(&one, 1, c->st, stage_ctr_for(c, c->st), c->stage_occ), "k_stage");
     }
 }
 // Issue a stream's pending batched stages (k_stage_multi; one program: k_stage).
@@ -1061,7 +1091,8 @@ static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter, hipEvent
                 fprintf(stderr, "\n");
             }
             ProfScope pr(c, s, name, bytes, 0, true);
-            hipck(launch_stage_multi(ps.data(), (int)ps.size(), s), "k_stage_multi");
+            hipck(launch_stage_pers(ps.data(), (int)ps.size(), s, stage_ctr_for(c, s), c->stage_occ),
+                  "k_stage_multi");
         }
     }
     if (waiter) stream_dep(c, s, waiter);
@@ -2599,10 +2630,24 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         // at most 60 % of the device memory (1024^2 P=63: 2 x 9.3 GB; 4096^2
         // P=63, 2 x 148 GB, runs unpipelined)
         const double wbytes = 32.0 * (double)(c->plan_val[0] + c->plan_val[1] + c->plan_val[2] + c->plan_val[3]);
-        c->in_pipe = c->pipeline && on_device && c->overlap && c->res_f64 && c->gemm_crt &&
-                     c->gemm_impl == SVDW_GEMM_MFMA && N <= 8192 && M <= 8192 &&
-                     (c->prod_cell > 0 || (c->prod_cell < 0 && sharded(c))) &&
-                     2.0 * wbytes <= 0.6 * (double)c->mem_total;
+        const bool qualifies = c->pipeline && on_device && c->overlap && c->res_f64 && c->gemm_crt &&
+                               c->gemm_impl == SVDW_GEMM_MFMA && N <= 8192 && M <= 8192 &&
+                               (c->prod_cell > 0 || (c->prod_cell < 0 && sharded(c)));
+        // The other cell set must already hold this witness, or its growth must
+        // fit in the device's free memory now (other contexts, the lane's state
+        // and torch's allocations count) with 10 % of the device to spare for
+        // scratch; else the call runs unpipelined and the set is released.
+        bool fits = qualifies;
+        if (qualifies) {
+            const double need = wbytes - set_bytes(c->alt);
+            if (need > 0) {
+                size_t fr = 0, tot = 0;
+                hipck(hipMemGetInfo(&fr, &tot), "hipMemGetInfo");
+                fits = need + 0.1 * (double)tot <= (double)fr;
+            }
+        }
+        if (qualifies && !fits) release_alt(c);
+        c->in_pipe = fits;
         if (c->in_pipe) {
             // the other cell set (last written by call j - 2): every stream waits
             // for that call's tail, the last reader of these cells and bit words
@@ -2627,9 +2672,31 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
             settle(c);
             after_previous(c);
         }
-        for (int p = 0; p < 2; ++p) {
-            grow(c, c->ph[p].adv, 0, c->ph[p].cap, c->plan_val[2 * p]);
-            grow(c, c->ph[p].lk, 0, c->ph[p].lcap, c->plan_val[2 * p + 1]);
+        auto grow_set = [&] {
+            for (int p = 0; p < 2; ++p) {
+                grow(c, c->ph[p].adv, 0, c->ph[p].cap, c->plan_val[2 * p]);
+                grow(c, c->ph[p].lk, 0, c->ph[p].lcap, c->plan_val[2 * p + 1]);
+            }
+        };
+        if (!c->in_pipe) {
+            grow_set();
+        } else {
+            try {
+                grow_set();
+            } catch (const SvdwError& e) {
+                if (e.code != SVDW_ENOMEM) throw;
+                // the other set could not be allocated after all: back to this
+                // set, unpipelined (the waits already queued are harmless)
+                for (int p = 0; p < 2; ++p) std::swap(c->ph[p], c->alt[p]);
+                std::swap(c->gpc, c->gpc_alt);
+                std::swap(c->gtab, c->gtab_alt);
+                c->in_pipe = false;
+                release_alt(c);
+                clear_streams(c);
+                settle(c);
+                after_previous(c);
+                grow_set();
+            }
         }
     }
     // examples/svd_example.rs:183-184 run rlc.load_rlc_cache((ctx_gate, ctx_rlc), gate, 1)
@@ -3049,30 +3116,43 @@ static svdw_counts vmg_restore(svdw_ctx* c, const Fr& gamma) {
     c->ph[1].nl = g.counts.lookup1;
     return g.counts;
 }
+// Every scratch buffer of a state (release, footprint).
+static std::vector<DBuf*> dbufs(svdw_ctx* c) {
+    std::vector<DBuf*> v = {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1],
+                            &c->w1c, &c->w1t, &c->w2c, &c->w2t, &c->bits, &c->gpc, &c->gtab, &c->gpc_alt,
+                            &c->gtab_alt, &c->crtR, &c->gbits, &c->colpart, &c->qfold, &c->ing_x, &c->ing_e,
+                            &c->ing_c, &c->ing_p10, &c->ing_val, &c->ing_npos, &c->ing_nd, &c->ing_rpos,
+                            &c->ing_kpos, &c->ing_err, &c->ing_q, &c->eq_cp, &c->eq_ks, &c->eq_reg, &c->eq_w,
+                            &c->eq_k, &c->eq_err, &c->eq_st, &c->stage_ctr};
+    for (int i = 0; i < kMaxScanJobs; ++i) {
+        v.push_back(&c->wbc[i]);
+        v.push_back(&c->wbt[i]);
+        v.push_back(&c->bvfull[i]);
+    }
+    return v;
+}
+// Device bytes a state holds (cell sets and scratch).
+static double state_bytes(svdw_ctx* c) {
+    double b = set_bytes(c->ph) + set_bytes(c->alt);
+    for (DBuf* d : dbufs(c)) b += (double)d->cap;
+    return b;
+}
+// Every device object is released on its own (a state whose creation failed
+// part-way holds some of them only).
 static void ctx_release(svdw_ctx* c) {
     if (!c) return;
     if (c->lane) ctx_release(c->lane);
-    if (!c->dry && c->st && c->st2) {
-        (void)hipStreamSynchronize(c->st);
-        (void)hipStreamSynchronize(c->st2);
-        if (c->st3) (void)hipStreamSynchronize(c->st3);
+    if (!c->dry) {
+        for (hipStream_t t : {c->st_cell ? c->st_cell : c->st, c->st2, c->st3})
+            if (t) (void)hipStreamSynchronize(t);
         vmg_drop(c);
         for (auto& s : c->ph) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
         for (auto& s : c->alt) { (void)hipFree(s.adv); (void)hipFree(s.lk); }
         for (auto& t : c->tail_ev)
             for (auto e : t)
                 if (e) (void)hipEventDestroy(e);
-        for (DBuf* b : {&c->f64in, &c->digA, &c->digB, &c->digC, &c->chk, &c->chkg, &c->gateq[0], &c->gateq[1], &c->w1c, &c->w1t, &c->w2c, &c->w2t,
-                        &c->bits, &c->gpc, &c->gtab, &c->gpc_alt, &c->gtab_alt, &c->crtR, &c->gbits, &c->colpart, &c->qfold,
-                        &c->ing_x, &c->ing_e, &c->ing_c, &c->ing_p10, &c->ing_val, &c->ing_npos, &c->ing_nd,
-                        &c->ing_rpos, &c->ing_kpos, &c->ing_err, &c->ing_q, &c->eq_cp, &c->eq_ks, &c->eq_reg,
-                        &c->eq_w, &c->eq_k, &c->eq_err, &c->eq_st})
+        for (DBuf* b : dbufs(c))
             if (b->p) (void)hipFree(b->p);
-        for (int i = 0; i < kMaxScanJobs; ++i) {
-            if (c->wbc[i].p) (void)hipFree(c->wbc[i].p);
-            if (c->wbt[i].p) (void)hipFree(c->wbt[i].p);
-            if (c->bvfull[i].p) (void)hipFree(c->bvfull[i].p);
-        }
         if (c->hbits) (void)hipHostFree(c->hbits);
         if (c->ev_bits) (void)hipEventDestroy(c->ev_bits);
         for (auto e : c->xev)
@@ -3080,15 +3160,21 @@ static void ctx_release(svdw_ctx* c) {
         for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
         for (auto e : c->pool) (void)hipEventDestroy(e);
         for (auto e : c->deps) (void)hipEventDestroy(e);
-        (void)hipStreamSynchronize(c->st2);
-        if (c->st3) {
-            (void)hipStreamSynchronize(c->st3);
-            (void)hipStreamDestroy(c->st3);
-        }
-        (void)hipStreamDestroy(c->st2);
-        (void)hipStreamDestroy(c->st);
+        for (hipStream_t t : {c->st3, c->st2, c->st_cell ? c->st_cell : c->st})
+            if (t) (void)hipStreamDestroy(t);
     }
     delete c;
+}
+// "lanes": may the next verify_mul_witness run on the other state? Yes when
+// that state already holds as much device memory as this one (the calls have
+// one shape), or when its growth to this one's footprint fits in free memory
+// with 10 % of the device to spare; else the call stays on this state.
+static bool lane_fits(svdw_ctx* c) {
+    const double need = state_bytes(c) - (c->lane ? state_bytes(c->lane) : 0.0);
+    if (need <= 0) return true;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
+    return need + 0.1 * (double)tot <= (double)fr;
 }
 // Device state of a new context: its three streams, the pinned bit words, events.
 static void ctx_init_device(svdw_ctx* c) {
@@ -3103,6 +3189,14 @@ static void ctx_init_device(svdw_ctx* c) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_bits, hipEventDisableTiming | hipEventReleaseToDevice);
     for (int k = 0; k < 4 && e == hipSuccess; ++k)
         e = hipEventCreateWithFlags(&c->tail_ev[k / 2][k % 2], hipEventDisableTiming | hipEventReleaseToDevice);
+    c->stream_id[0] = c->st;
+    c->stream_id[1] = c->st2;
+    c->stream_id[2] = c->st3;
+    if (e == hipSuccess) e = hipMalloc(&c->stage_ctr.p, 3 * 256);
+    if (e == hipSuccess) {
+        c->stage_ctr.cap = 3 * 256;
+        e = hipMemset(c->stage_ctr.p, 0, 3 * 256);     // (synchronous: before any launch)
+    }
     size_t mfree = 0;
     if (e == hipSuccess) e = hipMemGetInfo(&mfree, &c->mem_total);
     if (e != hipSuccess) fail(SVDW_EDEVICE, std::string("HIP device init failed: ") + hipGetErrorString(e));
@@ -3110,16 +3204,17 @@ static void ctx_init_device(svdw_ctx* c) {
 // The settings (options, shard, profiler) of `s` onto the lane `d`; a change
 // bumps the lane's epoch (its captured graph no longer applies).
 static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
-    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->gemm_crt, s->res_f64,
+    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->stage_occ, s->gemm_crt, s->res_f64,
                          s->phase1_overlap, s->prod_cell, s->hold_us, s->rlc_prefix, s->p1_at,
                          s->f64_views, s->overlap, s->stage_batch, s->graph_vm, s->pipeline,
                          s->shard_rank, s->shard_world, s->prof, s->host_trace};
-    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->gemm_crt, d->res_f64,
+    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->stage_occ, d->gemm_crt, d->res_f64,
                          d->phase1_overlap, d->prod_cell, d->hold_us, d->rlc_prefix, d->p1_at,
                          d->f64_views, d->overlap, d->stage_batch, d->graph_vm, d->pipeline,
                          d->shard_rank, d->shard_world, d->prof, d->host_trace};
     if (!memcmp(a, b, sizeof a) && d->prof_filter == s->prof_filter) return;
     d->gemm_impl = s->gemm_impl; d->stage_flags = s->stage_flags; d->stage_elems = s->stage_elems;
+    d->stage_occ = s->stage_occ;
     d->gemm_crt = s->gemm_crt; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
     d->prod_cell = s->prod_cell; d->hold_us = s->hold_us; d->rlc_prefix = s->rlc_prefix;
     d->p1_at = s->p1_at; d->f64_views = s->f64_views; d->overlap = s->overlap;
@@ -3159,7 +3254,7 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
                                           hipStream_t caller = nullptr, bool has_caller = false) {
     const bool plain = on_device && !c->dry && !c->prof && !c->hold_us && !sharded(c) && N >= 1 && K >= 1 &&
                        M >= 1;
-    if (plain && c->lanes > 1) lane_switch(c);
+    if (plain && c->lanes > 1 && lane_fits(c)) lane_switch(c);
     if (has_caller && !c->dry) {
         const hipEvent_t e = xevent(c, 0);
         hipck(hipEventRecord(e, caller), "hipEventRecord");
@@ -3502,6 +3597,28 @@ int svdw_debug_trace(void* buf) {
 }
 int svdw_sync(svdw_ctx* c) {
     return guarded([&] { REQUIRE(c, "null ctx"); sync(c); });
+}
+// 1 when every launch queued on the context (both lanes) has completed, 0
+// while some still runs; no host wait (hipStreamQuery).
+int svdw_query(svdw_ctx* c) {
+    int done = 1;
+    const int rc = guarded([&] {
+        REQUIRE(c, "null ctx");
+        if (c->dry) return;
+        for (svdw_ctx* x : {c, c->lane}) {
+            if (!x) continue;
+            for (hipStream_t t : {x->st, x->st2, x->st3}) {
+                if (!t) continue;
+                const hipError_t e = hipStreamQuery(t);
+                if (e == hipErrorNotReady) {
+                    done = 0;
+                    return;
+                }
+                hipck(e, "hipStreamQuery");
+            }
+        }
+    });
+    return rc ? rc : done;
 }
 uint64_t svdw_advice_len(const svdw_ctx* c, uint32_t phase) { return c && phase < 2 ? c->ph[phase].n : 0; }
 uint64_t svdw_lookup_len(const svdw_ctx* c, uint32_t phase) { return c && phase < 2 ? c->ph[phase].nl : 0; }
@@ -4365,6 +4482,17 @@ int svdw_shard_segments(const svdw_ctx* c, svdw_segment* out, uint64_t cap, uint
                                   c->owned[i].n};
     });
 }
+// Options removed in round 4 once their A/B had settled (fixed at the measured
+// best or dropped with their code): still accepted, as no-ops.
+static bool is_retired_option(const std::string& n) {
+    static const char* const kRetired[] = {"bits_fold",    "bounds_after", "colsum",         "d_checks_aside",
+                                           "dep_values",   "fused_quantize", "gemm_batch",    "gemm_priority",
+                                           "gemm_rt",      "prelaunch_at", "prod_blocks",     "prod_first",
+                                           "res_first",    "stage_align",  "stage_priority",  "stage_probe"};
+    for (const char* r : kRetired)
+        if (n == r) return true;
+    return false;
+}
 int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
     return guarded([&] {
         REQUIRE(c && name, "null argument");
@@ -4377,12 +4505,19 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "pipeline") {                // pipelined svd_witness (svd_witness)
             REQUIRE(value == 0 || value == 1, "pipeline: 0 or 1");
             c->pipeline = (int)value;
+            if (!value) {                            // the other cell set is not needed any more
+                release_alt(c);
+                if (c->lane) release_alt(c->lane);
+            }
         } else if (n == "graph") {                   // captured verify_mul_witness (vm_graph)
             REQUIRE(value == 0 || value == 1, "graph: 0 or 1");
             c->graph_vm = (int)value;
         } else if (n == "gemm_impl") {
             REQUIRE(value == SVDW_GEMM_MFMA || value == SVDW_GEMM_VALU, "gemm_impl: 0 (mfma) or 1 (valu)");
             c->gemm_impl = (int)value;
+        } else if (n == "stage_occ") {               // persistent stage streamer (0: off)
+            REQUIRE(value >= 0 && value <= 8, "stage_occ: 0..8 blocks per CU");
+            c->stage_occ = (uint32_t)value;
         } else if (n == "stage_elems") {
             REQUIRE(value >= 16 && value <= 256 && value % 16 == 0,
                     "stage_elems: a multiple of 16 in [16, 256]");
@@ -4412,6 +4547,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->p1_at = (int)value;
         } else if (n == "overlap") {
             c->overlap = value != 0;
+        } else if (is_retired_option(n)) {
+            // settled in round 4 (include/svdw.h, "Retired options"): accepted
+            // and ignored for one more ABI version, so existing callers run
         } else {
             fail(SVDW_EINVAL, "unknown option " + n);
         }

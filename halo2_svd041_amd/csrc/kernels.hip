@@ -810,6 +810,344 @@ hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t 
     return flush();
 }
 
+// ------------------------------------------------ persistent stage streamer
+// k_stage_pers: the same cell programs as k_stage / k_stage_multi, run by a
+// persistent grid (a few blocks per CU) that takes 64-element tiles in stream
+// order from a device counter. Per block:
+//   * wave 0 runs phase A (the micro-ops, one element per lane) of the NEXT
+//     tile into the other LDS buffer, with that tile's view loads issued one
+//     tile earlier and its index dequeued two tiles earlier, while
+//   * all four waves (wave 0 once its phase A is done) stream the CURRENT
+//     tile's cells, taking 2 KiB rounds (64 cells, one per lane: two 16-B
+//     stores) from an LDS counter, so the waves stay balanced.
+// One barrier per tile; a block's programme tables (constants, micro-ops,
+// views, per-cell descriptors and masks) are set up once per program it meets,
+// in one of two table sets, so a tile of the next program can run its phase A
+// while the current tile still reads the other set. Tiles are ~64-128 KiB of
+// cells: the grid's write front stays a compact range of the stream, and one
+// device counter serves the dequeues (one per tile, ~50 per µs at 6 TB/s).
+// The last block to leave resets the counter for the next launch on its stream.
+static constexpr uint32_t kPersTile = 64;
+
+// words of one table set: K | masks (8 per cell) | micro-ops | views | descriptors
+__host__ __device__ constexpr uint32_t pers_set_words(uint32_t cl) {
+    return (kMaxK * VW + 8 * cl + kMaxMicro * 2 + kMaxViews * 10 + cl + 3) / 4 * 4;
+}
+__host__ __device__ constexpr uint32_t pers_lds_bytes(uint32_t cl, uint32_t ev) {
+    return 4 * (2 * pers_set_words(cl) + 2 * (kPersTile * ev + 16));
+}
+struct PersSet {
+    uint32_t* K;
+    uint4* M;            // masks: 2 uint4 per cell
+    MicroOp* mo;
+    DView* vw;
+    uint32_t* D;         // descriptors
+};
+__device__ __forceinline__ PersSet pers_set(uint32_t* base, uint32_t cl) {
+    PersSet s;
+    s.K = base;
+    s.M = reinterpret_cast<uint4*>(base + kMaxK * VW);
+    s.mo = reinterpret_cast<MicroOp*>(base + kMaxK * VW + 8 * cl);
+    s.vw = reinterpret_cast<DView*>(base + kMaxK * VW + 8 * cl + kMaxMicro * 2);
+    s.D = base + kMaxK * VW + 8 * cl + kMaxMicro * 2 + kMaxViews * 10;
+    return s;
+}
+// One program's tables into set s, by the 64 lanes of one wave.
+__device__ __forceinline__ void pers_tables(const Rec& q, const PersSet& s, uint32_t lane) {
+    const StageArgs& a = *q.a;
+    for (uint32_t k = lane; k < a.nk; k += 64) lds_put(s.K + k * VW, q.K[k]);
+    for (uint32_t k = lane; k < a.nmo; k += 64) s.mo[k] = q.mo[k];
+    if (lane < kMaxViews) s.vw[lane] = a.view[lane];
+    for (uint32_t k = lane; k < a.C + a.L; k += 64) {
+        const SlotOp op = k < a.C ? q.adv[k] : q.lk[k - a.C];
+        const uint32_t lo = op.lo;
+        uint32_t nb = op.nbits ? op.nbits : 256u;
+        nb = min(nb, 256u - lo);
+        const bool elem = op.src < KSRC;
+        const uint32_t base = (elem ? op.src : op.src - KSRC) * VW;
+        s.D[k] = half_desc(base + (lo >> 5), lo & 31u, elem);
+        uint32_t w[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int keep = (int)nb - 32 * i;
+            w[i] = keep >= 32 ? 0xffffffffu : (keep <= 0 ? 0u : ((1u << keep) - 1u));
+        }
+        s.M[2 * k] = make_uint4(w[0], w[1], w[2], w[3]);
+        s.M[2 * k + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+    }
+}
+// View loads of element e (this lane) of a program (phase A's prefetch).
+__device__ __forceinline__ Prefetch pers_loads(const StageArgs& a, uint32_t e, bool valid) {
+    Prefetch f{fr_zero(), fr_zero(), false, false};
+    if (!valid) return f;
+    const uint32_t pi = e / a.cols, pj = e - pi * a.cols;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const DView& v = a.view[k];
+        Fr x = fr_zero();
+        bool in = false;
+        if (v.ptr && v.mode == VIEW_STRIDED && pi < v.rows && pj < v.cols) {
+            x = ld_fr(v.ptr + (int64_t)pi * v.rs + (int64_t)pj * v.cs);
+            in = true;
+        } else if (v.ptr && v.mode == VIEW_F64 && pi < v.rows && pj < v.cols) {
+            x = quantize_fr(reinterpret_cast<const double*>(v.ptr)[(int64_t)pi * v.rs + (int64_t)pj * v.cs],
+                            f64_scale(v));
+            in = true;
+        }
+        if (k == 0) { f.v0 = x; f.in0 = in; } else { f.v1 = x; f.in1 = in; }
+    }
+    return f;
+}
+// Cells [c0, c0 + n) of one region of a tile (advice or lookups, region
+// tables D / M at slot offset 0), cell c = element c / C, slot c % C; this
+// wave's round r covers the 64 cells of a 2 KiB-aligned window.
+__device__ __forceinline__ void pers_round(uint4* __restrict__ out, uint32_t total, uint32_t mis, uint32_t r,
+                                           uint32_t C, uint32_t magic, const uint32_t* __restrict__ D,
+                                           const uint4* __restrict__ M, const uint32_t* __restrict__ buf,
+                                           const uint32_t* __restrict__ kset, uint32_t ev, uint32_t lane) {
+    const int32_t c = (int32_t)(r * 64 + lane) - (int32_t)mis;
+    if (c < 0 || (uint32_t)c >= total) return;
+    const uint32_t el = fastdiv((uint32_t)c, C, magic), slot = (uint32_t)c - el * C;
+    const uint32_t d = D[slot];
+    const uint4 m0 = M[2 * slot], m1 = M[2 * slot + 1];
+    const uint32_t* x = ((d & kHalfElem) ? buf + el * ev : kset) + (d & 0xffffu);
+    const uint32_t sh = (d >> 16) & 31u;
+    uint32_t w[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) w[i] = x[i];
+    uint4* o = out + 2 * (uint32_t)c;
+    o[0] = make_uint4(__builtin_amdgcn_alignbit(w[1], w[0], sh) & m0.x, __builtin_amdgcn_alignbit(w[2], w[1], sh) & m0.y,
+                      __builtin_amdgcn_alignbit(w[3], w[2], sh) & m0.z, __builtin_amdgcn_alignbit(w[4], w[3], sh) & m0.w);
+    o[1] = make_uint4(__builtin_amdgcn_alignbit(w[5], w[4], sh) & m1.x, __builtin_amdgcn_alignbit(w[6], w[5], sh) & m1.y,
+                      __builtin_amdgcn_alignbit(w[7], w[6], sh) & m1.z, __builtin_amdgcn_alignbit(w[8], w[7], sh) & m1.w);
+}
+struct PersCtl {
+    uint32_t* ctr;       // [0] tile head, [1] blocks done (zero between launches)
+    uint32_t cl;         // max C + L over the programs (table set size)
+    uint32_t ev;         // max element words over the programs
+};
+struct SrcMulti {
+    const StageMulti* m;
+    __device__ uint32_t nprog() const { return m->nprog; }
+    __device__ uint32_t t0(uint32_t p) const { return m->blk0[p]; }
+    __device__ uint32_t prog_of(uint32_t t) const { return multi_prog(*m, t); }
+    __device__ Rec rec(uint32_t p) const { return multi_rec(*m, p); }
+};
+struct SrcSingle {
+    const StageArgs* a;
+    uint32_t ntiles;
+    __device__ uint32_t nprog() const { return 1; }
+    __device__ uint32_t t0(uint32_t p) const { return p ? ntiles : 0; }
+    __device__ uint32_t prog_of(uint32_t) const { return 0; }
+    __device__ Rec rec(uint32_t) const { return Rec{a, a->mo, a->adv, a->lk, a->K}; }
+};
+template <class SRC>
+__device__ __forceinline__ void stage_persist(const SRC& S, const PersCtl& pc) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    __shared__ uint32_t sTile[2], sSet[2], sRound[2], sProg[2];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint32_t T = S.t0(S.nprog());
+    const uint32_t sw = pers_set_words(pc.cl), bw = kPersTile * pc.ev + 16;
+    uint32_t* const setb[2] = {smem, smem + sw};
+    uint32_t* const bufb[2] = {smem + 2 * sw, smem + 2 * sw + bw};
+    // wave 0's look-ahead: tile n1 (its loads f1 in flight), tile n2 (dequeued)
+    uint32_t n1 = 0, n2 = 0;
+    Prefetch f1{fr_zero(), fr_zero(), false, false};
+    auto dequeue = [&]() -> uint32_t {
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(pc.ctr, 1u);
+        return __builtin_amdgcn_readfirstlane(t);
+    };
+    // element range of tile t (program p)
+    auto tile_elems = [&](uint32_t t, uint32_t p, const StageArgs& a, uint32_t* e0, uint32_t* ne) {
+        *e0 = a.e_begin + (t - S.t0(p)) * kPersTile;
+        *ne = min(kPersTile, a.e_end - *e0);
+    };
+    auto issue_loads = [&](uint32_t t) {
+        if (t >= T) { f1 = Prefetch{fr_zero(), fr_zero(), false, false}; return; }
+        const uint32_t p = S.prog_of(t);
+        const Rec q = S.rec(p);
+        uint32_t e0, ne;
+        tile_elems(t, p, *q.a, &e0, &ne);
+        f1 = pers_loads(*q.a, e0 + lane, lane < ne);
+    };
+    // phase A of tile t into buffer b (wave 0): tables into the set that does
+    // not hold the current tile's program unless it is the same program
+    auto phase_a = [&](uint32_t t, uint32_t b, uint32_t cur_set) {
+        if (t >= T) {
+            if (lane == 0) sTile[b] = T;
+            return;
+        }
+        const uint32_t p = S.prog_of(t);
+        const Rec q = S.rec(p);
+        uint32_t s = cur_set;
+        if (sProg[s] != p) {
+            s ^= 1u;
+            if (sProg[s] != p) {
+                pers_tables(q, pers_set(setb[s], pc.cl), lane);
+                if (lane == 0) sProg[s] = p;
+            }
+        }
+        const PersSet ts = pers_set(setb[s], pc.cl);
+        uint32_t e0, ne;
+        tile_elems(t, p, *q.a, &e0, &ne);
+        if (lane < ne)
+            element_program(*q.a, e0 + lane, bufb[b] + lane * pc.ev, ts.K, ts.mo, ts.vw, f1.v0, f1.in0, f1.v1,
+                            f1.in1);
+        if (lane == 0) {
+            sTile[b] = t;
+            sSet[b] = s;
+        }
+    };
+    if (tid < 2) {
+        sProg[tid] = ~0u;
+        sRound[tid] = 0;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const uint32_t t0 = dequeue();
+        n1 = dequeue();
+        n2 = dequeue();
+        issue_loads(t0);
+        phase_a(t0, 0, 0);
+        issue_loads(n1);
+    }
+    __syncthreads();
+    for (uint32_t k = 0;; ++k) {
+        const uint32_t b = k & 1u;
+        const uint32_t cur = sTile[b];
+        if (cur >= T) break;                                        // (uniform)
+        const uint32_t cset = sSet[b];
+        if (wave == 0) {
+            if (lane == 0) sRound[b ^ 1u] = 0;
+            phase_a(n1, b ^ 1u, cset);                              // the next tile, other buffer
+            n1 = n2;
+            issue_loads(n1);
+            n2 = dequeue();
+        }
+        // ---- phase B of the current tile: 2 KiB rounds from the LDS counter
+        const uint32_t p = S.prog_of(cur);
+        const Rec q = S.rec(p);
+        const StageArgs& a = *q.a;
+        uint32_t e0, ne;
+        tile_elems(cur, p, a, &e0, &ne);
+        const PersSet ts = pers_set(setb[cset], pc.cl);
+        uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
+        const uint32_t totA = ne * a.C, misA = (uint32_t)(reinterpret_cast<uintptr_t>(outA) >> 5) & 63u;
+        const uint32_t RA = (totA + misA + 63) / 64;
+        uint4* outL = nullptr;
+        uint32_t totL = 0, misL = 0, RL = 0;
+        if (a.L) {
+            outL = reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L);
+            totL = ne * a.L;
+            misL = (uint32_t)(reinterpret_cast<uintptr_t>(outL) >> 5) & 63u;
+            RL = (totL + misL + 63) / 64;
+        }
+        const uint32_t* buf = bufb[b];
+        for (;;) {
+            uint32_t r = 0;
+            if (lane == 0) r = atomicAdd(&sRound[b], 1u);
+            r = __builtin_amdgcn_readfirstlane(r);
+            if (r >= RA + RL) break;
+            if (r < RA)
+                pers_round(outA, totA, misA, r, a.C, a.cdiv_magic, ts.D, ts.M, buf, ts.K, pc.ev, lane);
+            else
+                pers_round(outL, totL, misL, r - RA, a.L, a.ldiv_magic, ts.D + a.C, ts.M + 2 * a.C, buf, ts.K,
+                           pc.ev, lane);
+        }
+        __syncthreads();
+    }
+    // the last block out resets the counters for the next launch on this stream
+    if (tid == 0) {
+        const uint32_t done = atomicAdd(pc.ctr + 1, 1u);
+        if (done == gridDim.x - 1) {
+            atomicExch(pc.ctr, 0u);
+            atomicExch(pc.ctr + 1, 0u);
+        }
+    }
+}
+__global__ __launch_bounds__(256) void k_stage_pers(const StageArgs a, const PersCtl pc, uint32_t ntiles) {
+    stage_persist(SrcSingle{&a, ntiles}, pc);
+}
+__global__ __launch_bounds__(256) void k_stage_pers_multi(const StageMulti m, const PersCtl pc) {
+    stage_persist(SrcMulti{&m}, pc);
+}
+static int g_cus = 0;
+static uint32_t pers_grid(uint32_t ntiles, uint32_t occ) {
+    if (!g_cus) {
+        int dev = 0, n = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        g_cus = n > 0 ? n : 256;
+    }
+    return std::max(1u, std::min(ntiles, occ * (uint32_t)g_cus));
+}
+hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t st, uint32_t* ctr, uint32_t occ) {
+    if (!ctr || !occ) return launch_stage_multi(progs, n, st);
+    StageMulti m;
+    m.nprog = 0;
+    uint32_t used = 0, tiles = 0, cl = 0, ev = 0;
+    const StageArgs* single = nullptr;
+    auto flush = [&]() -> hipError_t {
+        hipError_t e = hipSuccess;
+        if (m.nprog) {
+            PersCtl pc{ctr, cl, ev};
+            const uint32_t lds = pers_lds_bytes(cl, ev);
+            if (lds > 160u * 1024u) return hipErrorInvalidValue;
+            const uint32_t grid = pers_grid(tiles, occ);
+            if (m.nprog == 1) {
+                hipLaunchKernelGGL(k_stage_pers, dim3(grid), dim3(256), lds, st, *single, pc, tiles);
+            } else {
+                m.blk0[m.nprog] = tiles;
+                hipLaunchKernelGGL(k_stage_pers_multi, dim3(grid), dim3(256), lds, st, m, pc);
+            }
+            e = hipGetLastError();
+        }
+        m.nprog = 0;
+        used = tiles = cl = ev = 0;
+        return e;
+    };
+    for (int i = 0; i < n; ++i) {
+        const StageArgs& a = *progs[i];
+        if (a.e_end <= a.e_begin) continue;
+        if (a.C + a.L > kMaxAdv + kMaxLk || a.nv > kMaxV) return hipErrorInvalidValue;
+        const uint32_t rb = stage_record_bytes(a.nmo, a.C, a.L, a.nk);
+        if (m.nprog == (uint32_t)kMaxMulti || used + rb > kMultiBytes || (m.nprog && rb > kMultiBytes)) {
+            const hipError_t e = flush();
+            if (e != hipSuccess) return e;
+        }
+        if (rb > kMultiBytes) {                         // too large for a record: a launch of its own
+            single = &a;
+            m.nprog = 1;
+            tiles = (a.e_end - a.e_begin + kPersTile - 1) / kPersTile;
+            cl = a.C + a.L;
+            ev = stage_elem_words(a.nv ? a.nv : 1);
+            const hipError_t e = flush();
+            if (e != hipSuccess) return e;
+            continue;
+        }
+        uint8_t* r = m.data + used;
+        memcpy(r, &a, kRecHead);
+        uint8_t* q = r + kRecHead;
+        memcpy(q, a.mo, 8 * a.nmo);
+        q += 8 * a.nmo;
+        memcpy(q, a.adv, 4 * a.C);
+        q += 4 * a.C;
+        memcpy(q, a.lk, 4 * a.L);
+        q += 4 * a.L;
+        memcpy(q, a.K, 32 * a.nk);
+        m.off[m.nprog] = used;
+        m.blk0[m.nprog] = tiles;
+        ++m.nprog;
+        if (m.nprog == 1) single = &a;
+        used += rb;
+        tiles += (a.e_end - a.e_begin + kPersTile - 1) / kPersTile;
+        cl = std::max(cl, a.C + a.L);
+        ev = std::max(ev, stage_elem_words(a.nv ? a.nv : 1));
+    }
+    return flush();
+}
+
 // ----------------------------------------------------------------- maxbits
 __global__ __launch_bounds__(256) void k_maxbits(const DView v, uint32_t rows, uint32_t cols,
                                                  unsigned* out) {
@@ -1714,7 +2052,9 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
 // (the n loads issued before the first use: one memory latency, not n) and
 // writes four rows of 16 consecutive cells. C mod p = sum_k r_k E_k +
 // q (-Mtot mod p), q = floor(sum_k r_k inv_k / m_k + 1/2) in f64 (|C| < Mtot / 4
-// keeps it exact), accumulated carry-free in 16-bit limbs, one 9-word
+// keeps it exact), accumulated in eight 64-bit accumulators, one per 32-bit
+// word of E_k (each sum of n <= 40 products of an 8-bit residue and a 32-bit
+// word stays below 2^46: no carries until the end), then one 9-word
 // reduction. SYM: elements j >= i of the upper tiles (the GEMM computed upper
 // and diagonal 128-tiles), each also stored at (j, i).
 __device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t cblk) {

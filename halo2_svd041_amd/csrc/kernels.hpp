@@ -240,6 +240,11 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t st);
 // Independent stages (no stage reads another's cells) in as few k_stage_multi
 // launches as their records fit (stage_record_bytes, kMultiBytes); n >= 1.
 hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st);
+// The same stages on the persistent streamer (k_stage_pers): a grid of occ
+// blocks per CU taking 64-element tiles from the counters at ctr (two words,
+// zero between launches; one slot per stream: launches on one stream never
+// overlap). ctr null or occ 0: launch_stage_multi.
+hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t st, uint32_t* ctr, uint32_t occ);
 // does the record of `a` fit one k_stage_multi launch?
 bool stage_multi_fits(const StageArgs& a);
 // max over the view of bit-length(|signed(x)|): out[b] = max of block b

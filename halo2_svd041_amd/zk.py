@@ -114,13 +114,36 @@ class Context:
         self.last_svd = None
         self.layout_opts = {}
         self._h = ct.c_void_p()
+        # device input tensors whose reads may still be queued (include/svdw.h,
+        # "Lifetime of device inputs"): referenced until the context's work is
+        # known complete, so torch's allocator cannot hand their memory to a
+        # tensor written on another stream while a pipelined call still reads it
+        self._held = []
         p = Params(device, precision_bits, lookup_bits)
         check(lib().svdw_ctx_create(ct.byref(p), ct.byref(self._h)))
 
+    # above this many held tensors, a call first asks the device (svdw_query)
+    # whether the earlier calls are done; the bench's resident inputs are one set
+    HOLD_QUERY = 8
+
+    def _hold(self, *tensors) -> None:
+        """Keep device inputs alive until their readers have run (see _held)."""
+        held = self._held
+        if len(held) >= self.HOLD_QUERY:
+            rc = lib().svdw_query(self._h)
+            if rc < 0:
+                check(rc)
+            if rc == 1:
+                held.clear()
+        for t in tensors:
+            if not any(t is h for h in held):
+                held.append(t)
+
     def close(self) -> None:
         if self._h:
-            lib().svdw_ctx_destroy(self._h)
+            lib().svdw_ctx_destroy(self._h)      # (waits for the context's work)
             self._h = ct.c_void_p()
+        self._held = []
 
     def __del__(self):  # pragma: no cover - best effort
         try:
@@ -139,13 +162,24 @@ class Context:
         return self._h
 
     def reset(self) -> None:
-        check(lib().svdw_ctx_reset(self._h))
+        check(lib().svdw_ctx_reset(self._h))     # (synchronises)
+        self._held.clear()
 
     def reserve(self, phase: int, advice: int, lookups: int) -> None:
         check(lib().svdw_reserve(self._h, phase, advice, lookups))
 
     def sync(self) -> None:
         check(lib().svdw_sync(self._h))
+        self._held.clear()
+
+    def query(self) -> bool:
+        """svdw_query: has everything queued on the context completed?"""
+        rc = lib().svdw_query(self._h)
+        if rc < 0:
+            check(rc)
+        if rc == 1:
+            self._held.clear()
+        return rc == 1
 
     def advice_len(self, phase: int) -> int:
         return lib().svdw_advice_len(self._h, phase)
@@ -358,6 +392,7 @@ class ZkMatrix:
             rows, cols = matrix.shape
             _after_torch(ctx)
             check(lib().svdw_zkmatrix_new(ctx.handle, phase, dp, rows, cols, 1, ct.byref(out)))
+            ctx._hold(matrix)
         else:
             a = np.ascontiguousarray(matrix, dtype=np.float64)
             if a.ndim != 2:
@@ -416,6 +451,7 @@ class ZkVector:
         if dp is not None:
             _after_torch(ctx)
             check(lib().svdw_zkvector_new(ctx.handle, phase, dp, v.numel(), 1, ct.byref(out)))
+            ctx._hold(v)
         else:
             a = np.ascontiguousarray(v, dtype=np.float64).ravel()
             check(lib().svdw_zkvector_new(ctx.handle, phase, a.ctypes.data, a.size, 0,
@@ -598,6 +634,7 @@ def svd_witness(ctx: Context, m, u, v, d, gamma: int, cfg: SvdConfigPy = SvdConf
         N, M = m.shape
         _after_torch(ctx)
         check(lib().svdw_svd_witness(ctx.handle, *dps, N, M, 1, ct.byref(cfgc), g, ct.byref(cnt)))
+        ctx._hold(m, u, v, d)       # pipelined: the stages read them after the call returns
     else:
         arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (m, u, v, d)]
         N, M = arrs[0].shape
@@ -622,6 +659,7 @@ def verify_mul_witness(ctx: Context, a, b, gamma: int) -> dict:
             raise SvdwError(-1, "verify_mul_witness: a.num_col != b.num_rows")
         # (the hand-off to torch's stream inside the call, on the state that runs it)
         check(lib().svdw_verify_mul_witness_on(ctx.handle, _torch_stream(ctx), *dps, N, K, M, g, ct.byref(cnt)))
+        ctx._hold(a, b)             # lanes: the call still runs beside the next one
     else:
         arrs = [np.ascontiguousarray(x, dtype=np.float64) for x in (a, b)]
         (N, K), M = arrs[0].shape, arrs[1].shape[1]
@@ -687,6 +725,7 @@ def parse_svd_input_device(ctx: "Context", src):
     check(lib().svdw_parse_svd_input_device(ctx._h, t.data_ptr(), n, 0, ct.byref(dims),
                                             out["m"].data_ptr(), out["u"].data_ptr(),
                                             out["d"].data_ptr(), out["v"].data_ptr()))
+    ctx._hold(t)
     _before_torch(ctx)                  # torch kernels reading m, u, d, v run after the parse
     return out
 

@@ -93,8 +93,22 @@ int svdw_sync(svdw_ctx* ctx);
  * queued on `stream` so far. svdw_stream_signal(ctx, consumer) after a call
  * makes `stream` wait for everything the context has queued (its outputs).
  * The Python layer (halo2_svd041_amd.zk) does both around every on-device call
- * with torch's current stream. */
+ * with torch's current stream.
+ *
+ * Lifetime of device inputs. An on_device call returns before the device has
+ * read its inputs: with "pipeline" (svd_witness) the call's stage kernels and
+ * row scans read m, u, v, d straight from the f64 buffers after it returned,
+ * and with "lanes" (verify_mul_witness) the call runs beside the next one. The
+ * caller must keep every input buffer allocated and unmodified until the
+ * call's work has completed: svdw_sync(), or svdw_query() returning 1, or any
+ * stream ordered after svdw_stream_signal(ctx, stream) (a caching allocator
+ * that frees on that stream). The Python layer holds a reference to every
+ * device input tensor until svdw_query / sync / reset / close shows the work
+ * done. */
 int svdw_stream_wait(svdw_ctx* ctx, void* stream);
+/* 1 when everything queued on the context (both lanes) has completed, 0 while
+ * some of it still runs (no host wait), < 0 on error. */
+int svdw_query(svdw_ctx* ctx);
 /* Debug: the CRT GEMM's block timeline into device buffer buf (3 u64 per block:
  * start and end on the 100 MHz wall clock, XCC id << 32 | HW_ID); null: off. */
 int svdw_debug_trace(void* buf);
@@ -273,8 +287,10 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   device inputs: the products on the cell stream and the u / v bounds and u.d
  *   beside them; -1 on row-sharded contexts only);
  *   "pipeline" 1 | 0 (svd_witness with device inputs on the f64 CRT product
- *   path with the products on the cell stream, two cell sets within 60 % of
- *   the device memory: consecutive calls overlap -- a call returns with its
+ *   path with the products on the cell stream, when the second cell set is
+ *   already allocated or its growth fits in the device's free memory with 10 %
+ *   of the device to spare -- else the call runs unpipelined and the second set
+ *   is released, as it is by "pipeline" 0: consecutive calls overlap -- a call returns with its
  *   u.d / bound / diff stages and its phase-1 row scans still running on the
  *   second and third streams, and the next call's gamma tables, quantization
  *   and products start on the cell stream beside them, into the other cell
@@ -284,7 +300,9 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   between two complete context states, exchanged behind the handle at each
  *   call, so consecutive calls run beside each other on separate streams; the
  *   handle always shows the latest call's cells; svdw_sync, stream_wait /
- *   _signal, graph_stats and destroy cover both states);
+ *   _signal, graph_stats and destroy cover both states; a call stays on the
+ *   current state when the other one would have to grow beyond the device's
+ *   free memory less 10 % of the device);
  *   "graph" 1 | 0: svdw_verify_mul_witness with device inputs replays a HIP graph
  *   of its launch sequence. The second call of a key (N, K, M, the input
  *   pointers, no allocation or option change since) is captured, later calls
@@ -304,7 +322,12 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   the d checks and constant cells on the second stream, m, u, v, d quantized
  *   in one launch with the bit-length words folded inside it, b.g of a
  *   row-sharded rank from the f64 inputs, 4 KiB-aligned stage store windows,
- *   GEMM sizes decided on the device. */
+ *   GEMM sizes decided on the device.
+ * Retired options (accepted and ignored, so callers written against round 3
+ *   keep running; to be removed with the next ABI version): "bits_fold",
+ *   "bounds_after", "colsum", "d_checks_aside", "dep_values", "fused_quantize",
+ *   "gemm_batch", "gemm_priority", "gemm_rt", "prelaunch_at", "prod_blocks",
+ *   "prod_first", "res_first", "stage_align", "stage_priority", "stage_probe". */
 int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);
 /* Captures and replays of the verify_mul_witness graph ("graph") so far. */
 int svdw_graph_stats(svdw_ctx* ctx, uint64_t* captures, uint64_t* replays);

@@ -198,9 +198,12 @@ def test_lanes_back_to_back_then_svd(gpu_ctx_factory):
 @pytest.mark.gpu
 def test_pipelined_svd_and_lanes_interleaved(gpu_ctx_factory):
     """svd_witness (pipelined, alternating cell sets and gamma tables) and
-    verify_mul_witness (two lanes, captured graphs) interleaved on one handle
-    without a host wait, six rounds: each call's cells are the oracle's when
-    read right after it, and the last of each kind again at the end."""
+    verify_mul_witness (two lanes, captured graphs) interleaved on one handle,
+    six rounds, with no host wait except where cells are read: the svd
+    witness is read (and compared with the oracle) right after its call in
+    rounds 2 and 5, the verify_mul witness right after its call in rounds 1
+    and 4 (each read synchronises the handle; the other rounds run back to
+    back), and the last svd witness again at the end."""
     import torch
     import halo2_svd041_amd as hs
     from conftest import gen_svd_input
@@ -213,6 +216,10 @@ def test_pipelined_svd_and_lanes_interleaved(gpu_ctx_factory):
                       for x in (mm, u, v, d))
     for r in range(6):
         hs.svd_witness(ctx, dm, du, dv, dd, gamma_for(970 + r))
+        if r in (2, 5):
+            s0, sl0, s1 = corc.svd_witness(mm, u, v, d, P, 19, gamma_for(970 + r))
+            assert np.array_equal(ctx.advice(0), s0) and np.array_equal(ctx.advice(1), s1), r
+            assert np.array_equal(ctx.lookups(0), sl0), r
         hs.verify_mul_witness(ctx, ta, tb, gamma_for(980 + r))
         if r in (1, 4):
             c0, c1 = corc.verify_mul_witness(a, b, P, gamma_for(980 + r))

@@ -564,6 +564,71 @@ def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device, hol
     assert walk_window(ctx.layout(), get, {(0, 0): a0, (0, 1): l0, (1, 0): a1}, 0, row_lim) > 0
 
 
+@pytest.mark.parametrize("shapes,P,row_begin,row_lim,hold", [
+    (((1024, 1024),) * 3, 63, 500, 24, 0),
+    (((1024, 1024),) * 3, 63, 1000, 24, 3000),
+    (((512, 512), (512, 512), (2048, 1024)), 32, 300, 16, 0),
+])
+def test_pipelined_full_size_parity(gpu_ctx_factory, shapes, P, row_begin, row_lim, hold):
+    """The bench's own regime at full size: device-input svd_witness calls
+    queued back to back with no host wait, each with its own inputs and gamma
+    (call j + 1's quantization, residues, GEMM and combine run beside call j's
+    stage kernels and row scans, and call j + 2 reuses call j's cell set behind
+    its tail events). The last witness is then walked against the C oracle in a
+    row window away from the top rows: every load, d check and gamma power,
+    and rows [row_begin, row_begin + row_lim) of every row-parallel region.
+    hold: every call's streams also wait behind a spinning kernel, so each
+    call's launches sit fully queued before any of them runs. The third case
+    changes the shape inside the pipeline (two 512^2 then 2048 x 1024)."""
+    import halo2_svd041_amd as hs
+    from conftest import walk_window
+    ctx = gpu_ctx_factory(P)
+    if hold:
+        ctx.set_option("hold_us", hold)
+    ins = []
+    for k, (N, M) in enumerate(shapes):
+        m, u, d, v = gen_svd_input(N, M, seed=7000 + 31 * k + N + P)
+        ins.append((m, u, d, v, gamma_for(7100 + k)))
+    devs = [_on_device(m, u, v, d) for m, u, d, v, _ in ins]
+    for (m, u, d, v, g), dv in zip(ins, devs):
+        hs.svd_witness(ctx, *dv, g)                   # no host wait in between
+    ctx.sync()
+    m, u, d, v, g = ins[-1]
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g, row_lim=row_lim, row_begin=row_begin)
+    get = lambda ph, lk, off, n: (ctx.lookups if lk else ctx.advice)(ph, off, n)   # noqa: E731
+    assert walk_window(ctx.layout(), get, {(0, 0): a0, (0, 1): l0, (1, 0): a1}, row_begin, row_lim) > 0
+
+
+def test_device_input_lifetime(gpu_ctx_factory):
+    """Device inputs passed as temporaries (include/svdw.h, "Lifetime of device
+    inputs"): the call returns while its kernels are still held behind a
+    spinning kernel, the caller drops the tensors, and torch immediately
+    allocates tensors of the same sizes and fills them with other values on its
+    own stream (which does not wait for the engine). The Python layer keeps the
+    inputs referenced until the work is done, so torch cannot hand out their
+    memory: the witness still equals the oracle's for the original inputs."""
+    import torch
+    import halo2_svd041_amd as hs
+    N, M, P = 192, 160, 63
+    ctx = gpu_ctx_factory(P)
+    m2, u2, d2, v2 = gen_svd_input(N, M, seed=91)
+    for k in range(2):                                # every buffer allocated (both cell sets)
+        hs.svd_witness(ctx, *_on_device(m2, u2, v2, d2), gamma_for(92 + k))
+    ctx.sync()
+    ctx.reset()
+    ctx.set_option("hold_us", 20000)
+    m, u, d, v = gen_svd_input(N, M, seed=93)
+    g = gamma_for(94)
+    hs.svd_witness(ctx, *_on_device(m, u, v, d), g)   # the tensors are temporaries
+    dev = torch.device("cuda", 0)
+    junk = [torch.full(x.shape, -1.0e30, dtype=torch.float64, device=dev) for x in (m, u, v, d)]
+    assert not ctx.query()                            # the witness is still held
+    ctx.sync()
+    del junk
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+    _assert_streams(ctx, a0, l0, a1)
+
+
 @pytest.mark.parametrize("rank,opts", [(0, {}), (3, {}), (7, {}),
                                        (3, {"overlap": 0, "phase1_overlap": 0})])
 def test_full_size_shard_rank_parity(gpu_ctx_factory, rank, opts):
