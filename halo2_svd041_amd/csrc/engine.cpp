@@ -483,13 +483,14 @@ struct svdw_ctx {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
-    uint32_t stage_flags = STAGE_ALIGN;     // STAGE_* (4 KiB-aligned block store windows)
+    uint32_t stage_flags = STAGE_ALIGN | STAGE_CELL;   // STAGE_* (aligned block store windows, whole-cell lanes)
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
     // "stage_occ": blocks per CU of the persistent stage streamer (k_stage_pers);
     // 0: the one-block-per-chunk kernels (k_stage / k_stage_multi). Its tile
     // counters: one 256-byte slot per stream (cell stream, st2, st3), zero
     // between launches (each launch's last block resets its slot).
-    uint32_t stage_occ = 2;
+    uint32_t stage_occ = 0;
+    uint32_t stage_waves = 4;               // "stage_waves": 4 or 8 waves per persistent block
     DBuf stage_ctr;
     hipStream_t stream_id[3] = {};          // st, st2, st3 as created (st / st2 / st3 are swapped at times)
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
@@ -617,6 +618,14 @@ struct svdw_ctx {
     // same key; gamma enters only through k_gamma_prep, launched eagerly on st
     // ahead of the graph (gp_external), so the graph itself is gamma-free.
     int graph_vm = 1;                       // "graph": 0 off, 1 verify_mul_witness
+    // "vm_linear": the captured verify_mul_witness runs on the context stream
+    // alone (st2 = st3 = st while it is queued: a linear graph, no fork / join
+    // events); concurrency comes from the two lanes instead. `linear` is set
+    // while such a call is queued: stream_dep returns lin_ev (never recorded)
+    // and dep_wait skips it.
+    int vm_linear = 1;
+    bool linear = false;
+    hipEvent_t lin_ev = nullptr;
     bool capturing = false;                 // st is capturing: no allocation, no sync
     bool gp_external = false;               // verify_mul_witness: k_gamma_prep already queued
     const Fr* gp_ext_one = nullptr;         // the one cell it wrote (null: none)
@@ -686,6 +695,10 @@ static void release_alt(svdw_ctx* c) {
 // 0.417 -> 0.444 ms and 1024^2 2.078 -> 2.100 ms, 8-way ranks unchanged --
 // HIP runs those waits and writes as kernels of their own -- so it was removed.)
 static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
+    if (c->linear) {                                   // one stream: order is implicit
+        flush_batch(c, from);
+        return c->lin_ev;
+    }
     if (c->dep_next == c->deps.size()) {
         hipEvent_t e;
         // same-device consumer only: agent-scope release, no system-scope writeback
@@ -701,7 +714,8 @@ static hipEvent_t stream_dep(svdw_ctx* c, hipStream_t from, hipStream_t to) {
     return e;
 }
 // `s` waits for a dependency stream_dep returned (or any other event)
-static void dep_wait(svdw_ctx*, hipStream_t s, hipEvent_t e) {
+static void dep_wait(svdw_ctx* c, hipStream_t s, hipEvent_t e) {
+    if (c->linear && e == c->lin_ev) return;
     hipck(hipStreamWaitEvent(s, e, 0), "hipStreamWaitEvent");
 }
 // (Round 4 removed "gemm_priority", a high-priority second stream at 512 <=
@@ -794,9 +808,11 @@ struct ProfScope {
         if (!c->prof || c->dry) return;
         if (!c->prof_filter.empty() && name.compare(0, c->prof_filter.size(), c->prof_filter) != 0)
             return;
-        // launches on the cell stream (the phase-0 critical path of svd_witness)
-        // are tagged, so a bench can report their rate beside the all-stream average
-        svdw_ctx::Rec r{s == c->st_cell ? name + "@cell" : name, bytes, ops, ev(c), ev(c)};
+        // every launch is tagged with its stream (@cell, @s2, @s3 as created), so a
+        // bench can report the busiest stream's stage rate beside the all-stream one
+        const char* tag = s == c->stream_id[0] ? "@cell" : s == c->stream_id[1] ? "@s2"
+                          : s == c->stream_id[2] ? "@s3" : "";
+        svdw_ctx::Rec r{name + tag, bytes, ops, ev(c), ev(c)};
         hipck(hipEventRecord(r.e0, s), "hipEventRecord");
         c->recs.push_back(r);
         idx = (long)c->recs.size() - 1;
@@ -1056,7 +1072,7 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     {
         ProfScope ps(c, c->st, std::string("k_stage:") + tag, bytes, 0);
         const StageArgs* one = &a;
-        hipck(launch_stage_pers(&one, 1, c->st, stage_ctr_for(c, c->st), c->stage_occ), "k_stage");
+        hipck(launch_stage_pers(&one, 1, c->st, stage_ctr_for(c, c->st), c->stage_occ, c->stage_waves), "k_stage");
     }
 }
 // Issue a stream's pending batched stages (k_stage_multi; one program: k_stage).
@@ -1091,7 +1107,7 @@ static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter, hipEvent
                 fprintf(stderr, "\n");
             }
             ProfScope pr(c, s, name, bytes, 0, true);
-            hipck(launch_stage_pers(ps.data(), (int)ps.size(), s, stage_ctr_for(c, s), c->stage_occ),
+            hipck(launch_stage_pers(ps.data(), (int)ps.size(), s, stage_ctr_for(c, s), c->stage_occ, c->stage_waves),
                   "k_stage_multi");
         }
     }
@@ -3160,6 +3176,7 @@ static void ctx_release(svdw_ctx* c) {
         for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
         for (auto e : c->pool) (void)hipEventDestroy(e);
         for (auto e : c->deps) (void)hipEventDestroy(e);
+        if (c->lin_ev) (void)hipEventDestroy(c->lin_ev);
         for (hipStream_t t : {c->st3, c->st2, c->st_cell ? c->st_cell : c->st})
             if (t) (void)hipStreamDestroy(t);
     }
@@ -3204,21 +3221,23 @@ static void ctx_init_device(svdw_ctx* c) {
 // The settings (options, shard, profiler) of `s` onto the lane `d`; a change
 // bumps the lane's epoch (its captured graph no longer applies).
 static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
-    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->stage_occ, s->gemm_crt, s->res_f64,
+    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->stage_occ, s->stage_waves, s->gemm_crt, s->res_f64,
                          s->phase1_overlap, s->prod_cell, s->hold_us, s->rlc_prefix, s->p1_at,
-                         s->f64_views, s->overlap, s->stage_batch, s->graph_vm, s->pipeline,
+                         s->f64_views, s->overlap, s->stage_batch, s->graph_vm, s->vm_linear, s->pipeline,
                          s->shard_rank, s->shard_world, s->prof, s->host_trace};
-    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->stage_occ, d->gemm_crt, d->res_f64,
+    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->stage_occ, d->stage_waves, d->gemm_crt, d->res_f64,
                          d->phase1_overlap, d->prod_cell, d->hold_us, d->rlc_prefix, d->p1_at,
-                         d->f64_views, d->overlap, d->stage_batch, d->graph_vm, d->pipeline,
+                         d->f64_views, d->overlap, d->stage_batch, d->graph_vm, d->vm_linear, d->pipeline,
                          d->shard_rank, d->shard_world, d->prof, d->host_trace};
     if (!memcmp(a, b, sizeof a) && d->prof_filter == s->prof_filter) return;
     d->gemm_impl = s->gemm_impl; d->stage_flags = s->stage_flags; d->stage_elems = s->stage_elems;
     d->stage_occ = s->stage_occ;
+    d->stage_waves = s->stage_waves;
     d->gemm_crt = s->gemm_crt; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
     d->prod_cell = s->prod_cell; d->hold_us = s->hold_us; d->rlc_prefix = s->rlc_prefix;
     d->p1_at = s->p1_at; d->f64_views = s->f64_views; d->overlap = s->overlap;
     d->stage_batch = s->stage_batch; d->graph_vm = s->graph_vm; d->pipeline = s->pipeline;
+    d->vm_linear = s->vm_linear;
     d->shard_rank = s->shard_rank; d->shard_world = s->shard_world; d->prof = s->prof;
     d->host_trace = s->host_trace; d->prof_filter = s->prof_filter;
     ++d->epoch;
@@ -3268,6 +3287,26 @@ static svdw_counts verify_mul_witness_api(svdw_ctx* c, const double* a, const do
         return verify_mul_witness(c, a, b, N, K, M, on_device, gamma);
     }
     c->ht0 = std::chrono::steady_clock::now();
+    settle(c);                     // (before any linear scope: it waits on tail events)
+    struct Linear {                // vm_linear: every launch of the call on st
+        svdw_ctx* c;
+        hipStream_t s2 = nullptr, s3 = nullptr;
+        bool on = false;
+        explicit Linear(svdw_ctx* cc) : c(cc) {
+            if (!c->vm_linear) return;
+            if (!c->lin_ev) hipck(hipEventCreateWithFlags(&c->lin_ev, hipEventDisableTiming), "hipEventCreate");
+            s2 = c->st2;
+            s3 = c->st3;
+            c->st2 = c->st3 = c->st;
+            c->linear = on = true;
+        }
+        ~Linear() {
+            if (!on) return;
+            c->st2 = s2;
+            c->st3 = s3;
+            c->linear = false;
+        }
+    } lin{c};
     struct Flags {
         svdw_ctx* c;
         ~Flags() {
@@ -4509,6 +4548,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
                 release_alt(c);
                 if (c->lane) release_alt(c->lane);
             }
+        } else if (n == "vm_linear") {               // captured verify_mul_witness on one stream
+            REQUIRE(value == 0 || value == 1, "vm_linear: 0 or 1");
+            c->vm_linear = (int)value;
         } else if (n == "graph") {                   // captured verify_mul_witness (vm_graph)
             REQUIRE(value == 0 || value == 1, "graph: 0 or 1");
             c->graph_vm = (int)value;
@@ -4518,6 +4560,11 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "stage_occ") {               // persistent stage streamer (0: off)
             REQUIRE(value >= 0 && value <= 8, "stage_occ: 0..8 blocks per CU");
             c->stage_occ = (uint32_t)value;
+        } else if (n == "stage_cell") {              // phase B: a whole cell per lane (else half cells)
+            c->stage_flags = value ? (c->stage_flags | STAGE_CELL) : (c->stage_flags & ~STAGE_CELL);
+        } else if (n == "stage_waves") {
+            REQUIRE(value == 4 || value == 8, "stage_waves: 4 or 8");
+            c->stage_waves = (uint32_t)value;
         } else if (n == "stage_elems") {
             REQUIRE(value >= 16 && value <= 256 && value % 16 == 0,
                     "stage_elems: a multiple of 16 in [16, 256]");

@@ -401,6 +401,68 @@ __device__ __forceinline__ void stream_cells_desc(uint4* __restrict__ out, uint3
     }
 }
 
+// Phase B, one whole cell per lane (STAGE_CELL): a lane reads the cell's
+// descriptor and two mask words (per slot, built once per block), the nine
+// source words and writes the cell as two 16-B stores; a wave covers 64
+// consecutive cells (2 KiB) and the block's rounds whole 8 KiB windows. Half
+// the descriptor, mask and index work per byte of the half-cell form above.
+template <bool ALIGN>
+__device__ __forceinline__ void stream_cells_cell(uint4* __restrict__ out, uint32_t total,
+                                                  const uint32_t* __restrict__ sD,
+                                                  const uint4* __restrict__ sM, uint32_t C, uint32_t magic,
+                                                  const uint32_t* smem, uint32_t vbase0, uint32_t nv) {
+    const uint32_t step = blockDim.x;
+    const uint32_t dq = step / C, dr = step - dq * C, ev = stage_elem_words(nv);
+    uint32_t c0 = threadIdx.x;
+    if (ALIGN) {
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) >> 5) & (blockDim.x - 1);
+        c0 = threadIdx.x >= mis ? threadIdx.x - mis : threadIdx.x + blockDim.x - mis;
+    }
+    uint32_t el = fastdiv(c0, C, magic), slot = c0 - el * C;
+    uint32_t vbase = vbase0 + el * ev;
+    for (uint32_t c = c0; c < total; c += step) {
+        const uint32_t d = sD[slot];
+        const uint4 m0 = sM[2 * slot], m1 = sM[2 * slot + 1];
+        const uint32_t* x = smem + ((d & kHalfElem) ? vbase : 0u) + (d & 0xffffu);
+        const uint32_t r = (d >> 16) & 31u;
+        uint32_t w[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) w[i] = x[i];
+        out[2 * c] = make_uint4(__builtin_amdgcn_alignbit(w[1], w[0], r) & m0.x,
+                                __builtin_amdgcn_alignbit(w[2], w[1], r) & m0.y,
+                                __builtin_amdgcn_alignbit(w[3], w[2], r) & m0.z,
+                                __builtin_amdgcn_alignbit(w[4], w[3], r) & m0.w);
+        out[2 * c + 1] = make_uint4(__builtin_amdgcn_alignbit(w[5], w[4], r) & m1.x,
+                                    __builtin_amdgcn_alignbit(w[6], w[5], r) & m1.y,
+                                    __builtin_amdgcn_alignbit(w[7], w[6], r) & m1.z,
+                                    __builtin_amdgcn_alignbit(w[8], w[7], r) & m1.w);
+        slot += dr;
+        vbase += dq * ev;
+        if (slot >= C) {
+            slot -= C;
+            vbase += ev;
+        }
+    }
+}
+// Descriptor and masks of a whole cell of a slot (STAGE_CELL; see half_desc):
+// d = source word of the cell's window, m[0..1] = its eight mask words.
+__device__ __forceinline__ void make_cell(const SlotOp op, uint32_t* d, uint4* m) {
+    const uint32_t lo = op.lo;
+    uint32_t nb = op.nbits ? op.nbits : 256u;
+    nb = min(nb, 256u - lo);
+    const bool elem = op.src < KSRC;
+    const uint32_t base = (elem ? op.src : op.src - KSRC) * VW;
+    *d = half_desc(base + (lo >> 5), lo & 31u, elem);
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int keep = (int)nb - 32 * i;
+        w[i] = keep >= 32 ? 0xffffffffu : (keep <= 0 ? 0u : ((1u << keep) - 1u));
+    }
+    m[0] = make_uint4(w[0], w[1], w[2], w[3]);
+    m[1] = make_uint4(w[4], w[5], w[6], w[7]);
+}
+
 // Descriptor and masks of half h of a slot (see half_desc).
 __device__ __forceinline__ void make_half(const SlotOp op, uint32_t h, uint32_t* d, uint4* m) {
     const uint32_t lo = op.lo;
@@ -630,9 +692,14 @@ __device__ __forceinline__ void stage_setup(const StageArgs& a, const StageLds& 
     for (uint32_t k = tid; k < a.L; k += blockDim.x) L.sLk[k] = lk[k];
     for (uint32_t k = tid; k < a.nmo; k += blockDim.x) L.sMo[k] = mo[k];
     if (tid < kMaxViews) L.sVw[tid] = a.view[tid];
-    for (uint32_t k = tid; k < 2 * (a.C + a.L); k += blockDim.x) {
-        const uint32_t sl = k >> 1;
-        make_half(sl < a.C ? adv[sl] : lk[sl - a.C], k & 1, L.sHD + k, L.sHM + k);
+    if (a.flags & STAGE_CELL) {
+        for (uint32_t k = tid; k < a.C + a.L; k += blockDim.x)
+            make_cell(k < a.C ? adv[k] : lk[k - a.C], L.sHD + k, L.sHM + 2 * k);
+    } else {
+        for (uint32_t k = tid; k < 2 * (a.C + a.L); k += blockDim.x) {
+            const uint32_t sl = k >> 1;
+            make_half(sl < a.C ? adv[sl] : lk[sl - a.C], k & 1, L.sHD + k, L.sHM + k);
+        }
     }
 }
 // This thread's in-bounds strided view loads of block blk's element.
@@ -686,6 +753,13 @@ __device__ __forceinline__ void stage_chunk(const StageArgs& a, const StageLds& 
     uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
     uint4* outL = a.L ? reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L) : nullptr;
     const uint32_t vb0 = (uint32_t)(L.sV - smem);
+    if (a.flags & STAGE_CELL) {
+        stream_cells_cell<true>(outA, ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv);
+        if (a.L)
+            stream_cells_cell<true>(outL, ne * a.L, L.sHD + a.C, L.sHM + 2 * a.C, a.L, a.ldiv_magic, smem, vb0,
+                                    nv);
+        return;
+    }
     stream_cells_desc<true>(outA, 2 * ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv);
     if (a.L)
         stream_cells_desc<true>(outL, 2 * ne * a.L, L.sHD + 2 * a.C, L.sHM + 2 * a.C, a.L, a.ldiv_magic, smem,
@@ -843,6 +917,10 @@ struct PersSet {
     DView* vw;
     uint32_t* D;         // descriptors
 };
+// (base = smem + a word offset: pointers kept as offsets from the LDS array,
+// never selected from an array of pointers, stay in the LDS address space --
+// a selected pointer becomes a flat pointer, and flat loads count against the
+// store counter: every LDS read would then wait for the stores in flight)
 __device__ __forceinline__ PersSet pers_set(uint32_t* base, uint32_t cl) {
     PersSet s;
     s.K = base;
@@ -941,38 +1019,35 @@ struct SrcSingle {
     __device__ uint32_t prog_of(uint32_t) const { return 0; }
     __device__ Rec rec(uint32_t) const { return Rec{a, a->mo, a->adv, a->lk, a->K}; }
 };
-template <class SRC>
+// Roles: wave 0 is the producer (phase A of the next tile, the view loads of
+// the one after, the dequeue of the one after that), waves 1..NW-1 the
+// consumers (phase B). The producer issues no stores, so its waits (for its
+// loads and its dequeue) never wait for the stores in flight; it issues each
+// load and dequeue one tile before it uses the result.
+template <int NW, class SRC>
 __device__ __forceinline__ void stage_persist(const SRC& S, const PersCtl& pc) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     __shared__ uint32_t sTile[2], sSet[2], sRound[2], sProg[2];
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t T = S.t0(S.nprog());
-    const uint32_t sw = pers_set_words(pc.cl), bw = kPersTile * pc.ev + 16;
-    uint32_t* const setb[2] = {smem, smem + sw};
-    uint32_t* const bufb[2] = {smem + 2 * sw, smem + 2 * sw + bw};
-    // wave 0's look-ahead: tile n1 (its loads f1 in flight), tile n2 (dequeued)
-    uint32_t n1 = 0, n2 = 0;
+    const uint32_t sw = pers_set_words(pc.cl), bw = kPersTile * pc.ev + 16, ev = pc.ev, cl = pc.cl;
+    // word offsets of table set s and element buffer b (see pers_set)
+    auto set_off = [&](uint32_t s) { return s ? sw : 0u; };
+    auto buf_off = [&](uint32_t b) { return 2 * sw + (b ? bw : 0u); };
+    // producer look-ahead: tile n1 (its loads f1 in flight), tile n2 (known),
+    // the dequeue of the tile after n2 in flight (n3v, lane 0)
+    uint32_t n1 = 0, n2 = 0, n3v = 0;
     Prefetch f1{fr_zero(), fr_zero(), false, false};
-    auto dequeue = [&]() -> uint32_t {
-        uint32_t t = 0;
-        if (lane == 0) t = atomicAdd(pc.ctr, 1u);
-        return __builtin_amdgcn_readfirstlane(t);
-    };
-    // element range of tile t (program p)
-    auto tile_elems = [&](uint32_t t, uint32_t p, const StageArgs& a, uint32_t* e0, uint32_t* ne) {
-        *e0 = a.e_begin + (t - S.t0(p)) * kPersTile;
-        *ne = min(kPersTile, a.e_end - *e0);
-    };
     auto issue_loads = [&](uint32_t t) {
         if (t >= T) { f1 = Prefetch{fr_zero(), fr_zero(), false, false}; return; }
         const uint32_t p = S.prog_of(t);
         const Rec q = S.rec(p);
-        uint32_t e0, ne;
-        tile_elems(t, p, *q.a, &e0, &ne);
+        const uint32_t e0 = q.a->e_begin + (t - S.t0(p)) * kPersTile;
+        const uint32_t ne = min(kPersTile, q.a->e_end - e0);
         f1 = pers_loads(*q.a, e0 + lane, lane < ne);
     };
-    // phase A of tile t into buffer b (wave 0): tables into the set that does
-    // not hold the current tile's program unless it is the same program
+    // phase A of tile t into buffer b: its program's tables go into the set
+    // the current tile does not use, unless it is the same program
     auto phase_a = [&](uint32_t t, uint32_t b, uint32_t cur_set) {
         if (t >= T) {
             if (lane == 0) sTile[b] = T;
@@ -984,16 +1059,16 @@ __device__ __forceinline__ void stage_persist(const SRC& S, const PersCtl& pc) {
         if (sProg[s] != p) {
             s ^= 1u;
             if (sProg[s] != p) {
-                pers_tables(q, pers_set(setb[s], pc.cl), lane);
+                pers_tables(q, pers_set(smem + set_off(s), cl), lane);
                 if (lane == 0) sProg[s] = p;
             }
         }
-        const PersSet ts = pers_set(setb[s], pc.cl);
-        uint32_t e0, ne;
-        tile_elems(t, p, *q.a, &e0, &ne);
+        const PersSet ts = pers_set(smem + set_off(s), cl);
+        const uint32_t e0 = q.a->e_begin + (t - S.t0(p)) * kPersTile;
+        const uint32_t ne = min(kPersTile, q.a->e_end - e0);
         if (lane < ne)
-            element_program(*q.a, e0 + lane, bufb[b] + lane * pc.ev, ts.K, ts.mo, ts.vw, f1.v0, f1.in0, f1.v1,
-                            f1.in1);
+            element_program(*q.a, e0 + lane, smem + buf_off(b) + lane * ev, ts.K, ts.mo, ts.vw, f1.v0, f1.in0,
+                            f1.v1, f1.in1);
         if (lane == 0) {
             sTile[b] = t;
             sSet[b] = s;
@@ -1005,12 +1080,19 @@ __device__ __forceinline__ void stage_persist(const SRC& S, const PersCtl& pc) {
     }
     __syncthreads();
     if (wave == 0) {
-        const uint32_t t0 = dequeue();
-        n1 = dequeue();
-        n2 = dequeue();
+        uint32_t t0 = 0, t1 = 0, t2 = 0;
+        if (lane == 0) {
+            t0 = atomicAdd(pc.ctr, 1u);
+            t1 = atomicAdd(pc.ctr, 1u);
+            t2 = atomicAdd(pc.ctr, 1u);
+        }
+        t0 = __builtin_amdgcn_readfirstlane(t0);
+        n1 = __builtin_amdgcn_readfirstlane(t1);
+        n2 = __builtin_amdgcn_readfirstlane(t2);
         issue_loads(t0);
         phase_a(t0, 0, 0);
         issue_loads(n1);
+        if (lane == 0) n3v = atomicAdd(pc.ctr, 1u);
     }
     __syncthreads();
     for (uint32_t k = 0;; ++k) {
@@ -1019,46 +1101,53 @@ __device__ __forceinline__ void stage_persist(const SRC& S, const PersCtl& pc) {
         if (cur >= T) break;                                        // (uniform)
         const uint32_t cset = sSet[b];
         if (wave == 0) {
+            // ---- producer: the next tile's phase A into the other buffer
             if (lane == 0) sRound[b ^ 1u] = 0;
-            phase_a(n1, b ^ 1u, cset);                              // the next tile, other buffer
+            phase_a(n1, b ^ 1u, cset);
             n1 = n2;
+            n2 = __builtin_amdgcn_readfirstlane(n3v);               // (returned during phase A's waits)
             issue_loads(n1);
-            n2 = dequeue();
-        }
-        // ---- phase B of the current tile: 2 KiB rounds from the LDS counter
-        const uint32_t p = S.prog_of(cur);
-        const Rec q = S.rec(p);
-        const StageArgs& a = *q.a;
-        uint32_t e0, ne;
-        tile_elems(cur, p, a, &e0, &ne);
-        const PersSet ts = pers_set(setb[cset], pc.cl);
-        uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
-        const uint32_t totA = ne * a.C, misA = (uint32_t)(reinterpret_cast<uintptr_t>(outA) >> 5) & 63u;
-        const uint32_t RA = (totA + misA + 63) / 64;
-        uint4* outL = nullptr;
-        uint32_t totL = 0, misL = 0, RL = 0;
-        if (a.L) {
-            outL = reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L);
-            totL = ne * a.L;
-            misL = (uint32_t)(reinterpret_cast<uintptr_t>(outL) >> 5) & 63u;
-            RL = (totL + misL + 63) / 64;
-        }
-        const uint32_t* buf = bufb[b];
-        for (;;) {
-            uint32_t r = 0;
-            if (lane == 0) r = atomicAdd(&sRound[b], 1u);
-            r = __builtin_amdgcn_readfirstlane(r);
-            if (r >= RA + RL) break;
-            if (r < RA)
-                pers_round(outA, totA, misA, r, a.C, a.cdiv_magic, ts.D, ts.M, buf, ts.K, pc.ev, lane);
-            else
-                pers_round(outL, totL, misL, r - RA, a.L, a.ldiv_magic, ts.D + a.C, ts.M + 2 * a.C, buf, ts.K,
-                           pc.ev, lane);
+            if (lane == 0) n3v = atomicAdd(pc.ctr, 1u);
+        } else {
+            // ---- consumers: the current tile's cells, 2 KiB rounds from the LDS counter
+            const uint32_t p = S.prog_of(cur);
+            const Rec q = S.rec(p);
+            const uint32_t C = q.a->C, L = q.a->L, cmag = q.a->cdiv_magic, lmag = q.a->ldiv_magic;
+            const uint32_t e0 = q.a->e_begin + (cur - S.t0(p)) * kPersTile;
+            const uint32_t ne = min(kPersTile, q.a->e_end - e0);
+            const PersSet ts = pers_set(smem + set_off(cset), cl);
+            uint4* outA = reinterpret_cast<uint4*>(q.a->out_adv + (uint64_t)e0 * C);
+            const uint32_t totA = ne * C, misA = (uint32_t)(reinterpret_cast<uintptr_t>(outA) >> 5) & 63u;
+            const uint32_t RA = (totA + misA + 63) / 64;
+            uint4* outL = nullptr;
+            uint32_t totL = 0, misL = 0, RL = 0;
+            if (L) {
+                outL = reinterpret_cast<uint4*>(q.a->out_lk + (uint64_t)e0 * L);
+                totL = ne * L;
+                misL = (uint32_t)(reinterpret_cast<uintptr_t>(outL) >> 5) & 63u;
+                RL = (totL + misL + 63) / 64;
+            }
+            const uint32_t* buf = smem + buf_off(b);
+            auto grab = [&]() -> uint32_t {
+                uint32_t r = 0;
+                if (lane == 0) r = atomicAdd(&sRound[b], 1u);
+                return __builtin_amdgcn_readfirstlane(r);
+            };
+            for (uint32_t r = grab(); r < RA + RL;) {
+                const uint32_t rn = grab();                         // the next round, while this one runs
+                if (r < RA)
+                    pers_round(outA, totA, misA, r, C, cmag, ts.D, ts.M, buf, ts.K, ev, lane);
+                else
+                    pers_round(outL, totL, misL, r - RA, L, lmag, ts.D + C, ts.M + 2 * C, buf, ts.K, ev, lane);
+                r = rn;
+            }
         }
         __syncthreads();
     }
     // the last block out resets the counters for the next launch on this stream
+    // (after the producer's last dequeue has returned)
     if (tid == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t done = atomicAdd(pc.ctr + 1, 1u);
         if (done == gridDim.x - 1) {
             atomicExch(pc.ctr, 0u);
@@ -1067,10 +1156,16 @@ __device__ __forceinline__ void stage_persist(const SRC& S, const PersCtl& pc) {
     }
 }
 __global__ __launch_bounds__(256) void k_stage_pers(const StageArgs a, const PersCtl pc, uint32_t ntiles) {
-    stage_persist(SrcSingle{&a, ntiles}, pc);
+    stage_persist<4>(SrcSingle{&a, ntiles}, pc);
 }
 __global__ __launch_bounds__(256) void k_stage_pers_multi(const StageMulti m, const PersCtl pc) {
-    stage_persist(SrcMulti{&m}, pc);
+    stage_persist<4>(SrcMulti{&m}, pc);
+}
+__global__ __launch_bounds__(512) void k_stage_pers8(const StageArgs a, const PersCtl pc, uint32_t ntiles) {
+    stage_persist<8>(SrcSingle{&a, ntiles}, pc);
+}
+__global__ __launch_bounds__(512) void k_stage_pers8_multi(const StageMulti m, const PersCtl pc) {
+    stage_persist<8>(SrcMulti{&m}, pc);
 }
 static int g_cus = 0;
 static uint32_t pers_grid(uint32_t ntiles, uint32_t occ) {
@@ -1082,8 +1177,10 @@ static uint32_t pers_grid(uint32_t ntiles, uint32_t occ) {
     }
     return std::max(1u, std::min(ntiles, occ * (uint32_t)g_cus));
 }
-hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t st, uint32_t* ctr, uint32_t occ) {
+hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t st, uint32_t* ctr, uint32_t occ,
+                             uint32_t waves) {
     if (!ctr || !occ) return launch_stage_multi(progs, n, st);
+    if (waves != 4 && waves != 8) return hipErrorInvalidValue;
     StageMulti m;
     m.nprog = 0;
     uint32_t used = 0, tiles = 0, cl = 0, ev = 0;
@@ -1096,10 +1193,16 @@ hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t s
             if (lds > 160u * 1024u) return hipErrorInvalidValue;
             const uint32_t grid = pers_grid(tiles, occ);
             if (m.nprog == 1) {
-                hipLaunchKernelGGL(k_stage_pers, dim3(grid), dim3(256), lds, st, *single, pc, tiles);
+                if (waves == 8)
+                    hipLaunchKernelGGL(k_stage_pers8, dim3(grid), dim3(512), lds, st, *single, pc, tiles);
+                else
+                    hipLaunchKernelGGL(k_stage_pers, dim3(grid), dim3(256), lds, st, *single, pc, tiles);
             } else {
                 m.blk0[m.nprog] = tiles;
-                hipLaunchKernelGGL(k_stage_pers_multi, dim3(grid), dim3(256), lds, st, m, pc);
+                if (waves == 8)
+                    hipLaunchKernelGGL(k_stage_pers8_multi, dim3(grid), dim3(512), lds, st, m, pc);
+                else
+                    hipLaunchKernelGGL(k_stage_pers_multi, dim3(grid), dim3(256), lds, st, m, pc);
             }
             e = hipGetLastError();
         }

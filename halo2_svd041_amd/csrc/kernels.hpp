@@ -244,7 +244,9 @@ hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t 
 // blocks per CU taking 64-element tiles from the counters at ctr (two words,
 // zero between launches; one slot per stream: launches on one stream never
 // overlap). ctr null or occ 0: launch_stage_multi.
-hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t st, uint32_t* ctr, uint32_t occ);
+// waves: 4 or 8 per block (one producer wave, the rest consumers).
+hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t st, uint32_t* ctr, uint32_t occ,
+                             uint32_t waves);
 // does the record of `a` fit one k_stage_multi launch?
 bool stage_multi_fits(const StageArgs& a);
 // max over the view of bit-length(|signed(x)|): out[b] = max of block b

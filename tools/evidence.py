@@ -1,10 +1,12 @@
 #!/usr/bin/env python3
-"""Turn a tools/final_r04.sh run (gpurun_out/final_<tag>) into the committed
+"""Turn a tools/final_r0N.sh run (gpurun_out/final_<tag>) into the committed
 evidence under profiles/: PMC traffic summaries and GPU-only critical chains
 tagged with the kernel-source hash the run was collected on (bench.py uses
 only those of its own sources), kernel stats, timelines, bench lines.
 
-    python tools/evidence.py r04
+    python tools/evidence.py r05          # locally, on the merged gpurun_out
+    python tools/evidence.py r05 --pre    # on the GPU box, between the PMC /
+                                          # timeline passes and the bench lines
 """
 import json
 import os
@@ -27,11 +29,13 @@ def run(args, out=None):
 
 def main():
     tag = sys.argv[1]
+    pre = "--pre" in sys.argv[2:]
     src = os.path.join("gpurun_out", "final_" + tag)
     sha = open(os.path.join(ROOT, src, "sources_sha16")).read().strip()
     pro = "profiles"
     cfg = {"bench": "N=1024,M=1024,P=63,LB=19", "s8": "N=1024,M=1024,P=63,LB=19,world=8,rank=0",
-           "vm": "N=256,M=256,P=32,LB=19", "512": "N=512,M=512,P=32,LB=19"}
+           "vm": "N=256,M=256,P=32,LB=19", "512": "N=512,M=512,P=32,LB=19",
+           "2048": "N=2048,M=1024,P=32,LB=19"}
     for name, c in cfg.items():
         d = os.path.join(src, "pmc_" + name)
         if not os.path.isdir(os.path.join(ROOT, d)):
@@ -47,6 +51,12 @@ def main():
             continue
         run(["tools/timeline.py", tr, "--all", "--json", os.path.join(pro, f"{tag}_chain_{name}.json"),
              "--workload", wl, "--sha", sha, "--config", c], os.path.join(pro, f"{tag}_timeline_{name}.txt"))
+    steady = os.path.join(src, "steady_1024", "run_kernel_trace.csv")
+    if os.path.exists(os.path.join(ROOT, steady)):
+        run(["tools/steady.py", steady], os.path.join(pro, f"{tag}_steady_b1024.txt"))
+    if pre:
+        print("pre-bench evidence for sources", sha, "written under profiles/ as", tag + "_*")
+        return
     for f, dst in (("prof/run_kernel_stats.csv", f"{tag}_kernel_stats.csv"), ("bench.json", f"{tag}_bench.json"),
                    ("configs.jsonl", f"{tag}_configs.jsonl"), ("shard_sim.json", f"{tag}_shard_sim.json"),
                    ("ingest.jsonl", f"{tag}_ingest.jsonl")):
