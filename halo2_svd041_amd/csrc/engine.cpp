@@ -483,14 +483,16 @@ struct svdw_ctx {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
-    uint32_t stage_flags = STAGE_ALIGN | STAGE_CELL;   // STAGE_* (aligned block store windows, whole-cell lanes)
+    uint32_t stage_flags = STAGE_ALIGN;     // STAGE_* (4 KiB-aligned block store windows)
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
-    // "stage_occ": blocks per CU of the persistent stage streamer (k_stage_pers);
-    // 0: the one-block-per-chunk kernels (k_stage / k_stage_multi). Its tile
-    // counters: one 256-byte slot per stream (cell stream, st2, st3), zero
-    // between launches (each launch's last block resets its slot).
-    uint32_t stage_occ = 0;
-    uint32_t stage_waves = 4;               // "stage_waves": 4 or 8 waves per persistent block
+    // "stage_occ": blocks per CU of the persistent front streamer (k_stage_front)
+    // for stage batches of >= 64 MB; 0: the one-block-per-chunk kernels
+    // (k_stage / k_stage_multi). Its ticket counters: one 256-byte slot per
+    // stream (cell stream, st2, st3), zero between launches (each launch's last
+    // block resets its slot).
+    uint32_t stage_occ = 1;
+    bool small_spread = true;               // "small_spread": small stage launches over more blocks
+    double stage_front_min = 64.0 * (1 << 20);   // "stage_front_all" 1: 0 (tests: every batch)
     DBuf stage_ctr;
     hipStream_t stream_id[3] = {};          // st, st2, st3 as created (st / st2 / st3 are swapped at times)
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
@@ -982,6 +984,7 @@ static void check_mat(const svdw_ctx* c, const svdw_mat& m) {
 static void check_vec(const svdw_ctx* c, const svdw_vec& v) { check_mat(c, mat_of_vec(v)); }
 
 // ------------------------------------------------------- stage launches
+static constexpr uint32_t kSpreadBlocks = 128;
 // The persistent stage kernel's tile counters for a launch on stream s (null:
 // not one of the context's streams -> the one-block-per-chunk kernels).
 static uint32_t* stage_ctr_for(svdw_ctx* c, hipStream_t s) {
@@ -1010,6 +1013,14 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
         const int sid = c->st == c->st_cell ? 1 : c->st == c->st2 ? 2 : c->st == c->st3 ? 3 : 0;
         fprintf(stderr, "stage %-28s elems %8u C %3u L %3u nv %2u nmo %2u muls %u nk %u  s%d\n", tag, ee - eb,
                 a.C, a.L, a.nv, a.nmo, nmul, a.nk, sid);
+        if (getenv("SVDW_STAGE_LOG")[0] == '2') {        // the slot ops too: (src lo nbits) per cell
+            fprintf(stderr, "  slots");
+            for (uint32_t k = 0; k < a.C + a.L; ++k) {
+                const SlotOp& o = k < a.C ? a.adv[k] : a.lk[k - a.C];
+                fprintf(stderr, " %u:%u:%u", o.src, o.lo, o.nbits);
+            }
+            fprintf(stderr, "\n");
+        }
     }
     if (c->dry || ee <= eb) return;
     a.out_adv = cellp(c, phase, off);
@@ -1028,6 +1039,13 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     // keep the block's LDS (element values) within 64 KiB: fewer elements per
     // block for stages with many values (signed_div_scale)
     while (a.E > 64 && stage_lds_bytes(a.nv ? a.nv : 1, a.E, a.C + a.L) > 65536) a.E -= 64;
+    // small launches (d checks, is_equal rows, a row-sharded rank's tails):
+    // spread over >= kSpreadBlocks blocks -- one block writing a few hundred KB
+    // runs at one CU's store rate (29 us for the d checks on an 8-way rank)
+    if (c->small_spread) {
+        const uint32_t n = ee - eb;
+        while (a.E > 16 && a.E % 32 == 0 && (n + a.E - 1) / a.E < kSpreadBlocks) a.E /= 2;
+    }
     // 32-bit magics for fastdiv (divisor 1 is handled in the kernel)
     auto magic = [](uint64_t d) -> uint32_t { return d > 1 ? (uint32_t)(((1ull << 32) + d - 1) / d) : 0; };
     a.cdiv_magic = magic(a.C);
@@ -1072,7 +1090,7 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     {
         ProfScope ps(c, c->st, std::string("k_stage:") + tag, bytes, 0);
         const StageArgs* one = &a;
-        hipck(launch_stage_pers(&one, 1, c->st, stage_ctr_for(c, c->st), c->stage_occ, c->stage_waves), "k_stage");
+        hipck(launch_stage_pers(&one, 1, c->st, stage_ctr_for(c, c->st), c->stage_occ, c->stage_front_min), "k_stage");
     }
 }
 // Issue a stream's pending batched stages (k_stage_multi; one program: k_stage).
@@ -1107,7 +1125,7 @@ static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter, hipEvent
                 fprintf(stderr, "\n");
             }
             ProfScope pr(c, s, name, bytes, 0, true);
-            hipck(launch_stage_pers(ps.data(), (int)ps.size(), s, stage_ctr_for(c, s), c->stage_occ, c->stage_waves),
+            hipck(launch_stage_pers(ps.data(), (int)ps.size(), s, stage_ctr_for(c, s), c->stage_occ, c->stage_front_min),
                   "k_stage_multi");
         }
     }
@@ -3221,18 +3239,19 @@ static void ctx_init_device(svdw_ctx* c) {
 // The settings (options, shard, profiler) of `s` onto the lane `d`; a change
 // bumps the lane's epoch (its captured graph no longer applies).
 static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
-    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->stage_occ, s->stage_waves, s->gemm_crt, s->res_f64,
+    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->stage_occ, s->small_spread, (int64_t)s->stage_front_min, s->gemm_crt, s->res_f64,
                          s->phase1_overlap, s->prod_cell, s->hold_us, s->rlc_prefix, s->p1_at,
                          s->f64_views, s->overlap, s->stage_batch, s->graph_vm, s->vm_linear, s->pipeline,
                          s->shard_rank, s->shard_world, s->prof, s->host_trace};
-    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->stage_occ, d->stage_waves, d->gemm_crt, d->res_f64,
+    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->stage_occ, d->small_spread, (int64_t)d->stage_front_min, d->gemm_crt, d->res_f64,
                          d->phase1_overlap, d->prod_cell, d->hold_us, d->rlc_prefix, d->p1_at,
                          d->f64_views, d->overlap, d->stage_batch, d->graph_vm, d->vm_linear, d->pipeline,
                          d->shard_rank, d->shard_world, d->prof, d->host_trace};
     if (!memcmp(a, b, sizeof a) && d->prof_filter == s->prof_filter) return;
     d->gemm_impl = s->gemm_impl; d->stage_flags = s->stage_flags; d->stage_elems = s->stage_elems;
     d->stage_occ = s->stage_occ;
-    d->stage_waves = s->stage_waves;
+    d->small_spread = s->small_spread;
+    d->stage_front_min = s->stage_front_min;
     d->gemm_crt = s->gemm_crt; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
     d->prod_cell = s->prod_cell; d->hold_us = s->hold_us; d->rlc_prefix = s->rlc_prefix;
     d->p1_at = s->p1_at; d->f64_views = s->f64_views; d->overlap = s->overlap;
@@ -4557,14 +4576,15 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "gemm_impl") {
             REQUIRE(value == SVDW_GEMM_MFMA || value == SVDW_GEMM_VALU, "gemm_impl: 0 (mfma) or 1 (valu)");
             c->gemm_impl = (int)value;
-        } else if (n == "stage_occ") {               // persistent stage streamer (0: off)
-            REQUIRE(value >= 0 && value <= 8, "stage_occ: 0..8 blocks per CU");
+        } else if (n == "stage_occ") {               // persistent front streamer (0: off)
+            REQUIRE(value >= 0 && value <= 2, "stage_occ: 0, 1 or 2 blocks per CU");
             c->stage_occ = (uint32_t)value;
-        } else if (n == "stage_cell") {              // phase B: a whole cell per lane (else half cells)
-            c->stage_flags = value ? (c->stage_flags | STAGE_CELL) : (c->stage_flags & ~STAGE_CELL);
-        } else if (n == "stage_waves") {
-            REQUIRE(value == 4 || value == 8, "stage_waves: 4 or 8");
-            c->stage_waves = (uint32_t)value;
+        } else if (n == "small_spread") {
+            c->small_spread = value != 0;
+        } else if (n == "stage_diag") {              // timing diagnostic, process-wide (wrong cells)
+            set_front_diag((uint32_t)value);
+        } else if (n == "stage_front_all") {         // test hook: the front streamer for every batch
+            c->stage_front_min = value ? 0.0 : 64.0 * (1 << 20);
         } else if (n == "stage_elems") {
             REQUIRE(value >= 16 && value <= 256 && value % 16 == 0,
                     "stage_elems: a multiple of 16 in [16, 256]");

@@ -401,68 +401,6 @@ __device__ __forceinline__ void stream_cells_desc(uint4* __restrict__ out, uint3
     }
 }
 
-// Phase B, one whole cell per lane (STAGE_CELL): a lane reads the cell's
-// descriptor and two mask words (per slot, built once per block), the nine
-// source words and writes the cell as two 16-B stores; a wave covers 64
-// consecutive cells (2 KiB) and the block's rounds whole 8 KiB windows. Half
-// the descriptor, mask and index work per byte of the half-cell form above.
-template <bool ALIGN>
-__device__ __forceinline__ void stream_cells_cell(uint4* __restrict__ out, uint32_t total,
-                                                  const uint32_t* __restrict__ sD,
-                                                  const uint4* __restrict__ sM, uint32_t C, uint32_t magic,
-                                                  const uint32_t* smem, uint32_t vbase0, uint32_t nv) {
-    const uint32_t step = blockDim.x;
-    const uint32_t dq = step / C, dr = step - dq * C, ev = stage_elem_words(nv);
-    uint32_t c0 = threadIdx.x;
-    if (ALIGN) {
-        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) >> 5) & (blockDim.x - 1);
-        c0 = threadIdx.x >= mis ? threadIdx.x - mis : threadIdx.x + blockDim.x - mis;
-    }
-    uint32_t el = fastdiv(c0, C, magic), slot = c0 - el * C;
-    uint32_t vbase = vbase0 + el * ev;
-    for (uint32_t c = c0; c < total; c += step) {
-        const uint32_t d = sD[slot];
-        const uint4 m0 = sM[2 * slot], m1 = sM[2 * slot + 1];
-        const uint32_t* x = smem + ((d & kHalfElem) ? vbase : 0u) + (d & 0xffffu);
-        const uint32_t r = (d >> 16) & 31u;
-        uint32_t w[9];
-#pragma unroll
-        for (int i = 0; i < 9; ++i) w[i] = x[i];
-        out[2 * c] = make_uint4(__builtin_amdgcn_alignbit(w[1], w[0], r) & m0.x,
-                                __builtin_amdgcn_alignbit(w[2], w[1], r) & m0.y,
-                                __builtin_amdgcn_alignbit(w[3], w[2], r) & m0.z,
-                                __builtin_amdgcn_alignbit(w[4], w[3], r) & m0.w);
-        out[2 * c + 1] = make_uint4(__builtin_amdgcn_alignbit(w[5], w[4], r) & m1.x,
-                                    __builtin_amdgcn_alignbit(w[6], w[5], r) & m1.y,
-                                    __builtin_amdgcn_alignbit(w[7], w[6], r) & m1.z,
-                                    __builtin_amdgcn_alignbit(w[8], w[7], r) & m1.w);
-        slot += dr;
-        vbase += dq * ev;
-        if (slot >= C) {
-            slot -= C;
-            vbase += ev;
-        }
-    }
-}
-// Descriptor and masks of a whole cell of a slot (STAGE_CELL; see half_desc):
-// d = source word of the cell's window, m[0..1] = its eight mask words.
-__device__ __forceinline__ void make_cell(const SlotOp op, uint32_t* d, uint4* m) {
-    const uint32_t lo = op.lo;
-    uint32_t nb = op.nbits ? op.nbits : 256u;
-    nb = min(nb, 256u - lo);
-    const bool elem = op.src < KSRC;
-    const uint32_t base = (elem ? op.src : op.src - KSRC) * VW;
-    *d = half_desc(base + (lo >> 5), lo & 31u, elem);
-    uint32_t w[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int keep = (int)nb - 32 * i;
-        w[i] = keep >= 32 ? 0xffffffffu : (keep <= 0 ? 0u : ((1u << keep) - 1u));
-    }
-    m[0] = make_uint4(w[0], w[1], w[2], w[3]);
-    m[1] = make_uint4(w[4], w[5], w[6], w[7]);
-}
-
 // Descriptor and masks of half h of a slot (see half_desc).
 __device__ __forceinline__ void make_half(const SlotOp op, uint32_t h, uint32_t* d, uint4* m) {
     const uint32_t lo = op.lo;
@@ -692,14 +630,9 @@ __device__ __forceinline__ void stage_setup(const StageArgs& a, const StageLds& 
     for (uint32_t k = tid; k < a.L; k += blockDim.x) L.sLk[k] = lk[k];
     for (uint32_t k = tid; k < a.nmo; k += blockDim.x) L.sMo[k] = mo[k];
     if (tid < kMaxViews) L.sVw[tid] = a.view[tid];
-    if (a.flags & STAGE_CELL) {
-        for (uint32_t k = tid; k < a.C + a.L; k += blockDim.x)
-            make_cell(k < a.C ? adv[k] : lk[k - a.C], L.sHD + k, L.sHM + 2 * k);
-    } else {
-        for (uint32_t k = tid; k < 2 * (a.C + a.L); k += blockDim.x) {
-            const uint32_t sl = k >> 1;
-            make_half(sl < a.C ? adv[sl] : lk[sl - a.C], k & 1, L.sHD + k, L.sHM + k);
-        }
+    for (uint32_t k = tid; k < 2 * (a.C + a.L); k += blockDim.x) {
+        const uint32_t sl = k >> 1;
+        make_half(sl < a.C ? adv[sl] : lk[sl - a.C], k & 1, L.sHD + k, L.sHM + k);
     }
 }
 // This thread's in-bounds strided view loads of block blk's element.
@@ -753,13 +686,6 @@ __device__ __forceinline__ void stage_chunk(const StageArgs& a, const StageLds& 
     uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
     uint4* outL = a.L ? reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L) : nullptr;
     const uint32_t vb0 = (uint32_t)(L.sV - smem);
-    if (a.flags & STAGE_CELL) {
-        stream_cells_cell<true>(outA, ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv);
-        if (a.L)
-            stream_cells_cell<true>(outL, ne * a.L, L.sHD + a.C, L.sHM + 2 * a.C, a.L, a.ldiv_magic, smem, vb0,
-                                    nv);
-        return;
-    }
     stream_cells_desc<true>(outA, 2 * ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv);
     if (a.L)
         stream_cells_desc<true>(outL, 2 * ne * a.L, L.sHD + 2 * a.C, L.sHM + 2 * a.C, a.L, a.ldiv_magic, smem,
@@ -884,45 +810,56 @@ hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t 
     return flush();
 }
 
-// ------------------------------------------------ persistent stage streamer
-// k_stage_pers: the same cell programs as k_stage / k_stage_multi, run by a
-// persistent grid (a few blocks per CU) that takes 64-element tiles in stream
-// order from a device counter. Per block:
-//   * wave 0 runs phase A (the micro-ops, one element per lane) of the NEXT
-//     tile into the other LDS buffer, with that tile's view loads issued one
-//     tile earlier and its index dequeued two tiles earlier, while
-//   * all four waves (wave 0 once its phase A is done) stream the CURRENT
-//     tile's cells, taking 2 KiB rounds (64 cells, one per lane: two 16-B
-//     stores) from an LDS counter, so the waves stay balanced.
-// One barrier per tile; a block's programme tables (constants, micro-ops,
-// views, per-cell descriptors and masks) are set up once per program it meets,
-// in one of two table sets, so a tile of the next program can run its phase A
-// while the current tile still reads the other set. Tiles are ~64-128 KiB of
-// cells: the grid's write front stays a compact range of the stream, and one
-// device counter serves the dequeues (one per tile, ~50 per µs at 6 TB/s).
-// The last block to leave resets the counter for the next launch on its stream.
-static constexpr uint32_t kPersTile = 64;
+// ------------------------------------------------ persistent front streamer
+// k_stage_front: the cell programs of k_stage / k_stage_multi on a persistent
+// grid (one block per CU) that writes the cell streams in a compact moving
+// front. Every output region (a program's advice cells, its lookup cells) is
+// cut into 4 KiB windows (256 half-cells, aligned to 4 KiB in memory). A ticket
+// (taken in order from a device counter) is a block slot b of a super-round s:
+// the K windows (s K + j) G + b, j < K, of one region (G = the grid). With all
+// G blocks resident the whole chip writes G adjacent windows (1 MiB) at a time
+// and sweeps the stream, the store pattern that reaches the memset rate
+// (tools/probes/storepat8.hip: 6.4 TB/s against 5.5-5.8 for one long chunk per
+// block). Per block, five waves:
+//   * wave 0, the producer: phase A (the micro-ops) of the NEXT ticket's
+//     elements -- the <= kFrontElems elements its K windows touch, one per lane
+//     per pass -- into the other LDS buffer; its view loads are issued one
+//     ticket ahead and its dequeue two tickets ahead. It issues no stores, so
+//     its waits never wait for stores in flight.
+//   * waves 1-4, the consumers: the CURRENT ticket's windows, one half-cell
+//     (16 B) per lane per window, every wave store one contiguous 1 KiB, with
+//     no barrier between windows.
+// One barrier per ticket. A program's tables (constants, micro-ops, views, the
+// per (slot, half) descriptors and masks of stream_cells_desc) go into one of
+// two table sets, so the producer can start the next program while the
+// consumers still read the current one. The last block out resets the
+// counter for the next launch on its stream.
+static constexpr uint32_t kFrontElems = 128;          // element slots per ticket (two producer passes)
+static constexpr uint32_t kFrontWaves = 5;
+static constexpr int kMaxStreams = 2 * kMaxMulti;
 
-// words of one table set: K | masks (8 per cell) | micro-ops | views | descriptors
-__host__ __device__ constexpr uint32_t pers_set_words(uint32_t cl) {
-    return (kMaxK * VW + 8 * cl + kMaxMicro * 2 + kMaxViews * 10 + cl + 3) / 4 * 4;
+// words of one table set: K | masks (one uint4 per slot half) | micro-ops | views | descriptors
+__host__ __device__ constexpr uint32_t front_set_words(uint32_t cl) {
+    return (kMaxK * VW + 8 * cl + kMaxMicro * 2 + kMaxViews * 10 + 2 * cl + 3) / 4 * 4;
 }
-__host__ __device__ constexpr uint32_t pers_lds_bytes(uint32_t cl, uint32_t ev) {
-    return 4 * (2 * pers_set_words(cl) + 2 * (kPersTile * ev + 16));
+__host__ __device__ constexpr uint32_t front_lds_bytes(uint32_t cl, uint32_t ev) {
+    return 4 * (2 * front_set_words(cl) + 2 * (kFrontElems * ev + 16));
 }
-struct PersSet {
+// elements a 4 KiB window of a U-cell-per-element region touches, at most
+__host__ __device__ constexpr uint32_t front_epw(uint32_t U) { return 127 / U + 2; }
+struct FSet {
     uint32_t* K;
-    uint4* M;            // masks: 2 uint4 per cell
+    uint4* M;            // masks: one uint4 per (slot, half)
     MicroOp* mo;
     DView* vw;
-    uint32_t* D;         // descriptors
+    uint32_t* D;         // descriptors: one per (slot, half)
 };
 // (base = smem + a word offset: pointers kept as offsets from the LDS array,
 // never selected from an array of pointers, stay in the LDS address space --
 // a selected pointer becomes a flat pointer, and flat loads count against the
 // store counter: every LDS read would then wait for the stores in flight)
-__device__ __forceinline__ PersSet pers_set(uint32_t* base, uint32_t cl) {
-    PersSet s;
+__device__ __forceinline__ FSet front_set(uint32_t* base, uint32_t cl) {
+    FSet s;
     s.K = base;
     s.M = reinterpret_cast<uint4*>(base + kMaxK * VW);
     s.mo = reinterpret_cast<MicroOp*>(base + kMaxK * VW + 8 * cl);
@@ -931,31 +868,18 @@ __device__ __forceinline__ PersSet pers_set(uint32_t* base, uint32_t cl) {
     return s;
 }
 // One program's tables into set s, by the 64 lanes of one wave.
-__device__ __forceinline__ void pers_tables(const Rec& q, const PersSet& s, uint32_t lane) {
+__device__ __forceinline__ void front_tables(const Rec& q, const FSet& s, uint32_t lane) {
     const StageArgs& a = *q.a;
     for (uint32_t k = lane; k < a.nk; k += 64) lds_put(s.K + k * VW, q.K[k]);
     for (uint32_t k = lane; k < a.nmo; k += 64) s.mo[k] = q.mo[k];
     if (lane < kMaxViews) s.vw[lane] = a.view[lane];
-    for (uint32_t k = lane; k < a.C + a.L; k += 64) {
-        const SlotOp op = k < a.C ? q.adv[k] : q.lk[k - a.C];
-        const uint32_t lo = op.lo;
-        uint32_t nb = op.nbits ? op.nbits : 256u;
-        nb = min(nb, 256u - lo);
-        const bool elem = op.src < KSRC;
-        const uint32_t base = (elem ? op.src : op.src - KSRC) * VW;
-        s.D[k] = half_desc(base + (lo >> 5), lo & 31u, elem);
-        uint32_t w[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int keep = (int)nb - 32 * i;
-            w[i] = keep >= 32 ? 0xffffffffu : (keep <= 0 ? 0u : ((1u << keep) - 1u));
-        }
-        s.M[2 * k] = make_uint4(w[0], w[1], w[2], w[3]);
-        s.M[2 * k + 1] = make_uint4(w[4], w[5], w[6], w[7]);
+    for (uint32_t k = lane; k < 2 * (a.C + a.L); k += 64) {
+        const uint32_t sl = k >> 1;
+        make_half(sl < a.C ? q.adv[sl] : q.lk[sl - a.C], k & 1, s.D + k, s.M + k);
     }
 }
 // View loads of element e (this lane) of a program (phase A's prefetch).
-__device__ __forceinline__ Prefetch pers_loads(const StageArgs& a, uint32_t e, bool valid) {
+__device__ __forceinline__ Prefetch front_loads(const StageArgs& a, uint32_t e, bool valid) {
     Prefetch f{fr_zero(), fr_zero(), false, false};
     if (!valid) return f;
     const uint32_t pi = e / a.cols, pj = e - pi * a.cols;
@@ -976,115 +900,164 @@ __device__ __forceinline__ Prefetch pers_loads(const StageArgs& a, uint32_t e, b
     }
     return f;
 }
-// Cells [c0, c0 + n) of one region of a tile (advice or lookups, region
-// tables D / M at slot offset 0), cell c = element c / C, slot c % C; this
-// wave's round r covers the 64 cells of a 2 KiB-aligned window.
-__device__ __forceinline__ void pers_round(uint4* __restrict__ out, uint32_t total, uint32_t mis, uint32_t r,
-                                           uint32_t C, uint32_t magic, const uint32_t* __restrict__ D,
-                                           const uint4* __restrict__ M, const uint32_t* __restrict__ buf,
-                                           const uint32_t* __restrict__ kset, uint32_t ev, uint32_t lane) {
-    const int32_t c = (int32_t)(r * 64 + lane) - (int32_t)mis;
-    if (c < 0 || (uint32_t)c >= total) return;
-    const uint32_t el = fastdiv((uint32_t)c, C, magic), slot = (uint32_t)c - el * C;
-    const uint32_t d = D[slot];
-    const uint4 m0 = M[2 * slot], m1 = M[2 * slot + 1];
-    const uint32_t* x = ((d & kHalfElem) ? buf + el * ev : kset) + (d & 0xffffu);
-    const uint32_t sh = (d >> 16) & 31u;
-    uint32_t w[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) w[i] = x[i];
-    uint4* o = out + 2 * (uint32_t)c;
-    o[0] = make_uint4(__builtin_amdgcn_alignbit(w[1], w[0], sh) & m0.x, __builtin_amdgcn_alignbit(w[2], w[1], sh) & m0.y,
-                      __builtin_amdgcn_alignbit(w[3], w[2], sh) & m0.z, __builtin_amdgcn_alignbit(w[4], w[3], sh) & m0.w);
-    o[1] = make_uint4(__builtin_amdgcn_alignbit(w[5], w[4], sh) & m1.x, __builtin_amdgcn_alignbit(w[6], w[5], sh) & m1.y,
-                      __builtin_amdgcn_alignbit(w[7], w[6], sh) & m1.z, __builtin_amdgcn_alignbit(w[8], w[7], sh) & m1.w);
-}
-struct PersCtl {
-    uint32_t* ctr;       // [0] tile head, [1] blocks done (zero between launches)
-    uint32_t cl;         // max C + L over the programs (table set size)
-    uint32_t ev;         // max element words over the programs
+// One output region of one program, cut into 4 KiB windows.
+struct FStream {
+    uint64_t H;          // half-cells (2 U n)
+    uint32_t prog, lk;   // program, region (0 advice, 1 lookups)
+    uint32_t U, magic;   // cells per element, ceil(2^32 / U)
+    uint32_t mis;        // half-cells from the 4 KiB boundary below the region start
+    uint32_t epw, K;     // element slots per window, windows per ticket
+    uint32_t nw, t0;     // windows, first ticket
 };
+// Window j of a ticket: half-cells [h0, h1) of the region, the element of its
+// first cell (first) and that cell's slot in it (phase); false if past the end.
+struct FWin {
+    int64_t hb;          // half-cell of lane 0 (256 W - mis, may be negative)
+    uint32_t first, phase;
+};
+__device__ __forceinline__ bool front_win(const FStream& F, uint32_t s, uint32_t b, uint32_t j, uint32_t G,
+                                          FWin* w) {
+    if (j >= F.K) return false;
+    const uint64_t W = ((uint64_t)s * F.K + j) * G + b;
+    if (W >= F.nw) return false;
+    w->hb = (int64_t)(W * 256) - (int64_t)F.mis;
+    const uint64_t c0 = (uint64_t)(w->hb < 0 ? 0 : w->hb) >> 1;
+    w->first = (uint32_t)(c0 / F.U);
+    w->phase = (uint32_t)(c0 - (uint64_t)w->first * F.U);
+    return true;
+}
 struct SrcMulti {
     const StageMulti* m;
     __device__ uint32_t nprog() const { return m->nprog; }
-    __device__ uint32_t t0(uint32_t p) const { return m->blk0[p]; }
-    __device__ uint32_t prog_of(uint32_t t) const { return multi_prog(*m, t); }
     __device__ Rec rec(uint32_t p) const { return multi_rec(*m, p); }
 };
 struct SrcSingle {
     const StageArgs* a;
-    uint32_t ntiles;
     __device__ uint32_t nprog() const { return 1; }
-    __device__ uint32_t t0(uint32_t p) const { return p ? ntiles : 0; }
-    __device__ uint32_t prog_of(uint32_t) const { return 0; }
     __device__ Rec rec(uint32_t) const { return Rec{a, a->mo, a->adv, a->lk, a->K}; }
 };
-// Roles: wave 0 is the producer (phase A of the next tile, the view loads of
-// the one after, the dequeue of the one after that), waves 1..NW-1 the
-// consumers (phase B). The producer issues no stores, so its waits (for its
-// loads and its dequeue) never wait for the stores in flight; it issues each
-// load and dequeue one tile before it uses the result.
-template <int NW, class SRC>
-__device__ __forceinline__ void stage_persist(const SRC& S, const PersCtl& pc) {
+struct FrontCtl {
+    uint32_t* ctr;       // [0] ticket head, [1] blocks done (zero between launches)
+    uint32_t cl;         // max C + L over the programs (table set size)
+    uint32_t ev;         // max element words over the programs
+    uint32_t diag;       // timing diagnostic (wrong cells): 1 = the producer skips its view loads
+};
+template <class SRC>
+__device__ __forceinline__ void stage_front(const SRC& S, const FrontCtl& fc) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    __shared__ uint32_t sTile[2], sSet[2], sRound[2], sProg[2];
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const uint32_t T = S.t0(S.nprog());
-    const uint32_t sw = pers_set_words(pc.cl), bw = kPersTile * pc.ev + 16, ev = pc.ev, cl = pc.cl;
-    // word offsets of table set s and element buffer b (see pers_set)
-    auto set_off = [&](uint32_t s) { return s ? sw : 0u; };
-    auto buf_off = [&](uint32_t b) { return 2 * sw + (b ? bw : 0u); };
-    // producer look-ahead: tile n1 (its loads f1 in flight), tile n2 (known),
-    // the dequeue of the tile after n2 in flight (n3v, lane 0)
-    uint32_t n1 = 0, n2 = 0, n3v = 0;
-    Prefetch f1{fr_zero(), fr_zero(), false, false};
-    auto issue_loads = [&](uint32_t t) {
-        if (t >= T) { f1 = Prefetch{fr_zero(), fr_zero(), false, false}; return; }
-        const uint32_t p = S.prog_of(t);
-        const Rec q = S.rec(p);
-        const uint32_t e0 = q.a->e_begin + (t - S.t0(p)) * kPersTile;
-        const uint32_t ne = min(kPersTile, q.a->e_end - e0);
-        f1 = pers_loads(*q.a, e0 + lane, lane < ne);
-    };
-    // phase A of tile t into buffer b: its program's tables go into the set
-    // the current tile does not use, unless it is the same program
-    auto phase_a = [&](uint32_t t, uint32_t b, uint32_t cur_set) {
-        if (t >= T) {
-            if (lane == 0) sTile[b] = T;
-            return;
-        }
-        const uint32_t p = S.prog_of(t);
-        const Rec q = S.rec(p);
-        uint32_t s = cur_set;
-        if (sProg[s] != p) {
-            s ^= 1u;
-            if (sProg[s] != p) {
-                pers_tables(q, pers_set(smem + set_off(s), cl), lane);
-                if (lane == 0) sProg[s] = p;
+    __shared__ FStream sF[kMaxStreams];
+    __shared__ uint32_t sNS, sTT;
+    __shared__ uint32_t sTile[2], sSet[2], sProg[2];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, G = gridDim.x;
+    const uint32_t sw = front_set_words(fc.cl), bw = kFrontElems * fc.ev + 16, ev = fc.ev, cl = fc.cl;
+    auto set_off = [&](uint32_t x) { return x ? sw : 0u; };
+    auto buf_off = [&](uint32_t x) { return 2 * sw + (x ? bw : 0u); };
+    // ---- the regions and their tickets (one thread; <= 32 regions)
+    if (tid == 0) {
+        uint32_t ns = 0, tt = 0;
+        for (uint32_t p = 0; p < S.nprog(); ++p) {
+            const Rec q = S.rec(p);
+            const StageArgs& a = *q.a;
+            const uint32_t n = a.e_end - a.e_begin;
+            for (uint32_t lk = 0; lk < 2; ++lk) {
+                const uint32_t U = lk ? a.L : a.C;
+                if (!U || !n) continue;
+                FStream& F = sF[ns++];
+                const Fr* base = (lk ? a.out_lk + (uint64_t)a.e_begin * U : a.out_adv + (uint64_t)a.e_begin * U);
+                F.H = 2ull * U * n;
+                F.prog = p;
+                F.lk = lk;
+                F.U = U;
+                F.magic = U > 1 ? (uint32_t)(((1ull << 32) + U - 1) / U) : 0u;
+                F.mis = (uint32_t)(reinterpret_cast<uintptr_t>(base) >> 4) & 255u;
+                F.epw = front_epw(U);
+                F.K = kFrontElems / F.epw;
+                F.nw = (uint32_t)((F.H + F.mis + 255) / 256);
+                F.t0 = tt;
+                tt += (F.nw + F.K * G - 1) / (F.K * G) * G;
             }
         }
-        const PersSet ts = pers_set(smem + set_off(s), cl);
-        const uint32_t e0 = q.a->e_begin + (t - S.t0(p)) * kPersTile;
-        const uint32_t ne = min(kPersTile, q.a->e_end - e0);
-        if (lane < ne)
-            element_program(*q.a, e0 + lane, smem + buf_off(b) + lane * ev, ts.K, ts.mo, ts.vw, f1.v0, f1.in0,
-                            f1.v1, f1.in1);
-        if (lane == 0) {
-            sTile[b] = t;
-            sSet[b] = s;
-        }
-    };
-    if (tid < 2) {
-        sProg[tid] = ~0u;
-        sRound[tid] = 0;
+        sNS = ns;
+        sTT = tt;
+        sProg[0] = sProg[1] = ~0u;
     }
     __syncthreads();
+    const uint32_t NS = sNS, TT = sTT;
+    auto stream_of = [&](uint32_t q) {
+        uint32_t k = 0;
+        for (uint32_t i = 1; i < NS; ++i) k += q >= sF[i].t0;
+        return k;
+    };
+    // producer state: tile n1 (loads fa / fb of its two passes in flight), n2
+    // (known), dequeue n3v in flight
+    static_assert(kFrontElems == 128, "two producer passes");
+    uint32_t n1 = 0, n2 = 0, n3v = 0;
+    Prefetch fa{fr_zero(), fr_zero(), false, false}, fb = fa;
+    // element slot t of ticket q: its element (global index), or false
+    auto slot_elem = [&](uint32_t q, const FStream& F, uint32_t t, uint32_t* e) -> bool {
+        const uint32_t local = q - F.t0, s = local / G, b = local - s * G;
+        const uint32_t j = t / F.epw, kk = t - j * F.epw;
+        FWin w;
+        if (!front_win(F, s, b, j, G, &w)) return false;
+        const int64_t hl = w.hb + 255 < (int64_t)F.H - 1 ? w.hb + 255 : (int64_t)F.H - 1;
+        const uint32_t last = (uint32_t)(((uint64_t)hl >> 1) / F.U);
+        if (w.first + kk > last) return false;
+        *e = S.rec(F.prog).a->e_begin + w.first + kk;
+        return true;
+    };
+    auto issue_loads = [&](uint32_t q) {
+        if (q >= TT || fc.diag) return;
+        const FStream F = sF[stream_of(q)];
+        const Rec r = S.rec(F.prog);
+        uint32_t e0 = 0, e1 = 0;
+        const bool v0 = slot_elem(q, F, lane, &e0), v1 = slot_elem(q, F, 64 + lane, &e1);
+        fa = front_loads(*r.a, e0, v0);
+        fb = front_loads(*r.a, e1, v1);
+    };
+    // phase A of ticket q into buffer x; tables into the set the current ticket
+    // does not use, unless it is the same program
+    auto phase_a = [&](uint32_t q, uint32_t x, uint32_t cur_set) {
+        if (q >= TT) {
+            if (lane == 0) sTile[x] = TT;
+            return;
+        }
+        const FStream F = sF[stream_of(q)];
+        const Rec r = S.rec(F.prog);
+        uint32_t st = cur_set;
+        if (sProg[st] != F.prog) {
+            st ^= 1u;
+            if (sProg[st] != F.prog) {
+                front_tables(r, front_set(smem + set_off(st), cl), lane);
+                if (lane == 0) sProg[st] = F.prog;
+            }
+        }
+        const FSet ts = front_set(smem + set_off(st), cl);
+        for (uint32_t ps = 0; ps < 2; ++ps) {
+            uint32_t e = 0;
+            // (pass ps's prefetch, selected word by word: an indexed array of
+            // them would live in scratch)
+            Fr v0, v1;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) {
+                v0.w[w] = ps ? fb.v0.w[w] : fa.v0.w[w];
+                v1.w[w] = ps ? fb.v1.w[w] : fa.v1.w[w];
+            }
+            const bool in0 = ps ? fb.in0 : fa.in0, in1 = ps ? fb.in1 : fa.in1;
+            if (slot_elem(q, F, ps * 64 + lane, &e))
+                element_program(*r.a, e, smem + buf_off(x) + (ps * 64 + lane) * ev, ts.K, ts.mo, ts.vw, v0, in0,
+                                v1, in1);
+        }
+        if (lane == 0) {
+            sTile[x] = q;
+            sSet[x] = st;
+        }
+    };
     if (wave == 0) {
         uint32_t t0 = 0, t1 = 0, t2 = 0;
         if (lane == 0) {
-            t0 = atomicAdd(pc.ctr, 1u);
-            t1 = atomicAdd(pc.ctr, 1u);
-            t2 = atomicAdd(pc.ctr, 1u);
+            t0 = atomicAdd(fc.ctr, 1u);
+            t1 = atomicAdd(fc.ctr, 1u);
+            t2 = atomicAdd(fc.ctr, 1u);
         }
         t0 = __builtin_amdgcn_readfirstlane(t0);
         n1 = __builtin_amdgcn_readfirstlane(t1);
@@ -1092,54 +1065,55 @@ __device__ __forceinline__ void stage_persist(const SRC& S, const PersCtl& pc) {
         issue_loads(t0);
         phase_a(t0, 0, 0);
         issue_loads(n1);
-        if (lane == 0) n3v = atomicAdd(pc.ctr, 1u);
+        if (lane == 0) n3v = atomicAdd(fc.ctr, 1u);
     }
     __syncthreads();
     for (uint32_t k = 0;; ++k) {
-        const uint32_t b = k & 1u;
-        const uint32_t cur = sTile[b];
-        if (cur >= T) break;                                        // (uniform)
-        const uint32_t cset = sSet[b];
+        const uint32_t bx = k & 1u;
+        const uint32_t cur = sTile[bx];
+        if (cur >= TT) break;                                       // (uniform)
+        const uint32_t cset = sSet[bx];
         if (wave == 0) {
-            // ---- producer: the next tile's phase A into the other buffer
-            if (lane == 0) sRound[b ^ 1u] = 0;
-            phase_a(n1, b ^ 1u, cset);
+            // ---- producer: the next ticket's phase A into the other buffer
+            phase_a(n1, bx ^ 1u, cset);
             n1 = n2;
             n2 = __builtin_amdgcn_readfirstlane(n3v);               // (returned during phase A's waits)
             issue_loads(n1);
-            if (lane == 0) n3v = atomicAdd(pc.ctr, 1u);
+            if (lane == 0) n3v = atomicAdd(fc.ctr, 1u);
         } else {
-            // ---- consumers: the current tile's cells, 2 KiB rounds from the LDS counter
-            const uint32_t p = S.prog_of(cur);
-            const Rec q = S.rec(p);
-            const uint32_t C = q.a->C, L = q.a->L, cmag = q.a->cdiv_magic, lmag = q.a->ldiv_magic;
-            const uint32_t e0 = q.a->e_begin + (cur - S.t0(p)) * kPersTile;
-            const uint32_t ne = min(kPersTile, q.a->e_end - e0);
-            const PersSet ts = pers_set(smem + set_off(cset), cl);
-            uint4* outA = reinterpret_cast<uint4*>(q.a->out_adv + (uint64_t)e0 * C);
-            const uint32_t totA = ne * C, misA = (uint32_t)(reinterpret_cast<uintptr_t>(outA) >> 5) & 63u;
-            const uint32_t RA = (totA + misA + 63) / 64;
-            uint4* outL = nullptr;
-            uint32_t totL = 0, misL = 0, RL = 0;
-            if (L) {
-                outL = reinterpret_cast<uint4*>(q.a->out_lk + (uint64_t)e0 * L);
-                totL = ne * L;
-                misL = (uint32_t)(reinterpret_cast<uintptr_t>(outL) >> 5) & 63u;
-                RL = (totL + misL + 63) / 64;
-            }
-            const uint32_t* buf = smem + buf_off(b);
-            auto grab = [&]() -> uint32_t {
-                uint32_t r = 0;
-                if (lane == 0) r = atomicAdd(&sRound[b], 1u);
-                return __builtin_amdgcn_readfirstlane(r);
-            };
-            for (uint32_t r = grab(); r < RA + RL;) {
-                const uint32_t rn = grab();                         // the next round, while this one runs
-                if (r < RA)
-                    pers_round(outA, totA, misA, r, C, cmag, ts.D, ts.M, buf, ts.K, ev, lane);
-                else
-                    pers_round(outL, totL, misL, r - RA, L, lmag, ts.D + C, ts.M + 2 * C, buf, ts.K, ev, lane);
-                r = rn;
+            // ---- consumers: the current ticket's windows, one half-cell per lane
+            const FStream F = sF[stream_of(cur)];
+            const Rec r = S.rec(F.prog);
+            const StageArgs& a = *r.a;
+            const uint32_t local = cur - F.t0, s = local / G, b = local - s * G;
+            const FSet ts = front_set(smem + set_off(cset), cl);
+            const uint32_t rb = F.lk ? a.C : 0u;                    // the region's first slot
+            const uint32_t* Dr = ts.D + 2 * rb;
+            const uint4* Mr = ts.M + 2 * rb;
+            uint4* out = reinterpret_cast<uint4*>(F.lk ? a.out_lk + (uint64_t)a.e_begin * F.U
+                                                       : a.out_adv + (uint64_t)a.e_begin * F.U);
+            const uint32_t u = tid - 64, vb = buf_off(bx);
+            for (uint32_t j = 0;; ++j) {
+                FWin w;
+                if (!front_win(F, s, b, j, G, &w)) break;           // (uniform)
+                const int64_t hc = w.hb + (int64_t)u;
+                if (hc >= 0 && (uint64_t)hc < F.H) {
+                    // cell (hc >> 1) = first + (rel / U) elements, slot rel % U
+                    const uint32_t rel = (uint32_t)((uint64_t)(hc >> 1) - (((uint64_t)(w.hb < 0 ? 0 : w.hb)) >> 1)) +
+                                         w.phase;
+                    const uint32_t el = fastdiv(rel, F.U, F.magic), slot = rel - el * F.U;
+                    const uint32_t h = (uint32_t)hc & 1u, kx = 2 * slot + h;
+                    const uint32_t d = Dr[kx];
+                    const uint4 m = Mr[kx];
+                    const uint32_t* x = smem + ((d & kHalfElem) ? vb + (j * F.epw + el) * ev : set_off(cset)) +
+                                        (d & 0xffffu);
+                    const uint32_t sh = (d >> 16) & 31u;
+                    const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4];
+                    out[hc] = make_uint4(__builtin_amdgcn_alignbit(x1, x0, sh) & m.x,
+                                         __builtin_amdgcn_alignbit(x2, x1, sh) & m.y,
+                                         __builtin_amdgcn_alignbit(x3, x2, sh) & m.z,
+                                         __builtin_amdgcn_alignbit(x4, x3, sh) & m.w);
+                }
             }
         }
         __syncthreads();
@@ -1148,72 +1122,71 @@ __device__ __forceinline__ void stage_persist(const SRC& S, const PersCtl& pc) {
     // (after the producer's last dequeue has returned)
     if (tid == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t done = atomicAdd(pc.ctr + 1, 1u);
+        const uint32_t done = atomicAdd(fc.ctr + 1, 1u);
         if (done == gridDim.x - 1) {
-            atomicExch(pc.ctr, 0u);
-            atomicExch(pc.ctr + 1, 0u);
+            atomicExch(fc.ctr, 0u);
+            atomicExch(fc.ctr + 1, 0u);
         }
     }
 }
-__global__ __launch_bounds__(256) void k_stage_pers(const StageArgs a, const PersCtl pc, uint32_t ntiles) {
-    stage_persist<4>(SrcSingle{&a, ntiles}, pc);
+__global__ __launch_bounds__(64 * kFrontWaves) void k_stage_front(const StageArgs a, const FrontCtl fc) {
+    stage_front(SrcSingle{&a}, fc);
 }
-__global__ __launch_bounds__(256) void k_stage_pers_multi(const StageMulti m, const PersCtl pc) {
-    stage_persist<4>(SrcMulti{&m}, pc);
-}
-__global__ __launch_bounds__(512) void k_stage_pers8(const StageArgs a, const PersCtl pc, uint32_t ntiles) {
-    stage_persist<8>(SrcSingle{&a, ntiles}, pc);
-}
-__global__ __launch_bounds__(512) void k_stage_pers8_multi(const StageMulti m, const PersCtl pc) {
-    stage_persist<8>(SrcMulti{&m}, pc);
+__global__ __launch_bounds__(64 * kFrontWaves) void k_stage_front_multi(const StageMulti m, const FrontCtl fc) {
+    stage_front(SrcMulti{&m}, fc);
 }
 static int g_cus = 0;
-static uint32_t pers_grid(uint32_t ntiles, uint32_t occ) {
+static uint32_t cu_count() {
     if (!g_cus) {
         int dev = 0, n = 0;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
         g_cus = n > 0 ? n : 256;
     }
-    return std::max(1u, std::min(ntiles, occ * (uint32_t)g_cus));
+    return (uint32_t)g_cus;
 }
+// Small launches (a batch under min_bytes of cells) and regions of one cell per
+// element stay on the one-block-per-chunk kernels.
+static bool front_suits(const StageArgs* const* progs, int n, double min_bytes) {
+    double bytes = 0;
+    for (int i = 0; i < n; ++i) {
+        const StageArgs& a = *progs[i];
+        if (a.e_end <= a.e_begin) continue;
+        if (a.C + a.L > kMaxAdv + kMaxLk || a.nv > kMaxV) return false;
+        if ((a.C && kFrontElems / front_epw(a.C) == 0) || (a.L && kFrontElems / front_epw(a.L) == 0)) return false;
+        bytes += 32.0 * (a.e_end - a.e_begin) * (a.C + a.L);
+    }
+    return bytes > 0 && bytes >= min_bytes;
+}
+static uint32_t g_front_diag = 0;
+void set_front_diag(uint32_t d) { g_front_diag = d; }
 hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t st, uint32_t* ctr, uint32_t occ,
-                             uint32_t waves) {
-    if (!ctr || !occ) return launch_stage_multi(progs, n, st);
-    if (waves != 4 && waves != 8) return hipErrorInvalidValue;
+                             double min_bytes) {
+    if (!ctr || !occ || !front_suits(progs, n, min_bytes)) return launch_stage_multi(progs, n, st);
     StageMulti m;
     m.nprog = 0;
-    uint32_t used = 0, tiles = 0, cl = 0, ev = 0;
+    uint32_t used = 0, cl = 0, ev = 0;
     const StageArgs* single = nullptr;
+    const uint32_t grid = occ * cu_count();
     auto flush = [&]() -> hipError_t {
         hipError_t e = hipSuccess;
         if (m.nprog) {
-            PersCtl pc{ctr, cl, ev};
-            const uint32_t lds = pers_lds_bytes(cl, ev);
-            if (lds > 160u * 1024u) return hipErrorInvalidValue;
-            const uint32_t grid = pers_grid(tiles, occ);
-            if (m.nprog == 1) {
-                if (waves == 8)
-                    hipLaunchKernelGGL(k_stage_pers8, dim3(grid), dim3(512), lds, st, *single, pc, tiles);
-                else
-                    hipLaunchKernelGGL(k_stage_pers, dim3(grid), dim3(256), lds, st, *single, pc, tiles);
-            } else {
-                m.blk0[m.nprog] = tiles;
-                if (waves == 8)
-                    hipLaunchKernelGGL(k_stage_pers8_multi, dim3(grid), dim3(512), lds, st, m, pc);
-                else
-                    hipLaunchKernelGGL(k_stage_pers_multi, dim3(grid), dim3(256), lds, st, m, pc);
-            }
+            FrontCtl fc{ctr, cl, ev, g_front_diag};
+            const uint32_t lds = front_lds_bytes(cl, ev);
+            if (lds > 160u * 1024u - 2048u) return hipErrorInvalidValue;
+            if (m.nprog == 1)
+                hipLaunchKernelGGL(k_stage_front, dim3(grid), dim3(64 * kFrontWaves), lds, st, *single, fc);
+            else
+                hipLaunchKernelGGL(k_stage_front_multi, dim3(grid), dim3(64 * kFrontWaves), lds, st, m, fc);
             e = hipGetLastError();
         }
         m.nprog = 0;
-        used = tiles = cl = ev = 0;
+        used = cl = ev = 0;
         return e;
     };
     for (int i = 0; i < n; ++i) {
         const StageArgs& a = *progs[i];
         if (a.e_end <= a.e_begin) continue;
-        if (a.C + a.L > kMaxAdv + kMaxLk || a.nv > kMaxV) return hipErrorInvalidValue;
         const uint32_t rb = stage_record_bytes(a.nmo, a.C, a.L, a.nk);
         if (m.nprog == (uint32_t)kMaxMulti || used + rb > kMultiBytes || (m.nprog && rb > kMultiBytes)) {
             const hipError_t e = flush();
@@ -1222,7 +1195,6 @@ hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t s
         if (rb > kMultiBytes) {                         // too large for a record: a launch of its own
             single = &a;
             m.nprog = 1;
-            tiles = (a.e_end - a.e_begin + kPersTile - 1) / kPersTile;
             cl = a.C + a.L;
             ev = stage_elem_words(a.nv ? a.nv : 1);
             const hipError_t e = flush();
@@ -1240,11 +1212,10 @@ hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t s
         q += 4 * a.L;
         memcpy(q, a.K, 32 * a.nk);
         m.off[m.nprog] = used;
-        m.blk0[m.nprog] = tiles;
+        m.blk0[m.nprog] = 0;
         ++m.nprog;
         if (m.nprog == 1) single = &a;
         used += rb;
-        tiles += (a.e_end - a.e_begin + kPersTile - 1) / kPersTile;
         cl = std::max(cl, a.C + a.L);
         ev = std::max(ev, stage_elem_words(a.nv ? a.nv : 1));
     }

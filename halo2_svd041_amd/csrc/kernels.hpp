@@ -240,13 +240,16 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t st);
 // Independent stages (no stage reads another's cells) in as few k_stage_multi
 // launches as their records fit (stage_record_bytes, kMultiBytes); n >= 1.
 hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st);
-// The same stages on the persistent streamer (k_stage_pers): a grid of occ
-// blocks per CU taking 64-element tiles from the counters at ctr (two words,
-// zero between launches; one slot per stream: launches on one stream never
-// overlap). ctr null or occ 0: launch_stage_multi.
-// waves: 4 or 8 per block (one producer wave, the rest consumers).
+// The same stages on the persistent front streamer (k_stage_front): occ blocks
+// per CU writing every output region as a compact moving front of 4 KiB
+// windows, tickets from the counters at ctr (two words, zero between
+// launches; one slot per stream: launches on one stream never overlap).
+// ctr null, occ 0, a batch under min_bytes of cells or a region of one cell
+// per element: launch_stage_multi.
 hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t st, uint32_t* ctr, uint32_t occ,
-                             uint32_t waves);
+                             double min_bytes);
+// timing diagnostic of the front streamer (cells WRONG): 1 = no producer view loads
+void set_front_diag(uint32_t d);
 // does the record of `a` fit one k_stage_multi launch?
 bool stage_multi_fits(const StageArgs& a);
 // max over the view of bit-length(|signed(x)|): out[b] = max of block b

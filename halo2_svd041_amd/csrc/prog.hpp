@@ -66,7 +66,6 @@ struct SlotOp {
 static constexpr uint8_t KSRC = 0x80;
 
 static constexpr uint32_t STAGE_ALIGN = 256;     // 4 KiB-aligned block store windows
-static constexpr uint32_t STAGE_CELL = 512;      // phase B one whole cell per lane (8 KiB windows)
 
 static constexpr int kMaxViews = 2;
 static constexpr int kMaxMicro = 16;

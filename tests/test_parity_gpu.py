@@ -199,7 +199,9 @@ def test_crt_gemm_tiles_parity(gpu_ctx_factory, N, M, P, world, device):
                                   {"phase1_overlap": 0}, {"phase1_overlap": 2},
                                   {"overlap": 0},
                                   {"stage_batch": 0}, {"pipeline": 0}, {"pipeline": 0, "phase1_overlap": 2},
-                                  {"gemm_impl": 1}, {"res_f64": 0}, {"f64_views": 0}])
+                                  {"gemm_impl": 1}, {"res_f64": 0}, {"f64_views": 0},
+                                  {"stage_occ": 0}, {"stage_occ": 1, "stage_front_all": 1},
+                                  {"stage_occ": 2, "stage_front_all": 1}, {"small_spread": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
@@ -562,6 +564,28 @@ def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device, hol
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g, row_lim=row_lim)
     get = lambda ph, lk, off, n: (ctx.lookups if lk else ctx.advice)(ph, off, n)   # noqa: E731
     assert walk_window(ctx.layout(), get, {(0, 0): a0, (0, 1): l0, (1, 0): a1}, 0, row_lim) > 0
+
+
+@pytest.mark.parametrize("N,M,P,occ,pipe", [(256, 192, 63, 1, 1), (192, 256, 32, 2, 1), (300, 300, 42, 1, 0),
+                                          (1, 1, 32, 1, 0), (7, 130, 63, 1, 1)])
+def test_front_streamer_parity(gpu_ctx_factory, N, M, P, occ, pipe):
+    """k_stage_front (the persistent front streamer) on every stage batch of
+    the witness (stage_front_all: no size threshold), whole advice and lookup
+    streams against the oracle; device inputs, pipelined or not, two calls in
+    a row (the second reuses the ticket counters the first one's last block
+    reset)."""
+    import halo2_svd041_amd as hs
+    ctx = gpu_ctx_factory(P)
+    ctx.set_option("stage_occ", occ)
+    ctx.set_option("stage_front_all", 1)
+    ctx.set_option("pipeline", pipe)
+    for k in range(2):
+        m, u, d, v = gen_svd_input(N, M, seed=800 + k + N)
+        g = gamma_for(810 + k)
+        hs.svd_witness(ctx, *_on_device(m, u, v, d), g)
+    ctx.sync()
+    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
+    _assert_streams(ctx, a0, l0, a1)
 
 
 @pytest.mark.parametrize("shapes,P,row_begin,row_lim,hold", [
