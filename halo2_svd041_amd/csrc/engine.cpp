@@ -490,7 +490,7 @@ struct svdw_ctx {
     // (k_stage / k_stage_multi). Its ticket counters: one 256-byte slot per
     // stream (cell stream, st2, st3), zero between launches (each launch's last
     // block resets its slot).
-    uint32_t stage_occ = 1;
+    uint32_t stage_occ = 0;
     bool small_spread = true;               // "small_spread": small stage launches over more blocks
     double stage_front_min = 64.0 * (1 << 20);   // "stage_front_all" 1: 0 (tests: every batch)
     DBuf stage_ctr;

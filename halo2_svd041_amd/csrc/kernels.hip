@@ -900,32 +900,25 @@ __device__ __forceinline__ Prefetch front_loads(const StageArgs& a, uint32_t e, 
     }
     return f;
 }
-// One output region of one program, cut into 4 KiB windows.
+// One output region of one program, cut into 4 KiB windows (32-bit geometry:
+// the launcher keeps regions below 2^31 half-cells on this kernel).
 struct FStream {
-    uint64_t H;          // half-cells (2 U n)
+    uint32_t H;          // half-cells (2 U n)
     uint32_t prog, lk;   // program, region (0 advice, 1 lookups)
     uint32_t U, magic;   // cells per element, ceil(2^32 / U)
     uint32_t mis;        // half-cells from the 4 KiB boundary below the region start
     uint32_t epw, K;     // element slots per window, windows per ticket
     uint32_t nw, t0;     // windows, first ticket
 };
-// Window j of a ticket: half-cells [h0, h1) of the region, the element of its
-// first cell (first) and that cell's slot in it (phase); false if past the end.
+static constexpr uint32_t kMaxWin = kFrontElems / 2;   // K <= kFrontElems / epw, epw >= 2
+// Window j of a ticket (computed once per ticket by the producer, in LDS):
+// lane 0's half-cell hb (256 W - mis, negative for a region's first window),
+// the cell of its first in-range half-cell c0, that cell's element (first, in
+// the region) and slot (phase).
 struct FWin {
-    int64_t hb;          // half-cell of lane 0 (256 W - mis, may be negative)
-    uint32_t first, phase;
+    int32_t hb;
+    uint32_t c0, first, phase;
 };
-__device__ __forceinline__ bool front_win(const FStream& F, uint32_t s, uint32_t b, uint32_t j, uint32_t G,
-                                          FWin* w) {
-    if (j >= F.K) return false;
-    const uint64_t W = ((uint64_t)s * F.K + j) * G + b;
-    if (W >= F.nw) return false;
-    w->hb = (int64_t)(W * 256) - (int64_t)F.mis;
-    const uint64_t c0 = (uint64_t)(w->hb < 0 ? 0 : w->hb) >> 1;
-    w->first = (uint32_t)(c0 / F.U);
-    w->phase = (uint32_t)(c0 - (uint64_t)w->first * F.U);
-    return true;
-}
 struct SrcMulti {
     const StageMulti* m;
     __device__ uint32_t nprog() const { return m->nprog; }
@@ -946,8 +939,9 @@ template <class SRC>
 __device__ __forceinline__ void stage_front(const SRC& S, const FrontCtl& fc) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     __shared__ FStream sF[kMaxStreams];
+    __shared__ FWin sW[3][kMaxWin];          // ring: current, next, after-next ticket
     __shared__ uint32_t sNS, sTT;
-    __shared__ uint32_t sTile[2], sSet[2], sProg[2];
+    __shared__ uint32_t sTile[2], sSet[2], sNW[2], sProg[2];
     const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, G = gridDim.x;
     const uint32_t sw = front_set_words(fc.cl), bw = kFrontElems * fc.ev + 16, ev = fc.ev, cl = fc.cl;
     auto set_off = [&](uint32_t x) { return x ? sw : 0u; };
@@ -964,7 +958,7 @@ __device__ __forceinline__ void stage_front(const SRC& S, const FrontCtl& fc) {
                 if (!U || !n) continue;
                 FStream& F = sF[ns++];
                 const Fr* base = (lk ? a.out_lk + (uint64_t)a.e_begin * U : a.out_adv + (uint64_t)a.e_begin * U);
-                F.H = 2ull * U * n;
+                F.H = 2u * U * n;
                 F.prog = p;
                 F.lk = lk;
                 F.U = U;
@@ -972,7 +966,7 @@ __device__ __forceinline__ void stage_front(const SRC& S, const FrontCtl& fc) {
                 F.mis = (uint32_t)(reinterpret_cast<uintptr_t>(base) >> 4) & 255u;
                 F.epw = front_epw(U);
                 F.K = kFrontElems / F.epw;
-                F.nw = (uint32_t)((F.H + F.mis + 255) / 256);
+                F.nw = (F.H + F.mis + 255) / 256;
                 F.t0 = tt;
                 tt += (F.nw + F.K * G - 1) / (F.K * G) * G;
             }
@@ -988,35 +982,53 @@ __device__ __forceinline__ void stage_front(const SRC& S, const FrontCtl& fc) {
         for (uint32_t i = 1; i < NS; ++i) k += q >= sF[i].t0;
         return k;
     };
-    // producer state: tile n1 (loads fa / fb of its two passes in flight), n2
-    // (known), dequeue n3v in flight
+    // producer state: ticket n1 (view loads fa / fb of its two passes in
+    // flight), n2 (known), dequeue n3v in flight
     static_assert(kFrontElems == 128, "two producer passes");
     uint32_t n1 = 0, n2 = 0, n3v = 0;
     Prefetch fa{fr_zero(), fr_zero(), false, false}, fb = fa;
-    // element slot t of ticket q: its element (global index), or false
-    auto slot_elem = [&](uint32_t q, const FStream& F, uint32_t t, uint32_t* e) -> bool {
+    // the windows of ticket q into sW[x] (lane j: window j); returns their count
+    auto windows = [&](uint32_t q, const FStream& F, uint32_t x) -> uint32_t {
         const uint32_t local = q - F.t0, s = local / G, b = local - s * G;
+        const uint32_t w0 = s * F.K * G + b;                        // window of j = 0
+        const uint32_t nwin = w0 >= F.nw ? 0u : min(F.K, (F.nw - w0 + G - 1) / G);
+        if (lane < nwin) {
+            const uint32_t W = w0 + lane * G;
+            FWin w;
+            w.hb = (int32_t)(W * 256u) - (int32_t)F.mis;
+            w.c0 = (uint32_t)(w.hb < 0 ? 0 : w.hb) >> 1;
+            w.first = w.c0 / F.U;
+            w.phase = w.c0 - w.first * F.U;
+            sW[x][lane] = w;
+        }
+        return nwin;
+    };
+    // element slot t of the ticket whose windows are in sW[x]: its element in the region
+    auto slot_elem = [&](const FStream& F, uint32_t x, uint32_t nwin, uint32_t t, uint32_t* e) -> bool {
         const uint32_t j = t / F.epw, kk = t - j * F.epw;
-        FWin w;
-        if (!front_win(F, s, b, j, G, &w)) return false;
-        const int64_t hl = w.hb + 255 < (int64_t)F.H - 1 ? w.hb + 255 : (int64_t)F.H - 1;
-        const uint32_t last = (uint32_t)(((uint64_t)hl >> 1) / F.U);
-        if (w.first + kk > last) return false;
-        *e = S.rec(F.prog).a->e_begin + w.first + kk;
-        return true;
+        if (j >= nwin) return false;
+        const FWin w = sW[x][j];
+        const int32_t hl = min(w.hb + 255, (int32_t)F.H - 1);
+        const uint32_t last = ((uint32_t)hl >> 1) / F.U;
+        *e = w.first + kk;
+        return *e <= last;
     };
-    auto issue_loads = [&](uint32_t q) {
-        if (q >= TT || fc.diag) return;
+    // ticket q's windows into window slot x, and its view loads (fa, fb)
+    auto issue_loads = [&](uint32_t q, uint32_t x) {
+        if (q >= TT) return;
         const FStream F = sF[stream_of(q)];
-        const Rec r = S.rec(F.prog);
+        const uint32_t nwin = windows(q, F, x);
+        if (fc.diag) return;
+        const StageArgs& a = *S.rec(F.prog).a;
         uint32_t e0 = 0, e1 = 0;
-        const bool v0 = slot_elem(q, F, lane, &e0), v1 = slot_elem(q, F, 64 + lane, &e1);
-        fa = front_loads(*r.a, e0, v0);
-        fb = front_loads(*r.a, e1, v1);
+        const bool v0 = slot_elem(F, x, nwin, lane, &e0), v1 = slot_elem(F, x, nwin, 64 + lane, &e1);
+        fa = front_loads(a, a.e_begin + e0, v0);
+        fb = front_loads(a, a.e_begin + e1, v1);
     };
-    // phase A of ticket q into buffer x; tables into the set the current ticket
-    // does not use, unless it is the same program
-    auto phase_a = [&](uint32_t q, uint32_t x, uint32_t cur_set) {
+    // phase A of ticket q (windows already in window slot ws) into buffer x;
+    // tables into the set the current ticket does not use, unless it is the
+    // same program
+    auto phase_a = [&](uint32_t q, uint32_t x, uint32_t ws, uint32_t cur_set) {
         if (q >= TT) {
             if (lane == 0) sTile[x] = TT;
             return;
@@ -1032,6 +1044,9 @@ __device__ __forceinline__ void stage_front(const SRC& S, const FrontCtl& fc) {
             }
         }
         const FSet ts = front_set(smem + set_off(st), cl);
+        const uint32_t local = q - F.t0, s = local / G, b = local - s * G;
+        const uint32_t w0 = s * F.K * G + b;
+        const uint32_t nwin = w0 >= F.nw ? 0u : min(F.K, (F.nw - w0 + G - 1) / G);
         for (uint32_t ps = 0; ps < 2; ++ps) {
             uint32_t e = 0;
             // (pass ps's prefetch, selected word by word: an indexed array of
@@ -1043,13 +1058,14 @@ __device__ __forceinline__ void stage_front(const SRC& S, const FrontCtl& fc) {
                 v1.w[w] = ps ? fb.v1.w[w] : fa.v1.w[w];
             }
             const bool in0 = ps ? fb.in0 : fa.in0, in1 = ps ? fb.in1 : fa.in1;
-            if (slot_elem(q, F, ps * 64 + lane, &e))
-                element_program(*r.a, e, smem + buf_off(x) + (ps * 64 + lane) * ev, ts.K, ts.mo, ts.vw, v0, in0,
-                                v1, in1);
+            if (slot_elem(F, ws, nwin, ps * 64 + lane, &e))
+                element_program(*r.a, r.a->e_begin + e, smem + buf_off(x) + (ps * 64 + lane) * ev, ts.K, ts.mo,
+                                ts.vw, v0, in0, v1, in1);
         }
         if (lane == 0) {
             sTile[x] = q;
             sSet[x] = st;
+            sNW[x] = nwin;
         }
     };
     if (wave == 0) {
@@ -1062,58 +1078,79 @@ __device__ __forceinline__ void stage_front(const SRC& S, const FrontCtl& fc) {
         t0 = __builtin_amdgcn_readfirstlane(t0);
         n1 = __builtin_amdgcn_readfirstlane(t1);
         n2 = __builtin_amdgcn_readfirstlane(t2);
-        issue_loads(t0);
-        phase_a(t0, 0, 0);
-        issue_loads(n1);
+        issue_loads(t0, 0);
+        phase_a(t0, 0, 0, 0);
+        issue_loads(n1, 1);
         if (lane == 0) n3v = atomicAdd(fc.ctr, 1u);
     }
     __syncthreads();
-    for (uint32_t k = 0;; ++k) {
-        const uint32_t bx = k & 1u;
+    for (uint32_t k = 0, wk = 0;; ++k, wk = wk == 2 ? 0u : wk + 1) {
+        const uint32_t bx = k & 1u;                                 // buffers by parity, windows by k mod 3
+        const uint32_t wk1 = wk == 2 ? 0u : wk + 1, wk2 = wk1 == 2 ? 0u : wk1 + 1;
         const uint32_t cur = sTile[bx];
         if (cur >= TT) break;                                       // (uniform)
         const uint32_t cset = sSet[bx];
         if (wave == 0) {
             // ---- producer: the next ticket's phase A into the other buffer
-            phase_a(n1, bx ^ 1u, cset);
+            // (its windows and loads were prepared a round ago), then the
+            // windows and view loads of the ticket after it
+            phase_a(n1, bx ^ 1u, wk1, cset);
             n1 = n2;
             n2 = __builtin_amdgcn_readfirstlane(n3v);               // (returned during phase A's waits)
-            issue_loads(n1);
+            issue_loads(n1, wk2);
             if (lane == 0) n3v = atomicAdd(fc.ctr, 1u);
         } else {
-            // ---- consumers: the current ticket's windows, one half-cell per lane
+            // ---- consumers: the current ticket's windows, one half-cell per
+            // lane, two windows per step (their LDS reads in flight together)
             const FStream F = sF[stream_of(cur)];
-            const Rec r = S.rec(F.prog);
-            const StageArgs& a = *r.a;
-            const uint32_t local = cur - F.t0, s = local / G, b = local - s * G;
-            const FSet ts = front_set(smem + set_off(cset), cl);
+            const StageArgs& a = *S.rec(F.prog).a;
+            const uint32_t so = set_off(cset);
+            const FSet ts = front_set(smem + so, cl);
             const uint32_t rb = F.lk ? a.C : 0u;                    // the region's first slot
             const uint32_t* Dr = ts.D + 2 * rb;
             const uint4* Mr = ts.M + 2 * rb;
             uint4* out = reinterpret_cast<uint4*>(F.lk ? a.out_lk + (uint64_t)a.e_begin * F.U
                                                        : a.out_adv + (uint64_t)a.e_begin * F.U);
-            const uint32_t u = tid - 64, vb = buf_off(bx);
-            for (uint32_t j = 0;; ++j) {
-                FWin w;
-                if (!front_win(F, s, b, j, G, &w)) break;           // (uniform)
-                const int64_t hc = w.hb + (int64_t)u;
-                if (hc >= 0 && (uint64_t)hc < F.H) {
-                    // cell (hc >> 1) = first + (rel / U) elements, slot rel % U
-                    const uint32_t rel = (uint32_t)((uint64_t)(hc >> 1) - (((uint64_t)(w.hb < 0 ? 0 : w.hb)) >> 1)) +
-                                         w.phase;
-                    const uint32_t el = fastdiv(rel, F.U, F.magic), slot = rel - el * F.U;
-                    const uint32_t h = (uint32_t)hc & 1u, kx = 2 * slot + h;
-                    const uint32_t d = Dr[kx];
-                    const uint4 m = Mr[kx];
-                    const uint32_t* x = smem + ((d & kHalfElem) ? vb + (j * F.epw + el) * ev : set_off(cset)) +
-                                        (d & 0xffffu);
-                    const uint32_t sh = (d >> 16) & 31u;
-                    const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4];
+            const uint32_t u = tid - 64, vb = buf_off(bx), nwin = sNW[bx], U = F.U, mag = F.magic, H = F.H;
+            auto half = [&](uint32_t j, bool& ok, int32_t& hc, uint32_t& d, uint4& m, uint32_t& base) {
+                const FWin w = sW[wk][j];
+                hc = w.hb + (int32_t)u;
+                ok = hc >= 0 && (uint32_t)hc < H;
+                const uint32_t rel = ((uint32_t)max(hc, 0) >> 1) - w.c0 + w.phase;
+                const uint32_t el = fastdiv(rel, U, mag), slot = rel - el * U;
+                const uint32_t kx = 2 * slot + ((uint32_t)hc & 1u);
+                d = ok ? Dr[kx] : 0u;
+                m = ok ? Mr[kx] : make_uint4(0, 0, 0, 0);
+                base = ((d & kHalfElem) ? vb + (j * F.epw + el) * ev : so) + (d & 0xffffu);
+            };
+            auto put = [&](bool ok, int32_t hc, uint32_t d, const uint4& m, uint32_t base) {
+                const uint32_t sh = (d >> 16) & 31u;
+                const uint32_t* x = smem + base;
+                const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4];
+                if (ok)
                     out[hc] = make_uint4(__builtin_amdgcn_alignbit(x1, x0, sh) & m.x,
                                          __builtin_amdgcn_alignbit(x2, x1, sh) & m.y,
                                          __builtin_amdgcn_alignbit(x3, x2, sh) & m.z,
                                          __builtin_amdgcn_alignbit(x4, x3, sh) & m.w);
-                }
+            };
+            uint32_t j = 0;
+            for (; j + 2 <= nwin; j += 2) {
+                bool ok0, ok1;
+                int32_t h0, h1;
+                uint32_t d0, d1, b0, b1;
+                uint4 m0, m1;
+                half(j, ok0, h0, d0, m0, b0);
+                half(j + 1, ok1, h1, d1, m1, b1);
+                put(ok0, h0, d0, m0, b0);
+                put(ok1, h1, d1, m1, b1);
+            }
+            if (j < nwin) {
+                bool ok0;
+                int32_t h0;
+                uint32_t d0, b0;
+                uint4 m0;
+                half(j, ok0, h0, d0, m0, b0);
+                put(ok0, h0, d0, m0, b0);
             }
         }
         __syncthreads();
@@ -1155,6 +1192,7 @@ static bool front_suits(const StageArgs* const* progs, int n, double min_bytes) 
         if (a.C + a.L > kMaxAdv + kMaxLk || a.nv > kMaxV) return false;
         if ((a.C && kFrontElems / front_epw(a.C) == 0) || (a.L && kFrontElems / front_epw(a.L) == 0)) return false;
         bytes += 32.0 * (a.e_end - a.e_begin) * (a.C + a.L);
+        if (2.0 * (a.e_end - a.e_begin) * std::max(a.C, a.L) >= 2147483648.0 - 512.0) return false;
     }
     return bytes > 0 && bytes >= min_bytes;
 }
