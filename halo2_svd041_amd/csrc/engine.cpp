@@ -491,7 +491,6 @@ struct svdw_ctx {
     // stream (cell stream, st2, st3), zero between launches (each launch's last
     // block resets its slot).
     uint32_t stage_occ = 0;
-    bool small_spread = true;               // "small_spread": small stage launches over more blocks
     double stage_front_min = 64.0 * (1 << 20);   // "stage_front_all" 1: 0 (tests: every batch)
     DBuf stage_ctr;
     hipStream_t stream_id[3] = {};          // st, st2, st3 as created (st / st2 / st3 are swapped at times)
@@ -984,7 +983,6 @@ static void check_mat(const svdw_ctx* c, const svdw_mat& m) {
 static void check_vec(const svdw_ctx* c, const svdw_vec& v) { check_mat(c, mat_of_vec(v)); }
 
 // ------------------------------------------------------- stage launches
-static constexpr uint32_t kSpreadBlocks = 128;
 // The persistent stage kernel's tile counters for a launch on stream s (null:
 // not one of the context's streams -> the one-block-per-chunk kernels).
 static uint32_t* stage_ctr_for(svdw_ctx* c, hipStream_t s) {
@@ -1039,13 +1037,6 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     // keep the block's LDS (element values) within 64 KiB: fewer elements per
     // block for stages with many values (signed_div_scale)
     while (a.E > 64 && stage_lds_bytes(a.nv ? a.nv : 1, a.E, a.C + a.L) > 65536) a.E -= 64;
-    // small launches (d checks, is_equal rows, a row-sharded rank's tails):
-    // spread over >= kSpreadBlocks blocks -- one block writing a few hundred KB
-    // runs at one CU's store rate (29 us for the d checks on an 8-way rank)
-    if (c->small_spread) {
-        const uint32_t n = ee - eb;
-        while (a.E > 16 && a.E % 32 == 0 && (n + a.E - 1) / a.E < kSpreadBlocks) a.E /= 2;
-    }
     // 32-bit magics for fastdiv (divisor 1 is handled in the kernel)
     auto magic = [](uint64_t d) -> uint32_t { return d > 1 ? (uint32_t)(((1ull << 32) + d - 1) / d) : 0; };
     a.cdiv_magic = magic(a.C);
@@ -3239,18 +3230,17 @@ static void ctx_init_device(svdw_ctx* c) {
 // The settings (options, shard, profiler) of `s` onto the lane `d`; a change
 // bumps the lane's epoch (its captured graph no longer applies).
 static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
-    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->stage_occ, s->small_spread, (int64_t)s->stage_front_min, s->gemm_crt, s->res_f64,
+    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->stage_occ, (int64_t)s->stage_front_min, s->gemm_crt, s->res_f64,
                          s->phase1_overlap, s->prod_cell, s->hold_us, s->rlc_prefix, s->p1_at,
                          s->f64_views, s->overlap, s->stage_batch, s->graph_vm, s->vm_linear, s->pipeline,
                          s->shard_rank, s->shard_world, s->prof, s->host_trace};
-    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->stage_occ, d->small_spread, (int64_t)d->stage_front_min, d->gemm_crt, d->res_f64,
+    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->stage_occ, (int64_t)d->stage_front_min, d->gemm_crt, d->res_f64,
                          d->phase1_overlap, d->prod_cell, d->hold_us, d->rlc_prefix, d->p1_at,
                          d->f64_views, d->overlap, d->stage_batch, d->graph_vm, d->vm_linear, d->pipeline,
                          d->shard_rank, d->shard_world, d->prof, d->host_trace};
     if (!memcmp(a, b, sizeof a) && d->prof_filter == s->prof_filter) return;
     d->gemm_impl = s->gemm_impl; d->stage_flags = s->stage_flags; d->stage_elems = s->stage_elems;
     d->stage_occ = s->stage_occ;
-    d->small_spread = s->small_spread;
     d->stage_front_min = s->stage_front_min;
     d->gemm_crt = s->gemm_crt; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
     d->prod_cell = s->prod_cell; d->hold_us = s->hold_us; d->rlc_prefix = s->rlc_prefix;
@@ -4579,8 +4569,8 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "stage_occ") {               // persistent front streamer (0: off)
             REQUIRE(value >= 0 && value <= 2, "stage_occ: 0, 1 or 2 blocks per CU");
             c->stage_occ = (uint32_t)value;
-        } else if (n == "small_spread") {
-            c->small_spread = value != 0;
+        } else if (n == "stage_nt") {                // non-temporal stage cell stores
+            c->stage_flags = value ? (c->stage_flags | STAGE_NT) : (c->stage_flags & ~STAGE_NT);
         } else if (n == "stage_diag") {              // timing diagnostic, process-wide (wrong cells)
             set_front_diag((uint32_t)value);
         } else if (n == "stage_front_all") {         // test hook: the front streamer for every batch
