@@ -4571,8 +4571,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->stage_occ = (uint32_t)value;
         } else if (n == "stage_nt") {                // non-temporal stage cell stores
             c->stage_flags = value ? (c->stage_flags | STAGE_NT) : (c->stage_flags & ~STAGE_NT);
-        } else if (n == "gemm_split") {              // split-K of small CRT products (process-wide)
-            set_crt_split(value != 0);
         } else if (n == "stage_diag") {              // timing diagnostic, process-wide (wrong cells)
             set_front_diag((uint32_t)value);
         } else if (n == "stage_front_all") {         // test hook: the front streamer for every batch

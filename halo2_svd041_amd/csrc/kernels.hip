@@ -1964,20 +1964,6 @@ static constexpr int CT = CT_TILE;     // CRT GEMM block tile (4 waves of 64 x 6
 // fragment reads (16 rows x 1 part) both land on 16 distinct 4-bank groups.
 static constexpr int CROW = 64;
 static constexpr uint32_t kCrtTileBytes = CT * CT;             // residues of one (tile, modulus)
-// Split-K for products of few tiles (a row-sharded rank's row block, 512^2):
-// with one (tile, modulus) per block such a GEMM is a few hundred blocks, each
-// a serial chain of kpad / 64 chunk steps. Below kCrtSplitTiles tiles per job
-// the K dimension is cut into ksplit parts, each block multiplies one part
-// into residue planes of its own (crt_split_plane apart) and the combine adds
-// the parts' residues mod m_k (sum mod m = sum of residues mod m).
-static constexpr uint32_t kCrtSplitTiles = 32;
-static constexpr uint32_t kCrtMaxSplit = 4;
-__host__ __device__ constexpr uint32_t crt_ksplit(uint32_t nblk, uint32_t kpad) {
-    return nblk >= kCrtSplitTiles ? 1u : (kpad / 64) % 16 == 0 ? 4u : (kpad / 64) % 8 == 0 ? 2u : 1u;
-}
-__host__ __device__ constexpr uint64_t crt_split_plane(uint32_t nblk) {
-    return (uint64_t)kCrtMaxMod * nblk * kCrtTileBytes;
-}
 __device__ __forceinline__ uint32_t crt_lds(uint32_t row, uint32_t part) {
     return row * CROW + 16u * (part ^ ((row >> 2) & 3u));
 }
@@ -1996,7 +1982,7 @@ __device__ __forceinline__ uint32_t crt_lds(uint32_t row, uint32_t part) {
 // per step took ~1 us per step, ~16 us per tile, against ~0.1 us of MFMA.)
 constexpr int crt_lds_bytes() { return 4 * CT * CROW; }
 __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, const uint8_t* __restrict__ Br,
-                                              uint32_t astride, uint32_t bstride, uint32_t kpad, uint32_t kcn,
+                                              uint32_t astride, uint32_t bstride, uint32_t kpad,
                                               uint32_t nblk, uint32_t tile, uint8_t* __restrict__ R,
                                               uint32_t bi, uint32_t bj, int mod, uint8_t* __restrict__ S,
                                               uint64_t& tp1, uint64_t& tp2) {
@@ -2006,6 +1992,7 @@ __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, co
     const uint8_t* Bp = Br + ((uint64_t)mod * bstride + bj * CT) * kpad;
     // staging map: 512 x 16 B per operand chunk; thread -> (row, part) for q = tid, tid + 256
     const uint32_t r0 = tid >> 2, r1 = (tid + 256) >> 2, part = tid & 3;
+    const uint32_t kcn = kpad / 64;
     v4i acc[4][4];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -2064,8 +2051,7 @@ __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, co
     __syncthreads();
     tp1 = wall_clock64();
     CRT_FRAG(0);
-    // kcn is a multiple of 4 (kpad % 256 == 0, a split-K block's share of the
-    // chunks too, crt_ksplit): the steps are branch-free, so
+    // kcn is a multiple of 4 (kpad % 256 == 0): the steps are branch-free, so
     // the compiler's load counters see the four chunks in flight (a branch per
     // step made it drain every load before each LDS store). The last group's
     // stores and fragment reads of chunks >= kcn (clamped loads) are unused.
@@ -2166,8 +2152,7 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
     for (int j = 0; j < kMaxCrtJobs; ++j) {
         cnt[j] = 0;
         if ((uint32_t)j < b.njobs)
-            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk *
-                     b.job[j].ksplit;
+            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk;
         total += cnt[j];
     }
     const uint32_t per = (total + 7) / 8, k = blockIdx.x >> 3;
@@ -2179,17 +2164,12 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
     for (int q = 0; q < kMaxCrtJobs - 1; ++q)
         if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
     const CrtJob& q = b.job[j];
-    // unit -> (modulus, tile, K split): split s multiplies chunks [s c, (s + 1) c)
-    // of the K dimension into its own residue planes (the combine adds them)
-    const uint32_t per_mod = q.nblk * q.ksplit;
-    const uint32_t mod = u / per_mod, rest = u - mod * per_mod, t = rest / q.ksplit, sp = rest - t * q.ksplit;
-    const uint32_t kcs = q.kpad / 64 / q.ksplit;
+    const uint32_t mod = u / q.nblk, t = u - mod * q.nblk;
     uint32_t bi, bj;
     crt_tile_rc(q, t, &bi, &bj);
     uint64_t tp1 = 0, tp2 = 0;
-    crt_gemm_tile(q.Ar + sp * kcs * 64, (q.sym ? q.Ar : q.Br) + sp * kcs * 64, q.astride,
-                  q.sym ? q.astride : q.bstride, q.kpad, kcs, q.nblk, t,
-                  q.R + (uint64_t)sp * crt_split_plane(q.nblk), bi, bj, (int)mod, S, tp1, tp2);
+    crt_gemm_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.nblk, t,
+                  q.R, bi, bj, (int)mod, S, tp1, tp2);
     trace_block(t0, tp1, tp2);
 }
 // C from its n residues, written as canonical Fr to out[i*ors + j*ocs]: one
@@ -2221,19 +2201,6 @@ __device__ __forceinline__ void crt_combine_elem(const CrtJob& q, uint32_t cblk)
     uint32_t r[kCrtMaxMod];
 #pragma unroll
     for (int k = 0; k < kCrtMaxMod; ++k) r[k] = k < n ? rp[k * plane] : 0u;
-    if (q.ksplit > 1) {                                    // split-K: the residues of the splits' sums
-        const uint64_t sp = crt_split_plane(q.nblk);
-        for (uint32_t s = 1; s < q.ksplit; ++s) {
-#pragma unroll
-            for (int k = 0; k < kCrtMaxMod; ++k) r[k] += k < n ? rp[s * sp + k * plane] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < kCrtMaxMod; ++k) {
-            const uint32_t m = c_crt_mod[k];
-#pragma unroll
-            for (int it = 0; it < 3; ++it) r[k] -= r[k] >= m ? m : 0u;   // < 4 m before
-        }
-    }
     const int off = n * (n - 1) / 2;
     // one 64-bit accumulator per 32-bit word of E_k (v_mad_u64_u32): r (8 bit)
     // x word (32 bit) summed over n <= 40 moduli stays below 2^46 -> no carries
@@ -2280,12 +2247,10 @@ __global__ __launch_bounds__(256) void k_crt_combine_multi(const CrtBatch b, uin
 }
 
 size_t crt_scratch_bytes(uint32_t N, uint32_t M) {
-    // kCrtMaxMod planes of whole 128 x 128 tiles, per K split (crt_ksplit)
-    const uint64_t a = ((uint64_t)N + CT - 1) / CT, m = ((uint64_t)M + CT - 1) / CT;
-    return (size_t)(kCrtMaxMod * a * m * kCrtTileBytes) * (a * m < kCrtSplitTiles ? kCrtMaxSplit : 1);
+    // kCrtMaxMod planes of whole 128 x 128 tiles
+    const uint64_t a = ((uint64_t)N + CT - 1) / CT * CT, m = ((uint64_t)M + CT - 1) / CT * CT;
+    return (size_t)(kCrtMaxMod * a * m);
 }
-static bool g_crt_split = true;
-void set_crt_split(bool on) { g_crt_split = on; }
 hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
     CrtBatch b = b0;
     if (b.njobs < 1 || b.njobs > (uint32_t)kMaxCrtJobs) return hipErrorInvalidValue;
@@ -2305,8 +2270,7 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
         } else if (q.tile0) {
             return hipErrorInvalidValue;
         }
-        q.ksplit = g_crt_split ? crt_ksplit(q.nblk, q.kpad) : 1u;
-        units += kCrtMaxMod * q.nblk * q.ksplit;         // upper bound: n = kCrtMaxMod
+        units += kCrtMaxMod * q.nblk;                    // upper bound: n = kCrtMaxMod
         q.cblk0 = cblocks;
         cblocks += q.nblk * (kCrtTileBytes / 256);
     }

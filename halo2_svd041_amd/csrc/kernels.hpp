@@ -351,14 +351,11 @@ struct CrtJob {
     // all): a row block of a product (SYM: the upper tiles of rows of tiles
     // [b0, b1), whose mirrors land in later rows)
     uint32_t tile0, tcount;
-    uint32_t ksplit;     // K splits (set by the launcher, crt_ksplit)
 };
 struct CrtBatch {
     CrtJob job[kMaxCrtJobs];
     uint32_t njobs;
 };
-// split-K of small CRT products (crt_ksplit) on (default) / off, process-wide
-void set_crt_split(bool on);
 // R sized crt_scratch_bytes per job
 hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st);
 // residue scratch R one CRT product of N x M needs

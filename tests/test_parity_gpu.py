@@ -566,36 +566,6 @@ def test_full_size_sampled_parity(gpu_ctx_factory, N, M, P, row_lim, device, hol
     assert walk_window(ctx.layout(), get, {(0, 0): a0, (0, 1): l0, (1, 0): a1}, 0, row_lim) > 0
 
 
-@pytest.mark.parametrize("N,M,P,world,split", [(128, 1024, 63, 1, 1), (128, 1024, 63, 1, 0), (300, 600, 32, 1, 1),
-                                                (256, 768, 42, 4, 1), (640, 512, 63, 1, 1)])
-def test_split_k_parity(gpu_ctx_factory, N, M, P, world, split):
-    """Split-K of small CRT products (crt_ksplit: fewer than 32 output tiles,
-    K split in 4 or 2 with per-split residue planes that the combine adds mod
-    m_k): m.v^T of a 128 x 1024 matrix (8 tiles, K = 1024: 4 splits), products
-    with K = 512 (2 splits), a row-sharded rank's row blocks; whole advice and
-    lookup streams against the oracle, with the split on and off."""
-    import halo2_svd041_amd as hs
-    m, u, d, v = gen_svd_input(N, M, seed=N + 2 * M + P)
-    g = gamma_for(N + M)
-    a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
-    ctxs, counts = [], None
-    for rank in range(world):
-        ctx = gpu_ctx_factory(P)
-        ctx.set_option("gemm_split", split)
-        if world > 1:
-            ctx.set_shard(rank, world)
-        counts = hs.svd_witness(ctx, *_on_device(m, u, v, d), g)
-        ctxs.append(ctx)
-    ctxs[0].set_option("gemm_split", 1)                # (process-wide: restore the default)
-    if world == 1:
-        _assert_streams(ctxs[0], a0, l0, a1)
-        return
-    got = _reassemble(ctxs, counts)
-    for key, want in (((0, 0), a0), ((1, 0), a1), ((0, 1), l0)):
-        bad = np.nonzero(np.any(got[key] != want, axis=1))[0]
-        assert bad.size == 0, f"{key}: {bad.size} cells differ, first at {bad[:8]}"
-
-
 @pytest.mark.parametrize("N,M,P,occ,pipe", [(256, 192, 63, 1, 1), (192, 256, 32, 2, 1), (300, 300, 42, 1, 0),
                                           (1, 1, 32, 1, 0), (7, 130, 63, 1, 1)])
 def test_front_streamer_parity(gpu_ctx_factory, N, M, P, occ, pipe):
