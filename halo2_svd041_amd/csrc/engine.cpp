@@ -4536,7 +4536,8 @@ static bool is_retired_option(const std::string& n) {
     static const char* const kRetired[] = {"bits_fold",    "bounds_after", "colsum",         "d_checks_aside",
                                            "dep_values",   "fused_quantize", "gemm_batch",    "gemm_priority",
                                            "gemm_rt",      "prelaunch_at", "prod_blocks",     "prod_first",
-                                           "res_first",    "stage_align",  "stage_priority",  "stage_probe"};
+                                           "res_first",    "stage_align",  "stage_nt",        "stage_priority",
+                                           "stage_probe"};
     for (const char* r : kRetired)
         if (n == r) return true;
     return false;
@@ -4569,8 +4570,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "stage_occ") {               // persistent front streamer (0: off)
             REQUIRE(value >= 0 && value <= 2, "stage_occ: 0, 1 or 2 blocks per CU");
             c->stage_occ = (uint32_t)value;
-        } else if (n == "stage_nt") {                // non-temporal stage cell stores
-            c->stage_flags = value ? (c->stage_flags | STAGE_NT) : (c->stage_flags & ~STAGE_NT);
         } else if (n == "stage_diag") {              // timing diagnostic, process-wide (wrong cells)
             set_front_diag((uint32_t)value);
         } else if (n == "stage_front_all") {         // test hook: the front streamer for every batch

@@ -365,7 +365,7 @@ __device__ __forceinline__ uint32_t fastdiv(uint32_t x, uint32_t d, uint32_t mag
 // tracked incrementally (the cell index advances by blockDim / 2 per step).
 // ALIGN: the block's iterations cover whole (blockDim * 16 B)-aligned address
 // windows (the first one partially), so every wave store is one aligned 1 KiB.
-template <bool ALIGN, bool NT = false>
+template <bool ALIGN>
 __device__ __forceinline__ void stream_cells_desc(uint4* __restrict__ out, uint32_t total,
                                                   const uint32_t* __restrict__ sHD,
                                                   const uint4* __restrict__ sHM, uint32_t C,
@@ -385,20 +385,15 @@ __device__ __forceinline__ void stream_cells_desc(uint4* __restrict__ out, uint3
         const uint32_t k = 2 * slot + h;
         const uint32_t d = sHD[k];
         const uint4 m = sHM[k];
-        const uint32_t* x = smem + ((d & kHalfElem) ? vbase : 0u) + (d & 0xffffu);
+        const uint32_t wo = ((d & kHalfElem) ? vbase : 0u) + (d & 0xffffu);
         const uint32_t r = (d >> 16) & 31u;
+        const uint32_t* x = smem + wo;
         const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4];
         const uint4 v = make_uint4(__builtin_amdgcn_alignbit(x1, x0, r) & m.x,
                                    __builtin_amdgcn_alignbit(x2, x1, r) & m.y,
                                    __builtin_amdgcn_alignbit(x3, x2, r) & m.z,
                                    __builtin_amdgcn_alignbit(x4, x3, r) & m.w);
-        if (NT) {
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 nv4 = {v.x, v.y, v.z, v.w};
-            __builtin_nontemporal_store(nv4, reinterpret_cast<u32x4*>(out + hc));
-        } else {
-            out[hc] = v;
-        }
+        out[hc] = v;
         slot += dr;
         vbase += dq * ev;
         if (slot >= C) {
@@ -693,13 +688,6 @@ __device__ __forceinline__ void stage_chunk(const StageArgs& a, const StageLds& 
     uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
     uint4* outL = a.L ? reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L) : nullptr;
     const uint32_t vb0 = (uint32_t)(L.sV - smem);
-    if (a.flags & STAGE_NT) {                      // (A/B: non-temporal cell stores)
-        stream_cells_desc<true, true>(outA, 2 * ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv);
-        if (a.L)
-            stream_cells_desc<true, true>(outL, 2 * ne * a.L, L.sHD + 2 * a.C, L.sHM + 2 * a.C, a.L, a.ldiv_magic,
-                                          smem, vb0, nv);
-        return;
-    }
     stream_cells_desc<true>(outA, 2 * ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv);
     if (a.L)
         stream_cells_desc<true>(outL, 2 * ne * a.L, L.sHD + 2 * a.C, L.sHM + 2 * a.C, a.L, a.ldiv_magic, smem,

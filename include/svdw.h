@@ -263,7 +263,7 @@ int svdw_verify_mul_witness_on(svdw_ctx* ctx, void* stream, const double* a, con
 #define SVDW_GEMM_MFMA 0
 #define SVDW_GEMM_VALU 1
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
-/* Options (svdw_set_option; 15 of them). Tuning knobs, bit-identical results
+/* Options (svdw_set_option; 19 names). Tuning knobs, bit-identical results
  * for every value, defaults first:
  *   "gemm_impl" 0 | 1; "gemm_crt" 1 | 0 (CRT or digit-plane matrix-core GEMM);
  *   "overlap" 1 | 0 (the three check_svd_phase0 products run ahead on a second
@@ -309,7 +309,14 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   of the key replay it with one hipGraphLaunch; k_gamma_prep (gamma's tables,
  *   and the one / gamma-power cells) is queued on the context stream ahead of
  *   the graph, so gamma is never part of it. Off while profiling or hold_us is
- *   set.
+ *   set; "vm_linear" 1 | 0 (the captured sequence is queued on the context
+ *   stream alone, a linear graph, instead of forking to the second stream);
+ *   "stage_occ" 0 | 1 | 2 (stage launches of >= 64 MiB of cells use the
+ *   persistent front streamer at 1 or 2 blocks per CU, a compact store front of
+ *   4 KiB windows; 0: one block per 256 elements, the measured default);
+ *   test hooks: "stage_front_all" 0 | 1 (the front streamer for every stage
+ *   launch when stage_occ > 0), "stage_diag" 0 | 1 (process-wide timing
+ *   diagnostic of the front streamer: its cells are WRONG when non-zero).
  * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:
  *   phase 1 starts with the two ctx_gate constant cells [1, 0] that
  *   examples/svd_example.rs:183's rlc.load_rlc_cache(.., 1) appends as recalled
@@ -327,7 +334,8 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   keep running; to be removed with the next ABI version): "bits_fold",
  *   "bounds_after", "colsum", "d_checks_aside", "dep_values", "fused_quantize",
  *   "gemm_batch", "gemm_priority", "gemm_rt", "prelaunch_at", "prod_blocks",
- *   "prod_first", "res_first", "stage_align", "stage_priority", "stage_probe". */
+ *   "prod_first", "res_first", "stage_align", "stage_priority", "stage_probe";
+ *   "stage_nt" (non-temporal stage stores, round 5). */
 int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);
 /* Captures and replays of the verify_mul_witness graph ("graph") so far. */
 int svdw_graph_stats(svdw_ctx* ctx, uint64_t* captures, uint64_t* replays);

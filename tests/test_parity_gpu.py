@@ -201,7 +201,7 @@ def test_crt_gemm_tiles_parity(gpu_ctx_factory, N, M, P, world, device):
                                   {"stage_batch": 0}, {"pipeline": 0}, {"pipeline": 0, "phase1_overlap": 2},
                                   {"gemm_impl": 1}, {"res_f64": 0}, {"f64_views": 0},
                                   {"stage_occ": 0}, {"stage_occ": 1, "stage_front_all": 1},
-                                  {"stage_occ": 2, "stage_front_all": 1}])
+                                  {"stage_occ": 2, "stage_front_all": 1}, {"stage_elems": 64}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
