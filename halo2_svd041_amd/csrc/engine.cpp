@@ -526,6 +526,13 @@ struct svdw_ctx {
                                             // end; -1: auto (tools/shard_sim.py --opt p1_at=):
                                             // 0 on a rank of >= 4, 3 of 2-3, else 1
     std::function<void(const svdw_svd_payload&)> early_p1;   // that enqueue (svd_witness)
+    // pipelined svd_witness: "dchk_at" the d checks on the cell stream behind
+    // the products (0), on st2 with the bounds and u.d (1) or on st3 ahead of
+    // phase 1 (2); "gamma_at" k_gamma_prep at the head of the cell stream (0) or
+    // of st3 (1); -1: st3 on a row-sharded rank, whose cell stream (quantize ->
+    // residues -> GEMM -> combine, then the diff on st2) is the step's chain
+    // (8-way rank 0.331 -> 0.316-0.321 ms; 1024^2 / 512^2 +0.5 %, r5p / r5q)
+    int dchk_at = 0, gamma_at = -1;
     // Host-side replays cached for repeated calls of the same shape: the dry
     // plan of svd_witness's stream sizes (key: N, M, config) and prelaunch's
     // product offsets (key: stream state at entry, operand views, bounds).
@@ -2469,7 +2476,10 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
             }
             ~Swap() { if (other) std::swap(c->st, *other); }
             bool on() const { return other != nullptr; }
-        } sw(c, c->overlap && known_bits && !c->dry && c->bits_pending && !c->in_pipe, false);
+        };
+        // (pipelined: where dchk_at puts them; st3 only when it exists)
+        const int da = !c->in_pipe ? 1 : (c->dchk_at == 2 && !c->st3 ? 1 : c->dchk_at);
+        Swap sw(c, c->overlap && known_bits && !c->dry && c->bits_pending && da != 0, da == 2);
         // d loaded -- unless every load these stages (and the bounds and u.d
         // queued behind them with the products on the cell stream) read comes
         // from the registered f64 inputs (f64_view): then st2 starts at once
@@ -2753,7 +2763,8 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         // gamma^j depends on gamma only: queue it first, on its own stream, so it
         // runs beside quantization instead of on the phase-1 chain (pipelined: on
         // the cell stream, the least loaded one, into this parity's tables)
-        hipStream_t gs = c->in_pipe ? c->st_cell : c->st3;
+        const bool g3 = c->gamma_at == 1 || (c->gamma_at < 0 && sharded(c));
+        hipStream_t gs = c->in_pipe && !(g3 && c->st3) ? c->st_cell : c->st3;
         gamma_prep(c, std::max(N, M), gamma, gs);
         c->gp_ev = stream_dep(c, gs, nullptr);
         c->gp_st = gs;
@@ -3231,11 +3242,11 @@ static void ctx_init_device(svdw_ctx* c) {
 // bumps the lane's epoch (its captured graph no longer applies).
 static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
     const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->stage_occ, (int64_t)s->stage_front_min, s->gemm_crt, s->res_f64,
-                         s->phase1_overlap, s->prod_cell, s->hold_us, s->rlc_prefix, s->p1_at,
+                         s->phase1_overlap, s->prod_cell, s->hold_us, s->rlc_prefix, s->p1_at, s->dchk_at, s->gamma_at,
                          s->f64_views, s->overlap, s->stage_batch, s->graph_vm, s->vm_linear, s->pipeline,
                          s->shard_rank, s->shard_world, s->prof, s->host_trace};
     const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->stage_occ, (int64_t)d->stage_front_min, d->gemm_crt, d->res_f64,
-                         d->phase1_overlap, d->prod_cell, d->hold_us, d->rlc_prefix, d->p1_at,
+                         d->phase1_overlap, d->prod_cell, d->hold_us, d->rlc_prefix, d->p1_at, d->dchk_at, d->gamma_at,
                          d->f64_views, d->overlap, d->stage_batch, d->graph_vm, d->vm_linear, d->pipeline,
                          d->shard_rank, d->shard_world, d->prof, d->host_trace};
     if (!memcmp(a, b, sizeof a) && d->prof_filter == s->prof_filter) return;
@@ -3245,6 +3256,7 @@ static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
     d->gemm_crt = s->gemm_crt; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
     d->prod_cell = s->prod_cell; d->hold_us = s->hold_us; d->rlc_prefix = s->rlc_prefix;
     d->p1_at = s->p1_at; d->f64_views = s->f64_views; d->overlap = s->overlap;
+    d->dchk_at = s->dchk_at; d->gamma_at = s->gamma_at;
     d->stage_batch = s->stage_batch; d->graph_vm = s->graph_vm; d->pipeline = s->pipeline;
     d->vm_linear = s->vm_linear;
     d->shard_rank = s->shard_rank; d->shard_world = s->shard_world; d->prof = s->prof;
@@ -4601,6 +4613,12 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "p1_at") {
             REQUIRE(value >= -1 && value <= 3, "p1_at: -1 (auto), 0, 1, 2 or 3");
             c->p1_at = (int)value;
+        } else if (n == "dchk_at") {                 // pipelined: the d checks' stream
+            REQUIRE(value >= 0 && value <= 2, "dchk_at: 0 (cell stream), 1 (st2) or 2 (st3)");
+            c->dchk_at = (int)value;
+        } else if (n == "gamma_at") {                // pipelined: k_gamma_prep's stream
+            REQUIRE(value >= -1 && value <= 1, "gamma_at: -1 (auto), 0 (cell stream) or 1 (st3)");
+            c->gamma_at = (int)value;
         } else if (n == "overlap") {
             c->overlap = value != 0;
         } else if (is_retired_option(n)) {

@@ -263,7 +263,7 @@ int svdw_verify_mul_witness_on(svdw_ctx* ctx, void* stream, const double* a, con
 #define SVDW_GEMM_MFMA 0
 #define SVDW_GEMM_VALU 1
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
-/* Options (svdw_set_option; 19 names). Tuning knobs, bit-identical results
+/* Options (svdw_set_option; 21 names). Tuning knobs, bit-identical results
  * for every value, defaults first:
  *   "gemm_impl" 0 | 1; "gemm_crt" 1 | 0 (CRT or digit-plane matrix-core GEMM);
  *   "overlap" 1 | 0 (the three check_svd_phase0 products run ahead on a second
@@ -309,7 +309,11 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   of the key replay it with one hipGraphLaunch; k_gamma_prep (gamma's tables,
  *   and the one / gamma-power cells) is queued on the context stream ahead of
  *   the graph, so gamma is never part of it. Off while profiling or hold_us is
- *   set; "vm_linear" 1 | 0 (the captured sequence is queued on the context
+ *   set; "gamma_at" -1 | 0 | 1 and "dchk_at" 0 | 1 | 2 (pipelined svd_witness:
+ *   k_gamma_prep at the head of the cell stream (0) or of the third stream (1;
+ *   -1: the third on a row-sharded rank, else the cell stream); the d checks
+ *   on the cell stream behind the products (0), on the second stream with the
+ *   bounds and u.d (1) or on the third ahead of phase 1 (2)); "vm_linear" 1 | 0 (the captured sequence is queued on the context
  *   stream alone, a linear graph, instead of forking to the second stream);
  *   "stage_occ" 0 | 1 | 2 (stage launches of >= 64 MiB of cells use the
  *   persistent front streamer at 1 or 2 blocks per CU, a compact store front of

@@ -466,9 +466,11 @@ def test_products_on_cell_stream_parity(gpu_ctx_factory, world, opts):
         assert bad.size == 0, f"{key}: {bad.size} cells differ, first at {bad[:8]}"
 
 
-@pytest.mark.parametrize("N,M,P,world,hold", [(70, 53, 63, 1, 0), (53, 70, 32, 1, 200), (130, 97, 63, 4, 0),
-                                             (40, 33, 63, 1, 0)])
-def test_pipelined_witnesses_parity(gpu_ctx_factory, N, M, P, world, hold):
+@pytest.mark.parametrize("N,M,P,world,hold,opts", [
+    (70, 53, 63, 1, 0, {}), (53, 70, 32, 1, 200, {}), (130, 97, 63, 4, 0, {}), (40, 33, 63, 1, 0, {}),
+    (70, 53, 63, 1, 200, {"dchk_at": 1}), (53, 70, 32, 1, 200, {"dchk_at": 2, "gamma_at": 1}),
+    (130, 97, 63, 4, 200, {"dchk_at": 2, "gamma_at": 1}), (97, 130, 63, 4, 0, {"dchk_at": 1, "gamma_at": 1})])
+def test_pipelined_witnesses_parity(gpu_ctx_factory, N, M, P, world, hold, opts):
     """pipeline: consecutive svd_witness calls on one context overlap (a call
     returns with its stages and row scans still running; the next call's
     quantization and products start beside them, into the other cell set).
@@ -477,9 +479,12 @@ def test_pipelined_witnesses_parity(gpu_ctx_factory, N, M, P, world, hold):
     witness vs the oracle, then a non-pipelined call (check_svd_phase0 through
     the modular API would append cells: a verify_mul_witness) and a further
     pipelined witness, each vs the oracle. hold: every call's streams wait
-    behind a spinning kernel, so a missing cross-call dependency shows."""
+    behind a spinning kernel, so a missing cross-call dependency shows. opts:
+    the pipelined schedule's stream placements (dchk_at, gamma_at)."""
     import halo2_svd041_amd as hs
     ctx = gpu_ctx_factory(P)
+    for k, val in opts.items():
+        ctx.set_option(k, val)
     if world > 1:
         ctx.set_shard(world - 1, world)
     if hold:
@@ -654,7 +659,8 @@ def test_device_input_lifetime(gpu_ctx_factory):
 
 
 @pytest.mark.parametrize("rank,opts", [(0, {}), (3, {}), (7, {}),
-                                       (3, {"overlap": 0, "phase1_overlap": 0})])
+                                       (3, {"overlap": 0, "phase1_overlap": 0}),
+                                       (5, {"dchk_at": 2, "gamma_at": 1}), (6, {"dchk_at": 1})])
 def test_full_size_shard_rank_parity(gpu_ctx_factory, rank, opts):
     """BASELINE config 4 (1024^2, P=63, row blocks over 8 GPUs), rank by rank at
     full size, cell for cell: the rank's witness on the GPU (svdw_set_shard, the
