@@ -17,6 +17,10 @@
 //          groups (lane t: words t, t + 256, ...), with the whole pattern
 //          shifted by `off` words (a stage whose first cell is not 128-byte
 //          aligned: then every group boundary splits a line between blocks).
+//   xcd:   chunks as k_stage, block b writing chunk (b mod 8) G/8 + b / 8, so
+//          the blocks of one XCD (dispatched round-robin over the 8 XCDs)
+//          write adjacent chunks; wpw: each wave streams its own windows
+//          (window 4 i + wave) instead of the block sharing one.
 // spin: a per-block delay (s_sleep loop of `spin` iterations) before the
 // stores, standing in for phase A.
 // Usage: storepat9 [GiB]
@@ -67,6 +71,25 @@ __global__ __launch_bounds__(256) void groups(uint4* __restrict__ p, uint32_t gb
     if (r >= gb) { r -= gb; ++q; }
   }
 }
+template <bool XCD, bool WPW>
+__global__ __launch_bounds__(256) void chunks2(uint4* __restrict__ p, uint32_t cw, size_t n) {
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t c = XCD ? (b % 8) * (G / 8) + b / 8 : b;
+  const size_t c0 = (size_t)c * cw;
+  const uint32_t nwin = cw / 256, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (WPW) {
+    for (uint32_t i = 0; i < nwin; i += 4)
+      for (uint32_t q = 0; q < 4; ++q) {
+        const size_t k = c0 + (size_t)(i + wave) * 256 + q * 64 + lane;
+        if (i + wave < nwin && k < n) p[k] = make_uint4((uint32_t)k, 2, 3, 4);
+      }
+  } else {
+    for (uint32_t i = 0; i < nwin; ++i) {
+      const size_t k = c0 + (size_t)i * 256 + threadIdx.x;
+      if (k < n) p[k] = make_uint4((uint32_t)k, 2, 3, 4);
+    }
+  }
+}
 template <class F> double gbs(F f, size_t bytes) {
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   f(); CK(hipDeviceSynchronize());
@@ -81,15 +104,18 @@ int main(int argc, char** argv) {
   uint4* a;
   CK(hipMalloc(&a, bytes)); CK(hipMemset(a, 0, bytes));
   printf("memset: %.0f GB/s\n", gbs([&] { CK(hipMemsetAsync(a, 3, bytes)); }, bytes));
-  for (uint32_t gb : {128u, 256u, 512u, 1024u, 2048u})
-    for (uint32_t Q : {8u, 16u, 32u})
-      for (uint32_t sb : {1u, 8u, 32u, 128u, 256u, 512u}) {
-        if ((size_t)gb * Q > 65536) continue;
-        const uint32_t G = (uint32_t)((n - 8) / ((size_t)gb * Q));
+  for (int rep = 0; rep < 2; ++rep)
+    for (uint32_t kib : {32u, 136u, 480u})
+      for (int mode = 0; mode < 4; ++mode) {
+        const uint32_t cw = kib * 1024 / 16;
+        const uint32_t G = (uint32_t)(n / cw) / 8 * 8;
         const double r = gbs([&] {
-          hipLaunchKernelGGL(groups, dim3(G), dim3(256), 0, 0, a, gb, Q, sb, 0u, n);
-        }, (size_t)G * gb * Q * 16);
-        printf("groups gb %4u (%5u B) Q %2u off 0 SB %3u: %.0f GB/s\n", gb, gb * 16, Q, sb, r);
+          if (mode == 0) hipLaunchKernelGGL((chunks2<false, false>), dim3(G), dim3(256), 0, 0, a, cw, n);
+          if (mode == 1) hipLaunchKernelGGL((chunks2<true, false>), dim3(G), dim3(256), 0, 0, a, cw, n);
+          if (mode == 2) hipLaunchKernelGGL((chunks2<false, true>), dim3(G), dim3(256), 0, 0, a, cw, n);
+          if (mode == 3) hipLaunchKernelGGL((chunks2<true, true>), dim3(G), dim3(256), 0, 0, a, cw, n);
+        }, (size_t)G * cw * 16);
+        printf("chunk %3u KiB xcd %d wpw %d: %.0f GB/s\n", kib, mode & 1, mode >> 1, r);
       }
   printf("memset: %.0f GB/s\n", gbs([&] { CK(hipMemsetAsync(a, 3, bytes)); }, bytes));
   return 0;
