@@ -57,6 +57,6 @@ for a in "--n 512 --p 32" "--n 2048 --m 1024 --p 32" "--workload verify_mul --st
   timeout -k 10 600 python bench.py $a >> $O/configs.jsonl 2>> $O/configs.err || exit 16
 done
 echo configs ok
-timeout -k 10 600 python tools/shard_sim.py --worlds 1,2,4,8 --steps 10 > $O/shard_sim.json 2> $O/shard_sim.err || exit 17
+timeout -k 10 600 python tools/shard_sim.py --worlds 1,2,4,8 --steps 40 > $O/shard_sim.json 2> $O/shard_sim.err || exit 17
 timeout -k 10 300 python tools/ingest_time.py > $O/ingest.jsonl 2> $O/ingest.err || exit 18
 echo part b done
