@@ -809,8 +809,12 @@ struct ProfScope {
         return e;
     }
     hipStream_t s = nullptr;
+    bool ext = false;                       // stage launches: events recorded by their dispatch
+    // stage: the scope holds stage launches only (launch_stage*), which record
+    // the events themselves (set_launch_events): no event records between the
+    // launches, which cost a few us of stream time each
     ProfScope(svdw_ctx* cc, hipStream_t ss, const std::string& name, double bytes, double ops,
-              bool batch = false)
+              bool batch = false, bool stage = false)
         : c(cc), s(ss) {
         if (!batch) flush_batch(c, s);      // earlier batched stages go first
         if (!c->prof || c->dry) return;
@@ -821,12 +825,19 @@ struct ProfScope {
         const char* tag = s == c->stream_id[0] ? "@cell" : s == c->stream_id[1] ? "@s2"
                           : s == c->stream_id[2] ? "@s3" : "";
         svdw_ctx::Rec r{name + tag, bytes, ops, ev(c), ev(c)};
-        hipck(hipEventRecord(r.e0, s), "hipEventRecord");
+        ext = stage;
+        if (ext)
+            set_launch_events(r.e0, r.e1);
+        else
+            hipck(hipEventRecord(r.e0, s), "hipEventRecord");
         c->recs.push_back(r);
         idx = (long)c->recs.size() - 1;
     }
     ~ProfScope() {
-        if (idx >= 0) (void)hipEventRecord(c->recs[idx].e1, s);
+        if (idx < 0) return;
+        if (ext && launch_events_used()) return;
+        if (ext) (void)hipEventRecord(c->recs[idx].e0, s);       // nothing launched: an empty interval
+        (void)hipEventRecord(c->recs[idx].e1, s);
     }
 };
 
@@ -1086,7 +1097,7 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
         return;
     }
     {
-        ProfScope ps(c, c->st, std::string("k_stage:") + tag, bytes, 0);
+        ProfScope ps(c, c->st, std::string("k_stage:") + tag, bytes, 0, false, true);
         const StageArgs* one = &a;
         hipck(launch_stage_pers(&one, 1, c->st, stage_ctr_for(c, c->st), c->stage_occ, c->stage_front_min), "k_stage");
     }
@@ -1122,7 +1133,7 @@ static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter, hipEvent
                 for (const auto& q : grp) fprintf(stderr, " %s", q.name.c_str());
                 fprintf(stderr, "\n");
             }
-            ProfScope pr(c, s, name, bytes, 0, true);
+            ProfScope pr(c, s, name, bytes, 0, true, true);
             hipck(launch_stage_pers(ps.data(), (int)ps.size(), s, stage_ctr_for(c, s), c->stage_occ, c->stage_front_min),
                   "k_stage_multi");
         }

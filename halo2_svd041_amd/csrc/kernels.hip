@@ -11,6 +11,7 @@
 //  k_matvec_scan   field_mat_vec_mul rows (src/matrix/mod.rs:574-599): every
 //                  prefix sum of the row inner product is a cell -> block Fr scan
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <type_traits>
 #include <string.h>
 
@@ -748,6 +749,33 @@ __global__ __launch_bounds__(256) void k_stage_multi(const StageMulti m) {
     const Rec q = multi_rec(m, p);
     stage_block(*q.a, q.mo, q.adv, q.lk, q.K, blockIdx.x - m.blk0[p]);
 }
+// Profiled stage launches (set_launch_events): the kernel's own dispatch
+// records the profiler's events (hipExtLaunchKernelGGL: start on the first
+// launch of the scope, stop re-recorded by every launch, so the last one's end
+// counts) instead of event records between the launches, which cost a few us
+// of stream time each.
+static thread_local hipEvent_t tl_ev0 = nullptr, tl_ev1 = nullptr;
+static thread_local bool tl_used = false;
+void set_launch_events(hipEvent_t e0, hipEvent_t e1) {
+    tl_ev0 = e0;
+    tl_ev1 = e1;
+    tl_used = false;
+}
+bool launch_events_used() {
+    const bool u = tl_used;
+    tl_ev0 = tl_ev1 = nullptr;
+    tl_used = false;
+    return u;
+}
+template <class K, class... Args>
+static void launch_ev(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t st, Args... args) {
+    if (!tl_ev1) {
+        hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+        return;
+    }
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, st, tl_used ? nullptr : tl_ev0, tl_ev1, 0, args...);
+    tl_used = true;
+}
 hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     if (a.e_end <= a.e_begin) return hipSuccess;
     const uint32_t n = a.e_end - a.e_begin;
@@ -755,7 +783,7 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     if (E > kStageElems) return hipErrorInvalidValue;
     const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1, E, a.C + a.L);
     const uint32_t grid = (n + E - 1) / E;
-    hipLaunchKernelGGL(k_stage, dim3(grid), dim3(256), lds, st, a);
+    launch_ev(k_stage, dim3(grid), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 bool stage_multi_fits(const StageArgs& a) {
@@ -773,7 +801,7 @@ hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t 
             e = launch_stage(*single, st);
         } else if (m.nprog > 1) {
             m.blk0[m.nprog] = blocks;
-            hipLaunchKernelGGL(k_stage_multi, dim3(blocks), dim3(256), lds, st, m);
+            launch_ev(k_stage_multi, dim3(blocks), dim3(256), lds, st, m);
             e = hipGetLastError();
         }
         m.nprog = 0;
@@ -1215,9 +1243,9 @@ hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t s
             const uint32_t lds = front_lds_bytes(cl, ev);
             if (lds > 160u * 1024u - 2048u) return hipErrorInvalidValue;
             if (m.nprog == 1)
-                hipLaunchKernelGGL(k_stage_front, dim3(grid), dim3(64 * kFrontWaves), lds, st, *single, fc);
+                launch_ev(k_stage_front, dim3(grid), dim3(64 * kFrontWaves), lds, st, *single, fc);
             else
-                hipLaunchKernelGGL(k_stage_front_multi, dim3(grid), dim3(64 * kFrontWaves), lds, st, m, fc);
+                launch_ev(k_stage_front_multi, dim3(grid), dim3(64 * kFrontWaves), lds, st, m, fc);
             e = hipGetLastError();
         }
         m.nprog = 0;

@@ -248,6 +248,11 @@ hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t 
 // per element: launch_stage_multi.
 hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t st, uint32_t* ctr, uint32_t occ,
                              double min_bytes);
+// The next stage launches of this thread (launch_stage*, until
+// launch_events_used) record e0 at the first one's start and e1 at each one's
+// end through their dispatch; launch_events_used says whether any launched.
+void set_launch_events(hipEvent_t e0, hipEvent_t e1);
+bool launch_events_used();
 // timing diagnostic of the front streamer (cells WRONG): 1 = no producer view loads
 void set_front_diag(uint32_t d);
 // does the record of `a` fit one k_stage_multi launch?
