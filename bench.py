@@ -454,13 +454,12 @@ def main():
     # events around the dominant kernel's launches only: at config 2's size,
     # events around all ten launches of a step doubled the step time
     prefix = args.profile_prefix if args.profile_prefix is not None else ("k_stage" if svd else "k_matvec_scan")
-    # verify_mul: the timed steps replay the captured launch graph (option
-    # "graph"), which the event profiler would switch off, so the dominant
-    # kernel's launches are timed in a second pass of the same steps (eager
-    # launches of the same kernels with the same inputs), right after
+    # The timed steps run without the event profiler (its start markers cost
+    # 0.5-3.5 % of a step); the dominant kernel's launches
+    # are timed in a second, untimed pass of the same steps right after (for
+    # verify_mul also because the timed steps replay the captured launch
+    # graph, which the profiler would switch off).
     graph_vm = not svd and "graph=0" not in args.opt
-    if profile and not graph_vm:
-        ctx.profile(True, prefix)
     if dist is not None:
         dist.barrier()
     sync()
@@ -473,13 +472,16 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     host_ms = (t_issued - t0) / args.steps * 1e3
-    graph_stats = None
-    if profile and graph_vm:
-        graph_stats = ctx.graph_stats()
+    graph_stats = ctx.graph_stats() if profile and graph_vm else None
+    prof_elapsed = None
+    if profile:
         ctx.profile(True, prefix)
+        sync()
+        tp = time.perf_counter()
         for g in gammas:
             wl.step(g)
         sync()
+        prof_elapsed = time.perf_counter() - tp
     stats = ctx.profile_collect() if profile else []
     cells_step = cnt["advice0"] + cnt["advice1"]
 
@@ -676,7 +678,9 @@ def main():
             roof["sources_sha16"] = sources_sha16()
             sst = stage_stream_rate(stats, args.steps)
             if sst is not None and roof["kernel"] == "k_stage":
-                sst["busy_frac_of_step"] = round(sst["busy_ms_per_step"] / (elapsed / args.steps * 1e3), 4)
+                # against the step time of the profiled pass it was measured in
+                sst["busy_frac_of_step"] = round(sst["busy_ms_per_step"] / (prof_elapsed / args.steps * 1e3), 4)
+                sst["profiled_pass_ms_per_step"] = round(prof_elapsed / args.steps * 1e3, 4)
                 roof["stage_stream"] = sst
             if solo is not None and solo["kernel"] == roof["kernel"]:
                 roof["standalone"] = {k: solo[k] for k in ("achieved", "frac", "avg_launch_ms")}
@@ -704,10 +708,13 @@ def main():
                                         "per-kernel HBM fraction above is the dominant kernel's"}
                                if ch else {"note": "no committed GPU-only chain of these kernel sources "
                                                    "(profiles/*_chain_*.json)"})
-        if graph_stats is not None:
-            roof["timing_note"] = ("timed steps replay the captured launch graph (captures, replays "
-                                   "= %d, %d); the kernel's launches timed in a second, eager pass of "
-                                   "the same steps" % graph_stats)
+        if stats:
+            roof["timing_note"] = ("ms_per_step from the timed steps, profiler off; the kernel's "
+                                   "launches timed by HIP events in a second, untimed pass of the same "
+                                   "steps (%.4f ms per step with the events)" % (prof_elapsed / args.steps * 1e3))
+            if graph_stats is not None:
+                roof["timing_note"] += ("; the timed steps replay the captured launch graph (captures, "
+                                        "replays = %d, %d), the profiled pass runs eagerly" % graph_stats)
         out["roofline"] = roof
         if gemm is not None:
             out["field_gemm"] = gemm

@@ -122,6 +122,7 @@ SIGNATURES = {
     "svdw_stream_signal": (_i32, [_P, _P]),
     "svdw_debug_trace": (_i32, [_P]),
     "svdw_last_error": (ct.c_char_p, []),
+    "svdw_abi_version": (_i32, []),
     "svdw_advice_len": (_u64, [_P, _u32]),
     "svdw_lookup_len": (_u64, [_P, _u32]),
     "svdw_advice_device_ptr": (_P, [_P, _u32]),

@@ -485,14 +485,6 @@ struct svdw_ctx {
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
     uint32_t stage_flags = STAGE_ALIGN;     // STAGE_* (4 KiB-aligned block store windows)
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
-    // "stage_occ": blocks per CU of the persistent front streamer (k_stage_front)
-    // for stage batches of >= 64 MB; 0: the one-block-per-chunk kernels
-    // (k_stage / k_stage_multi). Its ticket counters: one 256-byte slot per
-    // stream (cell stream, st2, st3), zero between launches (each launch's last
-    // block resets its slot).
-    uint32_t stage_occ = 0;
-    double stage_front_min = 64.0 * (1 << 20);   // "stage_front_all" 1: 0 (tests: every batch)
-    DBuf stage_ctr;
     hipStream_t stream_id[3] = {};          // st, st2, st3 as created (st / st2 / st3 are swapped at times)
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
     bool gemm_batched = false;              // this witness's products went out as one batch
@@ -1001,13 +993,6 @@ static void check_mat(const svdw_ctx* c, const svdw_mat& m) {
 static void check_vec(const svdw_ctx* c, const svdw_vec& v) { check_mat(c, mat_of_vec(v)); }
 
 // ------------------------------------------------------- stage launches
-// The persistent stage kernel's tile counters for a launch on stream s (null:
-// not one of the context's streams -> the one-block-per-chunk kernels).
-static uint32_t* stage_ctr_for(svdw_ctx* c, hipStream_t s) {
-    if (!c->stage_occ || !c->stage_ctr.p) return nullptr;
-    const int k = s == c->stream_id[0] ? 0 : s == c->stream_id[1] ? 1 : s == c->stream_id[2] ? 2 : -1;
-    return k < 0 ? nullptr : reinterpret_cast<uint32_t*>(static_cast<char*>(c->stage_ctr.p) + 256 * k);
-}
 // Appends the stage's cells for `nelem` elements; returns the advice offset.
 // Launch a stage whose cells were appended at (off, loff) earlier.
 static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, uint32_t cols,
@@ -1099,7 +1084,7 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
     {
         ProfScope ps(c, c->st, std::string("k_stage:") + tag, bytes, 0, false, true);
         const StageArgs* one = &a;
-        hipck(launch_stage_pers(&one, 1, c->st, stage_ctr_for(c, c->st), c->stage_occ, c->stage_front_min), "k_stage");
+        hipck(launch_stage_multi(&one, 1, c->st), "k_stage");
     }
 }
 // Issue a stream's pending batched stages (k_stage_multi; one program: k_stage).
@@ -1134,8 +1119,7 @@ static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter, hipEvent
                 fprintf(stderr, "\n");
             }
             ProfScope pr(c, s, name, bytes, 0, true, true);
-            hipck(launch_stage_pers(ps.data(), (int)ps.size(), s, stage_ctr_for(c, s), c->stage_occ, c->stage_front_min),
-                  "k_stage_multi");
+            hipck(launch_stage_multi(ps.data(), (int)ps.size(), s), "k_stage_multi");
         }
     }
     if (waiter) stream_dep(c, s, waiter);
@@ -3170,7 +3154,7 @@ static std::vector<DBuf*> dbufs(svdw_ctx* c) {
                             &c->gtab_alt, &c->crtR, &c->gbits, &c->colpart, &c->qfold, &c->ing_x, &c->ing_e,
                             &c->ing_c, &c->ing_p10, &c->ing_val, &c->ing_npos, &c->ing_nd, &c->ing_rpos,
                             &c->ing_kpos, &c->ing_err, &c->ing_q, &c->eq_cp, &c->eq_ks, &c->eq_reg, &c->eq_w,
-                            &c->eq_k, &c->eq_err, &c->eq_st, &c->stage_ctr};
+                            &c->eq_k, &c->eq_err, &c->eq_st};
     for (int i = 0; i < kMaxScanJobs; ++i) {
         v.push_back(&c->wbc[i]);
         v.push_back(&c->wbt[i]);
@@ -3240,11 +3224,6 @@ static void ctx_init_device(svdw_ctx* c) {
     c->stream_id[0] = c->st;
     c->stream_id[1] = c->st2;
     c->stream_id[2] = c->st3;
-    if (e == hipSuccess) e = hipMalloc(&c->stage_ctr.p, 3 * 256);
-    if (e == hipSuccess) {
-        c->stage_ctr.cap = 3 * 256;
-        e = hipMemset(c->stage_ctr.p, 0, 3 * 256);     // (synchronous: before any launch)
-    }
     size_t mfree = 0;
     if (e == hipSuccess) e = hipMemGetInfo(&mfree, &c->mem_total);
     if (e != hipSuccess) fail(SVDW_EDEVICE, std::string("HIP device init failed: ") + hipGetErrorString(e));
@@ -3252,18 +3231,16 @@ static void ctx_init_device(svdw_ctx* c) {
 // The settings (options, shard, profiler) of `s` onto the lane `d`; a change
 // bumps the lane's epoch (its captured graph no longer applies).
 static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
-    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->stage_occ, (int64_t)s->stage_front_min, s->gemm_crt, s->res_f64,
+    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->gemm_crt, s->res_f64,
                          s->phase1_overlap, s->prod_cell, s->hold_us, s->rlc_prefix, s->p1_at, s->dchk_at, s->gamma_at,
                          s->f64_views, s->overlap, s->stage_batch, s->graph_vm, s->vm_linear, s->pipeline,
                          s->shard_rank, s->shard_world, s->prof, s->host_trace};
-    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->stage_occ, (int64_t)d->stage_front_min, d->gemm_crt, d->res_f64,
+    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->gemm_crt, d->res_f64,
                          d->phase1_overlap, d->prod_cell, d->hold_us, d->rlc_prefix, d->p1_at, d->dchk_at, d->gamma_at,
                          d->f64_views, d->overlap, d->stage_batch, d->graph_vm, d->vm_linear, d->pipeline,
                          d->shard_rank, d->shard_world, d->prof, d->host_trace};
     if (!memcmp(a, b, sizeof a) && d->prof_filter == s->prof_filter) return;
     d->gemm_impl = s->gemm_impl; d->stage_flags = s->stage_flags; d->stage_elems = s->stage_elems;
-    d->stage_occ = s->stage_occ;
-    d->stage_front_min = s->stage_front_min;
     d->gemm_crt = s->gemm_crt; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
     d->prod_cell = s->prod_cell; d->hold_us = s->hold_us; d->rlc_prefix = s->rlc_prefix;
     d->p1_at = s->p1_at; d->f64_views = s->f64_views; d->overlap = s->overlap;
@@ -4553,18 +4530,7 @@ int svdw_shard_segments(const svdw_ctx* c, svdw_segment* out, uint64_t cap, uint
                                   c->owned[i].n};
     });
 }
-// Options removed in round 4 once their A/B had settled (fixed at the measured
-// best or dropped with their code): still accepted, as no-ops.
-static bool is_retired_option(const std::string& n) {
-    static const char* const kRetired[] = {"bits_fold",    "bounds_after", "colsum",         "d_checks_aside",
-                                           "dep_values",   "fused_quantize", "gemm_batch",    "gemm_priority",
-                                           "gemm_rt",      "prelaunch_at", "prod_blocks",     "prod_first",
-                                           "res_first",    "stage_align",  "stage_nt",        "stage_priority",
-                                           "stage_probe"};
-    for (const char* r : kRetired)
-        if (n == r) return true;
-    return false;
-}
+int svdw_abi_version(void) { return SVDW_ABI_VERSION; }
 int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
     return guarded([&] {
         REQUIRE(c && name, "null argument");
@@ -4590,13 +4556,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "gemm_impl") {
             REQUIRE(value == SVDW_GEMM_MFMA || value == SVDW_GEMM_VALU, "gemm_impl: 0 (mfma) or 1 (valu)");
             c->gemm_impl = (int)value;
-        } else if (n == "stage_occ") {               // persistent front streamer (0: off)
-            REQUIRE(value >= 0 && value <= 2, "stage_occ: 0, 1 or 2 blocks per CU");
-            c->stage_occ = (uint32_t)value;
-        } else if (n == "stage_diag") {              // timing diagnostic, process-wide (wrong cells)
-            set_front_diag((uint32_t)value);
-        } else if (n == "stage_front_all") {         // test hook: the front streamer for every batch
-            c->stage_front_min = value ? 0.0 : 64.0 * (1 << 20);
         } else if (n == "stage_elems") {
             REQUIRE(value >= 16 && value <= 256 && value % 16 == 0,
                     "stage_elems: a multiple of 16 in [16, 256]");
@@ -4632,9 +4591,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             c->gamma_at = (int)value;
         } else if (n == "overlap") {
             c->overlap = value != 0;
-        } else if (is_retired_option(n)) {
-            // settled in round 4 (include/svdw.h, "Retired options"): accepted
-            // and ignored for one more ABI version, so existing callers run
         } else {
             fail(SVDW_EINVAL, "unknown option " + n);
         }

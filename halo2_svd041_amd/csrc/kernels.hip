@@ -840,456 +840,6 @@ hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t 
     return flush();
 }
 
-// ------------------------------------------------ persistent front streamer
-// k_stage_front: the cell programs of k_stage / k_stage_multi on a persistent
-// grid (one block per CU) that writes the cell streams in a compact moving
-// front. Every output region (a program's advice cells, its lookup cells) is
-// cut into 4 KiB windows (256 half-cells, aligned to 4 KiB in memory). A ticket
-// (taken in order from a device counter) is a block slot b of a super-round s:
-// the K windows (s K + j) G + b, j < K, of one region (G = the grid). With all
-// G blocks resident the whole chip writes G adjacent windows (1 MiB) at a time
-// and sweeps the stream, the store pattern that reaches the memset rate
-// (tools/probes/storepat8.hip: 6.4 TB/s against 5.5-5.8 for one long chunk per
-// block). Per block, five waves:
-//   * wave 0, the producer: phase A (the micro-ops) of the NEXT ticket's
-//     elements -- the <= kFrontElems elements its K windows touch, one per lane
-//     per pass -- into the other LDS buffer; its view loads are issued one
-//     ticket ahead and its dequeue two tickets ahead. It issues no stores, so
-//     its waits never wait for stores in flight.
-//   * waves 1-4, the consumers: the CURRENT ticket's windows, one half-cell
-//     (16 B) per lane per window, every wave store one contiguous 1 KiB, with
-//     no barrier between windows.
-// One barrier per ticket. A program's tables (constants, micro-ops, views, the
-// per (slot, half) descriptors and masks of stream_cells_desc) go into one of
-// two table sets, so the producer can start the next program while the
-// consumers still read the current one. The last block out resets the
-// counter for the next launch on its stream.
-static constexpr uint32_t kFrontElems = 128;          // element slots per ticket (two producer passes)
-static constexpr uint32_t kFrontWaves = 5;
-static constexpr int kMaxStreams = 2 * kMaxMulti;
-
-// words of one table set: K | masks (one uint4 per slot half) | micro-ops | views | descriptors
-__host__ __device__ constexpr uint32_t front_set_words(uint32_t cl) {
-    return (kMaxK * VW + 8 * cl + kMaxMicro * 2 + kMaxViews * 10 + 2 * cl + 3) / 4 * 4;
-}
-__host__ __device__ constexpr uint32_t front_lds_bytes(uint32_t cl, uint32_t ev) {
-    return 4 * (2 * front_set_words(cl) + 2 * (kFrontElems * ev + 16));
-}
-// elements a 4 KiB window of a U-cell-per-element region touches, at most
-__host__ __device__ constexpr uint32_t front_epw(uint32_t U) { return 127 / U + 2; }
-struct FSet {
-    uint32_t* K;
-    uint4* M;            // masks: one uint4 per (slot, half)
-    MicroOp* mo;
-    DView* vw;
-    uint32_t* D;         // descriptors: one per (slot, half)
-};
-// (base = smem + a word offset: pointers kept as offsets from the LDS array,
-// never selected from an array of pointers, stay in the LDS address space --
-// a selected pointer becomes a flat pointer, and flat loads count against the
-// store counter: every LDS read would then wait for the stores in flight)
-__device__ __forceinline__ FSet front_set(uint32_t* base, uint32_t cl) {
-    FSet s;
-    s.K = base;
-    s.M = reinterpret_cast<uint4*>(base + kMaxK * VW);
-    s.mo = reinterpret_cast<MicroOp*>(base + kMaxK * VW + 8 * cl);
-    s.vw = reinterpret_cast<DView*>(base + kMaxK * VW + 8 * cl + kMaxMicro * 2);
-    s.D = base + kMaxK * VW + 8 * cl + kMaxMicro * 2 + kMaxViews * 10;
-    return s;
-}
-// One program's tables into set s, by the 64 lanes of one wave.
-__device__ __forceinline__ void front_tables(const Rec& q, const FSet& s, uint32_t lane) {
-    const StageArgs& a = *q.a;
-    for (uint32_t k = lane; k < a.nk; k += 64) lds_put(s.K + k * VW, q.K[k]);
-    for (uint32_t k = lane; k < a.nmo; k += 64) s.mo[k] = q.mo[k];
-    if (lane < kMaxViews) s.vw[lane] = a.view[lane];
-    for (uint32_t k = lane; k < 2 * (a.C + a.L); k += 64) {
-        const uint32_t sl = k >> 1;
-        make_half(sl < a.C ? q.adv[sl] : q.lk[sl - a.C], k & 1, s.D + k, s.M + k);
-    }
-}
-// View loads of element e (this lane) of a program (phase A's prefetch).
-__device__ __forceinline__ Prefetch front_loads(const StageArgs& a, uint32_t e, bool valid) {
-    Prefetch f{fr_zero(), fr_zero(), false, false};
-    if (!valid) return f;
-    const uint32_t pi = e / a.cols, pj = e - pi * a.cols;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const DView& v = a.view[k];
-        Fr x = fr_zero();
-        bool in = false;
-        if (v.ptr && v.mode == VIEW_STRIDED && pi < v.rows && pj < v.cols) {
-            x = ld_fr(v.ptr + (int64_t)pi * v.rs + (int64_t)pj * v.cs);
-            in = true;
-        } else if (v.ptr && v.mode == VIEW_F64 && pi < v.rows && pj < v.cols) {
-            x = quantize_fr(reinterpret_cast<const double*>(v.ptr)[(int64_t)pi * v.rs + (int64_t)pj * v.cs],
-                            f64_scale(v));
-            in = true;
-        }
-        if (k == 0) { f.v0 = x; f.in0 = in; } else { f.v1 = x; f.in1 = in; }
-    }
-    return f;
-}
-// One output region of one program, cut into 4 KiB windows (32-bit geometry:
-// the launcher keeps regions below 2^31 half-cells on this kernel).
-struct FStream {
-    uint32_t H;          // half-cells (2 U n)
-    uint32_t prog, lk;   // program, region (0 advice, 1 lookups)
-    uint32_t U, magic;   // cells per element, ceil(2^32 / U)
-    uint32_t mis;        // half-cells from the 4 KiB boundary below the region start
-    uint32_t epw, K;     // element slots per window, windows per ticket
-    uint32_t nw, t0;     // windows, first ticket
-};
-static constexpr uint32_t kMaxWin = kFrontElems / 2;   // K <= kFrontElems / epw, epw >= 2
-// Window j of a ticket (computed once per ticket by the producer, in LDS):
-// lane 0's half-cell hb (256 W - mis, negative for a region's first window),
-// the cell of its first in-range half-cell c0, that cell's element (first, in
-// the region) and slot (phase).
-struct FWin {
-    int32_t hb;
-    uint32_t c0, first, phase;
-};
-struct SrcMulti {
-    const StageMulti* m;
-    __device__ uint32_t nprog() const { return m->nprog; }
-    __device__ Rec rec(uint32_t p) const { return multi_rec(*m, p); }
-};
-struct SrcSingle {
-    const StageArgs* a;
-    __device__ uint32_t nprog() const { return 1; }
-    __device__ Rec rec(uint32_t) const { return Rec{a, a->mo, a->adv, a->lk, a->K}; }
-};
-struct FrontCtl {
-    uint32_t* ctr;       // [0] ticket head, [1] blocks done (zero between launches)
-    uint32_t cl;         // max C + L over the programs (table set size)
-    uint32_t ev;         // max element words over the programs
-    uint32_t diag;       // timing diagnostic (wrong cells): 1 = the producer skips its view loads
-};
-template <class SRC>
-__device__ __forceinline__ void stage_front(const SRC& S, const FrontCtl& fc) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-    __shared__ FStream sF[kMaxStreams];
-    __shared__ FWin sW[3][kMaxWin];          // ring: current, next, after-next ticket
-    __shared__ uint32_t sNS, sTT;
-    __shared__ uint32_t sTile[2], sSet[2], sNW[2], sProg[2];
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, G = gridDim.x;
-    const uint32_t sw = front_set_words(fc.cl), bw = kFrontElems * fc.ev + 16, ev = fc.ev, cl = fc.cl;
-    auto set_off = [&](uint32_t x) { return x ? sw : 0u; };
-    auto buf_off = [&](uint32_t x) { return 2 * sw + (x ? bw : 0u); };
-    // ---- the regions and their tickets (one thread; <= 32 regions)
-    if (tid == 0) {
-        uint32_t ns = 0, tt = 0;
-        for (uint32_t p = 0; p < S.nprog(); ++p) {
-            const Rec q = S.rec(p);
-            const StageArgs& a = *q.a;
-            const uint32_t n = a.e_end - a.e_begin;
-            for (uint32_t lk = 0; lk < 2; ++lk) {
-                const uint32_t U = lk ? a.L : a.C;
-                if (!U || !n) continue;
-                FStream& F = sF[ns++];
-                const Fr* base = (lk ? a.out_lk + (uint64_t)a.e_begin * U : a.out_adv + (uint64_t)a.e_begin * U);
-                F.H = 2u * U * n;
-                F.prog = p;
-                F.lk = lk;
-                F.U = U;
-                F.magic = U > 1 ? (uint32_t)(((1ull << 32) + U - 1) / U) : 0u;
-                F.mis = (uint32_t)(reinterpret_cast<uintptr_t>(base) >> 4) & 255u;
-                F.epw = front_epw(U);
-                F.K = kFrontElems / F.epw;
-                F.nw = (F.H + F.mis + 255) / 256;
-                F.t0 = tt;
-                tt += (F.nw + F.K * G - 1) / (F.K * G) * G;
-            }
-        }
-        sNS = ns;
-        sTT = tt;
-        sProg[0] = sProg[1] = ~0u;
-    }
-    __syncthreads();
-    const uint32_t NS = sNS, TT = sTT;
-    auto stream_of = [&](uint32_t q) {
-        uint32_t k = 0;
-        for (uint32_t i = 1; i < NS; ++i) k += q >= sF[i].t0;
-        return k;
-    };
-    // producer state: ticket n1 (view loads fa / fb of its two passes in
-    // flight), n2 (known), dequeue n3v in flight
-    static_assert(kFrontElems == 128, "two producer passes");
-    uint32_t n1 = 0, n2 = 0, n3v = 0;
-    Prefetch fa{fr_zero(), fr_zero(), false, false}, fb = fa;
-    // the windows of ticket q into sW[x] (lane j: window j); returns their count
-    auto windows = [&](uint32_t q, const FStream& F, uint32_t x) -> uint32_t {
-        const uint32_t local = q - F.t0, s = local / G, b = local - s * G;
-        const uint32_t w0 = s * F.K * G + b;                        // window of j = 0
-        const uint32_t nwin = w0 >= F.nw ? 0u : min(F.K, (F.nw - w0 + G - 1) / G);
-        if (lane < nwin) {
-            const uint32_t W = w0 + lane * G;
-            FWin w;
-            w.hb = (int32_t)(W * 256u) - (int32_t)F.mis;
-            w.c0 = (uint32_t)(w.hb < 0 ? 0 : w.hb) >> 1;
-            w.first = w.c0 / F.U;
-            w.phase = w.c0 - w.first * F.U;
-            sW[x][lane] = w;
-        }
-        return nwin;
-    };
-    // element slot t of the ticket whose windows are in sW[x]: its element in the region
-    auto slot_elem = [&](const FStream& F, uint32_t x, uint32_t nwin, uint32_t t, uint32_t* e) -> bool {
-        const uint32_t j = t / F.epw, kk = t - j * F.epw;
-        if (j >= nwin) return false;
-        const FWin w = sW[x][j];
-        const int32_t hl = min(w.hb + 255, (int32_t)F.H - 1);
-        const uint32_t last = ((uint32_t)hl >> 1) / F.U;
-        *e = w.first + kk;
-        return *e <= last;
-    };
-    // ticket q's windows into window slot x, and its view loads (fa, fb)
-    auto issue_loads = [&](uint32_t q, uint32_t x) {
-        if (q >= TT) return;
-        const FStream F = sF[stream_of(q)];
-        const uint32_t nwin = windows(q, F, x);
-        if (fc.diag) return;
-        const StageArgs& a = *S.rec(F.prog).a;
-        uint32_t e0 = 0, e1 = 0;
-        const bool v0 = slot_elem(F, x, nwin, lane, &e0), v1 = slot_elem(F, x, nwin, 64 + lane, &e1);
-        fa = front_loads(a, a.e_begin + e0, v0);
-        fb = front_loads(a, a.e_begin + e1, v1);
-    };
-    // phase A of ticket q (windows already in window slot ws) into buffer x;
-    // tables into the set the current ticket does not use, unless it is the
-    // same program
-    auto phase_a = [&](uint32_t q, uint32_t x, uint32_t ws, uint32_t cur_set) {
-        if (q >= TT) {
-            if (lane == 0) sTile[x] = TT;
-            return;
-        }
-        const FStream F = sF[stream_of(q)];
-        const Rec r = S.rec(F.prog);
-        uint32_t st = cur_set;
-        if (sProg[st] != F.prog) {
-            st ^= 1u;
-            if (sProg[st] != F.prog) {
-                front_tables(r, front_set(smem + set_off(st), cl), lane);
-                if (lane == 0) sProg[st] = F.prog;
-            }
-        }
-        const FSet ts = front_set(smem + set_off(st), cl);
-        const uint32_t local = q - F.t0, s = local / G, b = local - s * G;
-        const uint32_t w0 = s * F.K * G + b;
-        const uint32_t nwin = w0 >= F.nw ? 0u : min(F.K, (F.nw - w0 + G - 1) / G);
-        for (uint32_t ps = 0; ps < 2; ++ps) {
-            uint32_t e = 0;
-            // (pass ps's prefetch, selected word by word: an indexed array of
-            // them would live in scratch)
-            Fr v0, v1;
-#pragma unroll
-            for (int w = 0; w < 8; ++w) {
-                v0.w[w] = ps ? fb.v0.w[w] : fa.v0.w[w];
-                v1.w[w] = ps ? fb.v1.w[w] : fa.v1.w[w];
-            }
-            const bool in0 = ps ? fb.in0 : fa.in0, in1 = ps ? fb.in1 : fa.in1;
-            if (slot_elem(F, ws, nwin, ps * 64 + lane, &e))
-                element_program(*r.a, r.a->e_begin + e, smem + buf_off(x) + (ps * 64 + lane) * ev, ts.K, ts.mo,
-                                ts.vw, v0, in0, v1, in1);
-        }
-        if (lane == 0) {
-            sTile[x] = q;
-            sSet[x] = st;
-            sNW[x] = nwin;
-        }
-    };
-    if (wave == 0) {
-        uint32_t t0 = 0, t1 = 0, t2 = 0;
-        if (lane == 0) {
-            t0 = atomicAdd(fc.ctr, 1u);
-            t1 = atomicAdd(fc.ctr, 1u);
-            t2 = atomicAdd(fc.ctr, 1u);
-        }
-        t0 = __builtin_amdgcn_readfirstlane(t0);
-        n1 = __builtin_amdgcn_readfirstlane(t1);
-        n2 = __builtin_amdgcn_readfirstlane(t2);
-        issue_loads(t0, 0);
-        phase_a(t0, 0, 0, 0);
-        issue_loads(n1, 1);
-        if (lane == 0) n3v = atomicAdd(fc.ctr, 1u);
-    }
-    __syncthreads();
-    for (uint32_t k = 0, wk = 0;; ++k, wk = wk == 2 ? 0u : wk + 1) {
-        const uint32_t bx = k & 1u;                                 // buffers by parity, windows by k mod 3
-        const uint32_t wk1 = wk == 2 ? 0u : wk + 1, wk2 = wk1 == 2 ? 0u : wk1 + 1;
-        const uint32_t cur = sTile[bx];
-        if (cur >= TT) break;                                       // (uniform)
-        const uint32_t cset = sSet[bx];
-        if (wave == 0) {
-            // ---- producer: the next ticket's phase A into the other buffer
-            // (its windows and loads were prepared a round ago), then the
-            // windows and view loads of the ticket after it
-            phase_a(n1, bx ^ 1u, wk1, cset);
-            n1 = n2;
-            n2 = __builtin_amdgcn_readfirstlane(n3v);               // (returned during phase A's waits)
-            issue_loads(n1, wk2);
-            if (lane == 0) n3v = atomicAdd(fc.ctr, 1u);
-        } else {
-            // ---- consumers: the current ticket's windows, one half-cell per
-            // lane, two windows per step (their LDS reads in flight together)
-            const FStream F = sF[stream_of(cur)];
-            const StageArgs& a = *S.rec(F.prog).a;
-            const uint32_t so = set_off(cset);
-            const FSet ts = front_set(smem + so, cl);
-            const uint32_t rb = F.lk ? a.C : 0u;                    // the region's first slot
-            const uint32_t* Dr = ts.D + 2 * rb;
-            const uint4* Mr = ts.M + 2 * rb;
-            uint4* out = reinterpret_cast<uint4*>(F.lk ? a.out_lk + (uint64_t)a.e_begin * F.U
-                                                       : a.out_adv + (uint64_t)a.e_begin * F.U);
-            const uint32_t u = tid - 64, vb = buf_off(bx), nwin = sNW[bx], U = F.U, mag = F.magic, H = F.H;
-            auto half = [&](uint32_t j, bool& ok, int32_t& hc, uint32_t& d, uint4& m, uint32_t& base) {
-                const FWin w = sW[wk][j];
-                hc = w.hb + (int32_t)u;
-                ok = hc >= 0 && (uint32_t)hc < H;
-                const uint32_t rel = ((uint32_t)max(hc, 0) >> 1) - w.c0 + w.phase;
-                const uint32_t el = fastdiv(rel, U, mag), slot = rel - el * U;
-                const uint32_t kx = 2 * slot + ((uint32_t)hc & 1u);
-                d = ok ? Dr[kx] : 0u;
-                m = ok ? Mr[kx] : make_uint4(0, 0, 0, 0);
-                base = ((d & kHalfElem) ? vb + (j * F.epw + el) * ev : so) + (d & 0xffffu);
-            };
-            auto put = [&](bool ok, int32_t hc, uint32_t d, const uint4& m, uint32_t base) {
-                const uint32_t sh = (d >> 16) & 31u;
-                const uint32_t* x = smem + base;
-                const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4];
-                if (ok)
-                    out[hc] = make_uint4(__builtin_amdgcn_alignbit(x1, x0, sh) & m.x,
-                                         __builtin_amdgcn_alignbit(x2, x1, sh) & m.y,
-                                         __builtin_amdgcn_alignbit(x3, x2, sh) & m.z,
-                                         __builtin_amdgcn_alignbit(x4, x3, sh) & m.w);
-            };
-            uint32_t j = 0;
-            for (; j + 2 <= nwin; j += 2) {
-                bool ok0, ok1;
-                int32_t h0, h1;
-                uint32_t d0, d1, b0, b1;
-                uint4 m0, m1;
-                half(j, ok0, h0, d0, m0, b0);
-                half(j + 1, ok1, h1, d1, m1, b1);
-                put(ok0, h0, d0, m0, b0);
-                put(ok1, h1, d1, m1, b1);
-            }
-            if (j < nwin) {
-                bool ok0;
-                int32_t h0;
-                uint32_t d0, b0;
-                uint4 m0;
-                half(j, ok0, h0, d0, m0, b0);
-                put(ok0, h0, d0, m0, b0);
-            }
-        }
-        __syncthreads();
-    }
-    // the last block out resets the counters for the next launch on this stream
-    // (after the producer's last dequeue has returned)
-    if (tid == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t done = atomicAdd(fc.ctr + 1, 1u);
-        if (done == gridDim.x - 1) {
-            atomicExch(fc.ctr, 0u);
-            atomicExch(fc.ctr + 1, 0u);
-        }
-    }
-}
-__global__ __launch_bounds__(64 * kFrontWaves) void k_stage_front(const StageArgs a, const FrontCtl fc) {
-    stage_front(SrcSingle{&a}, fc);
-}
-__global__ __launch_bounds__(64 * kFrontWaves) void k_stage_front_multi(const StageMulti m, const FrontCtl fc) {
-    stage_front(SrcMulti{&m}, fc);
-}
-static int g_cus = 0;
-static uint32_t cu_count() {
-    if (!g_cus) {
-        int dev = 0, n = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        g_cus = n > 0 ? n : 256;
-    }
-    return (uint32_t)g_cus;
-}
-// Small launches (a batch under min_bytes of cells) and regions of one cell per
-// element stay on the one-block-per-chunk kernels.
-static bool front_suits(const StageArgs* const* progs, int n, double min_bytes) {
-    double bytes = 0;
-    for (int i = 0; i < n; ++i) {
-        const StageArgs& a = *progs[i];
-        if (a.e_end <= a.e_begin) continue;
-        if (a.C + a.L > kMaxAdv + kMaxLk || a.nv > kMaxV) return false;
-        if ((a.C && kFrontElems / front_epw(a.C) == 0) || (a.L && kFrontElems / front_epw(a.L) == 0)) return false;
-        bytes += 32.0 * (a.e_end - a.e_begin) * (a.C + a.L);
-        if (2.0 * (a.e_end - a.e_begin) * std::max(a.C, a.L) >= 2147483648.0 - 512.0) return false;
-    }
-    return bytes > 0 && bytes >= min_bytes;
-}
-static uint32_t g_front_diag = 0;
-void set_front_diag(uint32_t d) { g_front_diag = d; }
-hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t st, uint32_t* ctr, uint32_t occ,
-                             double min_bytes) {
-    if (!ctr || !occ || !front_suits(progs, n, min_bytes)) return launch_stage_multi(progs, n, st);
-    StageMulti m;
-    m.nprog = 0;
-    uint32_t used = 0, cl = 0, ev = 0;
-    const StageArgs* single = nullptr;
-    const uint32_t grid = occ * cu_count();
-    auto flush = [&]() -> hipError_t {
-        hipError_t e = hipSuccess;
-        if (m.nprog) {
-            FrontCtl fc{ctr, cl, ev, g_front_diag};
-            const uint32_t lds = front_lds_bytes(cl, ev);
-            if (lds > 160u * 1024u - 2048u) return hipErrorInvalidValue;
-            if (m.nprog == 1)
-                launch_ev(k_stage_front, dim3(grid), dim3(64 * kFrontWaves), lds, st, *single, fc);
-            else
-                launch_ev(k_stage_front_multi, dim3(grid), dim3(64 * kFrontWaves), lds, st, m, fc);
-            e = hipGetLastError();
-        }
-        m.nprog = 0;
-        used = cl = ev = 0;
-        return e;
-    };
-    for (int i = 0; i < n; ++i) {
-        const StageArgs& a = *progs[i];
-        if (a.e_end <= a.e_begin) continue;
-        const uint32_t rb = stage_record_bytes(a.nmo, a.C, a.L, a.nk);
-        if (m.nprog == (uint32_t)kMaxMulti || used + rb > kMultiBytes || (m.nprog && rb > kMultiBytes)) {
-            const hipError_t e = flush();
-            if (e != hipSuccess) return e;
-        }
-        if (rb > kMultiBytes) {                         // too large for a record: a launch of its own
-            single = &a;
-            m.nprog = 1;
-            cl = a.C + a.L;
-            ev = stage_elem_words(a.nv ? a.nv : 1);
-            const hipError_t e = flush();
-            if (e != hipSuccess) return e;
-            continue;
-        }
-        uint8_t* r = m.data + used;
-        memcpy(r, &a, kRecHead);
-        uint8_t* q = r + kRecHead;
-        memcpy(q, a.mo, 8 * a.nmo);
-        q += 8 * a.nmo;
-        memcpy(q, a.adv, 4 * a.C);
-        q += 4 * a.C;
-        memcpy(q, a.lk, 4 * a.L);
-        q += 4 * a.L;
-        memcpy(q, a.K, 32 * a.nk);
-        m.off[m.nprog] = used;
-        m.blk0[m.nprog] = 0;
-        ++m.nprog;
-        if (m.nprog == 1) single = &a;
-        used += rb;
-        cl = std::max(cl, a.C + a.L);
-        ev = std::max(ev, stage_elem_words(a.nv ? a.nv : 1));
-    }
-    return flush();
-}
-
 // ----------------------------------------------------------------- maxbits
 __global__ __launch_bounds__(256) void k_maxbits(const DView v, uint32_t rows, uint32_t cols,
                                                  unsigned* out) {
@@ -2118,6 +1668,108 @@ __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, co
         }
 }
 
+// Residues of the 4 x 4 accumulator tiles of one wave, stored in MFMA order:
+// R[mod][tile][wave][a][b][lane][reg] (one u32 per lane and (a, b): a wave store
+// is 256 contiguous bytes); the combine reads the same order (crt_combine_elem).
+__device__ __forceinline__ void crt_store_residues(const v4i (&acc)[4][4], uint8_t* __restrict__ R,
+                                                   uint32_t nblk, uint32_t tile, int mod) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int m = (int)c_crt_mod[mod];
+    const float inv = c_crt_invf[mod];
+    uint32_t* Rt = reinterpret_cast<uint32_t*>(R + ((uint64_t)mod * nblk + tile) * kCrtTileBytes) +
+                   wave * 1024 + lane;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                // |acc| <= 2^27: fp32 quotient off by at most one (m >= 71)
+                const int av = acc[a][b][reg];
+                const int q = (int)floorf((float)av * inv);
+                int r = av - __mul24(q, m);
+                r += r < 0 ? m : 0;
+                r -= r >= m ? m : 0;
+                w |= (uint32_t)r << (8 * reg);
+            }
+            Rt[(a * 4 + b) * 64] = w;
+        }
+}
+
+// The same (128 x 128 tile, modulus) unit with the operand chunks staged by
+// LDS-DMA (global_load_lds_dwordx4: no staging registers, no ds_write pass).
+// A 64-k chunk of a 128-row operand tile is eight 16-row MFMA fragments; each
+// lands lane-linear as 1 KiB (lane l: row l & 15, k bytes 16 (l >> 4) ..), which
+// is exactly the v_mfma_i32_16x16x64_i8 operand layout, so the fragment reads
+// are contiguous ds_read_b128 (conflict-free) and no swizzle is needed. NBUF
+// LDS buffers of 16 KiB (A then B); wave w stages fragments 2w, 2w + 1 of both
+// operands. Chunk c + NBUF - 1 is issued while chunk c is multiplied; the one
+// barrier per chunk (its vmcnt(0) retires this wave's DMA of chunk c) also
+// orders the re-use of the buffer read one chunk earlier.
+template <int NBUF>
+__device__ __forceinline__ void crt_gemm_tile_dma(const uint8_t* __restrict__ Ar, const uint8_t* __restrict__ Br,
+                                                  uint32_t astride, uint32_t bstride, uint32_t kpad,
+                                                  uint32_t nblk, uint32_t tile, uint8_t* __restrict__ R,
+                                                  uint32_t bi, uint32_t bj, int mod, uint8_t* __restrict__ S) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t wr = wave >> 1, wc = wave & 1;
+    const uint32_t kcn = kpad / 64;
+    const uint8_t* Ap = Ar + ((uint64_t)mod * astride + bi * CT) * kpad;
+    const uint8_t* Bp = Br + ((uint64_t)mod * bstride + bj * CT) * kpad;
+    // this lane's source bytes of fragment f = 2 wave + h: row 16 f + (lane & 15), k part lane >> 4
+    const uint64_t lo0 = (uint64_t)(32 * wave + (lane & 15)) * kpad + (lane >> 4) * 16;
+    const uint64_t lo1 = lo0 + 16ull * kpad;
+    constexpr uint32_t BUF = 2 * CT * 64;                       // 16 KiB per chunk (A, B)
+    auto issue = [&](uint32_t c) {
+        uint8_t* d = S + (c % NBUF) * BUF + wave * 2048;
+        const uint64_t ko = (uint64_t)c * 64;
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(Ap + lo0 + ko),
+                                         (void __attribute__((address_space(3)))*)(d), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(Ap + lo1 + ko),
+                                         (void __attribute__((address_space(3)))*)(d + 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(Bp + lo0 + ko),
+                                         (void __attribute__((address_space(3)))*)(d + BUF / 2), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(Bp + lo1 + ko),
+                                         (void __attribute__((address_space(3)))*)(d + BUF / 2 + 1024), 16, 0, 0);
+    };
+    v4i acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = v4i{0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < NBUF - 1; ++c)
+        if ((uint32_t)c < kcn) issue(c);
+    for (uint32_t c = 0; c < kcn; ++c) {
+        if constexpr (NBUF == 2) {
+            __syncthreads();                              // chunk c landed; buffer (c - 1) % NBUF free
+        } else {
+            // chunks c + 1 .. c + NBUF - 2 stay in flight across the barrier
+            // (a __syncthreads() would wait for them too: vmcnt(0))
+            if (c + NBUF - 2 < kcn)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NBUF - 2)) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+        if (c + NBUF - 1 < kcn) issue(c + NBUF - 1);
+        const uint8_t* Ac = S + (c % NBUF) * BUF;
+        const uint8_t* Bc = Ac + BUF / 2;
+        v4i af[4], bf[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) af[a] = *reinterpret_cast<const v4i*>(Ac + (wr * 4 + a) * 1024 + lane * 16);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) bf[b] = *reinterpret_cast<const v4i*>(Bc + (wc * 4 + b) * 1024 + lane * 16);
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
+    }
+    crt_store_residues(acc, R, nblk, tile, mod);
+}
 
 // Debug timeline of the GEMM's blocks (svdw_debug_trace): per real block its
 // start and end on the 100 MHz wall clock and (XCC id << 16 | HW_ID).
@@ -2187,6 +1839,42 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
     crt_gemm_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.nblk, t,
                   q.R, bi, bj, (int)mod, S, tp1, tp2);
     trace_block(t0, tp1, tp2);
+}
+// (job, modulus, tile) unit u of the batch in the XCD-modulus-major order of
+// k_gemm_crt_multi; false for blocks past the units
+__device__ __forceinline__ bool crt_unit(const CrtBatch& b, uint32_t blk, uint32_t* jo, uint32_t* mo,
+                                         uint32_t* to) {
+    uint32_t cnt[kMaxCrtJobs], total = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxCrtJobs; ++j) {
+        cnt[j] = 0;
+        if ((uint32_t)j < b.njobs)
+            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk;
+        total += cnt[j];
+    }
+    const uint32_t per = (total + 7) / 8, k = blk >> 3;
+    if (k >= per) return false;
+    uint32_t u = (blk & 7) * per + k;
+    if (u >= total) return false;
+    uint32_t j = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxCrtJobs - 1; ++q)
+        if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
+    *jo = j;
+    *mo = u / b.job[j].nblk;
+    *to = u - *mo * b.job[j].nblk;
+    return true;
+}
+template <int NBUF>
+__global__ __launch_bounds__(256) void k_gemm_crt_dma(const CrtBatch b) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[NBUF * 2 * CT * 64];
+    uint32_t j, mod, t;
+    if (!crt_unit(b, blockIdx.x, &j, &mod, &t)) return;
+    const CrtJob& q = b.job[j];
+    uint32_t bi, bj;
+    crt_tile_rc(q, t, &bi, &bj);
+    crt_gemm_tile_dma<NBUF>(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad,
+                            q.nblk, t, q.R, bi, bj, (int)mod, S);
 }
 // C from its n residues, written as canonical Fr to out[i*ors + j*ocs]: one
 // element per thread in the GEMM's tile order (each block one 256-element
@@ -2267,10 +1955,11 @@ size_t crt_scratch_bytes(uint32_t N, uint32_t M) {
     const uint64_t a = ((uint64_t)N + CT - 1) / CT * CT, m = ((uint64_t)M + CT - 1) / CT * CT;
     return (size_t)(kCrtMaxMod * a * m);
 }
-hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
-    CrtBatch b = b0;
+// tile / block fields of a batch; units: GEMM blocks for n = kCrtMaxMod, cblocks: combine blocks
+static hipError_t prep_crt_batch(CrtBatch& b, uint32_t& units, uint32_t& cblocks) {
     if (b.njobs < 1 || b.njobs > (uint32_t)kMaxCrtJobs) return hipErrorInvalidValue;
-    uint32_t units = 0, cblocks = 0;
+    units = 0;
+    cblocks = 0;
     for (uint32_t j = 0; j < b.njobs; ++j) {
         CrtJob& q = b.job[j];
         q.tiles_a = (q.N + CT - 1) / CT;
@@ -2290,6 +1979,13 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
         q.cblk0 = cblocks;
         cblocks += q.nblk * (kCrtTileBytes / 256);
     }
+    return hipSuccess;
+}
+hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
+    CrtBatch b = b0;
+    uint32_t units, cblocks;
+    const hipError_t pe = prep_crt_batch(b, units, cblocks);
+    if (pe != hipSuccess) return pe;
     hipLaunchKernelGGL(k_gemm_crt_multi, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -240,21 +240,11 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t st);
 // Independent stages (no stage reads another's cells) in as few k_stage_multi
 // launches as their records fit (stage_record_bytes, kMultiBytes); n >= 1.
 hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t st);
-// The same stages on the persistent front streamer (k_stage_front): occ blocks
-// per CU writing every output region as a compact moving front of 4 KiB
-// windows, tickets from the counters at ctr (two words, zero between
-// launches; one slot per stream: launches on one stream never overlap).
-// ctr null, occ 0, a batch under min_bytes of cells or a region of one cell
-// per element: launch_stage_multi.
-hipError_t launch_stage_pers(const StageArgs* const* progs, int n, hipStream_t st, uint32_t* ctr, uint32_t occ,
-                             double min_bytes);
 // The next stage launches of this thread (launch_stage*, until
 // launch_events_used) record e0 at the first one's start and e1 at each one's
 // end through their dispatch; launch_events_used says whether any launched.
 void set_launch_events(hipEvent_t e0, hipEvent_t e1);
 bool launch_events_used();
-// timing diagnostic of the front streamer (cells WRONG): 1 = no producer view loads
-void set_front_diag(uint32_t d);
 // does the record of `a` fit one k_stage_multi launch?
 bool stage_multi_fits(const StageArgs& a);
 // max over the view of bit-length(|signed(x)|): out[b] = max of block b

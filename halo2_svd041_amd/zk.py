@@ -13,6 +13,7 @@ gfx950 kernels. Where the reference panics on a shape mismatch, these raise
 """
 from __future__ import annotations
 
+import collections
 import ctypes as ct
 from dataclasses import dataclass
 from typing import Optional
@@ -115,35 +116,62 @@ class Context:
         self.layout_opts = {}
         self._h = ct.c_void_p()
         # device input tensors whose reads may still be queued (include/svdw.h,
-        # "Lifetime of device inputs"): referenced until the context's work is
-        # known complete, so torch's allocator cannot hand their memory to a
+        # "Lifetime of device inputs"): id -> [tensor, sequence number of the
+        # last call that read it], kept until a checkpoint at or after that call
+        # has completed, so torch's allocator cannot hand their memory to a
         # tensor written on another stream while a pipelined call still reads it
-        self._held = []
+        self._held = {}
+        self._seq = 0
+        self._ckpts = collections.deque()      # (call sequence number, torch event)
+        self._ckpt_stream = None
         p = Params(device, precision_bits, lookup_bits)
         check(lib().svdw_ctx_create(ct.byref(p), ct.byref(self._h)))
 
-    # above this many held tensors, a call first asks the device (svdw_query)
-    # whether the earlier calls are done; the bench's resident inputs are one set
-    HOLD_QUERY = 8
+    # Per-call completion, at a cost amortised over calls: every HOLD_EVERY-th
+    # call that holds inputs records a checkpoint (a side stream made to wait for
+    # everything queued on the context, svdw_stream_signal, and an event on it);
+    # a held tensor is released once a checkpoint at or after its last reader has
+    # completed. At most HOLD_CKPTS checkpoints are pending: beyond that the
+    # oldest is waited for. So back-to-back calls on fresh tensors hold the inputs
+    # of at most HOLD_EVERY * (HOLD_CKPTS + 1) calls, whatever the device's
+    # progress, and each call costs one dict update plus an event query.
+    HOLD_EVERY = 8
+    HOLD_CKPTS = 4
 
     def _hold(self, *tensors) -> None:
-        """Keep device inputs alive until their readers have run (see _held)."""
+        """Keep device inputs alive until the calls reading them have run (see _held)."""
+        self._seq += 1
+        seq = self._seq
         held = self._held
-        if len(held) >= self.HOLD_QUERY:
-            rc = lib().svdw_query(self._h)
-            if rc < 0:
-                check(rc)
-            if rc == 1:
-                held.clear()
         for t in tensors:
-            if not any(t is h for h in held):
-                held.append(t)
+            held[id(t)] = [t, seq]
+        ck = self._ckpts
+        done = 0
+        while ck and (len(ck) > self.HOLD_CKPTS or ck[0][1].query()):
+            s0, ev = ck.popleft()
+            ev.synchronize()                     # (a no-op unless over HOLD_CKPTS)
+            done = s0
+        if done:
+            for k in [k for k, (_, s) in held.items() if s <= done]:
+                del held[k]
+        if seq % self.HOLD_EVERY == 0:
+            torch = _torch_mod()
+            if self._ckpt_stream is None:
+                self._ckpt_stream = torch.cuda.Stream(self.device)
+            check(lib().svdw_stream_signal(self._h, self._ckpt_stream.cuda_stream))
+            ev = torch.cuda.Event()
+            ev.record(self._ckpt_stream)
+            ck.append((seq, ev))
+
+    def _release_all(self) -> None:
+        self._held.clear()
+        self._ckpts.clear()
 
     def close(self) -> None:
         if self._h:
             lib().svdw_ctx_destroy(self._h)      # (waits for the context's work)
             self._h = ct.c_void_p()
-        self._held = []
+        self._release_all()
 
     def __del__(self):  # pragma: no cover - best effort
         try:
@@ -163,14 +191,14 @@ class Context:
 
     def reset(self) -> None:
         check(lib().svdw_ctx_reset(self._h))     # (synchronises)
-        self._held.clear()
+        self._release_all()
 
     def reserve(self, phase: int, advice: int, lookups: int) -> None:
         check(lib().svdw_reserve(self._h, phase, advice, lookups))
 
     def sync(self) -> None:
         check(lib().svdw_sync(self._h))
-        self._held.clear()
+        self._release_all()
 
     def query(self) -> bool:
         """svdw_query: has everything queued on the context completed?"""
@@ -178,7 +206,7 @@ class Context:
         if rc < 0:
             check(rc)
         if rc == 1:
-            self._held.clear()
+            self._release_all()
         return rc == 1
 
     def advice_len(self, phase: int) -> int:

@@ -263,7 +263,8 @@ int svdw_verify_mul_witness_on(svdw_ctx* ctx, void* stream, const double* a, con
 #define SVDW_GEMM_MFMA 0
 #define SVDW_GEMM_VALU 1
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
-/* Options (svdw_set_option; 21 names). Tuning knobs, bit-identical results
+/* Options (svdw_set_option; 18 names; any other name is SVDW_EINVAL). Tuning
+ * knobs, bit-identical results
  * for every value, defaults first:
  *   "gemm_impl" 0 | 1; "gemm_crt" 1 | 0 (CRT or digit-plane matrix-core GEMM);
  *   "overlap" 1 | 0 (the three check_svd_phase0 products run ahead on a second
@@ -314,13 +315,7 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   -1: the third on a row-sharded rank, else the cell stream); the d checks
  *   on the cell stream behind the products (0), on the second stream with the
  *   bounds and u.d (1) or on the third ahead of phase 1 (2)); "vm_linear" 1 | 0 (the captured sequence is queued on the context
- *   stream alone, a linear graph, instead of forking to the second stream);
- *   "stage_occ" 0 | 1 | 2 (stage launches of >= 64 MiB of cells use the
- *   persistent front streamer at 1 or 2 blocks per CU, a compact store front of
- *   4 KiB windows; 0: one block per 256 elements, the measured default);
- *   test hooks: "stage_front_all" 0 | 1 (the front streamer for every stage
- *   launch when stage_occ > 0), "stage_diag" 0 | 1 (process-wide timing
- *   diagnostic of the front streamer: its cells are WRONG when non-zero).
+ *   stream alone, a linear graph, instead of forking to the second stream).
  * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:
  *   phase 1 starts with the two ctx_gate constant cells [1, 0] that
  *   examples/svd_example.rs:183's rlc.load_rlc_cache(.., 1) appends as recalled
@@ -334,13 +329,17 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   in one launch with the bit-length words folded inside it, b.g of a
  *   row-sharded rank from the f64 inputs, 4 KiB-aligned stage store windows,
  *   GEMM sizes decided on the device.
- * Retired options (accepted and ignored, so callers written against round 3
- *   keep running; to be removed with the next ABI version): "bits_fold",
+ * ABI version 2 removed the options ABI 1 had retired as no-ops ("bits_fold",
  *   "bounds_after", "colsum", "d_checks_aside", "dep_values", "fused_quantize",
  *   "gemm_batch", "gemm_priority", "gemm_rt", "prelaunch_at", "prod_blocks",
- *   "prod_first", "res_first", "stage_align", "stage_priority", "stage_probe";
- *   "stage_nt" (non-temporal stage stores, round 5). */
+ *   "prod_first", "res_first", "stage_align", "stage_priority", "stage_probe",
+ *   "stage_nt") and the persistent front streamer with its options
+ *   ("stage_occ", "stage_front_all", and "stage_diag", a timing diagnostic
+ *   whose cells were wrong): they are unknown names now (SVDW_EINVAL). */
 int svdw_set_option(svdw_ctx* ctx, const char* name, int64_t value);
+/* SVDW_ABI_VERSION of the library (callers compare it with the header's). */
+#define SVDW_ABI_VERSION 2
+int svdw_abi_version(void);
 /* Captures and replays of the verify_mul_witness graph ("graph") so far. */
 int svdw_graph_stats(svdw_ctx* ctx, uint64_t* captures, uint64_t* replays);
 

@@ -130,3 +130,22 @@ def test_dry_rescale_shift_only():
     po.signed_div_scale(o, po.RangeChip(LB), po.load_witness(o, 5), P, S)
     assert ctx.advice_len(0) - n0 == 4 * (len(o.advice) - 1)
     ctx.close()
+
+
+def test_removed_options_are_rejected():
+    """ABI version 2: the front streamer's options, among
+    them "stage_diag" (a timing diagnostic that made the engine write wrong
+    cells), and the no-ops retired in ABI 1 are unknown names (SVDW_EINVAL);
+    live options still set."""
+    L = _lib.lib()
+    assert L.svdw_abi_version() == 2
+    ctx = hs.Context(device=-1, precision_bits=63, lookup_bits=19)
+    try:
+        for name in ("stage_diag", "stage_occ", "stage_front_all", "stage_nt", "bits_fold",
+                     "prod_first", "stage_probe"):
+            assert L.svdw_set_option(ctx.handle, name.encode(), 1) == -1, name
+            assert b"unknown option" in L.svdw_last_error()
+        ctx.set_option("stage_elems", 128)
+        ctx.set_option("pipeline", 0)
+    finally:
+        ctx.close()
