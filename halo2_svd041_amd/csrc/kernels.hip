@@ -711,8 +711,20 @@ __device__ __forceinline__ void stage_block(const StageArgs& a, const MicroOp* _
     stage_chunk(a, L, blk, f);
 }
 
+// XCD-contiguous order ("stage_xcd"): blocks are dealt round-robin to the 8
+// XCDs, so block b of a grid of 8 per takes chunk (b mod 8) per + b / 8 and the
+// blocks resident on one XCD write neighbouring chunks; false past the chunks
+__device__ __forceinline__ bool stage_xcd_block(uint32_t nchunks, uint32_t* g) {
+    const uint32_t per = gridDim.x >> 3;
+    *g = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    return *g < nchunks;
+}
+template <bool X>
 __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
-    stage_block(a, a.mo, a.adv, a.lk, a.K, blockIdx.x);
+    uint32_t g = blockIdx.x;
+    if (X && !stage_xcd_block((a.e_end - a.e_begin + (a.E ? a.E : kStageElems) - 1) / (a.E ? a.E : kStageElems), &g))
+        return;
+    stage_block(a, a.mo, a.adv, a.lk, a.K, g);
 }
 
 // the program of batch block g (m.blk0 ascending)
@@ -745,9 +757,11 @@ __device__ __forceinline__ Rec multi_rec(const StageMulti& m, uint32_t p) {
 // gamma powers, is_equal rows, ...) and the phase-0 stages that read only the
 // loaded matrices share one launch (one tail, one dispatch).
 __global__ __launch_bounds__(256) void k_stage_multi(const StageMulti m) {
-    const uint32_t p = multi_prog(m, blockIdx.x);
+    uint32_t g = blockIdx.x;
+    if (m.xcd && !stage_xcd_block(m.blk0[m.nprog], &g)) return;
+    const uint32_t p = multi_prog(m, g);
     const Rec q = multi_rec(m, p);
-    stage_block(*q.a, q.mo, q.adv, q.lk, q.K, blockIdx.x - m.blk0[p]);
+    stage_block(*q.a, q.mo, q.adv, q.lk, q.K, g - m.blk0[p]);
 }
 // Profiled stage launches (set_launch_events): the kernel's own dispatch
 // records the profiler's events (hipExtLaunchKernelGGL: start on the first
@@ -783,7 +797,10 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     if (E > kStageElems) return hipErrorInvalidValue;
     const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1, E, a.C + a.L);
     const uint32_t grid = (n + E - 1) / E;
-    launch_ev(k_stage, dim3(grid), dim3(256), lds, st, a);
+    if (a.flags & STAGE_XCD)
+        launch_ev(k_stage<true>, dim3((grid + 7) / 8 * 8), dim3(256), lds, st, a);
+    else
+        launch_ev(k_stage<false>, dim3(grid), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 bool stage_multi_fits(const StageArgs& a) {
@@ -801,7 +818,8 @@ hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t 
             e = launch_stage(*single, st);
         } else if (m.nprog > 1) {
             m.blk0[m.nprog] = blocks;
-            launch_ev(k_stage_multi, dim3(blocks), dim3(256), lds, st, m);
+            m.xcd = (single->flags & STAGE_XCD) ? 1u : 0u;
+            launch_ev(k_stage_multi, dim3(m.xcd ? (blocks + 7) / 8 * 8 : blocks), dim3(256), lds, st, m);
             e = hipGetLastError();
         }
         m.nprog = 0;
@@ -1547,6 +1565,9 @@ __device__ __forceinline__ uint32_t crt_lds(uint32_t row, uint32_t part) {
 // pipe. (A single buffer with a store / barrier / read / MFMA / barrier chain
 // per step took ~1 us per step, ~16 us per tile, against ~0.1 us of MFMA.)
 constexpr int crt_lds_bytes() { return 4 * CT * CROW; }
+__device__ __forceinline__ void crt_store_residues(const v4i (&acc)[4][4], uint8_t* __restrict__ R,
+                                                   uint32_t nblk, uint32_t tile, int mod);
+template <bool FASTEPI = false>
 __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, const uint8_t* __restrict__ Br,
                                               uint32_t astride, uint32_t bstride, uint32_t kpad,
                                               uint32_t nblk, uint32_t tile, uint8_t* __restrict__ R,
@@ -1641,6 +1662,10 @@ __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, co
 #undef CRT_LSTORE
 #undef CRT_FRAG
 #undef CRT_MMA
+    if constexpr (FASTEPI) {
+        crt_store_residues(acc, R, nblk, tile, mod);
+        return;
+    }
     // residues, stored in MFMA order: R[mod][tile][wave][a][b][lane][reg], so
     // a lane's four accumulator rows are one 4-byte word and a wave store is
     // 256 contiguous bytes (no LDS tile, no barrier); the combine reads the
@@ -1674,26 +1699,28 @@ __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, co
 __device__ __forceinline__ void crt_store_residues(const v4i (&acc)[4][4], uint8_t* __restrict__ R,
                                                    uint32_t nblk, uint32_t tile, int mod) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int m = (int)c_crt_mod[mod];
-    const float inv = c_crt_invf[mod];
+    const uint32_t m = c_crt_mod[mod], magic = c_crt_magic[mod], bias = c_crt_bias[mod];
     uint32_t* Rt = reinterpret_cast<uint32_t*>(R + ((uint64_t)mod * nblk + tile) * kCrtTileBytes) +
                    wave * 1024 + lane;
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            uint32_t w = 0;
+            uint32_t r[4];
 #pragma unroll
             for (int reg = 0; reg < 4; ++reg) {
-                // |acc| <= 2^27: fp32 quotient off by at most one (m >= 71)
-                const int av = acc[a][b][reg];
-                const int q = (int)floorf((float)av * inv);
-                int r = av - __mul24(q, m);
-                r += r < 0 ? m : 0;
-                r -= r >= m ? m : 0;
-                w |= (uint32_t)r << (8 * reg);
+                // |acc| <= K 2^14 <= 2^27, bias = m ceil(2^27 / m): x < 2^28 + 2^8,
+                // where the quotient by magic = ceil(2^32 / m) is floor(x / m) or
+                // one more (x (magic m - 2^32) < 2^32 m / 16), so x - q m is in
+                // [-m, m) and min_u32(r, r + m) is the residue: five VALU
+                // operations (the fp32 quotient with two corrections took twelve)
+                const uint32_t x = (uint32_t)acc[a][b][reg] + bias;
+                const uint32_t q = __umulhi(x, magic);
+                const uint32_t rr = (uint32_t)((int)x - __mul24((int)q, (int)m));
+                r[reg] = min(rr, rr + m);
             }
-            Rt[(a * 4 + b) * 64] = w;
+            Rt[(a * 4 + b) * 64] = __builtin_amdgcn_perm(r[1], r[0], 0x0c0c0400u) |
+                                   (__builtin_amdgcn_perm(r[3], r[2], 0x0c0c0400u) << 16);
         }
 }
 
@@ -1711,7 +1738,8 @@ template <int NBUF>
 __device__ __forceinline__ void crt_gemm_tile_dma(const uint8_t* __restrict__ Ar, const uint8_t* __restrict__ Br,
                                                   uint32_t astride, uint32_t bstride, uint32_t kpad,
                                                   uint32_t nblk, uint32_t tile, uint8_t* __restrict__ R,
-                                                  uint32_t bi, uint32_t bj, int mod, uint8_t* __restrict__ S) {
+                                                  uint32_t bi, uint32_t bj, int mod, uint8_t* __restrict__ S,
+                                                  uint64_t& tp1, uint64_t& tp2) {
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t wr = wave >> 1, wc = wave & 1;
@@ -1754,6 +1782,7 @@ __device__ __forceinline__ void crt_gemm_tile_dma(const uint8_t* __restrict__ Ar
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
         }
+        if (c == 0) tp1 = wall_clock64();
         if (c + NBUF - 1 < kcn) issue(c + NBUF - 1);
         const uint8_t* Ac = S + (c % NBUF) * BUF;
         const uint8_t* Bc = Ac + BUF / 2;
@@ -1768,6 +1797,7 @@ __device__ __forceinline__ void crt_gemm_tile_dma(const uint8_t* __restrict__ Ar
             for (int b = 0; b < 4; ++b)
                 acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
     }
+    tp2 = wall_clock64();
     crt_store_residues(acc, R, nblk, tile, mod);
 }
 
@@ -1840,6 +1870,34 @@ __global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
                   q.R, bi, bj, (int)mod, S, tp1, tp2);
     trace_block(t0, tp1, tp2);
 }
+__global__ __launch_bounds__(256) void k_gemm_crt_fe(const CrtBatch b) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes()];
+    const uint64_t t0 = wall_clock64();
+    uint32_t cnt[kMaxCrtJobs], total = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxCrtJobs; ++j) {
+        cnt[j] = 0;
+        if ((uint32_t)j < b.njobs)
+            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk;
+        total += cnt[j];
+    }
+    const uint32_t per = (total + 7) / 8, k = blockIdx.x >> 3;
+    if (k >= per) return;
+    uint32_t u = (blockIdx.x & 7) * per + k;
+    if (u >= total) return;
+    uint32_t j = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxCrtJobs - 1; ++q)
+        if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
+    const CrtJob& q = b.job[j];
+    const uint32_t mod = u / q.nblk, t = u - mod * q.nblk;
+    uint32_t bi, bj;
+    crt_tile_rc(q, t, &bi, &bj);
+    uint64_t tp1 = 0, tp2 = 0;
+    crt_gemm_tile<true>(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.nblk, t,
+                        q.R, bi, bj, (int)mod, S, tp1, tp2);
+    trace_block(t0, tp1, tp2);
+}
 // (job, modulus, tile) unit u of the batch in the XCD-modulus-major order of
 // k_gemm_crt_multi; false for blocks past the units
 __device__ __forceinline__ bool crt_unit(const CrtBatch& b, uint32_t blk, uint32_t* jo, uint32_t* mo,
@@ -1868,13 +1926,164 @@ __device__ __forceinline__ bool crt_unit(const CrtBatch& b, uint32_t blk, uint32
 template <int NBUF>
 __global__ __launch_bounds__(256) void k_gemm_crt_dma(const CrtBatch b) {
     __shared__ __attribute__((aligned(16))) uint8_t S[NBUF * 2 * CT * 64];
+    const uint64_t t0 = wall_clock64();
     uint32_t j, mod, t;
     if (!crt_unit(b, blockIdx.x, &j, &mod, &t)) return;
     const CrtJob& q = b.job[j];
     uint32_t bi, bj;
     crt_tile_rc(q, t, &bi, &bj);
+    uint64_t tp1 = 0, tp2 = 0;
     crt_gemm_tile_dma<NBUF>(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad,
-                            q.nblk, t, q.R, bi, bj, (int)mod, S);
+                            q.nblk, t, q.R, bi, bj, (int)mod, S, tp1, tp2);
+    trace_block(t0, tp1, tp2);
+}
+
+// persistent CRT GEMM blocks per XCD label: two per CU (32 CUs per XCD)
+static constexpr uint32_t kCrtPersPerXcd = 64;
+// Operand row-tile bases and output place of one (job, modulus, tile) unit.
+struct CrtUnitPtr {
+    const uint8_t* Ap;
+    const uint8_t* Bp;
+    uint8_t* R;
+    uint32_t nblk, t, mod;
+};
+__device__ __forceinline__ CrtUnitPtr crt_unit_ptr(const CrtBatch& b, const uint32_t (&cnt)[kMaxCrtJobs],
+                                                   uint32_t u) {
+    uint32_t j = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxCrtJobs - 1; ++q)
+        if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
+    const CrtJob& q = b.job[j];
+    CrtUnitPtr o;
+    o.mod = u / q.nblk;
+    o.t = u - o.mod * q.nblk;
+    o.nblk = q.nblk;
+    o.R = q.R;
+    uint32_t bi, bj;
+    crt_tile_rc(q, o.t, &bi, &bj);
+    o.Ap = q.Ar + ((uint64_t)o.mod * q.astride + bi * CT) * q.kpad;
+    o.Bp = (q.sym ? q.Ar : q.Br) + ((uint64_t)o.mod * (q.sym ? q.astride : q.bstride) + bj * CT) * q.kpad;
+    return o;
+}
+// The register-staged tile loop of crt_gemm_tile on a persistent grid: block b
+// (XCD label b mod 8, slot b / 8 of nb8) takes the units lo + slot, lo + slot +
+// nb8, ... of its XCD's eighth [lo, hi) of the batch's units (the order of
+// k_gemm_crt_multi), and its chunk pipeline runs on across unit boundaries: the
+// loads of the next unit's first chunks are in flight while the current unit's
+// last chunks are multiplied and its residues reduced and stored, so a block's
+// prologue (3.3 us per 128 x 128 x 1024 unit, gemmprobe timeline) is paid once
+// instead of per unit. Needs one kpad for all jobs with at least 8 chunks (a
+// load is then at most one unit ahead); launch_gemm_crt_multi checks.
+__global__ __launch_bounds__(256, 2) void k_gemm_crt_pers(const CrtBatch b) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes()];
+    const uint64_t t0 = wall_clock64();
+    uint32_t cnt[kMaxCrtJobs], total = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxCrtJobs; ++j) {
+        cnt[j] = 0;
+        if ((uint32_t)j < b.njobs)
+            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk;
+        total += cnt[j];
+    }
+    const uint32_t per = (total + 7) / 8, x = blockIdx.x & 7, slot = blockIdx.x >> 3, nb8 = gridDim.x >> 3;
+    const uint32_t lo = x * per, hi = min(lo + per, total);
+    if (lo + slot >= hi) return;
+    const uint32_t nunits = (hi - lo - slot + nb8 - 1) / nb8;
+    const uint32_t kpad = b.job[0].kpad, kcn = kpad / 64;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t wr = wave >> 1, wc = wave & 1;
+    const uint32_t r0 = tid >> 2, r1 = (tid + 256) >> 2, part = tid & 3;
+    const uint32_t frow = lane & 15, fk = (lane >> 4) * 16;
+    const uint64_t o0 = (uint64_t)r0 * kpad + part * 16, o1 = (uint64_t)r1 * kpad + part * 16;
+    CrtUnitPtr cur = crt_unit_ptr(b, cnt, lo + slot);
+    CrtUnitPtr nxt = nunits > 1 ? crt_unit_ptr(b, cnt, lo + slot + nb8) : cur;
+    v4i acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[a][q] = v4i{0, 0, 0, 0};
+    // chunk ch of the current unit (ch >= kcn: chunk ch - kcn of the next one,
+    // the current unit's last chunk when there is none)
+#define CRP_GLOAD(g, ch)                                                                      \
+    {                                                                                         \
+        const uint32_t c_ = (ch);                                                             \
+        const bool nx_ = c_ >= kcn;                                                           \
+        const uint8_t* A_ = nx_ ? nxt.Ap : cur.Ap;                                            \
+        const uint8_t* B_ = nx_ ? nxt.Bp : cur.Bp;                                            \
+        const uint64_t ko = (uint64_t)(nx_ ? c_ - kcn : c_) * 64;                             \
+        g##a0 = *reinterpret_cast<const uint4*>(A_ + o0 + ko);                                \
+        g##a1 = *reinterpret_cast<const uint4*>(A_ + o1 + ko);                                \
+        g##b0 = *reinterpret_cast<const uint4*>(B_ + o0 + ko);                                \
+        g##b1 = *reinterpret_cast<const uint4*>(B_ + o1 + ko);                                \
+    }
+#define CRP_LSTORE(g, buf)                                                                    \
+    {                                                                                         \
+        uint8_t* Ac = S + (buf) * 2 * CT * CROW;                                              \
+        uint8_t* Bc = Ac + CT * CROW;                                                         \
+        *reinterpret_cast<uint4*>(Ac + crt_lds(r0, part)) = g##a0;                            \
+        *reinterpret_cast<uint4*>(Ac + crt_lds(r1, part)) = g##a1;                            \
+        *reinterpret_cast<uint4*>(Bc + crt_lds(r0, part)) = g##b0;                            \
+        *reinterpret_cast<uint4*>(Bc + crt_lds(r1, part)) = g##b1;                            \
+    }
+#define CRP_FRAG(buf)                                                                         \
+    {                                                                                         \
+        const uint8_t* Ac = S + (buf) * 2 * CT * CROW;                                        \
+        const uint8_t* Bc = Ac + CT * CROW;                                                   \
+        _Pragma("unroll") for (int a = 0; a < 4; ++a)                                         \
+            af[a] = *reinterpret_cast<const v4i*>(Ac + crt_lds(wr * 64 + a * 16 + frow, fk >> 4)); \
+        _Pragma("unroll") for (int q = 0; q < 4; ++q)                                         \
+            bf[q] = *reinterpret_cast<const v4i*>(Bc + crt_lds(wc * 64 + q * 16 + frow, fk >> 4)); \
+    }
+#define CRP_MMA()                                                                             \
+    {                                                                                         \
+        _Pragma("unroll") for (int a = 0; a < 4; ++a)                                         \
+            _Pragma("unroll") for (int q = 0; q < 4; ++q)                                     \
+                acc[a][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[q], acc[a][q], 0, 0, 0); \
+    }
+#define CRP_STEP(g, c)                                                                        \
+    {                                                                                         \
+        CRP_LSTORE(g, ((c) + 1) & 1);                                                         \
+        CRP_GLOAD(g, (c) + 5);                                                                \
+        CRP_MMA();                                                                            \
+        __syncthreads();                                                                      \
+        CRP_FRAG(((c) + 1) & 1);                                                              \
+    }
+    uint4 g0a0, g0a1, g0b0, g0b1, g1a0, g1a1, g1b0, g1b1;
+    uint4 g2a0, g2a1, g2b0, g2b1, g3a0, g3a1, g3b0, g3b1;
+    v4i af[4], bf[4];
+    CRP_GLOAD(g0, 0);
+    CRP_GLOAD(g1, 1);
+    CRP_GLOAD(g2, 2);
+    CRP_GLOAD(g3, 3);
+    CRP_LSTORE(g0, 0);
+    CRP_GLOAD(g0, 4);
+    __syncthreads();
+    const uint64_t tp1 = wall_clock64();
+    CRP_FRAG(0);
+    for (uint32_t k = 0; k < nunits; ++k) {
+        if (k + 1 >= nunits) nxt = cur;
+        // (the last unit's loads past its end re-read its first chunks: the
+        // stores and fragment reads of those are never multiplied)
+        for (uint32_t c0 = 0; c0 < kcn; c0 += 4) {
+            CRP_STEP(g1, c0)
+            CRP_STEP(g2, c0 + 1)
+            CRP_STEP(g3, c0 + 2)
+            CRP_STEP(g0, c0 + 3)
+        }
+        crt_store_residues(acc, cur.R, cur.nblk, cur.t, (int)cur.mod);
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[a][q] = v4i{0, 0, 0, 0};
+        cur = nxt;
+        if (k + 2 < nunits) nxt = crt_unit_ptr(b, cnt, lo + slot + (k + 2) * nb8);
+    }
+    trace_block(t0, tp1, wall_clock64());
+#undef CRP_STEP
+#undef CRP_GLOAD
+#undef CRP_LSTORE
+#undef CRP_FRAG
+#undef CRP_MMA
 }
 // C from its n residues, written as canonical Fr to out[i*ors + j*ocs]: one
 // element per thread in the GEMM's tile order (each block one 256-element
@@ -1986,7 +2195,23 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
     uint32_t units, cblocks;
     const hipError_t pe = prep_crt_batch(b, units, cblocks);
     if (pe != hipSuccess) return pe;
-    hipLaunchKernelGGL(k_gemm_crt_multi, dim3((units + 7) / 8 * 8), dim3(256), 0, st, b);
+    const dim3 grid((units + 7) / 8 * 8);
+    switch (b.kern) {
+    case 0: hipLaunchKernelGGL(k_gemm_crt_multi, grid, dim3(256), 0, st, b); break;
+    case 1: hipLaunchKernelGGL(k_gemm_crt_fe, grid, dim3(256), 0, st, b); break;
+    case 2: hipLaunchKernelGGL(k_gemm_crt_dma<3>, grid, dim3(256), 0, st, b); break;
+    case 3: hipLaunchKernelGGL(k_gemm_crt_dma<4>, grid, dim3(256), 0, st, b); break;
+    case 4: {
+        // persistent: one kpad of >= 8 chunks for every job, else the per-unit kernel
+        bool ok = b.job[0].kpad >= 512;
+        for (uint32_t j = 1; j < b.njobs; ++j) ok = ok && b.job[j].kpad == b.job[0].kpad;
+        const uint32_t pg = std::min<uint32_t>((units + 7) / 8 * 8, 8 * kCrtPersPerXcd);
+        if (ok) hipLaunchKernelGGL(k_gemm_crt_pers, dim3(pg), dim3(256), 0, st, b);
+        else hipLaunchKernelGGL(k_gemm_crt_fe, grid, dim3(256), 0, st, b);
+        break;
+    }
+    default: return hipErrorInvalidValue;
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_crt_combine_multi, dim3((cblocks + 7) / 8 * 8), dim3(256), 0, st, b, cblocks);
@@ -1996,11 +2221,12 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st) {
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st, uint32_t kern) {
     if (sym && (N != M || astride != bstride)) return hipErrorInvalidValue;
     CrtBatch b;
     memset(&b, 0, sizeof b);
     b.njobs = 1;
+    b.kern = kern;
     CrtJob& q = b.job[0];
     q.Ar = Ar;
     q.Br = sym ? Ar : Br;
@@ -2673,6 +2899,12 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
     const Fr* __restrict__ wm = tab_slot(J.tab, J.tl, na);
     const Fr* __restrict__ wn = wm + J.tl;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    switch (B.prio) {                                   // (uniform; an immediate operand)
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    default: break;
+    }
     const uint32_t lb = blockIdx.x - J.blk0;
     const uint32_t rb = (J.blk0 & 7) ? lb : scan_row(lb, J.rows), r = J.r_begin + rb;
     Fr* rowout = J.out + (uint64_t)rb * (3ull * L + 1);

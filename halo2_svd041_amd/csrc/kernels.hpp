@@ -56,6 +56,7 @@ struct ScanBatch {
     uint32_t njobs;
     const unsigned* bitw;     // device bit-length words of the NaSpecs (na = 0 launches)
     ScaleTab f;               // slot factors for the pc / ptab epilogue
+    uint32_t prio;            // s_setprio of the scan waves (0-3; "scan_prio")
 };
 // gamma powers from host-side Montgomery tables: g^j = t[j & 15] t[16 + (j >> 4 & 15)]
 // t[32 + (j >> 8)] (j < 256 * nhi)
@@ -320,7 +321,7 @@ hipError_t launch_residues_f64(const ResSegs& q, const unsigned* W, int precisio
 hipError_t launch_gemm_crt(bool sym, const uint8_t* Ar, const uint8_t* Br, uint32_t N, uint32_t M,
                            uint32_t astride, uint32_t bstride, uint32_t kpad, uint8_t* R, Fr* out,
                            int64_t ors, int64_t ocs, const unsigned* bits_a,
-                           const unsigned* bits_b, uint32_t lk, hipStream_t st);
+                           const unsigned* bits_b, uint32_t lk, hipStream_t st, uint32_t kern = 0);
 // Debug: record the CRT GEMM's block timeline into buf (3 u64 per block; null: off).
 hipError_t set_debug_trace(void* buf);
 static constexpr int kCrtMaxResidues = 40;   // = kCrtMaxMod (crt_tables.hpp)
@@ -350,6 +351,11 @@ struct CrtJob {
 struct CrtBatch {
     CrtJob job[kMaxCrtJobs];
     uint32_t njobs;
+    // GEMM kernel (bit-identical; round-6 A/B): 0 register-staged chunks,
+    // 1 the same with the five-operation residue epilogue, 2 / 3 LDS-DMA
+    // staging with 3 / 4 chunk buffers, 4 kernel 1 on a persistent grid
+    // (k_gemm_crt_pers: one block's chunk pipeline runs across its units)
+    uint32_t kern;
 };
 // R sized crt_scratch_bytes per job
 hipError_t launch_gemm_crt_multi(const CrtBatch& b, hipStream_t st);

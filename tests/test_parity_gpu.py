@@ -199,7 +199,10 @@ def test_crt_gemm_tiles_parity(gpu_ctx_factory, N, M, P, world, device):
                                   {"phase1_overlap": 0}, {"phase1_overlap": 2},
                                   {"overlap": 0},
                                   {"stage_batch": 0}, {"pipeline": 0}, {"pipeline": 0, "phase1_overlap": 2},
-                                  {"gemm_impl": 1}, {"res_f64": 0}, {"f64_views": 0}])
+                                  {"gemm_impl": 1}, {"res_f64": 0}, {"f64_views": 0},
+                                  {"gemm_kern": 1}, {"gemm_kern": 2}, {"gemm_kern": 3},
+                                  {"gemm_kern": 4}, {"scan_prio": 3}, {"stage_xcd": 1},
+                                  {"stage_xcd": 1, "stage_elems": 64}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
@@ -632,6 +635,33 @@ def test_device_input_lifetime(gpu_ctx_factory):
     del junk
     a0, l0, a1 = corc.svd_witness(m, u, v, d, P, 19, g)
     _assert_streams(ctx, a0, l0, a1)
+
+
+@pytest.mark.parametrize("kern", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,M", [(320, 300), (300, 520)])
+def test_gemm_kern_full_streams(gpu_ctx_factory, kern, N, M):
+    """Every CRT GEMM kernel (option gemm_kern) against the shipped one (kernel
+    0, oracle-checked throughout this file) on pipelined device-input witnesses
+    at K >= 300 (>= 8 chunks of 64: the persistent kernel runs, its chunk
+    pipeline crossing unit boundaries; 300 x 520 mixes kpads, where it falls
+    back to kernel 1): whole advice and lookup streams of both phases, two calls
+    in a row."""
+    import halo2_svd041_amd as hs
+    P = 63
+    outs = []
+    for k in (0, kern):
+        ctx = gpu_ctx_factory(P)
+        ctx.set_option("gemm_kern", k)
+        for c in range(2):
+            m, u, d, v = gen_svd_input(N, M, seed=4100 + c + N)
+            hs.svd_witness(ctx, *_on_device(m, u, v, d), gamma_for(4200 + c))
+        ctx.sync()
+        outs.append((ctx.advice(0), ctx.lookups(0), ctx.advice(1)))
+        ctx.close()
+    for name, a, b in zip(("advice0", "lookup0", "advice1"), outs[0], outs[1]):
+        assert a.shape == b.shape
+        bad = np.nonzero(np.any(a != b, axis=1))[0]
+        assert bad.size == 0, f"{name}: {bad.size} cells differ, first at {bad[:8]}"
 
 
 def test_held_inputs_bounded(gpu_ctx_factory):

@@ -18,10 +18,43 @@
 
 using namespace svdw;
 
+// A stand-in for k_stage beside the GEMM: 256-thread blocks holding 63 KiB of
+// LDS (two per CU, as k_stage_multi's 256-element blocks), each writing one
+// contiguous 64 KiB chunk in 16-byte lane stores after five LDS word reads per
+// store (phase B's descriptor + source words).
+__global__ __launch_bounds__(256) void k_standin(uint4* __restrict__ out, size_t n16) {
+    extern __shared__ uint32_t L[];
+    const uint32_t t = threadIdx.x;
+    for (uint32_t i = t; i < 63 * 256; i += 256) L[i] = i * 2654435761u;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * 4096;
+    for (uint32_t r = 0; r < 16; ++r) {
+        const uint32_t k = (r * 256 + t) * 5;
+        uint4 v = make_uint4(L[k % 16128], L[(k + 1) % 16128], L[(k + 2) % 16128], L[(k + 3) % 16128]);
+        v.x ^= L[(k + 4) % 16128];
+        const size_t o = base + r * 256 + t;
+        if (o < n16) out[o] = v;
+    }
+}
+
+static constexpr int NV = 6;
+static const char* vname[NV] = {"shipped(reg)", "dma2", "dma3", "dma4", "reg+fastepi", "persistent"};
+static void launch_variant(int v, dim3 g, hipStream_t st, const CrtBatch& b) {
+    switch (v) {
+    case 0: hipLaunchKernelGGL(k_gemm_crt_multi, g, dim3(256), 0, st, b); break;
+    case 1: hipLaunchKernelGGL(k_gemm_crt_dma<2>, g, dim3(256), 0, st, b); break;
+    case 2: hipLaunchKernelGGL(k_gemm_crt_dma<3>, g, dim3(256), 0, st, b); break;
+    case 3: hipLaunchKernelGGL(k_gemm_crt_dma<4>, g, dim3(256), 0, st, b); break;
+    case 4: hipLaunchKernelGGL(k_gemm_crt_fe, g, dim3(256), 0, st, b); break;
+    default: hipLaunchKernelGGL(k_gemm_crt_pers, dim3(std::min<uint32_t>(g.x, 8 * kCrtPersPerXcd)), dim3(256), 0, st, b); break;
+    }
+}
+
 __global__ void k_nmod(const unsigned* W, uint32_t lk, int* out) { *out = crt_nmod(W[0], W[1], lk); }
 
 int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? atoi(argv[1]) : 1024, reps = argc > 2 ? atoi(argv[2]) : 20;
+    const bool quick = argc > 3 && !strcmp(argv[3], "quick");     // one round, no stand-in (PMC runs)
     const uint32_t kpad = (n + 255) / 256 * 256, rp = (n + 127) / 128 * 128;
     uint32_t lk = 0;
     while ((1u << lk) < n) ++lk;
@@ -68,20 +101,19 @@ int main(int argc, char** argv) {
          2 * nnn * (nm[0] + 2 * nm[1] * symfrac)},
     };
     std::vector<uint8_t*> Rs;
-    for (int v = 0; v < 4; ++v) {
+    for (int v = 0; v < NV; ++v) {
         uint8_t* R;
         CK(hipMalloc(&R, 3 * rbytes));
         CK(hipMemset(R, 0, 3 * rbytes));
         Rs.push_back(R);
     }
-    const char* vname[4] = {"shipped(reg)", "dma2", "dma3", "dma4"};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (const Case& cs : cases) {
-        double best[4] = {1e9, 1e9, 1e9, 1e9};
-        for (int round = 0; round < 3; ++round)
-            for (int v = 0; v < 4; ++v) {
+        double best[NV] = {1e9, 1e9, 1e9, 1e9, 1e9, 1e9};
+        for (int round = 0; round < (quick ? 1 : 3); ++round)
+            for (int v = 0; v < NV; ++v) {
                 CrtBatch b;
                 memset(&b, 0, sizeof b);
                 b.njobs = cs.njobs;
@@ -90,12 +122,7 @@ int main(int argc, char** argv) {
                 uint32_t units, cblocks;
                 CK(prep_crt_batch(b, units, cblocks));
                 const dim3 g((units + 7) / 8 * 8);
-                auto launch = [&] {
-                    if (v == 0) hipLaunchKernelGGL(k_gemm_crt_multi, g, dim3(256), 0, 0, b);
-                    else if (v == 1) hipLaunchKernelGGL(k_gemm_crt_dma<2>, g, dim3(256), 0, 0, b);
-                    else if (v == 2) hipLaunchKernelGGL(k_gemm_crt_dma<3>, g, dim3(256), 0, 0, b);
-                    else hipLaunchKernelGGL(k_gemm_crt_dma<4>, g, dim3(256), 0, 0, b);
-                };
+                auto launch = [&] { launch_variant(v, g, 0, b); };
                 for (int w = 0; w < 3; ++w) launch();
                 CK(hipDeviceSynchronize());
                 CK(hipEventRecord(e0));
@@ -110,7 +137,7 @@ int main(int argc, char** argv) {
         // residue bytes of every variant against the shipped kernel (all jobs' scratch)
         std::vector<uint8_t> r0(3 * rbytes), r1(3 * rbytes);
         CK(hipMemcpy(r0.data(), Rs[0], 3 * rbytes, hipMemcpyDeviceToHost));
-        for (int v = 0; v < 4; ++v) {
+        for (int v = 0; v < NV; ++v) {
             size_t diff = 0;
             if (v) {
                 CK(hipMemcpy(r1.data(), Rs[v], 3 * rbytes, hipMemcpyDeviceToHost));
@@ -120,7 +147,99 @@ int main(int argc, char** argv) {
                    cs.name, vname[v], best[v], cs.ops / (best[v] * 1e-6) / 1e15,
                    100.0 * cs.ops / (best[v] * 1e-6) / 5.03e15, diff);
         }
-        for (int v = 0; v < 4; ++v) CK(hipMemset(Rs[v], 0, 3 * rbytes));
+        // per-block timeline of one launch per variant (svdw_debug_trace's clocks,
+        // 100 MHz): prologue (start -> first chunk staged), K loop, epilogue
+        if (!quick) {
+            const size_t nb = 16384;
+            unsigned long long* tr;
+            CK(hipMalloc(&tr, nb * 5 * 8));
+            std::vector<unsigned long long> h(nb * 5);
+            for (int v = 0; v < NV; ++v) {
+                CrtBatch b;
+                memset(&b, 0, sizeof b);
+                b.njobs = cs.njobs;
+                for (int j = 0; j < cs.njobs; ++j)
+                    job(b.job[j], cs.sym[j], W + cs.wa[j], W + cs.wb[j], Rs[v] + j * rbytes);
+                uint32_t units, cblocks;
+                CK(prep_crt_batch(b, units, cblocks));
+                const dim3 g((units + 7) / 8 * 8);
+                if (g.x > nb) continue;
+                CK(hipMemset(tr, 0, nb * 5 * 8));
+                CK(set_debug_trace(tr));
+                launch_variant(v, g, 0, b);
+                CK(hipDeviceSynchronize());
+                CK(set_debug_trace(nullptr));
+                CK(hipMemcpy(h.data(), tr, nb * 5 * 8, hipMemcpyDeviceToHost));
+                unsigned long long lo = ~0ull, hi = 0;
+                double sp = 0, sl = 0, se = 0;
+                size_t cnt = 0;
+                for (size_t k = 0; k < g.x; ++k) {
+                    const unsigned long long* r = &h[5 * k];
+                    if (!r[0]) continue;
+                    ++cnt;
+                    lo = r[0] < lo ? r[0] : lo;
+                    hi = r[3] > hi ? r[3] : hi;
+                    sp += (double)(r[1] - r[0]);
+                    sl += (double)(r[2] - r[1]);
+                    se += (double)(r[3] - r[2]);
+                }
+                if (cnt)
+                    printf("%-7s %-13s timeline: %zu blocks, span %.1f us; per block: prologue %.2f us, "
+                           "K loop %.2f us, epilogue %.2f us\n", cs.name, vname[v], cnt, (hi - lo) / 100.0,
+                           sp / cnt / 100.0, sl / cnt / 100.0, se / cnt / 100.0);
+            }
+            CK(hipFree(tr));
+        }
+        for (int v = 0; v < NV; ++v) CK(hipMemset(Rs[v], 0, 3 * rbytes));
+    }
+    if (quick) return 0;
+    // beside the stand-in store stream: the stand-in alone, then with each
+    // variant's three-job batch launched on a second stream just after it
+    {
+        const size_t sbytes = (size_t)2 << 30, n16 = sbytes / 16;
+        uint4* so;
+        CK(hipMalloc(&so, sbytes));
+        hipStream_t sa, sb;
+        CK(hipStreamCreateWithFlags(&sa, hipStreamNonBlocking));
+        CK(hipStreamCreateWithFlags(&sb, hipStreamNonBlocking));
+        hipEvent_t a0, a1, b0, b1;
+        CK(hipEventCreate(&a0)); CK(hipEventCreate(&a1)); CK(hipEventCreate(&b0)); CK(hipEventCreate(&b1));
+        const uint32_t sgrid = (uint32_t)(n16 / 4096);
+        CK(hipFuncSetAttribute((const void*)k_standin, hipFuncAttributeMaxDynamicSharedMemorySize, 63 * 1024));
+        const Case& cs = cases[2];
+        for (int round = 0; round < 3; ++round)
+            for (int v = -1; v < NV; ++v) {
+                CrtBatch b;
+                memset(&b, 0, sizeof b);
+                b.njobs = cs.njobs;
+                for (int j = 0; j < cs.njobs; ++j)
+                    job(b.job[j], cs.sym[j], W + cs.wa[j], W + cs.wb[j], Rs[v < 0 ? 0 : v] + j * rbytes);
+                uint32_t units, cblocks;
+                CK(prep_crt_batch(b, units, cblocks));
+                const dim3 g((units + 7) / 8 * 8);
+                float sms = 0, gms = 0;
+                for (int rep = 0; rep < 4; ++rep) {
+                    CK(hipDeviceSynchronize());
+                    CK(hipEventRecord(a0, sa));
+                    hipLaunchKernelGGL(k_standin, dim3(sgrid), dim3(256), 63 * 1024, sa, so, n16);
+                    CK(hipEventRecord(a1, sa));
+                    if (v >= 0) {
+                        CK(hipEventRecord(b0, sb));
+                        launch_variant(v, g, sb, b);
+                        CK(hipEventRecord(b1, sb));
+                    }
+                    CK(hipDeviceSynchronize());
+                    float x;
+                    CK(hipEventElapsedTime(&x, a0, a1));
+                    if (rep) sms += x / 3;
+                    if (v >= 0) {
+                        CK(hipEventElapsedTime(&x, b0, b1));
+                        if (rep) gms += x / 3;
+                    }
+                }
+                printf("beside stand-in (2 GiB, 2 blocks/CU x 63 KiB): %-13s stand-in %8.1f us (%5.0f GB/s)  gemm batch3 %8.1f us\n",
+                       v < 0 ? "none" : vname[v], sms * 1e3, sbytes / (sms * 1e-3) / 1e9, gms * 1e3);
+            }
     }
     return 0;
 }
