@@ -487,8 +487,12 @@ struct svdw_ctx {
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
     hipStream_t stream_id[3] = {};          // st, st2, st3 as created (st / st2 / st3 are swapped at times)
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
-    uint32_t gemm_kern = 0;                 // "gemm_kern": CRT GEMM kernel (CrtBatch::kern)
-    uint32_t scan_prio = 0;                 // "scan_prio": s_setprio of the row-scan waves
+    // "gemm_kern": CRT GEMM kernel (CrtBatch::kern); -1: the persistent grid for
+    // a product queued on its own (svdw_honest_prover_mat_mul, gemm_solo),
+    // one block per unit inside the witness calls, beside their stage kernels
+    int gemm_kern = -1;
+    bool gemm_solo = false;
+    int res_wait = -1;                      // "res_wait": stages wait for the residue planes
     bool gemm_batched = false;              // this witness's products went out as one batch
     bool res_f64 = true;                    // "res_f64": CRT residue planes of m, u, v from the
                                             // f64 inputs, one launch (else from the cells)
@@ -1623,7 +1627,8 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
             ProfScope ps(c, s, std::string("k_gemm_crt") + (sym ? ":s" : ""), 32.0 * N * M,
                          (double)N * M * K);
             hipck(launch_gemm_crt(sym, Ar, Br, N, M, rpa, sym ? rpa : rpb,
-                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s, c->gemm_kern),
+                                  kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s,
+                                  c->gemm_kern >= 0 ? (uint32_t)c->gemm_kern : (c->gemm_solo ? 1u : 0u)),
                   "k_gemm_crt");
         }
         if (!quantized)
@@ -2075,7 +2080,6 @@ static void verify_mul_many(svdw_ctx* c, uint32_t phase, const VMul* vm, int n, 
         S.sb.f = scale_tab();
         const int na = batch_na_host(c, S.ms, (int)S.sb.njobs);
         ProfScope ps(c, c->st, name, S.bytes, S.ops);
-        S.sb.prio = c->scan_prio;
         hipck(launch_scan_batch(S.sb, na, c->st), "k_matvec_scan");
     };
     // b.g of job i: the b scan of the first job with the same b (m.v^T and
@@ -2295,7 +2299,14 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
     // the stages beside the products wait for the residue planes, which then
     // run alone instead of beside the first (HBM-saturating) stages (same box:
     // 512^2 0.427 -> 0.422 ms, 1024^2 2.098 -> 2.072 ms, 8-way rank 0.36 -> 0.35)
-    stream_dep(c, pst, pst != c->st ? c->st : c->st2);
+    // ("res_wait" 0, pipelined with every load read from the f64 inputs: the
+    // stages need nothing of this chain before the products, so st2 goes on
+    // without waiting for the residue planes; -1: so on unsharded contexts,
+    // tools/ab.py r6f: 512^2 0.378 -> 0.371 ms, 1024^2 2.035 -> 2.026 ms, while
+    // the 8-way rank's chain is better served by the wait, 0.321 -> 0.327 ms)
+    const bool rw = c->res_wait >= 0 ? c->res_wait != 0 : sharded(c);
+    if (rw || !c->in_pipe || !c->f64_views || c->f64reg.empty())
+        stream_dep(c, pst, pst != c->st ? c->st : c->st2);
     const uint8_t* P[3] = {(const uint8_t*)c->digA.p, (const uint8_t*)c->digC.p,
                            (const uint8_t*)c->digB.p};                 // A planes of m, u, v
     const uint32_t stride[3] = {rp_m, rp_u, rp_v}, kp[3] = {kpM, kpN, kpM}, lk[3] = {lkM, lkN, lkM};
@@ -2341,7 +2352,7 @@ static void prelaunch_products_f64(svdw_ctx* c, const svdw_mat (&A)[3], const sv
             roff += rbytes[g];
         }
         c->gemm_batched = true;
-        b.kern = c->gemm_kern;
+        b.kern = c->gemm_kern >= 0 ? (uint32_t)c->gemm_kern : 0u;
         if (b.njobs) {
             ProfScope ps(c, pst, "k_gemm_crt:multi", bytes, ops);
             hipck(launch_gemm_crt_multi(b, pst), "k_gemm_crt_multi");
@@ -3074,7 +3085,7 @@ static svdw_counts verify_mul_witness(svdw_ctx* c, const double* a, const double
             ProfScope ps(c, c->st, "k_gemm_crt", 32.0 * N * M, (double)N * M * K);
             hipck(launch_gemm_crt(false, (const uint8_t*)c->digA.p, (const uint8_t*)c->digB.p, N, M, rpa, rpb,
                                   kpad, (uint8_t*)c->crtR.p, cellp(c, 0, off), M, 1, dbits, dbits + 1, lk,
-                                  c->st, c->gemm_kern),
+                                  c->st, c->gemm_kern >= 0 ? (uint32_t)c->gemm_kern : 0u),
                   "k_gemm_crt");
         }
     } else if (!c->dry) {
@@ -3235,17 +3246,17 @@ static void ctx_init_device(svdw_ctx* c) {
 // The settings (options, shard, profiler) of `s` onto the lane `d`; a change
 // bumps the lane's epoch (its captured graph no longer applies).
 static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
-    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->gemm_crt, s->gemm_kern, s->scan_prio, s->res_f64,
+    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->gemm_crt, s->gemm_kern, s->res_wait, s->res_f64,
                          s->phase1_overlap, s->prod_cell, s->hold_us, s->rlc_prefix, s->p1_at, s->dchk_at, s->gamma_at,
                          s->f64_views, s->overlap, s->stage_batch, s->graph_vm, s->vm_linear, s->pipeline,
                          s->shard_rank, s->shard_world, s->prof, s->host_trace};
-    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->gemm_crt, d->gemm_kern, d->scan_prio, d->res_f64,
+    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->gemm_crt, d->gemm_kern, d->res_wait, d->res_f64,
                          d->phase1_overlap, d->prod_cell, d->hold_us, d->rlc_prefix, d->p1_at, d->dchk_at, d->gamma_at,
                          d->f64_views, d->overlap, d->stage_batch, d->graph_vm, d->vm_linear, d->pipeline,
                          d->shard_rank, d->shard_world, d->prof, d->host_trace};
     if (!memcmp(a, b, sizeof a) && d->prof_filter == s->prof_filter) return;
     d->gemm_impl = s->gemm_impl; d->stage_flags = s->stage_flags; d->stage_elems = s->stage_elems;
-    d->gemm_crt = s->gemm_crt; d->gemm_kern = s->gemm_kern; d->scan_prio = s->scan_prio; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
+    d->gemm_crt = s->gemm_crt; d->gemm_kern = s->gemm_kern; d->res_wait = s->res_wait; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
     d->prod_cell = s->prod_cell; d->hold_us = s->hold_us; d->rlc_prefix = s->rlc_prefix;
     d->p1_at = s->p1_at; d->f64_views = s->f64_views; d->overlap = s->overlap;
     d->dchk_at = s->dchk_at; d->gamma_at = s->gamma_at;
@@ -3879,6 +3890,11 @@ int svdw_honest_prover_mat_mul(svdw_ctx* c, uint32_t phase, const svdw_mat* a, c
         REQUIRE(c && a && b && out, "null argument");
         check_mat(c, *a);
         check_mat(c, *b);
+        struct Solo {                        // a product queued on its own: the persistent GEMM
+            svdw_ctx* c;
+            ~Solo() { c->gemm_solo = false; }
+        } solo{c};
+        c->gemm_solo = true;
         *out = honest_prover_mat_mul(c, phase, *a, *b);
     });
 }
@@ -4580,15 +4596,12 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "gemm_crt") {
             REQUIRE(value == 0 || value == 1, "gemm_crt: 0 or 1");
             c->gemm_crt = (int)value;
-        } else if (n == "scan_prio") {               // row-scan wave priority
-            REQUIRE(value >= 0 && value <= 3, "scan_prio: 0..3");
-            c->scan_prio = (uint32_t)value;
-        } else if (n == "stage_xcd") {               // XCD-contiguous stage block order
-            REQUIRE(value == 0 || value == 1, "stage_xcd: 0 or 1");
-            c->stage_flags = value ? (c->stage_flags | STAGE_XCD) : (c->stage_flags & ~STAGE_XCD);
+        } else if (n == "res_wait") {                // pipelined: st2 waits for the residue planes
+            REQUIRE(value >= -1 && value <= 1, "res_wait: -1 (auto), 0 or 1");
+            c->res_wait = (int)value;
         } else if (n == "gemm_kern") {               // CRT GEMM kernel variant (bit-identical)
-            REQUIRE(value >= 0 && value <= 4, "gemm_kern: 0..4");
-            c->gemm_kern = (uint32_t)value;
+            REQUIRE(value >= -1 && value <= 1, "gemm_kern: -1 (auto), 0 or 1");
+            c->gemm_kern = (int)value;
         } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
             c->stage_batch = value != 0;
         } else if (n == "f64_views") {

@@ -711,20 +711,8 @@ __device__ __forceinline__ void stage_block(const StageArgs& a, const MicroOp* _
     stage_chunk(a, L, blk, f);
 }
 
-// XCD-contiguous order ("stage_xcd"): blocks are dealt round-robin to the 8
-// XCDs, so block b of a grid of 8 per takes chunk (b mod 8) per + b / 8 and the
-// blocks resident on one XCD write neighbouring chunks; false past the chunks
-__device__ __forceinline__ bool stage_xcd_block(uint32_t nchunks, uint32_t* g) {
-    const uint32_t per = gridDim.x >> 3;
-    *g = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    return *g < nchunks;
-}
-template <bool X>
 __global__ __launch_bounds__(256) void k_stage(const StageArgs a) {
-    uint32_t g = blockIdx.x;
-    if (X && !stage_xcd_block((a.e_end - a.e_begin + (a.E ? a.E : kStageElems) - 1) / (a.E ? a.E : kStageElems), &g))
-        return;
-    stage_block(a, a.mo, a.adv, a.lk, a.K, g);
+    stage_block(a, a.mo, a.adv, a.lk, a.K, blockIdx.x);
 }
 
 // the program of batch block g (m.blk0 ascending)
@@ -757,11 +745,9 @@ __device__ __forceinline__ Rec multi_rec(const StageMulti& m, uint32_t p) {
 // gamma powers, is_equal rows, ...) and the phase-0 stages that read only the
 // loaded matrices share one launch (one tail, one dispatch).
 __global__ __launch_bounds__(256) void k_stage_multi(const StageMulti m) {
-    uint32_t g = blockIdx.x;
-    if (m.xcd && !stage_xcd_block(m.blk0[m.nprog], &g)) return;
-    const uint32_t p = multi_prog(m, g);
+    const uint32_t p = multi_prog(m, blockIdx.x);
     const Rec q = multi_rec(m, p);
-    stage_block(*q.a, q.mo, q.adv, q.lk, q.K, g - m.blk0[p]);
+    stage_block(*q.a, q.mo, q.adv, q.lk, q.K, blockIdx.x - m.blk0[p]);
 }
 // Profiled stage launches (set_launch_events): the kernel's own dispatch
 // records the profiler's events (hipExtLaunchKernelGGL: start on the first
@@ -797,10 +783,7 @@ hipError_t launch_stage(const StageArgs& a, hipStream_t st) {
     if (E > kStageElems) return hipErrorInvalidValue;
     const uint32_t lds = stage_lds_bytes(a.nv ? a.nv : 1, E, a.C + a.L);
     const uint32_t grid = (n + E - 1) / E;
-    if (a.flags & STAGE_XCD)
-        launch_ev(k_stage<true>, dim3((grid + 7) / 8 * 8), dim3(256), lds, st, a);
-    else
-        launch_ev(k_stage<false>, dim3(grid), dim3(256), lds, st, a);
+    launch_ev(k_stage, dim3(grid), dim3(256), lds, st, a);
     return hipGetLastError();
 }
 bool stage_multi_fits(const StageArgs& a) {
@@ -818,8 +801,7 @@ hipError_t launch_stage_multi(const StageArgs* const* progs, int n, hipStream_t 
             e = launch_stage(*single, st);
         } else if (m.nprog > 1) {
             m.blk0[m.nprog] = blocks;
-            m.xcd = (single->flags & STAGE_XCD) ? 1u : 0u;
-            launch_ev(k_stage_multi, dim3(m.xcd ? (blocks + 7) / 8 * 8 : blocks), dim3(256), lds, st, m);
+            launch_ev(k_stage_multi, dim3(blocks), dim3(256), lds, st, m);
             e = hipGetLastError();
         }
         m.nprog = 0;
@@ -1565,9 +1547,36 @@ __device__ __forceinline__ uint32_t crt_lds(uint32_t row, uint32_t part) {
 // pipe. (A single buffer with a store / barrier / read / MFMA / barrier chain
 // per step took ~1 us per step, ~16 us per tile, against ~0.1 us of MFMA.)
 constexpr int crt_lds_bytes() { return 4 * CT * CROW; }
+// Residues of the 4 x 4 accumulator tiles of one wave, stored in MFMA order:
+// R[mod][tile][wave][a][b][lane][reg] (one u32 per lane and (a, b): a wave store
+// is 256 contiguous bytes); the combine reads the same order (crt_combine_elem).
 __device__ __forceinline__ void crt_store_residues(const v4i (&acc)[4][4], uint8_t* __restrict__ R,
-                                                   uint32_t nblk, uint32_t tile, int mod);
-template <bool FASTEPI = false>
+                                                   uint32_t nblk, uint32_t tile, int mod) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t m = c_crt_mod[mod], magic = c_crt_magic[mod], bias = c_crt_bias[mod];
+    uint32_t* Rt = reinterpret_cast<uint32_t*>(R + ((uint64_t)mod * nblk + tile) * kCrtTileBytes) +
+                   wave * 1024 + lane;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            uint32_t r[4];
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) {
+                // |acc| <= K 2^14 <= 2^27, bias = m ceil(2^27 / m): x < 2^28 + 2^8,
+                // where the quotient by magic = ceil(2^32 / m) is floor(x / m) or
+                // one more (x (magic m - 2^32) < 2^32 m / 16), so x - q m is in
+                // [-m, m) and min_u32(r, r + m) is the residue: five VALU
+                // operations (the fp32 quotient with two corrections took twelve)
+                const uint32_t x = (uint32_t)acc[a][b][reg] + bias;
+                const uint32_t q = __umulhi(x, magic);
+                const uint32_t rr = (uint32_t)((int)x - __mul24((int)q, (int)m));
+                r[reg] = min(rr, rr + m);
+            }
+            Rt[(a * 4 + b) * 64] = __builtin_amdgcn_perm(r[1], r[0], 0x0c0c0400u) |
+                                   (__builtin_amdgcn_perm(r[3], r[2], 0x0c0c0400u) << 16);
+        }
+}
 __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, const uint8_t* __restrict__ Br,
                                               uint32_t astride, uint32_t bstride, uint32_t kpad,
                                               uint32_t nblk, uint32_t tile, uint8_t* __restrict__ R,
@@ -1662,144 +1671,9 @@ __device__ __forceinline__ void crt_gemm_tile(const uint8_t* __restrict__ Ar, co
 #undef CRT_LSTORE
 #undef CRT_FRAG
 #undef CRT_MMA
-    if constexpr (FASTEPI) {
-        crt_store_residues(acc, R, nblk, tile, mod);
-        return;
-    }
-    // residues, stored in MFMA order: R[mod][tile][wave][a][b][lane][reg], so
-    // a lane's four accumulator rows are one 4-byte word and a wave store is
-    // 256 contiguous bytes (no LDS tile, no barrier); the combine reads the
-    // same order (crt_combine_elem)
-    const int m = (int)c_crt_mod[mod];
-    const float inv = c_crt_invf[mod];
-    uint32_t* Rt = reinterpret_cast<uint32_t*>(R + ((uint64_t)mod * nblk + tile) * kCrtTileBytes) +
-                   wave * 1024 + lane;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            uint32_t w = 0;
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-                // |acc| <= 2^27: fp32 quotient off by at most one (m >= 71)
-                const int av = acc[a][b][reg];
-                const int q = (int)floorf((float)av * inv);
-                int r = av - __mul24(q, m);
-                r += r < 0 ? m : 0;
-                r -= r >= m ? m : 0;
-                w |= (uint32_t)r << (8 * reg);
-            }
-            Rt[(a * 4 + b) * 64] = w;
-        }
-}
-
-// Residues of the 4 x 4 accumulator tiles of one wave, stored in MFMA order:
-// R[mod][tile][wave][a][b][lane][reg] (one u32 per lane and (a, b): a wave store
-// is 256 contiguous bytes); the combine reads the same order (crt_combine_elem).
-__device__ __forceinline__ void crt_store_residues(const v4i (&acc)[4][4], uint8_t* __restrict__ R,
-                                                   uint32_t nblk, uint32_t tile, int mod) {
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t m = c_crt_mod[mod], magic = c_crt_magic[mod], bias = c_crt_bias[mod];
-    uint32_t* Rt = reinterpret_cast<uint32_t*>(R + ((uint64_t)mod * nblk + tile) * kCrtTileBytes) +
-                   wave * 1024 + lane;
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            uint32_t r[4];
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) {
-                // |acc| <= K 2^14 <= 2^27, bias = m ceil(2^27 / m): x < 2^28 + 2^8,
-                // where the quotient by magic = ceil(2^32 / m) is floor(x / m) or
-                // one more (x (magic m - 2^32) < 2^32 m / 16), so x - q m is in
-                // [-m, m) and min_u32(r, r + m) is the residue: five VALU
-                // operations (the fp32 quotient with two corrections took twelve)
-                const uint32_t x = (uint32_t)acc[a][b][reg] + bias;
-                const uint32_t q = __umulhi(x, magic);
-                const uint32_t rr = (uint32_t)((int)x - __mul24((int)q, (int)m));
-                r[reg] = min(rr, rr + m);
-            }
-            Rt[(a * 4 + b) * 64] = __builtin_amdgcn_perm(r[1], r[0], 0x0c0c0400u) |
-                                   (__builtin_amdgcn_perm(r[3], r[2], 0x0c0c0400u) << 16);
-        }
-}
-
-// The same (128 x 128 tile, modulus) unit with the operand chunks staged by
-// LDS-DMA (global_load_lds_dwordx4: no staging registers, no ds_write pass).
-// A 64-k chunk of a 128-row operand tile is eight 16-row MFMA fragments; each
-// lands lane-linear as 1 KiB (lane l: row l & 15, k bytes 16 (l >> 4) ..), which
-// is exactly the v_mfma_i32_16x16x64_i8 operand layout, so the fragment reads
-// are contiguous ds_read_b128 (conflict-free) and no swizzle is needed. NBUF
-// LDS buffers of 16 KiB (A then B); wave w stages fragments 2w, 2w + 1 of both
-// operands. Chunk c + NBUF - 1 is issued while chunk c is multiplied; the one
-// barrier per chunk (its vmcnt(0) retires this wave's DMA of chunk c) also
-// orders the re-use of the buffer read one chunk earlier.
-template <int NBUF>
-__device__ __forceinline__ void crt_gemm_tile_dma(const uint8_t* __restrict__ Ar, const uint8_t* __restrict__ Br,
-                                                  uint32_t astride, uint32_t bstride, uint32_t kpad,
-                                                  uint32_t nblk, uint32_t tile, uint8_t* __restrict__ R,
-                                                  uint32_t bi, uint32_t bj, int mod, uint8_t* __restrict__ S,
-                                                  uint64_t& tp1, uint64_t& tp2) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t wr = wave >> 1, wc = wave & 1;
-    const uint32_t kcn = kpad / 64;
-    const uint8_t* Ap = Ar + ((uint64_t)mod * astride + bi * CT) * kpad;
-    const uint8_t* Bp = Br + ((uint64_t)mod * bstride + bj * CT) * kpad;
-    // this lane's source bytes of fragment f = 2 wave + h: row 16 f + (lane & 15), k part lane >> 4
-    const uint64_t lo0 = (uint64_t)(32 * wave + (lane & 15)) * kpad + (lane >> 4) * 16;
-    const uint64_t lo1 = lo0 + 16ull * kpad;
-    constexpr uint32_t BUF = 2 * CT * 64;                       // 16 KiB per chunk (A, B)
-    auto issue = [&](uint32_t c) {
-        uint8_t* d = S + (c % NBUF) * BUF + wave * 2048;
-        const uint64_t ko = (uint64_t)c * 64;
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(Ap + lo0 + ko),
-                                         (void __attribute__((address_space(3)))*)(d), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(Ap + lo1 + ko),
-                                         (void __attribute__((address_space(3)))*)(d + 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(Bp + lo0 + ko),
-                                         (void __attribute__((address_space(3)))*)(d + BUF / 2), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(Bp + lo1 + ko),
-                                         (void __attribute__((address_space(3)))*)(d + BUF / 2 + 1024), 16, 0, 0);
-    };
-    v4i acc[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = v4i{0, 0, 0, 0};
-#pragma unroll
-    for (int c = 0; c < NBUF - 1; ++c)
-        if ((uint32_t)c < kcn) issue(c);
-    for (uint32_t c = 0; c < kcn; ++c) {
-        if constexpr (NBUF == 2) {
-            __syncthreads();                              // chunk c landed; buffer (c - 1) % NBUF free
-        } else {
-            // chunks c + 1 .. c + NBUF - 2 stay in flight across the barrier
-            // (a __syncthreads() would wait for them too: vmcnt(0))
-            if (c + NBUF - 2 < kcn)
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * (NBUF - 2)) : "memory");
-            else
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-        }
-        if (c == 0) tp1 = wall_clock64();
-        if (c + NBUF - 1 < kcn) issue(c + NBUF - 1);
-        const uint8_t* Ac = S + (c % NBUF) * BUF;
-        const uint8_t* Bc = Ac + BUF / 2;
-        v4i af[4], bf[4];
-#pragma unroll
-        for (int a = 0; a < 4; ++a) af[a] = *reinterpret_cast<const v4i*>(Ac + (wr * 4 + a) * 1024 + lane * 16);
-#pragma unroll
-        for (int b = 0; b < 4; ++b) bf[b] = *reinterpret_cast<const v4i*>(Bc + (wc * 4 + b) * 1024 + lane * 16);
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
-    }
-    tp2 = wall_clock64();
     crt_store_residues(acc, R, nblk, tile, mod);
 }
+
 
 // Debug timeline of the GEMM's blocks (svdw_debug_trace): per real block its
 // start and end on the 100 MHz wall clock and (XCC id << 16 | HW_ID).
@@ -1842,64 +1716,8 @@ __device__ __forceinline__ void crt_tile_rc(const CrtJob& q, uint32_t t, uint32_
 // planes through its own L2 while it computes that modulus's tiles, instead of
 // every XCD reading strips of every plane. Blocks past the units exit at once
 // (the grid is sized for n = kCrtMaxMod).
-__global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
-    __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes()];
-    const uint64_t t0 = wall_clock64();
-    uint32_t cnt[kMaxCrtJobs], total = 0;
-#pragma unroll
-    for (int j = 0; j < kMaxCrtJobs; ++j) {
-        cnt[j] = 0;
-        if ((uint32_t)j < b.njobs)
-            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk;
-        total += cnt[j];
-    }
-    const uint32_t per = (total + 7) / 8, k = blockIdx.x >> 3;
-    if (k >= per) return;
-    uint32_t u = (blockIdx.x & 7) * per + k;
-    if (u >= total) return;
-    uint32_t j = 0;
-#pragma unroll
-    for (int q = 0; q < kMaxCrtJobs - 1; ++q)
-        if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
-    const CrtJob& q = b.job[j];
-    const uint32_t mod = u / q.nblk, t = u - mod * q.nblk;
-    uint32_t bi, bj;
-    crt_tile_rc(q, t, &bi, &bj);
-    uint64_t tp1 = 0, tp2 = 0;
-    crt_gemm_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.nblk, t,
-                  q.R, bi, bj, (int)mod, S, tp1, tp2);
-    trace_block(t0, tp1, tp2);
-}
-__global__ __launch_bounds__(256) void k_gemm_crt_fe(const CrtBatch b) {
-    __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes()];
-    const uint64_t t0 = wall_clock64();
-    uint32_t cnt[kMaxCrtJobs], total = 0;
-#pragma unroll
-    for (int j = 0; j < kMaxCrtJobs; ++j) {
-        cnt[j] = 0;
-        if ((uint32_t)j < b.njobs)
-            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * b.job[j].nblk;
-        total += cnt[j];
-    }
-    const uint32_t per = (total + 7) / 8, k = blockIdx.x >> 3;
-    if (k >= per) return;
-    uint32_t u = (blockIdx.x & 7) * per + k;
-    if (u >= total) return;
-    uint32_t j = 0;
-#pragma unroll
-    for (int q = 0; q < kMaxCrtJobs - 1; ++q)
-        if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
-    const CrtJob& q = b.job[j];
-    const uint32_t mod = u / q.nblk, t = u - mod * q.nblk;
-    uint32_t bi, bj;
-    crt_tile_rc(q, t, &bi, &bj);
-    uint64_t tp1 = 0, tp2 = 0;
-    crt_gemm_tile<true>(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.nblk, t,
-                        q.R, bi, bj, (int)mod, S, tp1, tp2);
-    trace_block(t0, tp1, tp2);
-}
 // (job, modulus, tile) unit u of the batch in the XCD-modulus-major order of
-// k_gemm_crt_multi; false for blocks past the units
+// the GEMM kernels; false for blocks past the units
 __device__ __forceinline__ bool crt_unit(const CrtBatch& b, uint32_t blk, uint32_t* jo, uint32_t* mo,
                                          uint32_t* to) {
     uint32_t cnt[kMaxCrtJobs], total = 0;
@@ -1923,9 +1741,8 @@ __device__ __forceinline__ bool crt_unit(const CrtBatch& b, uint32_t blk, uint32
     *to = u - *mo * b.job[j].nblk;
     return true;
 }
-template <int NBUF>
-__global__ __launch_bounds__(256) void k_gemm_crt_dma(const CrtBatch b) {
-    __shared__ __attribute__((aligned(16))) uint8_t S[NBUF * 2 * CT * 64];
+__global__ __launch_bounds__(256) void k_gemm_crt_multi(const CrtBatch b) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[crt_lds_bytes()];
     const uint64_t t0 = wall_clock64();
     uint32_t j, mod, t;
     if (!crt_unit(b, blockIdx.x, &j, &mod, &t)) return;
@@ -1933,11 +1750,10 @@ __global__ __launch_bounds__(256) void k_gemm_crt_dma(const CrtBatch b) {
     uint32_t bi, bj;
     crt_tile_rc(q, t, &bi, &bj);
     uint64_t tp1 = 0, tp2 = 0;
-    crt_gemm_tile_dma<NBUF>(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad,
-                            q.nblk, t, q.R, bi, bj, (int)mod, S, tp1, tp2);
+    crt_gemm_tile(q.Ar, q.sym ? q.Ar : q.Br, q.astride, q.sym ? q.astride : q.bstride, q.kpad, q.nblk, t,
+                  q.R, bi, bj, (int)mod, S, tp1, tp2);
     trace_block(t0, tp1, tp2);
 }
-
 // persistent CRT GEMM blocks per XCD label: two per CU (32 CUs per XCD)
 static constexpr uint32_t kCrtPersPerXcd = 64;
 // Operand row-tile bases and output place of one (job, modulus, tile) unit.
@@ -2196,22 +2012,15 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
     const hipError_t pe = prep_crt_batch(b, units, cblocks);
     if (pe != hipSuccess) return pe;
     const dim3 grid((units + 7) / 8 * 8);
-    switch (b.kern) {
-    case 0: hipLaunchKernelGGL(k_gemm_crt_multi, grid, dim3(256), 0, st, b); break;
-    case 1: hipLaunchKernelGGL(k_gemm_crt_fe, grid, dim3(256), 0, st, b); break;
-    case 2: hipLaunchKernelGGL(k_gemm_crt_dma<3>, grid, dim3(256), 0, st, b); break;
-    case 3: hipLaunchKernelGGL(k_gemm_crt_dma<4>, grid, dim3(256), 0, st, b); break;
-    case 4: {
-        // persistent: one kpad of >= 8 chunks for every job, else the per-unit kernel
-        bool ok = b.job[0].kpad >= 512;
-        for (uint32_t j = 1; j < b.njobs; ++j) ok = ok && b.job[j].kpad == b.job[0].kpad;
-        const uint32_t pg = std::min<uint32_t>((units + 7) / 8 * 8, 8 * kCrtPersPerXcd);
-        if (ok) hipLaunchKernelGGL(k_gemm_crt_pers, dim3(pg), dim3(256), 0, st, b);
-        else hipLaunchKernelGGL(k_gemm_crt_fe, grid, dim3(256), 0, st, b);
-        break;
-    }
-    default: return hipErrorInvalidValue;
-    }
+    // persistent: one kpad of >= 8 chunks for every job, else the per-unit kernel
+    bool pers = b.kern == 1 && b.job[0].kpad >= 512;
+    for (uint32_t j = 1; j < b.njobs; ++j) pers = pers && b.job[j].kpad == b.job[0].kpad;
+    if (b.kern > 1) return hipErrorInvalidValue;
+    if (pers)
+        hipLaunchKernelGGL(k_gemm_crt_pers, dim3(std::min<uint32_t>(grid.x, 8 * kCrtPersPerXcd)), dim3(256), 0,
+                           st, b);
+    else
+        hipLaunchKernelGGL(k_gemm_crt_multi, grid, dim3(256), 0, st, b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_crt_combine_multi, dim3((cblocks + 7) / 8 * 8), dim3(256), 0, st, b, cblocks);
@@ -2899,12 +2708,6 @@ __global__ __launch_bounds__(256) void k_matvec_scan_dpp(const ScanBatch B) {
     const Fr* __restrict__ wm = tab_slot(J.tab, J.tl, na);
     const Fr* __restrict__ wn = wm + J.tl;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    switch (B.prio) {                                   // (uniform; an immediate operand)
-    case 1: __builtin_amdgcn_s_setprio(1); break;
-    case 2: __builtin_amdgcn_s_setprio(2); break;
-    case 3: __builtin_amdgcn_s_setprio(3); break;
-    default: break;
-    }
     const uint32_t lb = blockIdx.x - J.blk0;
     const uint32_t rb = (J.blk0 & 7) ? lb : scan_row(lb, J.rows), r = J.r_begin + rb;
     Fr* rowout = J.out + (uint64_t)rb * (3ull * L + 1);

@@ -56,7 +56,6 @@ struct ScanBatch {
     uint32_t njobs;
     const unsigned* bitw;     // device bit-length words of the NaSpecs (na = 0 launches)
     ScaleTab f;               // slot factors for the pc / ptab epilogue
-    uint32_t prio;            // s_setprio of the scan waves (0-3; "scan_prio")
 };
 // gamma powers from host-side Montgomery tables: g^j = t[j & 15] t[16 + (j >> 4 & 15)]
 // t[32 + (j >> 8)] (j < 256 * nhi)
@@ -351,10 +350,9 @@ struct CrtJob {
 struct CrtBatch {
     CrtJob job[kMaxCrtJobs];
     uint32_t njobs;
-    // GEMM kernel (bit-identical; round-6 A/B): 0 register-staged chunks,
-    // 1 the same with the five-operation residue epilogue, 2 / 3 LDS-DMA
-    // staging with 3 / 4 chunk buffers, 4 kernel 1 on a persistent grid
-    // (k_gemm_crt_pers: one block's chunk pipeline runs across its units)
+    // GEMM kernel (bit-identical): 0 one block per (tile, modulus) unit
+    // (k_gemm_crt_multi), 1 a persistent grid whose blocks' chunk pipelines
+    // run across their units (k_gemm_crt_pers; jobs of one kpad >= 512)
     uint32_t kern;
 };
 // R sized crt_scratch_bytes per job

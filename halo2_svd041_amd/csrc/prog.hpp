@@ -66,7 +66,6 @@ struct SlotOp {
 static constexpr uint8_t KSRC = 0x80;
 
 static constexpr uint32_t STAGE_ALIGN = 256;     // 4 KiB-aligned block store windows
-static constexpr uint32_t STAGE_XCD = 512;       // XCD-contiguous block order ("stage_xcd")
 
 static constexpr int kMaxViews = 2;
 static constexpr int kMaxMicro = 16;
@@ -110,7 +109,7 @@ struct StageMulti {
     uint32_t nprog;
     uint32_t blk0[kMaxMulti + 1];
     uint32_t off[kMaxMulti];
-    uint32_t xcd;             // XCD-contiguous block order (grid a multiple of 8)
+    uint32_t _pad;
     alignas(8) uint8_t data[kMultiBytes];
 };
 static_assert(sizeof(StageMulti) < 4096, "kernel argument block too large");

@@ -1,6 +1,6 @@
-// Standalone timing of the CRT GEMM kernels (round 6): the shipped
-// register-staged k_gemm_crt_multi against the LDS-DMA variants
-// k_gemm_crt_dma<NBUF>, on random balanced residue planes shaped like the
+// Standalone timing of the CRT GEMM kernels (round 6): the per-unit
+// k_gemm_crt_multi against the persistent k_gemm_crt_pers, on random balanced
+// residue planes shaped like the
 // 1024^2 P=63 witness (m.v^T: 19 moduli; u.u^T and v.v^T symmetric: 18), alone
 // and as the step's three-job batch. Every variant's residue bytes are compared
 // with the shipped kernel's.
@@ -37,17 +37,13 @@ __global__ __launch_bounds__(256) void k_standin(uint4* __restrict__ out, size_t
     }
 }
 
-static constexpr int NV = 6;
-static const char* vname[NV] = {"shipped(reg)", "dma2", "dma3", "dma4", "reg+fastepi", "persistent"};
+// (round 6 also measured LDS-DMA staging with 2-4 chunk buffers and the
+// per-unit kernel with the old fp32-quotient epilogue: profiles/r06_ab/r6c)
+static constexpr int NV = 2;
+static const char* vname[NV] = {"per-unit", "persistent"};
 static void launch_variant(int v, dim3 g, hipStream_t st, const CrtBatch& b) {
-    switch (v) {
-    case 0: hipLaunchKernelGGL(k_gemm_crt_multi, g, dim3(256), 0, st, b); break;
-    case 1: hipLaunchKernelGGL(k_gemm_crt_dma<2>, g, dim3(256), 0, st, b); break;
-    case 2: hipLaunchKernelGGL(k_gemm_crt_dma<3>, g, dim3(256), 0, st, b); break;
-    case 3: hipLaunchKernelGGL(k_gemm_crt_dma<4>, g, dim3(256), 0, st, b); break;
-    case 4: hipLaunchKernelGGL(k_gemm_crt_fe, g, dim3(256), 0, st, b); break;
-    default: hipLaunchKernelGGL(k_gemm_crt_pers, dim3(std::min<uint32_t>(g.x, 8 * kCrtPersPerXcd)), dim3(256), 0, st, b); break;
-    }
+    if (v == 0) hipLaunchKernelGGL(k_gemm_crt_multi, g, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL(k_gemm_crt_pers, dim3(std::min<uint32_t>(g.x, 8 * kCrtPersPerXcd)), dim3(256), 0, st, b);
 }
 
 __global__ void k_nmod(const unsigned* W, uint32_t lk, int* out) { *out = crt_nmod(W[0], W[1], lk); }
@@ -111,7 +107,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (const Case& cs : cases) {
-        double best[NV] = {1e9, 1e9, 1e9, 1e9, 1e9, 1e9};
+        double best[NV] = {1e9, 1e9};
         for (int round = 0; round < (quick ? 1 : 3); ++round)
             for (int v = 0; v < NV; ++v) {
                 CrtBatch b;
