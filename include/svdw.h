@@ -263,7 +263,7 @@ int svdw_verify_mul_witness_on(svdw_ctx* ctx, void* stream, const double* a, con
 #define SVDW_GEMM_MFMA 0
 #define SVDW_GEMM_VALU 1
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
-/* Options (svdw_set_option; 18 names; any other name is SVDW_EINVAL). Tuning
+/* Options (svdw_set_option; 21 names; any other name is SVDW_EINVAL). Tuning
  * knobs, bit-identical results
  * for every value, defaults first:
  *   "gemm_impl" 0 | 1; "gemm_crt" 1 | 0 (CRT or digit-plane matrix-core GEMM);
@@ -315,7 +315,19 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   -1: the third on a row-sharded rank, else the cell stream); the d checks
  *   on the cell stream behind the products (0), on the second stream with the
  *   bounds and u.d (1) or on the third ahead of phase 1 (2)); "vm_linear" 1 | 0 (the captured sequence is queued on the context
- *   stream alone, a linear graph, instead of forking to the second stream).
+ *   stream alone, a linear graph, instead of forking to the second stream);
+ *   "gemm_kern" -1 | 0 | 1 (CRT GEMM: 0 one block per (128 x 128 tile,
+ *   modulus) unit, 1 a persistent grid whose blocks' chunk pipelines run on
+ *   across their units (jobs of one K >= 512); -1: 1 for a product queued on its
+ *   own (svdw_honest_prover_mat_mul), 0 inside the witness calls);
+ *   "res_wait" -1 | 0 | 1 (pipelined svd_witness reading its loads from the f64
+ *   inputs: the second stream's stages wait for the residue planes (1) or not
+ *   (0); -1: 1 on a row-sharded context, else 0);
+ *   "st2_defer" -1 | 0 | 1 (pipelined svd_witness: the diff and ids, a call's
+ *   last launch on the second stream, go out in one launch with the next call's
+ *   bounds and u.d (1) or on their own (0); -1: 1 unless row-sharded; held-back
+ *   work is launched by svdw_sync / svdw_query / svdw_stream_signal and by any
+ *   other call on the context).
  * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:
  *   phase 1 starts with the two ctx_gate constant cells [1, 0] that
  *   examples/svd_example.rs:183's rlc.load_rlc_cache(.., 1) appends as recalled
