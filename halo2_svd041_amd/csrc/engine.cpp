@@ -612,19 +612,6 @@ struct svdw_ctx {
         size_t last = 0;                   // group of the latest stage
     };
     std::vector<Batch> batches;
-    // "st2_defer" (-1: on unsharded contexts): a pipelined witness's last stage
-    // launch on st2 (the diff and the two ids, waiting for its products) is held
-    // back and goes out in one k_stage_multi launch with the next witness's
-    // first st2 batch (the bounds and u.d, which need nothing), so st2 runs one
-    // launch per witness: one launch boundary and one block tail fewer. Its st2
-    // tail event is recorded behind that launch; anything else that touches the
-    // context launches it first (flush_deferred).
-    int st2_defer = -1;
-    struct Deferred {
-        bool on = false;
-        int par = 0;                        // the parity of the call it belongs to
-        std::vector<std::vector<Pending>> groups;
-    } dfr;
     bool stage_batch = true;
     bool stage_front = false;               // stage_launch: the stage goes ahead of the batch's groups
     // device ingest (svdw_parse_svd_input_device) scratch
@@ -671,7 +658,6 @@ struct svdw_ctx {
 };
 
 static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter = nullptr, hipEvent_t then_wait = nullptr);
-static void flush_deferred(svdw_ctx* c, std::vector<svdw_ctx::Pending>* with = nullptr);
 // debug logs (read once: getenv scans the environment)
 static bool env_flag(const char* name) { const char* v = getenv(name); return v && *v && *v != '0'; }
 static const bool g_batch_log = env_flag("SVDW_BATCH_LOG");
@@ -679,7 +665,6 @@ static const bool g_stage_log = env_flag("SVDW_STAGE_LOG");
 static void sync(svdw_ctx* c) {
     if (c->dry) return;
     REQUIRE(!c->capturing, "internal: synchronisation during graph capture");
-    flush_deferred(c);
     hipck(hipStreamSynchronize(c->st), "hipStreamSynchronize");
     hipck(hipStreamSynchronize(c->st2), "hipStreamSynchronize");
     if (c->st3) hipck(hipStreamSynchronize(c->st3), "hipStreamSynchronize");
@@ -689,9 +674,7 @@ static void sync(svdw_ctx* c) {
 // After a pipelined svd_witness its tail (st2, st3) is not joined into st:
 // anything else queued on the context waits for it first.
 static void settle(svdw_ctx* c) {
-    if (c->dry || c->in_pipe) return;
-    flush_deferred(c);
-    if (!c->tail_pending) return;
+    if (c->dry || !c->tail_pending || c->in_pipe) return;
     for (int k = 0; k < 2; ++k)
         hipck(hipStreamWaitEvent(c->st, c->tail_ev[c->tail_last][k], 0), "hipStreamWaitEvent");
     c->tail_pending = false;
@@ -897,7 +880,6 @@ static void bits_words(svdw_ctx* c, QuantSegs& qs, uint32_t nred, const BitSegs&
 }
 static void grow(svdw_ctx* c, Fr*& ptr, uint64_t used, uint64_t& cap, uint64_t need) {
     if (c->dry || need <= cap) return;
-    flush_deferred(c);                      // (its stages may write this buffer)
     REQUIRE(!c->capturing, "internal: allocation during graph capture");
     ++c->epoch;
     uint64_t ncap = std::max(need, cap + cap / 2);
@@ -1116,23 +1098,6 @@ static void stage_launch(svdw_ctx* c, uint32_t phase, PB& pb, uint32_t nelem, ui
 // (it needs that stage and what came before on s, not the later groups: those
 // hold stages queued earlier that depend on other pending ones).
 // then_wait: s waits for this event before the groups after that point.
-static void launch_group(svdw_ctx* c, hipStream_t s, const std::vector<svdw_ctx::Pending>& grp) {
-    if (grp.empty()) return;
-    std::vector<const StageArgs*> ps;
-    double bytes = 0;
-    for (const auto& q : grp) {
-        ps.push_back(&q.a);
-        bytes += q.bytes;
-    }
-    const std::string name = grp.size() == 1 ? grp[0].name : "k_stage:multi";
-    if (g_batch_log) {
-        fprintf(stderr, "batch stream %p group:", (void*)s);
-        for (const auto& q : grp) fprintf(stderr, " %s", q.name.c_str());
-        fprintf(stderr, "\n");
-    }
-    ProfScope pr(c, s, name, bytes, 0, true, true);
-    hipck(launch_stage_multi(ps.data(), (int)ps.size(), s), "k_stage_multi");
-}
 static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter, hipEvent_t then_wait) {
     for (auto& b : c->batches) {
         if (b.st != s || b.groups.empty()) continue;
@@ -1140,32 +1105,31 @@ static void flush_batch(svdw_ctx* c, hipStream_t s, hipStream_t waiter, hipEvent
         groups.swap(b.groups);               // (cleared before launching: no re-entry)
         const size_t upto = b.last;
         for (size_t gi = 0; gi < groups.size(); ++gi) {
+            const auto& grp = groups[gi];
             if (gi == upto + 1 && waiter) {
                 stream_dep(c, s, waiter);
                 waiter = nullptr;
                 if (then_wait) dep_wait(c, s, then_wait);
             }
-            launch_group(c, s, groups[gi]);
+            if (grp.empty()) continue;
+            std::vector<const StageArgs*> ps;
+            double bytes = 0;
+            for (const auto& q : grp) {
+                ps.push_back(&q.a);
+                bytes += q.bytes;
+            }
+            const std::string name = grp.size() == 1 ? grp[0].name : "k_stage:multi";
+            if (g_batch_log) {
+                fprintf(stderr, "batch stream %p group %zu/%zu (last %zu):", (void*)s, gi, groups.size(), upto);
+                for (const auto& q : grp) fprintf(stderr, " %s", q.name.c_str());
+                fprintf(stderr, "\n");
+            }
+            ProfScope pr(c, s, name, bytes, 0, true, true);
+            hipck(launch_stage_multi(ps.data(), (int)ps.size(), s), "k_stage_multi");
         }
     }
     if (waiter) stream_dep(c, s, waiter);
 }
-// The held-back st2 launch of a pipelined witness (st2_defer), with `with`
-// (the next witness's first st2 group; may be null) in the same launch, then
-// that witness's st2 tail event.
-static void flush_deferred(svdw_ctx* c, std::vector<svdw_ctx::Pending>* with) {
-    if (!c->dfr.on) return;
-    c->dfr.on = false;
-    std::vector<std::vector<svdw_ctx::Pending>> groups;
-    groups.swap(c->dfr.groups);
-    if (with && !groups.empty()) {
-        groups.back().insert(groups.back().end(), with->begin(), with->end());
-        with->clear();
-    }
-    for (const auto& g : groups) launch_group(c, c->st2, g);
-    hipck(hipEventRecord(c->tail_ev[c->dfr.par][0], c->st2), "hipEventRecord");
-}
-static bool st2_defer_on(const svdw_ctx* c) { return c->st2_defer >= 0 ? c->st2_defer != 0 : !sharded(c); }
 // RAII: stage launches on the current stream between construction and end()
 // are batched (k_stage_multi); nested scopes on the same stream join the outer
 // one. Without end() (an exception) the pending stages are dropped.
@@ -2607,16 +2571,6 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
         // the cell stream waits for u.d (and what precedes it on st2), not for
         // the d checks' dependent second group batched behind it; pipelined,
         // the diff is on st2 itself and st carries the next call: no wait
-        if (c->dfr.on && c->in_pipe) {
-            // the previous witness's held-back diff and ids go out in one
-            // launch with this witness's bounds and u.d (st2_defer)
-            for (auto& b : c->batches)
-                if (b.st == c->st2 && b.groups.size() == 1) {
-                    flush_deferred(c, &b.groups[0]);
-                    b.groups.clear();
-                }
-            flush_deferred(c);                        // (other batch shapes: on its own)
-        }
         flush_batch(c, c->st2, c->in_pipe ? nullptr : c->st);
     }
     if (batched) {
@@ -2649,17 +2603,6 @@ static svdw_svd_payload check_svd_phase0(svdw_ctx* c, const svdw_mat& m, const s
     check_mat_id(c, uut, q2, eu, &qq);
     svdw_mat vvt = honest_prover_mat_mul(c, m.phase, v, vt, bv, bv);
     check_mat_id(c, vvt, q2, eu, &qq);
-    if (dst2 && !c->dry && st2_defer_on(c)) {
-        // the diff and ids (with the constant cell batched beside them) are
-        // held back until the next witness's first st2 launch (st2_defer)
-        for (auto& b : c->batches)
-            if (b.st == c->st && !b.groups.empty()) {
-                REQUIRE(!c->dfr.on, "internal: st2 launch already held back");
-                c->dfr.groups.swap(b.groups);
-                c->dfr.on = true;
-                c->dfr.par = c->pipe_par;
-            }
-    }
     bs2.end();
     if (dst2) std::swap(c->st, c->st2);
     aside.end();
@@ -2706,7 +2649,6 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         ~PipeGuard() {
             if (!c->in_pipe) return;
             const int par = c->pipe_par;
-            try { flush_deferred(c); } catch (...) {}
             (void)hipEventRecord(c->tail_ev[par][0], c->st2);
             (void)hipEventRecord(c->tail_ev[par][1], c->st3);
             c->tail_valid[par] = true;
@@ -2969,10 +2911,9 @@ static svdw_counts svd_witness(svdw_ctx* c, const double* m, const double* u, co
         // no join into st: the next call's product chain starts on st while this
         // call's stages (st2) and row scans (st3) finish; they end at tail_ev
         const int par = c->pipe_par;
-        if (c->dfr.on && c->dfr.par != par) flush_deferred(c);   // (an earlier call's, not merged)
         flush_batch(c, c->st2);
         flush_batch(c, c->st3);
-        if (!c->dfr.on) hipck(hipEventRecord(c->tail_ev[par][0], c->st2), "hipEventRecord");
+        hipck(hipEventRecord(c->tail_ev[par][0], c->st2), "hipEventRecord");
         hipck(hipEventRecord(c->tail_ev[par][1], c->st3), "hipEventRecord");
         c->tail_valid[par] = true;
         c->tail_pending = true;
@@ -3305,17 +3246,17 @@ static void ctx_init_device(svdw_ctx* c) {
 // The settings (options, shard, profiler) of `s` onto the lane `d`; a change
 // bumps the lane's epoch (its captured graph no longer applies).
 static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
-    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->gemm_crt, s->gemm_kern, s->res_wait, s->st2_defer, s->res_f64,
+    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->gemm_crt, s->gemm_kern, s->res_wait, s->res_f64,
                          s->phase1_overlap, s->prod_cell, s->hold_us, s->rlc_prefix, s->p1_at, s->dchk_at, s->gamma_at,
                          s->f64_views, s->overlap, s->stage_batch, s->graph_vm, s->vm_linear, s->pipeline,
                          s->shard_rank, s->shard_world, s->prof, s->host_trace};
-    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->gemm_crt, d->gemm_kern, d->res_wait, d->st2_defer, d->res_f64,
+    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->gemm_crt, d->gemm_kern, d->res_wait, d->res_f64,
                          d->phase1_overlap, d->prod_cell, d->hold_us, d->rlc_prefix, d->p1_at, d->dchk_at, d->gamma_at,
                          d->f64_views, d->overlap, d->stage_batch, d->graph_vm, d->vm_linear, d->pipeline,
                          d->shard_rank, d->shard_world, d->prof, d->host_trace};
     if (!memcmp(a, b, sizeof a) && d->prof_filter == s->prof_filter) return;
     d->gemm_impl = s->gemm_impl; d->stage_flags = s->stage_flags; d->stage_elems = s->stage_elems;
-    d->gemm_crt = s->gemm_crt; d->gemm_kern = s->gemm_kern; d->res_wait = s->res_wait; d->st2_defer = s->st2_defer; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
+    d->gemm_crt = s->gemm_crt; d->gemm_kern = s->gemm_kern; d->res_wait = s->res_wait; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
     d->prod_cell = s->prod_cell; d->hold_us = s->hold_us; d->rlc_prefix = s->rlc_prefix;
     d->p1_at = s->p1_at; d->f64_views = s->f64_views; d->overlap = s->overlap;
     d->dchk_at = s->dchk_at; d->gamma_at = s->gamma_at;
@@ -3703,7 +3644,6 @@ int svdw_stream_signal(svdw_ctx* c, void* stream) {
         const hipStream_t s = (hipStream_t)stream;
         for (svdw_ctx* x : {c, c->lane}) {
             if (!x) continue;
-            flush_deferred(x);
             int i = 1;
             for (hipStream_t t : {x->st, x->st2, x->st3}) {
                 if (!t) continue;
@@ -3730,7 +3670,6 @@ int svdw_query(svdw_ctx* c) {
         if (c->dry) return;
         for (svdw_ctx* x : {c, c->lane}) {
             if (!x) continue;
-            flush_deferred(x);                      // (held back: not queued yet)
             for (hipStream_t t : {x->st, x->st2, x->st3}) {
                 if (!t) continue;
                 const hipError_t e = hipStreamQuery(t);
@@ -4657,9 +4596,6 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "gemm_crt") {
             REQUIRE(value == 0 || value == 1, "gemm_crt: 0 or 1");
             c->gemm_crt = (int)value;
-        } else if (n == "st2_defer") {               // pipelined: diff + ids with the next bounds
-            REQUIRE(value >= -1 && value <= 1, "st2_defer: -1 (auto), 0 or 1");
-            c->st2_defer = (int)value;
         } else if (n == "res_wait") {                // pipelined: st2 waits for the residue planes
             REQUIRE(value >= -1 && value <= 1, "res_wait: -1 (auto), 0 or 1");
             c->res_wait = (int)value;

@@ -263,7 +263,7 @@ int svdw_verify_mul_witness_on(svdw_ctx* ctx, void* stream, const double* a, con
 #define SVDW_GEMM_MFMA 0
 #define SVDW_GEMM_VALU 1
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
-/* Options (svdw_set_option; 21 names; any other name is SVDW_EINVAL). Tuning
+/* Options (svdw_set_option; 20 names; any other name is SVDW_EINVAL). Tuning
  * knobs, bit-identical results
  * for every value, defaults first:
  *   "gemm_impl" 0 | 1; "gemm_crt" 1 | 0 (CRT or digit-plane matrix-core GEMM);
@@ -322,12 +322,7 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   own (svdw_honest_prover_mat_mul), 0 inside the witness calls);
  *   "res_wait" -1 | 0 | 1 (pipelined svd_witness reading its loads from the f64
  *   inputs: the second stream's stages wait for the residue planes (1) or not
- *   (0); -1: 1 on a row-sharded context, else 0);
- *   "st2_defer" -1 | 0 | 1 (pipelined svd_witness: the diff and ids, a call's
- *   last launch on the second stream, go out in one launch with the next call's
- *   bounds and u.d (1) or on their own (0); -1: 1 unless row-sharded; held-back
- *   work is launched by svdw_sync / svdw_query / svdw_stream_signal and by any
- *   other call on the context).
+ *   (0); -1: 1 on a row-sharded context, else 0).
  * Layout option (changes the phase-1 stream): "rlc_prefix" 0 | 1 (svd_witness:
  *   phase 1 starts with the two ctx_gate constant cells [1, 0] that
  *   examples/svd_example.rs:183's rlc.load_rlc_cache(.., 1) appends as recalled
