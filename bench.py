@@ -338,7 +338,7 @@ class VerifyMulWorkload:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=None,
                     help="untimed steps (default 3; verify_mul 8: each of its two lanes "
                          "captures its launch graph on its second or third call)")

@@ -118,6 +118,9 @@ SIGNATURES = {
     "svdw_reserve": (_i32, [_P, _u32, _u64, _u64]),
     "svdw_sync": (_i32, [_P]),
     "svdw_query": (_i32, [_P]),
+    "svdw_mark": (_i32, [_P, ct.POINTER(ct.c_uint64)]),
+    "svdw_mark_done": (_i32, [_P, _u64]),
+    "svdw_mark_wait": (_i32, [_P, _u64]),
     "svdw_stream_wait": (_i32, [_P, _P]),
     "svdw_stream_signal": (_i32, [_P, _P]),
     "svdw_debug_trace": (_i32, [_P]),

@@ -565,6 +565,13 @@ struct svdw_ctx {
     hipStream_t st3 = nullptr;
     hipStream_t st_cell = nullptr;          // the cell stream proper (st is swapped at times)
     hipEvent_t xev[4] = {};                 // svdw_stream_wait / _signal (caller's stream)
+    // svdw_mark ring: slot k holds ticket mk_t[k]'s events (one per stream of
+    // both lanes), recorded on the context's own streams (no waits)
+    static constexpr int kMarks = 16;
+    hipEvent_t mk_ev[kMarks][6] = {};
+    uint64_t mk_t[kMarks] = {};
+    uint8_t mk_used[kMarks] = {};
+    uint64_t mk_seq = 0;
     bool overlap = true;
     struct PreGemm {
         uint64_t off;
@@ -3203,6 +3210,9 @@ static void ctx_release(svdw_ctx* c) {
         if (c->ev_bits) (void)hipEventDestroy(c->ev_bits);
         for (auto e : c->xev)
             if (e) (void)hipEventDestroy(e);
+        for (auto& m : c->mk_ev)
+            for (auto e : m)
+                if (e) (void)hipEventDestroy(e);
         for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
         for (auto e : c->pool) (void)hipEventDestroy(e);
         for (auto e : c->deps) (void)hipEventDestroy(e);
@@ -3682,6 +3692,65 @@ int svdw_query(svdw_ctx* c) {
         }
     });
     return rc ? rc : done;
+}
+// Completion marks (svdw_mark / svdw_mark_done / svdw_mark_wait): an event on
+// each stream of both lanes, recorded behind what is queued there (pending
+// batched stages launched first), so no stream waits for anything. A slot is
+// reused 16 marks later; a ticket whose slot holds a later mark is answered
+// by that mark (later done implies earlier done; not done reads as 0).
+int svdw_mark(svdw_ctx* c, uint64_t* ticket) {
+    return guarded([&] {
+        REQUIRE(c && ticket, "null argument");
+        const uint64_t t = ++c->mk_seq;
+        *ticket = t;
+        if (c->dry) return;
+        const int k = (int)(t % svdw_ctx::kMarks);
+        int i = 0;
+        for (svdw_ctx* x : {c, c->lane}) {
+            if (!x) continue;
+            for (hipStream_t st : {x->st, x->st2, x->st3}) {
+                if (!st) continue;
+                flush_batch(x, st);
+                hipEvent_t& e = c->mk_ev[k][i++];
+                if (!e) hipck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+                hipck(hipEventRecord(e, st), "hipEventRecord");
+            }
+        }
+        c->mk_used[k] = (uint8_t)i;
+        c->mk_t[k] = t;
+    });
+}
+// the slot answering ticket t, or -1 (t not issued)
+static int mark_slot(const svdw_ctx* c, uint64_t t) {
+    if (!t || t > c->mk_seq) return -1;
+    return (int)(t % svdw_ctx::kMarks);
+}
+int svdw_mark_done(svdw_ctx* c, uint64_t ticket) {
+    int done = 1;
+    const int rc = guarded([&] {
+        REQUIRE(c, "null ctx");
+        const int k = mark_slot(c, ticket);
+        REQUIRE(k >= 0, "svdw_mark_done: ticket not issued");
+        if (c->dry) return;
+        for (int i = 0; i < c->mk_used[k]; ++i) {
+            const hipError_t e = hipEventQuery(c->mk_ev[k][i]);
+            if (e == hipErrorNotReady) {
+                done = 0;
+                return;
+            }
+            hipck(e, "hipEventQuery");
+        }
+    });
+    return rc ? rc : done;
+}
+int svdw_mark_wait(svdw_ctx* c, uint64_t ticket) {
+    return guarded([&] {
+        REQUIRE(c, "null ctx");
+        const int k = mark_slot(c, ticket);
+        REQUIRE(k >= 0, "svdw_mark_wait: ticket not issued");
+        if (c->dry) return;
+        for (int i = 0; i < c->mk_used[k]; ++i) hipck(hipEventSynchronize(c->mk_ev[k][i]), "hipEventSynchronize");
+    });
 }
 uint64_t svdw_advice_len(const svdw_ctx* c, uint32_t phase) { return c && phase < 2 ? c->ph[phase].n : 0; }
 uint64_t svdw_lookup_len(const svdw_ctx* c, uint32_t phase) { return c && phase < 2 ? c->ph[phase].nl : 0; }

@@ -117,24 +117,26 @@ class Context:
         self._h = ct.c_void_p()
         # device input tensors whose reads may still be queued (include/svdw.h,
         # "Lifetime of device inputs"): id -> [tensor, sequence number of the
-        # last call that read it], kept until a checkpoint at or after that call
+        # last call that read it], kept until a completion mark at or after that call
         # has completed, so torch's allocator cannot hand their memory to a
         # tensor written on another stream while a pipelined call still reads it
         self._held = {}
         self._seq = 0
-        self._ckpts = collections.deque()      # (call sequence number, torch event)
-        self._ckpt_stream = None
+        self._ckpts = collections.deque()      # (call sequence number, svdw_mark ticket)
         p = Params(device, precision_bits, lookup_bits)
         check(lib().svdw_ctx_create(ct.byref(p), ct.byref(self._h)))
 
     # Per-call completion, at a cost amortised over calls: every HOLD_EVERY-th
-    # call that holds inputs records a checkpoint (a side stream made to wait for
-    # everything queued on the context, svdw_stream_signal, and an event on it);
-    # a held tensor is released once a checkpoint at or after its last reader has
-    # completed. At most HOLD_CKPTS checkpoints are pending: beyond that the
-    # oldest is waited for. So back-to-back calls on fresh tensors hold the inputs
-    # of at most HOLD_EVERY * (HOLD_CKPTS + 1) calls, whatever the device's
-    # progress, and each call costs one dict update plus an event query.
+    # call that holds inputs records a completion mark (svdw_mark: an event on
+    # each of the context's streams, no waits); a held tensor is released once
+    # a mark at or after its last reader has completed. At most HOLD_CKPTS
+    # marks are pending: beyond that the oldest is waited for. So back-to-back
+    # calls on fresh tensors hold the inputs of at most
+    # HOLD_EVERY * (HOLD_CKPTS + 1) calls, whatever the device's progress, and
+    # each call costs one dict update plus an event query. (The marks replaced
+    # a side stream ordered after the context by svdw_stream_signal: with 4
+    # hardware queues per process that stream shared one with a context stream,
+    # whose next call then waited behind it -- 3.5 % of a 512^2 step.)
     HOLD_EVERY = 8
     HOLD_CKPTS = 4
 
@@ -147,21 +149,25 @@ class Context:
             held[id(t)] = [t, seq]
         ck = self._ckpts
         done = 0
-        while ck and (len(ck) > self.HOLD_CKPTS or ck[0][1].query()):
-            s0, ev = ck.popleft()
-            ev.synchronize()                     # (a no-op unless over HOLD_CKPTS)
+        while ck:
+            s0, ticket = ck[0]
+            if len(ck) > self.HOLD_CKPTS:
+                check(lib().svdw_mark_wait(self._h, ticket))
+            else:
+                rc = lib().svdw_mark_done(self._h, ticket)
+                if rc < 0:
+                    check(rc)
+                if rc != 1:
+                    break
+            ck.popleft()
             done = s0
         if done:
             for k in [k for k, (_, s) in held.items() if s <= done]:
                 del held[k]
         if seq % self.HOLD_EVERY == 0:
-            torch = _torch_mod()
-            if self._ckpt_stream is None:
-                self._ckpt_stream = torch.cuda.Stream(self.device)
-            check(lib().svdw_stream_signal(self._h, self._ckpt_stream.cuda_stream))
-            ev = torch.cuda.Event()
-            ev.record(self._ckpt_stream)
-            ck.append((seq, ev))
+            ticket = ct.c_uint64(0)
+            check(lib().svdw_mark(self._h, ct.byref(ticket)))
+            ck.append((seq, ticket.value))
 
     def _release_all(self) -> None:
         self._held.clear()

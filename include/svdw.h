@@ -103,12 +103,25 @@ int svdw_sync(svdw_ctx* ctx);
  * call's work has completed: svdw_sync(), or svdw_query() returning 1, or any
  * stream ordered after svdw_stream_signal(ctx, stream) (a caching allocator
  * that frees on that stream). The Python layer holds a reference to every
- * device input tensor until svdw_query / sync / reset / close shows the work
- * done. */
+ * device input tensor until a completion mark (svdw_mark, below) after its
+ * call, or sync / reset / close, shows the work done. */
 int svdw_stream_wait(svdw_ctx* ctx, void* stream);
 /* 1 when everything queued on the context (both lanes) has completed, 0 while
  * some of it still runs (no host wait), < 0 on error. */
 int svdw_query(svdw_ctx* ctx);
+/* Completion marks: svdw_mark records how far the context's work is queued
+ * (an event on each of its streams behind what is queued there; no stream
+ * waits) and returns a ticket. svdw_mark_done(ticket) is 1 once everything
+ * queued before the mark has completed, 0 while some of it runs (no host
+ * wait), < 0 on error; svdw_mark_wait(ticket) waits for it on the host. The
+ * last 16 marks are kept; an older ticket is answered by the mark that reused
+ * its slot (done implies done; otherwise 0). (svdw_stream_signal onto a side
+ * stream does the same job, but with 4 hardware queues per process that
+ * stream may share a queue with one of the context's streams, whose later
+ * work then waits behind the side stream's wait.) */
+int svdw_mark(svdw_ctx* ctx, uint64_t* ticket);
+int svdw_mark_done(svdw_ctx* ctx, uint64_t ticket);
+int svdw_mark_wait(svdw_ctx* ctx, uint64_t ticket);
 /* Debug: the CRT GEMM's block timeline into device buffer buf (3 u64 per block:
  * start and end on the 100 MHz wall clock, XCC id << 32 | HW_ID); null: off. */
 int svdw_debug_trace(void* buf);

@@ -149,3 +149,26 @@ def test_removed_options_are_rejected():
         ctx.set_option("pipeline", 0)
     finally:
         ctx.close()
+
+
+def test_completion_marks_dry():
+    """svdw_mark / svdw_mark_done / svdw_mark_wait on the planning context:
+    tickets count up from 1, a dry context's marks are complete at once, and a
+    ticket never issued is an error."""
+    import ctypes as ct
+    L = _lib.lib()
+    ctx = hs.Context(device=-1, precision_bits=63, lookup_bits=19)
+    try:
+        t = ct.c_uint64(0)
+        got = []
+        for _ in range(3):
+            assert L.svdw_mark(ctx.handle, ct.byref(t)) == 0
+            got.append(t.value)
+        assert got == [1, 2, 3]
+        assert L.svdw_mark_done(ctx.handle, 2) == 1
+        assert L.svdw_mark_wait(ctx.handle, 3) == 0
+        assert L.svdw_mark_done(ctx.handle, 0) < 0
+        assert L.svdw_mark_done(ctx.handle, 4) < 0
+        assert b"not issued" in L.svdw_last_error()
+    finally:
+        ctx.close()

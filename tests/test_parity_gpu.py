@@ -690,10 +690,41 @@ def test_gemm_kern_full_streams(gpu_ctx_factory, N, M):
         assert bad.size == 0, f"{name}: {bad.size} cells differ, first at {bad[:8]}"
 
 
+def test_completion_marks(gpu_ctx_factory):
+    """svdw_mark behind a held witness (hold_us: a spinning kernel at the head
+    of the step) reads not-done until the work completes; svdw_mark_wait waits
+    for it; 20 further marks reuse every slot of the 16-entry ring, and the
+    oldest ticket is then answered by the mark that took its slot."""
+    import ctypes as ct
+    import halo2_svd041_amd as hs
+    from halo2_svd041_amd import _lib
+    L = _lib.lib()
+    N, M, P = 64, 48, 63
+    ctx = gpu_ctx_factory(P)
+    m, u, d, v = gen_svd_input(N, M, seed=71)
+    for k in range(2):
+        hs.svd_witness(ctx, *_on_device(m, u, v, d), gamma_for(72 + k))
+    ctx.sync()
+    ctx.set_option("hold_us", 20000)
+    hs.svd_witness(ctx, *_on_device(m, u, v, d), gamma_for(74))
+    t = ct.c_uint64(0)
+    assert L.svdw_mark(ctx.handle, ct.byref(t)) == 0
+    first = t.value
+    assert L.svdw_mark_done(ctx.handle, first) == 0
+    assert L.svdw_mark_wait(ctx.handle, first) == 0
+    assert L.svdw_mark_done(ctx.handle, first) == 1
+    assert ctx.query()
+    ctx.set_option("hold_us", 0)
+    for _ in range(20):
+        assert L.svdw_mark(ctx.handle, ct.byref(t)) == 0
+    ctx.sync()
+    assert L.svdw_mark_done(ctx.handle, first) == 1 and L.svdw_mark_done(ctx.handle, t.value) == 1
+
+
 def test_held_inputs_bounded(gpu_ctx_factory):
     """back-to-back pipelined witnesses on fresh device tensors with
     no sync and no readback. The Python layer releases each call's inputs once a
-    checkpoint after that call has completed, so the held set stays bounded
+    completion mark (svdw_mark) after that call has completed, so the held set stays bounded
     (HOLD_EVERY * (HOLD_CKPTS + 1) calls at most) instead of growing until the
     device is out of memory; the last witness still equals the oracle's."""
     import halo2_svd041_amd as hs

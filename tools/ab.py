@@ -92,7 +92,8 @@ def main():
     for name, _ in variants:
         med = statistics.median(res[name])
         print(f"{name:12s} median {med:.4f} ms  min {min(res[name]):.4f}  -> {cells / med / 1e6:.2f} Gcells/s"
-              f"  samples {' '.join(f'{x:.3f}' for x in sorted(res[name]))}")
+              f"  samples {' '.join(f'{x:.3f}' for x in sorted(res[name]))}"
+              f"  (in order {' '.join(f'{x:.3f}' for x in res[name])})")
         top = sorted(kern[name].items(), key=lambda kv: -statistics.median(kv[1]))[:a.top]
         print("   " + "  ".join(f"{k}={statistics.median(vv):.3f}" for k, vv in top))
     print(json.dumps({n: statistics.median(r) for n, r in res.items()}))
