@@ -565,13 +565,16 @@ struct svdw_ctx {
     hipStream_t st3 = nullptr;
     hipStream_t st_cell = nullptr;          // the cell stream proper (st is swapped at times)
     hipEvent_t xev[4] = {};                 // svdw_stream_wait / _signal (caller's stream)
-    // svdw_mark ring: slot k holds ticket mk_t[k]'s events (one per stream of
-    // both lanes), recorded on the context's own streams (no waits)
+    // svdw_mark ring: slot k holds ticket t[k]'s events (one per stream of
+    // both lanes), recorded on the context's own streams (no waits); it stays
+    // with the handle when lanes exchange states (lane_switch)
     static constexpr int kMarks = 16;
-    hipEvent_t mk_ev[kMarks][6] = {};
-    uint64_t mk_t[kMarks] = {};
-    uint8_t mk_used[kMarks] = {};
-    uint64_t mk_seq = 0;
+    struct Marks {
+        hipEvent_t ev[kMarks][6] = {};
+        uint64_t t[kMarks] = {};
+        uint8_t used[kMarks] = {};
+        uint64_t seq = 0;
+    } mk;
     bool overlap = true;
     struct PreGemm {
         uint64_t off;
@@ -3210,7 +3213,7 @@ static void ctx_release(svdw_ctx* c) {
         if (c->ev_bits) (void)hipEventDestroy(c->ev_bits);
         for (auto e : c->xev)
             if (e) (void)hipEventDestroy(e);
-        for (auto& m : c->mk_ev)
+        for (auto& m : c->mk.ev)
             for (auto e : m)
                 if (e) (void)hipEventDestroy(e);
         for (auto& r : c->recs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
@@ -3298,6 +3301,7 @@ static void lane_switch(svdw_ctx* c) {
     std::swap(*c, *L);
     std::swap(c->lane, L->lane);                  // (the handle keeps the lane and the option)
     std::swap(c->lanes, L->lanes);
+    std::swap(c->mk, L->mk);
 }
 static hipEvent_t xevent(svdw_ctx* c, int i);
 // caller: the caller's stream (svdw_verify_mul_witness_on), waited for by the
@@ -3701,7 +3705,7 @@ int svdw_query(svdw_ctx* c) {
 int svdw_mark(svdw_ctx* c, uint64_t* ticket) {
     return guarded([&] {
         REQUIRE(c && ticket, "null argument");
-        const uint64_t t = ++c->mk_seq;
+        const uint64_t t = ++c->mk.seq;
         *ticket = t;
         if (c->dry) return;
         const int k = (int)(t % svdw_ctx::kMarks);
@@ -3711,18 +3715,18 @@ int svdw_mark(svdw_ctx* c, uint64_t* ticket) {
             for (hipStream_t st : {x->st, x->st2, x->st3}) {
                 if (!st) continue;
                 flush_batch(x, st);
-                hipEvent_t& e = c->mk_ev[k][i++];
+                hipEvent_t& e = c->mk.ev[k][i++];
                 if (!e) hipck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
                 hipck(hipEventRecord(e, st), "hipEventRecord");
             }
         }
-        c->mk_used[k] = (uint8_t)i;
-        c->mk_t[k] = t;
+        c->mk.used[k] = (uint8_t)i;
+        c->mk.t[k] = t;
     });
 }
 // the slot answering ticket t, or -1 (t not issued)
 static int mark_slot(const svdw_ctx* c, uint64_t t) {
-    if (!t || t > c->mk_seq) return -1;
+    if (!t || t > c->mk.seq) return -1;
     return (int)(t % svdw_ctx::kMarks);
 }
 int svdw_mark_done(svdw_ctx* c, uint64_t ticket) {
@@ -3732,8 +3736,8 @@ int svdw_mark_done(svdw_ctx* c, uint64_t ticket) {
         const int k = mark_slot(c, ticket);
         REQUIRE(k >= 0, "svdw_mark_done: ticket not issued");
         if (c->dry) return;
-        for (int i = 0; i < c->mk_used[k]; ++i) {
-            const hipError_t e = hipEventQuery(c->mk_ev[k][i]);
+        for (int i = 0; i < c->mk.used[k]; ++i) {
+            const hipError_t e = hipEventQuery(c->mk.ev[k][i]);
             if (e == hipErrorNotReady) {
                 done = 0;
                 return;
@@ -3749,7 +3753,7 @@ int svdw_mark_wait(svdw_ctx* c, uint64_t ticket) {
         const int k = mark_slot(c, ticket);
         REQUIRE(k >= 0, "svdw_mark_wait: ticket not issued");
         if (c->dry) return;
-        for (int i = 0; i < c->mk_used[k]; ++i) hipck(hipEventSynchronize(c->mk_ev[k][i]), "hipEventSynchronize");
+        for (int i = 0; i < c->mk.used[k]; ++i) hipck(hipEventSynchronize(c->mk.ev[k][i]), "hipEventSynchronize");
     });
 }
 uint64_t svdw_advice_len(const svdw_ctx* c, uint32_t phase) { return c && phase < 2 ? c->ph[phase].n : 0; }
