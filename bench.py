@@ -49,6 +49,15 @@ import time
 
 import numpy as np
 
+# Hardware queues per process (read by HIP at its first call, so before torch
+# touches the GPU). The engine runs three streams and torch one; a rank's RCCL
+# group adds its own, and with the box default of 4 some of them share a queue
+# with a context stream: tools/r6/rccl1.py with the group created before the
+# context, 1024^2 1.818 -> 1.804 ms and the 8-way rank 0.306 -> 0.302 ms at 8
+# queues; created after it, 1.92 -> 1.80 and 0.368 -> 0.309 ms (DESIGN.md,
+# round 6, r6w). One GPU without a group is unchanged (512^2 0.375 ms both).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 ORACLE_DIR = os.path.join(ROOT, "oracle")   # cpu_baseline leg only
