@@ -487,9 +487,10 @@ struct svdw_ctx {
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
     hipStream_t stream_id[3] = {};          // st, st2, st3 as created (st / st2 / st3 are swapped at times)
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
-    // "gemm_kern": CRT GEMM kernel (CrtBatch::kern); -1: the persistent grid for
-    // a product queued on its own (svdw_honest_prover_mat_mul, gemm_solo),
-    // one block per unit inside the witness calls, beside their stage kernels
+    // "gemm_kern": CRT GEMM kernel (CrtBatch::kern); -1: wide tiles or the
+    // persistent grid for a product queued on its own (svdw_honest_prover_mat_mul,
+    // gemm_solo; CrtBatch::kern 3), one block per unit inside the witness calls,
+    // beside their stage kernels
     int gemm_kern = -1;
     bool gemm_solo = false;
     int res_wait = -1;                      // "res_wait": stages wait for the residue planes
@@ -1638,7 +1639,7 @@ static void gemm_exec(svdw_ctx* c, hipStream_t s, const svdw_mat& a, const svdw_
                          (double)N * M * K);
             hipck(launch_gemm_crt(sym, Ar, Br, N, M, rpa, sym ? rpa : rpb,
                                   kpad, (uint8_t*)c->crtR.p, out, M, 1, sa, sym ? sa : sb, lk, s,
-                                  c->gemm_kern >= 0 ? (uint32_t)c->gemm_kern : (c->gemm_solo ? 1u : 0u)),
+                                  c->gemm_kern >= 0 ? (uint32_t)c->gemm_kern : (c->gemm_solo ? 3u : 0u)),
                   "k_gemm_crt");
         }
         if (!quantized)
@@ -4673,7 +4674,7 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
             REQUIRE(value >= -1 && value <= 1, "res_wait: -1 (auto), 0 or 1");
             c->res_wait = (int)value;
         } else if (n == "gemm_kern") {               // CRT GEMM kernel variant (bit-identical)
-            REQUIRE(value >= -1 && value <= 1, "gemm_kern: -1 (auto), 0 or 1");
+            REQUIRE(value >= -1 && value <= 2, "gemm_kern: -1 (auto), 0, 1 or 2");
             c->gemm_kern = (int)value;
         } else if (n == "stage_batch") {          // small independent stages share k_stage_multi launches
             c->stage_batch = value != 0;

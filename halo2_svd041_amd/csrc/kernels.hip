@@ -1901,6 +1901,158 @@ __global__ __launch_bounds__(256, 2) void k_gemm_crt_pers(const CrtBatch b) {
 #undef CRP_FRAG
 #undef CRP_MMA
 }
+// 256 x 128 block tile: two vertically adjacent 128 x 128 tiles of the job's
+// tile grid per (tile pair, modulus) unit, 4 waves of 128 x 64. Per 64-k step a
+// wave reads 8 A and 4 B fragments (12 KiB) for 32 MFMAs: half the LDS bytes
+// per MFMA of the 64 x 64 wave tiles (16 fragments for 16 MFMAs), which bound
+// those near 40 % of the matrix-core rate. 48 KiB of LDS (two 24 KiB buffers),
+// two chunks in flight in registers, two blocks per CU. Non-symmetric jobs of
+// whole tile grids only (launch_gemm_crt_multi checks); a pair's second tile
+// past the last tile row reads clamped rows and stores nothing. Residues go to
+// the 128 x 128 tiles' places in the per-unit kernel's MFMA order, so the
+// combine is unchanged: wave (wr, wc)'s accumulator rows a < 4 / a >= 4 are the
+// per-unit kernel's waves 2 * 0 + wc / 2 * 1 + wc of tile 2 bi2 + wr.
+static constexpr int CTW = 2 * CT;
+constexpr int crt_wide_lds_bytes() { return 2 * (CTW + CT) * CROW; }
+__device__ __forceinline__ uint32_t crt_npairs(const CrtJob& q) { return (q.tiles_a + 1) / 2 * q.tiles_m; }
+__device__ __forceinline__ bool crt_unit_wide(const CrtBatch& b, uint32_t blk, uint32_t* jo, uint32_t* mo,
+                                              uint32_t* po) {
+    uint32_t cnt[kMaxCrtJobs], total = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxCrtJobs; ++j) {
+        cnt[j] = 0;
+        if ((uint32_t)j < b.njobs)
+            cnt[j] = (uint32_t)crt_nmod(*b.job[j].bits_a, *b.job[j].bits_b, b.job[j].lk) * crt_npairs(b.job[j]);
+        total += cnt[j];
+    }
+    const uint32_t per = (total + 7) / 8, k = blk >> 3;
+    if (k >= per) return false;
+    uint32_t u = (blk & 7) * per + k;
+    if (u >= total) return false;
+    uint32_t j = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxCrtJobs - 1; ++q)
+        if (j == (uint32_t)q && u >= cnt[q]) { u -= cnt[q]; ++j; }
+    const uint32_t np = crt_npairs(b.job[j]);
+    *jo = j;
+    *mo = u / np;
+    *po = u - *mo * np;
+    return true;
+}
+__global__ __launch_bounds__(256, 2) void k_gemm_crt_wide(const CrtBatch b) {
+    __shared__ __attribute__((aligned(16))) uint8_t S[crt_wide_lds_bytes()];
+    const uint64_t t0 = wall_clock64();
+    uint32_t j, mod, pr;
+    if (!crt_unit_wide(b, blockIdx.x, &j, &mod, &pr)) return;
+    const CrtJob& q = b.job[j];
+    const uint32_t bi2 = pr / q.tiles_m, bj = pr - bi2 * q.tiles_m;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t wr = wave >> 1, wc = wave & 1;
+    const uint32_t kpad = q.kpad, kcn = kpad / 64;
+    const uint32_t rlast = q.tiles_a * CT - 1;            // staged A rows stay in the job's tile rows
+    const uint8_t* Ap = q.Ar + (uint64_t)mod * q.astride * kpad;
+    const uint8_t* Bp = q.Br + ((uint64_t)mod * q.bstride + bj * CT) * kpad;
+    const uint32_t rr = tid >> 2, part = tid & 3;
+    uint64_t ao[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ao[i] = (uint64_t)min(bi2 * CTW + rr + 64u * i, rlast) * kpad + part * 16;
+    const uint64_t bo0 = (uint64_t)rr * kpad + part * 16, bo1 = (uint64_t)(rr + 64) * kpad + part * 16;
+    const uint32_t frow = lane & 15, fp = lane >> 4;
+    v4i acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[a][c] = v4i{0, 0, 0, 0};
+#define CRW_GLOAD(g, chunk)                                                                   \
+    {                                                                                         \
+        const uint64_t ko = (uint64_t)min((uint32_t)(chunk), kcn - 1) * 64;                   \
+        g##a0 = *reinterpret_cast<const uint4*>(Ap + ao[0] + ko);                             \
+        g##a1 = *reinterpret_cast<const uint4*>(Ap + ao[1] + ko);                             \
+        g##a2 = *reinterpret_cast<const uint4*>(Ap + ao[2] + ko);                             \
+        g##a3 = *reinterpret_cast<const uint4*>(Ap + ao[3] + ko);                             \
+        g##b0 = *reinterpret_cast<const uint4*>(Bp + bo0 + ko);                               \
+        g##b1 = *reinterpret_cast<const uint4*>(Bp + bo1 + ko);                               \
+    }
+#define CRW_LSTORE(g, buf)                                                                    \
+    {                                                                                         \
+        uint8_t* Ac = S + (buf) * (CTW + CT) * CROW;                                          \
+        uint8_t* Bc = Ac + CTW * CROW;                                                        \
+        *reinterpret_cast<uint4*>(Ac + crt_lds(rr, part)) = g##a0;                            \
+        *reinterpret_cast<uint4*>(Ac + crt_lds(rr + 64, part)) = g##a1;                       \
+        *reinterpret_cast<uint4*>(Ac + crt_lds(rr + 128, part)) = g##a2;                      \
+        *reinterpret_cast<uint4*>(Ac + crt_lds(rr + 192, part)) = g##a3;                      \
+        *reinterpret_cast<uint4*>(Bc + crt_lds(rr, part)) = g##b0;                            \
+        *reinterpret_cast<uint4*>(Bc + crt_lds(rr + 64, part)) = g##b1;                       \
+    }
+#define CRW_FRAG(buf)                                                                         \
+    {                                                                                         \
+        const uint8_t* Ac = S + (buf) * (CTW + CT) * CROW;                                    \
+        const uint8_t* Bc = Ac + CTW * CROW;                                                  \
+        _Pragma("unroll") for (int a = 0; a < 8; ++a)                                         \
+            af[a] = *reinterpret_cast<const v4i*>(Ac + crt_lds(wr * 128 + a * 16 + frow, fp)); \
+        _Pragma("unroll") for (int c = 0; c < 4; ++c)                                         \
+            bf[c] = *reinterpret_cast<const v4i*>(Bc + crt_lds(wc * 64 + c * 16 + frow, fp));  \
+    }
+#define CRW_MMA()                                                                             \
+    {                                                                                         \
+        _Pragma("unroll") for (int a = 0; a < 8; ++a)                                         \
+            _Pragma("unroll") for (int c = 0; c < 4; ++c)                                     \
+                acc[a][c] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[c], acc[a][c], 0, 0, 0); \
+    }
+    // chunk c + 1 into the other LDS buffer, chunk c + 3 into the registers it
+    // came from, chunk c multiplied, then the fragments of chunk c + 1
+#define CRW_STEP(g, c)                                                                        \
+    {                                                                                         \
+        CRW_LSTORE(g, ((c) + 1) & 1);                                                         \
+        CRW_GLOAD(g, (c) + 3);                                                                \
+        CRW_MMA();                                                                            \
+        __syncthreads();                                                                      \
+        CRW_FRAG(((c) + 1) & 1);                                                              \
+    }
+    uint4 g0a0, g0a1, g0a2, g0a3, g0b0, g0b1, g1a0, g1a1, g1a2, g1a3, g1b0, g1b1;
+    v4i af[8], bf[4];
+    CRW_GLOAD(g0, 0);
+    CRW_GLOAD(g1, 1);
+    CRW_LSTORE(g0, 0);
+    CRW_GLOAD(g0, 2);
+    __syncthreads();
+    const uint64_t tp1 = wall_clock64();
+    CRW_FRAG(0);
+    // (kcn is a multiple of 4: whole pairs of steps)
+    for (uint32_t c0 = 0; c0 < kcn; c0 += 2) {
+        CRW_STEP(g1, c0)
+        CRW_STEP(g0, c0 + 1)
+    }
+    const uint64_t tp2 = wall_clock64();
+#undef CRW_STEP
+#undef CRW_GLOAD
+#undef CRW_LSTORE
+#undef CRW_FRAG
+#undef CRW_MMA
+    const uint32_t ti = bi2 * 2 + wr;                       // this wave's 128 x 128 tile row
+    if (ti < q.tiles_a) {
+        const uint32_t m = c_crt_mod[mod], magic = c_crt_magic[mod], bias = c_crt_bias[mod];
+        uint32_t* Rt = reinterpret_cast<uint32_t*>(q.R + ((uint64_t)mod * q.nblk + ti * q.tiles_m + bj) *
+                                                            kCrtTileBytes) + lane;
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                uint32_t r[4];
+#pragma unroll
+                for (int reg = 0; reg < 4; ++reg) {           // (crt_store_residues' reduction)
+                    const uint32_t x = (uint32_t)acc[a][c][reg] + bias;
+                    const uint32_t qq = __umulhi(x, magic);
+                    const uint32_t rv = (uint32_t)((int)x - __mul24((int)qq, (int)m));
+                    r[reg] = min(rv, rv + m);
+                }
+                Rt[((a >> 2) * 2 + wc) * 1024 + ((a & 3) * 4 + c) * 64] =
+                    __builtin_amdgcn_perm(r[1], r[0], 0x0c0c0400u) |
+                    (__builtin_amdgcn_perm(r[3], r[2], 0x0c0c0400u) << 16);
+            }
+    }
+    trace_block(t0, tp1, tp2);
+}
 // C from its n residues, written as canonical Fr to out[i*ors + j*ocs]: one
 // element per thread in the GEMM's tile order (each block one 256-element
 // stretch of a tile), so a wave reads 64 consecutive residue bytes per modulus
@@ -2012,11 +2164,26 @@ hipError_t launch_gemm_crt_multi(const CrtBatch& b0, hipStream_t st) {
     const hipError_t pe = prep_crt_batch(b, units, cblocks);
     if (pe != hipSuccess) return pe;
     const dim3 grid((units + 7) / 8 * 8);
-    // persistent: one kpad of >= 8 chunks for every job, else the per-unit kernel
-    bool pers = b.kern == 1 && b.job[0].kpad >= 512;
+    if (b.kern > 3) return hipErrorInvalidValue;
+    // wide tiles: non-symmetric jobs over whole tile grids (kern 3: and at
+    // least 64 tile pairs, ~1200 units at n = 19, two rounds of two blocks per
+    // CU; gemmprobe: 2048^2 m.v^T 209 -> 186 us against the persistent kernel,
+    // but 1024^2's 608 units 35 -> 37 us), else the persistent kernel (one
+    // kpad of >= 8 chunks for every job), else the per-unit one
+    bool wide = b.kern >= 2;
+    uint32_t wunits = 0, pairs = 0;
+    for (uint32_t j = 0; j < b.njobs; ++j) {
+        const CrtJob& q = b.job[j];
+        wide = wide && !q.sym && !q.tile0 && !q.tcount;
+        pairs += (q.tiles_a + 1) / 2 * q.tiles_m;
+    }
+    wunits = kCrtMaxMod * pairs;
+    if (b.kern == 3 && pairs < 64) wide = false;
+    bool pers = b.kern >= 1 && b.job[0].kpad >= 512;
     for (uint32_t j = 1; j < b.njobs; ++j) pers = pers && b.job[j].kpad == b.job[0].kpad;
-    if (b.kern > 1) return hipErrorInvalidValue;
-    if (pers)
+    if (wide)
+        hipLaunchKernelGGL(k_gemm_crt_wide, dim3((wunits + 7) / 8 * 8), dim3(256), 0, st, b);
+    else if (pers)
         hipLaunchKernelGGL(k_gemm_crt_pers, dim3(std::min<uint32_t>(grid.x, 8 * kCrtPersPerXcd)), dim3(256), 0,
                            st, b);
     else

@@ -352,7 +352,9 @@ struct CrtBatch {
     uint32_t njobs;
     // GEMM kernel (bit-identical): 0 one block per (tile, modulus) unit
     // (k_gemm_crt_multi), 1 a persistent grid whose blocks' chunk pipelines
-    // run across their units (k_gemm_crt_pers; jobs of one kpad >= 512)
+    // run across their units (k_gemm_crt_pers; jobs of one kpad >= 512), 2
+    // 256 x 128 tiles (k_gemm_crt_wide; non-symmetric whole jobs), 3 wide
+    // from 64 tile pairs on, else persistent (products queued on their own)
     uint32_t kern;
 };
 // R sized crt_scratch_bytes per job

@@ -329,10 +329,12 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   on the cell stream behind the products (0), on the second stream with the
  *   bounds and u.d (1) or on the third ahead of phase 1 (2)); "vm_linear" 1 | 0 (the captured sequence is queued on the context
  *   stream alone, a linear graph, instead of forking to the second stream);
- *   "gemm_kern" -1 | 0 | 1 (CRT GEMM: 0 one block per (128 x 128 tile,
+ *   "gemm_kern" -1 | 0 | 1 | 2 (CRT GEMM: 0 one block per (128 x 128 tile,
  *   modulus) unit, 1 a persistent grid whose blocks' chunk pipelines run on
- *   across their units (jobs of one K >= 512); -1: 1 for a product queued on its
- *   own (svdw_honest_prover_mat_mul), 0 inside the witness calls);
+ *   across their units (jobs of one K >= 512), 2 256 x 128 tiles (non-symmetric
+ *   products; others as 1); -1: for a product queued on its own
+ *   (svdw_honest_prover_mat_mul) 2 from 64 tile pairs of 256 x 128 on, else 1,
+ *   and 0 inside the witness calls);
  *   "res_wait" -1 | 0 | 1 (pipelined svd_witness reading its loads from the f64
  *   inputs: the second stream's stages wait for the residue planes (1) or not
  *   (0); -1: 1 on a row-sharded context, else 0).

@@ -166,31 +166,37 @@ def test_honest_prover_mat_mul_k_beyond_chunks(gpu_ctx_factory):
                     | (int(got[i, j, 3]) << 192) == want
 
 
-@pytest.mark.parametrize("kern", [-1, 0])
-def test_honest_prover_mat_mul_persistent(gpu_ctx_factory, kern):
-    """svdw_honest_prover_mat_mul queued on its own runs the persistent CRT GEMM
-    (gemm_kern -1: K = 700 gives 12 chunks of 64, several units per block, the
-    chunk pipeline crossing unit boundaries); sampled entries against exact
-    integer sums of the quantized operands, and the whole product against the
-    per-unit kernel's (gemm_kern 0)."""
+@pytest.mark.parametrize("kern,N,K,M", [(-1, 300, 700, 260), (2, 300, 700, 260), (-1, 2048, 1024, 1100),
+                                         (1, 2048, 1024, 1100)])
+def test_honest_prover_mat_mul_persistent(gpu_ctx_factory, kern, N, K, M):
+    """svdw_honest_prover_mat_mul queued on its own: gemm_kern -1 runs the
+    persistent CRT GEMM below 64 tile pairs of 256 x 128 (300 x 700 x 260: K =
+    700 gives 12 chunks of 64, several units per block, the chunk pipeline
+    crossing unit boundaries) and the wide-tile kernel from there on (2048 x
+    1024 x 1100: 72 pairs, a partial last tile column); gemm_kern 2 forces the
+    wide kernel on 3 tile rows (a pair whose second tile is past the end). Sampled
+    entries against exact integer sums of the quantized operands, and the whole
+    product against the per-unit kernel's (gemm_kern 0)."""
     import halo2_svd041_amd as hs
     import pyoracle as po
     rs = np.random.RandomState(9)
-    A = rs.uniform(-3, 3, (300, 700))
-    B = rs.uniform(-3, 3, (700, 260))
+    A = rs.uniform(-3, 3, (N, K))
+    B = rs.uniform(-3, 3, (K, M))
     outs = []
     for k in (kern, 0):
         ctx = gpu_ctx_factory(63)
         ctx.set_option("gemm_kern", k)
         za, zb = hs.ZkMatrix.new(ctx, A), hs.ZkMatrix.new(ctx, B)
         outs.append(hs.honest_prover_mat_mul(ctx, za, zb).values())
+        ctx.close()
     assert np.array_equal(outs[0], outs[1])
     got = outs[0]
-    qa = [[po.quantize(x, 63) for x in r] for r in A.tolist()]
-    qb = [[po.quantize(x, 63) for x in r] for r in B.tolist()]
-    for i in (0, 129, 299):
-        for j in (0, 128, 259):
-            want = sum(qa[i][k] * qb[k][j] for k in range(700)) % po.P_MOD
+    rows, cols = (0, 129, N - 1), (0, 128, M - 1)
+    qa = {i: [po.quantize(x, 63) for x in A[i].tolist()] for i in rows}
+    qb = {j: [po.quantize(x, 63) for x in B[:, j].tolist()] for j in cols}
+    for i in rows:
+        for j in cols:
+            want = sum(x * y for x, y in zip(qa[i], qb[j])) % po.P_MOD
             assert int(got[i, j, 0]) | (int(got[i, j, 1]) << 64) | (int(got[i, j, 2]) << 128) \
                 | (int(got[i, j, 3]) << 192) == want
 
@@ -229,7 +235,8 @@ def test_crt_gemm_tiles_parity(gpu_ctx_factory, N, M, P, world, device):
                                   {"overlap": 0},
                                   {"stage_batch": 0}, {"pipeline": 0}, {"pipeline": 0, "phase1_overlap": 2},
                                   {"gemm_impl": 1}, {"res_f64": 0}, {"f64_views": 0},
-                                  {"gemm_kern": 0}, {"gemm_kern": 1}, {"res_wait": 0}, {"res_wait": 1}])
+                                  {"gemm_kern": 0}, {"gemm_kern": 1}, {"gemm_kern": 2}, {"res_wait": 0},
+                                  {"res_wait": 1}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
@@ -666,7 +673,10 @@ def test_device_input_lifetime(gpu_ctx_factory):
 
 @pytest.mark.parametrize("N,M", [(320, 300), (300, 520)])
 def test_gemm_kern_full_streams(gpu_ctx_factory, N, M):
-    """The persistent CRT GEMM (gemm_kern 1) against the per-unit one (0,
+    """The persistent CRT GEMM (gemm_kern 1) and gemm_kern 2 (the batch holds
+    the symmetric u.u^T and v.v^T, so it falls back to 1 as a whole; the wide
+    kernel runs inside a witness on row-sharded ranks, test_full_size_shard_rank_parity)
+    against the per-unit one (0,
     oracle-checked throughout this file) on pipelined device-input witnesses at
     K >= 300 (>= 8 chunks of 64: the persistent grid runs, its chunk pipeline
     crossing unit boundaries; 300 x 520 mixes kpads, where it falls back to
@@ -675,7 +685,7 @@ def test_gemm_kern_full_streams(gpu_ctx_factory, N, M):
     import halo2_svd041_amd as hs
     P = 63
     outs = []
-    for k in (0, 1):
+    for k in (0, 1, 2):
         ctx = gpu_ctx_factory(P)
         ctx.set_option("gemm_kern", k)
         for c in range(2):
@@ -684,10 +694,11 @@ def test_gemm_kern_full_streams(gpu_ctx_factory, N, M):
         ctx.sync()
         outs.append((ctx.advice(0), ctx.lookups(0), ctx.advice(1)))
         ctx.close()
-    for name, a, b in zip(("advice0", "lookup0", "advice1"), outs[0], outs[1]):
-        assert a.shape == b.shape
-        bad = np.nonzero(np.any(a != b, axis=1))[0]
-        assert bad.size == 0, f"{name}: {bad.size} cells differ, first at {bad[:8]}"
+    for k, out in zip((1, 2), outs[1:]):
+        for name, a, b in zip(("advice0", "lookup0", "advice1"), outs[0], out):
+            assert a.shape == b.shape
+            bad = np.nonzero(np.any(a != b, axis=1))[0]
+            assert bad.size == 0, f"gemm_kern {k} {name}: {bad.size} cells differ, first at {bad[:8]}"
 
 
 def test_completion_marks(gpu_ctx_factory):
@@ -747,7 +758,8 @@ def test_held_inputs_bounded(gpu_ctx_factory):
 
 @pytest.mark.parametrize("rank,opts", [(0, {}), (3, {}), (7, {}),
                                        (3, {"overlap": 0, "phase1_overlap": 0}),
-                                       (5, {"dchk_at": 2, "gamma_at": 1}), (6, {"dchk_at": 1})])
+                                       (5, {"dchk_at": 2, "gamma_at": 1}), (6, {"dchk_at": 1}),
+                                       (2, {"gemm_kern": 2})])
 def test_full_size_shard_rank_parity(gpu_ctx_factory, rank, opts):
     """BASELINE config 4 (1024^2, P=63, row blocks over 8 GPUs), rank by rank at
     full size, cell for cell: the rank's witness on the GPU (svdw_set_shard, the

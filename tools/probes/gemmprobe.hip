@@ -1,5 +1,6 @@
 // Standalone timing of the CRT GEMM kernels (round 6): the per-unit
-// k_gemm_crt_multi against the persistent k_gemm_crt_pers, on random balanced
+// k_gemm_crt_multi against the persistent k_gemm_crt_pers and the 256 x 128
+// tile k_gemm_crt_wide (non-symmetric jobs only), on random balanced
 // residue planes shaped like the
 // 1024^2 P=63 witness (m.v^T: 19 moduli; u.u^T and v.v^T symmetric: 18), alone
 // and as the step's three-job batch. Every variant's residue bytes are compared
@@ -39,11 +40,23 @@ __global__ __launch_bounds__(256) void k_standin(uint4* __restrict__ out, size_t
 
 // (round 6 also measured LDS-DMA staging with 2-4 chunk buffers and the
 // per-unit kernel with the old fp32-quotient epilogue: profiles/r06_ab/r6c)
-static constexpr int NV = 2;
-static const char* vname[NV] = {"per-unit", "persistent"};
+static constexpr int NV = 3;
+static const char* vname[NV] = {"per-unit", "persistent", "wide"};
+static bool has_sym(const CrtBatch& b) {
+    for (uint32_t j = 0; j < b.njobs; ++j)
+        if (b.job[j].sym) return true;
+    return false;
+}
 static void launch_variant(int v, dim3 g, hipStream_t st, const CrtBatch& b) {
-    if (v == 0) hipLaunchKernelGGL(k_gemm_crt_multi, g, dim3(256), 0, st, b);
-    else hipLaunchKernelGGL(k_gemm_crt_pers, dim3(std::min<uint32_t>(g.x, 8 * kCrtPersPerXcd)), dim3(256), 0, st, b);
+    if (v == 0) {
+        hipLaunchKernelGGL(k_gemm_crt_multi, g, dim3(256), 0, st, b);
+    } else if (v == 1) {
+        hipLaunchKernelGGL(k_gemm_crt_pers, dim3(std::min<uint32_t>(g.x, 8 * kCrtPersPerXcd)), dim3(256), 0, st, b);
+    } else {
+        uint32_t w = 0;
+        for (uint32_t j = 0; j < b.njobs; ++j) w += kCrtMaxMod * ((b.job[j].tiles_a + 1) / 2 * b.job[j].tiles_m);
+        hipLaunchKernelGGL(k_gemm_crt_wide, dim3((w + 7) / 8 * 8), dim3(256), 0, st, b);
+    }
 }
 
 __global__ void k_nmod(const unsigned* W, uint32_t lk, int* out) { *out = crt_nmod(W[0], W[1], lk); }
@@ -107,7 +120,8 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (const Case& cs : cases) {
-        double best[NV] = {1e9, 1e9};
+        double best[NV] = {1e9, 1e9, 1e9};
+        bool skip[NV] = {false, false, false};
         for (int round = 0; round < (quick ? 1 : 3); ++round)
             for (int v = 0; v < NV; ++v) {
                 CrtBatch b;
@@ -117,6 +131,10 @@ int main(int argc, char** argv) {
                     job(b.job[j], cs.sym[j], W + cs.wa[j], W + cs.wb[j], Rs[v] + j * rbytes);
                 uint32_t units, cblocks;
                 CK(prep_crt_batch(b, units, cblocks));
+                if (v == 2 && has_sym(b)) {
+                    skip[v] = true;
+                    continue;
+                }
                 const dim3 g((units + 7) / 8 * 8);
                 auto launch = [&] { launch_variant(v, g, 0, b); };
                 for (int w = 0; w < 3; ++w) launch();
@@ -134,6 +152,7 @@ int main(int argc, char** argv) {
         std::vector<uint8_t> r0(3 * rbytes), r1(3 * rbytes);
         CK(hipMemcpy(r0.data(), Rs[0], 3 * rbytes, hipMemcpyDeviceToHost));
         for (int v = 0; v < NV; ++v) {
+            if (skip[v]) continue;
             size_t diff = 0;
             if (v) {
                 CK(hipMemcpy(r1.data(), Rs[v], 3 * rbytes, hipMemcpyDeviceToHost));
@@ -159,7 +178,7 @@ int main(int argc, char** argv) {
                 uint32_t units, cblocks;
                 CK(prep_crt_batch(b, units, cblocks));
                 const dim3 g((units + 7) / 8 * 8);
-                if (g.x > nb) continue;
+                if (g.x > nb || (v == 2 && has_sym(b))) continue;
                 CK(hipMemset(tr, 0, nb * 5 * 8));
                 CK(set_debug_trace(tr));
                 launch_variant(v, g, 0, b);
@@ -204,7 +223,7 @@ int main(int argc, char** argv) {
         CK(hipFuncSetAttribute((const void*)k_standin, hipFuncAttributeMaxDynamicSharedMemorySize, 63 * 1024));
         const Case& cs = cases[2];
         for (int round = 0; round < 3; ++round)
-            for (int v = -1; v < NV; ++v) {
+            for (int v = -1; v < 2; ++v) {
                 CrtBatch b;
                 memset(&b, 0, sizeof b);
                 b.njobs = cs.njobs;
