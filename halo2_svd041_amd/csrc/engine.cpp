@@ -483,7 +483,10 @@ struct svdw_ctx {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
     int gemm_impl = SVDW_GEMM_MFMA;         // svdw_set_gemm_impl
-    uint32_t stage_flags = STAGE_ALIGN;     // STAGE_* (4 KiB-aligned block store windows)
+    // STAGE_* (4 KiB-aligned block store windows; "stage_rot" 1: phase B from a
+    // block-dependent window on, tools/r6/place_ab.py over 8 placements of the
+    // 1024^2 cell streams: 1.739-1.891 -> 1.728-1.825 ms, mean 1.815 -> 1.751)
+    uint32_t stage_flags = STAGE_ALIGN | STAGE_ROT;
     uint32_t stage_elems = kStageElems;     // "stage_elems": elements per stage block (16..256)
     hipStream_t stream_id[3] = {};          // st, st2, st3 as created (st / st2 / st3 are swapped at times)
     int gemm_crt = 1;                       // "gemm_crt": multi-modular GEMM (else digits)
@@ -4673,6 +4676,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "res_wait") {                // pipelined: st2 waits for the residue planes
             REQUIRE(value >= -1 && value <= 1, "res_wait: -1 (auto), 0 or 1");
             c->res_wait = (int)value;
+        } else if (n == "stage_rot") {               // phase B from a block-dependent window on
+            REQUIRE(value == 0 || value == 1, "stage_rot: 0 or 1");
+            c->stage_flags = value ? (c->stage_flags | STAGE_ROT) : (c->stage_flags & ~STAGE_ROT);
         } else if (n == "gemm_kern") {               // CRT GEMM kernel variant (bit-identical)
             REQUIRE(value >= -1 && value <= 2, "gemm_kern: -1 (auto), 0, 1 or 2");
             c->gemm_kern = (int)value;

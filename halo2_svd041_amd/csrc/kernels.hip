@@ -366,23 +366,18 @@ __device__ __forceinline__ uint32_t fastdiv(uint32_t x, uint32_t d, uint32_t mag
 // tracked incrementally (the cell index advances by blockDim / 2 per step).
 // ALIGN: the block's iterations cover whole (blockDim * 16 B)-aligned address
 // windows (the first one partially), so every wave store is one aligned 1 KiB.
-template <bool ALIGN>
-__device__ __forceinline__ void stream_cells_desc(uint4* __restrict__ out, uint32_t total,
-                                                  const uint32_t* __restrict__ sHD,
-                                                  const uint4* __restrict__ sHM, uint32_t C,
-                                                  uint32_t magic, const uint32_t* smem,
-                                                  uint32_t vbase0, uint32_t nv) {
+// Half-cells [.., hc_end) of the windows from the one holding hc_begin on (hc_begin
+// is this lane's first half-cell: lane tid's half-cells are hc_begin + k * blockDim).
+__device__ __forceinline__ void stream_cells_run(uint4* __restrict__ out, uint32_t hc_begin, uint32_t hc_end,
+                                                 const uint32_t* __restrict__ sHD,
+                                                 const uint4* __restrict__ sHM, uint32_t C, uint32_t magic,
+                                                 const uint32_t* smem, uint32_t vbase0, uint32_t nv) {
     const uint32_t h = threadIdx.x & 1, step = blockDim.x >> 1;
     const uint32_t dq = step / C, dr = step - dq * C, ev = stage_elem_words(nv);
-    uint32_t hc0 = threadIdx.x;
-    if (ALIGN) {
-        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) >> 4) & (blockDim.x - 1);
-        hc0 = threadIdx.x >= mis ? threadIdx.x - mis : threadIdx.x + blockDim.x - mis;
-    }
-    uint32_t c = hc0 >> 1;
+    uint32_t c = hc_begin >> 1;
     uint32_t el = fastdiv(c, C, magic), slot = c - el * C;
     uint32_t vbase = vbase0 + el * ev;                    // LDS word of this element's values
-    for (uint32_t hc = hc0; hc < total; hc += blockDim.x) {
+    for (uint32_t hc = hc_begin; hc < hc_end; hc += blockDim.x) {
         const uint32_t k = 2 * slot + h;
         const uint32_t d = sHD[k];
         const uint4 m = sHM[k];
@@ -402,6 +397,30 @@ __device__ __forceinline__ void stream_cells_desc(uint4* __restrict__ out, uint3
             vbase += ev;
         }
     }
+}
+// rot: the block starts at window rot mod (its window count) and wraps around
+// ("stage_rot"), so that blocks started together do not all write the same
+// window offset of their chunks at the same time.
+template <bool ALIGN>
+__device__ __forceinline__ void stream_cells_desc(uint4* __restrict__ out, uint32_t total,
+                                                  const uint32_t* __restrict__ sHD,
+                                                  const uint4* __restrict__ sHM, uint32_t C,
+                                                  uint32_t magic, const uint32_t* smem,
+                                                  uint32_t vbase0, uint32_t nv, uint32_t rot = 0) {
+    const uint32_t B = blockDim.x, tid = threadIdx.x;
+    const uint32_t mis = ALIGN ? (uint32_t)(reinterpret_cast<uintptr_t>(out) >> 4) & (B - 1) : 0u;
+    // lane tid's half-cells: tid - mis + k B (k >= 0, >= 0); window k holds
+    // [k B - mis, (k + 1) B - mis)
+    const uint32_t first = tid >= mis ? tid - mis : tid + B - mis;
+    const uint32_t nw = (total + mis + B - 1) / B;
+    const uint32_t r = nw > 1 ? rot % nw : 0u;
+    if (!r) {
+        stream_cells_run(out, first, total, sHD, sHM, C, magic, smem, vbase0, nv);
+        return;
+    }
+    const uint32_t cut = r * B - mis;                     // first half-cell of window r
+    stream_cells_run(out, cut + tid, total, sHD, sHM, C, magic, smem, vbase0, nv);
+    stream_cells_run(out, first, cut, sHD, sHM, C, magic, smem, vbase0, nv);
 }
 
 // Descriptor and masks of half h of a slot (see half_desc).
@@ -689,10 +708,11 @@ __device__ __forceinline__ void stage_chunk(const StageArgs& a, const StageLds& 
     uint4* outA = reinterpret_cast<uint4*>(a.out_adv + (uint64_t)e0 * a.C);
     uint4* outL = a.L ? reinterpret_cast<uint4*>(a.out_lk + (uint64_t)e0 * a.L) : nullptr;
     const uint32_t vb0 = (uint32_t)(L.sV - smem);
-    stream_cells_desc<true>(outA, 2 * ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv);
+    const uint32_t rot = (a.flags & STAGE_ROT) ? blk * 37u : 0u;
+    stream_cells_desc<true>(outA, 2 * ne * a.C, L.sHD, L.sHM, a.C, a.cdiv_magic, smem, vb0, nv, rot);
     if (a.L)
         stream_cells_desc<true>(outL, 2 * ne * a.L, L.sHD + 2 * a.C, L.sHM + 2 * a.C, a.L, a.ldiv_magic, smem,
-                                vb0, nv);
+                                vb0, nv, rot);
 }
 
 // One block of a stage: `a` supplies the scalar fields and the views (StageArgs

@@ -66,6 +66,7 @@ struct SlotOp {
 static constexpr uint8_t KSRC = 0x80;
 
 static constexpr uint32_t STAGE_ALIGN = 256;     // 4 KiB-aligned block store windows
+static constexpr uint32_t STAGE_ROT = 512;       // blocks start phase B at a block-dependent window
 
 static constexpr int kMaxViews = 2;
 static constexpr int kMaxMicro = 16;

@@ -236,7 +236,7 @@ def test_crt_gemm_tiles_parity(gpu_ctx_factory, N, M, P, world, device):
                                   {"stage_batch": 0}, {"pipeline": 0}, {"pipeline": 0, "phase1_overlap": 2},
                                   {"gemm_impl": 1}, {"res_f64": 0}, {"f64_views": 0},
                                   {"gemm_kern": 0}, {"gemm_kern": 1}, {"gemm_kern": 2}, {"res_wait": 0},
-                                  {"res_wait": 1}])
+                                  {"res_wait": 1}, {"stage_rot": 0}, {"stage_rot": 0, "pipeline": 0}])
 def test_tuning_options_parity(gpu_ctx_factory, opts):
     """Every tuning knob of svdw_set_option leaves the witness bit-identical."""
     import halo2_svd041_amd as hs
