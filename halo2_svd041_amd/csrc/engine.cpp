@@ -497,6 +497,7 @@ struct svdw_ctx {
     int gemm_kern = -1;
     bool gemm_solo = false;
     int res_wait = -1;                      // "res_wait": stages wait for the residue planes
+    int place_trials = 6;                   // "place_trials": candidate placements of a new cell stream
     bool gemm_batched = false;              // this witness's products went out as one batch
     bool res_f64 = true;                    // "res_f64": CRT residue planes of m, u, v from the
                                             // f64 inputs, one launch (else from the cells)
@@ -892,13 +893,88 @@ static void bits_words(svdw_ctx* c, QuantSegs& qs, uint32_t nred, const BitSegs&
     for (uint32_t s = 0; s <= nred; ++s) f.b[s] = qs.blk0[s];
     *folded = true;
 }
+// Write rate of the stage kernel's store pattern over `cells` cells at buf: a
+// stage of 61 constant cells per element (no loads, no micro-ops), one warm and
+// one timed launch on the cell stream.
+static double stage_store_rate(svdw_ctx* c, Fr* buf, uint64_t cells) {
+    StageArgs a;
+    memset(&a, 0, sizeof a);
+    const uint32_t C = 61;
+    const uint64_t ne = std::min<uint64_t>(cells / C, 1ull << 26);
+    if (ne < 1024) return 0.0;
+    a.out_adv = buf;
+    a.e_begin = 0;
+    a.e_end = (uint32_t)ne;
+    a.cols = 1;
+    a.C = C;
+    a.nv = 1;
+    a.nk = 1;
+    a.flags = c->stage_flags;
+    a.cdiv_magic = (uint32_t)(((1ull << 32) + C - 1) / C);
+    for (uint32_t k = 0; k < C; ++k) a.adv[k] = SlotOp{(uint8_t)KSRC, (uint8_t)(8 * (k % 8)), 0, 0};
+    a.K[0] = fr_from_u64(0x9e3779b97f4a7c15ull);
+    hipEvent_t e0, e1;
+    hipck(hipEventCreate(&e0), "hipEventCreate");
+    hipck(hipEventCreate(&e1), "hipEventCreate");
+    hipck(launch_stage(a, c->st), "k_stage (placement probe)");
+    hipck(hipEventRecord(e0, c->st), "hipEventRecord");
+    hipck(launch_stage(a, c->st), "k_stage (placement probe)");
+    hipck(hipEventRecord(e1, c->st), "hipEventRecord");
+    hipck(hipEventSynchronize(e1), "hipEventSynchronize");
+    float ms = 0;
+    hipck(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return ms > 0 ? 32.0 * C * ne / (ms * 1e-3) : 0.0;
+}
+// A new cell stream of >= 256 MiB with "place_trials" k > 1 (default 6): k
+// buffers are allocated side by side (so they lie in different places of HBM),
+// the stage store pattern is timed on each, and the fastest is kept. The same
+// witness runs 1.73-2.03 ms per step depending on where its streams lie, and a
+// fresh process's first placement is a slow one (fresh
+// bench.py processes at 1024^2, one box: 2.010-2.014 ms without trials,
+// 1.848-1.861 with 3, 1.721-1.767 with 6, tools/r6/r6pt3.sh).
+// The trials need k times the stream in free memory (fewer when it is short:
+// none at 4096^2) and a few ms once per allocation.
+static Fr* place_cells(svdw_ctx* c, uint64_t cells) {
+    const uint64_t bytes = cells * sizeof(Fr);
+    int k = c->place_trials;
+    if (k > 1 && bytes >= (256ull << 20)) {
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
+        while (k > 1 && (double)k * bytes > 0.5 * (double)fr) --k;
+    }
+    Fr* best = nullptr;
+    if (k <= 1 || bytes < (256ull << 20)) {
+        if (hipMalloc((void**)&best, bytes) != hipSuccess) return nullptr;
+        return best;
+    }
+    sync(c);
+    std::vector<Fr*> cand;
+    double br = -1.0;
+    for (int i = 0; i < k; ++i) {
+        Fr* p = nullptr;
+        if (hipMalloc((void**)&p, bytes) != hipSuccess) break;
+        cand.push_back(p);
+        const double r = stage_store_rate(c, p, cells);
+        if (c->host_trace) fprintf(stderr, "place_cells: %.2f GB candidate %d at %p: %.3f TB/s\n", bytes / 1e9, i,
+                                   (void*)p, r / 1e12);
+        if (r > br) {
+            br = r;
+            best = p;
+        }
+    }
+    for (Fr* p : cand)
+        if (p != best) hipck(hipFree(p), "hipFree");
+    return best;
+}
 static void grow(svdw_ctx* c, Fr*& ptr, uint64_t used, uint64_t& cap, uint64_t need) {
     if (c->dry || need <= cap) return;
     REQUIRE(!c->capturing, "internal: allocation during graph capture");
     ++c->epoch;
     uint64_t ncap = std::max(need, cap + cap / 2);
-    Fr* np = nullptr;
-    if (hipMalloc((void**)&np, ncap * sizeof(Fr)) != hipSuccess)
+    Fr* np = ptr ? nullptr : place_cells(c, ncap);
+    if (!np && hipMalloc((void**)&np, ncap * sizeof(Fr)) != hipSuccess)
         fail(SVDW_ENOMEM, "device allocation failed (cell stream of " + std::to_string(ncap) + " cells)");
     if (ptr) {
         hipck(hipMemcpyAsync(np, ptr, used * sizeof(Fr), hipMemcpyDeviceToDevice, c->st), "copy");
@@ -3263,17 +3339,17 @@ static void ctx_init_device(svdw_ctx* c) {
 // The settings (options, shard, profiler) of `s` onto the lane `d`; a change
 // bumps the lane's epoch (its captured graph no longer applies).
 static void copy_settings(svdw_ctx* d, const svdw_ctx* s) {
-    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->gemm_crt, s->gemm_kern, s->res_wait, s->res_f64,
+    const int64_t a[] = {s->gemm_impl, s->stage_flags, s->stage_elems, s->gemm_crt, s->gemm_kern, s->res_wait, s->place_trials, s->res_f64,
                          s->phase1_overlap, s->prod_cell, s->hold_us, s->rlc_prefix, s->p1_at, s->dchk_at, s->gamma_at,
                          s->f64_views, s->overlap, s->stage_batch, s->graph_vm, s->vm_linear, s->pipeline,
                          s->shard_rank, s->shard_world, s->prof, s->host_trace};
-    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->gemm_crt, d->gemm_kern, d->res_wait, d->res_f64,
+    const int64_t b[] = {d->gemm_impl, d->stage_flags, d->stage_elems, d->gemm_crt, d->gemm_kern, d->res_wait, d->place_trials, d->res_f64,
                          d->phase1_overlap, d->prod_cell, d->hold_us, d->rlc_prefix, d->p1_at, d->dchk_at, d->gamma_at,
                          d->f64_views, d->overlap, d->stage_batch, d->graph_vm, d->vm_linear, d->pipeline,
                          d->shard_rank, d->shard_world, d->prof, d->host_trace};
     if (!memcmp(a, b, sizeof a) && d->prof_filter == s->prof_filter) return;
     d->gemm_impl = s->gemm_impl; d->stage_flags = s->stage_flags; d->stage_elems = s->stage_elems;
-    d->gemm_crt = s->gemm_crt; d->gemm_kern = s->gemm_kern; d->res_wait = s->res_wait; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
+    d->gemm_crt = s->gemm_crt; d->gemm_kern = s->gemm_kern; d->res_wait = s->res_wait; d->place_trials = s->place_trials; d->res_f64 = s->res_f64; d->phase1_overlap = s->phase1_overlap;
     d->prod_cell = s->prod_cell; d->hold_us = s->hold_us; d->rlc_prefix = s->rlc_prefix;
     d->p1_at = s->p1_at; d->f64_views = s->f64_views; d->overlap = s->overlap;
     d->dchk_at = s->dchk_at; d->gamma_at = s->gamma_at;
@@ -4676,6 +4752,9 @@ int svdw_set_option(svdw_ctx* c, const char* name, int64_t value) {
         } else if (n == "res_wait") {                // pipelined: st2 waits for the residue planes
             REQUIRE(value >= -1 && value <= 1, "res_wait: -1 (auto), 0 or 1");
             c->res_wait = (int)value;
+        } else if (n == "place_trials") {            // cell streams >= 256 MiB: best of this many placements
+            REQUIRE(value >= 0 && value <= 8, "place_trials: 0..8");
+            c->place_trials = (int)value;
         } else if (n == "stage_rot") {               // phase B from a block-dependent window on
             REQUIRE(value == 0 || value == 1, "stage_rot: 0 or 1");
             c->stage_flags = value ? (c->stage_flags | STAGE_ROT) : (c->stage_flags & ~STAGE_ROT);

@@ -276,7 +276,7 @@ int svdw_verify_mul_witness_on(svdw_ctx* ctx, void* stream, const double* a, con
 #define SVDW_GEMM_MFMA 0
 #define SVDW_GEMM_VALU 1
 int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
-/* Options (svdw_set_option; 21 names; any other name is SVDW_EINVAL). Tuning
+/* Options (svdw_set_option; 22 names; any other name is SVDW_EINVAL). Tuning
  * knobs, bit-identical results
  * for every value, defaults first:
  *   "gemm_impl" 0 | 1; "gemm_crt" 1 | 0 (CRT or digit-plane matrix-core GEMM);
@@ -289,6 +289,9 @@ int svdw_set_gemm_impl(svdw_ctx* ctx, int impl);
  *   phase-0 stages, 3 after all of phase 0; -1: 0 on a rank of a >= 4-way shard, 3 of a
  *   2-3-way shard, else 1);
  *   "stage_elems" 256 (elements per stage block, multiple of 16 in [16, 256]);
+ *   "place_trials" 6 | 0..8 (a cell stream of >= 256 MiB allocated from now on
+ *   is chosen among that many placements in HBM by timing the stage kernels'
+ *   store pattern on each; 0 or 1: the first one);
  *   "stage_rot" 1 | 0 (a stage block writes its chunk of cells from a
  *   block-dependent 4 KiB window on, wrapping around, instead of from its
  *   start, so that blocks started together write different window offsets);

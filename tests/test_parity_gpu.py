@@ -701,6 +701,31 @@ def test_gemm_kern_full_streams(gpu_ctx_factory, N, M):
             assert bad.size == 0, f"gemm_kern {k} {name}: {bad.size} cells differ, first at {bad[:8]}"
 
 
+def test_place_trials_full_streams(gpu_ctx_factory):
+    """place_trials 3 (6 by default): each cell stream of >= 256 MiB is chosen among three
+    placements by timing the stage store pattern on each (the probe writes
+    constant cells over the candidates). 1024^2 P=32 pipelined device-input
+    witnesses, two calls (both cell sets), against a context without trials (0):
+    whole advice and lookup streams of both phases."""
+    import halo2_svd041_amd as hs
+    N = M = 1024
+    P = 32
+    outs = []
+    for k in (0, 3):
+        ctx = gpu_ctx_factory(P)
+        ctx.set_option("place_trials", k)
+        for c in range(2):
+            m, u, d, v = gen_svd_input(N, M, seed=4300 + c)
+            hs.svd_witness(ctx, *_on_device(m, u, v, d), gamma_for(4400 + c))
+        ctx.sync()
+        outs.append((ctx.advice(0), ctx.lookups(0), ctx.advice(1)))
+        ctx.close()
+    for name, a, b in zip(("advice0", "lookup0", "advice1"), outs[0], outs[1]):
+        assert a.shape == b.shape
+        bad = np.nonzero(np.any(a != b, axis=1))[0]
+        assert bad.size == 0, f"{name}: {bad.size} cells differ, first at {bad[:8]}"
+
+
 def test_completion_marks(gpu_ctx_factory):
     """svdw_mark behind a held witness (hold_us: a spinning kernel at the head
     of the step) reads not-done until the work completes; svdw_mark_wait waits

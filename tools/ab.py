@@ -33,7 +33,7 @@ def parse_variant(s):
 DEFAULTS = {"gemm_impl": 0, "overlap": 1, "gemm_crt": 1, "stage_elems": 256,
             "phase1_overlap": 1, "p1_at": -1, "prod_cell": 1, "res_f64": 1,
             "stage_batch": 1, "f64_views": 1, "pipeline": 1, "vm_linear": 1,
-            "dchk_at": 0, "gamma_at": -1, "gemm_kern": -1, "res_wait": -1, "stage_rot": 1}
+            "dchk_at": 0, "gamma_at": -1, "gemm_kern": -1, "res_wait": -1, "stage_rot": 1, "place_trials": 6}
 # pseudo-option "prof": event profiler during the timed steps (0 off, 1 all, 2 k_stage only)
 PROF_PREFIX = {1: "", 2: "k_stage"}
 
